@@ -1,0 +1,116 @@
+/*
+ * ORACLE -- test infrastructure only.
+ *
+ * CPU restatement (plain C) of the reference's keyed window-aggregation path:
+ *   SQL:        SlicingWindowOperator + SliceAssigners + AbstractWindowAggProcessor
+ *               + Slice(Un)SharedWindowAggProcessor + RecordsWindowBuffer + AggCombiner
+ *               + InternalTimerServiceImpl (event time, heap timers, dedup)
+ *   DataStream: WindowOperator + Tumbling/SlidingEventTimeWindows + EventTimeTrigger
+ *               + SumAggregator (ReducingState)
+ *   Routing:    KeyGroupRangeAssignment + MathUtils.murmurHash + BinaryRowData Murmur3.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / the reported CPU baseline.  Nothing in the
+ * product path (flink_amd/, include/) links or calls it.
+ *
+ * Parity pinning: the restatement is checked against the reference's own known-answer
+ * tests transcribed under tests/golden/ (see tests/golden/make_golden.py for the
+ * file:line of every vector).  Key-group routing has no literal known-answer test in
+ * the reference and is pinned by restatement only.
+ */
+#ifndef FLINK_ORACLE_H
+#define FLINK_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { OR_MODE_SQL = 0, OR_MODE_DATASTREAM = 1 };
+enum { OR_TUMBLE = 0, OR_HOP = 1, OR_CUMULATE = 2 };
+enum { OR_VAL_NONE = 0, OR_VAL_I64 = 1, OR_VAL_F64 = 2 };
+
+typedef struct or_config {
+    int32_t mode;             /* OR_MODE_SQL / OR_MODE_DATASTREAM */
+    int32_t kind;             /* OR_TUMBLE / OR_HOP / OR_CUMULATE (DataStream: TUMBLE / HOP=sliding) */
+    int64_t size;             /* tumble size, hop size, cumulate max size (ms) */
+    int64_t slide;            /* hop slide, cumulate step (ms); ignored for tumble */
+    int64_t offset;           /* window offset (ms) */
+    int64_t tz_offset_ms;     /* fixed-offset shift time zone (no DST); 0 = UTC */
+    int32_t val_type;         /* OR_VAL_* */
+    int32_t count_star_index; /* >= 0 when the agg list holds COUNT(*) (required for HOP) */
+} or_config;
+
+/* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v). */
+typedef struct or_row {
+    int64_t key;
+    int64_t window_start;
+    int64_t window_end;
+    int64_t cnt_star;
+    int64_t cnt_val;
+    int64_t sum_i;      /* SUM for i64 values (valid when !sum_null)            */
+    double  sum_d;      /* SUM for f64 values (valid when !sum_null)            */
+    int64_t avg_i;      /* AVG for i64 values: Java long division (valid when !avg_null) */
+    double  avg_d;      /* AVG for f64 values: sum / (double) count            */
+    int32_t sum_null;
+    int32_t avg_null;
+    int64_t out_ts;     /* DataStream: emitted StreamRecord timestamp (end - 1) */
+} or_row;
+
+typedef struct or_op or_op;
+
+/* Returns NULL on invalid parameters; err receives the reference's exception message. */
+or_op*  or_open(const or_config* cfg, char* err, int errlen);
+void    or_close(or_op* op);
+/* processElement for n records. val points at int64_t[] or double[] (or NULL for NONE);
+ * isnull may be NULL. */
+void    or_process_batch(or_op* op, int64_t n, const int64_t* key, const int64_t* ts,
+                         const void* val, const uint8_t* isnull);
+void    or_process_watermark(or_op* op, int64_t wm);
+/* prepareSnapshotPreBarrier: RecordsWindowBuffer.flush() (no-op for DataStream). */
+void    or_prepare_snapshot(or_op* op);
+/* snapshot -> close -> initializeState -> open: state and timers survive, the buffer
+ * (empty after prepare_snapshot), processor progress and timer watermark reset. */
+or_op*  or_restore_copy(const or_op* op);
+int64_t or_num_rows(const or_op* op);
+const or_row* or_rows(const or_op* op);
+void    or_clear_rows(or_op* op);
+int64_t or_late_dropped(const or_op* op);
+int64_t or_state_entries(const or_op* op);
+int64_t or_pending_timers(const or_op* op);
+
+/* --- slice assigner restatement (SliceAssigners.java) ------------------------- */
+int64_t or_assign_slice_end(const or_op* op, int64_t ts);
+int64_t or_get_window_start(const or_op* op, int64_t window_end);
+int64_t or_get_last_window_end(const or_op* op, int64_t slice_end);
+/* writes up to 2 slices, returns count */
+int32_t or_expired_slices(const or_op* op, int64_t window_end, int64_t* out);
+/* HOP/CUMULATE mergeSlices: *merge_result = MIN when null namespace; returns #toBeMerged */
+int32_t or_merge_slices(const or_op* op, int64_t slice_end, int64_t* merge_result, int64_t* out, int32_t cap);
+/* nextTriggerWindow: returns 1 and *next when present */
+int32_t or_next_trigger_window(const or_op* op, int64_t window_end, int32_t is_empty, int64_t* next);
+int64_t or_next_trigger_watermark(int64_t wm, int64_t interval);
+int64_t or_window_start_with_offset(int64_t ts, int64_t offset, int64_t size);
+
+/* --- key groups (KeyGroupRangeAssignment / MathUtils / MurmurHashUtils) ------- */
+int32_t or_binaryrow_hash_i64(int64_t key);          /* BinaryRowData(BIGINT).hashCode() */
+int32_t or_long_hash(int64_t key);                    /* java.lang.Long.hashCode() */
+int32_t or_murmur_hash(int32_t code);                 /* MathUtils.murmurHash */
+int32_t or_key_group(int32_t key_hash, int32_t max_parallelism);
+int32_t or_operator_index(int32_t max_parallelism, int32_t parallelism, int32_t key_group);
+int32_t or_default_max_parallelism(int32_t parallelism);
+void    or_key_groups_binaryrow(int64_t n, const int64_t* key, int32_t max_parallelism, int32_t* out);
+
+/* --- CPU baseline: P operator instances, one per core, records routed by key group.
+ * Watermark wm_val[j] is delivered after record index wm_at[j] (exclusive prefix).
+ * Returns elapsed seconds of the parallel processing region (routing excluded);
+ * *rows_out receives total fired rows, *checksum an order-independent checksum. */
+double  or_run_partitioned(const or_config* cfg, int32_t parallelism, int32_t max_parallelism,
+                           int64_t n, const int64_t* key, const int64_t* ts, const void* val,
+                           int32_t n_wm, const int64_t* wm_at, const int64_t* wm_val,
+                           int64_t* rows_out, uint64_t* checksum, int64_t* late_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,373 @@
+"""Generate the golden fixtures under tests/golden/ from the reference's own tests.
+
+The reference is Java; nothing of it can run here (no JDK). Every vector
+below is TRANSCRIBED DATA: the input sequence and the expected output that a
+reference test asserts, with the test's file:line.  String keys of the reference tests
+are mapped to i64 ids (key identity is the only property the aggregation uses; outputs
+are compared sorted, as the reference's assertors do).  Timestamps are epoch millis.
+
+Paths:
+  TRT = flink-table/flink-table-runtime-blink/src/test/java/org/apache/flink/table/runtime/
+  TPT = flink-table/flink-table-planner-blink/src/test/scala/org/apache/flink/table/planner/
+  SJT = flink-streaming-java/src/test/java/org/apache/flink/streaming/
+
+Run:  python tests/golden/make_golden.py   (rewrites the *.json next to this file)
+"""
+from __future__ import annotations
+
+import datetime as dt
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SHANGHAI = 8 * 3600 * 1000          # Asia/Shanghai: fixed +08:00, useDaylightTime() == false
+JMAX = (1 << 63) - 1
+
+
+def utc_ms(s: str) -> int:
+    """LocalDateTime string read as UTC -> epoch millis (the tests' utcMills())."""
+    d = dt.datetime.fromisoformat(s).replace(tzinfo=dt.timezone.utc)
+    return int(round(d.timestamp() * 1000))
+
+
+def E(key, val, ts, isnull=0):
+    return ["e", key, val, ts, isnull]
+
+
+def WM(w):
+    return ["wm", w]
+
+
+SNAP = ["snapshot_restore"]
+
+
+# ----------------------------------------------------------------------------------------
+# SlicingWindowAggOperatorTest (TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java)
+# SumAndCountAggsFunction (:821-951) computes SUM(f1), COUNT(f1) over an INT column; the
+# output row is (key, sum, count, window_start, window_end) with window times in
+# localMills() = toUtcTimestampMills(epoch, shiftTimeZone).  key1 -> 1, key2 -> 2.
+# Columns checked: key, sum, count(= COUNT(f1)), window_start, window_end.
+# ----------------------------------------------------------------------------------------
+def slicing_operator_fixtures():
+    out = []
+    for tzname, tz in (("UTC", 0), ("Asia/Shanghai", SHANGHAI)):
+        L = lambda x: x + tz   # localMills(x)
+        # testEventTimeHoppingWindows :116-222 (hop 3s/1s, countStarIndex 1)
+        ev = [E(2, 1, 3999), E(2, 1, 3000), E(1, 1, 20), E(1, 1, 0), E(1, 1, 999),
+              E(2, 1, 1998), E(2, 1, 1999), E(2, 1, 1000)]
+        steps = []
+        ev.append(WM(999)); steps.append((len(ev) - 1, [[1, 3, 3, L(-2000), L(1000)]]))
+        ev.append(WM(1999)); steps.append((len(ev) - 1, [[1, 3, 3, L(-1000), L(2000)], [2, 3, 3, L(-1000), L(2000)]]))
+        ev.append(WM(2999)); steps.append((len(ev) - 1, [[1, 3, 3, L(0), L(3000)], [2, 3, 3, L(0), L(3000)]]))
+        ev.append(SNAP)
+        ev.append(WM(3999)); steps.append((len(ev) - 1, [[2, 5, 5, L(1000), L(4000)]]))
+        ev.append(E(2, 1, 3500))   # late for [1K,4K) but accumulated into [2K,5K), [3K,6K)
+        ev.append(WM(4999)); steps.append((len(ev) - 1, [[2, 3, 3, L(2000), L(5000)]]))
+        ev.append(E(1, 1, 2999))   # late for all assigned windows -> dropped
+        ev.append(WM(5999)); steps.append((len(ev) - 1, [[2, 3, 3, L(3000), L(6000)]]))
+        ev.append(WM(6999)); steps.append((len(ev) - 1, []))
+        ev.append(WM(7999)); steps.append((len(ev) - 1, []))
+        out.append(dict(
+            name=f"sql_hop_3s_1s_{tzname}", source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:116-222",
+            config=dict(mode="sql", kind="hop", size=3000, slide=1000, offset=0, tz_offset_ms=tz,
+                        val_type="i64", count_star_index=1),
+            columns=["key", "sum", "count", "window_start", "window_end"],
+            events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=1))
+
+        # testEventTimeCumulativeWindows :345-452 (cumulate 3s/1s, no count star)
+        ev = [E(2, 1, 2999), E(2, 1, 3000), E(1, 1, 20), E(1, 1, 0), E(1, 1, 999),
+              E(2, 1, 1998), E(2, 1, 1999), E(2, 1, 1000)]
+        steps = []
+        ev.append(WM(999)); steps.append((len(ev) - 1, [[1, 3, 3, L(0), L(1000)]]))
+        ev.append(WM(1999)); steps.append((len(ev) - 1, [[1, 3, 3, L(0), L(2000)], [2, 3, 3, L(0), L(2000)]]))
+        ev.append(WM(2999)); steps.append((len(ev) - 1, [[1, 3, 3, L(0), L(3000)], [2, 4, 4, L(0), L(3000)]]))
+        ev.append(SNAP)
+        ev.append(WM(3999)); steps.append((len(ev) - 1, [[2, 1, 1, L(3000), L(4000)]]))
+        ev.append(E(1, 2, 3500))   # late for [3K,4K) but accumulated into [3K,5K), [3K,6K)
+        ev.append(WM(4999)); steps.append((len(ev) - 1, [[2, 1, 1, L(3000), L(5000)], [1, 2, 1, L(3000), L(5000)]]))
+        ev.append(E(1, 1, 2999))   # late for all assigned windows -> dropped
+        ev.append(WM(5999)); steps.append((len(ev) - 1, [[2, 1, 1, L(3000), L(6000)], [1, 2, 1, L(3000), L(6000)]]))
+        ev.append(WM(6999)); steps.append((len(ev) - 1, []))
+        ev.append(WM(7999)); steps.append((len(ev) - 1, []))
+        out.append(dict(
+            name=f"sql_cumulate_3s_1s_{tzname}", source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:345-452",
+            config=dict(mode="sql", kind="cumulate", size=3000, slide=1000, offset=0, tz_offset_ms=tz,
+                        val_type="i64", count_star_index=-1),
+            columns=["key", "sum", "count", "window_start", "window_end"],
+            events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=1))
+
+        # testEventTimeTumblingWindows :589-688 (tumble 3s)
+        ev = [E(2, 1, 3999), E(2, 1, 3000), E(1, 1, 20), E(1, 1, 0), E(1, 1, 999),
+              E(2, 1, 1998), E(2, 1, 1999), E(2, 1, 1000)]
+        steps = []
+        ev.append(WM(999)); steps.append((len(ev) - 1, []))
+        ev.append(WM(1999)); steps.append((len(ev) - 1, []))
+        ev.append(SNAP)
+        ev.append(WM(2999)); steps.append((len(ev) - 1, [[1, 3, 3, L(0), L(3000)], [2, 3, 3, L(0), L(3000)]]))
+        ev.append(WM(3999)); steps.append((len(ev) - 1, []))
+        ev.append(E(1, 1, 2500))   # late -> dropped
+        ev.append(WM(4999)); steps.append((len(ev) - 1, []))
+        ev.append(E(2, 1, 2999))   # late -> dropped
+        ev.append(WM(5999)); steps.append((len(ev) - 1, [[2, 2, 2, L(3000), L(6000)]]))
+        ev.append(WM(6999)); steps.append((len(ev) - 1, []))
+        ev.append(WM(7999)); steps.append((len(ev) - 1, []))
+        out.append(dict(
+            name=f"sql_tumble_3s_{tzname}", source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:589-688",
+            config=dict(mode="sql", kind="tumble", size=3000, slide=0, offset=0, tz_offset_ms=tz,
+                        val_type="i64", count_star_index=-1),
+            columns=["key", "sum", "count", "window_start", "window_end"],
+            events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=2))
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# WindowOperatorTest (SJT/runtime/operators/windowing/WindowOperatorTest.java): SumReducer
+# over Tuple2<String,Integer>; output StreamRecord((key, sum), window.maxTimestamp()).
+# Columns checked: key, sum, out_ts.
+# ----------------------------------------------------------------------------------------
+def datastream_fixtures():
+    out = []
+    base = [E(2, 1, 3999), E(2, 1, 3000), E(1, 1, 20), E(1, 1, 0), E(1, 1, 999),
+            E(2, 1, 1998), E(2, 1, 1999), E(2, 1, 1000)]
+    # testTumblingEventTimeWindows :293-353 driven by testTumblingEventTimeWindowsReduce :398-433
+    ev = list(base)
+    steps = []
+    ev.append(WM(999)); steps.append((len(ev) - 1, []))
+    ev.append(WM(1999)); steps.append((len(ev) - 1, []))
+    ev.append(SNAP)
+    ev.append(WM(2999)); steps.append((len(ev) - 1, [[1, 3, 2999], [2, 3, 2999]]))
+    ev.append(WM(3999)); steps.append((len(ev) - 1, []))
+    ev.append(WM(4999)); steps.append((len(ev) - 1, []))
+    ev.append(WM(5999)); steps.append((len(ev) - 1, [[2, 2, 5999]]))
+    ev.append(WM(6999)); steps.append((len(ev) - 1, []))
+    ev.append(WM(7999)); steps.append((len(ev) - 1, []))
+    out.append(dict(
+        name="ds_tumble_3s_reduce", source="SJT/runtime/operators/windowing/WindowOperatorTest.java:293-353,398-433",
+        config=dict(mode="datastream", kind="tumble", size=3000, slide=0, offset=0, tz_offset_ms=0,
+                    val_type="i64", count_star_index=-1),
+        columns=["key", "sum", "out_ts"],
+        events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
+    # testSlidingEventTimeWindows :108-211 driven by testSlidingEventTimeWindowsReduce :215-
+    ev = list(base)
+    steps = []
+    ev.append(WM(999)); steps.append((len(ev) - 1, [[1, 3, 999]]))
+    ev.append(WM(1999)); steps.append((len(ev) - 1, [[1, 3, 1999], [2, 3, 1999]]))
+    ev.append(WM(2999)); steps.append((len(ev) - 1, [[1, 3, 2999], [2, 3, 2999]]))
+    ev.append(SNAP)
+    ev.append(WM(3999)); steps.append((len(ev) - 1, [[2, 5, 3999]]))
+    ev.append(WM(4999)); steps.append((len(ev) - 1, [[2, 2, 4999]]))
+    ev.append(WM(5999)); steps.append((len(ev) - 1, [[2, 2, 5999]]))
+    ev.append(WM(6999)); steps.append((len(ev) - 1, []))
+    ev.append(WM(7999)); steps.append((len(ev) - 1, []))
+    out.append(dict(
+        name="ds_sliding_3s_1s_reduce", source="SJT/runtime/operators/windowing/WindowOperatorTest.java:108-211,215-250",
+        config=dict(mode="datastream", kind="hop", size=3000, slide=1000, offset=0, tz_offset_ms=0,
+                    val_type="i64", count_star_index=-1),
+        columns=["key", "sum", "out_ts"],
+        events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
+    return out
+
+
+# ----------------------------------------------------------------------------------------
+# WindowAggregateITCase (TPT/runtime/stream/sql/WindowAggregateITCase.scala) over
+# TestData.windowDataWithTimestamp (TPT/runtime/utils/TestData.scala:601-615):
+#   (ts, `double`, name); name a -> 1, b -> 2, null -> 3.
+# WATERMARK rowtime - INTERVAL '1' SECOND (:127), emitted after every record here; end of
+# input emits Long.MAX_VALUE. Checked: COUNT(*) per (name, window) and whether the
+# column `double` had any non-null value (MAX(`double`) is null iff COUNT(`double`) = 0).
+# Columns: key, window_start, window_end, cnt_star, val_all_null.
+# ----------------------------------------------------------------------------------------
+ITCASE_ROWS = [  # (ts, double or None, name)
+    ("2020-10-10 00:00:01", 1.0, 1), ("2020-10-10 00:00:02", 2.0, 1), ("2020-10-10 00:00:03", 2.0, 1),
+    ("2020-10-10 00:00:04", 5.0, 1), ("2020-10-10 00:00:07", 3.0, 2), ("2020-10-10 00:00:06", 6.0, 2),
+    ("2020-10-10 00:00:08", None, 1), ("2020-10-10 00:00:04", 5.0, 1), ("2020-10-10 00:00:16", 4.0, 2),
+    ("2020-10-10 00:00:32", 7.0, 3), ("2020-10-10 00:00:34", 3.0, 2),
+]
+
+
+def itcase_fixtures():
+    ev = []
+    mx = -(1 << 63)
+    for ts, d, name in ITCASE_ROWS:
+        t = utc_ms(ts.replace(" ", "T"))
+        ev.append(E(name, 0.0 if d is None else d, t, 1 if d is None else 0))
+        mx = max(mx, t)
+        ev.append(WM(mx - 1000))
+    ev.append(WM(JMAX))
+    T = lambda s: utc_ms("2020-10-10T" + s)
+    Tm = lambda s: utc_ms("2020-10-09T" + s)
+    tumble = [  # testEventTimeTumbleWindow :176-207
+        [1, T("00:00:00"), T("00:00:05"), 4, 0], [1, T("00:00:05"), T("00:00:10"), 1, 1],
+        [2, T("00:00:05"), T("00:00:10"), 2, 0], [2, T("00:00:15"), T("00:00:20"), 1, 0],
+        [2, T("00:00:30"), T("00:00:35"), 1, 0], [3, T("00:00:30"), T("00:00:35"), 1, 0],
+    ]
+    hop = [  # testEventTimeHopWindow :394-430 (HOP slide 5s, size 10s)
+        [1, Tm("23:59:55"), T("00:00:05"), 4, 0], [1, T("00:00:00"), T("00:00:10"), 6, 0],
+        [1, T("00:00:05"), T("00:00:15"), 1, 1], [2, T("00:00:00"), T("00:00:10"), 2, 0],
+        [2, T("00:00:05"), T("00:00:15"), 2, 0], [2, T("00:00:10"), T("00:00:20"), 1, 0],
+        [2, T("00:00:15"), T("00:00:25"), 1, 0], [2, T("00:00:25"), T("00:00:35"), 1, 0],
+        [2, T("00:00:30"), T("00:00:40"), 1, 0], [3, T("00:00:25"), T("00:00:35"), 1, 0],
+        [3, T("00:00:30"), T("00:00:40"), 1, 0],
+    ]
+    cumulate = [  # testEventTimeCumulateWindow :519-562 (CUMULATE step 5s, max 15s)
+        [1, T("00:00:00"), T("00:00:05"), 4, 0], [1, T("00:00:00"), T("00:00:10"), 6, 0],
+        [1, T("00:00:00"), T("00:00:15"), 6, 0], [2, T("00:00:00"), T("00:00:10"), 2, 0],
+        [2, T("00:00:00"), T("00:00:15"), 2, 0], [2, T("00:00:15"), T("00:00:20"), 1, 0],
+        [2, T("00:00:15"), T("00:00:25"), 1, 0], [2, T("00:00:15"), T("00:00:30"), 1, 0],
+        [2, T("00:00:30"), T("00:00:35"), 1, 0], [2, T("00:00:30"), T("00:00:40"), 1, 0],
+        [2, T("00:00:30"), T("00:00:45"), 1, 0], [3, T("00:00:30"), T("00:00:35"), 1, 0],
+        [3, T("00:00:30"), T("00:00:40"), 1, 0], [3, T("00:00:30"), T("00:00:45"), 1, 0],
+    ]
+    base = "TPT/runtime/stream/sql/WindowAggregateITCase.scala"
+    cols = ["key", "window_start", "window_end", "cnt_star", "val_all_null"]
+    mk = lambda name, src, cfg, rows: dict(
+        name=name, source=src + "; data TPT/runtime/utils/TestData.scala:601-615",
+        config=cfg, columns=cols, events=ev,
+        expected=[dict(after_event="end", rows=rows)], expected_late_dropped=None)
+    return [
+        mk("itcase_tumble_5s", base + ":176-207",
+           dict(mode="sql", kind="tumble", size=5000, slide=0, offset=0, tz_offset_ms=0, val_type="f64",
+                count_star_index=0), tumble),
+        mk("itcase_hop_10s_5s", base + ":394-430",
+           dict(mode="sql", kind="hop", size=10000, slide=5000, offset=0, tz_offset_ms=0, val_type="f64",
+                count_star_index=0), hop),
+        mk("itcase_cumulate_15s_5s", base + ":519-562",
+           dict(mode="sql", kind="cumulate", size=15000, slide=5000, offset=0, tz_offset_ms=0, val_type="f64",
+                count_star_index=0), cumulate),
+    ]
+
+
+# ----------------------------------------------------------------------------------------
+# Slice assigner known answers (TRT/operators/window/slicing/*SliceAssignerTest.java),
+# parameterized there over America/Los_Angeles and Asia/Shanghai; the fixed-offset zone
+# Asia/Shanghai (and UTC) are transcribed. Inputs to assignSliceEnd are localMills(str)
+# = utc(str) - tz; all other functions take and return utcMills.
+# ----------------------------------------------------------------------------------------
+def assigner_fixtures():
+    H = 3600 * 1000
+    U = lambda s: utc_ms(s)
+    cases = []
+    for tzname, tz in (("UTC", 0), ("Asia/Shanghai", SHANGHAI)):
+        A = lambda s: U(s) - tz
+        cases.append(dict(
+            name=f"tumbling_{tzname}", source="TRT/operators/window/slicing/TumblingSliceAssignerTest.java:47-153",
+            config=dict(kind="tumble", size=5 * H, slide=0, offset=0, tz_offset_ms=tz),
+            assign=[[A("1970-01-01T00:00:00"), U("1970-01-01T05:00:00")],
+                    [A("1970-01-01T04:59:59.999"), U("1970-01-01T05:00:00")],
+                    [A("1970-01-01T05:00:00"), U("1970-01-01T10:00:00")]],
+            window_start=[[U("1970-01-01T00:00:00"), U("1969-12-31T19:00:00")],
+                          [U("1970-01-01T05:00:00"), U("1970-01-01T00:00:00")],
+                          [U("1970-01-01T10:00:00"), U("1970-01-01T05:00:00")]],
+            expired=[[U("1970-01-01T00:00:00"), [U("1970-01-01T00:00:00")]],
+                     [U("1970-01-01T05:00:00"), [U("1970-01-01T05:00:00")]],
+                     [U("1970-01-01T10:00:00"), [U("1970-01-01T10:00:00")]]]))
+        cases.append(dict(
+            name=f"tumbling_offset_{tzname}", source="TRT/operators/window/slicing/TumblingSliceAssignerTest.java:62-77",
+            config=dict(kind="tumble", size=5 * H, slide=0, offset=100, tz_offset_ms=tz),
+            assign=[[A("1970-01-01T00:00:00.100"), U("1970-01-01T05:00:00.100")],
+                    [A("1970-01-01T05:00:00.099"), U("1970-01-01T05:00:00.100")],
+                    [A("1970-01-01T05:00:00.100"), U("1970-01-01T10:00:00.100")]]))
+        cases.append(dict(
+            name=f"hopping_{tzname}", source="TRT/operators/window/slicing/HoppingSliceAssignerTest.java:49-251",
+            config=dict(kind="hop", size=5 * H, slide=1 * H, offset=0, tz_offset_ms=tz),
+            assign=[[A("1970-01-01T00:00:00"), U("1970-01-01T01:00:00")],
+                    [A("1970-01-01T04:59:59.999"), U("1970-01-01T05:00:00")],
+                    [A("1970-01-01T05:00:00"), U("1970-01-01T06:00:00")]],
+            window_start=[[U(f"1970-01-01T{h:02d}:00:00"), U(f"1969-12-31T{19 + h:02d}:00:00")] for h in range(5)]
+            + [[U("1970-01-01T05:00:00"), U("1970-01-01T00:00:00")], [U("1970-01-01T06:00:00"), U("1970-01-01T01:00:00")],
+               [U("1970-01-01T10:00:00"), U("1970-01-01T05:00:00")]],
+            merge=[[U("1970-01-01T00:00:00"), None, [U("1970-01-01T00:00:00"), U("1969-12-31T23:00:00"), U("1969-12-31T22:00:00"),
+                                                      U("1969-12-31T21:00:00"), U("1969-12-31T20:00:00")]],
+                   [U("1970-01-01T05:00:00"), None, [U(f"1970-01-01T0{h}:00:00") for h in (5, 4, 3, 2, 1)]],
+                   [U("1970-01-01T06:00:00"), None, [U(f"1970-01-01T0{h}:00:00") for h in (6, 5, 4, 3, 2)]]],
+            next_trigger=[[U(f"1970-01-01T0{h}:00:00"), False, U(f"1970-01-01T0{h + 1}:00:00")] for h in range(7)]
+            + [[U(f"1970-01-01T0{h}:00:00"), True, None] for h in range(7)]))
+        cases.append(dict(
+            name=f"hopping_expired_{tzname}", source="TRT/operators/window/slicing/HoppingSliceAssignerTest.java:150-165",
+            config=dict(kind="hop", size=4 * H, slide=1 * H, offset=0, tz_offset_ms=tz),
+            expired=[[U("1970-01-01T00:00:00"), [U("1969-12-31T21:00:00")]],
+                     [U("1970-01-01T04:00:00"), [U("1970-01-01T01:00:00")]],
+                     [U("1970-01-01T08:00:00"), [U("1970-01-01T05:00:00")]]]))
+        cases.append(dict(
+            name=f"hopping_offset_{tzname}", source="TRT/operators/window/slicing/HoppingSliceAssignerTest.java:65-80",
+            config=dict(kind="hop", size=5 * H, slide=1 * H, offset=100, tz_offset_ms=tz),
+            assign=[[A("1970-01-01T00:00:00.100"), U("1970-01-01T01:00:00.100")],
+                    [A("1970-01-01T05:00:00.099"), U("1970-01-01T05:00:00.100")],
+                    [A("1970-01-01T05:00:00.100"), U("1970-01-01T06:00:00.100")]]))
+        cases.append(dict(
+            name=f"cumulative_day_{tzname}", source="TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:48-63",
+            config=dict(kind="cumulate", size=24 * H, slide=1 * H, offset=0, tz_offset_ms=tz),
+            assign=[[A("1970-01-01T00:00:00"), U("1970-01-01T01:00:00")],
+                    [A("1970-01-02T22:59:59.999"), U("1970-01-02T23:00:00")],
+                    [A("1970-01-02T23:00:00"), U("1970-01-03T00:00:00")]]))
+        cases.append(dict(
+            name=f"cumulative_offset_{tzname}", source="TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:65-80",
+            config=dict(kind="cumulate", size=5 * H, slide=1 * H, offset=100, tz_offset_ms=tz),
+            assign=[[A("1970-01-01T00:00:00.100"), U("1970-01-01T01:00:00.100")],
+                    [A("1970-01-01T05:00:00.099"), U("1970-01-01T05:00:00.100")],
+                    [A("1970-01-01T05:00:00.100"), U("1970-01-01T06:00:00.100")]]))
+        c5 = lambda s: U("1970-01-01T" + s)
+        cases.append(dict(
+            name=f"cumulative_5h_1h_{tzname}", source="TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:120-310",
+            config=dict(kind="cumulate", size=5 * H, slide=1 * H, offset=0, tz_offset_ms=tz),
+            window_start=[[c5("00:00:00"), U("1969-12-31T19:00:00")]]
+            + [[c5(f"0{h}:00:00"), c5("00:00:00")] for h in (1, 2, 3, 4, 5)]
+            + [[c5("06:00:00"), c5("05:00:00")], [c5("08:00:00"), c5("05:00:00")]],
+            expired=[[c5("01:00:00"), []], [c5("02:00:00"), [c5("02:00:00")]], [c5("03:00:00"), [c5("03:00:00")]],
+                     [c5("04:00:00"), [c5("04:00:00")]], [c5("05:00:00"), [c5("05:00:00"), c5("01:00:00")]],
+                     [c5("06:00:00"), []], [c5("10:00:00"), [c5("10:00:00"), c5("06:00:00")]],
+                     [c5("00:00:00"), [c5("00:00:00"), U("1969-12-31T20:00:00")]]],
+            merge=[[c5("01:00:00"), c5("01:00:00"), []]]
+            + [[c5(f"0{h}:00:00"), c5("01:00:00"), [c5(f"0{h}:00:00")]] for h in (2, 3, 4, 5)]
+            + [[c5("06:00:00"), c5("06:00:00"), []], [c5("08:00:00"), c5("06:00:00"), [c5("08:00:00")]],
+               [c5("10:00:00"), c5("06:00:00"), [c5("10:00:00")]],
+               [c5("00:00:00"), U("1969-12-31T20:00:00"), [c5("00:00:00")]]],
+            next_trigger=[[c5("00:00:00"), False, None]]
+            + [[c5(f"0{h}:00:00"), False, c5(f"0{h + 1}:00:00")] for h in (1, 2, 3, 4)]
+            + [[c5("05:00:00"), False, None], [c5("06:00:00"), False, c5("07:00:00")], [c5("00:00:00"), True, None]]
+            + [[c5(f"0{h}:00:00"), True, c5(f"0{h + 1}:00:00")] for h in (1, 2, 3, 4)]
+            + [[c5("05:00:00"), True, None], [c5("06:00:00"), True, c5("07:00:00")]]))
+    errors = [  # testInvalidParameters of each assigner test
+        dict(config=dict(kind="tumble", size=-1000, slide=0, offset=0),
+             message="Tumbling Window parameters must satisfy size > 0, but got size -1000ms.",
+             source="TRT/operators/window/slicing/TumblingSliceAssignerTest.java:155-160"),
+        dict(config=dict(kind="tumble", size=10000, slide=0, offset=20000),
+             message="Tumbling Window parameters must satisfy abs(offset) < size, bot got size 10000ms and offset 20000ms.",
+             source="TRT/operators/window/slicing/TumblingSliceAssignerTest.java:162-167"),
+        dict(config=dict(kind="hop", size=-2000, slide=1000, offset=0),
+             message="Hopping Window must satisfy slide > 0 and size > 0, but got slide 1000ms and size -2000ms.",
+             source="TRT/operators/window/slicing/HoppingSliceAssignerTest.java:268-272"),
+        dict(config=dict(kind="hop", size=2000, slide=-1000, offset=0),
+             message="Hopping Window must satisfy slide > 0 and size > 0, but got slide -1000ms and size 2000ms.",
+             source="TRT/operators/window/slicing/HoppingSliceAssignerTest.java:274-278"),
+        dict(config=dict(kind="hop", size=5000, slide=2000, offset=0),
+             message="Slicing Hopping Window requires size must be an integral multiple of slide, but got size 5000ms and slide 2000ms.",
+             source="TRT/operators/window/slicing/HoppingSliceAssignerTest.java:280-284"),
+        dict(config=dict(kind="cumulate", size=-5000, slide=1000, offset=0),
+             message="Cumulative Window parameters must satisfy maxSize > 0 and step > 0, but got maxSize -5000ms and step 1000ms.",
+             source="TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:316-321"),
+        dict(config=dict(kind="cumulate", size=5000, slide=-1000, offset=0),
+             message="Cumulative Window parameters must satisfy maxSize > 0 and step > 0, but got maxSize 5000ms and step -1000ms.",
+             source="TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:322-327"),
+        dict(config=dict(kind="cumulate", size=5000, slide=2000, offset=0),
+             message="Cumulative Window requires maxSize must be an integral multiple of step, but got maxSize 5000ms and step 2000ms.",
+             source="TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:328-333"),
+        dict(config=dict(kind="hop", size=3000, slide=1000, offset=0, count_star_index=-1),
+             message="Hopping window requires a COUNT(*) in the aggregate functions.",
+             source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:769-792"),
+    ]
+    return cases, errors
+
+
+def main():
+    ops = slicing_operator_fixtures() + datastream_fixtures() + itcase_fixtures()
+    with open(os.path.join(HERE, "operator_cases.json"), "w") as f:
+        json.dump(ops, f, indent=1)
+    cases, errors = assigner_fixtures()
+    with open(os.path.join(HERE, "assigner_cases.json"), "w") as f:
+        json.dump(dict(cases=cases, errors=errors), f, indent=1)
+    print(f"wrote {len(ops)} operator cases, {len(cases)} assigner cases, {len(errors)} error cases")
+
+
+if __name__ == "__main__":
+    main()
