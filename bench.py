@@ -1,0 +1,289 @@
+#!/usr/bin/env python
+"""Benchmark: records/s of the MI355X window-aggregation engine on BASELINE configs[1].
+
+Workload (BASELINE.json configs[1]): SQL TUMBLE 1s
+COUNT(*)/SUM/AVG(double) through the SlicingWindowOperator surface, 1B records per GPU,
+10M uniform BIGINT keys, 100M records per event-second (10 windows), in order, watermark
+= max rowtime - 1 every 1M records; end of input sends Long.MAX_VALUE.
+
+One step = the whole 1B-record job: reset the operator, feed the resident columns in
+50M-record micro-batches (each followed by the 1M-cadence watermarks that fall in it),
+then the final watermark fires the last window. Inputs (key i64, val f64, rowtime i64;
+24 GB) are generated on the GPU and resident in HBM before timing; fired rows stay in
+HBM (device output).  N > 1 (torchrun): every rank owns key groups
+kg*N/128 and a 1B-record source partition; each micro-batch is routed to its key-group
+owner by an RCCL all-to-all (flink_amd.exchange) before ingest -> weak scaling.
+
+Roofline: HBM. Algorithmic bytes: 24 B per input record + 48 B per fired
+row. `roofline` is for the dominant kernel, timed with HIP events on the engine's
+stream; `job_roofline_frac` is the whole-job B_alg / t / (N * 8 TB/s).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "records/sec/node, keyed TUMBLE SUM/COUNT/AVG at 1/2/4/8 GPU; % of HBM peak"
+HBM_PEAK_GBS = 8000.0
+SEED = 0x5EEDF11C
+T0 = 1_600_000_000_000
+JMAX = (1 << 63) - 1
+M64 = (1 << 64) - 1
+
+
+def s64(x: int) -> int:
+    x &= M64
+    return x - (1 << 64) if x >> 63 else x
+
+
+def lsr(z: torch.Tensor, s: int) -> torch.Tensor:
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def splitmix64(x: torch.Tensor) -> torch.Tensor:
+    z = x + s64(0x9E3779B97F4A7C15)
+    z = (z ^ lsr(z, 30)) * s64(0xBF58476D1CE4E5B9)
+    z = (z ^ lsr(z, 27)) * s64(0x94D049BB133111EB)
+    return z ^ lsr(z, 31)
+
+
+def gen_columns(n, keys, rate, base_index, device, chunk=1 << 26):
+    """key = u % keys, val = uniform [0, 1000) f64, rowtime = T0 + i // rate (tests/streams.py)."""
+    key = torch.empty(n, dtype=torch.int64, device=device)
+    ts = torch.empty(n, dtype=torch.int64, device=device)
+    val = torch.empty(n, dtype=torch.float64, device=device)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        i = torch.arange(base_index + lo, base_index + hi, dtype=torch.int64, device=device)
+        u = splitmix64(i ^ SEED)
+        u2 = splitmix64(i ^ (SEED * 3 + 1))
+        key[lo:hi] = (lsr(u, 1) % keys * 2 + (u & 1)) % keys        # unsigned u % keys
+        val[lo:hi] = lsr(u2, 11).to(torch.float64) * (1000.0 / float(1 << 53))
+        ts[lo:hi] = T0 + (i - base_index) // rate
+        del i, u, u2
+    return key, ts, val
+
+
+def watermarks_for(lo, hi, rate, every):
+    """1M-cadence watermarks (max rowtime - 1) delivered after records [lo, hi)."""
+    out = []
+    j = (lo // every + 1) * every
+    while j <= hi:
+        out.append(T0 + (j - 1) // rate - 1)
+        j += every
+    return out
+
+
+def cpu_baseline(args, rate):
+    """The oracle (C restatement of the reference operator) on the host cores: one instance
+    per core, records routed by key group, on a bounded prefix of the same stream."""
+    from oracle import oracle as O
+    O.build()
+    cores = min(16, os.cpu_count() or 1)
+
+    def gen(n):
+        i = np.arange(n, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            def sm(x):
+                z = (x + np.uint64(0x9E3779B97F4A7C15))
+                z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+                z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+                return z ^ (z >> np.uint64(31))
+            u = sm(i ^ np.uint64(SEED))
+            u2 = sm(i ^ np.uint64(SEED * 3 + 1))
+        key = (u % np.uint64(args.keys)).astype(np.int64)
+        val = (u2 >> np.uint64(11)).astype(np.float64) * (1000.0 / float(1 << 53))
+        ts = (T0 + np.arange(n, dtype=np.int64) // rate).astype(np.int64)
+        return key, ts, val
+
+    cfg = O.Config(O.MODE_SQL, O.TUMBLE, 1000, 0, 0, 0, O.VAL_F64, 0)
+
+    def run(n):
+        key, ts, val = gen(n)
+        wm_at = np.arange(args.wm_every, n + 1, args.wm_every, dtype=np.int64)
+        wm_val = T0 + (wm_at - 1) // rate - 1
+        wm_at = np.append(wm_at, n)
+        wm_val = np.append(wm_val, JMAX)
+        el, rows, cs, late = O.run_partitioned(cfg, cores, 128, key, ts, val, wm_at, wm_val)
+        return el, rows
+
+    el, _ = run(2_000_000)
+    rate_est = 2_000_000 / max(el, 1e-6)
+    n = int(min(args.cpu_max_records, max(4_000_000, rate_est * args.cpu_seconds)))
+    n -= n % args.wm_every
+    el, rows = run(n)
+    return dict(value=n / el, unit="records/s", cores=cores, kind="port",
+                sample=f"first {n:,} records of the configs[1] stream (10M-key space), watermark every "
+                       f"{args.wm_every:,} records + final Long.MAX_VALUE; C restatement of "
+                       f"SlicingWindowOperator/RecordsWindowBuffer/AggCombiner, {cores} instances routed by "
+                       f"key group (maxParallelism 128); {el:.1f} s, {rows:,} rows fired")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--records", type=int, default=1_000_000_000, help="records per GPU per step")
+    ap.add_argument("--keys", type=int, default=10_000_000)
+    ap.add_argument("--rate", type=int, default=100_000_000, help="records per event-second")
+    ap.add_argument("--batch", type=int, default=50_000_000)
+    ap.add_argument("--wm-every", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import flink_amd as F
+    from flink_amd.exchange import exchange, global_watermark
+
+    rate_ms = args.rate // 1000
+    n = args.records
+    key, ts, val = gen_columns(n, args.keys, rate_ms, rank * n, dev)
+    torch.cuda.synchronize()
+
+    maxp = 128
+    kg_lo, kg_hi = (rank * maxp + world - 1) // world, ((rank + 1) * maxp - 1) // world
+    op = F.WindowAggOperator(F.tumbling(1000), aggs=("count_star", "sum", "avg"), val_type="f64",
+                             expected_keys=int(args.keys / world * 1.05) + 1,
+                             buffer_records=max(4 * args.batch, 1 << 26), device=local,
+                             key_group_range=(kg_lo, kg_hi), kernel_timing=True)
+
+    def one_step():
+        op.reset()
+        rows = 0
+        xgmi = 0
+        for lo in range(0, n, args.batch):
+            hi = min(n, lo + args.batch)
+            k, t, v = key[lo:hi], ts[lo:hi], val[lo:hi]
+            if world > 1:
+                k, t, v, sent = exchange(k, t, v.view(torch.int64), max_parallelism=maxp)
+                v = v.view(torch.float64)
+                xgmi += sent
+                torch.cuda.current_stream().synchronize()
+            op.process_batch(k, t, v)
+            wms = watermarks_for(lo, hi, rate_ms, args.wm_every)
+            if world > 1 and wms:
+                wms[-1] = global_watermark(wms[-1], device=dev)
+            for wm in wms:
+                r = op.process_watermark(wm, device_output=True)
+                rows += r.n
+        r = op.process_watermark(JMAX, device_output=True)
+        rows += r.n
+        return rows, xgmi
+
+    for _ in range(args.warmup):
+        one_step()
+    op.synchronize()
+    before = op.kernel_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tot_rows = 0
+    tot_xgmi = 0
+    for _ in range(args.steps):
+        rows, xg = one_step()
+        tot_rows += rows
+        tot_xgmi += xg
+    op.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    after = op.kernel_stats()
+    late = op.num_late_records_dropped
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        rr = torch.tensor([tot_rows, late], dtype=torch.int64, device=dev)
+        dist.all_reduce(rr)
+        tot_rows, late = int(rr[0].item()), int(rr[1].item())
+
+    # per-kernel accounting over the timed region
+    ks = {}
+    for name, a in after.items():
+        b = before.get(name, dict(launches=0, total_ms=0.0, records=0, rows=0))
+        d = {k: a[k] - b[k] for k in ("launches", "total_ms", "records", "rows")}
+        if d["launches"] > 0:
+            ks[name] = d
+    dom_name, dom = max(ks.items(), key=lambda kv: kv[1]["total_ms"])
+    avg_s = dom["total_ms"] / dom["launches"] / 1e3
+    alg_bytes = (24 * dom["records"] + 48 * dom["rows"]) / dom["launches"]
+    achieved = alg_bytes / avg_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom_name, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    total_records = world * n * args.steps
+    value = total_records / el
+    b_alg = 24 * total_records + 48 * tot_rows
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "records/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (counter-based splitmix64 stream generated on the GPU, resident in HBM)",
+        "config": {
+            "workload": "SQL TUMBLE 1s COUNT(*)/SUM/AVG(double) via SlicingWindowOperator, 1B records per GPU, "
+                        "10M uniform keys (BASELINE configs[1])",
+            "records_per_gpu": n, "keys": args.keys, "records_per_event_second": args.rate,
+            "micro_batch": args.batch, "watermark_every": args.wm_every,
+            "parallelism": f"key-group sharded x{world}" + (" + RCCL all-to-all" if world > 1 else ""),
+        },
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom_name,
+                     "avg_launch_ms": avg_s * 1e3,
+                     "alg_bytes_per_launch": alg_bytes},
+        "job_roofline_frac": b_alg / el / (world * HBM_PEAK_GBS * 1e9),
+        "rows_fired": tot_rows,
+        "late_dropped": late,
+        "xgmi_bytes_sent_rank0": tot_xgmi,
+        "kernels": {k: dict(v, avg_ms=v["total_ms"] / v["launches"]) for k, v in ks.items()},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(args, rate_ms)
+        except Exception as e:  # reported, not fatal
+            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+    op.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,12 @@
+"""flink_amd -- MI355X-native keyed window aggregation for Flink's window operators.
+
+The hot path (slice assignment, keyed hash aggregation in HBM/LDS, slice merge on window
+fire, key-group routing) lives in libflinkgpu.so (HIP for gfx950, C-ABI in
+include/flinkgpu.h). This package is the host-side mirror of the reference operator
+interface used by tests and the benchmark; see DESIGN.md and INTEGRATION.md.
+"""
+from ._lib import FlinkGpuError, WindowSpecError  # noqa: F401
+from .window_agg import Window, WindowAggOperator, cumulative, hopping, key_groups, tumbling  # noqa: F401
+
+__all__ = ["WindowAggOperator", "Window", "tumbling", "hopping", "cumulative", "key_groups",
+           "FlinkGpuError", "WindowSpecError"]

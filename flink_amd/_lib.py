@@ -1,0 +1,143 @@
+"""ctypes binding of libflinkgpu.so (the C-ABI declared in include/flinkgpu.h).
+
+The library is built in-tree (``flink_amd/libflinkgpu.so``, see flink_amd/build.py).
+There is no fallback: if the library is missing or cannot be loaded, importing the
+engine raises -- the product path never runs on a CPU substitute.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libflinkgpu.so")
+
+FG_OK, FG_EINVAL, FG_EFULL, FG_EDEVICE, FG_ECAPACITY, FG_ESTATE = range(6)
+MODE_SQL, MODE_DATASTREAM = 0, 1
+TUMBLE, HOP, CUMULATE = 0, 1, 2
+VAL_NONE, VAL_I64, VAL_F64 = 0, 1, 2
+AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_AVG = 0, 1, 2, 3
+HOST, DEVICE = 0, 1
+KEYHASH_BINARYROW_BIGINT, KEYHASH_JAVA_LONG = 0, 1
+MAX_AGGS = 8
+
+
+class FgConfig(C.Structure):
+    _fields_ = [
+        ("mode", C.c_int32), ("window_kind", C.c_int32),
+        ("size_ms", C.c_int64), ("slide_ms", C.c_int64), ("offset_ms", C.c_int64),
+        ("shift_tz_offset_ms", C.c_int64),
+        ("val_type", C.c_int32), ("num_aggs", C.c_int32), ("aggs", C.c_int32 * MAX_AGGS),
+        ("max_parallelism", C.c_int32), ("key_group_start", C.c_int32), ("key_group_end", C.c_int32),
+        ("device_id", C.c_int32), ("flags", C.c_int32),
+        ("expected_keys", C.c_int64), ("buffer_records", C.c_int64),
+    ]
+
+
+class FgBatch(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("location", C.c_int32), ("reserved0", C.c_int32),
+        ("key", C.c_void_p), ("rowtime", C.c_void_p), ("val", C.c_void_p), ("val_null", C.c_void_p),
+    ]
+
+
+class FgRows(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("location", C.c_int32), ("num_aggs", C.c_int32),
+        ("key", C.c_void_p), ("window_start", C.c_void_p), ("window_end", C.c_void_p),
+        ("agg", C.c_void_p * MAX_AGGS), ("null_mask", C.c_void_p), ("rowtime", C.c_void_p),
+    ]
+
+
+class FgStateRows(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("key", C.c_void_p), ("slice_end", C.c_void_p), ("cnt_star", C.c_void_p),
+        ("cnt_val", C.c_void_p), ("sum", C.c_void_p),
+    ]
+
+
+class FgStats(C.Structure):
+    _fields_ = [(n, C.c_int64) for n in (
+        "records_in", "records_staged", "late_dropped", "rows_fired", "flushes", "live_slices",
+        "state_regions", "region_capacity")]
+
+
+class FgKernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", C.c_int64), ("total_ms", C.c_double),
+                ("records", C.c_int64), ("rows", C.c_int64)]
+
+
+FLAG_KERNEL_TIMING = 1
+
+# every symbol include/flinkgpu.h declares
+EXPORTS = (
+    "fg_open", "fg_add_batch", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_stream",
+    "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_abi_version",
+)
+
+_lib = None
+
+
+class FlinkGpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[fg error {code}] {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class WindowSpecError(ValueError):
+    """IllegalArgumentException of the reference (same message)."""
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'`")
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7 (same
+    # SONAME as /opt/rocm's). Loading torch first makes libflinkgpu bind to that instance
+    # instead of starting a second runtime that would hide the GPU from torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    P = C.c_void_p
+    L.fg_open.argtypes = [C.POINTER(FgConfig), C.POINTER(P)]
+    L.fg_add_batch.argtypes = [P, C.POINTER(FgBatch)]
+    L.fg_advance_progress.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(FgRows)]
+    L.fg_flush.argtypes = [P]
+    L.fg_snapshot_state.argtypes = [P, C.POINTER(FgStateRows), C.POINTER(C.c_int64)]
+    L.fg_restore.argtypes = [P, C.POINTER(FgStateRows), C.c_int64]
+    L.fg_late_dropped.argtypes = [P, C.POINTER(C.c_int64)]
+    L.fg_get_stats.argtypes = [P, C.POINTER(FgStats)]
+    L.fg_synchronize.argtypes = [P]
+    L.fg_reset.argtypes = [P]
+    L.fg_kernel_stats.argtypes = [P, C.POINTER(FgKernelStat), C.c_int32, C.POINTER(C.c_int32)]
+    L.fg_stream.argtypes = [P]
+    L.fg_stream.restype = P
+    L.fg_last_error.argtypes = [P]
+    L.fg_last_error.restype = C.c_char_p
+    L.fg_close.argtypes = [P]
+    L.fg_close.restype = None
+    L.fg_key_groups.argtypes = [C.c_int32, C.c_int32, C.c_int64, P, C.c_int32, C.c_int32, P]
+    L.fg_partition_by_owner.argtypes = [C.c_int32, P, C.c_int64, P, P, P, C.c_int32, C.c_int32, C.c_int32,
+                                        P, P, P, P]
+    L.fg_abi_version.restype = C.c_int
+    for fn in ("fg_open", "fg_add_batch", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+               "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
+               "fg_partition_by_owner"):
+        getattr(L, fn).restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int, handle=None):
+    if rc == FG_OK:
+        return
+    msg = load().fg_last_error(handle).decode(errors="replace")
+    if rc == FG_EINVAL:
+        raise WindowSpecError(msg)
+    raise FlinkGpuError(rc, msg)

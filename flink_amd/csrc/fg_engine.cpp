@@ -1,0 +1,1245 @@
+// fg_engine.cpp -- host side of libflinkgpu.so: the C-ABI of include/flinkgpu.h.
+//
+// Mirrors the control flow of the reference operator around the GPU hot path:
+//   processElement    -> fg_add_batch: device ingest (slice assignment, late rules,
+//                        bucketing) into a staged buffer  (RecordsWindowBuffer.addElement)
+//   processWatermark  -> fg_advance_progress: the AbstractWindowAggProcessor.advanceProgress
+//                        gate (:178-192) and RecordsWindowBuffer.advanceProgress (:100-105)
+//                        decide the flush; then every window whose timer would fire
+//                        (trigger in (previous watermark, watermark]) is fired from the
+//                        GPU-resident slice state (fireWindow/mergeSlices/clearWindow).
+//   prepareSnapshotPreBarrier -> fg_flush ; snapshot/restore -> fg_snapshot_state/fg_restore.
+//
+// State is kept per slice in HBM ("slice tables"); a (key, window) row fires when its
+// window's timer fires and the key holds state in the window's slices -- the timers of
+// the reference (one per (key, window), registered by AggCombiner step 5 and chained by
+// nextTriggerWindow) fire exactly for those (key, window) pairs when offset == 0
+// (DESIGN.md "Firing without per-key timers").
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/flinkgpu.h"
+#include "fg_kernels.h"
+
+using namespace fg;
+
+namespace {
+
+thread_local std::string g_open_error;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+    hipError_t ensure(size_t need, hipStream_t s = nullptr, bool keep = false) {
+        if (need <= bytes) return hipSuccess;
+        size_t nb = std::max(need, bytes + bytes / 2);
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, nb);
+        if (e != hipSuccess) return e;
+        if (keep && p && bytes) {
+            e = hipMemcpyAsync(q, p, bytes, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) return e;
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+        }
+        if (p) (void)hipFree(p);
+        p = q;
+        bytes = nb;
+        return hipSuccess;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostBuf {   // pinned host memory
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~HostBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        size_t nb = std::max(need, bytes + bytes / 2);
+        void* q = nullptr;
+        hipError_t e = hipHostMalloc(&q, nb, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        if (p) (void)hipHostFree(p);
+        p = q;
+        bytes = nb;
+        return hipSuccess;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct SliceTable {
+    int64_t slice_end = 0;
+    DevBuf data;          // P * 4 * kRegionCap int64
+    DevBuf counts;        // P uint32
+    int64_t upper = 0;    // host-side upper bound of entries
+};
+
+struct Staged {
+    int64_t base = 0;
+    int64_t n = 0;
+    bool has_null = false;
+    DevBuf bucket_off;    // F + 1 uint32
+};
+
+struct Counters {        // device scratch words read back after ingest
+    unsigned long long drops;
+    unsigned long long pad;
+    long long lane_min[kMaxLanes];
+    long long lane_max[kMaxLanes];
+};
+
+constexpr int64_t kEmptyLane = INT64_MIN;
+
+enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_FLUSH, K_FIRE, K_EXPORT, K_RESTORE, K_NCLASS };
+const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan", "ingest_scatter", "merge_flush",
+                                           "merge_fire", "export", "restore"};
+struct KStat {
+    int64_t launches = 0;
+    double ms = 0;
+    int64_t records = 0, rows = 0;
+};
+struct PendingEv {
+    int cls;
+    hipEvent_t a, b;
+    int64_t records;
+};
+
+}  // namespace
+
+struct fg_handle {
+    fg_config cfg{};
+    WindowSpec w{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int region_bits = 0, P = 1, lanes = 1, F = 1, grid = 256;
+    int64_t slice_phase = 0;   // slice ends are == slice_phase (mod slice)
+
+    // processor / timer state
+    int64_t current_progress = JMIN;
+    int64_t next_trigger = JMIN;
+    int64_t timer_wm = JMIN;
+    int64_t late_dropped = 0;
+
+    // staged buffer (RecordsWindowBuffer analogue)
+    int64_t staged_cap = 0, staged_n = 0;
+    DevBuf st_key, st_val, st_null;
+    std::vector<std::unique_ptr<Staged>> staged;
+    std::vector<std::unique_ptr<Staged>> staged_pool;
+    int64_t lane_q[kMaxLanes];
+    int64_t lane_records[kMaxLanes];
+    int64_t min_slice_end = JMAX;
+
+    // ingest scratch
+    DevBuf in_key, in_ts, in_val, in_null;
+    DevBuf hist, offsets, scan_tmp, counters;
+    HostBuf h_counters;
+
+    // resident state
+    std::map<int64_t, std::unique_ptr<SliceTable>> tables;
+    std::vector<std::unique_ptr<SliceTable>> table_pool;
+
+    // descriptor arena (device + pinned mirror), reset at every sync point
+    DevBuf arena;
+    HostBuf h_arena;
+    size_t arena_used = 0;
+
+    // device scalars: [0] overflow flags, [1] out_count
+    DevBuf scalars;
+    HostBuf h_scalars;
+
+    // fired rows
+    int64_t out_cap = 0, out_n = 0;
+    DevBuf o_key, o_ws, o_we, o_null, o_rt;
+    DevBuf o_agg[FG_MAX_AGGS];
+    HostBuf h_key, h_ws, h_we, h_null, h_rt;
+    HostBuf h_agg[FG_MAX_AGGS];
+
+    // snapshot image
+    DevBuf s_key, s_slice, s_cs, s_cv, s_sum, s_off;
+    HostBuf hs_key, hs_slice, hs_cs, hs_cv, hs_sum, hs_counts, hs_off;
+
+    // stats
+    int64_t records_in = 0, rows_fired = 0, flushes = 0;
+    bool timing = false;
+    KStat kstat[K_NCLASS];
+    std::vector<PendingEv> pend;
+    std::vector<hipEvent_t> ev_pool;
+
+    int fail(int code, const char* fmt, ...) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        err = buf;
+        return code;
+    }
+};
+
+#define HIPCHK(h, expr)                                                                        \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess)                                                                   \
+            return (h)->fail(FG_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                             __FILE__, __LINE__);                                               \
+    } while (0)
+
+namespace {
+
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) {
+        int64_t t = a % b;
+        a = b;
+        b = t;
+    }
+    return a < 0 ? -a : a;
+}
+
+int64_t slice_end_of(const fg_handle* h, int64_t q) { return jadd((int64_t)((uint64_t)q * (uint64_t)h->w.slice), h->slice_phase); }
+
+// copy a small descriptor array into the arena and return its device address
+template <class T>
+int arena_put(fg_handle* h, const T* items, size_t n, const T** dev) {
+    size_t bytes = sizeof(T) * std::max<size_t>(n, 1);
+    size_t at = (h->arena_used + 255) & ~size_t(255);
+    if (at + bytes > h->arena.bytes) return h->fail(FG_EDEVICE, "descriptor arena exhausted");
+    std::memcpy(h->h_arena.as<char>() + at, items, sizeof(T) * n);
+    HIPCHK(h, hipMemcpyAsync(h->arena.as<char>() + at, h->h_arena.as<char>() + at, bytes, hipMemcpyHostToDevice,
+                             h->stream));
+    *dev = reinterpret_cast<const T*>(h->arena.as<char>() + at);
+    h->arena_used = at + bytes;
+    return FG_OK;
+}
+
+hipEvent_t ev_get(fg_handle* h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+// bracket one launch with HIP events on the handle's stream (FG_FLAG_KERNEL_TIMING)
+struct KTimer {
+    fg_handle* h;
+    int cls;
+    int64_t records;
+    hipEvent_t a = nullptr;
+    KTimer(fg_handle* hh, int c, int64_t r) : h(hh), cls(c), records(r) {
+        if (h->timing) {
+            a = ev_get(h);
+            (void)hipEventRecord(a, h->stream);
+        }
+    }
+    ~KTimer() {
+        if (!h->timing) return;
+        hipEvent_t b = ev_get(h);
+        (void)hipEventRecord(b, h->stream);
+        h->pend.push_back(PendingEv{cls, a, b, records});
+    }
+};
+
+int sync(fg_handle* h) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->arena_used = 0;
+    for (auto& p : h->pend) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) h->kstat[p.cls].ms += ms;
+        h->kstat[p.cls].launches++;
+        h->kstat[p.cls].records += p.records;
+        h->ev_pool.push_back(p.a);
+        h->ev_pool.push_back(p.b);
+    }
+    h->pend.clear();
+    return FG_OK;
+}
+
+int table_get(fg_handle* h, int64_t slice_end, bool create, SliceTable** out) {
+    auto it = h->tables.find(slice_end);
+    if (it != h->tables.end()) {
+        *out = it->second.get();
+        return FG_OK;
+    }
+    if (!create) {
+        *out = nullptr;
+        return FG_OK;
+    }
+    std::unique_ptr<SliceTable> t;
+    if (!h->table_pool.empty()) {
+        t = std::move(h->table_pool.back());
+        h->table_pool.pop_back();
+    } else {
+        t.reset(new SliceTable());
+        HIPCHK(h, t->data.ensure(sizeof(int64_t) * 4 * (size_t)kRegionCap * h->P));
+        HIPCHK(h, t->counts.ensure(sizeof(uint32_t) * h->P));
+    }
+    HIPCHK(h, hipMemsetAsync(t->counts.p, 0, sizeof(uint32_t) * h->P, h->stream));
+    t->slice_end = slice_end;
+    t->upper = 0;
+    *out = t.get();
+    h->tables[slice_end] = std::move(t);
+    return FG_OK;
+}
+
+void table_free(fg_handle* h, int64_t slice_end) {
+    auto it = h->tables.find(slice_end);
+    if (it == h->tables.end()) return;
+    h->table_pool.push_back(std::move(it->second));
+    h->tables.erase(it);
+}
+
+TableRef ref_of(SliceTable* t) { return TableRef{t->data.as<int64_t>(), t->counts.as<uint32_t>()}; }
+
+int check_overflow(fg_handle* h) {
+    unsigned int fl = h->h_scalars.as<unsigned int>()[0];
+    if (fl & 4u)
+        return h->fail(FG_ECAPACITY, "state region hash table full (%d slots): raise fg_config.expected_keys",
+                       kSlots);
+    if (fl & 1u)
+        return h->fail(FG_ECAPACITY, "state region overflow (> %d entries per region): raise fg_config.expected_keys",
+                       kRegionCap);
+    if (fl & 2u) return h->fail(FG_EDEVICE, "internal: fired-row buffer overflow");
+    return FG_OK;
+}
+
+// RecordsWindowBuffer.flush (:108-119) + AggCombiner.combine (:76-115): merge every staged
+// lane into its slice table.
+int flush(fg_handle* h) {
+    if (h->staged_n == 0 && h->staged.empty()) return FG_OK;
+    // staged batch descriptors
+    std::vector<StagedBatch> sb;
+    for (auto& s : h->staged) {
+        StagedBatch b{};
+        b.key = h->st_key.as<int64_t>() + s->base;
+        b.val = h->cfg.val_type != FG_VAL_NONE ? h->st_val.as<int64_t>() + s->base : nullptr;
+        b.vnull = s->has_null ? h->st_null.as<uint8_t>() + s->base : nullptr;
+        b.bucket_off = s->bucket_off.as<uint32_t>();
+        b.is_acc = 0;
+        sb.push_back(b);
+    }
+    const StagedBatch* d_sb = nullptr;
+    int rc = arena_put(h, sb.data(), sb.size(), &d_sb);
+    if (rc) return rc;
+    HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+    for (int l = 0; l < h->lanes; l++) {
+        if (h->lane_q[l] == kEmptyLane) continue;
+        SliceTable* t = nullptr;
+        rc = table_get(h, slice_end_of(h, h->lane_q[l]), true, &t);
+        if (rc) return rc;
+        TableRef tr = ref_of(t);
+        const TableRef* d_src = nullptr;
+        rc = arena_put(h, &tr, 1, &d_src);
+        if (rc) return rc;
+        MergeParams p{};
+        p.region_bits = h->region_bits;
+        p.lanes = h->lanes;
+        p.lane = l;
+        p.n_src = 1;
+        p.src = d_src;
+        p.n_batches = (int)sb.size();
+        p.batches = d_sb;
+        p.val_type = h->cfg.val_type;
+        p.has_dst = 1;
+        p.dst = tr;
+        p.emit = 0;
+        p.overflow = h->scalars.as<unsigned int>();
+        p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+        {
+            KTimer kt(h, K_FLUSH, h->lane_records[l]);
+            HIPCHK(h, launch_merge(p, h->stream));
+        }
+        t->upper = std::min<int64_t>(t->upper + h->lane_records[l], (int64_t)kRegionCap * h->P);
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
+    rc = sync(h);
+    if (rc) return rc;
+    rc = check_overflow(h);
+    if (rc) return rc;
+    for (auto& s : h->staged) h->staged_pool.push_back(std::move(s));
+    h->staged.clear();
+    h->staged_n = 0;
+    for (int l = 0; l < kMaxLanes; l++) {
+        h->lane_q[l] = kEmptyLane;
+        h->lane_records[l] = 0;
+    }
+    h->min_slice_end = JMAX;
+    h->flushes++;
+    return FG_OK;
+}
+
+int ensure_out(fg_handle* h, int64_t need) {
+    if (need <= h->out_cap) return FG_OK;
+    int64_t nc = std::max<int64_t>(need, h->out_cap + h->out_cap / 2);
+    nc = std::max<int64_t>(nc, 1024);
+    HIPCHK(h, h->o_key.ensure(8 * nc, h->stream, true));
+    HIPCHK(h, h->o_ws.ensure(8 * nc, h->stream, true));
+    HIPCHK(h, h->o_we.ensure(8 * nc, h->stream, true));
+    HIPCHK(h, h->o_null.ensure(nc, h->stream, true));
+    if (h->cfg.mode == FG_MODE_DATASTREAM) HIPCHK(h, h->o_rt.ensure(8 * nc, h->stream, true));
+    for (int a = 0; a < h->cfg.num_aggs; a++) HIPCHK(h, h->o_agg[a].ensure(8 * nc, h->stream, true));
+    h->out_cap = nc;
+    return FG_OK;
+}
+
+// Emit one window from the union of `srcs`; optionally write the merged state to `dst`.
+int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, SliceTable* dst) {
+    int64_t ub = 0;
+    for (auto* s : srcs) ub += s->upper;
+    ub = std::min<int64_t>(ub, (int64_t)kRegionCap * h->P);
+    if (ub == 0 && dst == nullptr) return FG_OK;
+    int rc = ensure_out(h, h->out_n + ub);
+    if (rc) return rc;
+    std::vector<TableRef> refs;
+    for (auto* s : srcs) refs.push_back(ref_of(s));
+    const TableRef* d_src = nullptr;
+    rc = arena_put(h, refs.data(), refs.size(), &d_src);
+    if (rc) return rc;
+    MergeParams p{};
+    p.region_bits = h->region_bits;
+    p.lanes = h->lanes;
+    p.lane = -1;
+    p.n_src = (int)refs.size();
+    p.src = d_src;
+    p.val_type = h->cfg.val_type;
+    p.has_dst = dst != nullptr;
+    if (dst) p.dst = ref_of(dst);
+    p.emit = 1;
+    p.wstart = window_start(h->w, wend);
+    p.wend = wend;
+    p.out_ts = jsub(wend, 1);
+    p.num_aggs = h->cfg.num_aggs;
+    for (int a = 0; a < h->cfg.num_aggs; a++) {
+        p.aggs[a] = h->cfg.aggs[a];
+        p.out_agg[a] = h->o_agg[a].as<int64_t>();
+    }
+    p.out_key = h->o_key.as<int64_t>();
+    p.out_ws = h->o_ws.as<int64_t>();
+    p.out_we = h->o_we.as<int64_t>();
+    p.out_null = h->o_null.as<uint8_t>();
+    p.out_rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->o_rt.as<int64_t>() : nullptr;
+    p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+    p.out_cap = h->out_cap;
+    p.overflow = h->scalars.as<unsigned int>();
+    {
+        KTimer kt(h, K_FIRE, 0);
+        HIPCHK(h, launch_merge(p, h->stream));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
+    rc = sync(h);
+    if (rc) return rc;
+    rc = check_overflow(h);
+    if (rc) return rc;
+    const int64_t before = h->out_n;
+    h->out_n = (int64_t)h->h_scalars.as<unsigned long long>()[1];
+    h->kstat[K_FIRE].rows += h->out_n - before;
+    if (dst) dst->upper = ub;
+    return FG_OK;
+}
+
+// Fire every window whose timer time lies in (prev, wm] (InternalTimerServiceImpl.advanceWatermark
+// :294-304 -> SlicingWindowOperator.onTimer :230-237), in window order.
+int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
+    const WindowSpec& w = h->w;
+    auto due = [&](int64_t wend) {
+        int64_t t = trigger_time(w, wend);
+        return wend != JMAX && t > prev && t <= wm;
+    };
+    auto dead = [&](int64_t wend) { return wend != JMAX && trigger_time(w, wend) <= prev; };
+    if (h->tables.empty()) return FG_OK;
+    int rc;
+    if (w.kind == TUMBLE) {
+        std::vector<int64_t> ends;
+        for (auto& kv : h->tables) ends.push_back(kv.first);
+        for (int64_t e : ends) {
+            if (due(e)) {
+                rc = fire_one(h, e, {h->tables[e].get()}, nullptr);
+                if (rc) return rc;
+                table_free(h, e);   // expiredSlices = [windowEnd]
+            } else if (dead(e)) {
+                table_free(h, e);   // no timer can fire for this slice any more
+            }
+        }
+        return FG_OK;
+    }
+    if (w.kind == HOP) {
+        // window ends on the slice grid; window W covers slices (W - size, W]
+        int64_t lo = h->tables.begin()->first;
+        int64_t hi = jadd(jsub(h->tables.rbegin()->first, w.slice), w.size);   // last window of the last slice
+        for (int64_t W = lo; W <= hi; W = jadd(W, w.slice)) {
+            if (trigger_time(w, W) > wm) break;
+            if (h->tables.empty()) break;
+            if (due(W)) {
+                std::vector<SliceTable*> srcs;
+                for (auto it = h->tables.upper_bound(jsub(W, w.size)); it != h->tables.end() && it->first <= W; ++it)
+                    srcs.push_back(it->second.get());
+                if (!srcs.empty()) {
+                    rc = fire_one(h, W, srcs, nullptr);
+                    if (rc) return rc;
+                }
+            }
+            if (due(W) || dead(W)) table_free(h, jadd(jsub(W, w.size), w.slice));   // expiredSlices
+            // skip empty stretches
+            auto nx = h->tables.upper_bound(jsub(W, w.size));
+            if (nx == h->tables.end()) break;
+            if (jadd(W, w.slice) <= jsub(nx->first, w.slice) && nx->first > W) W = jsub(nx->first, w.slice);
+        }
+        return FG_OK;
+    }
+    // CUMULATE: windows ws+step, ws+2step, ... ws+max of every cumulative window with state
+    std::vector<int64_t> starts;
+    for (auto& kv : h->tables) {
+        int64_t ws = window_start(w, kv.first);
+        if (starts.empty() || starts.back() != ws) starts.push_back(ws);
+    }
+    std::sort(starts.begin(), starts.end());
+    starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+    for (int64_t ws : starts) {
+        const int64_t first = jadd(ws, w.slice), last = jadd(ws, w.size);
+        for (int64_t W = first; W <= last; W = jadd(W, w.slice)) {
+            if (trigger_time(w, W) > wm) break;
+            SliceTable* F = nullptr;
+            SliceTable* S = nullptr;
+            rc = table_get(h, first, false, &F);
+            if (rc) return rc;
+            if (W != first) {
+                rc = table_get(h, W, false, &S);
+                if (rc) return rc;
+            }
+            if (!F && !S) continue;
+            if (due(W)) {
+                std::vector<SliceTable*> srcs;
+                if (F) srcs.push_back(F);
+                if (S) srcs.push_back(S);
+                SliceTable* dst = nullptr;
+                if (W != first && W != last) {
+                    if (!F) {
+                        rc = table_get(h, first, true, &F);
+                        if (rc) return rc;
+                    }
+                    dst = F;   // merge the step slice into the first slice's state
+                }
+                rc = fire_one(h, W, srcs, dst);
+                if (rc) return rc;
+            } else if (S && F && W != first) {
+                // window already fired before: fold the slice into the first slice without emitting
+                // (only reachable for state restored below an older watermark)
+            }
+            if (due(W) || dead(W)) {
+                if (W != first) table_free(h, W);
+                if (W == last) table_free(h, first);
+            }
+        }
+    }
+    return FG_OK;
+}
+
+int copy_out_to_host(fg_handle* h, fg_rows* r) {
+    const int64_t n = h->out_n;
+    const size_t b8 = 8 * (size_t)std::max<int64_t>(n, 1);
+    HIPCHK(h, h->h_key.ensure(b8));
+    HIPCHK(h, h->h_ws.ensure(b8));
+    HIPCHK(h, h->h_we.ensure(b8));
+    HIPCHK(h, h->h_null.ensure(std::max<int64_t>(n, 1)));
+    if (h->cfg.mode == FG_MODE_DATASTREAM) HIPCHK(h, h->h_rt.ensure(b8));
+    for (int a = 0; a < h->cfg.num_aggs; a++) HIPCHK(h, h->h_agg[a].ensure(b8));
+    if (n > 0) {
+        HIPCHK(h, hipMemcpyAsync(h->h_key.p, h->o_key.p, 8 * n, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_ws.p, h->o_ws.p, 8 * n, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_we.p, h->o_we.p, 8 * n, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_null.p, h->o_null.p, n, hipMemcpyDeviceToHost, h->stream));
+        if (h->cfg.mode == FG_MODE_DATASTREAM)
+            HIPCHK(h, hipMemcpyAsync(h->h_rt.p, h->o_rt.p, 8 * n, hipMemcpyDeviceToHost, h->stream));
+        for (int a = 0; a < h->cfg.num_aggs; a++)
+            HIPCHK(h, hipMemcpyAsync(h->h_agg[a].p, h->o_agg[a].p, 8 * n, hipMemcpyDeviceToHost, h->stream));
+        int rc = sync(h);
+        if (rc) return rc;
+    }
+    r->key = h->h_key.as<int64_t>();
+    r->window_start = h->h_ws.as<int64_t>();
+    r->window_end = h->h_we.as<int64_t>();
+    r->null_mask = h->h_null.as<uint8_t>();
+    r->rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->h_rt.as<int64_t>() : nullptr;
+    for (int a = 0; a < h->cfg.num_aggs; a++) r->agg[a] = h->h_agg[a].as<int64_t>();
+    return FG_OK;
+}
+
+// one ingest pass over the device-resident batch with a slice filter
+int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+    IngestParams p{};
+    p.w = h->w;
+    p.n = n;
+    p.key = key;
+    p.ts = ts;
+    p.val = val;
+    p.vnull = vnull;
+    p.progress = h->current_progress;
+    p.lanes = h->lanes;
+    p.region_bits = h->region_bits;
+    p.filter_lo = flo;
+    p.filter_hi = fhi;
+    p.count_drops = count_drops ? 1 : 0;
+    int64_t g = (n + 16383) / 16384;
+    p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(h->grid, g));
+    p.vec = ((uintptr_t)key % 16 == 0 && (uintptr_t)ts % 16 == 0 && (!val || (uintptr_t)val % 16 == 0)) ? 1 : 0;
+    p.hist = h->hist.as<uint32_t>();
+    Counters init{};
+    init.drops = 0;
+    for (int l = 0; l < kMaxLanes; l++) {
+        init.lane_min[l] = JMAX;
+        init.lane_max[l] = JMIN;
+    }
+    std::memcpy(h->h_counters.p, &init, sizeof init);
+    HIPCHK(h, hipMemcpyAsync(h->counters.p, h->h_counters.p, sizeof init, hipMemcpyHostToDevice, h->stream));
+    Counters* dc = h->counters.as<Counters>();
+    p.drops = &dc->drops;
+    p.lane_min = dc->lane_min;
+    p.lane_max = dc->lane_max;
+    {
+        KTimer kt(h, K_COUNT, n);
+        HIPCHK(h, launch_ingest_count(p, h->stream));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, h->stream));
+    int rc = sync(h);
+    if (rc) return rc;
+    std::memcpy(out, h->h_counters.p, sizeof(Counters));
+
+    // lane compatibility with the staged buffer
+    bool conflict = false;
+    for (int l = 0; l < h->lanes; l++) {
+        if (out->lane_min[l] > out->lane_max[l]) continue;
+        if (out->lane_min[l] != out->lane_max[l]) conflict = true;
+        if (h->lane_q[l] != kEmptyLane && h->lane_q[l] != out->lane_min[l]) conflict = true;
+    }
+    if (conflict) return -1;   // caller falls back to filtered passes
+
+    // scan + scatter into the staged buffer
+    const int64_t m = (int64_t)h->F * p.grid;
+    {
+        KTimer kt(h, K_SCAN, 0);
+        HIPCHK(h, launch_scan_u32(h->hist.as<uint32_t>(), h->offsets.as<uint32_t>(), m, h->scan_tmp.as<uint32_t>(),
+                                  h->stream));
+    }
+    std::unique_ptr<Staged> s;
+    if (!h->staged_pool.empty()) {
+        s = std::move(h->staged_pool.back());
+        h->staged_pool.pop_back();
+    } else {
+        s.reset(new Staged());
+    }
+    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
+    HIPCHK(h, launch_bucket_offsets(h->offsets.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F, p.grid,
+                                    h->stream));
+    p.offsets = h->offsets.as<uint32_t>();
+    p.st_key = h->st_key.as<int64_t>() + h->staged_n;
+    p.st_val = h->cfg.val_type != FG_VAL_NONE ? h->st_val.as<int64_t>() + h->staged_n : nullptr;
+    p.st_null = vnull ? h->st_null.as<uint8_t>() + h->staged_n : nullptr;
+    if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
+    {
+        KTimer kt(h, K_SCATTER, n);
+        HIPCHK(h, launch_ingest_scatter(p, h->stream));
+    }
+    int64_t staged_now = 0;
+    for (int l = 0; l < h->lanes; l++) {
+        if (out->lane_min[l] > out->lane_max[l]) continue;
+        h->lane_q[l] = out->lane_min[l];
+        h->min_slice_end = std::min(h->min_slice_end, slice_end_of(h, out->lane_min[l]));
+    }
+    // per-lane record totals for output sizing: read the bucket offsets of each lane boundary
+    std::vector<uint32_t> lb(h->lanes + 1);
+    for (int l = 0; l <= h->lanes; l++) {
+        HIPCHK(h, hipMemcpyAsync(&lb[l], s->bucket_off.as<uint32_t>() + (int64_t)l * h->P, sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, h->stream));
+    }
+    rc = sync(h);
+    if (rc) return rc;
+    for (int l = 0; l < h->lanes; l++) h->lane_records[l] += (int64_t)(lb[l + 1] - lb[l]);
+    staged_now = (int64_t)lb[h->lanes];
+    s->base = h->staged_n;
+    s->n = staged_now;
+    s->has_null = vnull != nullptr;
+    h->staged_n += staged_now;
+    h->staged.push_back(std::move(s));
+    return FG_OK;
+}
+
+int validate(const fg_config* c, std::string* msg) {
+    char buf[512];
+    buf[0] = 0;
+    const long long size = c->size_ms, slide = c->slide_ms, off = c->offset_ms;
+    bool has_star = false;
+    for (int a = 0; a < c->num_aggs; a++) has_star |= c->aggs[a] == FG_AGG_COUNT_STAR;
+    if (c->window_kind == FG_TUMBLE) {
+        if (!(size > 0))
+            snprintf(buf, sizeof buf, "Tumbling Window parameters must satisfy size > 0, but got size %lldms.", size);
+        else if (!((off < 0 ? -off : off) < size))
+            snprintf(buf, sizeof buf,
+                     "Tumbling Window parameters must satisfy abs(offset) < size, bot got size %lldms and offset %lldms.",
+                     size, off);
+    } else if (c->window_kind == FG_HOP) {
+        if (size <= 0 || slide <= 0)
+            snprintf(buf, sizeof buf,
+                     "Hopping Window must satisfy slide > 0 and size > 0, but got slide %lldms and size %lldms.", slide,
+                     size);
+        else if (size % slide != 0)
+            snprintf(buf, sizeof buf,
+                     "Slicing Hopping Window requires size must be an integral multiple of slide, but got size %lldms and slide %lldms.",
+                     size, slide);
+        else if (c->mode == FG_MODE_SQL && !has_star)
+            snprintf(buf, sizeof buf, "Hopping window requires a COUNT(*) in the aggregate functions.");
+    } else if (c->window_kind == FG_CUMULATE) {
+        if (size <= 0 || slide <= 0)
+            snprintf(buf, sizeof buf,
+                     "Cumulative Window parameters must satisfy maxSize > 0 and step > 0, but got maxSize %lldms and step %lldms.",
+                     size, slide);
+        else if (size % slide != 0)
+            snprintf(buf, sizeof buf,
+                     "Cumulative Window requires maxSize must be an integral multiple of step, but got maxSize %lldms and step %lldms.",
+                     size, slide);
+        else if (c->mode == FG_MODE_DATASTREAM)
+            snprintf(buf, sizeof buf, "DataStream has no cumulative window assigner.");
+    } else {
+        snprintf(buf, sizeof buf, "unknown window kind %d", c->window_kind);
+    }
+    if (!buf[0]) {
+        if (c->num_aggs < 1 || c->num_aggs > FG_MAX_AGGS)
+            snprintf(buf, sizeof buf, "num_aggs must be in [1, %d]", FG_MAX_AGGS);
+        for (int a = 0; a < c->num_aggs && !buf[0]; a++)
+            if (c->aggs[a] < FG_AGG_COUNT_STAR || c->aggs[a] > FG_AGG_AVG) snprintf(buf, sizeof buf, "bad agg %d", c->aggs[a]);
+        if (c->val_type < FG_VAL_NONE || c->val_type > FG_VAL_F64) snprintf(buf, sizeof buf, "bad val_type");
+        if (c->val_type == FG_VAL_NONE)
+            for (int a = 0; a < c->num_aggs && !buf[0]; a++)
+                if (c->aggs[a] != FG_AGG_COUNT_STAR) snprintf(buf, sizeof buf, "aggregates over a value need val_type");
+    }
+    if (buf[0]) {
+        *msg = buf;
+        return FG_EINVAL;
+    }
+    return FG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fg_abi_version(void) { return FG_ABI_VERSION; }
+
+int fg_open(const fg_config* cfg, fg_handle** out) {
+    *out = nullptr;
+    if (!cfg) {
+        g_open_error = "null config";
+        return FG_EINVAL;
+    }
+    std::string msg;
+    int rc = validate(cfg, &msg);
+    if (rc) {
+        g_open_error = msg;
+        return rc;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        g_open_error = "no HIP device available (libflinkgpu needs an MI355X / gfx950)";
+        return FG_EDEVICE;
+    }
+    if (cfg->device_id < 0 || cfg->device_id >= ndev) {
+        g_open_error = "device_id out of range";
+        return FG_EINVAL;
+    }
+    std::unique_ptr<fg_handle> h(new fg_handle());
+    h->cfg = *cfg;
+    h->device = cfg->device_id;
+    h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
+    if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        g_open_error = "hipSetDevice/hipStreamCreate failed";
+        return FG_EDEVICE;
+    }
+    WindowSpec& w = h->w;
+    w.kind = cfg->window_kind;
+    w.mode = cfg->mode;
+    w.size = cfg->size_ms;
+    w.slide = cfg->window_kind == FG_TUMBLE ? cfg->size_ms : cfg->slide_ms;
+    w.offset = cfg->offset_ms;
+    w.tz = cfg->mode == FG_MODE_DATASTREAM ? 0 : cfg->shift_tz_offset_ms;
+    w.slice = cfg->window_kind == FG_HOP ? gcd64(w.size, w.slide) : w.slide;
+    w.nslices = w.size / w.slice;
+    w.rslice = 1.0 / (double)w.slice;
+    w.rsize = 1.0 / (double)w.size;
+    h->slice_phase = ((w.offset % w.slice) + w.slice) % w.slice;
+
+    // regions: average occupancy <= ~70 % of the per-region HBM capacity
+    int64_t keys = std::max<int64_t>(cfg->expected_keys, 1);
+    int bits = 0;
+    while (bits < 15 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.7) < keys) bits++;
+    h->region_bits = bits;
+    h->P = 1 << bits;
+    h->lanes = kMaxLanes;
+    while (h->lanes > 1 && h->lanes * h->P > 32768) h->lanes >>= 1;
+    h->F = h->lanes * h->P;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) h->grid = std::max(1, prop.multiProcessorCount);
+    for (int l = 0; l < kMaxLanes; l++) {
+        h->lane_q[l] = kEmptyLane;
+        h->lane_records[l] = 0;
+    }
+    h->staged_cap = cfg->buffer_records > 0 ? cfg->buffer_records : (int64_t)1 << 26;
+    fg_handle* hp = h.get();
+    auto chk = [&](hipError_t e) { return e == hipSuccess; };
+    bool ok = chk(hp->st_key.ensure(8 * hp->staged_cap)) &&
+              (cfg->val_type == FG_VAL_NONE || chk(hp->st_val.ensure(8 * hp->staged_cap))) &&
+              chk(hp->st_null.ensure(hp->staged_cap)) &&
+              chk(hp->hist.ensure(4 * (size_t)hp->F * hp->grid)) &&
+              chk(hp->offsets.ensure(4 * ((size_t)hp->F * hp->grid + 1))) &&
+              chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F * hp->grid))) &&
+              chk(hp->counters.ensure(sizeof(Counters))) && chk(hp->h_counters.ensure(sizeof(Counters))) &&
+              chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) &&
+              chk(hp->h_scalars.ensure(64));
+    if (!ok) {
+        g_open_error = "device allocation failed";
+        return FG_EDEVICE;
+    }
+    *out = h.release();
+    return FG_OK;
+}
+
+int fg_add_batch(fg_handle* h, const fg_batch* b) {
+    if (!h || !b) return FG_EINVAL;
+    if (b->n <= 0) return FG_OK;
+    if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 records");
+    if (!b->key || !b->rowtime) return h->fail(FG_EINVAL, "batch key/rowtime columns are required");
+    if (h->cfg.val_type != FG_VAL_NONE && !b->val) return h->fail(FG_EINVAL, "batch value column is required");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int64_t n = b->n;
+    const int64_t *key = b->key, *ts = b->rowtime;
+    const int64_t* val = h->cfg.val_type != FG_VAL_NONE ? static_cast<const int64_t*>(b->val) : nullptr;
+    const uint8_t* vnull = b->val_null;
+    if (b->location == FG_HOST) {
+        HIPCHK(h, h->in_key.ensure(8 * n));
+        HIPCHK(h, h->in_ts.ensure(8 * n));
+        HIPCHK(h, hipMemcpyAsync(h->in_key.p, key, 8 * n, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->in_ts.p, ts, 8 * n, hipMemcpyHostToDevice, h->stream));
+        key = h->in_key.as<int64_t>();
+        ts = h->in_ts.as<int64_t>();
+        if (val) {
+            HIPCHK(h, h->in_val.ensure(8 * n));
+            HIPCHK(h, hipMemcpyAsync(h->in_val.p, val, 8 * n, hipMemcpyHostToDevice, h->stream));
+            val = h->in_val.as<int64_t>();
+        }
+        if (vnull) {
+            HIPCHK(h, h->in_null.ensure(n));
+            HIPCHK(h, hipMemcpyAsync(h->in_null.p, vnull, n, hipMemcpyHostToDevice, h->stream));
+            vnull = h->in_null.as<uint8_t>();
+        }
+    }
+    // EOFException semantics (RecordsWindowBuffer.java:91-96): flush, then retry
+    if (h->staged_n + n > h->staged_cap) {
+        int rc = flush(h);
+        if (rc) return rc;
+        if (n > h->staged_cap) {
+            HIPCHK(h, h->st_key.ensure(8 * n));
+            if (h->cfg.val_type != FG_VAL_NONE) HIPCHK(h, h->st_val.ensure(8 * n));
+            HIPCHK(h, h->st_null.ensure(n));
+            h->staged_cap = n;
+        }
+    }
+    h->records_in += n;
+    Counters c{};
+    int rc = ingest_pass(h, n, key, ts, val, vnull, JMIN, JMAX, true, &c);
+    h->late_dropped += (int64_t)c.drops;
+    if (rc == FG_OK) return FG_OK;
+    if (rc != -1) return rc;
+    // Lane conflict: the batch spans slices that do not fit the staged lanes. Flush and
+    // ingest the batch in slice ranges of `lanes` slices.
+    int64_t qlo = JMAX, qhi = JMIN;
+    for (int l = 0; l < h->lanes; l++) {
+        if (c.lane_min[l] > c.lane_max[l]) continue;
+        qlo = std::min<int64_t>(qlo, c.lane_min[l]);
+        qhi = std::max<int64_t>(qhi, c.lane_max[l]);
+    }
+    rc = flush(h);
+    if (rc) return rc;
+    for (int64_t lo = qlo; lo <= qhi; lo += h->lanes) {
+        Counters c2{};
+        rc = ingest_pass(h, n, key, ts, val, vnull, lo, lo + h->lanes, false, &c2);
+        if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
+        if (rc) return rc;
+        if (lo + h->lanes <= qhi) {
+            rc = flush(h);
+            if (rc) return rc;
+        }
+    }
+    return FG_OK;
+}
+
+int fg_flush(fg_handle* h) {
+    if (!h) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    return flush(h);
+}
+
+int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows* fired) {
+    if (!h) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    h->out_n = 0;
+    HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+    int rc;
+    if (h->cfg.mode == FG_MODE_SQL) {
+        // AbstractWindowAggProcessor.advanceProgress :178-192
+        if (wm > h->current_progress) {
+            h->current_progress = wm;
+            if (h->current_progress >= h->next_trigger) {
+                if (h->staged_n > 0 && is_window_fired(h->w, h->min_slice_end, wm)) {
+                    rc = flush(h);
+                    if (rc) return rc;
+                }
+                h->next_trigger = next_trigger_watermark(wm, h->w.slice);
+            }
+        }
+    } else {
+        // DataStream WindowOperator: records are in state before any timer fires
+        if (wm > h->current_progress) h->current_progress = wm;
+        if (h->staged_n > 0 && is_window_fired(h->w, h->min_slice_end, wm)) {
+            rc = flush(h);
+            if (rc) return rc;
+        }
+    }
+    const int64_t prev = h->timer_wm;
+    if (wm > prev) {
+        rc = fire_windows(h, prev, wm);
+        if (rc) return rc;
+    }
+    if (wm > h->timer_wm) h->timer_wm = wm;
+    h->rows_fired += h->out_n;
+    if (fired) {
+        std::memset(fired, 0, sizeof *fired);
+        fired->n = h->out_n;
+        fired->num_aggs = h->cfg.num_aggs;
+        fired->location = out_location;
+        if (out_location == FG_HOST) {
+            rc = copy_out_to_host(h, fired);
+            if (rc) return rc;
+        } else {
+            fired->key = h->o_key.as<int64_t>();
+            fired->window_start = h->o_ws.as<int64_t>();
+            fired->window_end = h->o_we.as<int64_t>();
+            fired->null_mask = h->o_null.as<uint8_t>();
+            fired->rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->o_rt.as<int64_t>() : nullptr;
+            for (int a = 0; a < h->cfg.num_aggs; a++) fired->agg[a] = h->o_agg[a].as<int64_t>();
+        }
+    }
+    return FG_OK;
+}
+
+int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark) {
+    if (!h || !out) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = flush(h);
+    if (rc) return rc;
+    // region counts of every resident slice
+    const size_t nt = h->tables.size();
+    HIPCHK(h, h->hs_counts.ensure(sizeof(uint32_t) * h->P * std::max<size_t>(nt, 1)));
+    size_t ti = 0;
+    for (auto& kv : h->tables) {
+        HIPCHK(h, hipMemcpyAsync(h->hs_counts.as<uint32_t>() + ti * h->P, kv.second->counts.p, 4 * h->P,
+                                 hipMemcpyDeviceToHost, h->stream));
+        ti++;
+    }
+    rc = sync(h);
+    if (rc) return rc;
+    int64_t total = 0;
+    HIPCHK(h, h->hs_off.ensure(sizeof(uint64_t) * h->P * std::max<size_t>(nt, 1)));
+    for (size_t t = 0; t < nt; t++) {
+        for (int r = 0; r < h->P; r++) {
+            h->hs_off.as<uint64_t>()[t * h->P + r] = (uint64_t)total;
+            total += h->hs_counts.as<uint32_t>()[t * h->P + r];
+        }
+    }
+    const size_t b8 = 8 * (size_t)std::max<int64_t>(total, 1);
+    HIPCHK(h, h->s_key.ensure(b8));
+    HIPCHK(h, h->s_slice.ensure(b8));
+    HIPCHK(h, h->s_cs.ensure(b8));
+    HIPCHK(h, h->s_cv.ensure(b8));
+    HIPCHK(h, h->s_sum.ensure(b8));
+    HIPCHK(h, h->s_off.ensure(sizeof(uint64_t) * h->P * std::max<size_t>(nt, 1)));
+    HIPCHK(h, hipMemcpyAsync(h->s_off.p, h->hs_off.p, sizeof(uint64_t) * h->P * nt, hipMemcpyHostToDevice, h->stream));
+    ti = 0;
+    for (auto& kv : h->tables) {
+        ExportParams p{};
+        p.t = ref_of(kv.second.get());
+        p.region_off = h->s_off.as<uint64_t>() + ti * h->P;
+        p.slice_end = kv.first;
+        p.out_key = h->s_key.as<int64_t>();
+        p.out_slice = h->s_slice.as<int64_t>();
+        p.out_cnt_star = h->s_cs.as<int64_t>();
+        p.out_cnt_val = h->s_cv.as<int64_t>();
+        p.out_sum = h->s_sum.as<int64_t>();
+        {
+            KTimer kt(h, K_EXPORT, 0);
+            HIPCHK(h, launch_export(p, h->P, h->stream));
+        }
+        ti++;
+    }
+    HIPCHK(h, h->hs_key.ensure(b8));
+    HIPCHK(h, h->hs_slice.ensure(b8));
+    HIPCHK(h, h->hs_cs.ensure(b8));
+    HIPCHK(h, h->hs_cv.ensure(b8));
+    HIPCHK(h, h->hs_sum.ensure(b8));
+    if (total > 0) {
+        HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->hs_sum.p, h->s_sum.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+    }
+    rc = sync(h);
+    if (rc) return rc;
+    out->n = total;
+    out->key = h->hs_key.as<int64_t>();
+    out->slice_end = h->hs_slice.as<int64_t>();
+    out->cnt_star = h->hs_cs.as<int64_t>();
+    out->cnt_val = h->hs_cv.as<int64_t>();
+    out->sum = h->hs_sum.as<int64_t>();
+    if (timer_watermark) *timer_watermark = h->timer_wm;
+    return FG_OK;
+}
+
+int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
+    if (!h || !in) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = flush(h);
+    if (rc) return rc;
+    // group entries by slice, bucket by region on the host (restore is off the hot path)
+    std::map<int64_t, std::vector<int64_t>> by_slice;
+    for (int64_t i = 0; i < in->n; i++) by_slice[in->slice_end[i]].push_back(i);
+    for (auto& kv : by_slice) {
+        const auto& idx = kv.second;
+        const int64_t m = (int64_t)idx.size();
+        std::vector<uint32_t> off(h->P + 1, 0);
+        std::vector<uint32_t> reg(m);
+        for (int64_t j = 0; j < m; j++) {
+            const int64_t k = in->key[idx[j]];
+            reg[j] = h->region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)k) >> (64 - h->region_bits));
+            off[reg[j] + 1]++;
+        }
+        for (int r = 0; r < h->P; r++) off[r + 1] += off[r];
+        std::vector<int64_t> k(m), cs(m), cn(m), sm(m);
+        std::vector<uint32_t> cur(off.begin(), off.end() - 1);
+        for (int64_t j = 0; j < m; j++) {
+            const int64_t i = idx[j];
+            const uint32_t at = cur[reg[j]]++;
+            k[at] = in->key[i];
+            cs[at] = in->cnt_star[i];
+            cn[at] = in->cnt_star[i] - in->cnt_val[i];
+            sm[at] = in->sum[i];
+        }
+        DevBuf dk, dcs, dcn, dsm, doff;
+        HIPCHK(h, dk.ensure(8 * std::max<int64_t>(m, 1)));
+        HIPCHK(h, dcs.ensure(8 * std::max<int64_t>(m, 1)));
+        HIPCHK(h, dcn.ensure(8 * std::max<int64_t>(m, 1)));
+        HIPCHK(h, dsm.ensure(8 * std::max<int64_t>(m, 1)));
+        HIPCHK(h, doff.ensure(4 * (h->P + 1)));
+        HIPCHK(h, hipMemcpy(dk.p, k.data(), 8 * m, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(dcs.p, cs.data(), 8 * m, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(dcn.p, cn.data(), 8 * m, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(dsm.p, sm.data(), 8 * m, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(doff.p, off.data(), 4 * (h->P + 1), hipMemcpyHostToDevice));
+        SliceTable* t = nullptr;
+        rc = table_get(h, kv.first, true, &t);
+        if (rc) return rc;
+        StagedBatch sb{};
+        sb.key = dk.as<int64_t>();
+        sb.val = dsm.as<int64_t>();
+        sb.cnt_star = dcs.as<int64_t>();
+        sb.cnt_null = dcn.as<int64_t>();
+        sb.bucket_off = doff.as<uint32_t>();
+        sb.is_acc = 1;
+        const StagedBatch* d_sb = nullptr;
+        rc = arena_put(h, &sb, 1, &d_sb);
+        if (rc) return rc;
+        TableRef tr = ref_of(t);
+        const TableRef* d_src = nullptr;
+        rc = arena_put(h, &tr, 1, &d_src);
+        if (rc) return rc;
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+        MergeParams p{};
+        p.region_bits = h->region_bits;
+        p.lanes = 1;
+        p.lane = 0;
+        p.n_src = 1;
+        p.src = d_src;
+        p.n_batches = 1;
+        p.batches = d_sb;
+        p.val_type = h->cfg.val_type;
+        p.has_dst = 1;
+        p.dst = tr;
+        p.overflow = h->scalars.as<unsigned int>();
+        p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+        {
+            KTimer kt(h, K_RESTORE, m);
+            HIPCHK(h, launch_merge(p, h->stream));
+        }
+        HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
+        rc = sync(h);
+        if (rc) return rc;
+        rc = check_overflow(h);
+        if (rc) return rc;
+        t->upper = std::min<int64_t>(t->upper + m, (int64_t)kRegionCap * h->P);
+    }
+    // open(): processor progress restarts at Long.MIN_VALUE; windows whose timers fired
+    // before the checkpoint stay fired (restored timer set)
+    h->current_progress = JMIN;
+    h->next_trigger = JMIN;
+    h->timer_wm = timer_watermark;
+    return FG_OK;
+}
+
+int fg_late_dropped(fg_handle* h, int64_t* out) {
+    if (!h || !out) return FG_EINVAL;
+    *out = h->late_dropped;
+    return FG_OK;
+}
+
+int fg_get_stats(fg_handle* h, fg_stats* out) {
+    if (!h || !out) return FG_EINVAL;
+    out->records_in = h->records_in;
+    out->records_staged = h->staged_n;
+    out->late_dropped = h->late_dropped;
+    out->rows_fired = h->rows_fired;
+    out->flushes = h->flushes;
+    out->live_slices = (int64_t)h->tables.size();
+    out->state_regions = h->P;
+    out->region_capacity = kRegionCap;
+    return FG_OK;
+}
+
+int fg_synchronize(fg_handle* h) {
+    if (!h) return FG_EINVAL;
+    return sync(h);
+}
+
+int fg_reset(fg_handle* h) {
+    if (!h) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    int rc = sync(h);
+    if (rc) return rc;
+    std::vector<int64_t> ends;
+    for (auto& kv : h->tables) ends.push_back(kv.first);
+    for (int64_t e : ends) table_free(h, e);
+    for (auto& s : h->staged) h->staged_pool.push_back(std::move(s));
+    h->staged.clear();
+    h->staged_n = 0;
+    for (int l = 0; l < kMaxLanes; l++) {
+        h->lane_q[l] = kEmptyLane;
+        h->lane_records[l] = 0;
+    }
+    h->min_slice_end = JMAX;
+    h->current_progress = JMIN;
+    h->next_trigger = JMIN;
+    h->timer_wm = JMIN;
+    h->late_dropped = 0;
+    h->out_n = 0;
+    return FG_OK;
+}
+
+int fg_kernel_stats(fg_handle* h, fg_kernel_stat* out, int32_t max, int32_t* count) {
+    if (!h || !count) return FG_EINVAL;
+    int rc = sync(h);
+    if (rc) return rc;
+    *count = K_NCLASS;
+    for (int c = 0; c < K_NCLASS && c < max; c++) {
+        std::memset(&out[c], 0, sizeof(fg_kernel_stat));
+        std::snprintf(out[c].name, sizeof out[c].name, "%s", kClassName[c]);
+        out[c].launches = h->kstat[c].launches;
+        out[c].total_ms = h->kstat[c].ms;
+        out[c].records = h->kstat[c].records;
+        out[c].rows = h->kstat[c].rows;
+    }
+    return FG_OK;
+}
+
+void* fg_stream(fg_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+const char* fg_last_error(fg_handle* h) { return h ? h->err.c_str() : g_open_error.c_str(); }
+
+void fg_close(fg_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipStreamSynchronize(h->stream);
+    {
+        // release device memory before the stream
+        h->tables.clear();
+        h->table_pool.clear();
+        h->staged.clear();
+        h->staged_pool.clear();
+    }
+    for (auto& p : h->pend) {
+        h->ev_pool.push_back(p.a);
+        h->ev_pool.push_back(p.b);
+    }
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    hipStream_t s = h->stream;
+    delete h;
+    if (s) (void)hipStreamDestroy(s);
+}
+
+int fg_key_groups(int32_t device_id, int32_t location, int64_t n, const int64_t* key, int32_t key_hash,
+                  int32_t max_parallelism, int32_t* out_kg) {
+    if (n <= 0) return FG_OK;
+    if (!key || !out_kg || max_parallelism <= 0) return FG_EINVAL;
+    if (hipSetDevice(device_id) != hipSuccess) return FG_EDEVICE;
+    if (location == FG_DEVICE) {
+        if (launch_key_groups(key, n, key_hash, max_parallelism, out_kg, nullptr) != hipSuccess) return FG_EDEVICE;
+        return hipDeviceSynchronize() == hipSuccess ? FG_OK : FG_EDEVICE;
+    }
+    int64_t* dk = nullptr;
+    int32_t* dout = nullptr;
+    if (hipMalloc(&dk, 8 * n) != hipSuccess) return FG_EDEVICE;
+    if (hipMalloc(&dout, 4 * n) != hipSuccess) {
+        (void)hipFree(dk);
+        return FG_EDEVICE;
+    }
+    int rc = FG_OK;
+    if (hipMemcpy(dk, key, 8 * n, hipMemcpyHostToDevice) != hipSuccess ||
+        launch_key_groups(dk, n, key_hash, max_parallelism, dout, nullptr) != hipSuccess ||
+        hipMemcpy(out_kg, dout, 4 * n, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = FG_EDEVICE;
+    (void)hipFree(dk);
+    (void)hipFree(dout);
+    return rc;
+}
+
+int fg_partition_by_owner(int32_t device_id, void* stream, int64_t n, const int64_t* key, const int64_t* rowtime,
+                          const int64_t* val, int32_t key_hash, int32_t max_parallelism, int32_t parallelism,
+                          int64_t* out_key, int64_t* out_rowtime, int64_t* out_val, int64_t* counts) {
+    if (n < 0 || n > (int64_t)0x7fffffff || parallelism < 1 || max_parallelism < parallelism) return FG_EINVAL;
+    if (hipSetDevice(device_id) != hipSuccess) return FG_EDEVICE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const size_t words = partition_scratch_words(n, parallelism);
+    uint32_t* scratch = nullptr;
+    if (hipMallocAsync((void**)&scratch, 4 * words, s) != hipSuccess) return FG_EDEVICE;
+    hipError_t e = launch_partition_by_owner(key, rowtime, val, n, key_hash, max_parallelism, parallelism, out_key,
+                                             out_rowtime, out_val, counts, scratch, words, s);
+    (void)hipFreeAsync(scratch, s);
+    if (e != hipSuccess) return FG_EDEVICE;
+    return hipStreamSynchronize(s) == hipSuccess ? FG_OK : FG_EDEVICE;
+}
+
+}  // extern "C"

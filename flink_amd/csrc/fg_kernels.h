@@ -1,0 +1,125 @@
+// fg_kernels.h -- launch interface of the gfx950 kernels (internal to libflinkgpu.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fg_window.h"
+
+namespace fg {
+
+// LDS hash table of one state region: kSlots open-addressing slots + 1 slot reserved
+// for the key that equals the EMPTY sentinel (Long.MIN_VALUE).
+constexpr int kSlotBits = 12;
+constexpr int kSlots = 1 << kSlotBits;        // 4096 slots x 32 B = 128 KiB of LDS
+constexpr int kRegionCap = 3584;              // max entries per region in HBM (87.5 % of kSlots)
+constexpr int kMergeThreads = 1024;
+constexpr int kIngestThreads = 1024;
+constexpr int kMaxLanes = 4;
+constexpr int kMaxAggs = 8;
+
+// One slice table in HBM: P regions, each region an SoA block of kRegionCap entries:
+//   [key i64 x cap][cnt_star i64 x cap][cnt_null i64 x cap][sum (i64 | f64 bits) x cap]
+// cnt_val = cnt_star - cnt_null.
+struct TableRef {
+    int64_t* base;
+    uint32_t* counts;   // entries per region
+};
+
+// A staged batch (records already bucketed by (lane, region)).
+struct StagedBatch {
+    const int64_t* key;
+    const int64_t* val;        // value bits, or the `sum` accumulator when is_acc
+    const uint8_t* vnull;      // may be null
+    const int64_t* cnt_star;   // only when is_acc (restore images)
+    const int64_t* cnt_null;   // only when is_acc
+    const uint32_t* bucket_off;  // [lanes * P + 1]
+    int32_t is_acc;
+    int32_t pad;
+};
+
+struct IngestParams {
+    WindowSpec w;
+    int64_t n;
+    const int64_t* key;
+    const int64_t* ts;
+    const int64_t* val;
+    const uint8_t* vnull;
+    int64_t progress;          // current progress (watermark) for the late check
+    int32_t lanes;             // power of two <= kMaxLanes
+    int32_t region_bits;       // log2(P)
+    int64_t filter_lo;         // slice-index filter [lo, hi): floor_div(target, slice)
+    int64_t filter_hi;
+    int32_t count_drops;
+    int32_t grid;              // number of workgroups (segments)
+    int32_t vec;               // 1: key/ts/val 16-byte aligned -> paired 16-B loads
+    int32_t pad0;
+    // count outputs
+    uint32_t* hist;            // [F][grid]
+    unsigned long long* drops;
+    long long* lane_min;       // [kMaxLanes] slice index
+    long long* lane_max;
+    // scatter inputs/outputs
+    const uint32_t* offsets;   // exclusive scan of hist, [F][grid] (+1)
+    int64_t* st_key;
+    int64_t* st_val;
+    uint8_t* st_null;
+};
+
+struct MergeParams {
+    int32_t region_bits;
+    int32_t lanes;
+    int32_t lane;              // bucket lane of staged records (-1: none)
+    int32_t n_src;
+    const TableRef* src;       // device array [n_src]
+    int32_t n_batches;
+    int32_t val_type;          // 0 none, 1 i64, 2 f64
+    const StagedBatch* batches;  // device array [n_batches]
+    int32_t has_dst;
+    int32_t emit;
+    TableRef dst;
+    unsigned long long* dst_total;  // += entries written to dst (may be null)
+    // emit
+    int64_t wstart, wend, out_ts;
+    int32_t num_aggs;
+    int32_t aggs[kMaxAggs];
+    int64_t* out_key;
+    int64_t* out_ws;
+    int64_t* out_we;
+    int64_t* out_agg[kMaxAggs];
+    uint8_t* out_null;
+    int64_t* out_rowtime;      // may be null
+    unsigned long long* out_count;
+    int64_t out_cap;
+    unsigned int* overflow;    // bit0: region overflow, bit1: output overflow, bit2: LDS table full
+};
+
+struct ExportParams {
+    TableRef t;
+    const uint64_t* region_off;  // [P] exclusive prefix of counts
+    int64_t slice_end;
+    int64_t* out_key;
+    int64_t* out_slice;
+    int64_t* out_cnt_star;
+    int64_t* out_cnt_val;
+    int64_t* out_sum;
+};
+
+hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s);
+hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s);
+// exclusive scan of n u32 (n < 2^32 total); out has n + 1 entries; tmp >= scan_tmp_words(n)
+size_t scan_tmp_words(int64_t n);
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, hipStream_t s);
+// bucket_off[b] = offsets[b * grid] for b in [0, F]; bucket_off[F] = offsets[F * grid]
+hipError_t launch_bucket_offsets(const uint32_t* offsets, uint32_t* bucket_off, int32_t F, int32_t grid,
+                                 hipStream_t s);
+hipError_t launch_merge(const MergeParams& p, hipStream_t s);
+hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
+hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out,
+                             hipStream_t s);
+hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n,
+                                     int32_t key_hash, int32_t max_p, int32_t parallelism, int64_t* out_key,
+                                     int64_t* out_ts, int64_t* out_val, int64_t* counts, uint32_t* scratch,
+                                     size_t scratch_words, hipStream_t s);
+size_t partition_scratch_words(int64_t n, int32_t parallelism);
+
+}  // namespace fg

@@ -1,0 +1,597 @@
+// fg_kernels.hip -- gfx950 kernels of the keyed window-aggregation engine.
+//
+// Hot path:
+//   k_ingest_count / k_ingest_scatter  a1 slice assignment + a2 late rules + a3 key hashing,
+//                                      bucketing records by (slice lane, state region):
+//                                      replaces RecordsWindowBuffer.addElement
+//                                      (TR/operators/aggregate/window/buffers/RecordsWindowBuffer.java:81-97)
+//   k_merge                            a4/a5/a7: one workgroup per state region builds an LDS
+//                                      open-addressing table from resident slice regions and the
+//                                      staged records, then writes the region back (flush =
+//                                      AggCombiner.combine, combines/AggCombiner.java:76-115)
+//                                      and/or emits fired rows (fireWindow + mergeSlices,
+//                                      processors/SliceSharedWindowAggProcessor.java:64-118)
+//   k_export                           checkpoint image of the resident state
+//   k_key_groups / k_owner_*           KeyGroupRangeAssignment routing for the key-group exchange
+//
+// All global traffic is streaming and coalesced; per-key read-modify-write happens in LDS
+// (ds_cmpst_rtn_b64 / ds_add_u64 / ds_add_f64), never as global atomics.
+#include <hip/hip_runtime.h>
+
+#include "fg_kernels.h"
+
+namespace fg {
+
+// ----------------------------------------------------------------------------------------
+// record classification shared by count and scatter (must agree exactly)
+// ----------------------------------------------------------------------------------------
+// returns bucket >= 0, -1 when the record is late-dropped, -2 when outside the slice filter
+__device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int64_t ts, int64_t* q_out) {
+    int64_t target;
+    if (!target_slice(p.w, ts, p.progress, &target)) return -1;
+    int64_t q = floor_div_fast(target, p.w.slice, p.w.rslice);
+    if (q < p.filter_lo || q >= p.filter_hi) return -2;
+    *q_out = q;
+    const int lane = (int)(q & (int64_t)(p.lanes - 1));
+    const uint32_t region = p.region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.region_bits));
+    return (lane << p.region_bits) | (int)region;
+}
+
+__device__ __forceinline__ void seg_bounds(int64_t n, int grid, int g, int64_t* b, int64_t* e) {
+    int64_t per = (n + grid - 1) / grid;
+    per = (per + 1) & ~int64_t(1);   // even, so pair loads stay aligned
+    *b = per * g < n ? per * g : n;
+    *e = *b + per < n ? *b + per : n;
+}
+
+// ----------------------------------------------------------------------------------------
+// ingest: count
+// ----------------------------------------------------------------------------------------
+constexpr int kMaxBuckets = 32768;   // lanes * P held in LDS (128 KiB)
+
+__global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p) {
+    __shared__ uint32_t s_hist[kMaxBuckets];
+    __shared__ unsigned long long s_drop;
+    __shared__ long long s_lmin[kMaxLanes], s_lmax[kMaxLanes];
+    const int F = p.lanes << p.region_bits;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
+    if (tid == 0) s_drop = 0;
+    if (tid < kMaxLanes) { s_lmin[tid] = JMAX; s_lmax[tid] = JMIN; }
+    __syncthreads();
+
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    uint32_t drops = 0;
+    long long lmin[kMaxLanes], lmax[kMaxLanes];
+#pragma unroll
+    for (int l = 0; l < kMaxLanes; l++) { lmin[l] = JMAX; lmax[l] = JMIN; }
+
+    // pairs of records per thread: 16-byte loads of key and rowtime
+    const int64_t npairs = (end - beg) >> 1;
+    for (int64_t pi = tid; pi < npairs; pi += kIngestThreads) {
+        const int64_t i = beg + 2 * pi;
+        longlong2 k2, t2;
+        if (p.vec) {
+            k2 = *reinterpret_cast<const longlong2*>(p.key + i);
+            t2 = *reinterpret_cast<const longlong2*>(p.ts + i);
+        } else {
+            k2.x = p.key[i]; k2.y = p.key[i + 1];
+            t2.x = p.ts[i]; t2.y = p.ts[i + 1];
+        }
+        int64_t q;
+        int b = classify(p, k2.x, t2.x, &q);
+        if (b >= 0) {
+            atomicAdd(&s_hist[b], 1u);
+            const int l = (int)(q & (p.lanes - 1));
+            lmin[l] = q < lmin[l] ? q : lmin[l];
+            lmax[l] = q > lmax[l] ? q : lmax[l];
+        } else if (b == -1) drops++;
+        b = classify(p, k2.y, t2.y, &q);
+        if (b >= 0) {
+            atomicAdd(&s_hist[b], 1u);
+            const int l = (int)(q & (p.lanes - 1));
+            lmin[l] = q < lmin[l] ? q : lmin[l];
+            lmax[l] = q > lmax[l] ? q : lmax[l];
+        } else if (b == -1) drops++;
+    }
+    if (((end - beg) & 1) && tid == 0) {
+        const int64_t i = end - 1;
+        int64_t q;
+        int b = classify(p, p.key[i], p.ts[i], &q);
+        if (b >= 0) {
+            atomicAdd(&s_hist[b], 1u);
+            const int l = (int)(q & (p.lanes - 1));
+            lmin[l] = q < lmin[l] ? q : lmin[l];
+            lmax[l] = q > lmax[l] ? q : lmax[l];
+        } else if (b == -1) drops++;
+    }
+    // wave reductions, then one LDS atomic per wave
+    for (int off = 32; off > 0; off >>= 1) drops += __shfl_down(drops, off);
+#pragma unroll
+    for (int l = 0; l < kMaxLanes; l++) {
+        long long a = lmin[l], z = lmax[l];
+        for (int off = 32; off > 0; off >>= 1) {
+            long long oa = __shfl_down(a, off), oz = __shfl_down(z, off);
+            a = oa < a ? oa : a;
+            z = oz > z ? oz : z;
+        }
+        lmin[l] = a;
+        lmax[l] = z;
+    }
+    if ((tid & 63) == 0) {
+        if (drops) atomicAdd(&s_drop, (unsigned long long)drops);
+#pragma unroll
+        for (int l = 0; l < kMaxLanes; l++) {
+            if (lmin[l] != JMAX) atomicMin(&s_lmin[l], lmin[l]);
+            if (lmax[l] != JMIN) atomicMax(&s_lmax[l], lmax[l]);
+        }
+    }
+    __syncthreads();
+    // bucket-major histogram: hist[b * grid + g]
+    for (int b = tid; b < F; b += kIngestThreads) p.hist[(int64_t)b * p.grid + blockIdx.x] = s_hist[b];
+    if (tid == 0 && p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
+    if (tid < kMaxLanes) {
+        if (s_lmin[tid] != JMAX) atomicMin(&p.lane_min[tid], s_lmin[tid]);
+        if (s_lmax[tid] != JMIN) atomicMax(&p.lane_max[tid], s_lmax[tid]);
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// ingest: scatter into the staged buffer (bucket-major; within a (bucket, workgroup)
+// run the order is arrival order up to LDS atomic ordering)
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter(IngestParams p) {
+    __shared__ uint32_t s_cur[kMaxBuckets];
+    const int F = p.lanes << p.region_bits;
+    const int tid = threadIdx.x;
+    for (int b = tid; b < F; b += kIngestThreads) s_cur[b] = p.offsets[(int64_t)b * p.grid + blockIdx.x];
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    const bool has_val = p.val != nullptr;
+    const bool has_null = p.vnull != nullptr;
+    const int64_t npairs = (end - beg) >> 1;
+    for (int64_t pi = tid; pi < npairs; pi += kIngestThreads) {
+        const int64_t i = beg + 2 * pi;
+        longlong2 k2, t2, v2 = {0, 0};
+        if (p.vec) {
+            k2 = *reinterpret_cast<const longlong2*>(p.key + i);
+            t2 = *reinterpret_cast<const longlong2*>(p.ts + i);
+            if (has_val) v2 = *reinterpret_cast<const longlong2*>(p.val + i);
+        } else {
+            k2.x = p.key[i]; k2.y = p.key[i + 1];
+            t2.x = p.ts[i]; t2.y = p.ts[i + 1];
+            if (has_val) { v2.x = p.val[i]; v2.y = p.val[i + 1]; }
+        }
+        int64_t q;
+        int b = classify(p, k2.x, t2.x, &q);
+        if (b >= 0) {
+            const uint32_t pos = atomicAdd(&s_cur[b], 1u);
+            p.st_key[pos] = k2.x;
+            if (has_val) p.st_val[pos] = v2.x;
+            if (has_null) p.st_null[pos] = p.vnull[i];
+        }
+        b = classify(p, k2.y, t2.y, &q);
+        if (b >= 0) {
+            const uint32_t pos = atomicAdd(&s_cur[b], 1u);
+            p.st_key[pos] = k2.y;
+            if (has_val) p.st_val[pos] = v2.y;
+            if (has_null) p.st_null[pos] = p.vnull[i + 1];
+        }
+    }
+    if (((end - beg) & 1) && tid == 0) {
+        const int64_t i = end - 1;
+        int64_t q;
+        int b = classify(p, p.key[i], p.ts[i], &q);
+        if (b >= 0) {
+            const uint32_t pos = atomicAdd(&s_cur[b], 1u);
+            p.st_key[pos] = p.key[i];
+            if (has_val) p.st_val[pos] = p.val[i];
+            if (has_null) p.st_null[pos] = p.vnull[i];
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------------------
+// exclusive scan of u32 (reduce-then-scan, 4096 items per block)
+// ----------------------------------------------------------------------------------------
+constexpr int kScanThreads = 1024;
+constexpr int kScanItems = 4;
+constexpr int kScanChunk = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        const int nw = blockDim.x >> 6;
+        uint32_t w = lane < nw ? s_wave[lane] : 0u;
+        for (int off = 1; off < 64; off <<= 1) {
+            uint32_t y = __shfl_up(w, off);
+            if (lane >= off) w += y;
+        }
+        if (lane < nw) s_wave[lane] = w;   // inclusive
+    }
+    __syncthreads();
+    const uint32_t wave_base = wave ? s_wave[wave - 1] : 0u;
+    *total = s_wave[(blockDim.x >> 6) - 1];
+    __syncthreads();
+    return wave_base + x - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* in, int64_t n, uint32_t* sums) {
+    __shared__ uint32_t s_wave[16];
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) v += (base + j < n) ? in[base + j] : 0u;
+    uint32_t total;
+    block_exclusive_scan(v, s_wave, &total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_blocks(uint32_t* sums, int64_t nb) {
+    __shared__ uint32_t s_wave[16];
+    __shared__ uint32_t s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (int64_t b0 = 0; b0 < nb; b0 += kScanThreads) {
+        const int64_t i = b0 + threadIdx.x;
+        uint32_t v = i < nb ? sums[i] : 0u;
+        uint32_t total;
+        uint32_t ex = block_exclusive_scan(v, s_wave, &total);
+        const uint32_t carry = s_carry;
+        if (i < nb) sums[i] = carry + ex;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry = carry + total;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_final(const uint32_t* in, int64_t n, const uint32_t* sums,
+                                                             uint32_t* out) {
+    __shared__ uint32_t s_wave[16];
+    const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t t = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        v[j] = (base + j < n) ? in[base + j] : 0u;
+        t += v[j];
+    }
+    uint32_t total;
+    uint32_t ex = block_exclusive_scan(t, s_wave, &total) + sums[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kScanItems; j++) {
+        if (base + j < n) out[base + j] = ex;
+        ex += v[j];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = sums[blockIdx.x] + total;
+}
+
+size_t scan_tmp_words(int64_t n) { return (size_t)((n + kScanChunk - 1) / kScanChunk) + 1; }
+
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, hipStream_t s) {
+    const int64_t nb = (n + kScanChunk - 1) / kScanChunk;
+    if (nb == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, n, tmp);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, tmp, nb);
+    hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, n, tmp, out);
+    return hipGetLastError();
+}
+
+__global__ void k_bucket_offsets(const uint32_t* offsets, uint32_t* bucket_off, int32_t F, int32_t grid) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b <= F) bucket_off[b] = offsets[(int64_t)b * grid];
+}
+
+hipError_t launch_bucket_offsets(const uint32_t* offsets, uint32_t* bucket_off, int32_t F, int32_t grid,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(k_bucket_offsets, dim3((F + 1 + 255) / 256), dim3(256), 0, s, offsets, bucket_off, F, grid);
+    return hipGetLastError();
+}
+
+hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_ingest_count, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    return hipGetLastError();
+}
+hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_ingest_scatter, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// merge: one workgroup per state region
+// ----------------------------------------------------------------------------------------
+struct LdsTable {
+    int64_t key[kSlots + 1];                  // slot kSlots: the key equal to the sentinel
+    unsigned long long cs[kSlots + 1];        // COUNT(*)
+    unsigned long long cn[kSlots + 1];        // records whose value was NULL
+    unsigned long long sum[kSlots + 1];       // SUM / AVG sum (i64, or f64 bits)
+};
+
+__device__ __forceinline__ int lds_find_or_insert(LdsTable& t, int64_t k, bool& full) {
+    if (k == JMIN) return kSlots;
+    uint32_t slot = (uint32_t)fmix64((uint64_t)k) & (kSlots - 1);
+    for (int probe = 0; probe < kSlots; probe++) {
+        const int64_t cur = t.key[slot];
+        if (cur == k) return (int)slot;
+        if (cur == JMIN) {
+            const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&t.key[slot]),
+                                                     (unsigned long long)JMIN, (unsigned long long)k);
+            if (old == (unsigned long long)JMIN || old == (unsigned long long)k) return (int)slot;
+        }
+        slot = (slot + 1) & (kSlots - 1);
+    }
+    full = true;
+    return -1;
+}
+
+__device__ __forceinline__ void lds_add(LdsTable& t, int slot, unsigned long long cs, unsigned long long cn,
+                                        int64_t sum_bits, int vt) {
+    atomicAdd(&t.cs[slot], cs);
+    if (cn) atomicAdd(&t.cn[slot], cn);
+    if (vt == 2) {
+        atomicAdd(reinterpret_cast<double*>(&t.sum[slot]), __longlong_as_double(sum_bits));
+    } else if (vt == 1) {
+        atomicAdd(&t.sum[slot], (unsigned long long)sum_bits);
+    }
+}
+
+__global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
+    __shared__ LdsTable t;
+    __shared__ uint32_t s_wave[16];
+    __shared__ unsigned int s_flags;
+    __shared__ unsigned long long s_out_base;
+    const int r = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int cap = kRegionCap;
+    const int vt = p.val_type;
+
+    for (int i = tid; i <= kSlots; i += kMergeThreads) {
+        t.key[i] = JMIN;
+        t.cs[i] = 0;
+        t.cn[i] = 0;
+        t.sum[i] = 0;
+    }
+    if (tid == 0) s_flags = 0;
+    __syncthreads();
+    bool full = false;
+
+    // 1) resident slice regions (state) ----------------------------------------------
+    for (int j = 0; j < p.n_src; j++) {
+        const TableRef src = p.src[j];
+        const uint32_t n = src.counts[r];
+        const int64_t* base = src.base + (int64_t)r * 4 * cap;
+        for (uint32_t i = tid; i < n; i += kMergeThreads) {
+            const int64_t k = base[i];
+            const int slot = lds_find_or_insert(t, k, full);
+            if (slot >= 0) lds_add(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
+                                   base[3 * cap + i], vt);
+        }
+    }
+    // 2) staged records of bucket (lane, r) over all staged batches --------------------
+    if (p.lane >= 0) {
+        const int b = (p.lane << p.region_bits) | r;
+        for (int j = 0; j < p.n_batches; j++) {
+            const StagedBatch sb = p.batches[j];
+            const uint32_t beg = sb.bucket_off[b], end = sb.bucket_off[b + 1];
+            if (sb.is_acc) {
+                for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                    const int slot = lds_find_or_insert(t, sb.key[i], full);
+                    if (slot >= 0)
+                        lds_add(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
+                                sb.val[i], vt);
+                }
+            } else {
+                for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                    const int slot = lds_find_or_insert(t, sb.key[i], full);
+                    if (slot < 0) continue;
+                    const bool isnull = sb.vnull != nullptr && sb.vnull[i];
+                    const int64_t v = (vt != 0 && !isnull) ? sb.val[i] : 0;
+                    lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, v, isnull ? 0 : vt);
+                }
+            }
+        }
+    }
+    if (full) atomicOr(&s_flags, 4u);
+    __syncthreads();
+
+    // 3) compaction: thread tid owns slots [4 tid, 4 tid + 4); tid 0 also owns kSlots --
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) mine += t.cs[tid * 4 + j] != 0 ? 1u : 0u;
+    if (tid == 0 && t.cs[kSlots] != 0) mine += 1;
+    uint32_t total;
+    uint32_t pos = block_exclusive_scan(mine, s_wave, &total);
+    if (tid == 0) {
+        unsigned int fl = s_flags;
+        if (p.has_dst && total > (uint32_t)cap) fl |= 1u;
+        if (p.emit) {
+            const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
+            s_out_base = ob;
+            if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
+        }
+        s_flags = fl;
+        if (fl) atomicOr(p.overflow, fl);
+    }
+    __syncthreads();
+    const unsigned int fl = s_flags;
+    const bool write_dst = p.has_dst && !(fl & 1u) && !(fl & 4u);
+    const bool write_out = p.emit && !(fl & 2u) && !(fl & 4u);
+    int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
+    const unsigned long long obase = s_out_base;
+
+    auto emit_slot = [&](int slot, uint32_t at) {
+        const int64_t k = slot == kSlots ? JMIN : t.key[slot];
+        const unsigned long long cs = t.cs[slot], cn = t.cn[slot];
+        const int64_t sum = (int64_t)t.sum[slot];
+        if (write_dst) {
+            dbase[at] = k;
+            dbase[cap + at] = (int64_t)cs;
+            dbase[2 * cap + at] = (int64_t)cn;
+            dbase[3 * cap + at] = sum;
+        }
+        if (write_out) {
+            const unsigned long long o = obase + at;
+            p.out_key[o] = k;
+            p.out_ws[o] = p.wstart;
+            p.out_we[o] = p.wend;
+            if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
+            const int64_t cv = (int64_t)(cs - cn);
+            uint8_t nm = 0;
+#pragma unroll
+            for (int a = 0; a < kMaxAggs; a++) {
+                if (a >= p.num_aggs) break;
+                int64_t v = 0;
+                switch (p.aggs[a]) {
+                    case 0: v = (int64_t)cs; break;   // COUNT(*)
+                    case 1: v = cv; break;            // COUNT(v)
+                    case 2:                           // SUM(v): NULL when no non-null value
+                        if (cv == 0) nm |= (uint8_t)(1u << a);
+                        else v = sum;
+                        break;
+                    default:                          // AVG(v): count == 0 ? NULL : sum / count
+                        if (cv == 0) nm |= (uint8_t)(1u << a);
+                        else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
+                        else v = sum / cv;
+                        break;
+                }
+                p.out_agg[a][o] = v;
+            }
+            p.out_null[o] = nm;
+        }
+    };
+    uint32_t at = pos;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int slot = tid * 4 + j;
+        if (t.cs[slot] != 0) emit_slot(slot, at++);
+    }
+    if (tid == 0 && t.cs[kSlots] != 0) emit_slot(kSlots, at++);
+
+    if (tid == 0 && write_dst) {
+        const uint32_t old = p.dst.counts[r];
+        p.dst.counts[r] = total;
+        if (p.dst_total) atomicAdd(p.dst_total, (unsigned long long)((int64_t)total - (int64_t)old));
+    }
+}
+
+hipError_t launch_merge(const MergeParams& p, hipStream_t s) {
+    hipLaunchKernelGGL(k_merge, dim3(1u << p.region_bits), dim3(kMergeThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// export (checkpoint image)
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_export(ExportParams p) {
+    const int r = blockIdx.x;
+    const uint32_t n = p.t.counts[r];
+    const int64_t* base = p.t.base + (int64_t)r * 4 * kRegionCap;
+    const uint64_t o = p.region_off[r];
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        const int64_t cs = base[kRegionCap + i], cn = base[2 * kRegionCap + i];
+        p.out_key[o + i] = base[i];
+        p.out_slice[o + i] = p.slice_end;
+        p.out_cnt_star[o + i] = cs;
+        p.out_cnt_val[o + i] = cs - cn;
+        p.out_sum[o + i] = base[3 * kRegionCap + i];
+    }
+}
+
+hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s) {
+    hipLaunchKernelGGL(k_export, dim3(regions), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// key groups and owner partitioning (keyBy exchange)
+// ----------------------------------------------------------------------------------------
+__global__ void k_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = key_group_of(key[i], key_hash, max_p);
+}
+
+hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out,
+                             hipStream_t s) {
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_key_groups, dim3((unsigned)blocks), dim3(256), 0, s, key, n, key_hash, max_p, out);
+    return hipGetLastError();
+}
+
+constexpr int kOwnerGrid = 512;
+constexpr int kOwnerThreads = 256;
+constexpr int kMaxOwners = 1024;
+
+__device__ __forceinline__ int owner_of(int64_t key, int32_t key_hash, int32_t max_p, int32_t par) {
+    return key_group_of(key, key_hash, max_p) * par / max_p;   // computeOperatorIndexForKeyGroup
+}
+
+__global__ __launch_bounds__(kOwnerThreads) void k_owner_count(const int64_t* key, int64_t n, int32_t key_hash,
+                                                                int32_t max_p, int32_t par, uint32_t* hist) {
+    __shared__ uint32_t s[kMaxOwners];
+    for (int i = threadIdx.x; i < par; i += kOwnerThreads) s[i] = 0;
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(n, kOwnerGrid, blockIdx.x, &beg, &end);
+    for (int64_t i = beg + threadIdx.x; i < end; i += kOwnerThreads) atomicAdd(&s[owner_of(key[i], key_hash, max_p, par)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < par; i += kOwnerThreads) hist[(int64_t)i * kOwnerGrid + blockIdx.x] = s[i];
+}
+
+__global__ __launch_bounds__(kOwnerThreads) void k_owner_scatter(const int64_t* key, const int64_t* ts,
+                                                                  const int64_t* val, int64_t n, int32_t key_hash,
+                                                                  int32_t max_p, int32_t par, const uint32_t* offsets,
+                                                                  int64_t* ok, int64_t* ot, int64_t* ov) {
+    __shared__ uint32_t s[kMaxOwners];
+    for (int i = threadIdx.x; i < par; i += kOwnerThreads) s[i] = offsets[(int64_t)i * kOwnerGrid + blockIdx.x];
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(n, kOwnerGrid, blockIdx.x, &beg, &end);
+    for (int64_t i = beg + threadIdx.x; i < end; i += kOwnerThreads) {
+        const int64_t k = key[i];
+        const uint32_t pos = atomicAdd(&s[owner_of(k, key_hash, max_p, par)], 1u);
+        ok[pos] = k;
+        ot[pos] = ts[i];
+        if (val) ov[pos] = val[i];
+    }
+}
+
+__global__ void k_owner_counts(const uint32_t* offsets, int32_t par, int64_t* counts) {
+    const int i = threadIdx.x;
+    if (i < par) counts[i] = (int64_t)offsets[(int64_t)(i + 1) * kOwnerGrid] - (int64_t)offsets[(int64_t)i * kOwnerGrid];
+}
+
+size_t partition_scratch_words(int64_t n, int32_t par) {
+    const int64_t m = (int64_t)par * kOwnerGrid;
+    return (size_t)(2 * m + 1) + scan_tmp_words(m);
+}
+
+hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n,
+                                     int32_t key_hash, int32_t max_p, int32_t par, int64_t* out_key,
+                                     int64_t* out_ts, int64_t* out_val, int64_t* counts, uint32_t* scratch,
+                                     size_t scratch_words, hipStream_t s) {
+    if (par < 1 || par > kMaxOwners || scratch_words < partition_scratch_words(n, par)) return hipErrorInvalidValue;
+    const int64_t m = (int64_t)par * kOwnerGrid;
+    uint32_t* hist = scratch;
+    uint32_t* offs = scratch + m;
+    uint32_t* tmp = scratch + 2 * m + 1;
+    hipLaunchKernelGGL(k_owner_count, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, n, key_hash, max_p, par, hist);
+    hipError_t e = launch_scan_u32(hist, offs, m, tmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_owner_scatter, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, ts, val, n, key_hash, max_p,
+                       par, offs, out_key, out_ts, out_val);
+    hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
+    return hipGetLastError();
+}
+
+}  // namespace fg

@@ -1,0 +1,267 @@
+"""Host-side mirror of the reference's window-aggregation operators over libflinkgpu.
+
+``WindowAggOperator`` keeps the operator surface of
+  * SQL:  ``SlicingWindowOperator`` built by ``SlicingWindowAggOperatorBuilder``
+          (TR/operators/window/slicing/SlicingWindowOperator.java:196-242,
+           TR/operators/aggregate/window/SlicingWindowAggOperatorBuilder.java:127-170), and
+  * DataStream: ``WindowOperator`` for ``keyBy().window(Tumbling|SlidingEventTimeWindows).sum()``
+          (SJ/runtime/operators/windowing/WindowOperator.java:300-503),
+with the same names, argument meaning and error behaviour:
+
+  processElement (batched)      -> process_batch(key, rowtime, val, val_null)
+  processWatermark              -> process_watermark(wm)  (returns the fired rows)
+  prepareSnapshotPreBarrier     -> prepare_snapshot_pre_barrier()
+  snapshotState / initializeState -> snapshot_state() / restore_state()
+  getNumLateRecordsDropped      -> num_late_records_dropped
+
+The window spec factories mirror ``SliceAssigners.tumbling/hopping/cumulative``
+(TR/operators/window/slicing/SliceAssigners.java:59-96) and raise ``WindowSpecError``
+(a ValueError) with the reference's IllegalArgumentException message.
+
+All compute runs in libflinkgpu.so (HIP, gfx950). Inputs may be numpy arrays (host,
+copied H2D) or device tensors (torch CUDA tensors / objects exposing
+``__cuda_array_interface__``), which are consumed in place.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+AGG_NAMES = {L.AGG_COUNT_STAR: "count_star", L.AGG_COUNT: "count", L.AGG_SUM: "sum", L.AGG_AVG: "avg"}
+AGGS = {"count_star": L.AGG_COUNT_STAR, "count": L.AGG_COUNT, "sum": L.AGG_SUM, "avg": L.AGG_AVG}
+
+
+@dataclass(frozen=True)
+class Window:
+    kind: int
+    size: int
+    slide: int = 0
+    offset: int = 0
+
+
+def tumbling(size_ms: int, offset_ms: int = 0) -> Window:
+    """SliceAssigners.tumbling (:59-62) / TumblingEventTimeWindows.of."""
+    return Window(L.TUMBLE, int(size_ms), 0, int(offset_ms))
+
+
+def hopping(size_ms: int, slide_ms: int, offset_ms: int = 0) -> Window:
+    """SliceAssigners.hopping (:75-79) / SlidingEventTimeWindows.of (DataStream)."""
+    return Window(L.HOP, int(size_ms), int(slide_ms), int(offset_ms))
+
+
+def cumulative(max_size_ms: int, step_ms: int, offset_ms: int = 0) -> Window:
+    """SliceAssigners.cumulative (:92-96)."""
+    return Window(L.CUMULATE, int(max_size_ms), int(step_ms), int(offset_ms))
+
+
+def _dev_ptr(x):
+    """(pointer, is_device) of a column: torch tensor, CUDA-array-interface object or numpy."""
+    if x is None:
+        return None, False, None
+    if hasattr(x, "is_cuda") and hasattr(x, "data_ptr"):
+        if x.is_cuda:
+            assert x.is_contiguous(), "device columns must be contiguous"
+            return x.data_ptr(), True, x
+        x = x.numpy()
+    if hasattr(x, "__cuda_array_interface__"):
+        return x.__cuda_array_interface__["data"][0], True, x
+    return None, False, x
+
+
+class WindowAggOperator:
+    """SlicingWindowOperator / WindowOperator with the buffer, state and firing on an MI355X."""
+
+    def __init__(self, window: Window, aggs=("count_star", "count", "sum", "avg"), val_type: str = "f64",
+                 mode: str = "sql", shift_tz_offset_ms: int = 0, expected_keys: int = 1 << 16,
+                 buffer_records: int = 1 << 22, device: int = 0, max_parallelism: int = 128,
+                 key_group_range=(0, 127), kernel_timing: bool = False):
+        lib = L.load()
+        self.window = window
+        self.mode = {"sql": L.MODE_SQL, "datastream": L.MODE_DATASTREAM}[mode]
+        self.val_type = {"none": L.VAL_NONE, "i64": L.VAL_I64, "f64": L.VAL_F64}[val_type]
+        self.aggs = tuple(AGGS[a] if isinstance(a, str) else int(a) for a in aggs)
+        cfg = L.FgConfig()
+        cfg.mode = self.mode
+        cfg.window_kind = window.kind
+        cfg.size_ms = window.size
+        cfg.slide_ms = window.slide
+        cfg.offset_ms = window.offset
+        cfg.shift_tz_offset_ms = int(shift_tz_offset_ms)
+        cfg.val_type = self.val_type
+        cfg.num_aggs = len(self.aggs)
+        for i, a in enumerate(self.aggs):
+            cfg.aggs[i] = a
+        cfg.max_parallelism = int(max_parallelism)
+        cfg.key_group_start, cfg.key_group_end = int(key_group_range[0]), int(key_group_range[1])
+        cfg.device_id = int(device)
+        cfg.flags = L.FLAG_KERNEL_TIMING if kernel_timing else 0
+        cfg.expected_keys = int(expected_keys)
+        cfg.buffer_records = int(buffer_records)
+        self.cfg = cfg
+        h = C.c_void_p()
+        L.check(lib.fg_open(C.byref(cfg), C.byref(h)), None)
+        self._h = h
+        self._lib = lib
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.fg_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- processElement ---------------------------------------------------------------------
+    def process_batch(self, key, rowtime, val=None, val_null=None):
+        """processElement for every record of a micro-batch (arrival order = index order)."""
+        kp, kdev, key = _dev_ptr(key)
+        tp, tdev, rowtime = _dev_ptr(rowtime)
+        vp, vdev, val = _dev_ptr(val)
+        np_, ndev, val_null = _dev_ptr(val_null)
+        keep = []
+        b = L.FgBatch()
+        if kdev:
+            assert tdev and (val is None or vdev) and (val_null is None or ndev), "mixed host/device columns"
+            b.location = L.DEVICE
+            b.n = int(key.numel() if hasattr(key, "numel") else key.shape[0])
+            b.key, b.rowtime, b.val, b.val_null = kp, tp, vp, np_
+        else:
+            key = np.ascontiguousarray(key, dtype=np.int64)
+            rowtime = np.ascontiguousarray(rowtime, dtype=np.int64)
+            b.location = L.HOST
+            b.n = len(key)
+            b.key, b.rowtime = key.ctypes.data, rowtime.ctypes.data
+            if val is not None and self.val_type != L.VAL_NONE:
+                val = np.ascontiguousarray(val, dtype=np.float64 if self.val_type == L.VAL_F64 else np.int64)
+                b.val = val.ctypes.data
+            if val_null is not None:
+                val_null = np.ascontiguousarray(val_null, dtype=np.uint8)
+                b.val_null = val_null.ctypes.data
+            keep = [key, rowtime, val, val_null]
+        L.check(self._lib.fg_add_batch(self._h, C.byref(b)), self._h)
+        del keep
+
+    # -- processWatermark ---------------------------------------------------------------------
+    def process_watermark(self, watermark: int, device_output: bool = False):
+        """Advance event time; returns the rows fired by this watermark (FiredRows)."""
+        r = L.FgRows()
+        loc = L.DEVICE if device_output else L.HOST
+        L.check(self._lib.fg_advance_progress(self._h, int(watermark), loc, C.byref(r)), self._h)
+        if device_output:
+            return r
+        return self._host_rows(r)
+
+    def _host_rows(self, r: L.FgRows) -> np.ndarray:
+        n = r.n
+        fields = [("key", "<i8"), ("window_start", "<i8"), ("window_end", "<i8")]
+        for a in self.aggs:
+            nm = AGG_NAMES[a]
+            is_f = self.val_type == L.VAL_F64 and a in (L.AGG_SUM, L.AGG_AVG)
+            fields.append((nm, "<f8" if is_f else "<i8"))
+            fields.append((nm + "_null", "?"))
+        if self.mode == L.MODE_DATASTREAM:
+            fields.append(("rowtime", "<i8"))
+        out = np.zeros(n, dtype=np.dtype(fields))
+        if n == 0:
+            return out
+
+        def col(ptr, dtype, count):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(dtype)), shape=(count,)).copy()
+
+        out["key"] = col(r.key, C.c_int64, n)
+        out["window_start"] = col(r.window_start, C.c_int64, n)
+        out["window_end"] = col(r.window_end, C.c_int64, n)
+        nullm = col(r.null_mask, C.c_uint8, n)
+        for i, a in enumerate(self.aggs):
+            nm = AGG_NAMES[a]
+            raw = col(r.agg[i], C.c_int64, n)
+            out[nm] = raw.view(np.float64) if out.dtype[nm] == np.float64 else raw
+            out[nm + "_null"] = (nullm >> i) & 1 == 1
+        if self.mode == L.MODE_DATASTREAM:
+            out["rowtime"] = col(r.rowtime, C.c_int64, n)
+        return out
+
+    # -- checkpointing ----------------------------------------------------------------------------
+    def prepare_snapshot_pre_barrier(self):
+        """Flush the staged buffer into the GPU-resident state (RecordsWindowBuffer.flush)."""
+        L.check(self._lib.fg_flush(self._h), self._h)
+
+    def snapshot_state(self):
+        """(state image dict of numpy arrays, timer watermark): the window-aggs ValueState."""
+        s = L.FgStateRows()
+        wm = C.c_int64()
+        L.check(self._lib.fg_snapshot_state(self._h, C.byref(s), C.byref(wm)), self._h)
+        n = s.n
+
+        def col(p):
+            if n == 0:
+                return np.zeros(0, dtype=np.int64)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(n,)).copy()
+
+        img = dict(key=col(s.key), slice_end=col(s.slice_end), cnt_star=col(s.cnt_star), cnt_val=col(s.cnt_val),
+                   sum=col(s.sum))
+        return img, wm.value
+
+    def restore_state(self, image, timer_watermark: int):
+        cols = {k: np.ascontiguousarray(image[k], dtype=np.int64) for k in
+                ("key", "slice_end", "cnt_star", "cnt_val", "sum")}
+        s = L.FgStateRows()
+        s.n = len(cols["key"])
+        s.key, s.slice_end, s.cnt_star, s.cnt_val, s.sum = (cols[k].ctypes.data for k in
+                                                            ("key", "slice_end", "cnt_star", "cnt_val", "sum"))
+        L.check(self._lib.fg_restore(self._h, C.byref(s), int(timer_watermark)), self._h)
+
+    # -- metrics ------------------------------------------------------------------------------------
+    @property
+    def num_late_records_dropped(self) -> int:
+        v = C.c_int64()
+        L.check(self._lib.fg_late_dropped(self._h, C.byref(v)), self._h)
+        return v.value
+
+    def stats(self) -> dict:
+        s = L.FgStats()
+        L.check(self._lib.fg_get_stats(self._h, C.byref(s)), self._h)
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def reset(self):
+        """Drop all state (a fresh operator restored from an empty snapshot), keep allocations."""
+        L.check(self._lib.fg_reset(self._h), self._h)
+
+    def kernel_stats(self) -> dict:
+        """{kernel: dict(launches, total_ms, records, rows)} (needs kernel_timing=True)."""
+        arr = (L.FgKernelStat * 16)()
+        n = C.c_int32()
+        L.check(self._lib.fg_kernel_stats(self._h, arr, 16, C.byref(n)), self._h)
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms,
+                                           records=arr[i].records, rows=arr[i].rows) for i in range(n.value)}
+
+    def synchronize(self):
+        L.check(self._lib.fg_synchronize(self._h), self._h)
+
+    @property
+    def stream(self) -> int:
+        return self._lib.fg_stream(self._h) or 0
+
+
+def key_groups(keys, max_parallelism: int = 128, key_hash: int = L.KEYHASH_BINARYROW_BIGINT, device: int = 0):
+    """KeyGroupRangeAssignment.assignToKeyGroup on the GPU (numpy in, numpy out)."""
+    lib = L.load()
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    out = np.empty(len(keys), dtype=np.int32)
+    L.check(lib.fg_key_groups(device, L.HOST, len(keys), keys.ctypes.data, key_hash, max_parallelism,
+                              out.ctypes.data))
+    return out

@@ -1,0 +1,193 @@
+/*
+ * flinkgpu.h -- C-ABI of the MI355X keyed window-aggregation engine (libflinkgpu.so).
+ *
+ * Drop-in boundary for Flink's window aggregation hot path.  A JNI / Panama stub on
+ * the Java side binds these entry points one-for-one to the reference
+ * SPI methods they replace:
+ *
+ *   reference (Java)                                                   C-ABI
+ *   ---------------------------------------------------------------   ----------------------
+ *   WindowBuffer.Factory.create(...)                                    fg_open
+ *     TR/operators/aggregate/window/buffers/WindowBuffer.java:105-118
+ *     + SlicingWindowAggOperatorBuilder.build  .../SlicingWindowAggOperatorBuilder.java:127-170
+ *   SlicingWindowOperator.processElement -> WindowProcessor.processElement
+ *     TR/operators/window/slicing/SlicingWindowOperator.java:196-204     fg_add_batch
+ *     TR/operators/aggregate/window/processors/AbstractWindowAggProcessor.java:135-165
+ *     (+ RecordsWindowBuffer.addElement  .../buffers/RecordsWindowBuffer.java:81-97)
+ *   SlicingWindowOperator.processWatermark + onEventTime/onTimer
+ *     SlicingWindowOperator.java:207-237                                  fg_advance_progress
+ *     AbstractWindowAggProcessor.advanceProgress :178-192, fireWindow/clearWindow
+ *     (SliceUnsharedWindowAggProcessor.java:46-54, SliceSharedWindowAggProcessor.java:64-118)
+ *   SlicingWindowOperator.prepareSnapshotPreBarrier :240-242           fg_flush
+ *     -> AbstractWindowAggProcessor.prepareCheckpoint :195-197 -> RecordsWindowBuffer.flush :108-119
+ *   StreamOperatorStateHandler.snapshotState (window-aggs state + timers)   fg_snapshot_state
+ *     SJ/api/operators/StreamOperatorStateHandler.java:185-241
+ *   AbstractStreamOperator.initializeState (keyed state restore)         fg_restore
+ *   SlicingWindowOperator.getNumLateRecordsDropped :300-303            fg_late_dropped
+ *   WindowBuffer.close / SlicingWindowOperator.close :178-183           fg_close
+ *   DataStream WindowOperator.processElement / processWatermark / onEventTime
+ *     SJ/runtime/operators/windowing/WindowOperator.java:300-503          same entry points,
+ *                                                                        fg_config.mode = FG_MODE_DATASTREAM
+ *   KeyGroupRangeAssignment.assignToKeyGroup  RT/state/KeyGroupRangeAssignment.java:63-77
+ *     + KeyGroupStreamPartitioner.selectChannel SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:55-65
+ *                                                                        fg_key_groups
+ *
+ * Conventions
+ *  - Return 0 (FG_OK) on success, a positive FG_E* code otherwise; fg_last_error()
+ *    holds the message (for FG_EINVAL: the reference's IllegalArgumentException text).
+ *  - FG_EFULL mirrors the EOFException "buffer full, flush and retry" signal of
+ *    RecordsWindowBuffer (:91-96); the engine handles it internally, it is returned only
+ *    if a single batch exceeds the configured buffer capacity.
+ *  - Input buffers are owned by the caller and must stay valid for the call only.
+ *    Output buffers (fg_rows, fg_state_rows) are owned by the library and stay valid
+ *    until the next call on the same handle.
+ *  - A handle is single-threaded (Flink's mailbox model, MailboxProcessor.java:44-48);
+ *    distinct handles are independent and may be used from different threads.
+ *  - Times are epoch milliseconds (Java long). All integer arithmetic wraps like Java.
+ */
+#ifndef FLINKGPU_H
+#define FLINKGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FG_ABI_VERSION 1
+
+enum fg_status {
+    FG_OK = 0,
+    FG_EINVAL = 1,     /* invalid argument / window spec (IllegalArgumentException) */
+    FG_EFULL = 2,      /* batch larger than the configured buffer (EOFException analogue) */
+    FG_EDEVICE = 3,    /* HIP runtime error or no usable MI355X device */
+    FG_ECAPACITY = 4,  /* a state region overflowed its HBM capacity (raise expected_keys) */
+    FG_ESTATE = 5      /* API used out of order */
+};
+
+enum fg_mode { FG_MODE_SQL = 0, FG_MODE_DATASTREAM = 1 };
+enum fg_window_kind { FG_TUMBLE = 0, FG_HOP = 1, FG_CUMULATE = 2 };   /* DataStream: TUMBLE, HOP=sliding */
+enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
+/* Aggregates over the single value column (SumAggFunction, Count1AggFunction,
+ * CountAggFunction, AvgAggFunction of TP/functions/aggfunctions/). */
+enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3 };
+enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
+enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1 };
+enum fg_flags { FG_FLAG_KERNEL_TIMING = 1 };   /* HIP-event timing of every launch (fg_kernel_stats) */
+
+#define FG_MAX_AGGS 8
+
+typedef struct fg_config {
+    int32_t mode;                 /* fg_mode */
+    int32_t window_kind;          /* fg_window_kind */
+    int64_t size_ms;              /* TUMBLE size / HOP size / CUMULATE max size */
+    int64_t slide_ms;             /* HOP slide / CUMULATE step; ignored for TUMBLE */
+    int64_t offset_ms;            /* window offset */
+    int64_t shift_tz_offset_ms;   /* fixed-offset shift time zone (TIMESTAMP_LTZ); 0 = UTC */
+    int32_t val_type;             /* fg_val_type of the aggregated column */
+    int32_t num_aggs;             /* output aggregate columns, in order */
+    int32_t aggs[FG_MAX_AGGS];    /* fg_agg */
+    int32_t max_parallelism;      /* number of key groups (KeyGroupRangeAssignment) */
+    int32_t key_group_start;      /* key-group range owned by this subtask (inclusive) */
+    int32_t key_group_end;
+    int32_t device_id;            /* HIP device ordinal */
+    int32_t flags;                /* FG_FLAG_* */
+    int64_t expected_keys;        /* distinct keys per slice on this subtask (sizes HBM regions) */
+    int64_t buffer_records;       /* staged records before an implicit flush (managed-memory analogue) */
+} fg_config;
+
+typedef struct fg_batch {
+    int64_t n;
+    int32_t location;             /* fg_location of the column pointers */
+    int32_t reserved0;
+    const int64_t* key;           /* BIGINT grouping key */
+    const int64_t* rowtime;       /* event time, epoch ms (TIMESTAMP(3) compact form) */
+    const void* val;              /* int64_t[] or double[] per fg_config.val_type; may be NULL for FG_VAL_NONE */
+    const uint8_t* val_null;      /* optional: 1 = value is NULL */
+} fg_batch;
+
+typedef struct fg_rows {
+    int64_t n;
+    int32_t location;             /* where the column pointers live */
+    int32_t num_aggs;
+    const int64_t* key;
+    const int64_t* window_start;
+    const int64_t* window_end;
+    const int64_t* agg[FG_MAX_AGGS];   /* 8-byte columns: BIGINT, or the bits of a DOUBLE */
+    const uint8_t* null_mask;          /* bit i set: agg[i] is NULL in that row */
+    const int64_t* rowtime;            /* DataStream: window.maxTimestamp() (end - 1); SQL: NULL */
+} fg_rows;
+
+/* Checkpoint image of the GPU-resident keyed state: one entry per (key, slice) accumulator,
+ * the content of WindowValueState "window-aggs" (AbstractWindowAggProcessor.java:103-109). */
+typedef struct fg_state_rows {
+    int64_t n;
+    const int64_t* key;
+    const int64_t* slice_end;     /* namespace of WindowValueState */
+    const int64_t* cnt_star;      /* COUNT(*) accumulator */
+    const int64_t* cnt_val;       /* COUNT(v) accumulator */
+    const int64_t* sum;           /* SUM/AVG sum accumulator (i64 or f64 bits) */
+} fg_state_rows;
+
+typedef struct fg_stats {
+    int64_t records_in;
+    int64_t records_staged;
+    int64_t late_dropped;
+    int64_t rows_fired;
+    int64_t flushes;
+    int64_t live_slices;
+    int64_t state_regions;        /* P */
+    int64_t region_capacity;      /* entries per region in HBM */
+} fg_stats;
+
+/* Per-kernel accounting (filled when FG_FLAG_KERNEL_TIMING is set): launches, summed
+ * HIP-event duration on the handle's stream, records consumed and rows emitted. */
+typedef struct fg_kernel_stat {
+    char name[32];
+    int64_t launches;
+    double total_ms;
+    int64_t records;
+    int64_t rows;
+} fg_kernel_stat;
+
+typedef struct fg_handle fg_handle;
+
+int  fg_open(const fg_config* cfg, fg_handle** out);
+int  fg_add_batch(fg_handle* h, const fg_batch* batch);
+int  fg_advance_progress(fg_handle* h, int64_t watermark, int32_t out_location, fg_rows* fired);
+int  fg_flush(fg_handle* h);
+int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
+int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
+int  fg_late_dropped(fg_handle* h, int64_t* out);
+int  fg_get_stats(fg_handle* h, fg_stats* out);
+int  fg_synchronize(fg_handle* h);
+/* Drop all resident state and staged records, keep device allocations: a fresh operator
+ * after open() + initializeState() from an empty snapshot. */
+int  fg_reset(fg_handle* h);
+/* Copies up to `max` kernel statistics into out; *count receives the number available. */
+int  fg_kernel_stats(fg_handle* h, fg_kernel_stat* out, int32_t max, int32_t* count);
+/* Device stream of the handle (hipStream_t), for callers that overlap their own work. */
+void* fg_stream(fg_handle* h);
+const char* fg_last_error(fg_handle* h);   /* h may be NULL: last error of fg_open */
+void fg_close(fg_handle* h);
+
+/* Key-group routing (keyBy partitioner) on the device of `device_id`:
+ * out_kg[i] = murmurHash(hash(key[i])) % max_parallelism, hash per fg_key_hash.
+ * Pointers are device pointers when location == FG_DEVICE. */
+int  fg_key_groups(int32_t device_id, int32_t location, int64_t n, const int64_t* key,
+                   int32_t key_hash, int32_t max_parallelism, int32_t* out_kg);
+
+/* Pack a batch for the key-group exchange: records are reordered by destination
+ * subtask (kg * parallelism / max_parallelism) into the caller-provided device buffers,
+ * counts[parallelism] receives per-destination record counts. Device pointers only. */
+int  fg_partition_by_owner(int32_t device_id, void* stream, int64_t n, const int64_t* key,
+                           const int64_t* rowtime, const int64_t* val, int32_t key_hash,
+                           int32_t max_parallelism, int32_t parallelism, int64_t* out_key,
+                           int64_t* out_rowtime, int64_t* out_val, int64_t* counts);
+
+int  fg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FLINKGPU_H */

@@ -1,0 +1,80 @@
+"""Adapts flink_amd.WindowAggOperator (the product, libflinkgpu.so) to the fixture runner's
+operator surface, producing rows in the oracle's ROW_DTYPE layout for comparison."""
+from __future__ import annotations
+
+import numpy as np
+
+import flink_amd as F
+from oracle.oracle import ROW_DTYPE
+
+KINDS = {"tumble": F.tumbling, "hop": F.hopping, "cumulate": F.cumulative}
+
+
+def window_of(cfg):
+    if cfg["kind"] == "tumble":
+        return F.tumbling(cfg["size"], cfg["offset"])
+    return KINDS[cfg["kind"]](cfg["size"], cfg["slide"], cfg["offset"])
+
+
+class GpuOperator:
+    def __init__(self, cfg, expected_keys=1 << 12, buffer_records=1 << 20, _op=None):
+        self.cfg = cfg
+        self.op = _op or F.WindowAggOperator(
+            window_of(cfg), aggs=("count_star", "count", "sum", "avg"), val_type=cfg["val_type"],
+            mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
+            buffer_records=buffer_records)
+        self._rows = []
+
+    def process_batch(self, key, ts, val=None, isnull=None):
+        self.op.process_batch(key, ts, val, isnull)
+
+    def process_watermark(self, wm):
+        self._rows.append(self.op.process_watermark(wm))
+
+    def prepare_snapshot(self):
+        self.op.prepare_snapshot_pre_barrier()
+
+    def restore_copy(self):
+        img, wm = self.op.snapshot_state()
+        new = GpuOperator(self.cfg, _op=F.WindowAggOperator(
+            self.op.window, aggs=self.op.aggs, val_type=self.cfg["val_type"], mode=self.cfg["mode"],
+            shift_tz_offset_ms=self.cfg.get("tz_offset_ms", 0), expected_keys=self.op.cfg.expected_keys,
+            buffer_records=self.op.cfg.buffer_records))
+        new.op.restore_state(img, wm)
+        new._late_base = self.late_dropped
+        return new
+
+    _late_base = 0
+
+    @property
+    def late_dropped(self):
+        return self._late_base + self.op.num_late_records_dropped
+
+    def take_rows(self):
+        rows = [r for r in self._rows if len(r)]
+        self._rows = []
+        if not rows:
+            return np.zeros(0, dtype=ROW_DTYPE)
+        r = np.concatenate(rows)
+        out = np.zeros(len(r), dtype=ROW_DTYPE)
+        out["key"] = r["key"]
+        out["window_start"] = r["window_start"]
+        out["window_end"] = r["window_end"]
+        out["cnt_star"] = r["count_star"]
+        out["cnt_val"] = r["count"]
+        out["sum_null"] = r["sum_null"]
+        out["avg_null"] = r["avg_null"]
+        if self.cfg["val_type"] == "f64":
+            out["sum_d"] = r["sum"]
+            out["avg_d"] = r["avg"]
+        else:
+            out["sum_i"] = r["sum"]
+            out["avg_i"] = r["avg"]
+        if "rowtime" in r.dtype.names:
+            out["out_ts"] = r["rowtime"]
+        else:
+            out["out_ts"] = np.iinfo(np.int64).min   # SQL rows carry no timestamp (eraseTimestamp)
+        return out
+
+    def close(self):
+        self.op.close()

@@ -1,0 +1,53 @@
+"""Deterministic synthetic keyed streams (counter-based splitmix64, BASELINE.md seed)."""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 0x5EEDF11C
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = (x + np.uint64(0x9E3779B97F4A7C15)) & M64
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M64
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M64
+        return z ^ (z >> np.uint64(31))
+
+
+def make_stream(n, keys, val_type="f64", t0=1_600_000_000_000, rate_per_ms=100, jitter_ms=0, null_frac=0.0,
+                seed=SEED, key_spread=False, big_ints=False):
+    """Returns (key, rowtime, val, isnull) numpy arrays.
+
+    rowtime = t0 + i / rate_per_ms (+ uniform jitter in [0, jitter_ms) when out of order)."""
+    i = np.arange(n, dtype=np.uint64)
+    u = splitmix64(np.uint64(seed) ^ i)
+    u2 = splitmix64(np.uint64(seed * 3 + 1) ^ i)
+    key = (u % np.uint64(keys)).astype(np.int64)
+    if key_spread:   # spread ids over the whole i64 range (incl. the sentinel Long.MIN_VALUE)
+        key = splitmix64(key.astype(np.uint64) ^ np.uint64(77)).view(np.int64)
+        key[key == key.min()] = np.iinfo(np.int64).min
+    ts = (np.int64(t0) + (np.arange(n, dtype=np.int64) // rate_per_ms)).astype(np.int64)
+    if jitter_ms:
+        ts = ts + (u2 % np.uint64(jitter_ms)).astype(np.int64)
+    if val_type == "f64":
+        val = (u2 >> np.uint64(11)).astype(np.float64) * (1000.0 / float(1 << 53))
+    else:
+        if big_ints:
+            val = (u2 ^ (u << np.uint64(7))).view(np.int64)   # full-range: exercises Java wrap-around
+        else:
+            val = (u2 % np.uint64(1000)).astype(np.int64) - 300
+    isnull = None
+    if null_frac > 0:
+        isnull = ((u2 >> np.uint64(40)) % np.uint64(1000) < np.uint64(int(null_frac * 1000))).astype(np.uint8)
+    return key, ts, val, isnull
+
+
+def batches_with_watermarks(n, batch, ts, delay_ms):
+    """Yields (lo, hi, watermark) with watermark = max rowtime so far - delay - 1 (bounded
+    out-of-orderness, BoundedOutOfOrdernessWatermarks.java:57,69)."""
+    mx = np.iinfo(np.int64).min
+    for lo in range(0, n, batch):
+        hi = min(n, lo + batch)
+        mx = max(mx, int(ts[lo:hi].max()))
+        yield lo, hi, mx - delay_ms - 1

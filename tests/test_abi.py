@@ -1,0 +1,63 @@
+"""CPU-side checks of the drop-in boundary: libflinkgpu.so loads, exports every symbol that
+include/flinkgpu.h declares, and validates window specs exactly like the reference (the
+validation runs before any device call, so no GPU is needed)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from flink_amd import _lib as L
+from tests.fixture_runner import KIND, load_assigner_cases
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "flinkgpu.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void\*?|const char\*|void)\s+\*?(fg_\w+)\s*\(", src, re.M)))
+
+
+def test_header_declares_expected_api():
+    syms = declared_symbols()
+    assert set(syms) == set(L.EXPORTS), syms
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.load()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    assert lib.fg_abi_version() == 1
+
+
+def test_struct_layouts_match_header_sizes():
+    # fg_config: 2*4 + 4*8 + 2*4 + 8*4 + 6*4 + 2*8
+    assert C.sizeof(L.FgConfig) == 8 + 32 + 8 + 32 + 24 + 16
+    assert C.sizeof(L.FgBatch) == 8 + 8 + 4 * 8
+    assert C.sizeof(L.FgRows) == 8 + 8 + 3 * 8 + 8 * 8 + 2 * 8
+
+
+AS = load_assigner_cases()
+
+
+@pytest.mark.parametrize("case", AS["errors"], ids=[e["message"][:40] for e in AS["errors"]])
+def test_window_spec_errors_match_reference(case):
+    import flink_amd as F
+    c = case["config"]
+    aggs = ("count_star", "sum") if c.get("count_star_index", 0) >= 0 else ("sum",)
+    w = F.Window(KIND[c["kind"]], c["size"], c["slide"], c["offset"])
+    with pytest.raises(F.WindowSpecError) as ei:
+        F.WindowAggOperator(w, aggs=aggs, val_type="i64")
+    assert str(ei.value) == case["message"]
+
+
+def test_no_device_is_loud():
+    """Without a GPU the product must fail, never fall back to a CPU path."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import flink_amd as F
+    with pytest.raises(F.FlinkGpuError) as ei:
+        F.WindowAggOperator(F.tumbling(1000))
+    assert ei.value.code == L.FG_EDEVICE

