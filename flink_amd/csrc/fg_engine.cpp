@@ -106,9 +106,9 @@ struct Counters {        // device scratch words read back after ingest
 
 constexpr int64_t kEmptyLane = INT64_MIN;
 
-enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_FLUSH, K_FIRE, K_EXPORT, K_RESTORE, K_NCLASS };
+enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE, K_NCLASS };
 const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan", "ingest_scatter", "merge_flush",
-                                           "merge_fire", "export", "restore"};
+                                           "merge_flush_fire", "merge_fire", "export", "restore"};
 struct KStat {
     int64_t launches = 0;
     double ms = 0;
@@ -128,7 +128,7 @@ struct fg_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    int region_bits = 0, P = 1, lanes = 1, F = 1, grid = 256;
+    int region_bits = 0, stage_bits = 0, P = 1, lanes = 1, F = 1, grid = 256;
     int64_t slice_phase = 0;   // slice ends are == slice_phase (mod slice)
 
     // processor / timer state
@@ -139,7 +139,8 @@ struct fg_handle {
 
     // staged buffer (RecordsWindowBuffer analogue)
     int64_t staged_cap = 0, staged_n = 0;
-    DevBuf st_key, st_val, st_null;
+    int st_stride = 2;          // int64 words per staged record: {key, val} or {key}
+    DevBuf st_rec, st_null;
     std::vector<std::unique_ptr<Staged>> staged;
     std::vector<std::unique_ptr<Staged>> staged_pool;
     int64_t lane_q[kMaxLanes];
@@ -148,7 +149,7 @@ struct fg_handle {
 
     // ingest scratch
     DevBuf in_key, in_ts, in_val, in_null;
-    DevBuf hist, offsets, scan_tmp, counters;
+    DevBuf hist, totals, scan_tmp, counters;
     HostBuf h_counters;
 
     // resident state
@@ -163,9 +164,10 @@ struct fg_handle {
     // device scalars: [0] overflow flags, [1] out_count
     DevBuf scalars;
     HostBuf h_scalars;
+    bool out_count_reset = false;   // out_count zeroed for the current advance
 
     // fired rows
-    int64_t out_cap = 0, out_n = 0;
+    int64_t out_cap = 0, out_n = 0, pending_out = 0;
     DevBuf o_key, o_ws, o_we, o_null, o_rt;
     DevBuf o_agg[FG_MAX_AGGS];
     HostBuf h_key, h_ws, h_we, h_null, h_rt;
@@ -321,36 +323,88 @@ int check_overflow(fg_handle* h) {
     return FG_OK;
 }
 
+int ensure_out(fg_handle* h, int64_t need);
+
+// zero the overflow word and the fired-row counter once per advance
+int reset_out_count(fg_handle* h) {
+    if (!h->out_count_reset) {
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+        h->out_count_reset = true;
+    }
+    return FG_OK;
+}
+
+struct FireRange {   // windows whose timers fire in (prev, wm]
+    int64_t prev, wm;
+};
+
+void fill_emit(fg_handle* h, MergeParams& p, int64_t wend) {
+    p.emit = 1;
+    p.wstart = window_start(h->w, wend);
+    p.wend = wend;
+    p.out_ts = jsub(wend, 1);
+    p.num_aggs = h->cfg.num_aggs;
+    for (int a = 0; a < h->cfg.num_aggs; a++) {
+        p.aggs[a] = h->cfg.aggs[a];
+        p.out_agg[a] = h->o_agg[a].as<int64_t>();
+    }
+    p.out_key = h->o_key.as<int64_t>();
+    p.out_ws = h->o_ws.as<int64_t>();
+    p.out_we = h->o_we.as<int64_t>();
+    p.out_null = h->o_null.as<uint8_t>();
+    p.out_rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->o_rt.as<int64_t>() : nullptr;
+    p.out_cap = h->out_cap;
+}
+
 // RecordsWindowBuffer.flush (:108-119) + AggCombiner.combine (:76-115): merge every staged
-// lane into its slice table.
-int flush(fg_handle* h) {
+// lane into its slice table. With `fire` (TUMBLE only), a lane whose window's timer fires
+// in this advance is combined and fired in the same pass: its rows are emitted straight
+// from LDS and the slice is never written back (SliceUnsharedWindowAggProcessor.fireWindow
+// + clearWindow, :46-54 / AbstractWindowAggProcessor.java:200-206).
+int flush(fg_handle* h, const FireRange* fire = nullptr) {
     if (h->staged_n == 0 && h->staged.empty()) return FG_OK;
     // staged batch descriptors
     std::vector<StagedBatch> sb;
     for (auto& s : h->staged) {
         StagedBatch b{};
-        b.key = h->st_key.as<int64_t>() + s->base;
-        b.val = h->cfg.val_type != FG_VAL_NONE ? h->st_val.as<int64_t>() + s->base : nullptr;
+        b.rec = h->st_rec.as<int64_t>() + s->base * h->st_stride;
+        b.val = nullptr;
         b.vnull = s->has_null ? h->st_null.as<uint8_t>() + s->base : nullptr;
         b.bucket_off = s->bucket_off.as<uint32_t>();
         b.is_acc = 0;
+        b.stride = h->st_stride;
         sb.push_back(b);
     }
     const StagedBatch* d_sb = nullptr;
     int rc = arena_put(h, sb.data(), sb.size(), &d_sb);
     if (rc) return rc;
-    HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+    if (h->out_count_reset) HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
+    else HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+    std::vector<int64_t> fired_tables;
+    bool any_emit = false;
     for (int l = 0; l < h->lanes; l++) {
         if (h->lane_q[l] == kEmptyLane) continue;
+        const int64_t se = slice_end_of(h, h->lane_q[l]);
         SliceTable* t = nullptr;
-        rc = table_get(h, slice_end_of(h, h->lane_q[l]), true, &t);
+        rc = table_get(h, se, true, &t);
         if (rc) return rc;
+        const int64_t trig = trigger_time(h->w, se);
+        const bool fire_now = fire && h->w.kind == TUMBLE && se != JMAX && trig > fire->prev && trig <= fire->wm;
+        if (fire_now) {
+            rc = reset_out_count(h);
+            if (rc) return rc;
+            const int64_t ub = std::min<int64_t>(t->upper + h->lane_records[l], (int64_t)kRegionCap * h->P);
+            rc = ensure_out(h, h->out_n + h->pending_out + ub);
+            if (rc) return rc;
+            h->pending_out += ub;
+        }
         TableRef tr = ref_of(t);
         const TableRef* d_src = nullptr;
         rc = arena_put(h, &tr, 1, &d_src);
         if (rc) return rc;
         MergeParams p{};
         p.region_bits = h->region_bits;
+        p.stage_bits = h->stage_bits;
         p.lanes = h->lanes;
         p.lane = l;
         p.n_src = 1;
@@ -358,22 +412,35 @@ int flush(fg_handle* h) {
         p.n_batches = (int)sb.size();
         p.batches = d_sb;
         p.val_type = h->cfg.val_type;
-        p.has_dst = 1;
+        p.has_dst = fire_now ? 0 : 1;
         p.dst = tr;
         p.emit = 0;
+        if (fire_now) fill_emit(h, p, se);
         p.overflow = h->scalars.as<unsigned int>();
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
         {
-            KTimer kt(h, K_FLUSH, h->lane_records[l]);
+            KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, h->lane_records[l]);
             HIPCHK(h, launch_merge(p, h->stream));
         }
-        t->upper = std::min<int64_t>(t->upper + h->lane_records[l], (int64_t)kRegionCap * h->P);
+        if (fire_now) {
+            fired_tables.push_back(se);
+            any_emit = true;
+        } else {
+            t->upper = std::min<int64_t>(t->upper + h->lane_records[l], (int64_t)kRegionCap * h->P);
+        }
     }
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
     rc = sync(h);
     if (rc) return rc;
     rc = check_overflow(h);
     if (rc) return rc;
+    if (any_emit) {
+        const int64_t before = h->out_n;
+        h->out_n = (int64_t)h->h_scalars.as<unsigned long long>()[1];
+        h->kstat[K_FLUSH_FIRE].rows += h->out_n - before;
+        h->pending_out = 0;
+    }
+    for (int64_t se : fired_tables) table_free(h, se);
     for (auto& s : h->staged) h->staged_pool.push_back(std::move(s));
     h->staged.clear();
     h->staged_n = 0;
@@ -406,7 +473,9 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     for (auto* s : srcs) ub += s->upper;
     ub = std::min<int64_t>(ub, (int64_t)kRegionCap * h->P);
     if (ub == 0 && dst == nullptr) return FG_OK;
-    int rc = ensure_out(h, h->out_n + ub);
+    int rc = reset_out_count(h);
+    if (rc) return rc;
+    rc = ensure_out(h, h->out_n + ub);
     if (rc) return rc;
     std::vector<TableRef> refs;
     for (auto* s : srcs) refs.push_back(ref_of(s));
@@ -415,6 +484,7 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     if (rc) return rc;
     MergeParams p{};
     p.region_bits = h->region_bits;
+    p.stage_bits = h->stage_bits;
     p.lanes = h->lanes;
     p.lane = -1;
     p.n_src = (int)refs.size();
@@ -422,22 +492,8 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     p.val_type = h->cfg.val_type;
     p.has_dst = dst != nullptr;
     if (dst) p.dst = ref_of(dst);
-    p.emit = 1;
-    p.wstart = window_start(h->w, wend);
-    p.wend = wend;
-    p.out_ts = jsub(wend, 1);
-    p.num_aggs = h->cfg.num_aggs;
-    for (int a = 0; a < h->cfg.num_aggs; a++) {
-        p.aggs[a] = h->cfg.aggs[a];
-        p.out_agg[a] = h->o_agg[a].as<int64_t>();
-    }
-    p.out_key = h->o_key.as<int64_t>();
-    p.out_ws = h->o_ws.as<int64_t>();
-    p.out_we = h->o_we.as<int64_t>();
-    p.out_null = h->o_null.as<uint8_t>();
-    p.out_rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->o_rt.as<int64_t>() : nullptr;
+    fill_emit(h, p, wend);
     p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
-    p.out_cap = h->out_cap;
     p.overflow = h->scalars.as<unsigned int>();
     {
         KTimer kt(h, K_FIRE, 0);
@@ -594,7 +650,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.vnull = vnull;
     p.progress = h->current_progress;
     p.lanes = h->lanes;
-    p.region_bits = h->region_bits;
+    p.stage_bits = h->stage_bits;
     p.filter_lo = flo;
     p.filter_hi = fhi;
     p.count_drops = count_drops ? 1 : 0;
@@ -632,13 +688,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     }
     if (conflict) return -1;   // caller falls back to filtered passes
 
-    // scan + scatter into the staged buffer
-    const int64_t m = (int64_t)h->F * p.grid;
-    {
-        KTimer kt(h, K_SCAN, 0);
-        HIPCHK(h, launch_scan_u32(h->hist.as<uint32_t>(), h->offsets.as<uint32_t>(), m, h->scan_tmp.as<uint32_t>(),
-                                  h->stream));
-    }
+    // per-bucket prefix over workgroups, bucket bases, then scatter into the staged buffer
     std::unique_ptr<Staged> s;
     if (!h->staged_pool.empty()) {
         s = std::move(h->staged_pool.back());
@@ -647,11 +697,23 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         s.reset(new Staged());
     }
     HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
-    HIPCHK(h, launch_bucket_offsets(h->offsets.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F, p.grid,
-                                    h->stream));
-    p.offsets = h->offsets.as<uint32_t>();
-    p.st_key = h->st_key.as<int64_t>() + h->staged_n;
-    p.st_val = h->cfg.val_type != FG_VAL_NONE ? h->st_val.as<int64_t>() + h->staged_n : nullptr;
+    {
+        KTimer kt(h, K_SCAN, 0);
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), h->F, p.grid, h->stream));
+        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F,
+                                  h->scan_tmp.as<uint32_t>(), h->stream));
+    }
+    p.bucket_base = s->bucket_off.as<uint32_t>();
+    // tile-sorted scatter when at most two lanes are active and their buckets fit LDS
+    {
+        int nslots = 0;
+        for (int l = 0; l < kMaxLanes; l++) p.lane_slot[l] = -1;
+        for (int l = 0; l < h->lanes; l++)
+            if (out->lane_min[l] <= out->lane_max[l]) p.lane_slot[l] = nslots++;
+        p.sorted = (nslots >= 1 && nslots <= 2 && (nslots << h->stage_bits) <= kMaxSortedBuckets) ? 1 : 0;
+    }
+    p.st_stride = h->st_stride;
+    p.st_rec = h->st_rec.as<int64_t>() + h->staged_n * h->st_stride;
     p.st_null = vnull ? h->st_null.as<uint8_t>() + h->staged_n : nullptr;
     if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
     {
@@ -667,7 +729,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     // per-lane record totals for output sizing: read the bucket offsets of each lane boundary
     std::vector<uint32_t> lb(h->lanes + 1);
     for (int l = 0; l <= h->lanes; l++) {
-        HIPCHK(h, hipMemcpyAsync(&lb[l], s->bucket_off.as<uint32_t>() + (int64_t)l * h->P, sizeof(uint32_t),
+        HIPCHK(h, hipMemcpyAsync(&lb[l], s->bucket_off.as<uint32_t>() + ((int64_t)l << h->stage_bits), sizeof(uint32_t),
                                  hipMemcpyDeviceToHost, h->stream));
     }
     rc = sync(h);
@@ -788,12 +850,13 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
     int64_t keys = std::max<int64_t>(cfg->expected_keys, 1);
     int bits = 0;
-    while (bits < 15 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.7) < keys) bits++;
+    while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.7) < keys) bits++;
     h->region_bits = bits;
     h->P = 1 << bits;
+    h->stage_bits = std::max(bits - kStageDrop, 0);
     h->lanes = kMaxLanes;
-    while (h->lanes > 1 && h->lanes * h->P > 32768) h->lanes >>= 1;
-    h->F = h->lanes * h->P;
+    while (h->lanes > 1 && (h->lanes << h->stage_bits) > kMaxStageBuckets) h->lanes >>= 1;
+    h->F = h->lanes << h->stage_bits;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) h->grid = std::max(1, prop.multiProcessorCount);
     for (int l = 0; l < kMaxLanes; l++) {
@@ -803,12 +866,12 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     h->staged_cap = cfg->buffer_records > 0 ? cfg->buffer_records : (int64_t)1 << 26;
     fg_handle* hp = h.get();
     auto chk = [&](hipError_t e) { return e == hipSuccess; };
-    bool ok = chk(hp->st_key.ensure(8 * hp->staged_cap)) &&
-              (cfg->val_type == FG_VAL_NONE || chk(hp->st_val.ensure(8 * hp->staged_cap))) &&
+    hp->st_stride = cfg->val_type == FG_VAL_NONE ? 1 : 2;
+    bool ok = chk(hp->st_rec.ensure(8 * (size_t)hp->st_stride * hp->staged_cap)) &&
               chk(hp->st_null.ensure(hp->staged_cap)) &&
               chk(hp->hist.ensure(4 * (size_t)hp->F * hp->grid)) &&
-              chk(hp->offsets.ensure(4 * ((size_t)hp->F * hp->grid + 1))) &&
-              chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F * hp->grid))) &&
+              chk(hp->totals.ensure(4 * ((size_t)hp->F + 1))) &&
+              chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F))) &&
               chk(hp->counters.ensure(sizeof(Counters))) && chk(hp->h_counters.ensure(sizeof(Counters))) &&
               chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) &&
               chk(hp->h_scalars.ensure(64));
@@ -854,8 +917,7 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
         int rc = flush(h);
         if (rc) return rc;
         if (n > h->staged_cap) {
-            HIPCHK(h, h->st_key.ensure(8 * n));
-            if (h->cfg.val_type != FG_VAL_NONE) HIPCHK(h, h->st_val.ensure(8 * n));
+            HIPCHK(h, h->st_rec.ensure(8 * (size_t)h->st_stride * n));
             HIPCHK(h, h->st_null.ensure(n));
             h->staged_cap = n;
         }
@@ -899,15 +961,19 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
     h->out_n = 0;
-    HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+    h->pending_out = 0;
+    h->out_count_reset = false;
     int rc;
+    const int64_t prev = h->timer_wm;
+    const FireRange fr{prev, wm};
+    const FireRange* fuse = wm > prev ? &fr : nullptr;
     if (h->cfg.mode == FG_MODE_SQL) {
         // AbstractWindowAggProcessor.advanceProgress :178-192
         if (wm > h->current_progress) {
             h->current_progress = wm;
             if (h->current_progress >= h->next_trigger) {
                 if (h->staged_n > 0 && is_window_fired(h->w, h->min_slice_end, wm)) {
-                    rc = flush(h);
+                    rc = flush(h, fuse);
                     if (rc) return rc;
                 }
                 h->next_trigger = next_trigger_watermark(wm, h->w.slice);
@@ -917,11 +983,10 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
         // DataStream WindowOperator: records are in state before any timer fires
         if (wm > h->current_progress) h->current_progress = wm;
         if (h->staged_n > 0 && is_window_fired(h->w, h->min_slice_end, wm)) {
-            rc = flush(h);
+            rc = flush(h, fuse);
             if (rc) return rc;
         }
     }
-    const int64_t prev = h->timer_wm;
     if (wm > prev) {
         rc = fire_windows(h, prev, wm);
         if (rc) return rc;
@@ -1032,14 +1097,15 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     for (auto& kv : by_slice) {
         const auto& idx = kv.second;
         const int64_t m = (int64_t)idx.size();
-        std::vector<uint32_t> off(h->P + 1, 0);
+        const int NB = 1 << h->stage_bits;
+        std::vector<uint32_t> off(NB + 1, 0);
         std::vector<uint32_t> reg(m);
         for (int64_t j = 0; j < m; j++) {
             const int64_t k = in->key[idx[j]];
-            reg[j] = h->region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)k) >> (64 - h->region_bits));
+            reg[j] = h->stage_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)k) >> (64 - h->stage_bits));
             off[reg[j] + 1]++;
         }
-        for (int r = 0; r < h->P; r++) off[r + 1] += off[r];
+        for (int r = 0; r < NB; r++) off[r + 1] += off[r];
         std::vector<int64_t> k(m), cs(m), cn(m), sm(m);
         std::vector<uint32_t> cur(off.begin(), off.end() - 1);
         for (int64_t j = 0; j < m; j++) {
@@ -1055,17 +1121,18 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         HIPCHK(h, dcs.ensure(8 * std::max<int64_t>(m, 1)));
         HIPCHK(h, dcn.ensure(8 * std::max<int64_t>(m, 1)));
         HIPCHK(h, dsm.ensure(8 * std::max<int64_t>(m, 1)));
-        HIPCHK(h, doff.ensure(4 * (h->P + 1)));
+        HIPCHK(h, doff.ensure(4 * (NB + 1)));
         HIPCHK(h, hipMemcpy(dk.p, k.data(), 8 * m, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(dcs.p, cs.data(), 8 * m, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(dcn.p, cn.data(), 8 * m, hipMemcpyHostToDevice));
         HIPCHK(h, hipMemcpy(dsm.p, sm.data(), 8 * m, hipMemcpyHostToDevice));
-        HIPCHK(h, hipMemcpy(doff.p, off.data(), 4 * (h->P + 1), hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(doff.p, off.data(), 4 * (NB + 1), hipMemcpyHostToDevice));
         SliceTable* t = nullptr;
         rc = table_get(h, kv.first, true, &t);
         if (rc) return rc;
         StagedBatch sb{};
-        sb.key = dk.as<int64_t>();
+        sb.rec = dk.as<int64_t>();
+        sb.stride = 1;
         sb.val = dsm.as<int64_t>();
         sb.cnt_star = dcs.as<int64_t>();
         sb.cnt_null = dcn.as<int64_t>();
@@ -1081,6 +1148,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
         MergeParams p{};
         p.region_bits = h->region_bits;
+        p.stage_bits = h->stage_bits;
         p.lanes = 1;
         p.lane = 0;
         p.n_src = 1;
@@ -1156,6 +1224,7 @@ int fg_reset(fg_handle* h) {
     h->timer_wm = JMIN;
     h->late_dropped = 0;
     h->out_n = 0;
+    h->pending_out = 0;
     return FG_OK;
 }
 

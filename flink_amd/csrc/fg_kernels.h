@@ -15,6 +15,10 @@ constexpr int kRegionCap = 3584;              // max entries per region in HBM (
 constexpr int kMergeThreads = 1024;
 constexpr int kIngestThreads = 1024;
 constexpr int kMaxLanes = 4;
+constexpr int kStageDrop = 0;                 // state regions per staging bucket = 2^kStageDrop
+constexpr int kMaxStageBuckets = 32768;       // lanes << stage_bits (count / direct scatter LDS)
+constexpr int kMaxSortedBuckets = 8192;       // lane slots << stage_bits (tile-sorted scatter LDS)
+constexpr int kTile = 12288;                  // records per sorted-scatter tile (12 per thread)
 constexpr int kMaxAggs = 8;
 
 // One slice table in HBM: P regions, each region an SoA block of kRegionCap entries:
@@ -25,16 +29,17 @@ struct TableRef {
     uint32_t* counts;   // entries per region
 };
 
-// A staged batch (records already bucketed by (lane, region)).
+// A staged batch (records already bucketed by (lane, region)). Records are AoS
+// {key, value bits} (stride 2) or {key} (stride 1, COUNT(*)-only queries).
 struct StagedBatch {
-    const int64_t* key;
-    const int64_t* val;        // value bits, or the `sum` accumulator when is_acc
+    const int64_t* rec;        // is_acc == 0: records; is_acc == 1: keys
+    const int64_t* val;        // is_acc == 1 only: the `sum` accumulator
     const uint8_t* vnull;      // may be null
     const int64_t* cnt_star;   // only when is_acc (restore images)
     const int64_t* cnt_null;   // only when is_acc
     const uint32_t* bucket_off;  // [lanes * P + 1]
     int32_t is_acc;
-    int32_t pad;
+    int32_t stride;            // int64 words per record (1 or 2)
 };
 
 struct IngestParams {
@@ -46,27 +51,30 @@ struct IngestParams {
     const uint8_t* vnull;
     int64_t progress;          // current progress (watermark) for the late check
     int32_t lanes;             // power of two <= kMaxLanes
-    int32_t region_bits;       // log2(P)
+    int32_t stage_bits;        // log2(staging buckets per lane); bucket = top stage_bits of fmix64(key)
     int64_t filter_lo;         // slice-index filter [lo, hi): floor_div(target, slice)
     int64_t filter_hi;
     int32_t count_drops;
     int32_t grid;              // number of workgroups (segments)
     int32_t vec;               // 1: key/ts/val 16-byte aligned -> paired 16-B loads
-    int32_t pad0;
+    int32_t sorted;            // scatter variant: 1 tile-sorted (<= 2 lane slots), 0 direct
+    int32_t lane_slot[kMaxLanes];  // sorted scatter: lane -> slot (-1 inactive)
     // count outputs
-    uint32_t* hist;            // [F][grid]
+    uint32_t* hist;            // [grid][F] (workgroup-major); after k_hist_columns: per-wg prefix
     unsigned long long* drops;
     long long* lane_min;       // [kMaxLanes] slice index
     long long* lane_max;
     // scatter inputs/outputs
-    const uint32_t* offsets;   // exclusive scan of hist, [F][grid] (+1)
-    int64_t* st_key;
-    int64_t* st_val;
+    const uint32_t* bucket_base; // [F + 1] exclusive scan of bucket totals
+    int64_t* st_rec;           // AoS {key, val} (stride 2) or {key} (stride 1)
+    int32_t st_stride;
+    int32_t pad1;
     uint8_t* st_null;
 };
 
 struct MergeParams {
-    int32_t region_bits;
+    int32_t region_bits;       // log2(P): state regions, one workgroup each
+    int32_t stage_bits;        // staging bucket of region r = r >> (region_bits - stage_bits)
     int32_t lanes;
     int32_t lane;              // bucket lane of staged records (-1: none)
     int32_t n_src;
@@ -105,13 +113,12 @@ struct ExportParams {
 };
 
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s);
-hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s);
+hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s);   // picks the variant by p.sorted
 // exclusive scan of n u32 (n < 2^32 total); out has n + 1 entries; tmp >= scan_tmp_words(n)
 size_t scan_tmp_words(int64_t n);
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, hipStream_t s);
-// bucket_off[b] = offsets[b * grid] for b in [0, F]; bucket_off[F] = offsets[F * grid]
-hipError_t launch_bucket_offsets(const uint32_t* offsets, uint32_t* bucket_off, int32_t F, int32_t grid,
-                                 hipStream_t s);
+// per bucket b: hist[g][b] <- sum_{g' < g} hist[g'][b]; totals[b] <- sum_g hist[g][b]
+hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid, hipStream_t s);
 hipError_t launch_merge(const MergeParams& p, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
 hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out,

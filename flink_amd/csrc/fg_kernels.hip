@@ -33,8 +33,8 @@ __device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int6
     if (q < p.filter_lo || q >= p.filter_hi) return -2;
     *q_out = q;
     const int lane = (int)(q & (int64_t)(p.lanes - 1));
-    const uint32_t region = p.region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.region_bits));
-    return (lane << p.region_bits) | (int)region;
+    const uint32_t sb = p.stage_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.stage_bits));
+    return (lane << p.stage_bits) | (int)sb;
 }
 
 __device__ __forceinline__ void seg_bounds(int64_t n, int grid, int g, int64_t* b, int64_t* e) {
@@ -45,15 +45,47 @@ __device__ __forceinline__ void seg_bounds(int64_t n, int grid, int g, int64_t* 
 }
 
 // ----------------------------------------------------------------------------------------
+// exclusive scan of u32 (reduce-then-scan, 4096 items per block)
+// ----------------------------------------------------------------------------------------
+constexpr int kScanThreads = 1024;
+constexpr int kScanItems = 4;
+constexpr int kScanChunk = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        const int nw = blockDim.x >> 6;
+        uint32_t w = lane < nw ? s_wave[lane] : 0u;
+        for (int off = 1; off < 64; off <<= 1) {
+            uint32_t y = __shfl_up(w, off);
+            if (lane >= off) w += y;
+        }
+        if (lane < nw) s_wave[lane] = w;   // inclusive
+    }
+    __syncthreads();
+    const uint32_t wave_base = wave ? s_wave[wave - 1] : 0u;
+    *total = s_wave[(blockDim.x >> 6) - 1];
+    __syncthreads();
+    return wave_base + x - v;
+}
+
+// ----------------------------------------------------------------------------------------
 // ingest: count
 // ----------------------------------------------------------------------------------------
-constexpr int kMaxBuckets = 32768;   // lanes * P held in LDS (128 KiB)
+constexpr int kMaxBuckets = kMaxStageBuckets;
 
 __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p) {
     __shared__ uint32_t s_hist[kMaxBuckets];
     __shared__ unsigned long long s_drop;
     __shared__ long long s_lmin[kMaxLanes], s_lmax[kMaxLanes];
-    const int F = p.lanes << p.region_bits;
+    const int F = p.lanes << p.stage_bits;
     const int tid = threadIdx.x;
     for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
     if (tid == 0) s_drop = 0;
@@ -67,33 +99,43 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
 #pragma unroll
     for (int l = 0; l < kMaxLanes; l++) { lmin[l] = JMAX; lmax[l] = JMIN; }
 
-    // pairs of records per thread: 16-byte loads of key and rowtime
+    // pairs of records per thread: 16-byte loads of key and rowtime, 4 pairs in flight
     const int64_t npairs = (end - beg) >> 1;
-    for (int64_t pi = tid; pi < npairs; pi += kIngestThreads) {
-        const int64_t i = beg + 2 * pi;
-        longlong2 k2, t2;
-        if (p.vec) {
-            k2 = *reinterpret_cast<const longlong2*>(p.key + i);
-            t2 = *reinterpret_cast<const longlong2*>(p.ts + i);
-        } else {
-            k2.x = p.key[i]; k2.y = p.key[i + 1];
-            t2.x = p.ts[i]; t2.y = p.ts[i + 1];
-        }
+    auto account = [&](int64_t k, int64_t ts) {
         int64_t q;
-        int b = classify(p, k2.x, t2.x, &q);
+        const int b = classify(p, k, ts, &q);
         if (b >= 0) {
             atomicAdd(&s_hist[b], 1u);
             const int l = (int)(q & (p.lanes - 1));
             lmin[l] = q < lmin[l] ? q : lmin[l];
             lmax[l] = q > lmax[l] ? q : lmax[l];
-        } else if (b == -1) drops++;
-        b = classify(p, k2.y, t2.y, &q);
-        if (b >= 0) {
-            atomicAdd(&s_hist[b], 1u);
-            const int l = (int)(q & (p.lanes - 1));
-            lmin[l] = q < lmin[l] ? q : lmin[l];
-            lmax[l] = q > lmax[l] ? q : lmax[l];
-        } else if (b == -1) drops++;
+        } else if (b == -1) {
+            drops++;
+        }
+    };
+    constexpr int kU = 4;
+    for (int64_t p0 = 0; p0 < npairs; p0 += kU * kIngestThreads) {
+        longlong2 k2[kU], t2[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int64_t pi = p0 + u * kIngestThreads + tid;
+            if (pi >= npairs) continue;
+            const int64_t i = beg + 2 * pi;
+            if (p.vec) {
+                k2[u] = *reinterpret_cast<const longlong2*>(p.key + i);
+                t2[u] = *reinterpret_cast<const longlong2*>(p.ts + i);
+            } else {
+                k2[u].x = p.key[i]; k2[u].y = p.key[i + 1];
+                t2[u].x = p.ts[i]; t2[u].y = p.ts[i + 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int64_t pi = p0 + u * kIngestThreads + tid;
+            if (pi >= npairs) continue;
+            account(k2[u].x, t2[u].x);
+            account(k2[u].y, t2[u].y);
+        }
     }
     if (((end - beg) & 1) && tid == 0) {
         const int64_t i = end - 1;
@@ -128,8 +170,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
         }
     }
     __syncthreads();
-    // bucket-major histogram: hist[b * grid + g]
-    for (int b = tid; b < F; b += kIngestThreads) p.hist[(int64_t)b * p.grid + blockIdx.x] = s_hist[b];
+    // workgroup-major histogram: hist[g * F + b] (contiguous stores)
+    for (int b = tid; b < F; b += kIngestThreads) p.hist[(int64_t)blockIdx.x * F + b] = s_hist[b];
     if (tid == 0 && p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
     if (tid < kMaxLanes) {
         if (s_lmin[tid] != JMAX) atomicMin(&p.lane_min[tid], s_lmin[tid]);
@@ -141,88 +183,202 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
 // ingest: scatter into the staged buffer (bucket-major; within a (bucket, workgroup)
 // run the order is arrival order up to LDS atomic ordering)
 // ----------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter(IngestParams p) {
+// Direct scatter (any number of active lanes): one 16-B store per record at its
+// bucket cursor (LDS atomic); used when a batch touches more than two slice lanes.
+__global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_direct(IngestParams p) {
     __shared__ uint32_t s_cur[kMaxBuckets];
-    const int F = p.lanes << p.region_bits;
+    const int F = p.lanes << p.stage_bits;
     const int tid = threadIdx.x;
-    for (int b = tid; b < F; b += kIngestThreads) s_cur[b] = p.offsets[(int64_t)b * p.grid + blockIdx.x];
+    for (int b = tid; b < F; b += kIngestThreads) s_cur[b] = p.bucket_base[b] + p.hist[(int64_t)blockIdx.x * F + b];
     __syncthreads();
     int64_t beg, end;
     seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
     const bool has_val = p.val != nullptr;
     const bool has_null = p.vnull != nullptr;
-    const int64_t npairs = (end - beg) >> 1;
-    for (int64_t pi = tid; pi < npairs; pi += kIngestThreads) {
-        const int64_t i = beg + 2 * pi;
-        longlong2 k2, t2, v2 = {0, 0};
-        if (p.vec) {
-            k2 = *reinterpret_cast<const longlong2*>(p.key + i);
-            t2 = *reinterpret_cast<const longlong2*>(p.ts + i);
-            if (has_val) v2 = *reinterpret_cast<const longlong2*>(p.val + i);
-        } else {
-            k2.x = p.key[i]; k2.y = p.key[i + 1];
-            t2.x = p.ts[i]; t2.y = p.ts[i + 1];
-            if (has_val) { v2.x = p.val[i]; v2.y = p.val[i + 1]; }
-        }
+    const bool aos = p.st_stride == 2;
+    auto put = [&](int64_t i, int64_t k, int64_t ts, int64_t v) {
         int64_t q;
-        int b = classify(p, k2.x, t2.x, &q);
-        if (b >= 0) {
-            const uint32_t pos = atomicAdd(&s_cur[b], 1u);
-            p.st_key[pos] = k2.x;
-            if (has_val) p.st_val[pos] = v2.x;
-            if (has_null) p.st_null[pos] = p.vnull[i];
-        }
-        b = classify(p, k2.y, t2.y, &q);
-        if (b >= 0) {
-            const uint32_t pos = atomicAdd(&s_cur[b], 1u);
-            p.st_key[pos] = k2.y;
-            if (has_val) p.st_val[pos] = v2.y;
-            if (has_null) p.st_null[pos] = p.vnull[i + 1];
+        const int b = classify(p, k, ts, &q);
+        if (b < 0) return;
+        const uint32_t pos = atomicAdd(&s_cur[b], 1u);
+        if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = make_longlong2(k, v);
+        else p.st_rec[pos] = k;
+        if (has_null) p.st_null[pos] = p.vnull[i];
+    };
+    for (int64_t i = beg + tid; i < end; i += kIngestThreads)
+        put(i, p.key[i], p.ts[i], has_val ? p.val[i] : 0);
+}
+
+// Tile-sorted scatter (<= 2 active slice lanes): a workgroup reads kTile records into
+// registers (16 per thread), ranks them per bucket with LDS atomics, scans the tile
+// counts, then stages the records bucket-sorted through LDS in four rounds and writes
+// every bucket run with consecutive lanes: contiguous 16-B stores (~4 records = 64 B
+// per run at 4096 buckets) instead of one scattered 16-B store per record.
+constexpr int kPerThread = kTile / kIngestThreads;   // 16
+constexpr int kRound = 4096;                         // slots staged per round
+constexpr int kRounds = kTile / kRound;
+
+__global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(IngestParams p) {
+    __shared__ longlong2 s_rec[kRound];              // 64 KiB
+    __shared__ uint16_t s_bkt[kRound];               // 8 KiB
+    __shared__ uint32_t s_cur[kMaxSortedBuckets];    // global cursor per slot bucket (32 KiB)
+    __shared__ uint32_t s_off[kMaxSortedBuckets + 1];// tile counts, then tile offsets (32 KiB)
+    __shared__ uint32_t s_wave[16];
+    const int P = 1 << p.stage_bits;
+    const int F = p.lanes << p.stage_bits;
+    int nslots = 0;
+#pragma unroll
+    for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
+    const int FS = nslots << p.stage_bits;           // slot buckets
+    const int tid = threadIdx.x;
+    for (int l = 0; l < kMaxLanes; l++) {
+        const int sl = p.lane_slot[l];
+        if (sl < 0) continue;
+        for (int r = tid; r < P; r += kIngestThreads) {
+            const int bf = l * P + r;
+            s_cur[sl * P + r] = p.bucket_base[bf] + p.hist[(int64_t)blockIdx.x * F + bf];
         }
     }
-    if (((end - beg) & 1) && tid == 0) {
-        const int64_t i = end - 1;
-        int64_t q;
-        int b = classify(p, p.key[i], p.ts[i], &q);
-        if (b >= 0) {
-            const uint32_t pos = atomicAdd(&s_cur[b], 1u);
-            p.st_key[pos] = p.key[i];
-            if (has_val) p.st_val[pos] = p.val[i];
-            if (has_null) p.st_null[pos] = p.vnull[i];
+    for (int b = tid; b <= FS; b += kIngestThreads) s_off[b] = 0;
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    const bool has_val = p.val != nullptr;
+    const bool has_null = p.vnull != nullptr;
+    const bool aos = p.st_stride == 2;
+    const int per_thread_buckets = (FS + kIngestThreads - 1) / kIngestThreads;
+
+    for (int64_t t0 = beg; t0 < end; t0 += kTile) {
+        const int64_t tn = end - t0 < kTile ? end - t0 : kTile;
+        int64_t rk[kPerThread], rv[kPerThread];
+        uint32_t rbr[kPerThread];   // (rank << 13) | slot bucket, 0xffffffff = not staged
+        // 1) load (pairs: records t0 + 2*(tid + j*1024) + {0,1}) + classify
+#pragma unroll
+        for (int j = 0; j < kPerThread / 2; j++) {
+            const int64_t li = 2 * ((int64_t)tid + (int64_t)j * kIngestThreads);
+            const int64_t i = t0 + li;
+            longlong2 k2 = {0, 0}, t2 = {0, 0}, v2 = {0, 0};
+            if (li + 1 < tn && p.vec) {
+                k2 = *reinterpret_cast<const longlong2*>(p.key + i);
+                t2 = *reinterpret_cast<const longlong2*>(p.ts + i);
+                if (has_val) v2 = *reinterpret_cast<const longlong2*>(p.val + i);
+            } else {
+                if (li < tn) {
+                    k2.x = p.key[i];
+                    t2.x = p.ts[i];
+                    if (has_val) v2.x = p.val[i];
+                }
+                if (li + 1 < tn) {
+                    k2.y = p.key[i + 1];
+                    t2.y = p.ts[i + 1];
+                    if (has_val) v2.y = p.val[i + 1];
+                }
+            }
+            rk[2 * j] = k2.x;
+            rv[2 * j] = v2.x;
+            rk[2 * j + 1] = k2.y;
+            rv[2 * j + 1] = v2.y;
+            int64_t q;
+            int b0 = li < tn ? classify(p, k2.x, t2.x, &q) : -3;
+            int b1 = li + 1 < tn ? classify(p, k2.y, t2.y, &q) : -3;
+            // full-space bucket -> slot bucket
+            if (b0 >= 0) b0 = p.lane_slot[b0 >> p.stage_bits] * P + (b0 & (P - 1));
+            if (b1 >= 0) b1 = p.lane_slot[b1 >> p.stage_bits] * P + (b1 & (P - 1));
+            rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
+            rbr[2 * j + 1] = b1 >= 0 ? (atomicAdd(&s_off[b1], 1u) << 13) | (uint32_t)b1 : 0xffffffffu;
         }
+        __syncthreads();
+        // 3) exclusive scan of the tile counts in place (s_off[FS] = tile total)
+        {
+            uint32_t local = 0;
+            for (int q2 = 0; q2 < per_thread_buckets; q2++) {
+                const int b = tid * per_thread_buckets + q2;
+                if (b < FS) local += s_off[b];
+            }
+            uint32_t total;
+            uint32_t run = block_exclusive_scan(local, s_wave, &total);
+            for (int q2 = 0; q2 < per_thread_buckets; q2++) {
+                const int b = tid * per_thread_buckets + q2;
+                if (b < FS) {
+                    const uint32_t c = s_off[b];
+                    s_off[b] = run;
+                    run += c;
+                }
+            }
+            if (tid == 0) s_off[FS] = total;
+        }
+        __syncthreads();
+        const uint32_t tile_total = s_off[FS];
+        // 4) rounds: stage the slots of one round in bucket order, write the runs
+#pragma unroll
+        for (int round = 0; round < kRounds; round++) {
+            const uint32_t lo = (uint32_t)round * kRound;
+            if (lo >= tile_total) break;
+#pragma unroll
+            for (int j = 0; j < kPerThread; j++) {
+                if (rbr[j] == 0xffffffffu) continue;
+                const int b = (int)(rbr[j] & 8191u);
+                const uint32_t slot = s_off[b] + (rbr[j] >> 13);
+                if (slot - lo >= (uint32_t)kRound) continue;
+                s_rec[slot - lo] = make_longlong2(rk[j], rv[j]);
+                s_bkt[slot - lo] = (uint16_t)b;
+            }
+            __syncthreads();
+            const uint32_t hi = tile_total - lo < (uint32_t)kRound ? tile_total - lo : (uint32_t)kRound;
+            for (uint32_t i = tid; i < hi; i += kIngestThreads) {
+                const int b = s_bkt[i];
+                const uint32_t pos = s_cur[b] + (lo + i - s_off[b]);
+                const longlong2 r = s_rec[i];
+                if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = r;
+                else p.st_rec[pos] = r.x;
+            }
+            __syncthreads();
+        }
+        if (has_null) {   // rare path: NULL flags go straight to their final position
+#pragma unroll
+            for (int j = 0; j < kPerThread; j++) {
+                if (rbr[j] == 0xffffffffu) continue;
+                const int b = (int)(rbr[j] & 8191u);
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)(j >> 1) * kIngestThreads) + (j & 1);
+                p.st_null[s_cur[b] + (rbr[j] >> 13)] = p.vnull[t0 + li];
+            }
+        }
+        __syncthreads();
+        // 5) advance cursors by the tile counts (next offset - offset), clear counts
+        for (int b = tid; b < FS; b += kIngestThreads) s_cur[b] += s_off[b + 1] - s_off[b];
+        __syncthreads();
+        for (int b = tid; b <= FS; b += kIngestThreads) s_off[b] = 0;
+        __syncthreads();
     }
 }
 
-// ----------------------------------------------------------------------------------------
-// exclusive scan of u32 (reduce-then-scan, 4096 items per block)
-// ----------------------------------------------------------------------------------------
-constexpr int kScanThreads = 1024;
-constexpr int kScanItems = 4;
-constexpr int kScanChunk = kScanThreads * kScanItems;
-
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t x = v;
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
-    if (lane == 63) s_wave[wave] = x;
-    __syncthreads();
-    if (wave == 0) {
-        const int nw = blockDim.x >> 6;
-        uint32_t w = lane < nw ? s_wave[lane] : 0u;
-        for (int off = 1; off < 64; off <<= 1) {
-            uint32_t y = __shfl_up(w, off);
-            if (lane >= off) w += y;
+// per bucket: exclusive prefix over workgroups (column of the workgroup-major histogram)
+__global__ __launch_bounds__(256) void k_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= F) return;
+    uint32_t run = 0;
+    int g = 0;
+    for (; g + 8 <= grid; g += 8) {
+        uint32_t c[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) c[j] = hist[(int64_t)(g + j) * F + b];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            hist[(int64_t)(g + j) * F + b] = run;
+            run += c[j];
         }
-        if (lane < nw) s_wave[lane] = w;   // inclusive
     }
-    __syncthreads();
-    const uint32_t wave_base = wave ? s_wave[wave - 1] : 0u;
-    *total = s_wave[(blockDim.x >> 6) - 1];
-    __syncthreads();
-    return wave_base + x - v;
+    for (; g < grid; g++) {
+        const uint32_t c = hist[(int64_t)g * F + b];
+        hist[(int64_t)g * F + b] = run;
+        run += c;
+    }
+    totals[b] = run;
+}
+
+hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_hist_columns, dim3((F + 255) / 256), dim3(256), 0, s, hist, totals, F, grid);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const uint32_t* in, int64_t n, uint32_t* sums) {
@@ -286,23 +442,13 @@ hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_
     return hipGetLastError();
 }
 
-__global__ void k_bucket_offsets(const uint32_t* offsets, uint32_t* bucket_off, int32_t F, int32_t grid) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b <= F) bucket_off[b] = offsets[(int64_t)b * grid];
-}
-
-hipError_t launch_bucket_offsets(const uint32_t* offsets, uint32_t* bucket_off, int32_t F, int32_t grid,
-                                 hipStream_t s) {
-    hipLaunchKernelGGL(k_bucket_offsets, dim3((F + 1 + 255) / 256), dim3(256), 0, s, offsets, bucket_off, F, grid);
-    return hipGetLastError();
-}
-
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s) {
     hipLaunchKernelGGL(k_ingest_count, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     return hipGetLastError();
 }
 hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_ingest_scatter, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    if (p.sorted) hipLaunchKernelGGL(k_ingest_scatter_sorted, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    else hipLaunchKernelGGL(k_ingest_scatter_direct, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     return hipGetLastError();
 }
 
@@ -344,12 +490,25 @@ __device__ __forceinline__ void lds_add(LdsTable& t, int slot, unsigned long lon
     }
 }
 
+// Region of this workgroup. The 2^drop regions that share one staging bucket run as a
+// team on ONE XCD (blocks b and b + 8 share an XCD under round-robin dispatch), so the
+// bucket they all filter is read from HBM once and re-read from that XCD's L2
+// (placement affects speed only, never results).
+__device__ __forceinline__ int merge_region(int b, int region_bits, int stage_bits) {
+    const int drop = region_bits - stage_bits;
+    if (stage_bits < 3) return b;
+    const int x = b & 7, k = b >> 3;
+    const int j = k & ((1 << drop) - 1), m = k >> drop;
+    return (((m << 3) | x) << drop) | j;
+}
+
 __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     __shared__ LdsTable t;
     __shared__ uint32_t s_wave[16];
     __shared__ unsigned int s_flags;
     __shared__ unsigned long long s_out_base;
-    const int r = blockIdx.x;
+    const int r = merge_region(blockIdx.x, p.region_bits, p.stage_bits);
+    const int drop = p.region_bits - p.stage_bits;
     const int tid = threadIdx.x;
     const int cap = kRegionCap;
     const int vt = p.val_type;
@@ -369,33 +528,81 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
         const TableRef src = p.src[j];
         const uint32_t n = src.counts[r];
         const int64_t* base = src.base + (int64_t)r * 4 * cap;
-        for (uint32_t i = tid; i < n; i += kMergeThreads) {
-            const int64_t k = base[i];
-            const int slot = lds_find_or_insert(t, k, full);
-            if (slot >= 0) lds_add(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
-                                   base[3 * cap + i], vt);
+        for (uint32_t i0 = 0; i0 < n; i0 += 4 * kMergeThreads) {
+            int64_t k[4], cs[4], cn[4], sm[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {      // issue all loads first (latency hiding)
+                const uint32_t i = i0 + u * kMergeThreads + tid;
+                if (i < n) {
+                    k[u] = base[i];
+                    cs[u] = base[cap + i];
+                    cn[u] = base[2 * cap + i];
+                    sm[u] = base[3 * cap + i];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + u * kMergeThreads + tid;
+                if (i >= n) continue;
+                const int slot = lds_find_or_insert(t, k[u], full);
+                if (slot >= 0) lds_add(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
+            }
         }
     }
-    // 2) staged records of bucket (lane, r) over all staged batches --------------------
+    // 2) staged records of bucket (lane, r >> drop) over all staged batches, keeping the
+    //    keys of region r ----------------------------------------------------------------
+    auto in_region = [&](int64_t k) -> bool {
+        return drop == 0 || (int)(fmix64((uint64_t)k) >> (64 - p.region_bits)) == r;
+    };
     if (p.lane >= 0) {
-        const int b = (p.lane << p.region_bits) | r;
+        const int b = (p.lane << p.stage_bits) | (r >> drop);
         for (int j = 0; j < p.n_batches; j++) {
             const StagedBatch sb = p.batches[j];
             const uint32_t beg = sb.bucket_off[b], end = sb.bucket_off[b + 1];
             if (sb.is_acc) {
                 for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    const int slot = lds_find_or_insert(t, sb.key[i], full);
+                    if (!in_region(sb.rec[i])) continue;
+                    const int slot = lds_find_or_insert(t, sb.rec[i], full);
                     if (slot >= 0)
                         lds_add(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
                                 sb.val[i], vt);
                 }
+            } else if (sb.stride == 2) {
+                const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
+                if (sb.vnull == nullptr) {
+                    constexpr int kB = 8;
+                    for (uint32_t i0 = beg; i0 < end; i0 += kB * kMergeThreads) {
+                        longlong2 rc[kB];
+#pragma unroll
+                        for (int u = 0; u < kB; u++) {   // kB independent 16-B loads in flight
+                            const uint32_t i = i0 + u * kMergeThreads + tid;
+                            if (i < end) rc[u] = rec[i];
+                        }
+#pragma unroll
+                        for (int u = 0; u < kB; u++) {
+                            const uint32_t i = i0 + u * kMergeThreads + tid;
+                            if (i >= end || !in_region(rc[u].x)) continue;
+                            const int slot = lds_find_or_insert(t, rc[u].x, full);
+                            if (slot >= 0) lds_add(t, slot, 1ull, 0ull, rc[u].y, vt);
+                        }
+                    }
+                } else {
+                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                        const longlong2 rc = rec[i];
+                        if (!in_region(rc.x)) continue;
+                        const int slot = lds_find_or_insert(t, rc.x, full);
+                        if (slot < 0) continue;
+                        const bool isnull = sb.vnull[i] != 0;
+                        lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
+                    }
+                }
             } else {
                 for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    const int slot = lds_find_or_insert(t, sb.key[i], full);
+                    if (!in_region(sb.rec[i])) continue;
+                    const int slot = lds_find_or_insert(t, sb.rec[i], full);
                     if (slot < 0) continue;
                     const bool isnull = sb.vnull != nullptr && sb.vnull[i];
-                    const int64_t v = (vt != 0 && !isnull) ? sb.val[i] : 0;
-                    lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, v, isnull ? 0 : vt);
+                    lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
                 }
             }
         }

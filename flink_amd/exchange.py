@@ -47,6 +47,13 @@ def exchange(key, rowtime, val, group=None, max_parallelism: int = 128,
     ok, ot, ov, counts = partition_by_owner(key, rowtime, val, world, max_parallelism, key_hash)
     if world == 1:
         return ok, ot, ov, 0
+    return exchange_partitioned(ok, ot, ov, counts, group)
+
+
+def exchange_partitioned(ok, ot, ov, counts, group=None):
+    """The collective step alone: columns already grouped by destination rank with
+    `counts[d]` records for rank d. Works on any backend (RCCL on GPUs, gloo on CPU)."""
+    import torch.distributed as dist
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
     send = counts.cpu().tolist()
