@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libflinkgpu.so")
+LIB_PATH = os.environ.get("FLINKGPU_LIB", os.path.join(HERE, "libflinkgpu.so"))   # override: diagnostic builds
 
 FG_OK, FG_EINVAL, FG_EFULL, FG_EDEVICE, FG_ECAPACITY, FG_ESTATE = range(6)
 MODE_SQL, MODE_DATASTREAM = 0, 1

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -97,9 +98,14 @@ struct Staged {
     DevBuf bucket_off;    // F + 1 uint32
 };
 
-struct Counters {        // device scratch words read back after ingest
+struct DevCounters {     // device scratch words read back after the count pass
     unsigned long long drops;
-    unsigned long long pad;
+    unsigned long long lane_mask;
+    long long qmin, qmax;
+};
+struct Counters {        // host view: per-lane slice index ranges (min > max: lane idle)
+    unsigned long long drops;
+    long long qmin, qmax;
     long long lane_min[kMaxLanes];
     long long lane_max[kMaxLanes];
 };
@@ -146,6 +152,7 @@ struct fg_handle {
     int64_t lane_q[kMaxLanes];
     int64_t lane_records[kMaxLanes];
     int64_t min_slice_end = JMAX;
+    int64_t anchor_start = JMIN;   // a recent slice start: base of the 32-bit rowtime fast path
 
     // ingest scratch
     DevBuf in_key, in_ts, in_val, in_null;
@@ -180,6 +187,8 @@ struct fg_handle {
     // stats
     int64_t records_in = 0, rows_fired = 0, flushes = 0;
     bool timing = false;
+    bool stamps_on = false;
+    DevBuf d_stamps;
     KStat kstat[K_NCLASS];
     std::vector<PendingEv> pend;
     std::vector<hipEvent_t> ev_pool;
@@ -418,9 +427,25 @@ int flush(fg_handle* h, const FireRange* fire = nullptr) {
         if (fire_now) fill_emit(h, p, se);
         p.overflow = h->scalars.as<unsigned int>();
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+        if (h->stamps_on) {
+            HIPCHK(h, h->d_stamps.ensure(8 * 8 * (size_t)h->P));
+            HIPCHK(h, hipMemsetAsync(h->d_stamps.p, 0, 8 * 8 * (size_t)h->P, h->stream));
+            p.stamps = h->d_stamps.as<unsigned long long>();
+        }
         {
             KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, h->lane_records[l]);
             HIPCHK(h, launch_merge(p, h->stream));
+        }
+        if (h->stamps_on) {
+            std::vector<unsigned long long> st(8 * (size_t)h->P);
+            HIPCHK(h, hipMemcpyAsync(st.data(), h->d_stamps.p, 8 * st.size(), hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            double ph[4] = {0, 0, 0, 0};
+            for (int b = 0; b < h->P; b++)
+                for (int i = 0; i < 4; i++) ph[i] += (double)(st[b * 8 + i + 1] - st[b * 8 + i]);
+            fprintf(stderr, "[fg stamps] %s lane %d records %lld: init %.0f src %.0f staged %.0f out %.0f (avg cycles/WG)\n",
+                    fire_now ? "flush_fire" : "flush", l, (long long)h->lane_records[l], ph[0] / h->P, ph[1] / h->P,
+                    ph[2] / h->P, ph[3] / h->P);
         }
         if (fire_now) {
             fired_tables.push_back(se);
@@ -638,6 +663,45 @@ int copy_out_to_host(fg_handle* h, fg_rows* r) {
     return FG_OK;
 }
 
+// Rowtime fast path (k_ingest_*: classify): with tbase a slice start at or below the
+// batch's rowtimes, assignSliceEnd(ts) = tbase + S * (floor((ts + tz - tbase) / S) + 1)
+// whenever ts + tz - tbase < 2^32 (AbstractSliceAssigner.assignSliceEnd, SliceAssigners.java:573-577,
+// for ts - offset + S >= 0), and the slice is not fired iff its end > progress + 1 + tz
+// (isWindowFired, TimeWindowUtil.java:166-173). Everything else takes the exact 64-bit path.
+void set_fast_path(fg_handle* h, IngestParams* p) {
+    p->div_m = 0;
+    const int64_t S = h->w.slice;
+    if (h->anchor_start == JMIN || S < 2 || S >= ((int64_t)1 << 32)) return;
+    const __int128 margin = (__int128)S * (((int64_t)1 << 30) / S);
+    const __int128 tb = (__int128)h->anchor_start - margin;
+    if (tb < (__int128)h->w.offset || tb + ((__int128)1 << 33) + 4 * (__int128)S > (__int128)JMAX) return;
+    p->tbase = (int64_t)tb;
+    p->div_m = ~0ull / (uint64_t)S + 1;
+    p->qbase = floor_div(p->tbase, S) + 1;
+    __int128 lim = (__int128)h->current_progress + 1 + h->w.tz;
+    if (lim < (__int128)JMIN) lim = JMIN;
+    if (lim > (__int128)JMAX) lim = JMAX;
+    p->fired_lim = (int64_t)lim;
+}
+
+// Seed the fast-path anchor from the first rowtime when no batch has been seen yet.
+int seed_anchor(fg_handle* h, const int64_t* ts_dev, const int64_t* ts_host) {
+    if (h->anchor_start != JMIN) return FG_OK;
+    int64_t t0;
+    if (ts_host) {
+        t0 = ts_host[0];
+    } else {
+        HIPCHK(h, hipMemcpyAsync(h->h_counters.p, ts_dev, 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        std::memcpy(&t0, h->h_counters.p, 8);
+    }
+    if (t0 == JMAX || t0 == JMIN) return FG_OK;
+    const int64_t t = to_utc(h->w, t0);
+    const __int128 st = (__int128)floor_div(jsub(t, h->slice_phase), h->w.slice) * h->w.slice + h->slice_phase;
+    if (st > (__int128)JMIN + h->w.slice && st < (__int128)JMAX - h->w.slice) h->anchor_start = (int64_t)st;
+    return FG_OK;
+}
+
 // one ingest pass over the device-resident batch with a slice filter
 int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
                 const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
@@ -658,26 +722,45 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(h->grid, g));
     p.vec = ((uintptr_t)key % 16 == 0 && (uintptr_t)ts % 16 == 0 && (!val || (uintptr_t)val % 16 == 0)) ? 1 : 0;
     p.hist = h->hist.as<uint32_t>();
-    Counters init{};
+    set_fast_path(h, &p);
+    DevCounters init{};
     init.drops = 0;
-    for (int l = 0; l < kMaxLanes; l++) {
-        init.lane_min[l] = JMAX;
-        init.lane_max[l] = JMIN;
-    }
+    init.lane_mask = 0;
+    init.qmin = JMAX;
+    init.qmax = JMIN;
     std::memcpy(h->h_counters.p, &init, sizeof init);
     HIPCHK(h, hipMemcpyAsync(h->counters.p, h->h_counters.p, sizeof init, hipMemcpyHostToDevice, h->stream));
-    Counters* dc = h->counters.as<Counters>();
+    DevCounters* dc = h->counters.as<DevCounters>();
     p.drops = &dc->drops;
-    p.lane_min = dc->lane_min;
-    p.lane_max = dc->lane_max;
+    p.lane_mask = &dc->lane_mask;
+    p.qmin = &dc->qmin;
+    p.qmax = &dc->qmax;
     {
         KTimer kt(h, K_COUNT, n);
         HIPCHK(h, launch_ingest_count(p, h->stream));
     }
-    HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(Counters), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
     int rc = sync(h);
     if (rc) return rc;
-    std::memcpy(out, h->h_counters.p, sizeof(Counters));
+    {
+        DevCounters got;
+        std::memcpy(&got, h->h_counters.p, sizeof got);
+        out->drops = got.drops;
+        out->qmin = got.qmin;
+        out->qmax = got.qmax;
+        for (int l = 0; l < kMaxLanes; l++) {
+            out->lane_min[l] = JMAX;
+            out->lane_max[l] = JMIN;
+        }
+        if (got.qmin <= got.qmax) {
+            h->anchor_start = jsub(slice_end_of(h, got.qmin), h->w.slice);
+            if ((uint64_t)(got.qmax - got.qmin) >= (uint64_t)h->lanes) return -1;   // lanes conflict
+            for (int64_t q = got.qmin; q <= got.qmax; q++) {
+                const int l = (int)(q & (h->lanes - 1));
+                if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
+            }
+        }
+    }
 
     // lane compatibility with the staged buffer
     bool conflict = false;
@@ -716,9 +799,24 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.st_rec = h->st_rec.as<int64_t>() + h->staged_n * h->st_stride;
     p.st_null = vnull ? h->st_null.as<uint8_t>() + h->staged_n : nullptr;
     if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
+    if (h->stamps_on) {
+        HIPCHK(h, h->d_stamps.ensure(8 * 8 * (size_t)std::max(h->P, p.grid)));
+        HIPCHK(h, hipMemsetAsync(h->d_stamps.p, 0, 8 * 8 * (size_t)p.grid, h->stream));
+        p.stamps = h->d_stamps.as<unsigned long long>();
+    }
     {
         KTimer kt(h, K_SCATTER, n);
         HIPCHK(h, launch_ingest_scatter(p, h->stream));
+    }
+    if (h->stamps_on && p.sorted) {
+        std::vector<unsigned long long> st(8 * (size_t)p.grid);
+        HIPCHK(h, hipMemcpyAsync(st.data(), h->d_stamps.p, 8 * st.size(), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        double ph[4] = {0, 0, 0, 0};
+        for (int b = 0; b < p.grid; b++)
+            for (int i = 0; i < 4; i++) ph[i] += (double)st[b * 8 + i];
+        fprintf(stderr, "[fg stamps] scatter n %lld: load+classify+rank %.0f scan %.0f rounds %.0f cursors %.0f (avg cycles/WG)\n",
+                (long long)n, ph[0] / p.grid, ph[1] / p.grid, ph[2] / p.grid, ph[3] / p.grid);
     }
     int64_t staged_now = 0;
     for (int l = 0; l < h->lanes; l++) {
@@ -830,6 +928,9 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     h->cfg = *cfg;
     h->device = cfg->device_id;
     h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
+#ifdef FG_STAMPS
+    h->stamps_on = getenv("FG_MERGE_STAMPS") != nullptr;
+#endif
     if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         g_open_error = "hipSetDevice/hipStreamCreate failed";
         return FG_EDEVICE;
@@ -923,6 +1024,10 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
         }
     }
     h->records_in += n;
+    {
+        int rc0 = b->location == FG_HOST ? seed_anchor(h, nullptr, b->rowtime) : seed_anchor(h, ts, nullptr);
+        if (rc0) return rc0;
+    }
     Counters c{};
     int rc = ingest_pass(h, n, key, ts, val, vnull, JMIN, JMAX, true, &c);
     h->late_dropped += (int64_t)c.drops;
@@ -930,12 +1035,7 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     if (rc != -1) return rc;
     // Lane conflict: the batch spans slices that do not fit the staged lanes. Flush and
     // ingest the batch in slice ranges of `lanes` slices.
-    int64_t qlo = JMAX, qhi = JMIN;
-    for (int l = 0; l < h->lanes; l++) {
-        if (c.lane_min[l] > c.lane_max[l]) continue;
-        qlo = std::min<int64_t>(qlo, c.lane_min[l]);
-        qhi = std::max<int64_t>(qhi, c.lane_max[l]);
-    }
+    const int64_t qlo = c.qmin, qhi = c.qmax;
     rc = flush(h);
     if (rc) return rc;
     for (int64_t lo = qlo; lo <= qhi; lo += h->lanes) {
@@ -1219,6 +1319,7 @@ int fg_reset(fg_handle* h) {
         h->lane_records[l] = 0;
     }
     h->min_slice_end = JMAX;
+    h->anchor_start = JMIN;
     h->current_progress = JMIN;
     h->next_trigger = JMIN;
     h->timer_wm = JMIN;

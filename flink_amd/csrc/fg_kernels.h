@@ -50,6 +50,12 @@ struct IngestParams {
     const int64_t* val;
     const uint8_t* vnull;
     int64_t progress;          // current progress (watermark) for the late check
+    // fast path (host-precomputed): d = rowtime + tz - tbase in [0, 2^32) -> slice end
+    // tbase + S * (umulhi64(d, div_m) + 1); not late iff that end > fired_lim
+    int64_t tbase;             // a slice start (== offset mod S); fast path off when div_m == 0
+    uint64_t div_m;            // ceil(2^64 / S)
+    int64_t qbase;             // floor_div(tbase, S) + 1
+    int64_t fired_lim;         // progress + 1 + tz (saturated): slice ends <= fired_lim are fired
     int32_t lanes;             // power of two <= kMaxLanes
     int32_t stage_bits;        // log2(staging buckets per lane); bucket = top stage_bits of fmix64(key)
     int64_t filter_lo;         // slice-index filter [lo, hi): floor_div(target, slice)
@@ -62,14 +68,16 @@ struct IngestParams {
     // count outputs
     uint32_t* hist;            // [grid][F] (workgroup-major); after k_hist_columns: per-wg prefix
     unsigned long long* drops;
-    long long* lane_min;       // [kMaxLanes] slice index
-    long long* lane_max;
+    long long* qmin;           // min / max slice index of the accepted records
+    long long* qmax;
+    unsigned long long* lane_mask;   // bit l: some record has slice index == l (mod lanes)
     // scatter inputs/outputs
     const uint32_t* bucket_base; // [F + 1] exclusive scan of bucket totals
     int64_t* st_rec;           // AoS {key, val} (stride 2) or {key} (stride 1)
     int32_t st_stride;
     int32_t pad1;
     uint8_t* st_null;
+    unsigned long long* stamps;  // diagnostic builds only (FG_STAMPS): [grid][8] cycles per phase
 };
 
 struct MergeParams {
@@ -99,6 +107,7 @@ struct MergeParams {
     unsigned long long* out_count;
     int64_t out_cap;
     unsigned int* overflow;    // bit0: region overflow, bit1: output overflow, bit2: LDS table full
+    unsigned long long* stamps;  // diagnostic builds only (FG_STAMPS): [grid][8] s_memtime per phase
 };
 
 struct ExportParams {

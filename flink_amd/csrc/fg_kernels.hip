@@ -22,14 +22,32 @@
 
 namespace fg {
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS ops, not for its
+// global loads/stores (a __syncthreads() also drains vmcnt, stalling on in-flight stores).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+
 // ----------------------------------------------------------------------------------------
 // record classification shared by count and scatter (must agree exactly)
 // ----------------------------------------------------------------------------------------
 // returns bucket >= 0, -1 when the record is late-dropped, -2 when outside the slice filter
 __device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int64_t ts, int64_t* q_out) {
-    int64_t target;
-    if (!target_slice(p.w, ts, p.progress, &target)) return -1;
-    int64_t q = floor_div_fast(target, p.w.slice, p.w.rslice);
+    int64_t target, q;
+    const uint64_t d = (uint64_t)ts + (uint64_t)p.w.tz - (uint64_t)p.tbase;
+    const uint64_t qq = __umul64hi(d, p.div_m);
+    const int64_t end_fast = p.tbase + (int64_t)((qq + 1) * (uint64_t)p.w.slice);
+    if (p.div_m != 0 && d < (1ull << 32) && ts != JMAX && end_fast > p.fired_lim) {
+        target = end_fast;                      // assignSliceEnd, not fired: no late handling
+        q = p.qbase + (int64_t)qq;
+    } else {
+        if (!target_slice(p.w, ts, p.progress, &target)) return -1;
+        q = floor_div_fast(target, p.w.slice, p.w.rslice);
+    }
+    (void)target;
     if (q < p.filter_lo || q >= p.filter_hi) return -2;
     *q_out = q;
     const int lane = (int)(q & (int64_t)(p.lanes - 1));
@@ -51,7 +69,8 @@ constexpr int kScanThreads = 1024;
 constexpr int kScanItems = 4;
 constexpr int kScanChunk = kScanThreads * kScanItems;
 
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
+template <bool kLdsOnly>
+__device__ __forceinline__ uint32_t block_exclusive_scan_t(uint32_t v, uint32_t* s_wave, uint32_t* total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = v;
     for (int off = 1; off < 64; off <<= 1) {
@@ -59,7 +78,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
         if (lane >= off) x += y;
     }
     if (lane == 63) s_wave[wave] = x;
-    __syncthreads();
+    if (kLdsOnly) lds_barrier(); else __syncthreads();
     if (wave == 0) {
         const int nw = blockDim.x >> 6;
         uint32_t w = lane < nw ? s_wave[lane] : 0u;
@@ -69,11 +88,14 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
         }
         if (lane < nw) s_wave[lane] = w;   // inclusive
     }
-    __syncthreads();
+    if (kLdsOnly) lds_barrier(); else __syncthreads();
     const uint32_t wave_base = wave ? s_wave[wave - 1] : 0u;
     *total = s_wave[(blockDim.x >> 6) - 1];
-    __syncthreads();
+    if (kLdsOnly) lds_barrier(); else __syncthreads();
     return wave_base + x - v;
+}
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
+    return block_exclusive_scan_t<false>(v, s_wave, total);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -84,20 +106,19 @@ constexpr int kMaxBuckets = kMaxStageBuckets;
 __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p) {
     __shared__ uint32_t s_hist[kMaxBuckets];
     __shared__ unsigned long long s_drop;
-    __shared__ long long s_lmin[kMaxLanes], s_lmax[kMaxLanes];
+    __shared__ long long s_qmin, s_qmax;
+    __shared__ uint32_t s_mask;
     const int F = p.lanes << p.stage_bits;
     const int tid = threadIdx.x;
     for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
-    if (tid == 0) s_drop = 0;
-    if (tid < kMaxLanes) { s_lmin[tid] = JMAX; s_lmax[tid] = JMIN; }
+    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_mask = 0; }
     __syncthreads();
 
     int64_t beg, end;
     seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
-    uint32_t drops = 0;
-    long long lmin[kMaxLanes], lmax[kMaxLanes];
-#pragma unroll
-    for (int l = 0; l < kMaxLanes; l++) { lmin[l] = JMAX; lmax[l] = JMIN; }
+    uint32_t drops = 0, mask = 0;
+    long long qmin = JMAX, qmax = JMIN;
+    const int lm = p.lanes - 1;
 
     // pairs of records per thread: 16-byte loads of key and rowtime, 4 pairs in flight
     const int64_t npairs = (end - beg) >> 1;
@@ -106,9 +127,9 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
         const int b = classify(p, k, ts, &q);
         if (b >= 0) {
             atomicAdd(&s_hist[b], 1u);
-            const int l = (int)(q & (p.lanes - 1));
-            lmin[l] = q < lmin[l] ? q : lmin[l];
-            lmax[l] = q > lmax[l] ? q : lmax[l];
+            qmin = q < qmin ? q : qmin;
+            qmax = q > qmax ? q : qmax;
+            mask |= 1u << ((int)q & lm);
         } else if (b == -1) {
             drops++;
         }
@@ -137,45 +158,29 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
             account(k2[u].y, t2[u].y);
         }
     }
-    if (((end - beg) & 1) && tid == 0) {
-        const int64_t i = end - 1;
-        int64_t q;
-        int b = classify(p, p.key[i], p.ts[i], &q);
-        if (b >= 0) {
-            atomicAdd(&s_hist[b], 1u);
-            const int l = (int)(q & (p.lanes - 1));
-            lmin[l] = q < lmin[l] ? q : lmin[l];
-            lmax[l] = q > lmax[l] ? q : lmax[l];
-        } else if (b == -1) drops++;
-    }
+    if (((end - beg) & 1) && tid == 0) account(p.key[end - 1], p.ts[end - 1]);
     // wave reductions, then one LDS atomic per wave
-    for (int off = 32; off > 0; off >>= 1) drops += __shfl_down(drops, off);
-#pragma unroll
-    for (int l = 0; l < kMaxLanes; l++) {
-        long long a = lmin[l], z = lmax[l];
-        for (int off = 32; off > 0; off >>= 1) {
-            long long oa = __shfl_down(a, off), oz = __shfl_down(z, off);
-            a = oa < a ? oa : a;
-            z = oz > z ? oz : z;
-        }
-        lmin[l] = a;
-        lmax[l] = z;
+    for (int off = 32; off > 0; off >>= 1) {
+        drops += __shfl_down(drops, off);
+        mask |= __shfl_down(mask, off);
+        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off);
+        qmin = oa < qmin ? oa : qmin;
+        qmax = oz > qmax ? oz : qmax;
     }
     if ((tid & 63) == 0) {
         if (drops) atomicAdd(&s_drop, (unsigned long long)drops);
-#pragma unroll
-        for (int l = 0; l < kMaxLanes; l++) {
-            if (lmin[l] != JMAX) atomicMin(&s_lmin[l], lmin[l]);
-            if (lmax[l] != JMIN) atomicMax(&s_lmax[l], lmax[l]);
-        }
+        if (mask) atomicOr(&s_mask, mask);
+        if (qmin != JMAX) atomicMin(&s_qmin, qmin);
+        if (qmax != JMIN) atomicMax(&s_qmax, qmax);
     }
     __syncthreads();
     // workgroup-major histogram: hist[g * F + b] (contiguous stores)
     for (int b = tid; b < F; b += kIngestThreads) p.hist[(int64_t)blockIdx.x * F + b] = s_hist[b];
-    if (tid == 0 && p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
-    if (tid < kMaxLanes) {
-        if (s_lmin[tid] != JMAX) atomicMin(&p.lane_min[tid], s_lmin[tid]);
-        if (s_lmax[tid] != JMIN) atomicMax(&p.lane_max[tid], s_lmax[tid]);
+    if (tid == 0) {
+        if (p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
+        if (s_mask) atomicOr(p.lane_mask, (unsigned long long)s_mask);
+        if (s_qmin != JMAX) atomicMin(p.qmin, s_qmin);
+        if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
     }
 }
 
@@ -247,22 +252,69 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
     const bool has_null = p.vnull != nullptr;
     const bool aos = p.st_stride == 2;
     const int per_thread_buckets = (FS + kIngestThreads - 1) / kIngestThreads;
+#ifdef FG_STAMPS
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tprev = __builtin_amdgcn_s_memtime();
+#define SSTAMP(i)                                                      \
+    do {                                                               \
+        lds_barrier();                                                 \
+        const unsigned long long tn_ = __builtin_amdgcn_s_memtime();   \
+        acc[i] += tn_ - tprev;                                         \
+        tprev = tn_;                                                   \
+    } while (0)
+#else
+#define SSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
 
     for (int64_t t0 = beg; t0 < end; t0 += kTile) {
         const int64_t tn = end - t0 < kTile ? end - t0 : kTile;
         int64_t rk[kPerThread], rv[kPerThread];
         uint32_t rbr[kPerThread];   // (rank << 13) | slot bucket, 0xffffffff = not staged
-        // 1) load (pairs: records t0 + 2*(tid + j*1024) + {0,1}) + classify
+        // 1) load (pairs: records t0 + 2*(tid + j*1024) + {0,1}) + classify. Full aligned
+        //    tiles issue every load of the tile before the first use (all in flight).
+        const bool fast = tn == kTile && p.vec;
+        if (fast) {
+            // keys + rowtimes first (all in flight); values are loaded after ranking so their
+            // latency hides behind the bucket scan
+            longlong2 k2[kPerThread / 2], t2[kPerThread / 2];
 #pragma unroll
-        for (int j = 0; j < kPerThread / 2; j++) {
-            const int64_t li = 2 * ((int64_t)tid + (int64_t)j * kIngestThreads);
-            const int64_t i = t0 + li;
-            longlong2 k2 = {0, 0}, t2 = {0, 0}, v2 = {0, 0};
-            if (li + 1 < tn && p.vec) {
-                k2 = *reinterpret_cast<const longlong2*>(p.key + i);
-                t2 = *reinterpret_cast<const longlong2*>(p.ts + i);
-                if (has_val) v2 = *reinterpret_cast<const longlong2*>(p.val + i);
+            for (int j = 0; j < kPerThread / 2; j++) {
+                const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)j * kIngestThreads);
+                k2[j] = *reinterpret_cast<const longlong2*>(p.key + i);
+                t2[j] = *reinterpret_cast<const longlong2*>(p.ts + i);
+            }
+#pragma unroll
+            for (int j = 0; j < kPerThread / 2; j++) {
+                rk[2 * j] = k2[j].x;
+                rk[2 * j + 1] = k2[j].y;
+                int64_t q;
+                int b0 = classify(p, k2[j].x, t2[j].x, &q);
+                int b1 = classify(p, k2[j].y, t2[j].y, &q);
+                if (b0 >= 0) b0 = p.lane_slot[b0 >> p.stage_bits] * P + (b0 & (P - 1));
+                if (b1 >= 0) b1 = p.lane_slot[b1 >> p.stage_bits] * P + (b1 & (P - 1));
+                rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
+                rbr[2 * j + 1] = b1 >= 0 ? (atomicAdd(&s_off[b1], 1u) << 13) | (uint32_t)b1 : 0xffffffffu;
+            }
+            if (has_val) {
+#pragma unroll
+                for (int j = 0; j < kPerThread / 2; j++) {
+                    const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)j * kIngestThreads);
+                    const longlong2 v2 = *reinterpret_cast<const longlong2*>(p.val + i);
+                    rv[2 * j] = v2.x;
+                    rv[2 * j + 1] = v2.y;
+                }
             } else {
+#pragma unroll
+                for (int j = 0; j < kPerThread; j++) rv[j] = 0;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPerThread / 2; j++) {
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)j * kIngestThreads);
+                const int64_t i = t0 + li;
+                longlong2 k2 = {0, 0}, t2 = {0, 0}, v2 = {0, 0};
                 if (li < tn) {
                     k2.x = p.key[i];
                     t2.x = p.ts[i];
@@ -273,21 +325,21 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                     t2.y = p.ts[i + 1];
                     if (has_val) v2.y = p.val[i + 1];
                 }
+                rk[2 * j] = k2.x;
+                rv[2 * j] = v2.x;
+                rk[2 * j + 1] = k2.y;
+                rv[2 * j + 1] = v2.y;
+                int64_t q;
+                int b0 = li < tn ? classify(p, k2.x, t2.x, &q) : -3;
+                int b1 = li + 1 < tn ? classify(p, k2.y, t2.y, &q) : -3;
+                if (b0 >= 0) b0 = p.lane_slot[b0 >> p.stage_bits] * P + (b0 & (P - 1));
+                if (b1 >= 0) b1 = p.lane_slot[b1 >> p.stage_bits] * P + (b1 & (P - 1));
+                rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
+                rbr[2 * j + 1] = b1 >= 0 ? (atomicAdd(&s_off[b1], 1u) << 13) | (uint32_t)b1 : 0xffffffffu;
             }
-            rk[2 * j] = k2.x;
-            rv[2 * j] = v2.x;
-            rk[2 * j + 1] = k2.y;
-            rv[2 * j + 1] = v2.y;
-            int64_t q;
-            int b0 = li < tn ? classify(p, k2.x, t2.x, &q) : -3;
-            int b1 = li + 1 < tn ? classify(p, k2.y, t2.y, &q) : -3;
-            // full-space bucket -> slot bucket
-            if (b0 >= 0) b0 = p.lane_slot[b0 >> p.stage_bits] * P + (b0 & (P - 1));
-            if (b1 >= 0) b1 = p.lane_slot[b1 >> p.stage_bits] * P + (b1 & (P - 1));
-            rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
-            rbr[2 * j + 1] = b1 >= 0 ? (atomicAdd(&s_off[b1], 1u) << 13) | (uint32_t)b1 : 0xffffffffu;
         }
-        __syncthreads();
+        SSTAMP(0);
+        lds_barrier();
         // 3) exclusive scan of the tile counts in place (s_off[FS] = tile total)
         {
             uint32_t local = 0;
@@ -296,7 +348,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                 if (b < FS) local += s_off[b];
             }
             uint32_t total;
-            uint32_t run = block_exclusive_scan(local, s_wave, &total);
+            uint32_t run = block_exclusive_scan_t<true>(local, s_wave, &total);
             for (int q2 = 0; q2 < per_thread_buckets; q2++) {
                 const int b = tid * per_thread_buckets + q2;
                 if (b < FS) {
@@ -307,7 +359,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
             }
             if (tid == 0) s_off[FS] = total;
         }
-        __syncthreads();
+        lds_barrier();
+        SSTAMP(1);
         const uint32_t tile_total = s_off[FS];
         // 4) rounds: stage the slots of one round in bucket order, write the runs
 #pragma unroll
@@ -323,7 +376,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                 s_rec[slot - lo] = make_longlong2(rk[j], rv[j]);
                 s_bkt[slot - lo] = (uint16_t)b;
             }
-            __syncthreads();
+            lds_barrier();
             const uint32_t hi = tile_total - lo < (uint32_t)kRound ? tile_total - lo : (uint32_t)kRound;
             for (uint32_t i = tid; i < hi; i += kIngestThreads) {
                 const int b = s_bkt[i];
@@ -332,8 +385,9 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                 if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = r;
                 else p.st_rec[pos] = r.x;
             }
-            __syncthreads();
+            lds_barrier();
         }
+        SSTAMP(2);
         if (has_null) {   // rare path: NULL flags go straight to their final position
 #pragma unroll
             for (int j = 0; j < kPerThread; j++) {
@@ -343,13 +397,18 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                 p.st_null[s_cur[b] + (rbr[j] >> 13)] = p.vnull[t0 + li];
             }
         }
-        __syncthreads();
+        lds_barrier();
         // 5) advance cursors by the tile counts (next offset - offset), clear counts
         for (int b = tid; b < FS; b += kIngestThreads) s_cur[b] += s_off[b + 1] - s_off[b];
-        __syncthreads();
+        lds_barrier();
         for (int b = tid; b <= FS; b += kIngestThreads) s_off[b] = 0;
-        __syncthreads();
+        lds_barrier();
+        SSTAMP(3);
     }
+#ifdef FG_STAMPS
+    if (tid == 0 && p.stamps)
+        for (int i = 0; i < 4; i++) p.stamps[blockIdx.x * 8 + i] = acc[i];
+#endif
 }
 
 // per bucket: exclusive prefix over workgroups (column of the workgroup-major histogram)
@@ -509,6 +568,18 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     __shared__ unsigned long long s_out_base;
     const int r = merge_region(blockIdx.x, p.region_bits, p.stage_bits);
     const int drop = p.region_bits - p.stage_bits;
+#ifdef FG_STAMPS
+#define STAMP(i)                                                                           \
+    do {                                                                                   \
+        __syncthreads();                                                                   \
+        if (threadIdx.x == 0 && p.stamps) p.stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
+    STAMP(0);
     const int tid = threadIdx.x;
     const int cap = kRegionCap;
     const int vt = p.val_type;
@@ -522,6 +593,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     if (tid == 0) s_flags = 0;
     __syncthreads();
     bool full = false;
+    STAMP(1);
 
     // 1) resident slice regions (state) ----------------------------------------------
     for (int j = 0; j < p.n_src; j++) {
@@ -549,6 +621,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
             }
         }
     }
+    STAMP(2);
     // 2) staged records of bucket (lane, r >> drop) over all staged batches, keeping the
     //    keys of region r ----------------------------------------------------------------
     auto in_region = [&](int64_t k) -> bool {
@@ -609,6 +682,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     }
     if (full) atomicOr(&s_flags, 4u);
     __syncthreads();
+    STAMP(3);
 
     // 3) compaction: thread tid owns slots [4 tid, 4 tid + 4); tid 0 also owns kSlots --
     uint32_t mine = 0;
@@ -688,6 +762,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
         p.dst.counts[r] = total;
         if (p.dst_total) atomicAdd(p.dst_total, (unsigned long long)((int64_t)total - (int64_t)old));
     }
+    STAMP(4);
 }
 
 hipError_t launch_merge(const MergeParams& p, hipStream_t s) {
