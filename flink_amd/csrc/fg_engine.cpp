@@ -954,7 +954,9 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.7) < keys) bits++;
     h->region_bits = bits;
     h->P = 1 << bits;
-    h->stage_bits = std::max(bits - kStageDrop, 0);
+    int drop = kStageDrop;
+    if (const char* e = getenv("FG_STAGE_DROP")) drop = std::max(0, std::min(4, atoi(e)));   // tuning knob
+    h->stage_bits = std::max(bits - drop, 0);
     h->lanes = kMaxLanes;
     while (h->lanes > 1 && (h->lanes << h->stage_bits) > kMaxStageBuckets) h->lanes >>= 1;
     h->F = h->lanes << h->stage_bits;
