@@ -91,26 +91,39 @@ struct SliceTable {
     int64_t upper = 0;    // host-side upper bound of entries
 };
 
+// One ingest pass: the bucket scan of its records over all lanes; lane l's records sit at
+// [lane_start[l], lane_start[l] + lane_n[l]) of lane l's staged area.
 struct Staged {
-    int64_t base = 0;
-    int64_t n = 0;
+    DevBuf bucket_off;    // F + 1 uint32 (lane-major)
+    int64_t lane_start[kMaxLanes] = {0, 0, 0, 0};
+    int64_t lane_n[kMaxLanes] = {0, 0, 0, 0};
     bool has_null = false;
-    DevBuf bucket_off;    // F + 1 uint32
+    int refs = 0;         // lanes still holding records of this pass
+};
+
+// A slice lane of the staged buffer (RecordsWindowBuffer analogue, one per live slice):
+// slice index q = slice_end / slice (mod lanes == lane), records staged, and the passes
+// that hold them.
+constexpr int64_t kEmptyLane = INT64_MIN;
+struct Lane {
+    int64_t q = kEmptyLane;
+    int64_t fill = 0;
+    std::vector<Staged*> passes;
 };
 
 struct DevCounters {     // device scratch words read back after the count pass
     unsigned long long drops;
     unsigned long long lane_mask;
     long long qmin, qmax;
+    unsigned long long lane_total[kMaxLanes];
 };
 struct Counters {        // host view: per-lane slice index ranges (min > max: lane idle)
     unsigned long long drops;
     long long qmin, qmax;
     long long lane_min[kMaxLanes];
     long long lane_max[kMaxLanes];
+    long long lane_total[kMaxLanes];
 };
-
-constexpr int64_t kEmptyLane = INT64_MIN;
 
 enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE, K_NCLASS };
 const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan", "ingest_scatter", "merge_flush",
@@ -134,7 +147,7 @@ struct fg_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    int region_bits = 0, stage_bits = 0, P = 1, lanes = 1, F = 1, grid = 256;
+    int region_bits = 0, P = 1, lanes = 1, F = 1, grid = 256, merge_grid = 256;
     int64_t slice_phase = 0;   // slice ends are == slice_phase (mod slice)
 
     // processor / timer state
@@ -143,15 +156,13 @@ struct fg_handle {
     int64_t timer_wm = JMIN;
     int64_t late_dropped = 0;
 
-    // staged buffer (RecordsWindowBuffer analogue)
-    int64_t staged_cap = 0, staged_n = 0;
+    // staged buffer (RecordsWindowBuffer analogue): one area of lane_cap records per lane
+    int64_t lane_cap = 0;
     int st_stride = 2;          // int64 words per staged record: {key, val} or {key}
     DevBuf st_rec, st_null;
-    std::vector<std::unique_ptr<Staged>> staged;
-    std::vector<std::unique_ptr<Staged>> staged_pool;
-    int64_t lane_q[kMaxLanes];
-    int64_t lane_records[kMaxLanes];
-    int64_t min_slice_end = JMAX;
+    Lane lane[kMaxLanes];
+    std::vector<std::unique_ptr<Staged>> passes;       // live passes
+    std::vector<std::unique_ptr<Staged>> pass_pool;
     int64_t anchor_start = JMIN;   // a recent slice start: base of the 32-bit rowtime fast path
 
     // ingest scratch
@@ -187,8 +198,6 @@ struct fg_handle {
     // stats
     int64_t records_in = 0, rows_fired = 0, flushes = 0;
     bool timing = false;
-    bool stamps_on = false;
-    DevBuf d_stamps;
     KStat kstat[K_NCLASS];
     std::vector<PendingEv> pend;
     std::vector<hipEvent_t> ev_pool;
@@ -365,35 +374,71 @@ void fill_emit(fg_handle* h, MergeParams& p, int64_t wend) {
     p.out_cap = h->out_cap;
 }
 
-// RecordsWindowBuffer.flush (:108-119) + AggCombiner.combine (:76-115): merge every staged
-// lane into its slice table. With `fire` (TUMBLE only), a lane whose window's timer fires
-// in this advance is combined and fired in the same pass: its rows are emitted straight
-// from LDS and the slice is never written back (SliceUnsharedWindowAggProcessor.fireWindow
-// + clearWindow, :46-54 / AbstractWindowAggProcessor.java:200-206).
-int flush(fg_handle* h, const FireRange* fire = nullptr) {
-    if (h->staged_n == 0 && h->staged.empty()) return FG_OK;
-    // staged batch descriptors
-    std::vector<StagedBatch> sb;
-    for (auto& s : h->staged) {
-        StagedBatch b{};
-        b.rec = h->st_rec.as<int64_t>() + s->base * h->st_stride;
-        b.val = nullptr;
-        b.vnull = s->has_null ? h->st_null.as<uint8_t>() + s->base : nullptr;
-        b.bucket_off = s->bucket_off.as<uint32_t>();
-        b.is_acc = 0;
-        b.stride = h->st_stride;
-        sb.push_back(b);
+bool staged_any(const fg_handle* h) {
+    for (int l = 0; l < h->lanes; l++)
+        if (h->lane[l].q != kEmptyLane) return true;
+    return false;
+}
+int64_t staged_records(const fg_handle* h) {
+    int64_t n = 0;
+    for (int l = 0; l < h->lanes; l++) n += h->lane[l].fill;
+    return n;
+}
+int64_t min_staged_slice_end(const fg_handle* h) {
+    int64_t m = JMAX;
+    for (int l = 0; l < h->lanes; l++)
+        if (h->lane[l].q != kEmptyLane) m = std::min(m, slice_end_of(h, h->lane[l].q));
+    return m;
+}
+int64_t* lane_rec(const fg_handle* h, int l) { return h->st_rec.as<int64_t>() + (int64_t)l * h->lane_cap * h->st_stride; }
+uint8_t* lane_null(const fg_handle* h, int l) { return h->st_null.as<uint8_t>() + (int64_t)l * h->lane_cap; }
+
+// empty lane l; a pass returns to the pool once no lane holds its records
+void release_lane(fg_handle* h, int l) {
+    for (Staged* s : h->lane[l].passes) {
+        if (--s->refs > 0) continue;
+        for (size_t i = 0; i < h->passes.size(); i++) {
+            if (h->passes[i].get() != s) continue;
+            h->pass_pool.push_back(std::move(h->passes[i]));
+            h->passes.erase(h->passes.begin() + (long)i);
+            break;
+        }
     }
-    const StagedBatch* d_sb = nullptr;
-    int rc = arena_put(h, sb.data(), sb.size(), &d_sb);
-    if (rc) return rc;
+    h->lane[l] = Lane{};
+}
+
+int merge_grid(const fg_handle* h) { return std::min(h->P, h->merge_grid); }
+
+// RecordsWindowBuffer.flush (:108-119) + AggCombiner.combine (:76-115): merge staged slice
+// lanes into their slice tables -- every lane, or (only_fired) the lanes whose slice is
+// fired at the current progress, the only ones a window firing now can read; the others
+// stay staged (their merge order does not change results beyond f64 summation order).
+// With `fire` (TUMBLE only), a lane whose window's timer fires in this advance is combined
+// and fired in the same pass: its rows are emitted straight from LDS and the slice is
+// never written back (SliceUnsharedWindowAggProcessor.fireWindow + clearWindow, :46-54 /
+// AbstractWindowAggProcessor.java:200-206).
+int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire) {
+    if (sel.empty()) return FG_OK;
     if (h->out_count_reset) HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
     else HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
     std::vector<int64_t> fired_tables;
     bool any_emit = false;
-    for (int l = 0; l < h->lanes; l++) {
-        if (h->lane_q[l] == kEmptyLane) continue;
-        const int64_t se = slice_end_of(h, h->lane_q[l]);
+    int rc;
+    for (int l : sel) {
+        const Lane& ln = h->lane[l];
+        const int64_t se = slice_end_of(h, ln.q);
+        std::vector<StagedBatch> sb;
+        for (Staged* s : ln.passes) {
+            StagedBatch b{};
+            b.rec = lane_rec(h, l) + s->lane_start[l] * h->st_stride;
+            b.vnull = s->has_null ? lane_null(h, l) + s->lane_start[l] : nullptr;
+            b.bucket_off = s->bucket_off.as<uint32_t>() + ((int64_t)l << h->region_bits);
+            b.stride = h->st_stride;
+            sb.push_back(b);
+        }
+        const StagedBatch* d_sb = nullptr;
+        rc = arena_put(h, sb.data(), sb.size(), &d_sb);
+        if (rc) return rc;
         SliceTable* t = nullptr;
         rc = table_get(h, se, true, &t);
         if (rc) return rc;
@@ -402,21 +447,20 @@ int flush(fg_handle* h, const FireRange* fire = nullptr) {
         if (fire_now) {
             rc = reset_out_count(h);
             if (rc) return rc;
-            const int64_t ub = std::min<int64_t>(t->upper + h->lane_records[l], (int64_t)kRegionCap * h->P);
+            const int64_t ub = std::min<int64_t>(t->upper + ln.fill, (int64_t)kRegionCap * h->P);
             rc = ensure_out(h, h->out_n + h->pending_out + ub);
             if (rc) return rc;
             h->pending_out += ub;
         }
         TableRef tr = ref_of(t);
         const TableRef* d_src = nullptr;
-        rc = arena_put(h, &tr, 1, &d_src);
-        if (rc) return rc;
+        if (t->upper > 0) {
+            rc = arena_put(h, &tr, 1, &d_src);
+            if (rc) return rc;
+        }
         MergeParams p{};
         p.region_bits = h->region_bits;
-        p.stage_bits = h->stage_bits;
-        p.lanes = h->lanes;
-        p.lane = l;
-        p.n_src = 1;
+        p.n_src = t->upper > 0 ? 1 : 0;
         p.src = d_src;
         p.n_batches = (int)sb.size();
         p.batches = d_sb;
@@ -427,31 +471,15 @@ int flush(fg_handle* h, const FireRange* fire = nullptr) {
         if (fire_now) fill_emit(h, p, se);
         p.overflow = h->scalars.as<unsigned int>();
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
-        if (h->stamps_on) {
-            HIPCHK(h, h->d_stamps.ensure(8 * 8 * (size_t)h->P));
-            HIPCHK(h, hipMemsetAsync(h->d_stamps.p, 0, 8 * 8 * (size_t)h->P, h->stream));
-            p.stamps = h->d_stamps.as<unsigned long long>();
-        }
         {
-            KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, h->lane_records[l]);
-            HIPCHK(h, launch_merge(p, h->stream));
-        }
-        if (h->stamps_on) {
-            std::vector<unsigned long long> st(8 * (size_t)h->P);
-            HIPCHK(h, hipMemcpyAsync(st.data(), h->d_stamps.p, 8 * st.size(), hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(h, hipStreamSynchronize(h->stream));
-            double ph[4] = {0, 0, 0, 0};
-            for (int b = 0; b < h->P; b++)
-                for (int i = 0; i < 4; i++) ph[i] += (double)(st[b * 8 + i + 1] - st[b * 8 + i]);
-            fprintf(stderr, "[fg stamps] %s lane %d records %lld: init %.0f src %.0f staged %.0f out %.0f (avg cycles/WG)\n",
-                    fire_now ? "flush_fire" : "flush", l, (long long)h->lane_records[l], ph[0] / h->P, ph[1] / h->P,
-                    ph[2] / h->P, ph[3] / h->P);
+            KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
+            HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
         }
         if (fire_now) {
             fired_tables.push_back(se);
             any_emit = true;
         } else {
-            t->upper = std::min<int64_t>(t->upper + h->lane_records[l], (int64_t)kRegionCap * h->P);
+            t->upper = std::min<int64_t>(t->upper + ln.fill, (int64_t)kRegionCap * h->P);
         }
     }
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
@@ -466,17 +494,21 @@ int flush(fg_handle* h, const FireRange* fire = nullptr) {
         h->pending_out = 0;
     }
     for (int64_t se : fired_tables) table_free(h, se);
-    for (auto& s : h->staged) h->staged_pool.push_back(std::move(s));
-    h->staged.clear();
-    h->staged_n = 0;
-    for (int l = 0; l < kMaxLanes; l++) {
-        h->lane_q[l] = kEmptyLane;
-        h->lane_records[l] = 0;
-    }
-    h->min_slice_end = JMAX;
+    for (int l : sel) release_lane(h, l);
     h->flushes++;
     return FG_OK;
 }
+
+int flush(fg_handle* h, const FireRange* fire = nullptr, bool only_fired = false) {
+    std::vector<int> sel;
+    for (int l = 0; l < h->lanes; l++) {
+        if (h->lane[l].q == kEmptyLane) continue;
+        if (only_fired && !is_window_fired(h->w, slice_end_of(h, h->lane[l].q), h->current_progress)) continue;
+        sel.push_back(l);
+    }
+    return flush_lanes(h, sel, fire);
+}
+int flush_lane(fg_handle* h, int l) { return flush_lanes(h, std::vector<int>{l}, nullptr); }
 
 int ensure_out(fg_handle* h, int64_t need) {
     if (need <= h->out_cap) return FG_OK;
@@ -509,9 +541,6 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     if (rc) return rc;
     MergeParams p{};
     p.region_bits = h->region_bits;
-    p.stage_bits = h->stage_bits;
-    p.lanes = h->lanes;
-    p.lane = -1;
     p.n_src = (int)refs.size();
     p.src = d_src;
     p.val_type = h->cfg.val_type;
@@ -522,7 +551,7 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     p.overflow = h->scalars.as<unsigned int>();
     {
         KTimer kt(h, K_FIRE, 0);
-        HIPCHK(h, launch_merge(p, h->stream));
+        HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
     }
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
     rc = sync(h);
@@ -702,7 +731,21 @@ int seed_anchor(fg_handle* h, const int64_t* ts_dev, const int64_t* ts_host) {
     return FG_OK;
 }
 
-// one ingest pass over the device-resident batch with a slice filter
+// grow the per-lane staged areas to hold `need` records per lane (all lanes empty)
+int grow_lanes(fg_handle* h, int64_t need) {
+    if (need <= h->lane_cap) return FG_OK;
+    if (staged_any(h)) return h->fail(FG_ESTATE, "internal: staged areas grown while holding records");
+    const int64_t cap = std::max<int64_t>(need, h->lane_cap + h->lane_cap / 2);
+    HIPCHK(h, h->st_rec.ensure(8 * (size_t)h->st_stride * h->lanes * cap));
+    HIPCHK(h, h->st_null.ensure((size_t)h->lanes * cap));
+    h->lane_cap = cap;
+    return FG_OK;
+}
+
+// one ingest pass over the device-resident batch with a slice filter: count pass
+// (slice assignment, late rules, bucket histogram), then -- once the batch's slices are
+// known to fit the staged lanes -- bucket scan and scatter into the lanes' staged areas.
+// Returns -1 when the batch spans more slices than the lanes can hold.
 int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
                 const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
     IngestParams p{};
@@ -714,7 +757,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.vnull = vnull;
     p.progress = h->current_progress;
     p.lanes = h->lanes;
-    p.stage_bits = h->stage_bits;
+    p.region_bits = h->region_bits;
     p.filter_lo = flo;
     p.filter_hi = fhi;
     p.count_drops = count_drops ? 1 : 0;
@@ -724,8 +767,6 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.hist = h->hist.as<uint32_t>();
     set_fast_path(h, &p);
     DevCounters init{};
-    init.drops = 0;
-    init.lane_mask = 0;
     init.qmin = JMAX;
     init.qmax = JMIN;
     std::memcpy(h->h_counters.p, &init, sizeof init);
@@ -735,6 +776,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.lane_mask = &dc->lane_mask;
     p.qmin = &dc->qmin;
     p.qmax = &dc->qmax;
+    p.lane_total = dc->lane_total;
     {
         KTimer kt(h, K_COUNT, n);
         HIPCHK(h, launch_ingest_count(p, h->stream));
@@ -742,40 +784,61 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
     int rc = sync(h);
     if (rc) return rc;
+    DevCounters got;
+    std::memcpy(&got, h->h_counters.p, sizeof got);
+    out->drops = got.drops;
+    out->qmin = got.qmin;
+    out->qmax = got.qmax;
+    for (int l = 0; l < kMaxLanes; l++) {
+        out->lane_min[l] = JMAX;
+        out->lane_max[l] = JMIN;
+        out->lane_total[l] = (long long)got.lane_total[l];
+    }
+    if (got.qmin > got.qmax) return FG_OK;   // nothing accepted
+    h->anchor_start = jsub(slice_end_of(h, got.qmin), h->w.slice);
+    if ((uint64_t)(got.qmax - got.qmin) >= (uint64_t)h->lanes) return -1;   // more slices than lanes
+    for (int64_t q = got.qmin; q <= got.qmax; q++) {
+        const int l = (int)(q & (h->lanes - 1));
+        if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
+    }
+
+    // make room: a lane holding another slice, or without space for the batch's records,
+    // is flushed into its slice table first (the EOFException flush of RecordsWindowBuffer
+    // :91-96, per lane)
+    int64_t need = 0;
+    for (int l = 0; l < h->lanes; l++) need = std::max<int64_t>(need, out->lane_total[l]);
+    if (need > h->lane_cap) {
+        rc = flush(h);
+        if (rc) return rc;
+        rc = grow_lanes(h, need);
+        if (rc) return rc;
+    }
     {
-        DevCounters got;
-        std::memcpy(&got, h->h_counters.p, sizeof got);
-        out->drops = got.drops;
-        out->qmin = got.qmin;
-        out->qmax = got.qmax;
-        for (int l = 0; l < kMaxLanes; l++) {
-            out->lane_min[l] = JMAX;
-            out->lane_max[l] = JMIN;
+        bool any = false;
+        for (int l = 0; l < h->lanes; l++) {
+            if (out->lane_total[l] == 0) continue;
+            const Lane& ln = h->lane[l];
+            if (ln.q != kEmptyLane && (ln.q != out->lane_min[l] || ln.fill + out->lane_total[l] > h->lane_cap))
+                any = true;
         }
-        if (got.qmin <= got.qmax) {
-            h->anchor_start = jsub(slice_end_of(h, got.qmin), h->w.slice);
-            if ((uint64_t)(got.qmax - got.qmin) >= (uint64_t)h->lanes) return -1;   // lanes conflict
-            for (int64_t q = got.qmin; q <= got.qmax; q++) {
-                const int l = (int)(q & (h->lanes - 1));
-                if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
+        if (any) {
+            // flush only the blocking lanes: merge them (no fire) into their tables
+            for (int l = 0; l < h->lanes; l++) {
+                if (out->lane_total[l] == 0) continue;
+                const Lane& ln = h->lane[l];
+                if (ln.q == kEmptyLane || (ln.q == out->lane_min[l] && ln.fill + out->lane_total[l] <= h->lane_cap))
+                    continue;
+                rc = flush_lane(h, l);
+                if (rc) return rc;
             }
         }
     }
 
-    // lane compatibility with the staged buffer
-    bool conflict = false;
-    for (int l = 0; l < h->lanes; l++) {
-        if (out->lane_min[l] > out->lane_max[l]) continue;
-        if (out->lane_min[l] != out->lane_max[l]) conflict = true;
-        if (h->lane_q[l] != kEmptyLane && h->lane_q[l] != out->lane_min[l]) conflict = true;
-    }
-    if (conflict) return -1;   // caller falls back to filtered passes
-
-    // per-bucket prefix over workgroups, bucket bases, then scatter into the staged buffer
+    // per-bucket prefix over workgroups, bucket bases, then scatter into the lane areas
     std::unique_ptr<Staged> s;
-    if (!h->staged_pool.empty()) {
-        s = std::move(h->staged_pool.back());
-        h->staged_pool.pop_back();
+    if (!h->pass_pool.empty()) {
+        s = std::move(h->pass_pool.back());
+        h->pass_pool.pop_back();
     } else {
         s.reset(new Staged());
     }
@@ -787,58 +850,47 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
                                   h->scan_tmp.as<uint32_t>(), h->stream));
     }
     p.bucket_base = s->bucket_off.as<uint32_t>();
+    // staged position of bucket b (lane l) = bucket_base[b] - (records of lanes < l) + lane l's
+    // area start + its fill
+    int64_t before = 0;
+    for (int l = 0; l < kMaxLanes; l++) {
+        p.lane_shift[l] = 0;
+        s->lane_start[l] = 0;
+        s->lane_n[l] = 0;
+        if (l >= h->lanes) continue;
+        p.lane_shift[l] = (int64_t)l * h->lane_cap + h->lane[l].fill - before;
+        before += out->lane_total[l];
+    }
     // tile-sorted scatter when at most two lanes are active and their buckets fit LDS
     {
         int nslots = 0;
         for (int l = 0; l < kMaxLanes; l++) p.lane_slot[l] = -1;
         for (int l = 0; l < h->lanes; l++)
-            if (out->lane_min[l] <= out->lane_max[l]) p.lane_slot[l] = nslots++;
-        p.sorted = (nslots >= 1 && nslots <= 2 && (nslots << h->stage_bits) <= kMaxSortedBuckets) ? 1 : 0;
+            if (out->lane_total[l] > 0) p.lane_slot[l] = nslots++;
+        p.sorted = (nslots >= 1 && nslots <= 2 && (nslots << h->region_bits) <= kMaxSortedBuckets) ? 1 : 0;
     }
     p.st_stride = h->st_stride;
-    p.st_rec = h->st_rec.as<int64_t>() + h->staged_n * h->st_stride;
-    p.st_null = vnull ? h->st_null.as<uint8_t>() + h->staged_n : nullptr;
+    p.st_rec = h->st_rec.as<int64_t>();
+    p.st_null = vnull ? h->st_null.as<uint8_t>() : nullptr;
     if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
-    if (h->stamps_on) {
-        HIPCHK(h, h->d_stamps.ensure(8 * 8 * (size_t)std::max(h->P, p.grid)));
-        HIPCHK(h, hipMemsetAsync(h->d_stamps.p, 0, 8 * 8 * (size_t)p.grid, h->stream));
-        p.stamps = h->d_stamps.as<unsigned long long>();
-    }
     {
         KTimer kt(h, K_SCATTER, n);
         HIPCHK(h, launch_ingest_scatter(p, h->stream));
     }
-    if (h->stamps_on && p.sorted) {
-        std::vector<unsigned long long> st(8 * (size_t)p.grid);
-        HIPCHK(h, hipMemcpyAsync(st.data(), h->d_stamps.p, 8 * st.size(), hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        double ph[4] = {0, 0, 0, 0};
-        for (int b = 0; b < p.grid; b++)
-            for (int i = 0; i < 4; i++) ph[i] += (double)st[b * 8 + i];
-        fprintf(stderr, "[fg stamps] scatter n %lld: load+classify+rank %.0f scan %.0f rounds %.0f cursors %.0f (avg cycles/WG)\n",
-                (long long)n, ph[0] / p.grid, ph[1] / p.grid, ph[2] / p.grid, ph[3] / p.grid);
-    }
-    int64_t staged_now = 0;
-    for (int l = 0; l < h->lanes; l++) {
-        if (out->lane_min[l] > out->lane_max[l]) continue;
-        h->lane_q[l] = out->lane_min[l];
-        h->min_slice_end = std::min(h->min_slice_end, slice_end_of(h, out->lane_min[l]));
-    }
-    // per-lane record totals for output sizing: read the bucket offsets of each lane boundary
-    std::vector<uint32_t> lb(h->lanes + 1);
-    for (int l = 0; l <= h->lanes; l++) {
-        HIPCHK(h, hipMemcpyAsync(&lb[l], s->bucket_off.as<uint32_t>() + ((int64_t)l << h->stage_bits), sizeof(uint32_t),
-                                 hipMemcpyDeviceToHost, h->stream));
-    }
-    rc = sync(h);
-    if (rc) return rc;
-    for (int l = 0; l < h->lanes; l++) h->lane_records[l] += (int64_t)(lb[l + 1] - lb[l]);
-    staged_now = (int64_t)lb[h->lanes];
-    s->base = h->staged_n;
-    s->n = staged_now;
     s->has_null = vnull != nullptr;
-    h->staged_n += staged_now;
-    h->staged.push_back(std::move(s));
+    s->refs = 0;
+    for (int l = 0; l < h->lanes; l++) {
+        if (out->lane_total[l] == 0) continue;
+        Lane& ln = h->lane[l];
+        s->lane_start[l] = ln.fill;
+        s->lane_n[l] = out->lane_total[l];
+        s->refs++;
+        ln.q = out->lane_min[l];
+        ln.fill += out->lane_total[l];
+        ln.passes.push_back(s.get());
+    }
+    if (s->refs > 0) h->passes.push_back(std::move(s));
+    else h->pass_pool.push_back(std::move(s));
     return FG_OK;
 }
 
@@ -928,9 +980,6 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     h->cfg = *cfg;
     h->device = cfg->device_id;
     h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
-#ifdef FG_STAMPS
-    h->stamps_on = getenv("FG_MERGE_STAMPS") != nullptr;
-#endif
     if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         g_open_error = "hipSetDevice/hipStreamCreate failed";
         return FG_EDEVICE;
@@ -954,24 +1003,22 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.7) < keys) bits++;
     h->region_bits = bits;
     h->P = 1 << bits;
-    int drop = kStageDrop;
-    if (const char* e = getenv("FG_STAGE_DROP")) drop = std::max(0, std::min(4, atoi(e)));   // tuning knob
-    h->stage_bits = std::max(bits - drop, 0);
+    // the staging buckets are the state regions: one region per merge workgroup pass
     h->lanes = kMaxLanes;
-    while (h->lanes > 1 && (h->lanes << h->stage_bits) > kMaxStageBuckets) h->lanes >>= 1;
-    h->F = h->lanes << h->stage_bits;
+    while (h->lanes > 1 && (h->lanes << h->region_bits) > kMaxStageBuckets) h->lanes >>= 1;
+    h->F = h->lanes << h->region_bits;
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) h->grid = std::max(1, prop.multiProcessorCount);
-    for (int l = 0; l < kMaxLanes; l++) {
-        h->lane_q[l] = kEmptyLane;
-        h->lane_records[l] = 0;
+    if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) {
+        h->grid = std::max(1, prop.multiProcessorCount);
+        h->merge_grid = std::max(1, prop.multiProcessorCount);
     }
-    h->staged_cap = cfg->buffer_records > 0 ? cfg->buffer_records : (int64_t)1 << 26;
+    // per-lane staged areas: buffer_records records per lane
+    h->lane_cap = cfg->buffer_records > 0 ? cfg->buffer_records : (int64_t)1 << 26;
     fg_handle* hp = h.get();
     auto chk = [&](hipError_t e) { return e == hipSuccess; };
     hp->st_stride = cfg->val_type == FG_VAL_NONE ? 1 : 2;
-    bool ok = chk(hp->st_rec.ensure(8 * (size_t)hp->st_stride * hp->staged_cap)) &&
-              chk(hp->st_null.ensure(hp->staged_cap)) &&
+    bool ok = chk(hp->st_rec.ensure(8 * (size_t)hp->st_stride * hp->lanes * hp->lane_cap)) &&
+              chk(hp->st_null.ensure((size_t)hp->lanes * hp->lane_cap)) &&
               chk(hp->hist.ensure(4 * (size_t)hp->F * hp->grid)) &&
               chk(hp->totals.ensure(4 * ((size_t)hp->F + 1))) &&
               chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F))) &&
@@ -1015,16 +1062,8 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
             vnull = h->in_null.as<uint8_t>();
         }
     }
-    // EOFException semantics (RecordsWindowBuffer.java:91-96): flush, then retry
-    if (h->staged_n + n > h->staged_cap) {
-        int rc = flush(h);
-        if (rc) return rc;
-        if (n > h->staged_cap) {
-            HIPCHK(h, h->st_rec.ensure(8 * (size_t)h->st_stride * n));
-            HIPCHK(h, h->st_null.ensure(n));
-            h->staged_cap = n;
-        }
-    }
+    // EOFException semantics (RecordsWindowBuffer.java:91-96) are applied per lane inside
+    // ingest_pass: a lane without room is flushed into its slice table, then the pass stages
     h->records_in += n;
     {
         int rc0 = b->location == FG_HOST ? seed_anchor(h, nullptr, b->rowtime) : seed_anchor(h, ts, nullptr);
@@ -1074,8 +1113,8 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
         if (wm > h->current_progress) {
             h->current_progress = wm;
             if (h->current_progress >= h->next_trigger) {
-                if (h->staged_n > 0 && is_window_fired(h->w, h->min_slice_end, wm)) {
-                    rc = flush(h, fuse);
+                if (staged_any(h) && is_window_fired(h->w, min_staged_slice_end(h), wm)) {
+                    rc = flush(h, fuse, true);
                     if (rc) return rc;
                 }
                 h->next_trigger = next_trigger_watermark(wm, h->w.slice);
@@ -1084,8 +1123,8 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     } else {
         // DataStream WindowOperator: records are in state before any timer fires
         if (wm > h->current_progress) h->current_progress = wm;
-        if (h->staged_n > 0 && is_window_fired(h->w, h->min_slice_end, wm)) {
-            rc = flush(h, fuse);
+        if (staged_any(h) && is_window_fired(h->w, min_staged_slice_end(h), wm)) {
+            rc = flush(h, fuse, true);
             if (rc) return rc;
         }
     }
@@ -1199,12 +1238,12 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     for (auto& kv : by_slice) {
         const auto& idx = kv.second;
         const int64_t m = (int64_t)idx.size();
-        const int NB = 1 << h->stage_bits;
+        const int NB = 1 << h->region_bits;
         std::vector<uint32_t> off(NB + 1, 0);
         std::vector<uint32_t> reg(m);
         for (int64_t j = 0; j < m; j++) {
             const int64_t k = in->key[idx[j]];
-            reg[j] = h->stage_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)k) >> (64 - h->stage_bits));
+            reg[j] = h->region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)k) >> (64 - h->region_bits));
             off[reg[j] + 1]++;
         }
         for (int r = 0; r < NB; r++) off[r + 1] += off[r];
@@ -1250,9 +1289,6 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
         MergeParams p{};
         p.region_bits = h->region_bits;
-        p.stage_bits = h->stage_bits;
-        p.lanes = 1;
-        p.lane = 0;
         p.n_src = 1;
         p.src = d_src;
         p.n_batches = 1;
@@ -1264,7 +1300,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
         {
             KTimer kt(h, K_RESTORE, m);
-            HIPCHK(h, launch_merge(p, h->stream));
+            HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
         }
         HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
         rc = sync(h);
@@ -1290,7 +1326,7 @@ int fg_late_dropped(fg_handle* h, int64_t* out) {
 int fg_get_stats(fg_handle* h, fg_stats* out) {
     if (!h || !out) return FG_EINVAL;
     out->records_in = h->records_in;
-    out->records_staged = h->staged_n;
+    out->records_staged = staged_records(h);
     out->late_dropped = h->late_dropped;
     out->rows_fired = h->rows_fired;
     out->flushes = h->flushes;
@@ -1313,14 +1349,7 @@ int fg_reset(fg_handle* h) {
     std::vector<int64_t> ends;
     for (auto& kv : h->tables) ends.push_back(kv.first);
     for (int64_t e : ends) table_free(h, e);
-    for (auto& s : h->staged) h->staged_pool.push_back(std::move(s));
-    h->staged.clear();
-    h->staged_n = 0;
-    for (int l = 0; l < kMaxLanes; l++) {
-        h->lane_q[l] = kEmptyLane;
-        h->lane_records[l] = 0;
-    }
-    h->min_slice_end = JMAX;
+    for (int l = 0; l < h->lanes; l++) release_lane(h, l);
     h->anchor_start = JMIN;
     h->current_progress = JMIN;
     h->next_trigger = JMIN;
@@ -1359,8 +1388,9 @@ void fg_close(fg_handle* h) {
         // release device memory before the stream
         h->tables.clear();
         h->table_pool.clear();
-        h->staged.clear();
-        h->staged_pool.clear();
+        for (int l = 0; l < kMaxLanes; l++) h->lane[l] = Lane{};
+        h->passes.clear();
+        h->pass_pool.clear();
     }
     for (auto& p : h->pend) {
         h->ev_pool.push_back(p.a);

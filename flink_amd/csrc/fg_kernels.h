@@ -12,13 +12,12 @@ namespace fg {
 constexpr int kSlotBits = 12;
 constexpr int kSlots = 1 << kSlotBits;        // 4096 slots x 32 B = 128 KiB of LDS
 constexpr int kRegionCap = 3584;              // max entries per region in HBM (87.5 % of kSlots)
-constexpr int kMergeThreads = 1024;
+constexpr int kMergeThreads = 1024;           // persistent merge: one 1024-thread workgroup per CU
 constexpr int kIngestThreads = 1024;
 constexpr int kMaxLanes = 4;
-constexpr int kStageDrop = 0;                 // state regions per staging bucket = 2^kStageDrop
-constexpr int kMaxStageBuckets = 32768;       // lanes << stage_bits (count / direct scatter LDS)
-constexpr int kMaxSortedBuckets = 8192;       // lane slots << stage_bits (tile-sorted scatter LDS)
-constexpr int kTile = 12288;                  // records per sorted-scatter tile (12 per thread)
+constexpr int kMaxStageBuckets = 32768;       // lanes << region_bits (count / direct scatter LDS)
+constexpr int kMaxSortedBuckets = 8192;       // lane slots << region_bits (tile-sorted scatter LDS)
+constexpr int kTile = 8192;                   // records per sorted-scatter tile (8 per thread)
 constexpr int kMaxAggs = 8;
 
 // One slice table in HBM: P regions, each region an SoA block of kRegionCap entries:
@@ -29,15 +28,18 @@ struct TableRef {
     uint32_t* counts;   // entries per region
 };
 
-// A staged batch (records already bucketed by (lane, region)). Records are AoS
-// {key, value bits} (stride 2) or {key} (stride 1, COUNT(*)-only queries).
+// One staged batch of one slice lane. The records of region r are
+//   rec[bucket_off[r] - bucket_off[0] .. bucket_off[r + 1] - bucket_off[0])
+// (bucket_off points at the batch's lane slice of its [lanes * P + 1] bucket scan).
+// Records are AoS {key, value bits} (stride 2) or {key} (stride 1, COUNT(*)-only).
+// Restore images (is_acc) are SoA accumulators: rec = keys, val / cnt_star / cnt_null.
 struct StagedBatch {
-    const int64_t* rec;        // is_acc == 0: records; is_acc == 1: keys
-    const int64_t* val;        // is_acc == 1 only: the `sum` accumulator
-    const uint8_t* vnull;      // may be null
-    const int64_t* cnt_star;   // only when is_acc (restore images)
-    const int64_t* cnt_null;   // only when is_acc
-    const uint32_t* bucket_off;  // [lanes * P + 1]
+    const int64_t* rec;
+    const int64_t* val;        // is_acc only: the `sum` accumulator
+    const uint8_t* vnull;      // NULL flags aligned with rec (may be null)
+    const int64_t* cnt_star;   // is_acc only
+    const int64_t* cnt_null;   // is_acc only
+    const uint32_t* bucket_off;
     int32_t is_acc;
     int32_t stride;            // int64 words per record (1 or 2)
 };
@@ -57,7 +59,7 @@ struct IngestParams {
     int64_t qbase;             // floor_div(tbase, S) + 1
     int64_t fired_lim;         // progress + 1 + tz (saturated): slice ends <= fired_lim are fired
     int32_t lanes;             // power of two <= kMaxLanes
-    int32_t stage_bits;        // log2(staging buckets per lane); bucket = top stage_bits of fmix64(key)
+    int32_t region_bits;       // log2(P); bucket = (slice lane, top region_bits of fmix64(key))
     int64_t filter_lo;         // slice-index filter [lo, hi): floor_div(target, slice)
     int64_t filter_hi;
     int32_t count_drops;
@@ -70,21 +72,19 @@ struct IngestParams {
     unsigned long long* drops;
     long long* qmin;           // min / max slice index of the accepted records
     long long* qmax;
-    unsigned long long* lane_mask;   // bit l: some record has slice index == l (mod lanes)
+    unsigned long long* lane_mask;    // bit l: some record has slice index == l (mod lanes)
+    unsigned long long* lane_total;   // [kMaxLanes] accepted records per lane
     // scatter inputs/outputs
-    const uint32_t* bucket_base; // [F + 1] exclusive scan of bucket totals
-    int64_t* st_rec;           // AoS {key, val} (stride 2) or {key} (stride 1)
+    const uint32_t* bucket_base; // [F + 1] exclusive scan of bucket totals (lane-major)
+    int64_t lane_shift[kMaxLanes];  // staged position = bucket_base[b] + prefix + lane_shift[lane]
+    int64_t* st_rec;           // staged record area (all lanes), AoS {key, val} or {key}
     int32_t st_stride;
     int32_t pad1;
-    uint8_t* st_null;
-    unsigned long long* stamps;  // diagnostic builds only (FG_STAMPS): [grid][8] cycles per phase
+    uint8_t* st_null;          // NULL flags at the same positions (may be null)
 };
 
 struct MergeParams {
-    int32_t region_bits;       // log2(P): state regions, one workgroup each
-    int32_t stage_bits;        // staging bucket of region r = r >> (region_bits - stage_bits)
-    int32_t lanes;
-    int32_t lane;              // bucket lane of staged records (-1: none)
+    int32_t region_bits;       // log2(P): state regions
     int32_t n_src;
     const TableRef* src;       // device array [n_src]
     int32_t n_batches;
@@ -107,7 +107,6 @@ struct MergeParams {
     unsigned long long* out_count;
     int64_t out_cap;
     unsigned int* overflow;    // bit0: region overflow, bit1: output overflow, bit2: LDS table full
-    unsigned long long* stamps;  // diagnostic builds only (FG_STAMPS): [grid][8] s_memtime per phase
 };
 
 struct ExportParams {
@@ -128,7 +127,8 @@ size_t scan_tmp_words(int64_t n);
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, hipStream_t s);
 // per bucket b: hist[g][b] <- sum_{g' < g} hist[g'][b]; totals[b] <- sum_g hist[g][b]
 hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid, hipStream_t s);
-hipError_t launch_merge(const MergeParams& p, hipStream_t s);
+// persistent merge over the P regions: `workgroups` <= P workgroups, each a strided set of regions
+hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
 hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out,
                              hipStream_t s);

@@ -5,9 +5,10 @@
 //                                      bucketing records by (slice lane, state region):
 //                                      replaces RecordsWindowBuffer.addElement
 //                                      (TR/operators/aggregate/window/buffers/RecordsWindowBuffer.java:81-97)
-//   k_merge                            a4/a5/a7: one workgroup per state region builds an LDS
-//                                      open-addressing table from resident slice regions and the
-//                                      staged records, then writes the region back (flush =
+//   k_merge                            a4/a5/a7: a persistent workgroup per CU walks state regions;
+//                                      per region it builds an LDS open-addressing table from
+//                                      resident slice regions and the staged records, then writes
+//                                      the region back (flush =
 //                                      AggCombiner.combine, combines/AggCombiner.java:76-115)
 //                                      and/or emits fired rows (fireWindow + mergeSlices,
 //                                      processors/SliceSharedWindowAggProcessor.java:64-118)
@@ -41,18 +42,16 @@ __device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int6
     const uint64_t qq = __umul64hi(d, p.div_m);
     const int64_t end_fast = p.tbase + (int64_t)((qq + 1) * (uint64_t)p.w.slice);
     if (p.div_m != 0 && d < (1ull << 32) && ts != JMAX && end_fast > p.fired_lim) {
-        target = end_fast;                      // assignSliceEnd, not fired: no late handling
-        q = p.qbase + (int64_t)qq;
+        q = p.qbase + (int64_t)qq;              // assignSliceEnd, not fired: no late handling
     } else {
         if (!target_slice(p.w, ts, p.progress, &target)) return -1;
         q = floor_div_fast(target, p.w.slice, p.w.rslice);
     }
-    (void)target;
     if (q < p.filter_lo || q >= p.filter_hi) return -2;
     *q_out = q;
     const int lane = (int)(q & (int64_t)(p.lanes - 1));
-    const uint32_t sb = p.stage_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.stage_bits));
-    return (lane << p.stage_bits) | (int)sb;
+    const uint32_t rb = p.region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.region_bits));
+    return (lane << p.region_bits) | (int)rb;
 }
 
 __device__ __forceinline__ void seg_bounds(int64_t n, int grid, int g, int64_t* b, int64_t* e) {
@@ -99,7 +98,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 }
 
 // ----------------------------------------------------------------------------------------
-// ingest: count
+// ingest: count (a1 slice assignment + a2 late rules + bucket histogram per workgroup)
 // ----------------------------------------------------------------------------------------
 constexpr int kMaxBuckets = kMaxStageBuckets;
 
@@ -108,10 +107,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
     __shared__ unsigned long long s_drop;
     __shared__ long long s_qmin, s_qmax;
     __shared__ uint32_t s_mask;
-    const int F = p.lanes << p.stage_bits;
+    __shared__ uint32_t s_lane[kMaxLanes];
+    const int F = p.lanes << p.region_bits;
     const int tid = threadIdx.x;
     for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
     if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_mask = 0; }
+    if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
 
     int64_t beg, end;
@@ -174,8 +175,23 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
         if (qmax != JMIN) atomicMax(&s_qmax, qmax);
     }
     __syncthreads();
-    // workgroup-major histogram: hist[g * F + b] (contiguous stores)
-    for (int b = tid; b < F; b += kIngestThreads) p.hist[(int64_t)blockIdx.x * F + b] = s_hist[b];
+    // workgroup-major histogram: hist[g * F + b] (contiguous stores) + per-lane totals
+    uint32_t lane_part = 0;
+    int lane_of = -1;
+    for (int b = tid; b < F; b += kIngestThreads) {
+        const uint32_t c = s_hist[b];
+        p.hist[(int64_t)blockIdx.x * F + b] = c;
+        const int l = b >> p.region_bits;
+        if (l != lane_of) {
+            if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
+            lane_of = l;
+            lane_part = 0;
+        }
+        lane_part += c;
+    }
+    if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
+    __syncthreads();
+    if (tid < p.lanes && s_lane[tid]) atomicAdd(&p.lane_total[tid], (unsigned long long)s_lane[tid]);
     if (tid == 0) {
         if (p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
         if (s_mask) atomicOr(p.lane_mask, (unsigned long long)s_mask);
@@ -185,99 +201,86 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
 }
 
 // ----------------------------------------------------------------------------------------
-// ingest: scatter into the staged buffer (bucket-major; within a (bucket, workgroup)
-// run the order is arrival order up to LDS atomic ordering)
+// ingest: scatter into the per-lane staged areas (bucket-major within each batch; within
+// a (bucket, workgroup) run the order is arrival order up to LDS atomic ordering)
 // ----------------------------------------------------------------------------------------
 // Direct scatter (any number of active lanes): one 16-B store per record at its
 // bucket cursor (LDS atomic); used when a batch touches more than two slice lanes.
 __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_direct(IngestParams p) {
     __shared__ uint32_t s_cur[kMaxBuckets];
-    const int F = p.lanes << p.stage_bits;
+    const int F = p.lanes << p.region_bits;
     const int tid = threadIdx.x;
-    for (int b = tid; b < F; b += kIngestThreads) s_cur[b] = p.bucket_base[b] + p.hist[(int64_t)blockIdx.x * F + b];
+    for (int b = tid; b < F; b += kIngestThreads)
+        s_cur[b] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)blockIdx.x * F + b] +
+                              p.lane_shift[b >> p.region_bits]);
     __syncthreads();
     int64_t beg, end;
     seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
     const bool has_val = p.val != nullptr;
     const bool has_null = p.vnull != nullptr;
     const bool aos = p.st_stride == 2;
-    auto put = [&](int64_t i, int64_t k, int64_t ts, int64_t v) {
+    for (int64_t i = beg + tid; i < end; i += kIngestThreads) {
+        const int64_t k = p.key[i];
         int64_t q;
-        const int b = classify(p, k, ts, &q);
-        if (b < 0) return;
+        const int b = classify(p, k, p.ts[i], &q);
+        if (b < 0) continue;
         const uint32_t pos = atomicAdd(&s_cur[b], 1u);
-        if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = make_longlong2(k, v);
+        if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = make_longlong2(k, has_val ? p.val[i] : 0);
         else p.st_rec[pos] = k;
         if (has_null) p.st_null[pos] = p.vnull[i];
-    };
-    for (int64_t i = beg + tid; i < end; i += kIngestThreads)
-        put(i, p.key[i], p.ts[i], has_val ? p.val[i] : 0);
+    }
 }
 
-// Tile-sorted scatter (<= 2 active slice lanes): a workgroup reads kTile records into
-// registers (16 per thread), ranks them per bucket with LDS atomics, scans the tile
-// counts, then stages the records bucket-sorted through LDS in four rounds and writes
-// every bucket run with consecutive lanes: contiguous 16-B stores (~4 records = 64 B
-// per run at 4096 buckets) instead of one scattered 16-B store per record.
-constexpr int kPerThread = kTile / kIngestThreads;   // 16
+// Tile-sorted scatter (<= 2 active slice lanes). Per tile of kTile records (8 per thread,
+// kept in registers): rank each record in its bucket with an LDS atomic, scan the tile
+// counts (each thread owns 8 consecutive buckets), advance the buckets' staged cursors,
+// then stage the tile bucket-sorted through LDS in rounds of kRound slots and write
+// every bucket run with consecutive lanes (slot i of bucket b goes to
+// cursor[b] - offset[b + 1] + i). Only LDS is ordered by the barriers: stores stay in
+// flight.
+constexpr int kPerThread = kTile / kIngestThreads;   // 8
 constexpr int kRound = 4096;                         // slots staged per round
-constexpr int kRounds = kTile / kRound;
 
+template <int BPT>   // slot buckets per thread: FS <= BPT * kIngestThreads
 __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(IngestParams p) {
-    __shared__ longlong2 s_rec[kRound];              // 64 KiB
-    __shared__ uint16_t s_bkt[kRound];               // 8 KiB
-    __shared__ uint32_t s_cur[kMaxSortedBuckets];    // global cursor per slot bucket (32 KiB)
-    __shared__ uint32_t s_off[kMaxSortedBuckets + 1];// tile counts, then tile offsets (32 KiB)
+    __shared__ longlong2 s_rec[kRound];                // 64 KiB
+    __shared__ uint16_t s_bkt[kRound];                 // 8 KiB: bucket of each slot
+    __shared__ uint32_t s_off[kMaxSortedBuckets + 1];  // 32 KiB: tile counts, then tile offsets
+    __shared__ uint32_t s_cur[kMaxSortedBuckets];      // 32 KiB: staged cursor (end of the tile's run)
     __shared__ uint32_t s_wave[16];
-    const int P = 1 << p.stage_bits;
-    const int F = p.lanes << p.stage_bits;
-    int nslots = 0;
-#pragma unroll
-    for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
-    const int FS = nslots << p.stage_bits;           // slot buckets
+    const int P = 1 << p.region_bits;
+    const int F = p.lanes << p.region_bits;
     const int tid = threadIdx.x;
-    for (int l = 0; l < kMaxLanes; l++) {
-        const int sl = p.lane_slot[l];
-        if (sl < 0) continue;
-        for (int r = tid; r < P; r += kIngestThreads) {
-            const int bf = l * P + r;
-            s_cur[sl * P + r] = p.bucket_base[bf] + p.hist[(int64_t)blockIdx.x * F + bf];
+    int nslots = 0;
+    {
+        for (int l = 0; l < kMaxLanes; l++) {
+            const int sl = p.lane_slot[l];
+            if (sl < 0) continue;
+            nslots++;
+            for (int r = tid; r < P; r += kIngestThreads) {
+                const int bf = l * P + r;
+                s_cur[sl * P + r] =
+                    (uint32_t)((int64_t)p.bucket_base[bf] + p.hist[(int64_t)blockIdx.x * F + bf] + p.lane_shift[l]);
+            }
         }
+        for (int b = tid; b <= kMaxSortedBuckets; b += kIngestThreads) s_off[b] = 0;
     }
-    for (int b = tid; b <= FS; b += kIngestThreads) s_off[b] = 0;
+    // thread tid owns the slot buckets [tid * BPT, tid * BPT + BPT); bucket FS is the total
+    const int FS = nslots << p.region_bits;
+    constexpr int bpt = BPT;
     __syncthreads();
     int64_t beg, end;
     seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
     const bool has_val = p.val != nullptr;
     const bool has_null = p.vnull != nullptr;
     const bool aos = p.st_stride == 2;
-    const int per_thread_buckets = (FS + kIngestThreads - 1) / kIngestThreads;
-#ifdef FG_STAMPS
-    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
-    unsigned long long tprev = __builtin_amdgcn_s_memtime();
-#define SSTAMP(i)                                                      \
-    do {                                                               \
-        lds_barrier();                                                 \
-        const unsigned long long tn_ = __builtin_amdgcn_s_memtime();   \
-        acc[i] += tn_ - tprev;                                         \
-        tprev = tn_;                                                   \
-    } while (0)
-#else
-#define SSTAMP(i) \
-    do {          \
-    } while (0)
-#endif
 
     for (int64_t t0 = beg; t0 < end; t0 += kTile) {
         const int64_t tn = end - t0 < kTile ? end - t0 : kTile;
         int64_t rk[kPerThread], rv[kPerThread];
         uint32_t rbr[kPerThread];   // (rank << 13) | slot bucket, 0xffffffff = not staged
-        // 1) load (pairs: records t0 + 2*(tid + j*1024) + {0,1}) + classify. Full aligned
-        //    tiles issue every load of the tile before the first use (all in flight).
-        const bool fast = tn == kTile && p.vec;
-        if (fast) {
-            // keys + rowtimes first (all in flight); values are loaded after ranking so their
-            // latency hides behind the bucket scan
+        // 1) load (pairs: records t0 + 2*(tid + j*1024) + {0,1}) + classify + rank
+        if (tn == kTile && p.vec) {
             longlong2 k2[kPerThread / 2], t2[kPerThread / 2];
 #pragma unroll
             for (int j = 0; j < kPerThread / 2; j++) {
@@ -292,11 +295,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                 int64_t q;
                 int b0 = classify(p, k2[j].x, t2[j].x, &q);
                 int b1 = classify(p, k2[j].y, t2[j].y, &q);
-                if (b0 >= 0) b0 = p.lane_slot[b0 >> p.stage_bits] * P + (b0 & (P - 1));
-                if (b1 >= 0) b1 = p.lane_slot[b1 >> p.stage_bits] * P + (b1 & (P - 1));
+                if (b0 >= 0) b0 = p.lane_slot[b0 >> p.region_bits] * P + (b0 & (P - 1));
+                if (b1 >= 0) b1 = p.lane_slot[b1 >> p.region_bits] * P + (b1 & (P - 1));
                 rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
                 rbr[2 * j + 1] = b1 >= 0 ? (atomicAdd(&s_off[b1], 1u) << 13) | (uint32_t)b1 : 0xffffffffu;
             }
+            // values are not needed until staging: their latency hides behind the scan
             if (has_val) {
 #pragma unroll
                 for (int j = 0; j < kPerThread / 2; j++) {
@@ -314,59 +318,58 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
             for (int j = 0; j < kPerThread / 2; j++) {
                 const int64_t li = 2 * ((int64_t)tid + (int64_t)j * kIngestThreads);
                 const int64_t i = t0 + li;
-                longlong2 k2 = {0, 0}, t2 = {0, 0}, v2 = {0, 0};
+                longlong2 k2 = {0, 0}, t2 = {0, 0};
                 if (li < tn) {
                     k2.x = p.key[i];
                     t2.x = p.ts[i];
-                    if (has_val) v2.x = p.val[i];
                 }
                 if (li + 1 < tn) {
                     k2.y = p.key[i + 1];
                     t2.y = p.ts[i + 1];
-                    if (has_val) v2.y = p.val[i + 1];
                 }
                 rk[2 * j] = k2.x;
-                rv[2 * j] = v2.x;
                 rk[2 * j + 1] = k2.y;
-                rv[2 * j + 1] = v2.y;
                 int64_t q;
                 int b0 = li < tn ? classify(p, k2.x, t2.x, &q) : -3;
                 int b1 = li + 1 < tn ? classify(p, k2.y, t2.y, &q) : -3;
-                if (b0 >= 0) b0 = p.lane_slot[b0 >> p.stage_bits] * P + (b0 & (P - 1));
-                if (b1 >= 0) b1 = p.lane_slot[b1 >> p.stage_bits] * P + (b1 & (P - 1));
+                if (b0 >= 0) b0 = p.lane_slot[b0 >> p.region_bits] * P + (b0 & (P - 1));
+                if (b1 >= 0) b1 = p.lane_slot[b1 >> p.region_bits] * P + (b1 & (P - 1));
                 rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
                 rbr[2 * j + 1] = b1 >= 0 ? (atomicAdd(&s_off[b1], 1u) << 13) | (uint32_t)b1 : 0xffffffffu;
             }
+#pragma unroll
+            for (int j = 0; j < kPerThread; j++) {
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)(j >> 1) * kIngestThreads) + (j & 1);
+                rv[j] = has_val && li < tn ? p.val[t0 + li] : 0;
+            }
         }
-        SSTAMP(0);
         lds_barrier();
-        // 3) exclusive scan of the tile counts in place (s_off[FS] = tile total)
+        // 2) tile offsets (exclusive scan over the slot buckets, s_off[FS] = tile total);
+        //    the cursors advance past this tile's runs
         {
             uint32_t local = 0;
-            for (int q2 = 0; q2 < per_thread_buckets; q2++) {
-                const int b = tid * per_thread_buckets + q2;
+#pragma unroll
+            for (int q = 0; q < bpt; q++) {
+                const int b = tid * bpt + q;
                 if (b < FS) local += s_off[b];
             }
             uint32_t total;
             uint32_t run = block_exclusive_scan_t<true>(local, s_wave, &total);
-            for (int q2 = 0; q2 < per_thread_buckets; q2++) {
-                const int b = tid * per_thread_buckets + q2;
-                if (b < FS) {
-                    const uint32_t c = s_off[b];
-                    s_off[b] = run;
-                    run += c;
-                }
+#pragma unroll
+            for (int q = 0; q < bpt; q++) {   // each thread rewrites only its own buckets
+                const int b = tid * bpt + q;
+                if (b >= FS) break;
+                const uint32_t c = s_off[b];
+                s_off[b] = run;
+                s_cur[b] += c;
+                run += c;
             }
             if (tid == 0) s_off[FS] = total;
         }
         lds_barrier();
-        SSTAMP(1);
         const uint32_t tile_total = s_off[FS];
-        // 4) rounds: stage the slots of one round in bucket order, write the runs
-#pragma unroll
-        for (int round = 0; round < kRounds; round++) {
-            const uint32_t lo = (uint32_t)round * kRound;
-            if (lo >= tile_total) break;
+        // 3) rounds: stage the slots of one round in bucket order, write the runs
+        for (uint32_t lo = 0; lo < tile_total; lo += kRound) {
 #pragma unroll
             for (int j = 0; j < kPerThread; j++) {
                 if (rbr[j] == 0xffffffffu) continue;
@@ -379,36 +382,32 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
             lds_barrier();
             const uint32_t hi = tile_total - lo < (uint32_t)kRound ? tile_total - lo : (uint32_t)kRound;
             for (uint32_t i = tid; i < hi; i += kIngestThreads) {
-                const int b = s_bkt[i];
-                const uint32_t pos = s_cur[b] + (lo + i - s_off[b]);
                 const longlong2 r = s_rec[i];
-                if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = r;
+                const int b = s_bkt[i];   // run of bucket b = [cursor - count, cursor)
+                const int64_t pos = (int64_t)(s_cur[b] - s_off[b + 1] + lo + i);
+                if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * pos) = r;
                 else p.st_rec[pos] = r.x;
             }
-            lds_barrier();
+            if (lo + kRound < tile_total) lds_barrier();
         }
-        SSTAMP(2);
-        if (has_null) {   // rare path: NULL flags go straight to their final position
+        if (has_null) {   // rare path: NULL flags go straight to their staged position
 #pragma unroll
             for (int j = 0; j < kPerThread; j++) {
                 if (rbr[j] == 0xffffffffu) continue;
                 const int b = (int)(rbr[j] & 8191u);
                 const int64_t li = 2 * ((int64_t)tid + (int64_t)(j >> 1) * kIngestThreads) + (j & 1);
-                p.st_null[s_cur[b] + (rbr[j] >> 13)] = p.vnull[t0 + li];
+                p.st_null[s_cur[b] - (s_off[b + 1] - s_off[b]) + (rbr[j] >> 13)] = p.vnull[t0 + li];
             }
         }
+        lds_barrier();   // every write-out has read the offsets
+        // 4) clear the tile counts for the next tile
+#pragma unroll
+        for (int q = 0; q < bpt; q++) {
+            const int b = tid * bpt + q;
+            if (b < FS) s_off[b] = 0;
+        }
         lds_barrier();
-        // 5) advance cursors by the tile counts (next offset - offset), clear counts
-        for (int b = tid; b < FS; b += kIngestThreads) s_cur[b] += s_off[b + 1] - s_off[b];
-        lds_barrier();
-        for (int b = tid; b <= FS; b += kIngestThreads) s_off[b] = 0;
-        lds_barrier();
-        SSTAMP(3);
     }
-#ifdef FG_STAMPS
-    if (tid == 0 && p.stamps)
-        for (int i = 0; i < 4; i++) p.stamps[blockIdx.x * 8 + i] = acc[i];
-#endif
 }
 
 // per bucket: exclusive prefix over workgroups (column of the workgroup-major histogram)
@@ -506,13 +505,20 @@ hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
-    if (p.sorted) hipLaunchKernelGGL(k_ingest_scatter_sorted, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    int nslots = 0;
+    for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
+    const int FS = nslots << p.region_bits;
+    if (p.sorted && FS <= 4 * kIngestThreads)
+        hipLaunchKernelGGL(k_ingest_scatter_sorted<4>, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    else if (p.sorted)
+        hipLaunchKernelGGL(k_ingest_scatter_sorted<kMaxSortedBuckets / kIngestThreads>, dim3(p.grid),
+                           dim3(kIngestThreads), 0, s, p);
     else hipLaunchKernelGGL(k_ingest_scatter_direct, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     return hipGetLastError();
 }
 
 // ----------------------------------------------------------------------------------------
-// merge: one workgroup per state region
+// merge: persistent, one 1024-thread workgroup per CU walking a strided set of regions
 // ----------------------------------------------------------------------------------------
 struct LdsTable {
     int64_t key[kSlots + 1];                  // slot kSlots: the key equal to the sentinel
@@ -549,129 +555,118 @@ __device__ __forceinline__ void lds_add(LdsTable& t, int slot, unsigned long lon
     }
 }
 
-// Region of this workgroup. The 2^drop regions that share one staging bucket run as a
-// team on ONE XCD (blocks b and b + 8 share an XCD under round-robin dispatch), so the
-// bucket they all filter is read from HBM once and re-read from that XCD's L2
-// (placement affects speed only, never results).
-__device__ __forceinline__ int merge_region(int b, int region_bits, int stage_bits) {
-    const int drop = region_bits - stage_bits;
-    if (stage_bits < 3) return b;
-    const int x = b & 7, k = b >> 3;
-    const int j = k & ((1 << drop) - 1), m = k >> drop;
-    return (((m << 3) | x) << drop) | j;
-}
+constexpr int kMergeWaves = kMergeThreads / 64;
+constexpr int kCompRounds = kSlots / kMergeThreads + 1;   // + 1: the sentinel slot (thread 0)
+constexpr int kMergeU = 4;                                // 16-B staged loads per thread per chunk (x2 buffers)
 
 __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     __shared__ LdsTable t;
-    __shared__ uint32_t s_wave[16];
+    __shared__ uint32_t s_grp[kCompRounds * kMergeWaves];   // per (round, wave) row counts -> offsets
     __shared__ unsigned int s_flags;
+    __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
-    const int r = merge_region(blockIdx.x, p.region_bits, p.stage_bits);
-    const int drop = p.region_bits - p.stage_bits;
-#ifdef FG_STAMPS
-#define STAMP(i)                                                                           \
-    do {                                                                                   \
-        __syncthreads();                                                                   \
-        if (threadIdx.x == 0 && p.stamps) p.stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define STAMP(i) \
-    do {         \
-    } while (0)
-#endif
-    STAMP(0);
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
     const int cap = kRegionCap;
     const int vt = p.val_type;
+    const int P = 1 << p.region_bits;
 
-    for (int i = tid; i <= kSlots; i += kMergeThreads) {
-        t.key[i] = JMIN;
-        t.cs[i] = 0;
-        t.cn[i] = 0;
-        t.sum[i] = 0;
-    }
-    if (tid == 0) s_flags = 0;
-    __syncthreads();
-    bool full = false;
-    STAMP(1);
+    for (int r = blockIdx.x; r < P; r += gridDim.x) {
+        for (int i = tid; i < kSlots; i += kMergeThreads) {
+            t.key[i] = JMIN;
+            t.cs[i] = 0;
+            t.cn[i] = 0;
+            t.sum[i] = 0;
+        }
+        if (tid == 0) {
+            t.key[kSlots] = JMIN;
+            t.cs[kSlots] = 0;
+            t.cn[kSlots] = 0;
+            t.sum[kSlots] = 0;
+            s_flags = 0;
+        }
+        lds_barrier();
+        bool full = false;
 
-    // 1) resident slice regions (state) ----------------------------------------------
-    for (int j = 0; j < p.n_src; j++) {
-        const TableRef src = p.src[j];
-        const uint32_t n = src.counts[r];
-        const int64_t* base = src.base + (int64_t)r * 4 * cap;
-        for (uint32_t i0 = 0; i0 < n; i0 += 4 * kMergeThreads) {
-            int64_t k[4], cs[4], cn[4], sm[4];
+        // 1) resident slice regions (state) ------------------------------------------
+        for (int j = 0; j < p.n_src; j++) {
+            const TableRef src = p.src[j];
+            const uint32_t n = src.counts[r];
+            const int64_t* base = src.base + (int64_t)r * 4 * cap;
+            for (uint32_t i0 = 0; i0 < n; i0 += 4 * kMergeThreads) {
+                int64_t k[4], cs[4], cn[4], sm[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {      // issue all loads first (latency hiding)
-                const uint32_t i = i0 + u * kMergeThreads + tid;
-                if (i < n) {
-                    k[u] = base[i];
-                    cs[u] = base[cap + i];
-                    cn[u] = base[2 * cap + i];
-                    sm[u] = base[3 * cap + i];
+                for (int u = 0; u < 4; u++) {      // issue all loads first (latency hiding)
+                    const uint32_t i = i0 + u * kMergeThreads + tid;
+                    if (i < n) {
+                        k[u] = base[i];
+                        cs[u] = base[cap + i];
+                        cn[u] = base[2 * cap + i];
+                        sm[u] = base[3 * cap + i];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t i = i0 + u * kMergeThreads + tid;
+                    if (i >= n) continue;
+                    const int slot = lds_find_or_insert(t, k[u], full);
+                    if (slot >= 0) lds_add(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t i = i0 + u * kMergeThreads + tid;
-                if (i >= n) continue;
-                const int slot = lds_find_or_insert(t, k[u], full);
-                if (slot >= 0) lds_add(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
-            }
         }
-    }
-    STAMP(2);
-    // 2) staged records of bucket (lane, r >> drop) over all staged batches, keeping the
-    //    keys of region r ----------------------------------------------------------------
-    auto in_region = [&](int64_t k) -> bool {
-        return drop == 0 || (int)(fmix64((uint64_t)k) >> (64 - p.region_bits)) == r;
-    };
-    if (p.lane >= 0) {
-        const int b = (p.lane << p.stage_bits) | (r >> drop);
+        // 2) staged records of region r over the lane's staged batches ------------------
         for (int j = 0; j < p.n_batches; j++) {
             const StagedBatch sb = p.batches[j];
-            const uint32_t beg = sb.bucket_off[b], end = sb.bucket_off[b + 1];
+            const uint32_t b0 = sb.bucket_off[0];
+            uint32_t beg = sb.bucket_off[r] - b0;
+            const uint32_t end = sb.bucket_off[r + 1] - b0;
             if (sb.is_acc) {
                 for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    if (!in_region(sb.rec[i])) continue;
                     const int slot = lds_find_or_insert(t, sb.rec[i], full);
                     if (slot >= 0)
                         lds_add(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
                                 sb.val[i], vt);
                 }
+            } else if (sb.stride == 2 && sb.vnull == nullptr && beg < end) {
+                // double-buffered stream: the next chunk's loads are issued before this chunk's
+                // LDS inserts (indices clamped so every chunk issues exactly kMergeU loads)
+                const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
+                longlong2 ca[kMergeU], cb[kMergeU];
+                auto load = [&](longlong2 (&c)[kMergeU], uint32_t i0) {
+#pragma unroll
+                    for (int u = 0; u < kMergeU; u++) {
+                        const uint32_t i = i0 + u * kMergeThreads + tid;
+                        c[u] = rec[i < end ? i : end - 1];
+                    }
+                };
+                auto insert = [&](const longlong2 (&c)[kMergeU], uint32_t i0) {
+#pragma unroll
+                    for (int u = 0; u < kMergeU; u++) {
+                        if (i0 + u * kMergeThreads + tid >= end) continue;
+                        const int slot = lds_find_or_insert(t, c[u].x, full);
+                        if (slot >= 0) lds_add(t, slot, 1ull, 0ull, c[u].y, vt);
+                    }
+                };
+                constexpr uint32_t kChunk = kMergeU * kMergeThreads;
+                load(ca, beg);
+                for (uint32_t i0 = beg; i0 < end; i0 += 2 * kChunk) {
+                    if (i0 + kChunk < end) load(cb, i0 + kChunk);
+                    insert(ca, i0);
+                    if (i0 + kChunk >= end) break;
+                    if (i0 + 2 * kChunk < end) load(ca, i0 + 2 * kChunk);
+                    insert(cb, i0 + kChunk);
+                }
             } else if (sb.stride == 2) {
                 const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
-                if (sb.vnull == nullptr) {
-                    constexpr int kB = 8;
-                    for (uint32_t i0 = beg; i0 < end; i0 += kB * kMergeThreads) {
-                        longlong2 rc[kB];
-#pragma unroll
-                        for (int u = 0; u < kB; u++) {   // kB independent 16-B loads in flight
-                            const uint32_t i = i0 + u * kMergeThreads + tid;
-                            if (i < end) rc[u] = rec[i];
-                        }
-#pragma unroll
-                        for (int u = 0; u < kB; u++) {
-                            const uint32_t i = i0 + u * kMergeThreads + tid;
-                            if (i >= end || !in_region(rc[u].x)) continue;
-                            const int slot = lds_find_or_insert(t, rc[u].x, full);
-                            if (slot >= 0) lds_add(t, slot, 1ull, 0ull, rc[u].y, vt);
-                        }
-                    }
-                } else {
-                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                        const longlong2 rc = rec[i];
-                        if (!in_region(rc.x)) continue;
-                        const int slot = lds_find_or_insert(t, rc.x, full);
-                        if (slot < 0) continue;
-                        const bool isnull = sb.vnull[i] != 0;
-                        lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
-                    }
+                for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                    const longlong2 rc = rec[i];
+                    const int slot = lds_find_or_insert(t, rc.x, full);
+                    if (slot < 0) continue;
+                    const bool isnull = sb.vnull[i] != 0;
+                    lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
                 }
             } else {
                 for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    if (!in_region(sb.rec[i])) continue;
                     const int slot = lds_find_or_insert(t, sb.rec[i], full);
                     if (slot < 0) continue;
                     const bool isnull = sb.vnull != nullptr && sb.vnull[i];
@@ -679,94 +674,113 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
                 }
             }
         }
-    }
-    if (full) atomicOr(&s_flags, 4u);
-    __syncthreads();
-    STAMP(3);
+        if (full) atomicOr(&s_flags, 4u);
+        lds_barrier();
 
-    // 3) compaction: thread tid owns slots [4 tid, 4 tid + 4); tid 0 also owns kSlots --
-    uint32_t mine = 0;
+        // 3) compaction: round k covers slots [k*512, (k+1)*512) (round kCompRounds-1: the
+        //    sentinel slot, thread 0); rows of one (round, wave) are consecutive lanes, so the
+        //    row stores of a wave are contiguous
+        uint64_t occ_mask = 0;   // bit k: this thread's slot of round k is occupied
 #pragma unroll
-    for (int j = 0; j < 4; j++) mine += t.cs[tid * 4 + j] != 0 ? 1u : 0u;
-    if (tid == 0 && t.cs[kSlots] != 0) mine += 1;
-    uint32_t total;
-    uint32_t pos = block_exclusive_scan(mine, s_wave, &total);
-    if (tid == 0) {
-        unsigned int fl = s_flags;
-        if (p.has_dst && total > (uint32_t)cap) fl |= 1u;
-        if (p.emit) {
-            const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
-            s_out_base = ob;
-            if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
+        for (int k = 0; k < kCompRounds; k++) {
+            const int slot = k < kCompRounds - 1 ? k * kMergeThreads + tid : kSlots;
+            const bool occ = (k < kCompRounds - 1 || tid == 0) && t.cs[slot] != 0;
+            const uint64_t bal = __ballot(occ);
+            if (occ) occ_mask |= 1ull << k;
+            if (lane == 0) s_grp[k * kMergeWaves + wave] = (uint32_t)__popcll(bal);
         }
-        s_flags = fl;
-        if (fl) atomicOr(p.overflow, fl);
-    }
-    __syncthreads();
-    const unsigned int fl = s_flags;
-    const bool write_dst = p.has_dst && !(fl & 1u) && !(fl & 4u);
-    const bool write_out = p.emit && !(fl & 2u) && !(fl & 4u);
-    int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
-    const unsigned long long obase = s_out_base;
-
-    auto emit_slot = [&](int slot, uint32_t at) {
-        const int64_t k = slot == kSlots ? JMIN : t.key[slot];
-        const unsigned long long cs = t.cs[slot], cn = t.cn[slot];
-        const int64_t sum = (int64_t)t.sum[slot];
-        if (write_dst) {
-            dbase[at] = k;
-            dbase[cap + at] = (int64_t)cs;
-            dbase[2 * cap + at] = (int64_t)cn;
-            dbase[3 * cap + at] = sum;
-        }
-        if (write_out) {
-            const unsigned long long o = obase + at;
-            p.out_key[o] = k;
-            p.out_ws[o] = p.wstart;
-            p.out_we[o] = p.wend;
-            if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
-            const int64_t cv = (int64_t)(cs - cn);
-            uint8_t nm = 0;
-#pragma unroll
-            for (int a = 0; a < kMaxAggs; a++) {
-                if (a >= p.num_aggs) break;
-                int64_t v = 0;
-                switch (p.aggs[a]) {
-                    case 0: v = (int64_t)cs; break;   // COUNT(*)
-                    case 1: v = cv; break;            // COUNT(v)
-                    case 2:                           // SUM(v): NULL when no non-null value
-                        if (cv == 0) nm |= (uint8_t)(1u << a);
-                        else v = sum;
-                        break;
-                    default:                          // AVG(v): count == 0 ? NULL : sum / count
-                        if (cv == 0) nm |= (uint8_t)(1u << a);
-                        else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
-                        else v = sum / cv;
-                        break;
-                }
-                p.out_agg[a][o] = v;
+        lds_barrier();
+        if (wave == 0) {   // exclusive scan of the kCompRounds * kMergeWaves group counts (<= 128)
+            constexpr int NG = kCompRounds * kMergeWaves;
+            const uint32_t a = 2 * lane < NG ? s_grp[2 * lane] : 0u;
+            const uint32_t b = 2 * lane + 1 < NG ? s_grp[2 * lane + 1] : 0u;
+            uint32_t x = a + b;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= off) x += y;
             }
-            p.out_null[o] = nm;
+            const uint32_t ex = x - a - b;
+            if (2 * lane < NG) s_grp[2 * lane] = ex;
+            if (2 * lane + 1 < NG) s_grp[2 * lane + 1] = ex + a;
+            const uint32_t total = __shfl(x, 63);
+            if (lane == 0) {
+                unsigned int fl = s_flags;
+                if (p.has_dst && total > (uint32_t)cap) fl |= 1u;
+                if (p.emit) {
+                    const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
+                    s_out_base = ob;
+                    if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
+                }
+                s_flags = fl;
+                s_total = total;
+                if (fl) atomicOr(p.overflow, fl);
+            }
         }
-    };
-    uint32_t at = pos;
+        lds_barrier();
+        const unsigned int fl = s_flags;
+        const bool write_dst = p.has_dst && !(fl & 1u) && !(fl & 4u);
+        const bool write_out = p.emit && !(fl & 2u) && !(fl & 4u);
+        int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
+        const unsigned long long obase = s_out_base;
+        // per round: the wave's occupied lanes below this lane give the rank within the group
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int slot = tid * 4 + j;
-        if (t.cs[slot] != 0) emit_slot(slot, at++);
+        for (int k = 0; k < kCompRounds; k++) {
+            const bool occ = (occ_mask >> k) & 1;
+            const uint64_t bal = __ballot(occ);
+            if (!occ) continue;
+            const int slot = k < kCompRounds - 1 ? k * kMergeThreads + tid : kSlots;
+            const uint32_t at = s_grp[k * kMergeWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+            const int64_t key = slot == kSlots ? JMIN : t.key[slot];
+            const unsigned long long cs = t.cs[slot], cn = t.cn[slot];
+            const int64_t sum = (int64_t)t.sum[slot];
+            if (write_dst) {
+                dbase[at] = key;
+                dbase[cap + at] = (int64_t)cs;
+                dbase[2 * cap + at] = (int64_t)cn;
+                dbase[3 * cap + at] = sum;
+            }
+            if (write_out) {
+                const unsigned long long o = obase + at;
+                p.out_key[o] = key;
+                p.out_ws[o] = p.wstart;
+                p.out_we[o] = p.wend;
+                if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
+                const int64_t cv = (int64_t)(cs - cn);
+                uint8_t nm = 0;
+#pragma unroll
+                for (int a = 0; a < kMaxAggs; a++) {
+                    if (a >= p.num_aggs) break;
+                    int64_t v = 0;
+                    switch (p.aggs[a]) {
+                        case 0: v = (int64_t)cs; break;   // COUNT(*)
+                        case 1: v = cv; break;            // COUNT(v)
+                        case 2:                           // SUM(v): NULL when no non-null value
+                            if (cv == 0) nm |= (uint8_t)(1u << a);
+                            else v = sum;
+                            break;
+                        default:                          // AVG(v): count == 0 ? NULL : sum / count
+                            if (cv == 0) nm |= (uint8_t)(1u << a);
+                            else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
+                            else v = sum / cv;
+                            break;
+                    }
+                    p.out_agg[a][o] = v;
+                }
+                p.out_null[o] = nm;
+            }
+        }
+        if (tid == 0 && write_dst) {
+            const uint32_t total = s_total;
+            const uint32_t old = p.dst.counts[r];
+            p.dst.counts[r] = total;
+            if (p.dst_total) atomicAdd(p.dst_total, (unsigned long long)((int64_t)total - (int64_t)old));
+        }
+        lds_barrier();   // the table is cleared for the next region
     }
-    if (tid == 0 && t.cs[kSlots] != 0) emit_slot(kSlots, at++);
-
-    if (tid == 0 && write_dst) {
-        const uint32_t old = p.dst.counts[r];
-        p.dst.counts[r] = total;
-        if (p.dst_total) atomicAdd(p.dst_total, (unsigned long long)((int64_t)total - (int64_t)old));
-    }
-    STAMP(4);
 }
 
-hipError_t launch_merge(const MergeParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_merge, dim3(1u << p.region_bits), dim3(kMergeThreads), 0, s, p);
+hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {
+    hipLaunchKernelGGL(k_merge, dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     return hipGetLastError();
 }
 
