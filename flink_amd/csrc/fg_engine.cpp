@@ -125,9 +125,11 @@ struct Counters {        // host view: per-lane slice index ranges (min > max: l
     long long lane_total[kMaxLanes];
 };
 
-enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE, K_NCLASS };
-const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan", "ingest_scatter", "merge_flush",
-                                           "merge_flush_fire", "merge_fire", "export", "restore"};
+enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_PART1, K_PART2, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE,
+              K_NCLASS };
+const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan",      "ingest_scatter", "ingest_part1",
+                                           "ingest_part2", "merge_flush",      "merge_flush_fire", "merge_fire",
+                                           "export",       "restore"};
 struct KStat {
     int64_t launches = 0;
     double ms = 0;
@@ -167,6 +169,7 @@ struct fg_handle {
 
     // ingest scratch
     DevBuf in_key, in_ts, in_val, in_null;
+    DevBuf part_tmp, part_tmp_null, part_dir;   // two-pass partition: pass-1 tiles + directory
     DevBuf hist, totals, scan_tmp, counters;
     HostBuf h_counters;
 
@@ -766,6 +769,20 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.vec = ((uintptr_t)key % 16 == 0 && (uintptr_t)ts % 16 == 0 && (!val || (uintptr_t)val % 16 == 0)) ? 1 : 0;
     p.hist = h->hist.as<uint32_t>();
     set_fast_path(h, &p);
+    // two-pass partition when the regions split into 64-bucket coarse groups
+    const bool two_pass = h->region_bits >= kFineBits && h->F <= kMaxPart1Fine;
+    if (two_pass) {
+        p.max_tiles = part1_max_tiles(n, p.grid);
+        p.n_coarse = h->F >> kFineBits;
+        HIPCHK(h, h->part_tmp.ensure(16 * (size_t)n));
+        HIPCHK(h, h->part_dir.ensure(2 * (size_t)p.grid * p.max_tiles * (p.n_coarse + 1)));
+        p.tmp = h->part_tmp.as<longlong2>();
+        p.dir = h->part_dir.as<uint16_t>();
+        if (vnull) {
+            HIPCHK(h, h->part_tmp_null.ensure((size_t)n));
+            p.tmp_null = h->part_tmp_null.as<uint8_t>();
+        }
+    }
     DevCounters init{};
     init.qmin = JMAX;
     init.qmax = JMIN;
@@ -777,7 +794,10 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.qmin = &dc->qmin;
     p.qmax = &dc->qmax;
     p.lane_total = dc->lane_total;
-    {
+    if (two_pass) {
+        KTimer kt(h, K_PART1, n);
+        HIPCHK(h, launch_part1(p, h->stream));
+    } else {
         KTimer kt(h, K_COUNT, n);
         HIPCHK(h, launch_ingest_count(p, h->stream));
     }
@@ -873,7 +893,10 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.st_rec = h->st_rec.as<int64_t>();
     p.st_null = vnull ? h->st_null.as<uint8_t>() : nullptr;
     if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
-    {
+    if (two_pass) {
+        KTimer kt(h, K_PART2, n);
+        HIPCHK(h, launch_part2(p, h->stream));
+    } else {
         KTimer kt(h, K_SCATTER, n);
         HIPCHK(h, launch_ingest_scatter(p, h->stream));
     }
@@ -1000,12 +1023,17 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
     int64_t keys = std::max<int64_t>(cfg->expected_keys, 1);
     int bits = 0;
-    while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.7) < keys) bits++;
+    // (a region's keys are binomial around the mean: at 80 % of kRegionCap the largest of
+    // 8,192 regions stays below the cap for uniform keys; skew overflows loudly)
+    while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.8) < keys) bits++;
     h->region_bits = bits;
     h->P = 1 << bits;
     // the staging buckets are the state regions: one region per merge workgroup pass
     h->lanes = kMaxLanes;
+    // lanes x regions bounded by the count histogram and, for the two-pass partition, by
+    // pass 1's LDS histogram
     while (h->lanes > 1 && (h->lanes << h->region_bits) > kMaxStageBuckets) h->lanes >>= 1;
+    while (h->lanes > 2 && h->region_bits >= kFineBits && (h->lanes << h->region_bits) > kMaxPart1Fine) h->lanes >>= 1;
     h->F = h->lanes << h->region_bits;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) {

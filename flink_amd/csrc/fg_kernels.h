@@ -19,6 +19,15 @@ constexpr int kMaxStageBuckets = 32768;       // lanes << region_bits (count / d
 constexpr int kMaxSortedBuckets = 8192;       // lane slots << region_bits (tile-sorted scatter LDS)
 constexpr int kTile = 8192;                   // records per sorted-scatter tile (8 per thread)
 constexpr int kMaxAggs = 8;
+// two-pass partition (regions >= 64): pass 1 sorts tiles by coarse bucket (= fine >> 6)
+// into a tile-private buffer, pass 2 sorts each (coarse bucket, workgroup) unit by fine
+// bucket into the staged areas
+constexpr int kFineBits = 6;                  // fine buckets per coarse bucket = 64
+constexpr int kPart1Tile = 8192;              // pass-1 records per tile (8 per thread)
+constexpr int kMaxPart1Fine = 16384;          // lanes << region_bits for the two-pass path
+constexpr int kMaxCoarse = kMaxPart1Fine >> kFineBits;   // 256
+constexpr int kPart2Threads = 256;
+constexpr int kPart2Tile = 2048;              // pass-2 records per sub-tile (8 per thread)
 
 // One slice table in HBM: P regions, each region an SoA block of kRegionCap entries:
 //   [key i64 x cap][cnt_star i64 x cap][cnt_null i64 x cap][sum (i64 | f64 bits) x cap]
@@ -81,6 +90,12 @@ struct IngestParams {
     int32_t st_stride;
     int32_t pad1;
     uint8_t* st_null;          // NULL flags at the same positions (may be null)
+    // two-pass partition
+    longlong2* tmp;            // pass-1 output: tile (g, j) sorted by coarse bucket at its input offset
+    uint8_t* tmp_null;         // NULL flags of tmp (when vnull)
+    uint16_t* dir;             // [grid * max_tiles][n_coarse + 1] coarse offsets within each tile
+    int32_t max_tiles;         // tiles per workgroup segment (ceil(segment / kPart1Tile))
+    int32_t n_coarse;          // lanes << (region_bits - kFineBits)
 };
 
 struct MergeParams {
@@ -121,6 +136,13 @@ struct ExportParams {
 };
 
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s);
+// two-pass partition: pass 1 does the count pass's work (drops, slice range, lane totals,
+// fine histogram per workgroup) while sorting tiles by coarse bucket into p.tmp / p.dir
+hipError_t launch_part1(const IngestParams& p, hipStream_t s);
+// pass 2: one workgroup per (active coarse bucket, pass-1 workgroup); p.bucket_base, p.hist
+// (column prefixes), p.lane_shift and p.lane_slot as for the scatter
+hipError_t launch_part2(const IngestParams& p, hipStream_t s);
+int32_t part1_max_tiles(int64_t n, int32_t grid);
 hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s);   // picks the variant by p.sorted
 // exclusive scan of n u32 (n < 2^32 total); out has n + 1 entries; tmp >= scan_tmp_words(n)
 size_t scan_tmp_words(int64_t n);

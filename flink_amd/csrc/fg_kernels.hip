@@ -410,6 +410,323 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
     }
 }
 
+// ----------------------------------------------------------------------------------------
+// two-pass partition (regions >= 64). A single tile-sorted pass over 4,096+ buckets writes
+// ~2-record runs; two passes of 64-way sorting write sequential tiles, then 512-B+ runs.
+// ----------------------------------------------------------------------------------------
+// Pass 1: the count pass's bookkeeping (drops, slice range, lane totals, fine histogram per
+// workgroup) plus a tile sort by coarse bucket (fine >> 6) written back to the tile's own
+// input offset in p.tmp (fully sequential stores); p.dir holds each tile's coarse offsets.
+__global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
+    __shared__ uint32_t s_hist[kMaxPart1Fine];       // 64 KiB: fine histogram of this workgroup
+    __shared__ longlong2 s_rec[kRound];              // 64 KiB
+    __shared__ uint8_t s_nul[kRound];                // 4 KiB
+    __shared__ uint32_t s_cc[kMaxCoarse + 1];        // tile coarse counts, then offsets
+    __shared__ uint32_t s_wave[16];
+    __shared__ unsigned long long s_drop;
+    __shared__ long long s_qmin, s_qmax;
+    __shared__ uint32_t s_mask;
+    __shared__ uint32_t s_lane[kMaxLanes];
+    const int F = p.lanes << p.region_bits;
+    const int NC = p.n_coarse;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
+    for (int i = tid; i <= NC; i += kIngestThreads) s_cc[i] = 0;
+    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_mask = 0; }
+    if (tid < kMaxLanes) s_lane[tid] = 0;
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    const bool has_val = p.val != nullptr;
+    const bool has_null = p.vnull != nullptr;
+    uint32_t drops = 0, mask = 0;
+    long long qmin = JMAX, qmax = JMIN;
+    const int lm = p.lanes - 1;
+    constexpr int R = kPart1Tile / kIngestThreads;   // 8
+
+    int j = 0;
+    for (int64_t t0 = beg; t0 < end; t0 += kPart1Tile, j++) {
+        const int64_t tn = end - t0 < kPart1Tile ? end - t0 : kPart1Tile;
+        int64_t rk[R], rv[R];
+        uint32_t rcr[R];   // (rank << 9) | coarse, 0xffffffff = not staged
+        auto account = [&](int64_t k, int64_t ts) -> uint32_t {
+            int64_t q;
+            const int b = classify(p, k, ts, &q);
+            if (b >= 0) {
+                atomicAdd(&s_hist[b], 1u);
+                qmin = q < qmin ? q : qmin;
+                qmax = q > qmax ? q : qmax;
+                mask |= 1u << ((int)q & lm);
+                const uint32_t c = (uint32_t)b >> kFineBits;
+                return (atomicAdd(&s_cc[c], 1u) << 9) | c;
+            }
+            if (b == -1) drops++;
+            return 0xffffffffu;
+        };
+        if (tn == kPart1Tile && p.vec) {
+            longlong2 k2[R / 2], t2[R / 2];
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kIngestThreads);
+                k2[u] = *reinterpret_cast<const longlong2*>(p.key + i);
+                t2[u] = *reinterpret_cast<const longlong2*>(p.ts + i);
+            }
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                rk[2 * u] = k2[u].x;
+                rk[2 * u + 1] = k2[u].y;
+                rcr[2 * u] = account(k2[u].x, t2[u].x);
+                rcr[2 * u + 1] = account(k2[u].y, t2[u].y);
+            }
+            if (has_val) {   // values are not needed until staging: their latency hides behind the scan
+#pragma unroll
+                for (int u = 0; u < R / 2; u++) {
+                    const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kIngestThreads);
+                    const longlong2 v2 = *reinterpret_cast<const longlong2*>(p.val + i);
+                    rv[2 * u] = v2.x;
+                    rv[2 * u + 1] = v2.y;
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < R; u++) rv[u] = 0;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kIngestThreads) + (u & 1);
+                rk[u] = 0;
+                rcr[u] = 0xffffffffu;
+                if (li < tn) {
+                    rk[u] = p.key[t0 + li];
+                    rcr[u] = account(rk[u], p.ts[t0 + li]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kIngestThreads) + (u & 1);
+                rv[u] = has_val && li < tn ? p.val[t0 + li] : 0;
+            }
+        }
+        lds_barrier();
+        {   // exclusive scan of the tile's coarse counts; the offsets go to the directory
+            const uint32_t c = tid < NC ? s_cc[tid] : 0u;
+            uint32_t total;
+            const uint32_t off = block_exclusive_scan_t<true>(c, s_wave, &total);
+            if (tid < NC) s_cc[tid] = off;
+            if (tid == 0) s_cc[NC] = total;
+        }
+        lds_barrier();
+        uint16_t* drow = p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * (NC + 1);
+        for (int c = tid; c <= NC; c += kIngestThreads) drow[c] = (uint16_t)s_cc[c];
+        const uint32_t tile_total = s_cc[NC];
+        for (uint32_t lo = 0; lo < tile_total; lo += kRound) {
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                if (rcr[u] == 0xffffffffu) continue;
+                const uint32_t slot = s_cc[rcr[u] & 511u] + (rcr[u] >> 9);
+                if (slot - lo >= (uint32_t)kRound) continue;
+                s_rec[slot - lo] = make_longlong2(rk[u], rv[u]);
+                if (has_null) {
+                    const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kIngestThreads) + (u & 1);
+                    s_nul[slot - lo] = p.vnull[t0 + li];
+                }
+            }
+            lds_barrier();
+            const uint32_t hi = tile_total - lo < (uint32_t)kRound ? tile_total - lo : (uint32_t)kRound;
+            for (uint32_t i = tid; i < hi; i += kIngestThreads) {
+                p.tmp[t0 + lo + i] = s_rec[i];
+                if (has_null) p.tmp_null[t0 + lo + i] = s_nul[i];
+            }
+            if (lo + kRound < tile_total) lds_barrier();
+        }
+        lds_barrier();   // staging and the directory row have read the offsets
+        for (int c = tid; c <= NC; c += kIngestThreads) s_cc[c] = 0;
+        lds_barrier();
+    }
+    // bookkeeping as in k_ingest_count
+    for (int off = 32; off > 0; off >>= 1) {
+        drops += __shfl_down(drops, off);
+        mask |= __shfl_down(mask, off);
+        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off);
+        qmin = oa < qmin ? oa : qmin;
+        qmax = oz > qmax ? oz : qmax;
+    }
+    if ((tid & 63) == 0) {
+        if (drops) atomicAdd(&s_drop, (unsigned long long)drops);
+        if (mask) atomicOr(&s_mask, mask);
+        if (qmin != JMAX) atomicMin(&s_qmin, qmin);
+        if (qmax != JMIN) atomicMax(&s_qmax, qmax);
+    }
+    __syncthreads();
+    uint32_t lane_part = 0;
+    int lane_of = -1;
+    for (int b = tid; b < F; b += kIngestThreads) {
+        const uint32_t c = s_hist[b];
+        p.hist[(int64_t)blockIdx.x * F + b] = c;
+        const int l = b >> p.region_bits;
+        if (l != lane_of) {
+            if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
+            lane_of = l;
+            lane_part = 0;
+        }
+        lane_part += c;
+    }
+    if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
+    __syncthreads();
+    if (tid < p.lanes && s_lane[tid]) atomicAdd(&p.lane_total[tid], (unsigned long long)s_lane[tid]);
+    if (tid == 0) {
+        if (p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
+        if (s_mask) atomicOr(p.lane_mask, (unsigned long long)s_mask);
+        if (s_qmin != JMAX) atomicMin(p.qmin, s_qmin);
+        if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
+    }
+}
+
+// Pass 2: workgroup (active coarse bucket ca, pass-1 workgroup g) gathers the coarse
+// bucket's fragment of every tile of g, sorts it by fine bucket in sub-tiles of
+// kPart2Tile and writes each fine bucket's run at its staged cursor -- the positions
+// the single-pass scatter would use (bucket-major, workgroup-major within a bucket).
+constexpr int kPart2MaxTiles = 2048;   // pass-1 tiles per workgroup segment held in LDS
+
+__global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p) {
+    constexpr int NF = 1 << kFineBits;
+    constexpr int R = kPart2Tile / kPart2Threads;   // 8
+    __shared__ longlong2 s_rec[kPart2Tile];          // 32 KiB
+    __shared__ uint8_t s_fb[kPart2Tile];
+    __shared__ uint8_t s_nul[kPart2Tile];
+    __shared__ uint32_t s_fstart[kPart2MaxTiles + 1];  // prefix of fragment lengths
+    __shared__ uint32_t s_fsrc[kPart2MaxTiles];        // tmp position of each fragment
+    __shared__ uint32_t s_cnt[NF], s_off[NF + 1], s_cur[NF];
+    const int tid = threadIdx.x;
+    const int P = 1 << p.region_bits;
+    const int F = p.lanes << p.region_bits;
+    const int NC = p.n_coarse;
+    const int cpl = 1 << (p.region_bits - kFineBits);   // coarse buckets per lane
+    const int g = blockIdx.x % p.grid;
+    const int ca = blockIdx.x / p.grid;
+    int lane = 0;
+    {
+        const int sl = ca / cpl;
+        for (int l = 0; l < kMaxLanes; l++)
+            if (p.lane_slot[l] == sl) lane = l;
+    }
+    const int cl = ca % cpl;
+    const int c = lane * cpl + cl;
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, g, &beg, &end);
+    const int ntiles = (int)((end - beg + kPart1Tile - 1) / kPart1Tile);
+    for (int jt = tid; jt < ntiles; jt += kPart2Threads) {
+        const uint16_t* drow = p.dir + ((int64_t)g * p.max_tiles + jt) * (NC + 1);
+        const uint32_t a = drow[c], b = drow[c + 1];
+        s_fstart[jt + 1] = b - a;
+        s_fsrc[jt] = (uint32_t)(beg + (int64_t)jt * kPart1Tile + a);
+    }
+    if (tid < NF) {
+        const int b = lane * P + cl * NF + tid;
+        s_cur[tid] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)g * F + b] + p.lane_shift[lane]);
+        s_cnt[tid] = 0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        s_fstart[0] = 0;
+        for (int jt = 0; jt < ntiles; jt++) {
+            run += s_fstart[jt + 1];
+            s_fstart[jt + 1] = run;
+        }
+    }
+    __syncthreads();
+    const uint32_t total = s_fstart[ntiles];
+    const bool has_null = p.vnull != nullptr;
+    const bool aos = p.st_stride == 2;
+    for (uint32_t base = 0; base < total; base += kPart2Tile) {
+        longlong2 rr[R];
+        uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
+        uint8_t rn[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const uint32_t idx = base + (uint32_t)(u * kPart2Threads + tid);
+            rf[u] = 0xffffffffu;
+            rn[u] = 0;
+            if (idx >= total) continue;
+            int lo = 0, hi = ntiles;   // fragment: last fs with s_fstart[fs] <= idx
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_fstart[mid] <= idx) lo = mid;
+                else hi = mid;
+            }
+            const uint32_t src = s_fsrc[lo] + (idx - s_fstart[lo]);
+            rr[u] = p.tmp[src];
+            if (has_null) rn[u] = p.tmp_null[src];
+        }
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if (base + (uint32_t)(u * kPart2Threads + tid) >= total) continue;
+            const uint32_t f = (uint32_t)(fmix64((uint64_t)rr[u].x) >> (64 - p.region_bits)) & (NF - 1);
+            rf[u] = (atomicAdd(&s_cnt[f], 1u) << 6) | f;
+        }
+        __syncthreads();
+        if (tid < 64) {   // one wave: exclusive scan of the 64 fine counts
+            const uint32_t v = s_cnt[tid];
+            uint32_t x = v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (tid >= off) x += y;
+            }
+            s_off[tid] = x - v;
+            if (tid == 63) s_off[NF] = x;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if (rf[u] == 0xffffffffu) continue;
+            const uint32_t slot = s_off[rf[u] & (NF - 1)] + (rf[u] >> 6);
+            s_rec[slot] = rr[u];
+            s_fb[slot] = (uint8_t)(rf[u] & (NF - 1));
+            if (has_null) s_nul[slot] = rn[u];
+        }
+        __syncthreads();
+        const uint32_t sub = s_off[NF];
+        for (uint32_t i = tid; i < sub; i += kPart2Threads) {
+            const int f = s_fb[i];
+            const int64_t pos = (int64_t)(s_cur[f] + (i - s_off[f]));
+            const longlong2 r = s_rec[i];
+            if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * pos) = r;
+            else p.st_rec[pos] = r.x;
+            if (has_null) p.st_null[pos] = s_nul[i];
+        }
+        __syncthreads();
+        if (tid < NF) {
+            s_cur[tid] += s_cnt[tid];
+            s_cnt[tid] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+int32_t part1_max_tiles(int64_t n, int32_t grid) {
+    int64_t per = (n + grid - 1) / grid;
+    per = (per + 1) & ~int64_t(1);
+    return (int32_t)((per + kPart1Tile - 1) / kPart1Tile);
+}
+
+hipError_t launch_part1(const IngestParams& p, hipStream_t s) {
+    if (p.n_coarse < 1 || p.n_coarse > kMaxCoarse || (p.lanes << p.region_bits) > kMaxPart1Fine ||
+        p.region_bits < kFineBits || p.max_tiles > kPart2MaxTiles)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_part1, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
+    int nslots = 0;
+    for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
+    const int64_t units = (int64_t)nslots * (1 << (p.region_bits - kFineBits)) * p.grid;
+    if (units == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_part2, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p);
+    return hipGetLastError();
+}
+
 // per bucket: exclusive prefix over workgroups (column of the workgroup-major histogram)
 __global__ __launch_bounds__(256) void k_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid) {
     const int b = blockIdx.x * 256 + threadIdx.x;
