@@ -461,8 +461,11 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
             rc = arena_put(h, &tr, 1, &d_src);
             if (rc) return rc;
         }
+        bool plain = h->st_stride == 2 && !sb.empty() && sb.size() <= (size_t)kMaxMergeBatches;
+        for (Staged* s : ln.passes) plain = plain && !s->has_null;
         MergeParams p{};
         p.region_bits = h->region_bits;
+        p.fast_stream = plain ? 1 : 0;
         p.n_src = t->upper > 0 ? 1 : 0;
         p.src = d_src;
         p.n_batches = (int)sb.size();
@@ -1023,9 +1026,9 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
     int64_t keys = std::max<int64_t>(cfg->expected_keys, 1);
     int bits = 0;
-    // (a region's keys are binomial around the mean: at 80 % of kRegionCap the largest of
-    // 8,192 regions stays below the cap for uniform keys; skew overflows loudly)
-    while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kRegionCap * 0.8) < keys) bits++;
+    // Keys per region ~35 % of the kSlots LDS slots: linear probes stay short (a wave's
+    // probe loop runs at its lanes' probe counts); up to 2^13 regions, then denser.
+    while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kSlots * 0.35) < keys) bits++;
     h->region_bits = bits;
     h->P = 1 << bits;
     // the staging buckets are the state regions: one region per merge workgroup pass

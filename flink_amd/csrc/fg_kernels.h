@@ -98,8 +98,11 @@ struct IngestParams {
     int32_t n_coarse;          // lanes << (region_bits - kFineBits)
 };
 
+constexpr int kMaxMergeBatches = 32;         // pipelined merge: staged batches held in LDS
+
 struct MergeParams {
     int32_t region_bits;       // log2(P): state regions
+    int32_t fast_stream;       // every batch plain AoS {key, value}, n_batches <= kMaxMergeBatches
     int32_t n_src;
     const TableRef* src;       // device array [n_src]
     int32_t n_batches;

@@ -844,9 +844,15 @@ struct LdsTable {
     unsigned long long sum[kSlots + 1];       // SUM / AVG sum (i64, or f64 bits)
 };
 
+// home slot: a multiplicative hash of the key (the region already selects keys by the top
+// bits of fmix64, independent of these bits)
+__device__ __forceinline__ uint32_t lds_home(int64_t k) {
+    return (uint32_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> (64 - kSlotBits));
+}
+
 __device__ __forceinline__ int lds_find_or_insert(LdsTable& t, int64_t k, bool& full) {
     if (k == JMIN) return kSlots;
-    uint32_t slot = (uint32_t)fmix64((uint64_t)k) & (kSlots - 1);
+    uint32_t slot = lds_home(k);
     for (int probe = 0; probe < kSlots; probe++) {
         const int64_t cur = t.key[slot];
         if (cur == k) return (int)slot;
@@ -875,6 +881,20 @@ __device__ __forceinline__ void lds_add(LdsTable& t, int slot, unsigned long lon
 constexpr int kMergeWaves = kMergeThreads / 64;
 constexpr int kCompRounds = kSlots / kMergeThreads + 1;   // + 1: the sentinel slot (thread 0)
 constexpr int kMergeU = 4;                                // 16-B staged loads per thread per chunk (x2 buffers)
+constexpr uint32_t kChunk = kMergeU * kMergeThreads;
+
+// Pipelined staged stream (every batch plain {key, value} AoS, <= kMaxMergeBatches): the
+// workgroup walks its regions r0, r0 + G, ... as one stream of chunks (chunks never span
+// batches). Region ranges are loaded two regions ahead into LDS, and the chunk after a
+// region's last one -- the next region's first -- is loaded while that region is
+// inserted, compacted and emitted, so no region starts on a cold load.
+struct MergeCursor {
+    int ri;          // region ordinal of this workgroup (region = blockIdx.x + ri * gridDim.x)
+    int j;           // batch
+    uint32_t i0;     // first record of the chunk (batch-relative)
+    uint32_t end;    // end of region ri in batch j
+    bool ok;         // settled on a chunk (false: walked past the regions whose ranges are known)
+};
 
 __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     __shared__ LdsTable t;
@@ -882,13 +902,79 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
     __shared__ unsigned int s_flags;
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
+    __shared__ const longlong2* s_brec[kMaxMergeBatches];     // fast path: batch record bases
+    __shared__ uint32_t s_rng[3][kMaxMergeBatches][2];         // fast path: [ri % 3][batch] = (beg, end)
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int cap = kRegionCap;
     const int vt = p.val_type;
     const int P = 1 << p.region_bits;
+    const int G = gridDim.x;
+    const int nreg = ((int)blockIdx.x < P) ? (P - 1 - (int)blockIdx.x) / G + 1 : 0;
+    const bool fast = p.fast_stream != 0;
+    const int nb = p.n_batches;
 
-    for (int r = blockIdx.x; r < P; r += gridDim.x) {
+    // fast path state
+    auto range_of = [&](int ri, int j, uint32_t& beg, uint32_t& end) {
+        const int r = (int)blockIdx.x + ri * G;
+        const uint32_t* bo = p.batches[j].bucket_off;
+        const uint32_t b0 = bo[0];
+        beg = bo[r] - b0;
+        end = bo[r + 1] - b0;
+    };
+    // first non-empty chunk at or after (ri, j, i0) within regions <= maxri (whose ranges
+    // are in LDS); ri == nreg: stream exhausted
+    auto settle = [&](MergeCursor& c, int maxri) {
+        c.ok = false;
+        while (c.ri < nreg && c.ri <= maxri) {
+            const uint32_t* rg = s_rng[c.ri % 3][c.j];
+            if (c.i0 < rg[1]) {
+                c.end = rg[1];
+                c.ok = true;
+                return;
+            }
+            if (++c.j >= nb) {
+                c.j = 0;
+                if (++c.ri > maxri || c.ri >= nreg) return;   // i0 is set when re-settled
+            }
+            c.i0 = s_rng[c.ri % 3][c.j][0];
+        }
+    };
+    longlong2 ca[kMergeU], cb[kMergeU];
+    auto load = [&](longlong2 (&c)[kMergeU], const MergeCursor& m) {
+        const longlong2* rec = s_brec[m.j];
+#pragma unroll
+        for (int u = 0; u < kMergeU; u++) {
+            const uint32_t i = m.i0 + u * kMergeThreads + tid;
+            c[u] = rec[i < m.end ? i : m.end - 1];
+        }
+    };
+    auto insert = [&](const longlong2 (&c)[kMergeU], const MergeCursor& m, bool& full) {
+#pragma unroll
+        for (int u = 0; u < kMergeU; u++) {
+            if (m.i0 + u * kMergeThreads + tid >= m.end) continue;
+            const int slot = lds_find_or_insert(t, c[u].x, full);
+            if (slot >= 0) lds_add(t, slot, 1ull, 0ull, c[u].y, vt);
+        }
+    };
+    MergeCursor cur{nreg, 0, 0, 0};
+    if (fast) {
+        if (tid < nb) s_brec[tid] = reinterpret_cast<const longlong2*>(p.batches[tid].rec);
+        for (int q = tid; q < 2 * nb; q += kMergeThreads) {   // ranges of regions 0 and 1
+            const int ri = q / nb, j = q % nb;
+            uint32_t beg = 0, end = 0;
+            if (ri < nreg) range_of(ri, j, beg, end);
+            s_rng[ri][j][0] = beg;
+            s_rng[ri][j][1] = end;
+        }
+        __syncthreads();
+        cur = MergeCursor{0, 0, s_rng[0][0][0], 0, false};
+        settle(cur, 1);
+        if (cur.ok) load(ca, cur);
+    }
+
+    for (int ri = 0; ri < nreg; ri++) {
+        const int r = (int)blockIdx.x + ri * G;
         for (int i = tid; i < kSlots; i += kMergeThreads) {
             t.key[i] = JMIN;
             t.cs[i] = 0;
@@ -902,6 +988,9 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
             t.sum[kSlots] = 0;
             s_flags = 0;
         }
+        // fast path: ranges of region ri + 2 (written to LDS after this region's inserts)
+        uint32_t nbeg = 0, nend = 0;
+        if (fast && tid < nb && ri + 2 < nreg) range_of(ri + 2, tid, nbeg, nend);
         lds_barrier();
         bool full = false;
 
@@ -932,69 +1021,74 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
             }
         }
         // 2) staged records of region r over the lane's staged batches ------------------
-        for (int j = 0; j < p.n_batches; j++) {
-            const StagedBatch sb = p.batches[j];
-            const uint32_t b0 = sb.bucket_off[0];
-            uint32_t beg = sb.bucket_off[r] - b0;
-            const uint32_t end = sb.bucket_off[r + 1] - b0;
-            if (sb.is_acc) {
-                for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    const int slot = lds_find_or_insert(t, sb.rec[i], full);
-                    if (slot >= 0)
-                        lds_add(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
-                                sb.val[i], vt);
+        if (fast) {
+            // double-buffered: the next chunk's loads are issued before this chunk's inserts;
+            // the chunk in flight at the region's end is the next region's first
+            if (cur.ri == ri && !cur.ok) {   // walked past empty regions: settle now (cold load)
+                cur.j = 0;
+                cur.i0 = s_rng[ri % 3][0][0];
+                settle(cur, ri + 1);
+                if (cur.ok && cur.ri == ri) load(ca, cur);
+            }
+            bool in_a = true;
+            while (cur.ri == ri && cur.ok) {
+                MergeCursor nx = cur;
+                nx.i0 += kChunk;
+                settle(nx, ri + 1);
+                if (in_a) {
+                    if (nx.ok) load(cb, nx);
+                    insert(ca, cur, full);
+                } else {
+                    if (nx.ok) load(ca, nx);
+                    insert(cb, cur, full);
                 }
-            } else if (sb.stride == 2 && sb.vnull == nullptr && beg < end) {
-                // double-buffered stream: the next chunk's loads are issued before this chunk's
-                // LDS inserts (indices clamped so every chunk issues exactly kMergeU loads)
-                const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
-                longlong2 ca[kMergeU], cb[kMergeU];
-                auto load = [&](longlong2 (&c)[kMergeU], uint32_t i0) {
+                in_a = !in_a;
+                cur = nx;
+            }
+            if (!in_a) {   // the next region's first chunk sits in cb
 #pragma unroll
-                    for (int u = 0; u < kMergeU; u++) {
-                        const uint32_t i = i0 + u * kMergeThreads + tid;
-                        c[u] = rec[i < end ? i : end - 1];
+                for (int u = 0; u < kMergeU; u++) ca[u] = cb[u];
+            }
+        } else {
+            for (int j = 0; j < nb; j++) {
+                const StagedBatch sb = p.batches[j];
+                const uint32_t b0 = sb.bucket_off[0];
+                const uint32_t beg = sb.bucket_off[r] - b0;
+                const uint32_t end = sb.bucket_off[r + 1] - b0;
+                if (sb.is_acc) {
+                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                        const int slot = lds_find_or_insert(t, sb.rec[i], full);
+                        if (slot >= 0)
+                            lds_add(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
+                                    sb.val[i], vt);
                     }
-                };
-                auto insert = [&](const longlong2 (&c)[kMergeU], uint32_t i0) {
-#pragma unroll
-                    for (int u = 0; u < kMergeU; u++) {
-                        if (i0 + u * kMergeThreads + tid >= end) continue;
-                        const int slot = lds_find_or_insert(t, c[u].x, full);
-                        if (slot >= 0) lds_add(t, slot, 1ull, 0ull, c[u].y, vt);
+                } else if (sb.stride == 2) {
+                    const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
+                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                        const longlong2 rc = rec[i];
+                        const int slot = lds_find_or_insert(t, rc.x, full);
+                        if (slot < 0) continue;
+                        const bool isnull = sb.vnull != nullptr && sb.vnull[i] != 0;
+                        lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
                     }
-                };
-                constexpr uint32_t kChunk = kMergeU * kMergeThreads;
-                load(ca, beg);
-                for (uint32_t i0 = beg; i0 < end; i0 += 2 * kChunk) {
-                    if (i0 + kChunk < end) load(cb, i0 + kChunk);
-                    insert(ca, i0);
-                    if (i0 + kChunk >= end) break;
-                    if (i0 + 2 * kChunk < end) load(ca, i0 + 2 * kChunk);
-                    insert(cb, i0 + kChunk);
-                }
-            } else if (sb.stride == 2) {
-                const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
-                for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    const longlong2 rc = rec[i];
-                    const int slot = lds_find_or_insert(t, rc.x, full);
-                    if (slot < 0) continue;
-                    const bool isnull = sb.vnull[i] != 0;
-                    lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
-                }
-            } else {
-                for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                    const int slot = lds_find_or_insert(t, sb.rec[i], full);
-                    if (slot < 0) continue;
-                    const bool isnull = sb.vnull != nullptr && sb.vnull[i];
-                    lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
+                } else {
+                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                        const int slot = lds_find_or_insert(t, sb.rec[i], full);
+                        if (slot < 0) continue;
+                        const bool isnull = sb.vnull != nullptr && sb.vnull[i];
+                        lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
+                    }
                 }
             }
         }
         if (full) atomicOr(&s_flags, 4u);
+        if (fast && tid < nb && ri + 2 < nreg) {
+            s_rng[(ri + 2) % 3][tid][0] = nbeg;
+            s_rng[(ri + 2) % 3][tid][1] = nend;
+        }
         lds_barrier();
 
-        // 3) compaction: round k covers slots [k*512, (k+1)*512) (round kCompRounds-1: the
+        // 3) compaction: round k covers slots [k*T, (k+1)*T) (round kCompRounds-1: the
         //    sentinel slot, thread 0); rows of one (round, wave) are consecutive lanes, so the
         //    row stores of a wave are contiguous
         uint64_t occ_mask = 0;   // bit k: this thread's slot of round k is occupied
