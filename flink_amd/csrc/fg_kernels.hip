@@ -582,28 +582,41 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
     }
 }
 
-// Pass 2: workgroup (active coarse bucket ca, pass-1 workgroup g) gathers the coarse
-// bucket's fragment of every tile of g, sorts it by fine bucket in sub-tiles of
-// kPart2Tile and writes each fine bucket's run at its staged cursor -- the positions
-// the single-pass scatter would use (bucket-major, workgroup-major within a bucket).
-constexpr int kPart2MaxTiles = 2048;   // pass-1 tiles per workgroup segment held in LDS
+// Pass 2: workgroup (active coarse bucket ca, group of K consecutive pass-1 workgroups
+// [g0, g0 + K)) gathers the coarse bucket's fragment of every tile of the group, sorts it by
+// fine bucket in sub-tiles of kPart2Tile and writes each fine bucket's run at its cursor.
+// Within a bucket the staged layout is workgroup-major, so the K workgroups' records of
+// bucket b own the one contiguous range starting at the column prefix of g0 (their order
+// inside it is immaterial): one cursor per fine bucket serves the whole group.
+constexpr int kPart2MaxFrags = 1024;   // fragments (group tiles) per unit held in LDS
 
-__global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p) {
+int32_t part2_group(int32_t max_tiles) {
+    int32_t k = kPart2MaxFrags / (max_tiles > 0 ? max_tiles : 1);
+    return k < 1 ? 1 : (k > 8 ? 8 : k);
+}
+
+__global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t group) {
     constexpr int NF = 1 << kFineBits;
     constexpr int R = kPart2Tile / kPart2Threads;   // 8
+    constexpr int FPT = kPart2MaxFrags / kPart2Threads;   // 4 fragments per thread
     __shared__ longlong2 s_rec[kPart2Tile];          // 32 KiB
     __shared__ uint8_t s_fb[kPart2Tile];
     __shared__ uint8_t s_nul[kPart2Tile];
-    __shared__ uint32_t s_fstart[kPart2MaxTiles + 1];  // prefix of fragment lengths
-    __shared__ uint32_t s_fsrc[kPart2MaxTiles];        // tmp position of each fragment
+    __shared__ uint32_t s_fstart[kPart2MaxFrags + 1];  // prefix of fragment lengths
+    __shared__ uint32_t s_fsrc[kPart2MaxFrags];        // tmp position of each fragment
     __shared__ uint32_t s_cnt[NF], s_off[NF + 1], s_cur[NF];
+    __shared__ uint32_t s_wave[kPart2Threads / 64];
     const int tid = threadIdx.x;
     const int P = 1 << p.region_bits;
     const int F = p.lanes << p.region_bits;
     const int NC = p.n_coarse;
+    const int MT = p.max_tiles;
     const int cpl = 1 << (p.region_bits - kFineBits);   // coarse buckets per lane
-    const int g = blockIdx.x % p.grid;
-    const int ca = blockIdx.x / p.grid;
+    const int ngroups = (p.grid + group - 1) / group;
+    const int gi = blockIdx.x % ngroups;
+    const int ca = blockIdx.x / ngroups;
+    const int g0 = gi * group;
+    const int g1 = g0 + group < p.grid ? g0 + group : p.grid;
     int lane = 0;
     {
         const int sl = ca / cpl;
@@ -612,31 +625,39 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p) {
     }
     const int cl = ca % cpl;
     const int c = lane * cpl + cl;
-    int64_t beg, end;
-    seg_bounds(p.n, p.grid, g, &beg, &end);
-    const int ntiles = (int)((end - beg + kPart1Tile - 1) / kPart1Tile);
-    for (int jt = tid; jt < ntiles; jt += kPart2Threads) {
-        const uint16_t* drow = p.dir + ((int64_t)g * p.max_tiles + jt) * (NC + 1);
+    // fragment q = (workgroup g0 + q / MT, tile q % MT); missing tiles are empty fragments
+    const int nfr = (g1 - g0) * MT;
+    uint32_t len[FPT];
+    uint32_t local = 0;
+#pragma unroll
+    for (int k = 0; k < FPT; k++) {
+        const int q = tid * FPT + k;
+        len[k] = 0;
+        if (q >= nfr) continue;
+        const int g = g0 + q / MT, jt = q % MT;
+        int64_t beg, end;
+        seg_bounds(p.n, p.grid, g, &beg, &end);
+        if (beg + (int64_t)jt * kPart1Tile >= end) continue;
+        const uint16_t* drow = p.dir + ((int64_t)g * MT + jt) * (NC + 1);
         const uint32_t a = drow[c], b = drow[c + 1];
-        s_fstart[jt + 1] = b - a;
-        s_fsrc[jt] = (uint32_t)(beg + (int64_t)jt * kPart1Tile + a);
+        len[k] = b - a;
+        s_fsrc[q] = (uint32_t)(beg + (int64_t)jt * kPart1Tile + a);
+        local += len[k];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan(local, s_wave, &total);
+#pragma unroll
+    for (int k = 0; k < FPT; k++) {
+        const int q = tid * FPT + k;
+        if (q < nfr) s_fstart[q] = run;
+        run += len[k];
     }
     if (tid < NF) {
         const int b = lane * P + cl * NF + tid;
-        s_cur[tid] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)g * F + b] + p.lane_shift[lane]);
+        s_cur[tid] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)g0 * F + b] + p.lane_shift[lane]);
         s_cnt[tid] = 0;
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t run = 0;
-        s_fstart[0] = 0;
-        for (int jt = 0; jt < ntiles; jt++) {
-            run += s_fstart[jt + 1];
-            s_fstart[jt + 1] = run;
-        }
-    }
-    __syncthreads();
-    const uint32_t total = s_fstart[ntiles];
     const bool has_null = p.vnull != nullptr;
     const bool aos = p.st_stride == 2;
     for (uint32_t base = 0; base < total; base += kPart2Tile) {
@@ -646,10 +667,9 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p) {
 #pragma unroll
         for (int u = 0; u < R; u++) {
             const uint32_t idx = base + (uint32_t)(u * kPart2Threads + tid);
-            rf[u] = 0xffffffffu;
             rn[u] = 0;
             if (idx >= total) continue;
-            int lo = 0, hi = ntiles;   // fragment: last fs with s_fstart[fs] <= idx
+            int lo = 0, hi = nfr;   // fragment: last q with s_fstart[q] <= idx (never an empty one)
             while (hi - lo > 1) {
                 const int mid = (lo + hi) >> 1;
                 if (s_fstart[mid] <= idx) lo = mid;
@@ -661,6 +681,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p) {
         }
 #pragma unroll
         for (int u = 0; u < R; u++) {
+            rf[u] = 0xffffffffu;
             if (base + (uint32_t)(u * kPart2Threads + tid) >= total) continue;
             const uint32_t f = (uint32_t)(fmix64((uint64_t)rr[u].x) >> (64 - p.region_bits)) & (NF - 1);
             rf[u] = (atomicAdd(&s_cnt[f], 1u) << 6) | f;
@@ -712,7 +733,7 @@ int32_t part1_max_tiles(int64_t n, int32_t grid) {
 
 hipError_t launch_part1(const IngestParams& p, hipStream_t s) {
     if (p.n_coarse < 1 || p.n_coarse > kMaxCoarse || (p.lanes << p.region_bits) > kMaxPart1Fine ||
-        p.region_bits < kFineBits || p.max_tiles > kPart2MaxTiles)
+        p.region_bits < kFineBits || p.max_tiles > kPart2MaxFrags)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_part1, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     return hipGetLastError();
@@ -721,9 +742,10 @@ hipError_t launch_part1(const IngestParams& p, hipStream_t s) {
 hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
     int nslots = 0;
     for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
-    const int64_t units = (int64_t)nslots * (1 << (p.region_bits - kFineBits)) * p.grid;
+    const int32_t group = part2_group(p.max_tiles);
+    const int64_t units = (int64_t)nslots * (1 << (p.region_bits - kFineBits)) * ((p.grid + group - 1) / group);
     if (units == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_part2, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p);
+    hipLaunchKernelGGL(k_part2, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
     return hipGetLastError();
 }
 
