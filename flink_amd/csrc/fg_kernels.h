@@ -23,7 +23,8 @@ constexpr int kMaxAggs = 8;
 // into a tile-private buffer, pass 2 sorts each (coarse bucket, workgroup) unit by fine
 // bucket into the staged areas
 constexpr int kFineBits = 6;                  // fine buckets per coarse bucket = 64
-constexpr int kPart1Tile = 8192;              // pass-1 records per tile (8 per thread)
+constexpr int kPart1Threads = 768;            // 12 waves: 168 VGPRs per lane, room for a prefetched tile
+constexpr int kPart1Tile = 8 * kPart1Threads;  // pass-1 records per tile (8 per thread)
 constexpr int kMaxPart1Fine = 16384;          // lanes << region_bits for the two-pass path
 constexpr int kMaxCoarse = kMaxPart1Fine >> kFineBits;   // 256
 constexpr int kPart2Threads = 256;

@@ -417,12 +417,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
 // Pass 1: the count pass's bookkeeping (drops, slice range, lane totals, fine histogram per
 // workgroup) plus a tile sort by coarse bucket (fine >> 6) written back to the tile's own
 // input offset in p.tmp (fully sequential stores); p.dir holds each tile's coarse offsets.
-__global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
+__global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     __shared__ uint32_t s_hist[kMaxPart1Fine];       // 64 KiB: fine histogram of this workgroup
     __shared__ longlong2 s_rec[kRound];              // 64 KiB
     __shared__ uint8_t s_nul[kRound];                // 4 KiB
     __shared__ uint32_t s_cc[kMaxCoarse + 1];        // tile coarse counts, then offsets
-    __shared__ uint32_t s_wave[16];
+    __shared__ uint32_t s_wave[kPart1Threads / 64];
     __shared__ unsigned long long s_drop;
     __shared__ long long s_qmin, s_qmax;
     __shared__ uint32_t s_mask;
@@ -430,8 +430,8 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
     const int F = p.lanes << p.region_bits;
     const int NC = p.n_coarse;
     const int tid = threadIdx.x;
-    for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
-    for (int i = tid; i <= NC; i += kIngestThreads) s_cc[i] = 0;
+    for (int i = tid; i < F; i += kPart1Threads) s_hist[i] = 0;
+    for (int i = tid; i <= NC; i += kPart1Threads) s_cc[i] = 0;
     if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_mask = 0; }
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
     uint32_t drops = 0, mask = 0;
     long long qmin = JMAX, qmax = JMIN;
     const int lm = p.lanes - 1;
-    constexpr int R = kPart1Tile / kIngestThreads;   // 8
+    constexpr int R = kPart1Tile / kPart1Threads;   // 8
 
     int j = 0;
     for (int64_t t0 = beg; t0 < end; t0 += kPart1Tile, j++) {
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
             longlong2 k2[R / 2], t2[R / 2];
 #pragma unroll
             for (int u = 0; u < R / 2; u++) {
-                const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kIngestThreads);
+                const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kPart1Threads);
                 k2[u] = *reinterpret_cast<const longlong2*>(p.key + i);
                 t2[u] = *reinterpret_cast<const longlong2*>(p.ts + i);
             }
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
             if (has_val) {   // values are not needed until staging: their latency hides behind the scan
 #pragma unroll
                 for (int u = 0; u < R / 2; u++) {
-                    const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kIngestThreads);
+                    const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kPart1Threads);
                     const longlong2 v2 = *reinterpret_cast<const longlong2*>(p.val + i);
                     rv[2 * u] = v2.x;
                     rv[2 * u + 1] = v2.y;
@@ -493,7 +493,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
         } else {
 #pragma unroll
             for (int u = 0; u < R; u++) {
-                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kIngestThreads) + (u & 1);
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kPart1Threads) + (u & 1);
                 rk[u] = 0;
                 rcr[u] = 0xffffffffu;
                 if (li < tn) {
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
             }
 #pragma unroll
             for (int u = 0; u < R; u++) {
-                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kIngestThreads) + (u & 1);
+                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kPart1Threads) + (u & 1);
                 rv[u] = has_val && li < tn ? p.val[t0 + li] : 0;
             }
         }
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
         }
         lds_barrier();
         uint16_t* drow = p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * (NC + 1);
-        for (int c = tid; c <= NC; c += kIngestThreads) drow[c] = (uint16_t)s_cc[c];
+        for (int c = tid; c <= NC; c += kPart1Threads) drow[c] = (uint16_t)s_cc[c];
         const uint32_t tile_total = s_cc[NC];
         for (uint32_t lo = 0; lo < tile_total; lo += kRound) {
 #pragma unroll
@@ -527,20 +527,20 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
                 if (slot - lo >= (uint32_t)kRound) continue;
                 s_rec[slot - lo] = make_longlong2(rk[u], rv[u]);
                 if (has_null) {
-                    const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kIngestThreads) + (u & 1);
+                    const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kPart1Threads) + (u & 1);
                     s_nul[slot - lo] = p.vnull[t0 + li];
                 }
             }
             lds_barrier();
             const uint32_t hi = tile_total - lo < (uint32_t)kRound ? tile_total - lo : (uint32_t)kRound;
-            for (uint32_t i = tid; i < hi; i += kIngestThreads) {
+            for (uint32_t i = tid; i < hi; i += kPart1Threads) {
                 p.tmp[t0 + lo + i] = s_rec[i];
                 if (has_null) p.tmp_null[t0 + lo + i] = s_nul[i];
             }
             if (lo + kRound < tile_total) lds_barrier();
         }
         lds_barrier();   // staging and the directory row have read the offsets
-        for (int c = tid; c <= NC; c += kIngestThreads) s_cc[c] = 0;
+        for (int c = tid; c <= NC; c += kPart1Threads) s_cc[c] = 0;
         lds_barrier();
     }
     // bookkeeping as in k_ingest_count
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_part1(IngestParams p) {
     __syncthreads();
     uint32_t lane_part = 0;
     int lane_of = -1;
-    for (int b = tid; b < F; b += kIngestThreads) {
+    for (int b = tid; b < F; b += kPart1Threads) {
         const uint32_t c = s_hist[b];
         p.hist[(int64_t)blockIdx.x * F + b] = c;
         const int l = b >> p.region_bits;
@@ -735,7 +735,7 @@ hipError_t launch_part1(const IngestParams& p, hipStream_t s) {
     if (p.n_coarse < 1 || p.n_coarse > kMaxCoarse || (p.lanes << p.region_bits) > kMaxPart1Fine ||
         p.region_bits < kFineBits || p.max_tiles > kPart2MaxFrags)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_part1, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    hipLaunchKernelGGL(k_part1, dim3(p.grid), dim3(kPart1Threads), 0, s, p);
     return hipGetLastError();
 }
 

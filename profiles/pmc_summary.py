@@ -1,8 +1,28 @@
-"""Summarize rocprofv3 --pmc CSVs: mean counter value per dispatch for each fg:: kernel."""
+"""Summarize rocprofv3 --pmc CSVs: mean counter value per dispatch for each fg:: kernel.
+
+usage: python profiles/pmc_summary.py "<glob of run_counter_collection.csv>" [out.json]
+
+With an output path, also writes the per-launch HBM traffic of each engine kernel class
+(the `roofline.traffic` field bench.py reports), corrected as MI355X_MICROARCH.md's
+HBM/rocprofv3 section prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced streaming reads, which is
+how every engine kernel reads, so it is doubled; WRITE_SIZE is taken as is.
+"""
 import collections
 import csv
 import glob
+import json
 import sys
+
+# engine kernel -> fg_kernel_stats class names it is timed under
+CLASSES = {
+    "fg::k_part1": ["ingest_part1"],
+    "fg::k_part2": ["ingest_part2"],
+    "fg::k_ingest_count": ["ingest_count"],
+    "fg::k_ingest_scatter_sorted": ["ingest_scatter"],
+    "fg::k_ingest_scatter_direct": ["ingest_scatter"],
+    "fg::k_merge": ["merge_flush_fire", "merge_flush", "merge_fire", "restore"],
+}
 
 
 def summarize(paths):
@@ -14,6 +34,8 @@ def summarize(paths):
             if not k.startswith("fg::"):
                 continue
             k = k.split("(")[0]
+            if "<" in k:
+                k = k.split("<")[0]
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
     out = {}
@@ -22,9 +44,25 @@ def summarize(paths):
     return out
 
 
+def traffic(res):
+    t = {}
+    for k, cs in res.items():
+        if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
+            continue
+        fetch = 2.0 * cs["FETCH_SIZE"] * 1024.0
+        write = cs["WRITE_SIZE"] * 1024.0
+        for cls in CLASSES.get(k, []):
+            t[cls] = {"kernel": k, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+                      "hbm_bytes_per_launch": fetch + write}
+    return t
+
+
 if __name__ == "__main__":
     res = summarize(glob.glob(sys.argv[1]))
     for k, cs in sorted(res.items()):
         print(k)
         for c, v in sorted(cs.items()):
             print(f"   {c:28s} {v:16.1f}")
+    if len(sys.argv) > 2:
+        json.dump(traffic(res), open(sys.argv[2], "w"), indent=1)
+        print("wrote", sys.argv[2])
