@@ -467,6 +467,9 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         p.region_bits = h->region_bits;
         p.fast_stream = plain ? 1 : 0;
         p.n_src = t->upper > 0 ? 1 : 0;
+        // compact LDS table (two workgroups per CU) when no resident state is read and the
+        // COUNT(*) of a key cannot reach 2^32
+        p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) ? 1 : 0;
         p.src = d_src;
         p.n_batches = (int)sb.size();
         p.batches = d_sb;
@@ -479,7 +482,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
         {
             KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
-            HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+            HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
         }
         if (fire_now) {
             fired_tables.push_back(se);

@@ -13,6 +13,8 @@ constexpr int kSlotBits = 12;
 constexpr int kSlots = 1 << kSlotBits;        // 4096 slots x 32 B = 128 KiB of LDS
 constexpr int kRegionCap = 3584;              // max entries per region in HBM (87.5 % of kSlots)
 constexpr int kMergeThreads = 1024;           // persistent merge: one 1024-thread workgroup per CU
+constexpr int kCompactSlots = 3584;           // compact merge table: 3,584 x 20 B = 70 KiB of LDS
+constexpr int kCompactMergeThreads = 512;     // compact merge: two 512-thread workgroups per CU
 constexpr int kIngestThreads = 1024;
 constexpr int kMaxLanes = 4;
 constexpr int kMaxStageBuckets = 32768;       // lanes << region_bits (count / direct scatter LDS)
@@ -104,6 +106,7 @@ constexpr int kMaxMergeBatches = 32;         // pipelined merge: staged batches 
 struct MergeParams {
     int32_t region_bits;       // log2(P): state regions
     int32_t fast_stream;       // every batch plain AoS {key, value}, n_batches <= kMaxMergeBatches
+    int32_t compact;           // compact LDS table (fast_stream, no src tables, < 2^32 records)
     int32_t n_src;
     const TableRef* src;       // device array [n_src]
     int32_t n_batches;
@@ -153,7 +156,8 @@ size_t scan_tmp_words(int64_t n);
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, hipStream_t s);
 // per bucket b: hist[g][b] <- sum_{g' < g} hist[g'][b]; totals[b] <- sum_g hist[g][b]
 hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid, hipStream_t s);
-// persistent merge over the P regions: `workgroups` <= P workgroups, each a strided set of regions
+// persistent merge over the P regions: `workgroups` <= P workgroups, each a strided set of
+// regions (p.compact: two workgroups fit a CU)
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
 hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out,

@@ -859,23 +859,54 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
 // ----------------------------------------------------------------------------------------
 // merge: persistent, one 1024-thread workgroup per CU walking a strided set of regions
 // ----------------------------------------------------------------------------------------
-struct LdsTable {
+// LDS table layouts. Wide: 4,096 slots of {key, COUNT(*) u64, NULL count, sum} (128 KiB,
+// one 1,024-thread workgroup per CU) for every merge. Compact: 3,584 slots of {key, sum,
+// COUNT(*) u32} (70 KiB, two 512-thread workgroups per CU) for the common fire/flush of
+// plain staged records (no NULLs, no resident state, < 2^32 records).
+template <bool C>
+struct MergeCfg;
+template <>
+struct MergeCfg<false> {
+    static constexpr int kSlotsT = kSlots;
+    static constexpr int kThreads = kMergeThreads;
+};
+template <>
+struct MergeCfg<true> {
+    static constexpr int kSlotsT = kCompactSlots;
+    static constexpr int kThreads = kCompactMergeThreads;
+};
+
+template <bool C>
+struct LdsTableT;
+template <>
+struct LdsTableT<false> {
     int64_t key[kSlots + 1];                  // slot kSlots: the key equal to the sentinel
     unsigned long long cs[kSlots + 1];        // COUNT(*)
     unsigned long long cn[kSlots + 1];        // records whose value was NULL
     unsigned long long sum[kSlots + 1];       // SUM / AVG sum (i64, or f64 bits)
 };
+template <>
+struct LdsTableT<true> {
+    int64_t key[kCompactSlots + 1];
+    unsigned long long sum[kCompactSlots + 1];
+    uint32_t cs[kCompactSlots + 1];
+};
 
 // home slot: a multiplicative hash of the key (the region already selects keys by the top
-// bits of fmix64, independent of these bits)
+// bits of fmix64, independent of these bits), scaled to the table size
+template <bool C>
 __device__ __forceinline__ uint32_t lds_home(int64_t k) {
-    return (uint32_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> (64 - kSlotBits));
+    const uint64_t m = (uint64_t)k * 0x9E3779B97F4A7C15ull;
+    if constexpr (C) return (uint32_t)(((m >> 32) * (uint64_t)kCompactSlots) >> 32);
+    else return (uint32_t)(m >> (64 - kSlotBits));
 }
 
-__device__ __forceinline__ int lds_find_or_insert(LdsTable& t, int64_t k, bool& full) {
-    if (k == JMIN) return kSlots;
-    uint32_t slot = lds_home(k);
-    for (int probe = 0; probe < kSlots; probe++) {
+template <bool C>
+__device__ __forceinline__ int lds_find_or_insert(LdsTableT<C>& t, int64_t k, bool& full) {
+    constexpr int S = MergeCfg<C>::kSlotsT;
+    if (k == JMIN) return S;
+    uint32_t slot = lds_home<C>(k);
+    for (int probe = 0; probe < S; probe++) {
         const int64_t cur = t.key[slot];
         if (cur == k) return (int)slot;
         if (cur == JMIN) {
@@ -883,16 +914,21 @@ __device__ __forceinline__ int lds_find_or_insert(LdsTable& t, int64_t k, bool& 
                                                      (unsigned long long)JMIN, (unsigned long long)k);
             if (old == (unsigned long long)JMIN || old == (unsigned long long)k) return (int)slot;
         }
-        slot = (slot + 1) & (kSlots - 1);
+        slot = slot + 1 == (uint32_t)S ? 0u : slot + 1;
     }
     full = true;
     return -1;
 }
 
-__device__ __forceinline__ void lds_add(LdsTable& t, int slot, unsigned long long cs, unsigned long long cn,
+template <bool C>
+__device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long long cs, unsigned long long cn,
                                         int64_t sum_bits, int vt) {
-    atomicAdd(&t.cs[slot], cs);
-    if (cn) atomicAdd(&t.cn[slot], cn);
+    if constexpr (C) {
+        atomicAdd(&t.cs[slot], (uint32_t)cs);
+    } else {
+        atomicAdd(&t.cs[slot], cs);
+        if (cn) atomicAdd(&t.cn[slot], cn);
+    }
     if (vt == 2) {
         atomicAdd(reinterpret_cast<double*>(&t.sum[slot]), __longlong_as_double(sum_bits));
     } else if (vt == 1) {
@@ -900,10 +936,7 @@ __device__ __forceinline__ void lds_add(LdsTable& t, int slot, unsigned long lon
     }
 }
 
-constexpr int kMergeWaves = kMergeThreads / 64;
-constexpr int kCompRounds = kSlots / kMergeThreads + 1;   // + 1: the sentinel slot (thread 0)
 constexpr int kMergeU = 4;                                // 16-B staged loads per thread per chunk (x2 buffers)
-constexpr uint32_t kChunk = kMergeU * kMergeThreads;
 
 // Pipelined staged stream (every batch plain {key, value} AoS, <= kMaxMergeBatches): the
 // workgroup walks its regions r0, r0 + G, ... as one stream of chunks (chunks never span
@@ -918,9 +951,15 @@ struct MergeCursor {
     bool ok;         // settled on a chunk (false: walked past the regions whose ranges are known)
 };
 
-__global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
-    __shared__ LdsTable t;
-    __shared__ uint32_t s_grp[kCompRounds * kMergeWaves];   // per (round, wave) row counts -> offsets
+template <bool C>
+__global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) {
+    constexpr int S = MergeCfg<C>::kSlotsT;
+    constexpr int T = MergeCfg<C>::kThreads;
+    constexpr int kWaves = T / 64;
+    constexpr int kRounds = (S + T - 1) / T + 1;    // + 1: the sentinel slot (thread 0)
+    constexpr uint32_t kChunk = kMergeU * T;
+    __shared__ LdsTableT<C> t;
+    __shared__ uint32_t s_grp[kRounds * kWaves];   // per (round, wave) row counts -> offsets
     __shared__ unsigned int s_flags;
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
@@ -967,22 +1006,22 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
         const longlong2* rec = s_brec[m.j];
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
-            const uint32_t i = m.i0 + u * kMergeThreads + tid;
+            const uint32_t i = m.i0 + u * T + tid;
             c[u] = rec[i < m.end ? i : m.end - 1];
         }
     };
     auto insert = [&](const longlong2 (&c)[kMergeU], const MergeCursor& m, bool& full) {
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
-            if (m.i0 + u * kMergeThreads + tid >= m.end) continue;
-            const int slot = lds_find_or_insert(t, c[u].x, full);
-            if (slot >= 0) lds_add(t, slot, 1ull, 0ull, c[u].y, vt);
+            if (m.i0 + u * T + tid >= m.end) continue;
+            const int slot = lds_find_or_insert<C>(t, c[u].x, full);
+            if (slot >= 0) lds_add<C>(t, slot, 1ull, 0ull, c[u].y, vt);
         }
     };
     MergeCursor cur{nreg, 0, 0, 0};
     if (fast) {
         if (tid < nb) s_brec[tid] = reinterpret_cast<const longlong2*>(p.batches[tid].rec);
-        for (int q = tid; q < 2 * nb; q += kMergeThreads) {   // ranges of regions 0 and 1
+        for (int q = tid; q < 2 * nb; q += T) {   // ranges of regions 0 and 1
             const int ri = q / nb, j = q % nb;
             uint32_t beg = 0, end = 0;
             if (ri < nreg) range_of(ri, j, beg, end);
@@ -997,19 +1036,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
 
     for (int ri = 0; ri < nreg; ri++) {
         const int r = (int)blockIdx.x + ri * G;
-        for (int i = tid; i < kSlots; i += kMergeThreads) {
+        for (int i = tid; i <= S; i += T) {
             t.key[i] = JMIN;
             t.cs[i] = 0;
-            t.cn[i] = 0;
+            if constexpr (!C) t.cn[i] = 0;
             t.sum[i] = 0;
         }
-        if (tid == 0) {
-            t.key[kSlots] = JMIN;
-            t.cs[kSlots] = 0;
-            t.cn[kSlots] = 0;
-            t.sum[kSlots] = 0;
-            s_flags = 0;
-        }
+        if (tid == 0) s_flags = 0;
         // fast path: ranges of region ri + 2 (written to LDS after this region's inserts)
         uint32_t nbeg = 0, nend = 0;
         if (fast && tid < nb && ri + 2 < nreg) range_of(ri + 2, tid, nbeg, nend);
@@ -1017,15 +1050,15 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
         bool full = false;
 
         // 1) resident slice regions (state) ------------------------------------------
-        for (int j = 0; j < p.n_src; j++) {
+        for (int j = 0; !C && j < p.n_src; j++) {
             const TableRef src = p.src[j];
             const uint32_t n = src.counts[r];
             const int64_t* base = src.base + (int64_t)r * 4 * cap;
-            for (uint32_t i0 = 0; i0 < n; i0 += 4 * kMergeThreads) {
+            for (uint32_t i0 = 0; i0 < n; i0 += 4 * T) {
                 int64_t k[4], cs[4], cn[4], sm[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {      // issue all loads first (latency hiding)
-                    const uint32_t i = i0 + u * kMergeThreads + tid;
+                    const uint32_t i = i0 + u * T + tid;
                     if (i < n) {
                         k[u] = base[i];
                         cs[u] = base[cap + i];
@@ -1035,10 +1068,10 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    const uint32_t i = i0 + u * kMergeThreads + tid;
+                    const uint32_t i = i0 + u * T + tid;
                     if (i >= n) continue;
-                    const int slot = lds_find_or_insert(t, k[u], full);
-                    if (slot >= 0) lds_add(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
+                    const int slot = lds_find_or_insert<C>(t, k[u], full);
+                    if (slot >= 0) lds_add<C>(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
                 }
             }
         }
@@ -1071,34 +1104,34 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
 #pragma unroll
                 for (int u = 0; u < kMergeU; u++) ca[u] = cb[u];
             }
-        } else {
+        } else if constexpr (!C) {
             for (int j = 0; j < nb; j++) {
                 const StagedBatch sb = p.batches[j];
                 const uint32_t b0 = sb.bucket_off[0];
                 const uint32_t beg = sb.bucket_off[r] - b0;
                 const uint32_t end = sb.bucket_off[r + 1] - b0;
                 if (sb.is_acc) {
-                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                        const int slot = lds_find_or_insert(t, sb.rec[i], full);
+                    for (uint32_t i = beg + tid; i < end; i += T) {
+                        const int slot = lds_find_or_insert<C>(t, sb.rec[i], full);
                         if (slot >= 0)
-                            lds_add(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
+                            lds_add<C>(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
                                     sb.val[i], vt);
                     }
                 } else if (sb.stride == 2) {
                     const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
-                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
+                    for (uint32_t i = beg + tid; i < end; i += T) {
                         const longlong2 rc = rec[i];
-                        const int slot = lds_find_or_insert(t, rc.x, full);
+                        const int slot = lds_find_or_insert<C>(t, rc.x, full);
                         if (slot < 0) continue;
                         const bool isnull = sb.vnull != nullptr && sb.vnull[i] != 0;
-                        lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
+                        lds_add<C>(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
                     }
                 } else {
-                    for (uint32_t i = beg + tid; i < end; i += kMergeThreads) {
-                        const int slot = lds_find_or_insert(t, sb.rec[i], full);
+                    for (uint32_t i = beg + tid; i < end; i += T) {
+                        const int slot = lds_find_or_insert<C>(t, sb.rec[i], full);
                         if (slot < 0) continue;
                         const bool isnull = sb.vnull != nullptr && sb.vnull[i];
-                        lds_add(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
+                        lds_add<C>(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
                     }
                 }
             }
@@ -1110,21 +1143,21 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
         }
         lds_barrier();
 
-        // 3) compaction: round k covers slots [k*T, (k+1)*T) (round kCompRounds-1: the
+        // 3) compaction: round k covers slots [k*T, (k+1)*T) (round kRounds-1: the
         //    sentinel slot, thread 0); rows of one (round, wave) are consecutive lanes, so the
         //    row stores of a wave are contiguous
         uint64_t occ_mask = 0;   // bit k: this thread's slot of round k is occupied
 #pragma unroll
-        for (int k = 0; k < kCompRounds; k++) {
-            const int slot = k < kCompRounds - 1 ? k * kMergeThreads + tid : kSlots;
-            const bool occ = (k < kCompRounds - 1 || tid == 0) && t.cs[slot] != 0;
+        for (int k = 0; k < kRounds; k++) {
+            const int slot = k < kRounds - 1 ? k * T + tid : S;
+            const bool occ = (k < kRounds - 1 ? slot < S : tid == 0) && t.cs[slot] != 0;
             const uint64_t bal = __ballot(occ);
             if (occ) occ_mask |= 1ull << k;
-            if (lane == 0) s_grp[k * kMergeWaves + wave] = (uint32_t)__popcll(bal);
+            if (lane == 0) s_grp[k * kWaves + wave] = (uint32_t)__popcll(bal);
         }
         lds_barrier();
-        if (wave == 0) {   // exclusive scan of the kCompRounds * kMergeWaves group counts (<= 128)
-            constexpr int NG = kCompRounds * kMergeWaves;
+        if (wave == 0) {   // exclusive scan of the kRounds * kWaves group counts (<= 128)
+            constexpr int NG = kRounds * kWaves;
             const uint32_t a = 2 * lane < NG ? s_grp[2 * lane] : 0u;
             const uint32_t b = 2 * lane + 1 < NG ? s_grp[2 * lane + 1] : 0u;
             uint32_t x = a + b;
@@ -1157,14 +1190,15 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
         const unsigned long long obase = s_out_base;
         // per round: the wave's occupied lanes below this lane give the rank within the group
 #pragma unroll
-        for (int k = 0; k < kCompRounds; k++) {
+        for (int k = 0; k < kRounds; k++) {
             const bool occ = (occ_mask >> k) & 1;
             const uint64_t bal = __ballot(occ);
             if (!occ) continue;
-            const int slot = k < kCompRounds - 1 ? k * kMergeThreads + tid : kSlots;
-            const uint32_t at = s_grp[k * kMergeWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-            const int64_t key = slot == kSlots ? JMIN : t.key[slot];
-            const unsigned long long cs = t.cs[slot], cn = t.cn[slot];
+            const int slot = k < kRounds - 1 ? k * T + tid : S;
+            const uint32_t at = s_grp[k * kWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+            const int64_t key = slot == S ? JMIN : t.key[slot];
+            unsigned long long cs = t.cs[slot], cn = 0;
+            if constexpr (!C) cn = t.cn[slot];
             const int64_t sum = (int64_t)t.sum[slot];
             if (write_dst) {
                 dbase[at] = key;
@@ -1213,7 +1247,12 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge(MergeParams p) {
 }
 
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {
-    hipLaunchKernelGGL(k_merge, dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+    if (p.compact) {
+        if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_merge<true>, dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p);
+    } else {
+        hipLaunchKernelGGL(k_merge<false>, dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+    }
     return hipGetLastError();
 }
 
