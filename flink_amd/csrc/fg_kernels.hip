@@ -588,7 +588,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
 // Within a bucket the staged layout is workgroup-major, so the K workgroups' records of
 // bucket b own the one contiguous range starting at the column prefix of g0 (their order
 // inside it is immaterial): one cursor per fine bucket serves the whole group.
-constexpr int kPart2MaxFrags = 1024;   // fragments (group tiles) per unit held in LDS
+constexpr int kPart2MaxFrags = 512;    // fragments (group tiles) per unit held in LDS
 
 int32_t part2_group(int32_t max_tiles) {
     int32_t k = kPart2MaxFrags / (max_tiles > 0 ? max_tiles : 1);
@@ -598,10 +598,9 @@ int32_t part2_group(int32_t max_tiles) {
 __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t group) {
     constexpr int NF = 1 << kFineBits;
     constexpr int R = kPart2Tile / kPart2Threads;   // 8
-    constexpr int FPT = kPart2MaxFrags / kPart2Threads;   // 4 fragments per thread
+    constexpr int FPT = kPart2MaxFrags / kPart2Threads;   // fragments per thread
     __shared__ longlong2 s_rec[kPart2Tile];          // 32 KiB
-    __shared__ uint8_t s_fb[kPart2Tile];
-    __shared__ uint8_t s_nul[kPart2Tile];
+    __shared__ uint8_t s_fb[kPart2Tile];             // fine bucket | NULL flag << 7
     __shared__ uint32_t s_fstart[kPart2MaxFrags + 1];  // prefix of fragment lengths
     __shared__ uint32_t s_fsrc[kPart2MaxFrags];        // tmp position of each fragment
     __shared__ uint32_t s_cnt[NF], s_off[NF + 1], s_cur[NF];
@@ -660,10 +659,11 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     __syncthreads();
     const bool has_null = p.vnull != nullptr;
     const bool aos = p.st_stride == 2;
-    for (uint32_t base = 0; base < total; base += kPart2Tile) {
-        longlong2 rr[R];
-        uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
-        uint8_t rn[R];
+    // records of a sub-tile: idx = base + u * T + tid; the next sub-tile's loads are issued
+    // before this one is ranked, staged and written
+    longlong2 rr[R];
+    uint8_t rn[R];
+    auto load = [&](uint32_t base) {
 #pragma unroll
         for (int u = 0; u < R; u++) {
             const uint32_t idx = base + (uint32_t)(u * kPart2Threads + tid);
@@ -679,14 +679,26 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             rr[u] = p.tmp[src];
             if (has_null) rn[u] = p.tmp_null[src];
         }
+    };
+    if (total > 0) load(0);
+    for (uint32_t base = 0; base < total; base += kPart2Tile) {
+        longlong2 cr[R];
+        uint8_t cn[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            cr[u] = rr[u];
+            cn[u] = rn[u];
+        }
+        if (base + kPart2Tile < total) load(base + kPart2Tile);
+        uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
 #pragma unroll
         for (int u = 0; u < R; u++) {
             rf[u] = 0xffffffffu;
             if (base + (uint32_t)(u * kPart2Threads + tid) >= total) continue;
-            const uint32_t f = (uint32_t)(fmix64((uint64_t)rr[u].x) >> (64 - p.region_bits)) & (NF - 1);
+            const uint32_t f = (uint32_t)(fmix64((uint64_t)cr[u].x) >> (64 - p.region_bits)) & (NF - 1);
             rf[u] = (atomicAdd(&s_cnt[f], 1u) << 6) | f;
         }
-        __syncthreads();
+        lds_barrier();
         if (tid < 64) {   // one wave: exclusive scan of the 64 fine counts
             const uint32_t v = s_cnt[tid];
             uint32_t x = v;
@@ -697,31 +709,31 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             s_off[tid] = x - v;
             if (tid == 63) s_off[NF] = x;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int u = 0; u < R; u++) {
             if (rf[u] == 0xffffffffu) continue;
             const uint32_t slot = s_off[rf[u] & (NF - 1)] + (rf[u] >> 6);
-            s_rec[slot] = rr[u];
-            s_fb[slot] = (uint8_t)(rf[u] & (NF - 1));
-            if (has_null) s_nul[slot] = rn[u];
+            s_rec[slot] = cr[u];
+            s_fb[slot] = (uint8_t)((rf[u] & (NF - 1)) | (cn[u] ? 0x80u : 0u));
         }
-        __syncthreads();
+        lds_barrier();
         const uint32_t sub = s_off[NF];
         for (uint32_t i = tid; i < sub; i += kPart2Threads) {
-            const int f = s_fb[i];
+            const uint32_t fb = s_fb[i];
+            const int f = (int)(fb & (NF - 1));
             const int64_t pos = (int64_t)(s_cur[f] + (i - s_off[f]));
             const longlong2 r = s_rec[i];
             if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * pos) = r;
             else p.st_rec[pos] = r.x;
-            if (has_null) p.st_null[pos] = s_nul[i];
+            if (has_null) p.st_null[pos] = (uint8_t)(fb >> 7);
         }
-        __syncthreads();
+        lds_barrier();
         if (tid < NF) {
             s_cur[tid] += s_cnt[tid];
             s_cnt[tid] = 0;
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 

@@ -31,6 +31,8 @@ def summarize(paths):
     for p in paths:
         for r in csv.DictReader(open(p)):
             k = r["Kernel_Name"]
+            if k.startswith("void "):
+                k = k[5:]
             if not k.startswith("fg::"):
                 continue
             k = k.split("(")[0]
