@@ -1022,11 +1022,23 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
             c[u] = rec[i < m.end ? i : m.end - 1];
         }
     };
+    // the home-slot probes of the chunk's records are issued together; a record whose key
+    // sits in its home slot (every repeat of a key, at this load factor) is added at once,
+    // the others continue probing from the slot after home
     auto insert = [&](const longlong2 (&c)[kMergeU], const MergeCursor& m, bool& full) {
+        uint32_t home[kMergeU];
+        int64_t cur0[kMergeU];
+#pragma unroll
+        for (int u = 0; u < kMergeU; u++) {
+            home[u] = lds_home<C>(c[u].x);
+            cur0[u] = t.key[home[u]];
+        }
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             if (m.i0 + u * T + tid >= m.end) continue;
-            const int slot = lds_find_or_insert<C>(t, c[u].x, full);
+            int slot;
+            if (cur0[u] == c[u].x && c[u].x != JMIN) slot = (int)home[u];
+            else slot = lds_find_or_insert<C>(t, c[u].x, full);
             if (slot >= 0) lds_add<C>(t, slot, 1ull, 0ull, c[u].y, vt);
         }
     };

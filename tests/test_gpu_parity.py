@@ -112,6 +112,14 @@ STREAM_CASES = [
     ("ds_tumble_i64", cfg_of("tumble", 1000, vt="i64", mode="datastream"), dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=700)),
     ("ds_sliding_i64", cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=1500)),
     ("tumble_many_regions", cfg_of("tumble", 1000), dict(n=1_000_000, keys=400_000, batch=100_000, delay=0, jitter=0)),
+    # >= 64 state regions: two-pass partition + compact / wide merge paths
+    ("regions_f64_nulls_late", cfg_of("tumble", 700), dict(n=600_000, keys=150_000, batch=60_000, delay=100, jitter=1500, null_frac=0.2)),
+    ("regions_i64_ooo_lanes", cfg_of("tumble", 200, vt="i64"), dict(n=600_000, keys=120_000, batch=50_000, delay=150, jitter=450)),
+    ("regions_i64_wrap", cfg_of("tumble", 500, vt="i64"), dict(n=400_000, keys=100_000, batch=40_000, delay=0, jitter=200, big_ints=True)),
+    ("regions_hop_f64", cfg_of("hop", 3000, 1000), dict(n=600_000, keys=100_000, batch=40_000, delay=200, jitter=800)),
+    ("regions_cumulate_i64_late", cfg_of("cumulate", 4000, 500, vt="i64"), dict(n=500_000, keys=100_000, batch=20_000, delay=50, jitter=2500)),
+    ("regions_ds_sliding", cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), dict(n=400_000, keys=100_000, batch=30_000, delay=100, jitter=1500)),
+    ("regions_spread_keys", cfg_of("tumble", 1000), dict(n=500_000, keys=200_000, batch=50_000, delay=50, jitter=300, key_spread=True)),
 ]
 
 
@@ -130,6 +138,48 @@ def test_lane_conflict_slow_path(oracle_mod):
     """A batch spanning more slices than the staged lanes (filtered multi-pass ingest)."""
     cfg = cfg_of("tumble", 100)
     drive_both(oracle_mod, cfg, n=100_000, keys=500, batch=50_000, delay=0, jitter=0)
+
+
+def test_lane_conflict_slow_path_two_pass(oracle_mod):
+    """The same through the two-pass partition (>= 64 regions)."""
+    cfg = cfg_of("tumble", 20)
+    drive_both(oracle_mod, cfg, n=600_000, keys=100_000, batch=300_000, delay=0, jitter=0)
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_snapshot_restore_many_regions(oracle_mod, kind):
+    # jitter < watermark delay: no record older than the checkpoint's watermark arrives after
+    # the restore (that case re-fires windows in the reference -- DESIGN.md section 3, divergence 2)
+    cfg = cfg_of(kind, 4000, 0 if kind == "tumble" else 1000)
+    drive_both(oracle_mod, cfg, n=400_000, keys=100_000, batch=20_000, delay=100, jitter=80, snapshot_at=9)
+
+
+def test_count_star_only_many_regions(oracle_mod):
+    """COUNT(*) with no value column (8-byte staged records) vs the oracle's COUNT(*)."""
+    import flink_amd as F
+    n, keys = 500_000, 120_000
+    key, ts, val, _ = make_stream(n, keys, "f64", jitter_ms=300)
+    op = F.WindowAggOperator(F.tumbling(1000), aggs=("count_star",), val_type="none", expected_keys=keys,
+                             buffer_records=1 << 18)
+    o = oracle_mod.OracleOperator(kind=0, size=1000, val_type=2)
+    got, exp = [], []
+    for lo, hi, wm in batches_with_watermarks(n, 40_000, ts, 100):
+        op.process_batch(key[lo:hi], ts[lo:hi])
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        got.append(op.process_watermark(wm))
+        o.process_watermark(wm)
+        exp.append(o.take_rows())
+    got.append(op.process_watermark(JMAX))
+    o.process_watermark(JMAX)
+    exp.append(o.take_rows())
+    g, e = np.concatenate(got), np.concatenate(exp)
+    g = g[np.lexsort((g["key"], g["window_end"]))]
+    e = e[np.lexsort((e["key"], e["window_end"]))]
+    assert len(g) == len(e)
+    assert np.array_equal(g["key"], e["key"]) and np.array_equal(g["window_end"], e["window_end"])
+    assert np.array_equal(g["count_star"], e["cnt_star"])
+    assert op.num_late_records_dropped == o.late_dropped
+    op.close()
 
 
 def test_empty_and_ragged_batches(oracle_mod):
