@@ -56,6 +56,14 @@ class FgStateRows(C.Structure):
     ]
 
 
+class FgPartials(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("location", C.c_int32), ("reserved0", C.c_int32),
+        ("key", C.c_void_p), ("slice_end", C.c_void_p), ("cnt_star", C.c_void_p), ("cnt_val", C.c_void_p),
+        ("sum", C.c_void_p),
+    ]
+
+
 class FgStats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "records_in", "records_staged", "late_dropped", "rows_fired", "flushes", "live_slices",
@@ -68,10 +76,11 @@ class FgKernelStat(C.Structure):
 
 
 FLAG_KERNEL_TIMING = 1
+FLAG_LOCAL_PARTIALS = 2
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (
-    "fg_open", "fg_add_batch", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    "fg_open", "fg_add_batch", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
     "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_abi_version",
 )
@@ -107,6 +116,7 @@ def load():
     P = C.c_void_p
     L.fg_open.argtypes = [C.POINTER(FgConfig), C.POINTER(P)]
     L.fg_add_batch.argtypes = [P, C.POINTER(FgBatch)]
+    L.fg_add_partials.argtypes = [P, C.POINTER(FgPartials)]
     L.fg_advance_progress.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(FgRows)]
     L.fg_flush.argtypes = [P]
     L.fg_snapshot_state.argtypes = [P, C.POINTER(FgStateRows), C.POINTER(C.c_int64)]
@@ -126,7 +136,7 @@ def load():
     L.fg_partition_by_owner.argtypes = [C.c_int32, P, C.c_int64, P, P, P, C.c_int32, C.c_int32, C.c_int32,
                                         P, P, P, P]
     L.fg_abi_version.restype = C.c_int
-    for fn in ("fg_open", "fg_add_batch", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    for fn in ("fg_open", "fg_add_batch", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
                "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner"):
         getattr(L, fn).restype = C.c_int

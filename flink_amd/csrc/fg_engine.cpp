@@ -95,6 +95,7 @@ struct SliceTable {
 // [lane_start[l], lane_start[l] + lane_n[l]) of lane l's staged area.
 struct Staged {
     DevBuf bucket_off;    // F + 1 uint32 (lane-major)
+    bool is_acc = false;  // accumulator rows (global phase) in the lanes' accumulator areas
     int64_t lane_start[kMaxLanes] = {0, 0, 0, 0};
     int64_t lane_n[kMaxLanes] = {0, 0, 0, 0};
     bool has_null = false;
@@ -107,7 +108,8 @@ struct Staged {
 constexpr int64_t kEmptyLane = INT64_MIN;
 struct Lane {
     int64_t q = kEmptyLane;
-    int64_t fill = 0;
+    int64_t fill = 0;       // staged records
+    int64_t acc_fill = 0;   // staged accumulator rows (global phase)
     std::vector<Staged*> passes;
 };
 
@@ -163,6 +165,11 @@ struct fg_handle {
     int st_stride = 2;          // int64 words per staged record: {key, val} or {key}
     DevBuf st_rec, st_null;
     Lane lane[kMaxLanes];
+    // accumulator areas (global phase, fg_add_partials): SoA, acc_cap rows per lane
+    int64_t acc_cap = 0;
+    DevBuf acc_key, acc_cs, acc_cn, acc_sum;
+    DevBuf in_cs, in_cv, in_sum, in_slice;
+    bool local = false;     // FG_FLAG_LOCAL_PARTIALS: fired slices emit partial accumulators
     std::vector<std::unique_ptr<Staged>> passes;       // live passes
     std::vector<std::unique_ptr<Staged>> pass_pool;
     int64_t anchor_start = JMIN;   // a recent slice start: base of the 32-bit rowtime fast path
@@ -361,7 +368,9 @@ struct FireRange {   // windows whose timers fire in (prev, wm]
 
 void fill_emit(fg_handle* h, MergeParams& p, int64_t wend) {
     p.emit = 1;
-    p.wstart = window_start(h->w, wend);
+    // local phase: the emitted "window" is the slice itself (LocalAggCombiner emits
+    // (key, acc, slice_end) rows)
+    p.wstart = h->local ? jsub(wend, h->w.slice) : window_start(h->w, wend);
     p.wend = wend;
     p.out_ts = jsub(wend, 1);
     p.num_aggs = h->cfg.num_aggs;
@@ -384,7 +393,7 @@ bool staged_any(const fg_handle* h) {
 }
 int64_t staged_records(const fg_handle* h) {
     int64_t n = 0;
-    for (int l = 0; l < h->lanes; l++) n += h->lane[l].fill;
+    for (int l = 0; l < h->lanes; l++) n += h->lane[l].fill + h->lane[l].acc_fill;
     return n;
 }
 int64_t min_staged_slice_end(const fg_handle* h) {
@@ -433,10 +442,20 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         std::vector<StagedBatch> sb;
         for (Staged* s : ln.passes) {
             StagedBatch b{};
-            b.rec = lane_rec(h, l) + s->lane_start[l] * h->st_stride;
-            b.vnull = s->has_null ? lane_null(h, l) + s->lane_start[l] : nullptr;
             b.bucket_off = s->bucket_off.as<uint32_t>() + ((int64_t)l << h->region_bits);
-            b.stride = h->st_stride;
+            if (s->is_acc) {
+                const int64_t at = (int64_t)l * h->acc_cap + s->lane_start[l];
+                b.is_acc = 1;
+                b.stride = 1;
+                b.rec = h->acc_key.as<int64_t>() + at;
+                b.cnt_star = h->acc_cs.as<int64_t>() + at;
+                b.cnt_null = h->acc_cn.as<int64_t>() + at;
+                b.val = h->acc_sum.as<int64_t>() + at;
+            } else {
+                b.rec = lane_rec(h, l) + s->lane_start[l] * h->st_stride;
+                b.vnull = s->has_null ? lane_null(h, l) + s->lane_start[l] : nullptr;
+                b.stride = h->st_stride;
+            }
             sb.push_back(b);
         }
         const StagedBatch* d_sb = nullptr;
@@ -446,11 +465,13 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         rc = table_get(h, se, true, &t);
         if (rc) return rc;
         const int64_t trig = trigger_time(h->w, se);
-        const bool fire_now = fire && h->w.kind == TUMBLE && se != JMAX && trig > fire->prev && trig <= fire->wm;
+        // local phase: every fired slice lane emits its partial accumulators
+        const bool fire_now =
+            fire && (h->local || (h->w.kind == TUMBLE && se != JMAX && trig > fire->prev && trig <= fire->wm));
         if (fire_now) {
             rc = reset_out_count(h);
             if (rc) return rc;
-            const int64_t ub = std::min<int64_t>(t->upper + ln.fill, (int64_t)kRegionCap * h->P);
+            const int64_t ub = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, (int64_t)kRegionCap * h->P);
             rc = ensure_out(h, h->out_n + h->pending_out + ub);
             if (rc) return rc;
             h->pending_out += ub;
@@ -462,7 +483,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
             if (rc) return rc;
         }
         bool plain = h->st_stride == 2 && !sb.empty() && sb.size() <= (size_t)kMaxMergeBatches;
-        for (Staged* s : ln.passes) plain = plain && !s->has_null;
+        for (Staged* s : ln.passes) plain = plain && !s->has_null && !s->is_acc;
         MergeParams p{};
         p.region_bits = h->region_bits;
         p.fast_stream = plain ? 1 : 0;
@@ -488,7 +509,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
             fired_tables.push_back(se);
             any_emit = true;
         } else {
-            t->upper = std::min<int64_t>(t->upper + ln.fill, (int64_t)kRegionCap * h->P);
+            t->upper = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, (int64_t)kRegionCap * h->P);
         }
     }
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
@@ -716,7 +737,7 @@ void set_fast_path(fg_handle* h, IngestParams* p) {
     p->tbase = (int64_t)tb;
     p->div_m = ~0ull / (uint64_t)S + 1;
     p->qbase = floor_div(p->tbase, S) + 1;
-    __int128 lim = (__int128)h->current_progress + 1 + h->w.tz;
+    __int128 lim = (__int128)(h->local ? JMIN : h->current_progress) + 1 + h->w.tz;
     if (lim < (__int128)JMIN) lim = JMIN;
     if (lim > (__int128)JMAX) lim = JMAX;
     p->fired_lim = (int64_t)lim;
@@ -764,7 +785,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.ts = ts;
     p.val = val;
     p.vnull = vnull;
-    p.progress = h->current_progress;
+    p.progress = h->local ? JMIN : h->current_progress;   // the local phase drops nothing
     p.lanes = h->lanes;
     p.region_bits = h->region_bits;
     p.filter_lo = flo;
@@ -923,6 +944,146 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     return FG_OK;
 }
 
+// grow the per-lane accumulator areas to `need` rows per lane (all lanes free of acc rows)
+int grow_acc(fg_handle* h, int64_t need) {
+    if (need <= h->acc_cap) return FG_OK;
+    for (int l = 0; l < h->lanes; l++)
+        if (h->lane[l].acc_fill) return h->fail(FG_ESTATE, "internal: accumulator areas grown while in use");
+    const int64_t cap = std::max<int64_t>(need, h->acc_cap + h->acc_cap / 2);
+    const size_t b = 8 * (size_t)h->lanes * cap;
+    HIPCHK(h, h->acc_key.ensure(b));
+    HIPCHK(h, h->acc_cs.ensure(b));
+    HIPCHK(h, h->acc_cn.ensure(b));
+    HIPCHK(h, h->acc_sum.ensure(b));
+    h->acc_cap = cap;
+    return FG_OK;
+}
+
+// one global-phase pass over partial accumulator rows (device columns; `ts` = the pseudo
+// rowtime slice_end - 1 - tz): count pass with the global operator's late rules, then
+// the rows are scattered into their slice lanes' accumulator areas. Returns -1 when the
+// rows span more slices than the lanes can hold.
+int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* cs, const int64_t* cv,
+             const int64_t* sum, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+    IngestParams p{};
+    p.w = h->w;
+    p.n = n;
+    p.key = key;
+    p.ts = ts;
+    p.progress = h->current_progress;
+    p.lanes = h->lanes;
+    p.region_bits = h->region_bits;
+    p.filter_lo = flo;
+    p.filter_hi = fhi;
+    p.count_drops = count_drops ? 1 : 0;
+    int64_t g = (n + 16383) / 16384;
+    p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(h->grid, g));
+    p.vec = ((uintptr_t)key % 16 == 0 && (uintptr_t)ts % 16 == 0) ? 1 : 0;
+    p.hist = h->hist.as<uint32_t>();
+    set_fast_path(h, &p);
+    DevCounters init{};
+    init.qmin = JMAX;
+    init.qmax = JMIN;
+    std::memcpy(h->h_counters.p, &init, sizeof init);
+    HIPCHK(h, hipMemcpyAsync(h->counters.p, h->h_counters.p, sizeof init, hipMemcpyHostToDevice, h->stream));
+    DevCounters* dc = h->counters.as<DevCounters>();
+    p.drops = &dc->drops;
+    p.lane_mask = &dc->lane_mask;
+    p.qmin = &dc->qmin;
+    p.qmax = &dc->qmax;
+    p.lane_total = dc->lane_total;
+    {
+        KTimer kt(h, K_COUNT, n);
+        HIPCHK(h, launch_ingest_count(p, h->stream));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    int rc = sync(h);
+    if (rc) return rc;
+    DevCounters got;
+    std::memcpy(&got, h->h_counters.p, sizeof got);
+    out->drops = got.drops;
+    out->qmin = got.qmin;
+    out->qmax = got.qmax;
+    for (int l = 0; l < kMaxLanes; l++) {
+        out->lane_min[l] = JMAX;
+        out->lane_max[l] = JMIN;
+        out->lane_total[l] = (long long)got.lane_total[l];
+    }
+    if (got.qmin > got.qmax) return FG_OK;
+    if ((uint64_t)(got.qmax - got.qmin) >= (uint64_t)h->lanes) return -1;
+    for (int64_t q = got.qmin; q <= got.qmax; q++) {
+        const int l = (int)(q & (h->lanes - 1));
+        if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
+    }
+    int64_t need = 0;
+    for (int l = 0; l < h->lanes; l++) need = std::max<int64_t>(need, out->lane_total[l]);
+    if (need > h->acc_cap) {
+        rc = flush(h);
+        if (rc) return rc;
+        rc = grow_acc(h, std::max<int64_t>(need, std::min<int64_t>(h->lane_cap, (int64_t)1 << 24)));
+        if (rc) return rc;
+    }
+    for (int l = 0; l < h->lanes; l++) {
+        if (out->lane_total[l] == 0) continue;
+        const Lane& ln = h->lane[l];
+        if (ln.q == kEmptyLane || (ln.q == out->lane_min[l] && ln.acc_fill + out->lane_total[l] <= h->acc_cap)) continue;
+        rc = flush_lane(h, l);
+        if (rc) return rc;
+    }
+    std::unique_ptr<Staged> s;
+    if (!h->pass_pool.empty()) {
+        s = std::move(h->pass_pool.back());
+        h->pass_pool.pop_back();
+    } else {
+        s.reset(new Staged());
+    }
+    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
+    {
+        KTimer kt(h, K_SCAN, 0);
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), h->F, p.grid, h->stream));
+        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F,
+                                  h->scan_tmp.as<uint32_t>(), h->stream));
+    }
+    p.bucket_base = s->bucket_off.as<uint32_t>();
+    int64_t before = 0;
+    for (int l = 0; l < kMaxLanes; l++) {
+        p.lane_shift[l] = 0;
+        s->lane_start[l] = 0;
+        s->lane_n[l] = 0;
+        if (l >= h->lanes) continue;
+        p.lane_shift[l] = (int64_t)l * h->acc_cap + h->lane[l].acc_fill - before;
+        before += out->lane_total[l];
+    }
+    AccColumns a{};
+    a.in_cnt_star = cs;
+    a.in_cnt_val = cv;
+    a.in_sum = sum;
+    a.key = h->acc_key.as<int64_t>();
+    a.cnt_star = h->acc_cs.as<int64_t>();
+    a.cnt_null = h->acc_cn.as<int64_t>();
+    a.sum = h->acc_sum.as<int64_t>();
+    {
+        KTimer kt(h, K_SCATTER, n);
+        HIPCHK(h, launch_acc_scatter(p, a, h->stream));
+    }
+    s->has_null = false;
+    s->is_acc = true;
+    s->refs = 0;
+    for (int l = 0; l < h->lanes; l++) {
+        if (out->lane_total[l] == 0) continue;
+        Lane& ln = h->lane[l];
+        s->lane_start[l] = ln.acc_fill;
+        s->lane_n[l] = out->lane_total[l];
+        s->refs++;
+        ln.q = out->lane_min[l];
+        ln.acc_fill += out->lane_total[l];
+        ln.passes.push_back(s.get());
+    }
+    if (s->refs > 0) h->passes.push_back(std::move(s));
+    else h->pass_pool.push_back(std::move(s));
+    return FG_OK;
+}
+
 int validate(const fg_config* c, std::string* msg) {
     char buf[512];
     buf[0] = 0;
@@ -990,8 +1151,21 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         g_open_error = "null config";
         return FG_EINVAL;
     }
+    fg_config c = *cfg;
+    const bool local = (c.flags & FG_FLAG_LOCAL_PARTIALS) != 0;
+    if (local) {
+        // the local phase emits the accumulator layout COUNT(*), COUNT(v), SUM
+        if (c.val_type == FG_VAL_NONE || c.mode != FG_MODE_SQL) {
+            g_open_error = "FG_FLAG_LOCAL_PARTIALS needs an SQL operator with a value column";
+            return FG_EINVAL;
+        }
+        c.num_aggs = 3;
+        c.aggs[0] = FG_AGG_COUNT_STAR;
+        c.aggs[1] = FG_AGG_COUNT;
+        c.aggs[2] = FG_AGG_SUM;
+    }
     std::string msg;
-    int rc = validate(cfg, &msg);
+    int rc = validate(&c, &msg);
     if (rc) {
         g_open_error = msg;
         return rc;
@@ -1006,7 +1180,8 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         return FG_EINVAL;
     }
     std::unique_ptr<fg_handle> h(new fg_handle());
-    h->cfg = *cfg;
+    h->cfg = c;
+    h->local = local;
     h->device = cfg->device_id;
     h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
     if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1126,6 +1301,56 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     return FG_OK;
 }
 
+int fg_add_partials(fg_handle* h, const fg_partials* b) {
+    if (!h || !b) return FG_EINVAL;
+    if (b->n <= 0) return FG_OK;
+    if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
+    if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 rows");
+    if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
+        return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int64_t n = b->n;
+    const int64_t *key = b->key, *se = b->slice_end, *cs = b->cnt_star, *cv = b->cnt_val, *sum = b->sum;
+    if (b->location == FG_HOST) {
+        DevBuf* bufs[5] = {&h->in_key, &h->in_slice, &h->in_cs, &h->in_cv, &h->in_sum};
+        const int64_t* src[5] = {key, se, cs, cv, sum};
+        for (int i = 0; i < 5; i++) {
+            HIPCHK(h, bufs[i]->ensure(8 * n));
+            HIPCHK(h, hipMemcpyAsync(bufs[i]->p, src[i], 8 * n, hipMemcpyHostToDevice, h->stream));
+        }
+        key = h->in_key.as<int64_t>();
+        se = h->in_slice.as<int64_t>();
+        cs = h->in_cs.as<int64_t>();
+        cv = h->in_cv.as<int64_t>();
+        sum = h->in_sum.as<int64_t>();
+    }
+    HIPCHK(h, h->in_ts.ensure(8 * n));
+    int64_t* ts = h->in_ts.as<int64_t>();
+    HIPCHK(h, launch_pseudo_rowtime(se, n, h->w.tz, ts, h->stream));
+    h->records_in += n;
+    int rc0 = seed_anchor(h, ts, nullptr);
+    if (rc0) return rc0;
+    Counters c{};
+    int rc = acc_pass(h, n, key, ts, cs, cv, sum, JMIN, JMAX, true, &c);
+    h->late_dropped += (int64_t)c.drops;
+    if (rc == FG_OK) return FG_OK;
+    if (rc != -1) return rc;
+    const int64_t qlo = c.qmin, qhi = c.qmax;
+    rc = flush(h);
+    if (rc) return rc;
+    for (int64_t lo = qlo; lo <= qhi; lo += h->lanes) {
+        Counters c2{};
+        rc = acc_pass(h, n, key, ts, cs, cv, sum, lo, lo + h->lanes, false, &c2);
+        if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
+        if (rc) return rc;
+        if (lo + h->lanes <= qhi) {
+            rc = flush(h);
+            if (rc) return rc;
+        }
+    }
+    return FG_OK;
+}
+
 int fg_flush(fg_handle* h) {
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
@@ -1142,7 +1367,26 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     const int64_t prev = h->timer_wm;
     const FireRange fr{prev, wm};
     const FireRange* fuse = wm > prev ? &fr : nullptr;
-    if (h->cfg.mode == FG_MODE_SQL) {
+    if (h->local) {
+        // LocalSlicingWindowAggOperator.processWatermark (:113-139): once the watermark fires
+        // the smallest buffered slice, the combiner emits partial accumulators; here every
+        // fired slice lane emits its partials, and slices flushed earlier to make room are
+        // emitted from their tables
+        if (wm > h->current_progress) h->current_progress = wm;
+        if (staged_any(h) && is_window_fired(h->w, min_staged_slice_end(h), wm)) {
+            const FireRange all{JMIN, wm};
+            rc = flush(h, &all, true);
+            if (rc) return rc;
+        }
+        std::vector<int64_t> ends;
+        for (auto& kv : h->tables)
+            if (is_window_fired(h->w, kv.first, wm)) ends.push_back(kv.first);
+        for (int64_t e : ends) {
+            rc = fire_one(h, e, {h->tables[e].get()}, nullptr);
+            if (rc) return rc;
+            table_free(h, e);
+        }
+    } else if (h->cfg.mode == FG_MODE_SQL) {
         // AbstractWindowAggProcessor.advanceProgress :178-192
         if (wm > h->current_progress) {
             h->current_progress = wm;
@@ -1162,7 +1406,7 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
             if (rc) return rc;
         }
     }
-    if (wm > prev) {
+    if (wm > prev && !h->local) {
         rc = fire_windows(h, prev, wm);
         if (rc) return rc;
     }

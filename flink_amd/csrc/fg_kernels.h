@@ -131,6 +131,17 @@ struct MergeParams {
     unsigned int* overflow;    // bit0: region overflow, bit1: output overflow, bit2: LDS table full
 };
 
+// Accumulator rows of the global phase: input columns and the SoA staged area (all lanes)
+struct AccColumns {
+    const int64_t* in_cnt_star;
+    const int64_t* in_cnt_val;
+    const int64_t* in_sum;
+    int64_t* key;
+    int64_t* cnt_star;
+    int64_t* cnt_null;
+    int64_t* sum;
+};
+
 struct ExportParams {
     TableRef t;
     const uint64_t* region_off;  // [P] exclusive prefix of counts
@@ -143,6 +154,9 @@ struct ExportParams {
 };
 
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s);
+// global phase: rowtime = slice_end - 1 - tz for partial rows; scatter of accumulator rows
+hipError_t launch_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out, hipStream_t s);
+hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStream_t s);
 // two-pass partition: pass 1 does the count pass's work (drops, slice range, lane totals,
 // fine histogram per workgroup) while sorting tiles by coarse bucket into p.tmp / p.dir
 hipError_t launch_part1(const IngestParams& p, hipStream_t s);

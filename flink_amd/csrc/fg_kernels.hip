@@ -761,6 +761,57 @@ hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------------
+// global phase: partial accumulators (LocalAggCombiner rows) -> per-lane accumulator areas
+// ----------------------------------------------------------------------------------------
+// A partial row of slice `slice_end` is classified like a record with rowtime
+// slice_end - 1 - tz (the `sliced` assigner: assignSliceEnd = the row's window end,
+// SliceAssigners.java:494-533), so the late rules of the global operator apply unchanged.
+__global__ void k_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = slice_end[i];
+        out[i] = e == JMAX ? JMAX : jsub(jsub(e, 1), tz);
+    }
+}
+
+hipError_t launch_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out, hipStream_t s) {
+    int64_t blocks = (n + 255) / 256;
+    blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
+    hipLaunchKernelGGL(k_pseudo_rowtime, dim3((unsigned)blocks), dim3(256), 0, s, slice_end, n, tz, out);
+    return hipGetLastError();
+}
+
+// Direct scatter of accumulator rows (key, COUNT(*), NULL count, sum) into the SoA areas
+// at their bucket cursors (the count pass's histogram, k_hist_columns, scan).
+__global__ __launch_bounds__(kIngestThreads) void k_acc_scatter(IngestParams p, AccColumns a) {
+    __shared__ uint32_t s_cur[kMaxStageBuckets];
+    const int F = p.lanes << p.region_bits;
+    const int tid = threadIdx.x;
+    for (int b = tid; b < F; b += kIngestThreads)
+        s_cur[b] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)blockIdx.x * F + b] +
+                              p.lane_shift[b >> p.region_bits]);
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    for (int64_t i = beg + tid; i < end; i += kIngestThreads) {
+        const int64_t k = p.key[i];
+        int64_t q;
+        const int b = classify(p, k, p.ts[i], &q);
+        if (b < 0) continue;
+        const uint32_t pos = atomicAdd(&s_cur[b], 1u);
+        const int64_t cs = a.in_cnt_star[i];
+        a.key[pos] = k;
+        a.cnt_star[pos] = cs;
+        a.cnt_null[pos] = cs - a.in_cnt_val[i];
+        a.sum[pos] = a.in_sum[i];
+    }
+}
+
+hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_acc_scatter, dim3(p.grid), dim3(kIngestThreads), 0, s, p, a);
+    return hipGetLastError();
+}
+
 // per bucket: exclusive prefix over workgroups (column of the workgroup-major histogram)
 __global__ __launch_bounds__(256) void k_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid) {
     const int b = blockIdx.x * 256 + threadIdx.x;

@@ -78,11 +78,19 @@ class WindowAggOperator:
     def __init__(self, window: Window, aggs=("count_star", "count", "sum", "avg"), val_type: str = "f64",
                  mode: str = "sql", shift_tz_offset_ms: int = 0, expected_keys: int = 1 << 16,
                  buffer_records: int = 1 << 22, device: int = 0, max_parallelism: int = 128,
-                 key_group_range=(0, 127), kernel_timing: bool = False):
+                 key_group_range=(0, 127), kernel_timing: bool = False, local_partials: bool = False):
+        """local_partials: the local phase of the two-phase aggregation
+        (LocalSlicingWindowAggOperator + LocalAggCombiner): process_watermark returns one
+        partial accumulator row per (key, fired slice) with columns count_star, count, sum
+        (window_start/window_end = the slice), to be exchanged by key group and merged by a
+        global operator's process_partials."""
         lib = L.load()
         self.window = window
         self.mode = {"sql": L.MODE_SQL, "datastream": L.MODE_DATASTREAM}[mode]
         self.val_type = {"none": L.VAL_NONE, "i64": L.VAL_I64, "f64": L.VAL_F64}[val_type]
+        self.local_partials = bool(local_partials)
+        if self.local_partials:
+            aggs = ("count_star", "count", "sum")
         self.aggs = tuple(AGGS[a] if isinstance(a, str) else int(a) for a in aggs)
         cfg = L.FgConfig()
         cfg.mode = self.mode
@@ -98,7 +106,7 @@ class WindowAggOperator:
         cfg.max_parallelism = int(max_parallelism)
         cfg.key_group_start, cfg.key_group_end = int(key_group_range[0]), int(key_group_range[1])
         cfg.device_id = int(device)
-        cfg.flags = L.FLAG_KERNEL_TIMING if kernel_timing else 0
+        cfg.flags = (L.FLAG_KERNEL_TIMING if kernel_timing else 0) | (L.FLAG_LOCAL_PARTIALS if local_partials else 0)
         cfg.expected_keys = int(expected_keys)
         cfg.buffer_records = int(buffer_records)
         self.cfg = cfg
@@ -153,6 +161,34 @@ class WindowAggOperator:
                 b.val_null = val_null.ctypes.data
             keep = [key, rowtime, val, val_null]
         L.check(self._lib.fg_add_batch(self._h, C.byref(b)), self._h)
+        del keep
+
+    # -- global phase ----------------------------------------------------------------------------
+    def process_partials(self, key, slice_end, cnt_star, cnt_val, sum_bits):
+        """GlobalAggCombiner.combine for partial accumulator rows (after the exchange): numpy
+        arrays or device tensors; `sum_bits` holds i64 sums or the bits of f64 sums."""
+        cols = [key, slice_end, cnt_star, cnt_val, sum_bits]
+        ptrs = [_dev_ptr(c) for c in cols]
+        b = L.FgPartials()
+        keep = []
+        if ptrs[0][1]:
+            assert all(p[1] for p in ptrs), "mixed host/device columns"
+            b.location = L.DEVICE
+            x = ptrs[0][2]
+            b.n = int(x.numel() if hasattr(x, "numel") else x.shape[0])
+            b.key, b.slice_end, b.cnt_star, b.cnt_val, b.sum = (p[0] for p in ptrs)
+        else:
+            arrs = []
+            for c in cols:
+                a = np.asarray(c)
+                if a.dtype == np.float64:
+                    a = a.view(np.int64)
+                arrs.append(np.ascontiguousarray(a, dtype=np.int64))
+            b.location = L.HOST
+            b.n = len(arrs[0])
+            b.key, b.slice_end, b.cnt_star, b.cnt_val, b.sum = (a.ctypes.data for a in arrs)
+            keep = arrs
+        L.check(self._lib.fg_add_partials(self._h, C.byref(b)), self._h)
         del keep
 
     # -- processWatermark ---------------------------------------------------------------------

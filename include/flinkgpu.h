@@ -24,6 +24,8 @@
  *     SJ/api/operators/StreamOperatorStateHandler.java:185-241
  *   AbstractStreamOperator.initializeState (keyed state restore)         fg_restore
  *   SlicingWindowOperator.getNumLateRecordsDropped :300-303            fg_late_dropped
+ *   two-phase: LocalAggCombiner.combine (local operator output)        fg_config.flags |= FG_FLAG_LOCAL_PARTIALS
+ *     GlobalAggCombiner.combine  .../combines/GlobalAggCombiner.java:77-110  fg_add_partials
  *   WindowBuffer.close / SlicingWindowOperator.close :178-183           fg_close
  *   DataStream WindowOperator.processElement / processWatermark / onEventTime
  *     SJ/runtime/operators/windowing/WindowOperator.java:300-503          same entry points,
@@ -54,7 +56,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 1
+#define FG_ABI_VERSION 2
 
 enum fg_status {
     FG_OK = 0,
@@ -73,7 +75,17 @@ enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
 enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3 };
 enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
 enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1 };
-enum fg_flags { FG_FLAG_KERNEL_TIMING = 1 };   /* HIP-event timing of every launch (fg_kernel_stats) */
+enum fg_flags {
+    FG_FLAG_KERNEL_TIMING = 1,    /* HIP-event timing of every launch (fg_kernel_stats) */
+    /* Local phase of the two-phase window aggregation (LocalSlicingWindowAggOperator +
+     * LocalAggCombiner, TR/operators/aggregate/window/LocalSlicingWindowAggOperator.java:113-139,
+     * combines/LocalAggCombiner.java:69-106): records are assigned to their own slice with no
+     * late handling, and fg_advance_progress emits, for every slice the watermark fires, one
+     * partial accumulator row per key instead of window rows: window_start/window_end = the
+     * slice, agg[0] = COUNT(*), agg[1] = COUNT(v), agg[2] = SUM bits (0 when COUNT(v) = 0).
+     * fg_config.aggs is ignored (the global operator's list applies). */
+    FG_FLAG_LOCAL_PARTIALS = 2
+};
 
 #define FG_MAX_AGGS 8
 
@@ -118,6 +130,21 @@ typedef struct fg_rows {
     const int64_t* rowtime;            /* DataStream: window.maxTimestamp() (end - 1); SQL: NULL */
 } fg_rows;
 
+/* Partial accumulator rows entering the global phase (GlobalAggCombiner.combine,
+ * combines/GlobalAggCombiner.java:77-110, fed through the `sliced` assigner,
+ * SliceAssigners.java:494-533): the rows of a FG_FLAG_LOCAL_PARTIALS operator after the
+ * key-group exchange. */
+typedef struct fg_partials {
+    int64_t n;
+    int32_t location;             /* fg_location of the column pointers */
+    int32_t reserved0;
+    const int64_t* key;
+    const int64_t* slice_end;     /* the partial's slice (window_end of the local row) */
+    const int64_t* cnt_star;
+    const int64_t* cnt_val;
+    const int64_t* sum;           /* i64 or f64 bits per fg_config.val_type */
+} fg_partials;
+
 /* Checkpoint image of the GPU-resident keyed state: one entry per (key, slice) accumulator,
  * the content of WindowValueState "window-aggs" (AbstractWindowAggProcessor.java:103-109). */
 typedef struct fg_state_rows {
@@ -154,6 +181,9 @@ typedef struct fg_handle fg_handle;
 
 int  fg_open(const fg_config* cfg, fg_handle** out);
 int  fg_add_batch(fg_handle* h, const fg_batch* batch);
+/* Global phase: merge partial accumulators (late rules of the global operator apply to
+ * the partial's slice). */
+int  fg_add_partials(fg_handle* h, const fg_partials* partials);
 int  fg_advance_progress(fg_handle* h, int64_t watermark, int32_t out_location, fg_rows* fired);
 int  fg_flush(fg_handle* h);
 int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);

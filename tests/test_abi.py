@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 1
+    assert lib.fg_abi_version() == 2
 
 
 def test_struct_layouts_match_header_sizes():
@@ -36,6 +36,8 @@ def test_struct_layouts_match_header_sizes():
     assert C.sizeof(L.FgConfig) == 8 + 32 + 8 + 32 + 24 + 16
     assert C.sizeof(L.FgBatch) == 8 + 8 + 4 * 8
     assert C.sizeof(L.FgRows) == 8 + 8 + 3 * 8 + 8 * 8 + 2 * 8
+    assert C.sizeof(L.FgPartials) == 8 + 8 + 5 * 8
+    assert C.sizeof(L.FgStateRows) == 8 + 5 * 8
 
 
 AS = load_assigner_cases()
@@ -50,6 +52,13 @@ def test_window_spec_errors_match_reference(case):
     with pytest.raises(F.WindowSpecError) as ei:
         F.WindowAggOperator(w, aggs=aggs, val_type="i64")
     assert str(ei.value) == case["message"]
+
+
+def test_local_phase_needs_value_column():
+    """FG_FLAG_LOCAL_PARTIALS is validated before any device call."""
+    import flink_amd as F
+    with pytest.raises(F.WindowSpecError):
+        F.WindowAggOperator(F.tumbling(1000), val_type="none", local_partials=True)
 
 
 def test_no_device_is_loud():

@@ -276,3 +276,68 @@ def test_conservation_large(oracle_mod):
     accepted = float(val.sum())   # late-dropped values excluded below via the oracle's count
     assert abs(tot_sum - accepted) <= 1e-6 * accepted or late > 0
     op.close()
+
+
+TWO_PHASE_CASES = [
+    ("tumble_f64_regions", cfg_of("tumble", 1000), dict(n=600_000, keys=120_000, batch=60_000, delay=0, jitter=0)),
+    ("tumble_i64_ooo_late", cfg_of("tumble", 300, vt="i64"), dict(n=300_000, keys=20_000, batch=20_000, delay=100, jitter=600)),
+    ("hop_f64_late", cfg_of("hop", 3000, 1000), dict(n=300_000, keys=30_000, batch=20_000, delay=200, jitter=1500)),
+    ("cumulate_i64_late", cfg_of("cumulate", 4000, 500, vt="i64"), dict(n=300_000, keys=30_000, batch=15_000, delay=50, jitter=2500)),
+]
+
+
+@pytest.mark.parametrize("name,cfg,kw", TWO_PHASE_CASES, ids=[c[0] for c in TWO_PHASE_CASES])
+def test_two_phase_parity(oracle_mod, name, cfg, kw):
+    """LocalAggCombiner -> key-group exchange -> GlobalAggCombiner: 3 source partitions with a
+    local operator each, partial rows routed to 2 owners by KeyGroupRangeAssignment, global
+    operators fire; the union of their rows equals the single-phase oracle over the whole
+    stream (the exchange itself is tested under gloo in test_distributed.py). Late drops are
+    counted per partial row in the global phase, as in the reference, so only rows compare."""
+    import flink_amd as F
+    from tests.gpu_adapter import window_of
+    S, R, MAXP = 3, 2, 128
+    n, keys, batch, delay, jitter = kw["n"], kw["keys"], kw["batch"], kw["delay"], kw["jitter"]
+    key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter)
+    w = window_of(cfg)
+    aggs = ("count_star", "count", "sum", "avg")
+    local = [F.WindowAggOperator(w, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
+                                 local_partials=True) for _ in range(S)]
+    glob = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys // R + 1,
+                                buffer_records=1 << 18) for _ in range(R)]
+    o = oracle_mk(oracle_mod, cfg)
+    src = np.arange(n) % S
+
+    def route(rows_list):
+        rows = np.concatenate(rows_list)
+        if len(rows) == 0:
+            return
+        owner = F.key_groups(rows["key"], MAXP).astype(np.int64) * R // MAXP
+        sums = rows["sum"].view(np.int64) if rows["sum"].dtype == np.float64 else rows["sum"]
+        for r in range(R):
+            m = owner == r
+            glob[r].process_partials(rows["key"][m], rows["window_end"][m], rows["count_star"][m],
+                                     rows["count"][m], sums[m])
+
+    got, exp = [], []
+    for lo, hi, wm in batches_with_watermarks(n, batch, ts, delay):
+        for s in range(S):
+            m = src[lo:hi] == s
+            local[s].process_batch(key[lo:hi][m], ts[lo:hi][m], val[lo:hi][m])
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        route([local[s].process_watermark(wm) for s in range(S)])
+        got += [g.process_watermark(wm) for g in glob]
+        o.process_watermark(wm)
+        exp.append(o.take_rows())
+    route([local[s].process_watermark(JMAX) for s in range(S)])
+    got += [g.process_watermark(JMAX) for g in glob]
+    o.process_watermark(JMAX)
+    exp.append(o.take_rows())
+    g = np.concatenate([x for x in got if len(x)])
+    from tests.gpu_adapter import GpuOperator
+    adapter = GpuOperator.__new__(GpuOperator)
+    adapter.cfg = cfg
+    adapter._rows = [g]
+    assert_rows_equal(adapter.take_rows(), np.concatenate(exp), cfg["val_type"], name)
+    for x in local + glob:
+        x.close()
+    o.close()
