@@ -11,8 +11,13 @@ One step = the whole 1B-record job: reset the operator, feed the resident column
 then the final watermark fires the last window. Inputs (key i64, val f64, rowtime i64;
 24 GB) are generated on the GPU and resident in HBM before timing; fired rows stay in
 HBM (device output).  N > 1 (torchrun): every rank owns key groups
-kg*N/128 and a 1B-record source partition; each micro-batch is routed to its key-group
-owner by an RCCL all-to-all (flink_amd.exchange) before ingest -> weak scaling.
+kg*N/128 and a 1B-record source partition (weak scaling) and runs the two-phase plan of
+TwoStageOptimizedWindowAggregateRule: a local operator (LocalAggCombiner) aggregates its
+source partition per (key, slice); at each micro-batch's watermark the fired slices'
+partial accumulators are routed to their key-group owners by one RCCL all-to-all
+(flink_amd.exchange.exchange_partials) and merged by the owner's global operator
+(GlobalAggCombiner), which fires the windows. `--exchange raw` ships the records
+themselves instead (one all-to-all per micro-batch before a single-phase operator).
 
 Roofline: HBM. Algorithmic bytes: 24 B per input record + 48 B per fired
 row. `roofline` is for the dominant kernel, timed with HIP events on the engine's
@@ -141,20 +146,30 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
+    ap.add_argument("--exchange", choices=("partials", "raw"), default="partials",
+                    help="N > 1: exchange partial accumulators (two-phase) or raw records")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("BENCH_DEVICE", local))   # rehearsal: every rank on one device
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
+    # BENCH_DIST_BACKEND=gloo rehearses N > 1 on one device (collectives staged through
+    # host memory); the driver's multi-GPU runs use RCCL ("nccl")
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    via_cpu = backend == "gloo"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if via_cpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     import flink_amd as F
-    from flink_amd.exchange import exchange, global_watermark
+    from flink_amd.exchange import device_columns, exchange, exchange_partials, global_watermark
 
     rate_ms = args.rate // 1000
     n = args.records
@@ -163,38 +178,72 @@ def main():
 
     maxp = 128
     kg_lo, kg_hi = (rank * maxp + world - 1) // world, ((rank + 1) * maxp - 1) // world
+    two_phase = world > 1 and args.exchange == "partials"
     op = F.WindowAggOperator(F.tumbling(1000), aggs=("count_star", "sum", "avg"), val_type="f64",
                              expected_keys=int(args.keys / world * 1.05) + 1,
-                             buffer_records=max(4 * args.batch, 1 << 26), device=local,
-                             key_group_range=(kg_lo, kg_hi), kernel_timing=True)
+                             buffer_records=max(4 * args.batch, 1 << 26) if not two_phase else 1 << 24,
+                             device=local, key_group_range=(kg_lo, kg_hi), kernel_timing=True)
+    # two-phase: the local operator sees every key of its source partition
+    op_local = F.WindowAggOperator(F.tumbling(1000), val_type="f64", expected_keys=int(args.keys * 1.05) + 1,
+                                   buffer_records=max(4 * args.batch, 1 << 26), device=local,
+                                   kernel_timing=True, local_partials=True) if two_phase else None
+
+    def partials_round(wm):
+        """local fire -> exchange of partial accumulators -> global merge + fire"""
+        r = op_local.process_watermark(wm, device_output=True)
+        cols = device_columns(r, device=dev)
+        recv, sent = exchange_partials(cols, max_parallelism=maxp, via_cpu=via_cpu)
+        torch.cuda.current_stream().synchronize()
+        op.process_partials(*recv)
+        g = op.process_watermark(global_watermark(wm, device=dev), device_output=True)
+        return g.n, sent
 
     def one_step():
         op.reset()
+        if op_local:
+            op_local.reset()
         rows = 0
         xgmi = 0
         for lo in range(0, n, args.batch):
             hi = min(n, lo + args.batch)
             k, t, v = key[lo:hi], ts[lo:hi], val[lo:hi]
+            wms = watermarks_for(lo, hi, rate_ms, args.wm_every)
+            if two_phase:
+                op_local.process_batch(k, t, v)
+                if wms:   # the micro-batch's last watermark (in-order input: same output)
+                    nr, sent = partials_round(wms[-1])
+                    rows += nr
+                    xgmi += sent
+                continue
             if world > 1:
                 k, t, v, sent = exchange(k, t, v.view(torch.int64), max_parallelism=maxp)
                 v = v.view(torch.float64)
                 xgmi += sent
                 torch.cuda.current_stream().synchronize()
             op.process_batch(k, t, v)
-            wms = watermarks_for(lo, hi, rate_ms, args.wm_every)
             if world > 1 and wms:
                 wms[-1] = global_watermark(wms[-1], device=dev)
             for wm in wms:
                 r = op.process_watermark(wm, device_output=True)
                 rows += r.n
+        if two_phase:
+            nr, sent = partials_round(JMAX)
+            return rows + nr, xgmi + sent
         r = op.process_watermark(JMAX, device_output=True)
         rows += r.n
         return rows, xgmi
 
+    def kstats():
+        ks = op.kernel_stats()
+        if op_local:   # local-phase kernels under their own names
+            for name, d in op_local.kernel_stats().items():
+                ks["local_" + name] = d
+        return ks
+
     for _ in range(args.warmup):
         one_step()
     op.synchronize()
-    before = op.kernel_stats()
+    before = kstats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -210,7 +259,7 @@ def main():
     if dist:
         dist.barrier()
     el = time.perf_counter() - t0
-    after = op.kernel_stats()
+    after = kstats()
     late = op.num_late_records_dropped
     if dist:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
@@ -235,7 +284,7 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(dom_name, {}).get("hbm_bytes_per_launch")
+            traffic = json.load(open(pmc)).get(dom_name.replace("local_", ""), {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -260,7 +309,9 @@ def main():
                         "10M uniform keys (BASELINE configs[1])",
             "records_per_gpu": n, "keys": args.keys, "records_per_event_second": args.rate,
             "micro_batch": args.batch, "watermark_every": args.wm_every,
-            "parallelism": f"key-group sharded x{world}" + (" + RCCL all-to-all" if world > 1 else ""),
+            "parallelism": f"key-group sharded x{world}" + (
+                (" + RCCL all-to-all of partial accumulators (two-phase)" if two_phase else
+                 " + RCCL all-to-all of records") if world > 1 else ""),
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom_name,
@@ -279,6 +330,8 @@ def main():
         except Exception as e:  # reported, not fatal
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     op.close()
+    if op_local:
+        op_local.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

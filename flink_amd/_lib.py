@@ -82,7 +82,8 @@ FLAG_LOCAL_PARTIALS = 2
 EXPORTS = (
     "fg_open", "fg_add_batch", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
     "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_stream",
-    "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_abi_version",
+    "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
+    "fg_abi_version",
 )
 
 _lib = None
@@ -135,10 +136,12 @@ def load():
     L.fg_key_groups.argtypes = [C.c_int32, C.c_int32, C.c_int64, P, C.c_int32, C.c_int32, P]
     L.fg_partition_by_owner.argtypes = [C.c_int32, P, C.c_int64, P, P, P, C.c_int32, C.c_int32, C.c_int32,
                                         P, P, P, P]
+    L.fg_partition_columns_by_owner.argtypes = [C.c_int32, P, C.c_int64, C.c_int32, P, C.c_int32, C.c_int32,
+                                                C.c_int32, P, P]
     L.fg_abi_version.restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
                "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
-               "fg_partition_by_owner"):
+               "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int
     _lib = L
     return L

@@ -1706,6 +1706,29 @@ int fg_key_groups(int32_t device_id, int32_t location, int64_t n, const int64_t*
     return rc;
 }
 
+int fg_partition_columns_by_owner(int32_t device_id, void* stream, int64_t n, int32_t ncols, const int64_t* const* cols,
+                                  int32_t key_hash, int32_t max_parallelism, int32_t parallelism, int64_t* const* out_cols,
+                                  int64_t* counts) {
+    if (n < 0 || n > (int64_t)0x7fffffff || parallelism < 1 || max_parallelism < parallelism || ncols < 1 ||
+        ncols > kMaxOwnerCols || !cols || !out_cols || !counts)
+        return FG_EINVAL;
+    if (hipSetDevice(device_id) != hipSuccess) return FG_EDEVICE;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    OwnerCols c{};
+    c.ncols = ncols;
+    for (int j = 0; j < ncols; j++) {
+        c.in[j] = cols[j];
+        c.out[j] = out_cols[j];
+    }
+    const size_t words = partition_scratch_words(n, parallelism);
+    uint32_t* scratch = nullptr;
+    if (hipMallocAsync((void**)&scratch, 4 * words, s) != hipSuccess) return FG_EDEVICE;
+    hipError_t e = launch_partition_cols_by_owner(c, n, key_hash, max_parallelism, parallelism, counts, scratch, words, s);
+    (void)hipFreeAsync(scratch, s);
+    if (e != hipSuccess) return FG_EDEVICE;
+    return hipStreamSynchronize(s) == hipSuccess ? FG_OK : FG_EDEVICE;
+}
+
 int fg_partition_by_owner(int32_t device_id, void* stream, int64_t n, const int64_t* key, const int64_t* rowtime,
                           const int64_t* val, int32_t key_hash, int32_t max_parallelism, int32_t parallelism,
                           int64_t* out_key, int64_t* out_rowtime, int64_t* out_val, int64_t* counts) {

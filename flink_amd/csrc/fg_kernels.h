@@ -174,6 +174,15 @@ hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int3
 // regions (p.compact: two workgroups fit a CU)
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
+constexpr int kMaxOwnerCols = 8;
+struct OwnerCols {
+    int32_t ncols;
+    const int64_t* in[kMaxOwnerCols];   // in[0] = key
+    int64_t* out[kMaxOwnerCols];
+};
+hipError_t launch_partition_cols_by_owner(const OwnerCols& c, int64_t n, int32_t key_hash, int32_t max_p,
+                                          int32_t par, int64_t* counts, uint32_t* scratch, size_t scratch_words,
+                                          hipStream_t s);
 hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, int32_t max_p, int32_t* out,
                              hipStream_t s);
 hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n,

@@ -1409,9 +1409,46 @@ __global__ __launch_bounds__(kOwnerThreads) void k_owner_scatter(const int64_t* 
     }
 }
 
+// generic form for the partial-accumulator exchange: up to kMaxOwnerCols int64 columns
+// (key first) moved together by destination subtask
+__global__ __launch_bounds__(kOwnerThreads) void k_owner_scatter_cols(OwnerCols c, int64_t n, int32_t key_hash,
+                                                                       int32_t max_p, int32_t par,
+                                                                       const uint32_t* offsets) {
+    __shared__ uint32_t s[kMaxOwners];
+    for (int i = threadIdx.x; i < par; i += kOwnerThreads) s[i] = offsets[(int64_t)i * kOwnerGrid + blockIdx.x];
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(n, kOwnerGrid, blockIdx.x, &beg, &end);
+    for (int64_t i = beg + threadIdx.x; i < end; i += kOwnerThreads) {
+        const int64_t k = c.in[0][i];
+        const uint32_t pos = atomicAdd(&s[owner_of(k, key_hash, max_p, par)], 1u);
+        for (int j = 0; j < c.ncols; j++) c.out[j][pos] = c.in[j][i];
+    }
+}
+
 __global__ void k_owner_counts(const uint32_t* offsets, int32_t par, int64_t* counts) {
     const int i = threadIdx.x;
     if (i < par) counts[i] = (int64_t)offsets[(int64_t)(i + 1) * kOwnerGrid] - (int64_t)offsets[(int64_t)i * kOwnerGrid];
+}
+
+hipError_t launch_partition_cols_by_owner(const OwnerCols& c, int64_t n, int32_t key_hash, int32_t max_p,
+                                          int32_t par, int64_t* counts, uint32_t* scratch, size_t scratch_words,
+                                          hipStream_t s) {
+    if (par < 1 || par > kMaxOwners || c.ncols < 1 || c.ncols > kMaxOwnerCols ||
+        scratch_words < partition_scratch_words(n, par))
+        return hipErrorInvalidValue;
+    const int64_t m = (int64_t)par * kOwnerGrid;
+    uint32_t* hist = scratch;
+    uint32_t* offs = scratch + m;
+    uint32_t* tmp = scratch + 2 * m + 1;
+    hipLaunchKernelGGL(k_owner_count, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, c.in[0], n, key_hash, max_p, par,
+                       hist);
+    hipError_t e = launch_scan_u32(hist, offs, m, tmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_owner_scatter_cols, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, c, n, key_hash, max_p, par,
+                       offs);
+    hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
+    return hipGetLastError();
 }
 
 size_t partition_scratch_words(int64_t n, int32_t par) {

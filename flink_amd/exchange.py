@@ -8,6 +8,11 @@ subtasks: every rank packs its source partition by owner subtask
 (fg_partition_by_owner), then one RCCL all-to-all over xGMI delivers each owner its
 records. The watermark is combined with an all-reduce(min), as StatusWatermarkValve
 takes the minimum over input channels.
+
+Two-phase form (TwoStageOptimizedWindowAggregateRule.java:81-104): what crosses the
+exchange is the local phase's partial accumulator rows (LocalAggCombiner output: key,
+slice_end, COUNT(*), COUNT(v), SUM) instead of raw records -- at most one row per (key,
+slice) per source instead of one per record (exchange_partials).
 """
 from __future__ import annotations
 
@@ -72,11 +77,79 @@ def exchange_partitioned(ok, ot, ov, counts, group=None):
     return rk, rt, rv, sent_bytes
 
 
+class _DeviceColumn:
+    """Zero-copy view of an engine-owned device column (int64[n]) for torch.as_tensor."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (int(ptr or 0), False),
+                                         "version": 2}
+
+
+def device_columns(rows, names=("key", "window_end"), aggs=(0, 1, 2), device=None):
+    """int64 tensor views of an FgRows returned with device_output=True (valid until the
+    next call on the operator)."""
+    n = int(rows.n)
+    out = [torch.as_tensor(_DeviceColumn(getattr(rows, nm), n), device=device) for nm in names]
+    out += [torch.as_tensor(_DeviceColumn(rows.agg[a], n), device=device) for a in aggs]
+    return out
+
+
+def partition_columns_by_owner(cols, parallelism: int, max_parallelism: int = 128,
+                               key_hash: int = L.KEYHASH_BINARYROW_BIGINT, stream=None):
+    """Reorder int64 device columns (cols[0] = key) by destination subtask.
+    Returns (reordered columns, counts[parallelism])."""
+    lib = L.load()
+    n = cols[0].numel()
+    dev = cols[0].device
+    outs = [torch.empty_like(c) for c in cols]
+    counts = torch.empty(parallelism, dtype=torch.int64, device=dev)
+    if n == 0:
+        counts.zero_()
+        return outs, counts
+    k = len(cols)
+    ins = (C.c_void_p * k)(*[c.data_ptr() for c in cols])
+    ous = (C.c_void_p * k)(*[o.data_ptr() for o in outs])
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.fg_partition_columns_by_owner(dev.index or 0, C.c_void_p(s), n, k, ins, key_hash, max_parallelism,
+                                              parallelism, ous, counts.data_ptr()))
+    return outs, counts
+
+
+def exchange_partials(cols, group=None, max_parallelism: int = 128, key_hash: int = L.KEYHASH_BINARYROW_BIGINT,
+                      via_cpu: bool = False):
+    """Key-group exchange of partial accumulator rows (int64 device columns, key first).
+    Returns the received columns and the bytes this rank sent to peers. via_cpu stages the
+    collective through host memory (gloo; for rehearsing N > 1 on one device)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    outs, counts = partition_columns_by_owner(cols, world, max_parallelism, key_hash)
+    if world == 1:
+        return outs, 0
+    dev = cols[0].device
+    packed = torch.stack(outs, dim=1).contiguous() if outs[0].numel() else torch.empty((0, len(cols)),
+                                                                                       dtype=torch.int64, device=dev)
+    if via_cpu:
+        packed, counts = packed.cpu(), counts.cpu()
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    send = counts.cpu().tolist()
+    recv = recv_counts.cpu().tolist()
+    out = torch.empty((sum(recv), len(cols)), dtype=packed.dtype, device=packed.device)
+    dist.all_to_all_single(out, packed, output_split_sizes=recv, input_split_sizes=send, group=group)
+    if via_cpu:
+        out = out.to(dev)
+    rank = dist.get_rank(group)
+    sent_bytes = 8 * len(cols) * (sum(send) - send[rank])
+    return [out[:, j].contiguous() for j in range(len(cols))], sent_bytes
+
+
 def global_watermark(local_wm: int, group=None, device=None) -> int:
     """min over subtasks (StatusWatermarkValve)."""
     import torch.distributed as dist
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return int(local_wm)
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"
     t = torch.tensor([int(local_wm)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return int(t.item())

@@ -215,6 +215,13 @@ int  fg_partition_by_owner(int32_t device_id, void* stream, int64_t n, const int
                            int32_t max_parallelism, int32_t parallelism, int64_t* out_key,
                            int64_t* out_rowtime, int64_t* out_val, int64_t* counts);
 
+/* The same for `ncols` int64 columns moved together (cols[0] = the key), e.g. the partial
+ * accumulator rows (key, slice_end, cnt_star, cnt_val, sum) of the two-phase exchange.
+ * ncols <= 8. Device pointers only. */
+int  fg_partition_columns_by_owner(int32_t device_id, void* stream, int64_t n, int32_t ncols,
+                                   const int64_t* const* cols, int32_t key_hash, int32_t max_parallelism,
+                                   int32_t parallelism, int64_t* const* out_cols, int64_t* counts);
+
 int  fg_abi_version(void);
 
 #ifdef __cplusplus
