@@ -501,10 +501,30 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         if (fire_now) fill_emit(h, p, se);
         p.overflow = h->scalars.as<unsigned int>();
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+#ifdef FG_STAMPS
+        static DevBuf d_st;
+        if (getenv("FG_STAMPS")) {
+            HIPCHK(h, d_st.ensure(64));
+            HIPCHK(h, hipMemsetAsync(d_st.p, 0, 64, h->stream));
+            p.stamps = d_st.as<unsigned long long>();
+        }
+#endif
         {
             KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
             HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
         }
+#ifdef FG_STAMPS
+        if (p.stamps) {
+            unsigned long long st[4];
+            HIPCHK(h, hipMemcpyAsync(st, d_st.p, 32, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            const int waves = (p.compact ? std::min(h->P, 2 * h->merge_grid) * kCompactMergeThreads
+                                         : merge_grid(h) * kMergeThreads) / 64;
+            fprintf(stderr, "[fg stamps] merge %s P=%d records=%lld: clear %.0f stream %.0f compact %.0f emit %.0f (cycles/wave)\n",
+                    p.compact ? "compact" : "wide", h->P, (long long)ln.fill, (double)st[0] / waves,
+                    (double)st[1] / waves, (double)st[2] / waves, (double)st[3] / waves);
+        }
+#endif
         if (fire_now) {
             fired_tables.push_back(se);
             any_emit = true;

@@ -129,6 +129,7 @@ struct MergeParams {
     unsigned long long* out_count;
     int64_t out_cap;
     unsigned int* overflow;    // bit0: region overflow, bit1: output overflow, bit2: LDS table full
+    unsigned long long* stamps;  // diagnostic builds only (FG_STAMPS): per-phase cycles summed over waves
 };
 
 // Accumulator rows of the global phase: input columns and the SoA staged area (all lanes)

@@ -605,6 +605,10 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     __shared__ uint32_t s_fsrc[kPart2MaxFrags];        // tmp position of each fragment
     __shared__ uint32_t s_cnt[NF], s_off[NF + 1], s_cur[NF];
     __shared__ uint32_t s_wave[kPart2Threads / 64];
+    // u16 fragment of each record of the sub-tile being loaded (4 KiB): aliases s_rec, which
+    // is free from the end of one sub-tile's write-out to the staging of the next
+    uint4* s_map4 = reinterpret_cast<uint4*>(s_rec);
+    uint16_t* s_map = reinterpret_cast<uint16_t*>(s_rec);
     const int tid = threadIdx.x;
     const int P = 1 << p.region_bits;
     const int F = p.lanes << p.region_bits;
@@ -626,7 +630,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     const int c = lane * cpl + cl;
     // fragment q = (workgroup g0 + q / MT, tile q % MT); missing tiles are empty fragments
     const int nfr = (g1 - g0) * MT;
-    uint32_t len[FPT];
+    uint32_t len[FPT], fst[FPT];
     uint32_t local = 0;
 #pragma unroll
     for (int k = 0; k < FPT; k++) {
@@ -649,6 +653,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     for (int k = 0; k < FPT; k++) {
         const int q = tid * FPT + k;
         if (q < nfr) s_fstart[q] = run;
+        fst[k] = run;
         run += len[k];
     }
     if (tid < NF) {
@@ -660,7 +665,40 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     const bool has_null = p.vnull != nullptr;
     const bool aos = p.st_stride == 2;
     // records of a sub-tile: idx = base + u * T + tid; the next sub-tile's loads are issued
-    // before this one is ranked, staged and written
+    // before this one is ranked, staged and written. The fragment of each idx comes from a
+    // per-sub-tile map: every fragment marks its first record in the sub-tile, and an
+    // inclusive max-scan fills the map forward (fragment numbers grow with idx).
+    auto build_map = [&](uint32_t base) {
+        s_map4[tid] = make_uint4(0u, 0u, 0u, 0u);
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < FPT; k++) {
+            const int q = tid * FPT + k;
+            if (q < nfr && len[k] > 0 && fst[k] < base + kPart2Tile && fst[k] + len[k] > base)
+                s_map[fst[k] > base ? fst[k] - base : 0u] = (uint16_t)q;
+        }
+        lds_barrier();
+        const uint4 w = s_map4[tid];
+        uint32_t e[8] = {w.x & 0xffffu, w.x >> 16, w.y & 0xffffu, w.y >> 16,
+                         w.z & 0xffffu, w.z >> 16, w.w & 0xffffu, w.w >> 16};
+#pragma unroll
+        for (int j = 1; j < 8; j++) e[j] = e[j] > e[j - 1] ? e[j] : e[j - 1];
+        uint32_t x = e[7];
+        const int ln = tid & 63;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (ln >= off) x = x > y ? x : y;
+        }
+        if (ln == 63) s_wave[tid >> 6] = x;
+        uint32_t pre = __shfl_up(x, 1);
+        if (ln == 0) pre = 0;
+        lds_barrier();
+        for (int wv = 0; wv < (tid >> 6); wv++) pre = pre > s_wave[wv] ? pre : s_wave[wv];
+#pragma unroll
+        for (int j = 0; j < 8; j++) e[j] = e[j] > pre ? e[j] : pre;
+        s_map4[tid] = make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
+        lds_barrier();
+    };
     longlong2 rr[R];
     uint8_t rn[R];
     auto load = [&](uint32_t base) {
@@ -669,18 +707,17 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             const uint32_t idx = base + (uint32_t)(u * kPart2Threads + tid);
             rn[u] = 0;
             if (idx >= total) continue;
-            int lo = 0, hi = nfr;   // fragment: last q with s_fstart[q] <= idx (never an empty one)
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (s_fstart[mid] <= idx) lo = mid;
-                else hi = mid;
-            }
-            const uint32_t src = s_fsrc[lo] + (idx - s_fstart[lo]);
+            const int q = s_map[idx - base];
+            const uint32_t src = s_fsrc[q] + (idx - s_fstart[q]);
             rr[u] = p.tmp[src];
             if (has_null) rn[u] = p.tmp_null[src];
         }
     };
-    if (total > 0) load(0);
+    if (total > 0) {
+        build_map(0);
+        load(0);
+        lds_barrier();   // every wave has read the map before build_map(kPart2Tile) clears it
+    }
     for (uint32_t base = 0; base < total; base += kPart2Tile) {
         longlong2 cr[R];
         uint8_t cn[R];
@@ -689,7 +726,10 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             cr[u] = rr[u];
             cn[u] = rn[u];
         }
-        if (base + kPart2Tile < total) load(base + kPart2Tile);
+        if (base + kPart2Tile < total) {
+            build_map(base + kPart2Tile);
+            load(base + kPart2Tile);
+        }
         uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
 #pragma unroll
         for (int u = 0; u < R; u++) {
@@ -926,49 +966,64 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
 // one 1,024-thread workgroup per CU) for every merge. Compact: 3,584 slots of {key, sum,
 // COUNT(*) u32} (70 KiB, two 512-thread workgroups per CU) for the common fire/flush of
 // plain staged records (no NULLs, no resident state, < 2^32 records).
+//
+// staged-stream chunk of the compact merge: 16-B loads per thread (overridable for experiments)
+#ifndef FG_MERGE_U
+#define FG_MERGE_U 3
+#endif
+#ifndef FG_DIAG_MERGE
+#define FG_DIAG_MERGE 0    // diagnostic builds only (wrong results): bit0 no adds, bit1 no probe loop, bit2 no emit
+#endif
+
 template <bool C>
 struct MergeCfg;
 template <>
 struct MergeCfg<false> {
     static constexpr int kSlotsT = kSlots;
     static constexpr int kThreads = kMergeThreads;
+    static constexpr int kU = 2;      // 1,024 threads: 128 VGPRs
 };
 template <>
 struct MergeCfg<true> {
     static constexpr int kSlotsT = kCompactSlots;
     static constexpr int kThreads = kCompactMergeThreads;
+    static constexpr int kU = FG_MERGE_U;
 };
 
 template <bool C>
 struct LdsTableT;
 template <>
 struct LdsTableT<false> {
-    int64_t key[kSlots + 1];                  // slot kSlots: the key equal to the sentinel
+    alignas(16) int64_t key[kSlots + 1];      // slot kSlots: the key equal to the sentinel
     unsigned long long cs[kSlots + 1];        // COUNT(*)
     unsigned long long cn[kSlots + 1];        // records whose value was NULL
     unsigned long long sum[kSlots + 1];       // SUM / AVG sum (i64, or f64 bits)
 };
 template <>
 struct LdsTableT<true> {
-    int64_t key[kCompactSlots + 1];
+    alignas(16) int64_t key[kCompactSlots + 1];
     unsigned long long sum[kCompactSlots + 1];
     uint32_t cs[kCompactSlots + 1];
 };
 
-// home slot: a multiplicative hash of the key (the region already selects keys by the top
-// bits of fmix64, independent of these bits), scaled to the table size
+// Home bucket: a multiplicative hash of the key (the region already selects keys by the top
+// bits of fmix64, independent of these bits) picks an aligned bucket of kBucket slots, read
+// with one 32-byte LDS access; probing is linear, slot by slot, from the bucket's first slot.
+// At the regions' load factor (<= ~0.35) a key sits in its home bucket ~99 % of the time,
+// against ~84 % for a single home slot, so a wave's lanes rarely leave the fast path.
+constexpr int kBucket = 4;
 template <bool C>
 __device__ __forceinline__ uint32_t lds_home(int64_t k) {
+    constexpr uint32_t NB = (uint32_t)(MergeCfg<C>::kSlotsT / kBucket);
     const uint64_t m = (uint64_t)k * 0x9E3779B97F4A7C15ull;
-    if constexpr (C) return (uint32_t)(((m >> 32) * (uint64_t)kCompactSlots) >> 32);
-    else return (uint32_t)(m >> (64 - kSlotBits));
+    return (uint32_t)(((m >> 32) * (uint64_t)NB) >> 32) * kBucket;
 }
 
+// linear probe from `slot` (keys never leave the table during a region, so a key is at the
+// first slot from its home that was empty or held it when it was inserted)
 template <bool C>
-__device__ __forceinline__ int lds_find_or_insert(LdsTableT<C>& t, int64_t k, bool& full) {
+__device__ __forceinline__ int lds_find_or_insert_from(LdsTableT<C>& t, int64_t k, uint32_t slot, bool& full) {
     constexpr int S = MergeCfg<C>::kSlotsT;
-    if (k == JMIN) return S;
-    uint32_t slot = lds_home<C>(k);
     for (int probe = 0; probe < S; probe++) {
         const int64_t cur = t.key[slot];
         if (cur == k) return (int)slot;
@@ -981,6 +1036,12 @@ __device__ __forceinline__ int lds_find_or_insert(LdsTableT<C>& t, int64_t k, bo
     }
     full = true;
     return -1;
+}
+
+template <bool C>
+__device__ __forceinline__ int lds_find_or_insert(LdsTableT<C>& t, int64_t k, bool& full) {
+    if (k == JMIN) return MergeCfg<C>::kSlotsT;
+    return lds_find_or_insert_from<C>(t, k, lds_home<C>(k), full);
 }
 
 template <bool C>
@@ -999,7 +1060,14 @@ __device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long
     }
 }
 
-constexpr int kMergeU = 4;                                // 16-B staged loads per thread per chunk (x2 buffers)
+typedef long long RecV2 __attribute__((ext_vector_type(2)));
+typedef const RecV2 __attribute__((address_space(1)))* GlobalRec;
+// a pointer that was itself loaded from memory is generic (flat) to the compiler: view it in
+// the global address space so its loads are global_load (see `load` below)
+template <class T>
+__device__ __forceinline__ const T __attribute__((address_space(1)))* gbl(const T* q) {
+    return (const T __attribute__((address_space(1)))*)q;
+}
 
 // Pipelined staged stream (every batch plain {key, value} AoS, <= kMaxMergeBatches): the
 // workgroup walks its regions r0, r0 + G, ... as one stream of chunks (chunks never span
@@ -1015,11 +1083,13 @@ struct MergeCursor {
 };
 
 template <bool C>
-__global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) {
+// waves_per_eu(4): 128 VGPRs, so two compact workgroups (16 waves) fit a CU
+__global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_merge(MergeParams p) {
     constexpr int S = MergeCfg<C>::kSlotsT;
     constexpr int T = MergeCfg<C>::kThreads;
     constexpr int kWaves = T / 64;
     constexpr int kRounds = (S + T - 1) / T + 1;    // + 1: the sentinel slot (thread 0)
+    constexpr int kMergeU = MergeCfg<C>::kU;
     constexpr uint32_t kChunk = kMergeU * T;
     __shared__ LdsTableT<C> t;
     __shared__ uint32_t s_grp[kRounds * kWaves];   // per (round, wave) row counts -> offsets
@@ -1041,7 +1111,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
     // fast path state
     auto range_of = [&](int ri, int j, uint32_t& beg, uint32_t& end) {
         const int r = (int)blockIdx.x + ri * G;
-        const uint32_t* bo = p.batches[j].bucket_off;
+        const auto bo = gbl(p.batches[j].bucket_off);
         const uint32_t b0 = bo[0];
         beg = bo[r] - b0;
         end = bo[r + 1] - b0;
@@ -1066,34 +1136,96 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
     };
     longlong2 ca[kMergeU], cb[kMergeU];
     auto load = [&](longlong2 (&c)[kMergeU], const MergeCursor& m) {
-        const longlong2* rec = s_brec[m.j];
+        // the base comes back from LDS: cast to the global address space so these are
+        // global_load_dwordx4 (a flat load is waited for with vmcnt(0) AND lgkmcnt(0),
+        // serializing every LDS probe behind the loads in flight)
+        const GlobalRec rec = (GlobalRec)s_brec[m.j];
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             const uint32_t i = m.i0 + u * T + tid;
-            c[u] = rec[i < m.end ? i : m.end - 1];
+            const RecV2 v = rec[i < m.end ? i : m.end - 1];
+            c[u] = make_longlong2(v.x, v.y);
         }
     };
-    // the home-slot probes of the chunk's records are issued together; a record whose key
-    // sits in its home slot (every repeat of a key, at this load factor) is added at once,
-    // the others continue probing from the slot after home
+    // The home buckets of the chunk's records are read together. A record whose key is in
+    // its bucket (every repeat of a key, nearly always) is added at once; a new key claims
+    // the bucket's first empty slot with one CAS; only a full bucket or a lost CAS probes on.
     auto insert = [&](const longlong2 (&c)[kMergeU], const MergeCursor& m, bool& full) {
         uint32_t home[kMergeU];
-        int64_t cur0[kMergeU];
+        RecV2 b01[kMergeU], b23[kMergeU];
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             home[u] = lds_home<C>(c[u].x);
-            cur0[u] = t.key[home[u]];
+            const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
+            b01[u] = kb[0];
+            b23[u] = kb[1];
         }
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             if (m.i0 + u * T + tid >= m.end) continue;
+            const int64_t k = c[u].x;
+            const int64_t q[kBucket] = {b01[u].x, b01[u].y, b23[u].x, b23[u].y};
+            int hit = -1, empty = -1;
+#pragma unroll
+            for (int j = kBucket - 1; j >= 0; j--) {   // the first match / first empty slot
+                if (q[j] == k) hit = j;
+                if (q[j] == JMIN) empty = j;
+            }
+            constexpr uint32_t S_ = (uint32_t)MergeCfg<C>::kSlotsT;
             int slot;
-            if (cur0[u] == c[u].x && c[u].x != JMIN) slot = (int)home[u];
-            else slot = lds_find_or_insert<C>(t, c[u].x, full);
-            if (slot >= 0) lds_add<C>(t, slot, 1ull, 0ull, c[u].y, vt);
+            if (FG_DIAG_MERGE & 2) {
+                slot = (int)home[u] + (hit >= 0 ? hit : 0);
+                if (q[0] == JMIN) t.key[slot] = k;
+            } else if (k == JMIN) {
+                slot = (int)S_;
+            } else if (hit >= 0 && (empty < 0 || hit < empty)) {
+                slot = (int)home[u] + hit;
+            } else if (empty >= 0) {   // claim the first empty slot; a lost CAS probes on
+                const uint32_t e = home[u] + (uint32_t)empty;
+                const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&t.key[e]),
+                                                         (unsigned long long)JMIN, (unsigned long long)k);
+                if (old == (unsigned long long)JMIN || old == (unsigned long long)k) slot = (int)e;
+                else slot = lds_find_or_insert_from<C>(t, k, e + 1 >= S_ ? 0u : e + 1, full);
+            } else {                   // full bucket: probe on from the next one
+                const uint32_t nx = home[u] + kBucket;
+                slot = lds_find_or_insert_from<C>(t, k, nx >= S_ ? 0u : nx, full);
+            }
+            if (!(FG_DIAG_MERGE & 1) && slot >= 0) lds_add<C>(t, slot, 1ull, 0ull, c[u].y, vt);
+            if ((FG_DIAG_MERGE & 1) && slot >= 0) t.cs[slot] = 1;
         }
     };
-    MergeCursor cur{nreg, 0, 0, 0};
+#ifdef FG_STAMPS
+    // diagnostic build only: cycles per phase, summed over this workgroup's regions
+    unsigned long long st_acc[4] = {0, 0, 0, 0};
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define MSTAMP(i)                                                     \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        st_acc[i] += now_ - st_prev;                                  \
+        st_prev = now_;                                               \
+    } while (0)
+#else
+#define MSTAMP(i) \
+    do {          \
+    } while (0)
+#endif
+    // one chunk in flight while the current one is inserted. The buffer roles are static
+    // (the loop is unrolled by two): selecting a buffer at run time made the compiler copy
+    // registers, waiting for the loads in flight. At a region's end the next region's first
+    // chunk is in flight in buffer `nbuf`.
+    MergeCursor cur{nreg, 0, 0, 0, false};
+    int nbuf = 0;
+    auto step = [&](const longlong2 (&in)[kMergeU], longlong2 (&next)[kMergeU], int ri, bool& full) -> bool {
+        MergeCursor nx = cur;
+        nx.i0 += kChunk;
+        settle(nx, ri + 1);
+        // issued unconditionally (a dummy reload of this chunk past the stream's end): the
+        // counter-based wait before the inserts must know these loads are the newest
+        load(next, nx.ok ? nx : cur);
+        insert(in, cur, full);
+        cur = nx;
+        return cur.ri == ri && cur.ok;
+    };
     if (fast) {
         if (tid < nb) s_brec[tid] = reinterpret_cast<const longlong2*>(p.batches[tid].rec);
         for (int q = tid; q < 2 * nb; q += T) {   // ranges of regions 0 and 1
@@ -1124,11 +1256,12 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
         lds_barrier();
         bool full = false;
 
+        MSTAMP(0);   // clear + barrier
         // 1) resident slice regions (state) ------------------------------------------
         for (int j = 0; !C && j < p.n_src; j++) {
             const TableRef src = p.src[j];
-            const uint32_t n = src.counts[r];
-            const int64_t* base = src.base + (int64_t)r * 4 * cap;
+            const uint32_t n = gbl(src.counts)[r];
+            const auto base = gbl(src.base + (int64_t)r * 4 * cap);
             for (uint32_t i0 = 0; i0 < n; i0 += 4 * T) {
                 int64_t k[4], cs[4], cn[4], sm[4];
 #pragma unroll
@@ -1152,65 +1285,62 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
         }
         // 2) staged records of region r over the lane's staged batches ------------------
         if (fast) {
-            // double-buffered: the next chunk's loads are issued before this chunk's inserts;
-            // the chunk in flight at the region's end is the next region's first
             if (cur.ri == ri && !cur.ok) {   // walked past empty regions: settle now (cold load)
                 cur.j = 0;
                 cur.i0 = s_rng[ri % 3][0][0];
                 settle(cur, ri + 1);
+                nbuf = 0;
                 if (cur.ok && cur.ri == ri) load(ca, cur);
             }
-            bool in_a = true;
-            while (cur.ri == ri && cur.ok) {
-                MergeCursor nx = cur;
-                nx.i0 += kChunk;
-                settle(nx, ri + 1);
-                if (in_a) {
-                    if (nx.ok) load(cb, nx);
-                    insert(ca, cur, full);
-                } else {
-                    if (nx.ok) load(ca, nx);
-                    insert(cb, cur, full);
-                }
-                in_a = !in_a;
-                cur = nx;
+            bool go = cur.ri == ri && cur.ok;
+            if (go && nbuf == 1) {
+                go = step(cb, ca, ri, full);
+                nbuf = 0;
             }
-            if (!in_a) {   // the next region's first chunk sits in cb
-#pragma unroll
-                for (int u = 0; u < kMergeU; u++) ca[u] = cb[u];
+            while (go) {
+                go = step(ca, cb, ri, full);
+                if (!go) {
+                    nbuf = 1;
+                    break;
+                }
+                go = step(cb, ca, ri, full);
             }
         } else if constexpr (!C) {
             for (int j = 0; j < nb; j++) {
                 const StagedBatch sb = p.batches[j];
-                const uint32_t b0 = sb.bucket_off[0];
-                const uint32_t beg = sb.bucket_off[r] - b0;
-                const uint32_t end = sb.bucket_off[r + 1] - b0;
+                const auto bo = gbl(sb.bucket_off);
+                const uint32_t b0 = bo[0];
+                const uint32_t beg = bo[r] - b0;
+                const uint32_t end = bo[r + 1] - b0;
+                const auto srec = gbl(sb.rec);
+                const auto vnull = sb.vnull != nullptr ? gbl(sb.vnull) : nullptr;
                 if (sb.is_acc) {
+                    const auto cst = gbl(sb.cnt_star), cnl = gbl(sb.cnt_null), sval = gbl(sb.val);
                     for (uint32_t i = beg + tid; i < end; i += T) {
-                        const int slot = lds_find_or_insert<C>(t, sb.rec[i], full);
+                        const int slot = lds_find_or_insert<C>(t, srec[i], full);
                         if (slot >= 0)
-                            lds_add<C>(t, slot, (unsigned long long)sb.cnt_star[i], (unsigned long long)sb.cnt_null[i],
-                                    sb.val[i], vt);
+                            lds_add<C>(t, slot, (unsigned long long)cst[i], (unsigned long long)cnl[i], sval[i], vt);
                     }
                 } else if (sb.stride == 2) {
-                    const longlong2* rec = reinterpret_cast<const longlong2*>(sb.rec);
+                    const GlobalRec rec = (GlobalRec)sb.rec;
                     for (uint32_t i = beg + tid; i < end; i += T) {
-                        const longlong2 rc = rec[i];
+                        const RecV2 rc = rec[i];
                         const int slot = lds_find_or_insert<C>(t, rc.x, full);
                         if (slot < 0) continue;
-                        const bool isnull = sb.vnull != nullptr && sb.vnull[i] != 0;
+                        const bool isnull = vnull != nullptr && vnull[i] != 0;
                         lds_add<C>(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
                     }
                 } else {
                     for (uint32_t i = beg + tid; i < end; i += T) {
-                        const int slot = lds_find_or_insert<C>(t, sb.rec[i], full);
+                        const int slot = lds_find_or_insert<C>(t, srec[i], full);
                         if (slot < 0) continue;
-                        const bool isnull = sb.vnull != nullptr && sb.vnull[i];
+                        const bool isnull = vnull != nullptr && vnull[i];
                         lds_add<C>(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
                     }
                 }
             }
         }
+        MSTAMP(1);   // staged stream (this wave's share)
         if (full) atomicOr(&s_flags, 4u);
         if (fast && tid < nb && ri + 2 < nreg) {
             s_rng[(ri + 2) % 3][tid][0] = nbeg;
@@ -1258,9 +1388,10 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
             }
         }
         lds_barrier();
+        MSTAMP(2);   // compaction + scan + barriers
         const unsigned int fl = s_flags;
         const bool write_dst = p.has_dst && !(fl & 1u) && !(fl & 4u);
-        const bool write_out = p.emit && !(fl & 2u) && !(fl & 4u);
+        const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 2u) && !(fl & 4u);
         int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
         const unsigned long long obase = s_out_base;
         // per round: the wave's occupied lanes below this lane give the rank within the group
@@ -1318,7 +1449,12 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) void k_merge(MergeParams p) 
             if (p.dst_total) atomicAdd(p.dst_total, (unsigned long long)((int64_t)total - (int64_t)old));
         }
         lds_barrier();   // the table is cleared for the next region
+        MSTAMP(3);   // emit + barrier
     }
+#ifdef FG_STAMPS
+    if (p.stamps && (tid & 63) == 0)
+        for (int i = 0; i < 4; i++) atomicAdd(&p.stamps[i], st_acc[i]);
+#endif
 }
 
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {

@@ -120,6 +120,13 @@ STREAM_CASES = [
     ("regions_cumulate_i64_late", cfg_of("cumulate", 4000, 500, vt="i64"), dict(n=500_000, keys=100_000, batch=20_000, delay=50, jitter=2500)),
     ("regions_ds_sliding", cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), dict(n=400_000, keys=100_000, batch=30_000, delay=100, jitter=1500)),
     ("regions_spread_keys", cfg_of("tumble", 1000), dict(n=500_000, keys=200_000, batch=50_000, delay=50, jitter=300, key_spread=True)),
+    # micro-batches of millions of records: pass-2 units span many sub-tiles, merge regions
+    # stream many chunks
+    ("big_units_f64", cfg_of("tumble", 1000), dict(n=40_000_000, keys=4_000_000, batch=20_000_000, delay=0, jitter=0,
+                                                    rate_per_ms=20_000)),
+    ("big_units_i64_nulls_ooo", cfg_of("tumble", 1000, vt="i64"), dict(n=16_000_000, keys=500_000, batch=8_000_000,
+                                                                       delay=600, jitter=500, null_frac=0.1,
+                                                                       rate_per_ms=10_000)),
 ]
 
 
