@@ -61,29 +61,71 @@ def splitmix64(x: torch.Tensor) -> torch.Tensor:
     return z ^ lsr(z, 31)
 
 
-def gen_columns(n, keys, rate, base_index, device, chunk=1 << 26):
-    """key = u % keys, val = uniform [0, 1000) f64, rowtime = T0 + i // rate (tests/streams.py)."""
+# BASELINE configs by workload: window, key space, event-time rate, order
+WORKLOADS = {
+    # configs[1] (the bench's `value`): SQL TUMBLE 1s COUNT(*)/SUM/AVG(double)
+    "tumble": dict(window=("tumbling", 1000), keys=10_000_000, rate=100_000_000, jitter=0, delay=0, zipf=0.0,
+                   desc="SQL TUMBLE 1s COUNT(*)/SUM/AVG(double) via SlicingWindowOperator, 1B records per GPU, "
+                        "10M uniform keys (BASELINE configs[1])"),
+    # configs[2]: SQL HOP 5min/1min, rowtime over 30 event-minutes
+    "hop": dict(window=("hopping", 300_000, 60_000), keys=10_000_000, rate=1_000_000_000 // 1800, jitter=0, delay=0,
+                zipf=0.0, batch=25_000_000, desc="SQL HOP 5min/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 30 event-minutes, "
+                               "10M uniform keys (BASELINE configs[2])"),
+    # configs[3]: CUMULATE 1h/1min over 60 event-minutes; 100M keys sharded over 8 GPUs ->
+    # the per-GPU share (12.5M) at N = 1, the whole 100M space at N = 8
+    "cumulate": dict(window=("cumulative", 3_600_000, 60_000), keys=12_500_000, rate=1_000_000_000 // 3600,
+                     jitter=0, delay=0, zipf=0.0, batch=12_500_000,
+                     desc="SQL CUMULATE 1h/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 60 event-minutes, "
+                          "uniform keys: 12.5M per GPU = the per-GPU key-group share of 100M (BASELINE configs[3])"),
+    # configs[4]: TUMBLE 1s AVG(double), Zipf s = 1.1 keys, 2 s jitter, bounded out-of-orderness 2 s
+    "zipf": dict(window=("tumbling", 1000), keys=10_000_000, rate=100_000_000, jitter=2000, delay=2000, zipf=1.1,
+                 desc="SQL TUMBLE 1s AVG(double), 1B records per GPU, 10M Zipf(1.1) keys, rowtime jitter U[0,2s), "
+                      "watermark = max rowtime - 2s - 1 (BASELINE configs[4])"),
+}
+
+
+def zipf_cdf(keys, s, device):
+    """CDF of Zipf(s) over ranks 1..keys (float64, on the device)."""
+    r = torch.arange(1, keys + 1, dtype=torch.float64, device=device)
+    w = r.pow(-s)
+    c = torch.cumsum(w, 0)
+    return c / c[-1]
+
+
+def gen_columns(n, keys, rate_s, base_index, device, chunk=1 << 26, jitter=0, zipf=0.0):
+    """key = u % keys (or Zipf(zipf) rank - 1 by inverse CDF), val = uniform [0, 1000) f64,
+    rowtime = T0 + i * 1000 // rate_s (+ U[0, jitter) ms) (tests/streams.py)."""
     key = torch.empty(n, dtype=torch.int64, device=device)
     ts = torch.empty(n, dtype=torch.int64, device=device)
     val = torch.empty(n, dtype=torch.float64, device=device)
+    cdf = zipf_cdf(keys, zipf, device) if zipf > 0 else None
     for lo in range(0, n, chunk):
         hi = min(n, lo + chunk)
         i = torch.arange(base_index + lo, base_index + hi, dtype=torch.int64, device=device)
         u = splitmix64(i ^ SEED)
         u2 = splitmix64(i ^ (SEED * 3 + 1))
-        key[lo:hi] = (lsr(u, 1) % keys * 2 + (u & 1)) % keys        # unsigned u % keys
+        if cdf is not None:
+            q = lsr(u, 11).to(torch.float64) * (1.0 / float(1 << 53))
+            key[lo:hi] = torch.searchsorted(cdf, q).clamp_(max=keys - 1)
+            del q
+        else:
+            key[lo:hi] = (lsr(u, 1) % keys * 2 + (u & 1)) % keys        # unsigned u % keys
         val[lo:hi] = lsr(u2, 11).to(torch.float64) * (1000.0 / float(1 << 53))
-        ts[lo:hi] = T0 + (i - base_index) // rate
+        ts[lo:hi] = T0 + (i - base_index) * 1000 // rate_s
+        if jitter:
+            ts[lo:hi] += lsr(u2, 1) % jitter
         del i, u, u2
     return key, ts, val
 
 
-def watermarks_for(lo, hi, rate, every):
-    """1M-cadence watermarks (max rowtime - 1) delivered after records [lo, hi)."""
+def watermarks_for(lo, hi, rate_s, every, delay=0, jitter=0):
+    """1M-cadence watermarks delivered after records [lo, hi): max rowtime - delay - 1
+    (in order: max rowtime = T0 + (j - 1) * 1000 // rate_s; with jitter, a bound of the max)."""
     out = []
     j = (lo // every + 1) * every
     while j <= hi:
-        out.append(T0 + (j - 1) // rate - 1)
+        mx = T0 + (j - 1) * 1000 // rate_s + (jitter - 1 if jitter else 0)
+        out.append(mx - delay - 1)
         j += every
     return out
 
@@ -139,9 +181,13 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--records", type=int, default=1_000_000_000, help="records per GPU per step")
-    ap.add_argument("--keys", type=int, default=10_000_000)
-    ap.add_argument("--rate", type=int, default=100_000_000, help="records per event-second")
-    ap.add_argument("--batch", type=int, default=50_000_000)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="tumble",
+                    help="BASELINE config; `tumble` (configs[1]) is the bench's headline value")
+    ap.add_argument("--keys", type=int, default=None, help="key space (default: the workload's)")
+    ap.add_argument("--rate", type=int, default=None, help="records per event-second (default: the workload's)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="micro-batch records (default 50M; hop 25M and cumulate 12.5M so that a micro-batch "
+                         "spans at most two 1-minute slices, the staged lanes of a 10M-key operator)")
     ap.add_argument("--wm-every", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -149,6 +195,15 @@ def main():
     ap.add_argument("--exchange", choices=("partials", "raw"), default="partials",
                     help="N > 1: exchange partial accumulators (two-phase) or raw records")
     args = ap.parse_args()
+    wl = WORKLOADS[args.workload]
+    if args.keys is None:
+        args.keys = wl["keys"]
+    if args.rate is None:
+        args.rate = wl["rate"]
+    if args.batch is None:
+        args.batch = wl.get("batch", 50_000_000)
+    if args.workload != "tumble":
+        args.no_cpu_baseline = True   # the CPU baseline is quoted on configs[1]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -171,20 +226,22 @@ def main():
     import flink_amd as F
     from flink_amd.exchange import device_columns, exchange, exchange_partials, global_watermark
 
-    rate_ms = args.rate // 1000
     n = args.records
-    key, ts, val = gen_columns(n, args.keys, rate_ms, rank * n, dev)
+    key, ts, val = gen_columns(n, args.keys, args.rate, rank * n, dev, jitter=wl["jitter"], zipf=wl["zipf"])
     torch.cuda.synchronize()
 
     maxp = 128
     kg_lo, kg_hi = (rank * maxp + world - 1) // world, ((rank + 1) * maxp - 1) // world
     two_phase = world > 1 and args.exchange == "partials"
-    op = F.WindowAggOperator(F.tumbling(1000), aggs=("count_star", "sum", "avg"), val_type="f64",
+    wname, *wargs = wl["window"]
+    window = getattr(F, wname)(*wargs)
+    aggs = ("avg",) if args.workload == "zipf" else ("count_star", "sum", "avg")
+    op = F.WindowAggOperator(window, aggs=aggs, val_type="f64",
                              expected_keys=int(args.keys / world * 1.05) + 1,
                              buffer_records=max(4 * args.batch, 1 << 26) if not two_phase else 1 << 24,
                              device=local, key_group_range=(kg_lo, kg_hi), kernel_timing=True)
     # two-phase: the local operator sees every key of its source partition
-    op_local = F.WindowAggOperator(F.tumbling(1000), val_type="f64", expected_keys=int(args.keys * 1.05) + 1,
+    op_local = F.WindowAggOperator(window, val_type="f64", expected_keys=int(args.keys * 1.05) + 1,
                                    buffer_records=max(4 * args.batch, 1 << 26), device=local,
                                    kernel_timing=True, local_partials=True) if two_phase else None
 
@@ -207,7 +264,7 @@ def main():
         for lo in range(0, n, args.batch):
             hi = min(n, lo + args.batch)
             k, t, v = key[lo:hi], ts[lo:hi], val[lo:hi]
-            wms = watermarks_for(lo, hi, rate_ms, args.wm_every)
+            wms = watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"])
             if two_phase:
                 op_local.process_batch(k, t, v)
                 if wms:   # the micro-batch's last watermark (in-order input: same output)
@@ -305,8 +362,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic (counter-based splitmix64 stream generated on the GPU, resident in HBM)",
         "config": {
-            "workload": "SQL TUMBLE 1s COUNT(*)/SUM/AVG(double) via SlicingWindowOperator, 1B records per GPU, "
-                        "10M uniform keys (BASELINE configs[1])",
+            "workload": wl["desc"],
             "records_per_gpu": n, "keys": args.keys, "records_per_event_second": args.rate,
             "micro_batch": args.batch, "watermark_every": args.wm_every,
             "parallelism": f"key-group sharded x{world}" + (
@@ -326,7 +382,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(args, rate_ms)
+            result["cpu_baseline"] = cpu_baseline(args, args.rate // 1000)
         except Exception as e:  # reported, not fatal
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     op.close()

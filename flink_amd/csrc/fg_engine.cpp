@@ -99,6 +99,7 @@ struct Staged {
     int64_t lane_start[kMaxLanes] = {0, 0, 0, 0};
     int64_t lane_n[kMaxLanes] = {0, 0, 0, 0};
     bool has_null = false;
+    bool skew = false;    // some region may hold over kHeavyMin records of this pass (hot keys)
     int refs = 0;         // lanes still holding records of this pass
 };
 
@@ -118,6 +119,8 @@ struct DevCounters {     // device scratch words read back after the count pass
     unsigned long long lane_mask;
     long long qmin, qmax;
     unsigned long long lane_total[kMaxLanes];
+    unsigned int max_bucket;   // largest per-workgroup bucket count (skew hint)
+    unsigned int pad;
 };
 struct Counters {        // host view: per-lane slice index ranges (min > max: lane idle)
     unsigned long long drops;
@@ -125,13 +128,20 @@ struct Counters {        // host view: per-lane slice index ranges (min > max: l
     long long lane_min[kMaxLanes];
     long long lane_max[kMaxLanes];
     long long lane_total[kMaxLanes];
+    bool skew;
 };
 
+// skewed regions (hot keys): a region holding more than max(kHeavyMin, 8 x the mean) staged
+// records at merge time is merged in kHeavyChunk-record chunks (k_heavy_plan/_chunks +
+// the heavy pass), so that its work is spread over the GPU instead of one workgroup
+constexpr int64_t kHeavyMin = 1 << 16;
+constexpr int64_t kHeavyChunk = 1 << 16;
+
 enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_PART1, K_PART2, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE,
-              K_NCLASS };
+              K_HEAVY, K_NCLASS };
 const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan",      "ingest_scatter", "ingest_part1",
                                            "ingest_part2", "merge_flush",      "merge_flush_fire", "merge_fire",
-                                           "export",       "restore"};
+                                           "export",       "restore",          "merge_heavy"};
 struct KStat {
     int64_t launches = 0;
     double ms = 0;
@@ -177,6 +187,9 @@ struct fg_handle {
     // ingest scratch
     DevBuf in_key, in_ts, in_val, in_null;
     DevBuf part_tmp, part_tmp_null, part_dir;   // two-pass partition: pass-1 tiles + directory
+    // skewed-region plan and chunk partial tables
+    DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
+    int64_t hv_max_chunks = 0;
     DevBuf hist, totals, scan_tmp, counters;
     HostBuf h_counters;
 
@@ -421,6 +434,52 @@ void release_lane(fg_handle* h, int l) {
 
 int merge_grid(const fg_handle* h) { return std::min(h->P, h->merge_grid); }
 
+// Plan the skewed regions of one lane's merge (k_heavy_plan): regions over
+// max(kHeavyMin, 8 x mean) staged records, cut into kHeavyChunk-record chunks.
+int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, HeavyPlan* hp) {
+    const int64_t threshold = std::max<int64_t>(kHeavyMin, 8 * fill / h->P);
+    const int64_t max_chunks = fill / kHeavyChunk + fill / threshold + 2;
+    if (max_chunks > h->hv_max_chunks) {
+        const size_t e = (size_t)max_chunks * kPartStride;
+        HIPCHK(h, h->hv_clist.ensure(4 * (size_t)max_chunks));
+        HIPCHK(h, h->hv_v0.ensure(8 * (size_t)max_chunks));
+        HIPCHK(h, h->hv_v1.ensure(8 * (size_t)max_chunks));
+        HIPCHK(h, h->hv_pn.ensure(4 * (size_t)max_chunks));
+        HIPCHK(h, h->hv_key.ensure(8 * e));
+        HIPCHK(h, h->hv_cs.ensure(8 * e));
+        HIPCHK(h, h->hv_cn.ensure(8 * e));
+        HIPCHK(h, h->hv_sum.ensure(8 * e));
+        h->hv_max_chunks = max_chunks;
+    }
+    HIPCHK(h, h->hv_flags.ensure((size_t)h->P));
+    HIPCHK(h, h->hv_list.ensure(4 * (size_t)h->P));
+    HIPCHK(h, h->hv_chunk0.ensure(4 * ((size_t)h->P + 1)));
+    HIPCHK(h, h->hv_n.ensure(8));
+    hp->batches = d_sb;
+    hp->n_batches = nb;
+    hp->region_bits = h->region_bits;
+    hp->threshold = threshold;
+    hp->chunk = kHeavyChunk;
+    hp->max_chunks = (int32_t)std::min<int64_t>(h->hv_max_chunks, INT32_MAX);
+    hp->val_type = h->cfg.val_type;
+    hp->heavy = h->hv_flags.as<uint8_t>();
+    hp->region_list = h->hv_list.as<int32_t>();
+    hp->n_list = h->hv_n.as<int32_t>();
+    hp->chunk0 = h->hv_chunk0.as<int32_t>();
+    hp->chunk_list = h->hv_clist.as<int32_t>();
+    hp->chunk_v0 = h->hv_v0.as<int64_t>();
+    hp->chunk_v1 = h->hv_v1.as<int64_t>();
+    hp->part_key = h->hv_key.as<int64_t>();
+    hp->part_cs = h->hv_cs.as<int64_t>();
+    hp->part_cn = h->hv_cn.as<int64_t>();
+    hp->part_sum = h->hv_sum.as<int64_t>();
+    hp->part_n = h->hv_pn.as<uint32_t>();
+    hp->overflow = h->scalars.as<unsigned int>();
+    KTimer kt(h, K_HEAVY, 0);
+    HIPCHK(h, launch_heavy_plan(*hp, h->stream));
+    return FG_OK;
+}
+
 // RecordsWindowBuffer.flush (:108-119) + AggCombiner.combine (:76-115): merge staged slice
 // lanes into their slice tables -- every lane, or (only_fired) the lanes whose slice is
 // fired at the current progress, the only ones a window firing now can read; the others
@@ -509,9 +568,37 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
             p.stamps = d_st.as<unsigned long long>();
         }
 #endif
+        bool skew = false;
+        for (Staged* s : ln.passes) skew = skew || s->skew;
+        HeavyPlan hp{};
+        if (skew) {
+            rc = plan_heavy(h, d_sb, (int)sb.size(), ln.fill + ln.acc_fill, &hp);
+            if (rc) return rc;
+            p.heavy = hp.heavy;
+        }
         {
             KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
             HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
+        }
+        if (skew) {
+            // the heavy regions: chunk tables, then their merge with the region's state
+            KTimer kt(h, K_HEAVY, 0);
+            HIPCHK(h, launch_heavy_chunks(hp, h->merge_grid, h->stream));
+            MergeParams q = p;
+            q.compact = 0;
+            q.fast_stream = 0;
+            q.n_batches = 0;
+            q.batches = nullptr;
+            q.heavy = nullptr;
+            q.region_list = hp.region_list;
+            q.n_list = hp.n_list;
+            q.chunk0 = hp.chunk0;
+            q.part_key = hp.part_key;
+            q.part_cs = hp.part_cs;
+            q.part_cn = hp.part_cn;
+            q.part_sum = hp.part_sum;
+            q.part_n = hp.part_n;
+            HIPCHK(h, launch_merge(q, merge_grid(h), h->stream));
         }
 #ifdef FG_STAMPS
         if (p.stamps) {
@@ -841,6 +928,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.qmin = &dc->qmin;
     p.qmax = &dc->qmax;
     p.lane_total = dc->lane_total;
+    p.max_bucket = &dc->max_bucket;
     if (two_pass) {
         KTimer kt(h, K_PART1, n);
         HIPCHK(h, launch_part1(p, h->stream));
@@ -856,6 +944,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     out->drops = got.drops;
     out->qmin = got.qmin;
     out->qmax = got.qmax;
+    out->skew = (int64_t)got.max_bucket * p.grid > kHeavyMin;
     for (int l = 0; l < kMaxLanes; l++) {
         out->lane_min[l] = JMAX;
         out->lane_max[l] = JMIN;
@@ -948,6 +1037,8 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         HIPCHK(h, launch_ingest_scatter(p, h->stream));
     }
     s->has_null = vnull != nullptr;
+    s->is_acc = false;
+    s->skew = out->skew;
     s->refs = 0;
     for (int l = 0; l < h->lanes; l++) {
         if (out->lane_total[l] == 0) continue;
@@ -1088,6 +1179,7 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     }
     s->has_null = false;
     s->is_acc = true;
+    s->skew = false;
     s->refs = 0;
     for (int l = 0; l < h->lanes; l++) {
         if (out->lane_total[l] == 0) continue;

@@ -86,6 +86,7 @@ struct IngestParams {
     long long* qmax;
     unsigned long long* lane_mask;    // bit l: some record has slice index == l (mod lanes)
     unsigned long long* lane_total;   // [kMaxLanes] accepted records per lane
+    unsigned int* max_bucket;  // max over workgroups and buckets of a workgroup's bucket count (skew hint)
     // scatter inputs/outputs
     const uint32_t* bucket_base; // [F + 1] exclusive scan of bucket totals (lane-major)
     int64_t lane_shift[kMaxLanes];  // staged position = bucket_base[b] + prefix + lane_shift[lane]
@@ -102,6 +103,7 @@ struct IngestParams {
 };
 
 constexpr int kMaxMergeBatches = 32;         // pipelined merge: staged batches held in LDS
+constexpr int kPartStride = kSlots + 1;      // heavy chunks: partial-table entries per chunk
 
 struct MergeParams {
     int32_t region_bits;       // log2(P): state regions
@@ -130,6 +132,46 @@ struct MergeParams {
     int64_t out_cap;
     unsigned int* overflow;    // bit0: region overflow, bit1: output overflow, bit2: LDS table full
     unsigned long long* stamps;  // diagnostic builds only (FG_STAMPS): per-phase cycles summed over waves
+    // skewed (heavy) regions, split off by k_heavy_plan (may be null):
+    const uint8_t* heavy;      // [P] 1: the region is merged by the heavy pass, skipped here
+    // heavy pass (wide kernel only): regions = region_list[0 .. *n_list), each with the
+    // partial tables of its chunks [chunk0[i], chunk0[i + 1]) as an extra source
+    const int32_t* region_list;
+    const int32_t* n_list;
+    const int32_t* chunk0;
+    const int64_t* part_key;   // [chunk * kSlots + e]
+    const int64_t* part_cs;
+    const int64_t* part_cn;
+    const int64_t* part_sum;
+    const uint32_t* part_n;    // entries per chunk
+};
+
+// Skewed regions (Zipf hot keys): a region whose staged records exceed `threshold` is
+// merged in chunks of `chunk` records by k_heavy_chunks (one LDS table per chunk, with a
+// wave-level pre-reduction of equal keys), then the chunks' partial tables (and the
+// region's resident state) by the heavy pass of the wide merge, so that no region's work
+// lands on one workgroup.
+struct HeavyPlan {
+    const StagedBatch* batches;
+    int32_t n_batches;
+    int32_t region_bits;
+    int64_t threshold;
+    int64_t chunk;
+    int32_t max_chunks;
+    int32_t val_type;
+    uint8_t* heavy;            // [P]
+    int32_t* region_list;      // [P]
+    int32_t* n_list;           // [2]: heavy regions, chunks
+    int32_t* chunk0;           // [P + 1]
+    int32_t* chunk_list;       // [max_chunks]: list index of the chunk's region
+    int64_t* chunk_v0;         // [max_chunks]: first record of the chunk within the region's
+    int64_t* chunk_v1;         //   records, batches concatenated in order
+    int64_t* part_key;         // [max_chunks * kSlots]
+    int64_t* part_cs;
+    int64_t* part_cn;
+    int64_t* part_sum;
+    uint32_t* part_n;          // [max_chunks]
+    unsigned int* overflow;
 };
 
 // Accumulator rows of the global phase: input columns and the SoA staged area (all lanes)
@@ -175,6 +217,8 @@ hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int3
 // regions (p.compact: two workgroups fit a CU)
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
+hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s);
+hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s);
 constexpr int kMaxOwnerCols = 8;
 struct OwnerCols {
     int32_t ncols;

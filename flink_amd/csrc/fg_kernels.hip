@@ -23,6 +23,10 @@
 
 namespace fg {
 
+#ifndef FG_DIAG_PART2
+#define FG_DIAG_PART2 0    // diagnostic builds only (wrong results): bit0 no writes, bit1 no loads, bit2 no map
+#endif
+
 // Workgroup barrier that orders LDS only: waits for this wave's LDS ops, not for its
 // global loads/stores (a __syncthreads() also drains vmcnt, stalling on in-flight stores).
 __device__ __forceinline__ void lds_barrier() {
@@ -176,11 +180,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
     }
     __syncthreads();
     // workgroup-major histogram: hist[g * F + b] (contiguous stores) + per-lane totals
-    uint32_t lane_part = 0;
+    uint32_t lane_part = 0, bmax = 0;
     int lane_of = -1;
     for (int b = tid; b < F; b += kIngestThreads) {
         const uint32_t c = s_hist[b];
         p.hist[(int64_t)blockIdx.x * F + b] = c;
+        bmax = c > bmax ? c : bmax;
         const int l = b >> p.region_bits;
         if (l != lane_of) {
             if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
@@ -190,6 +195,11 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
         lane_part += c;
     }
     if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t y = __shfl_xor(bmax, off);
+        bmax = y > bmax ? y : bmax;
+    }
+    if ((tid & 63) == 0 && p.max_bucket && bmax) atomicMax(p.max_bucket, bmax);
     __syncthreads();
     if (tid < p.lanes && s_lane[tid]) atomicAdd(&p.lane_total[tid], (unsigned long long)s_lane[tid]);
     if (tid == 0) {
@@ -558,11 +568,12 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
         if (qmax != JMIN) atomicMax(&s_qmax, qmax);
     }
     __syncthreads();
-    uint32_t lane_part = 0;
+    uint32_t lane_part = 0, bmax = 0;
     int lane_of = -1;
     for (int b = tid; b < F; b += kPart1Threads) {
         const uint32_t c = s_hist[b];
         p.hist[(int64_t)blockIdx.x * F + b] = c;
+        bmax = c > bmax ? c : bmax;
         const int l = b >> p.region_bits;
         if (l != lane_of) {
             if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
@@ -572,6 +583,11 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
         lane_part += c;
     }
     if (lane_part) atomicAdd(&s_lane[lane_of], lane_part);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t y = __shfl_xor(bmax, off);
+        bmax = y > bmax ? y : bmax;
+    }
+    if ((tid & 63) == 0 && p.max_bucket && bmax) atomicMax(p.max_bucket, bmax);
     __syncthreads();
     if (tid < p.lanes && s_lane[tid]) atomicAdd(&p.lane_total[tid], (unsigned long long)s_lane[tid]);
     if (tid == 0) {
@@ -709,6 +725,10 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             if (idx >= total) continue;
             const int q = s_map[idx - base];
             const uint32_t src = s_fsrc[q] + (idx - s_fstart[q]);
+            if (FG_DIAG_PART2 & 2) {
+                rr[u] = make_longlong2((long long)src * 0x9E3779B97F4A7C15ll, src);
+                continue;
+            }
             rr[u] = p.tmp[src];
             if (has_null) rn[u] = p.tmp_null[src];
         }
@@ -727,7 +747,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             cn[u] = rn[u];
         }
         if (base + kPart2Tile < total) {
-            build_map(base + kPart2Tile);
+            if (!(FG_DIAG_PART2 & 4)) build_map(base + kPart2Tile);
             load(base + kPart2Tile);
         }
         uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
@@ -758,15 +778,31 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             s_fb[slot] = (uint8_t)((rf[u] & (NF - 1)) | (cn[u] ? 0x80u : 0u));
         }
         lds_barrier();
+        // write-out: all of the thread's LDS reads first, then its stores back to back
         const uint32_t sub = s_off[NF];
-        for (uint32_t i = tid; i < sub; i += kPart2Threads) {
-            const uint32_t fb = s_fb[i];
-            const int f = (int)(fb & (NF - 1));
+        uint32_t wfb[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const uint32_t i = (uint32_t)(u * kPart2Threads + tid);
+            wfb[u] = 0xffffffffu;
+            if (i < sub) {
+                wfb[u] = s_fb[i];
+                cr[u] = s_rec[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if (wfb[u] == 0xffffffffu) continue;
+            const uint32_t i = (uint32_t)(u * kPart2Threads + tid);
+            const int f = (int)(wfb[u] & (NF - 1));
             const int64_t pos = (int64_t)(s_cur[f] + (i - s_off[f]));
-            const longlong2 r = s_rec[i];
-            if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * pos) = r;
-            else p.st_rec[pos] = r.x;
-            if (has_null) p.st_null[pos] = (uint8_t)(fb >> 7);
+            if (FG_DIAG_PART2 & 1) {
+                if (cr[u].x == 0x5555 && cr[u].y == 0x7777) p.st_rec[0] = pos;   // keep the reads alive
+                continue;
+            }
+            if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * pos) = cr[u];
+            else p.st_rec[pos] = cr[u].x;
+            if (has_null) p.st_null[pos] = (uint8_t)(wfb[u] >> 7);
         }
         lds_barrier();
         if (tid < NF) {
@@ -1104,17 +1140,25 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     const int vt = p.val_type;
     const int P = 1 << p.region_bits;
     const int G = gridDim.x;
-    const int nreg = ((int)blockIdx.x < P) ? (P - 1 - (int)blockIdx.x) / G + 1 : 0;
+    // regions: all P (strided over the grid), or the heavy pass's list
+    const int NR = p.region_list ? *gbl(p.n_list) : P;
+    const int nreg = ((int)blockIdx.x < NR) ? (NR - 1 - (int)blockIdx.x) / G + 1 : 0;
+    auto region_at = [&](int ri) -> int {
+        const int x = (int)blockIdx.x + ri * G;
+        return p.region_list ? gbl(p.region_list)[x] : x;
+    };
+    // heavy regions are left to the heavy pass (no state read, nothing emitted or written)
+    auto skipped = [&](int r) -> bool { return p.heavy != nullptr && gbl(p.heavy)[r] != 0; };
     const bool fast = p.fast_stream != 0;
     const int nb = p.n_batches;
 
     // fast path state
     auto range_of = [&](int ri, int j, uint32_t& beg, uint32_t& end) {
-        const int r = (int)blockIdx.x + ri * G;
+        const int r = region_at(ri);
         const auto bo = gbl(p.batches[j].bucket_off);
         const uint32_t b0 = bo[0];
         beg = bo[r] - b0;
-        end = bo[r + 1] - b0;
+        end = skipped(r) ? beg : bo[r + 1] - b0;
     };
     // first non-empty chunk at or after (ri, j, i0) within regions <= maxri (whose ranges
     // are in LDS); ri == nreg: stream exhausted
@@ -1242,7 +1286,8 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     }
 
     for (int ri = 0; ri < nreg; ri++) {
-        const int r = (int)blockIdx.x + ri * G;
+        const int r = region_at(ri);
+        const bool skip = skipped(r);
         for (int i = tid; i <= S; i += T) {
             t.key[i] = JMIN;
             t.cs[i] = 0;
@@ -1258,7 +1303,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
 
         MSTAMP(0);   // clear + barrier
         // 1) resident slice regions (state) ------------------------------------------
-        for (int j = 0; !C && j < p.n_src; j++) {
+        for (int j = 0; !C && !skip && j < p.n_src; j++) {
             const TableRef src = p.src[j];
             const uint32_t n = gbl(src.counts)[r];
             const auto base = gbl(src.base + (int64_t)r * 4 * cap);
@@ -1306,7 +1351,21 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 go = step(cb, ca, ri, full);
             }
         } else if constexpr (!C) {
-            for (int j = 0; j < nb; j++) {
+            if (p.region_list) {   // heavy pass: the partial tables of the region's chunks
+                const int li = (int)blockIdx.x + ri * G;
+                const int c0 = gbl(p.chunk0)[li], c1 = gbl(p.chunk0)[li + 1];
+                for (int c = c0; c < c1; c++) {
+                    const uint32_t n = gbl(p.part_n)[c];
+                    const int64_t at = (int64_t)c * kPartStride;
+                    for (uint32_t i = tid; i < n; i += T) {
+                        const int slot = lds_find_or_insert<C>(t, gbl(p.part_key)[at + i], full);
+                        if (slot >= 0)
+                            lds_add<C>(t, slot, (unsigned long long)gbl(p.part_cs)[at + i],
+                                       (unsigned long long)gbl(p.part_cn)[at + i], gbl(p.part_sum)[at + i], vt);
+                    }
+                }
+            }
+            for (int j = 0; !skip && j < nb; j++) {
                 const StagedBatch sb = p.batches[j];
                 const auto bo = gbl(sb.bucket_off);
                 const uint32_t b0 = bo[0];
@@ -1390,7 +1449,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
         lds_barrier();
         MSTAMP(2);   // compaction + scan + barriers
         const unsigned int fl = s_flags;
-        const bool write_dst = p.has_dst && !(fl & 1u) && !(fl & 4u);
+        const bool write_dst = !skip && p.has_dst && !(fl & 1u) && !(fl & 4u);
         const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 2u) && !(fl & 4u);
         int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
         const unsigned long long obase = s_out_base;
@@ -1464,6 +1523,185 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
     } else {
         hipLaunchKernelGGL(k_merge<false>, dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     }
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// skewed regions (hot keys): plan, chunk tables; the heavy pass is k_merge with a region list
+// ----------------------------------------------------------------------------------------
+constexpr int kPlanThreads = 1024;
+constexpr int kPlanPer = (1 << 13) / kPlanThreads;   // regions per thread (P <= 8192)
+
+// One workgroup: staged records per region over the batches; regions above the threshold
+// are listed with ceil(records / chunk) chunks each. A plan that would exceed max_chunks
+// lists nothing (every region then takes the regular merge: slower, same result).
+__global__ __launch_bounds__(kPlanThreads) void k_heavy_plan(HeavyPlan hp) {
+    __shared__ uint32_t s_wave[kPlanThreads / 64];
+    const int tid = threadIdx.x;
+    const int P = 1 << hp.region_bits;
+    int64_t size[kPlanPer];
+    uint32_t nh = 0, nc = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanPer; k++) {
+        const int r = tid * kPlanPer + k;
+        size[k] = 0;
+        if (r >= P) continue;
+        for (int j = 0; j < hp.n_batches; j++) {
+            const auto bo = gbl(hp.batches[j].bucket_off);
+            size[k] += (int64_t)(bo[r + 1] - bo[r]);
+        }
+        if (size[k] > hp.threshold) {
+            nh++;
+            nc += (uint32_t)((size[k] + hp.chunk - 1) / hp.chunk);
+        }
+    }
+    uint32_t tot_h, tot_c;
+    const uint32_t hbase = block_exclusive_scan(nh, s_wave, &tot_h);
+    const uint32_t cbase = block_exclusive_scan(nc, s_wave, &tot_c);
+    const bool ok = tot_c <= (uint32_t)hp.max_chunks;
+    uint32_t hi = hbase, ci = cbase;
+#pragma unroll
+    for (int k = 0; k < kPlanPer; k++) {
+        const int r = tid * kPlanPer + k;
+        if (r >= P) continue;
+        const bool heavy = ok && size[k] > hp.threshold;
+        hp.heavy[r] = heavy ? 1 : 0;
+        if (!heavy) continue;
+        hp.region_list[hi] = r;
+        hp.chunk0[hi] = (int32_t)ci;
+        for (int64_t v = 0; v < size[k]; v += hp.chunk) {
+            hp.chunk_list[ci] = (int32_t)hi;
+            hp.chunk_v0[ci] = v;
+            hp.chunk_v1[ci] = v + hp.chunk < size[k] ? v + hp.chunk : size[k];
+            ci++;
+        }
+        hi++;
+    }
+    if (tid == 0) {
+        hp.n_list[0] = ok ? (int32_t)tot_h : 0;
+        hp.n_list[1] = ok ? (int32_t)tot_c : 0;
+        hp.chunk0[ok ? tot_h : 0] = ok ? (int32_t)tot_c : 0;
+    }
+}
+
+// Persistent over the chunks: each chunk's records (its slice of the region's records,
+// batches in order) are combined in a wide LDS table and the table is written out as the
+// chunk's partial rows {key, COUNT(*), NULL count, sum}. Equal keys within a wave (the hot
+// key of a Zipf region fills most lanes) are reduced with cross-lane adds first, so the
+// LDS atomics of a hot slot drop from one per record to one per wave.
+__global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
+    constexpr int T = kMergeThreads;
+    __shared__ LdsTableT<false> t;
+    __shared__ uint32_t s_n;
+    __shared__ unsigned int s_full;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int vt = hp.val_type;
+    const int nch = *gbl(hp.n_list + 1);
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+        for (int i = tid; i <= kSlots; i += T) {
+            t.key[i] = JMIN;
+            t.cs[i] = 0;
+            t.cn[i] = 0;
+            t.sum[i] = 0;
+        }
+        if (tid == 0) {
+            s_n = 0;
+            s_full = 0;
+        }
+        lds_barrier();
+        bool full = false;
+        const int r = gbl(hp.region_list)[gbl(hp.chunk_list)[c]];
+        const int64_t v0 = gbl(hp.chunk_v0)[c], v1 = gbl(hp.chunk_v1)[c];
+        int64_t acc = 0;
+        for (int j = 0; j < hp.n_batches && acc < v1; j++) {
+            const StagedBatch sb = hp.batches[j];
+            const auto bo = gbl(sb.bucket_off);
+            const int64_t beg = (int64_t)(bo[r] - bo[0]);
+            const int64_t len = (int64_t)(bo[r + 1] - bo[r]);
+            const int64_t lo = acc > v0 ? acc : v0;
+            const int64_t hi = acc + len < v1 ? acc + len : v1;
+            for (int64_t xb = lo; xb < hi; xb += T) {   // wave-uniform trip count
+                const int64_t x = xb + tid;
+                const bool valid = x < hi;
+                const int64_t i = beg + (x - acc);
+                int64_t k = JMIN, sum = 0;
+                unsigned long long cs = 1, cn = 0;
+                if (valid) {
+                    if (sb.is_acc) {
+                        k = gbl(sb.rec)[i];
+                        cs = (unsigned long long)gbl(sb.cnt_star)[i];
+                        cn = (unsigned long long)gbl(sb.cnt_null)[i];
+                        sum = gbl(sb.val)[i];
+                    } else if (sb.stride == 2) {
+                        const RecV2 rc = ((GlobalRec)sb.rec)[i];
+                        k = rc.x;
+                        sum = rc.y;
+                    } else {
+                        k = gbl(sb.rec)[i];
+                    }
+                    if (!sb.is_acc && sb.vnull != nullptr && gbl(sb.vnull)[i] != 0) {
+                        cn = 1;
+                        sum = 0;
+                    }
+                }
+                if (!sb.is_acc && sb.stride != 2) sum = 0;
+                // wave pre-reduction of the records equal to the first lane's key (no NULLs)
+                bool done = !valid;
+                const int64_t k0 = __builtin_amdgcn_readfirstlane(k);
+                const uint64_t m = __ballot(valid && cn == 0 && k == k0 && !sb.is_acc);
+                if (__popcll(m) > 1) {
+                    const bool in = (m >> lane) & 1;
+                    int64_t part = in ? sum : 0;
+                    if (vt == 2) {
+                        double d = in ? __longlong_as_double(sum) : 0.0;
+                        for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+                        part = __double_as_longlong(d);
+                    } else {
+                        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+                    }
+                    if (in) {
+                        done = true;
+                        if (lane == __ffsll((long long)m) - 1) {
+                            const int slot = lds_find_or_insert<false>(t, k0, full);
+                            if (slot >= 0) lds_add<false>(t, slot, (unsigned long long)__popcll(m), 0ull, part, vt);
+                        }
+                    }
+                }
+                if (!done) {
+                    const int slot = lds_find_or_insert<false>(t, k, full);
+                    if (slot >= 0) lds_add<false>(t, slot, cs, cn, sum, cn == 1 && !sb.is_acc ? 0 : vt);
+                }
+            }
+            acc += len;
+        }
+        if (full) atomicOr(&s_full, 1u);
+        lds_barrier();
+        const int64_t at = (int64_t)c * kPartStride;
+        for (int i = tid; i <= kSlots; i += T) {
+            if (t.cs[i] == 0) continue;
+            const uint32_t o = atomicAdd(&s_n, 1u);
+            hp.part_key[at + o] = i == kSlots ? JMIN : t.key[i];
+            hp.part_cs[at + o] = (int64_t)t.cs[i];
+            hp.part_cn[at + o] = (int64_t)t.cn[i];
+            hp.part_sum[at + o] = (int64_t)t.sum[i];
+        }
+        lds_barrier();
+        if (tid == 0) {
+            hp.part_n[c] = s_n;
+            if (s_full) atomicOr(hp.overflow, 4u);
+        }
+        lds_barrier();   // the table is cleared for the next chunk
+    }
+}
+
+hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s) {
+    if (hp.region_bits > 13 || hp.n_batches < 1 || hp.chunk < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_heavy_plan, dim3(1), dim3(kPlanThreads), 0, s, hp);
+    return hipGetLastError();
+}
+
+hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s) {
+    hipLaunchKernelGGL(k_heavy_chunks, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
     return hipGetLastError();
 }
 

@@ -134,8 +134,19 @@ class WindowAggOperator:
         self.close()
 
     # -- processElement ---------------------------------------------------------------------
+    def _after_producers(self, cols):
+        """Device columns are read on the engine's stream: order it after the torch stream
+        that produced them (an event wait, no host synchronization)."""
+        for c in cols:
+            if hasattr(c, "is_cuda") and c.is_cuda:
+                import torch
+                cur = torch.cuda.current_stream(c.device)
+                torch.cuda.ExternalStream(self.stream, device=c.device).wait_stream(cur)
+                return
+
     def process_batch(self, key, rowtime, val=None, val_null=None):
         """processElement for every record of a micro-batch (arrival order = index order)."""
+        self._after_producers((key, rowtime, val, val_null))
         kp, kdev, key = _dev_ptr(key)
         tp, tdev, rowtime = _dev_ptr(rowtime)
         vp, vdev, val = _dev_ptr(val)
@@ -168,6 +179,7 @@ class WindowAggOperator:
         """GlobalAggCombiner.combine for partial accumulator rows (after the exchange): numpy
         arrays or device tensors; `sum_bits` holds i64 sums or the bits of f64 sums."""
         cols = [key, slice_end, cnt_star, cnt_val, sum_bits]
+        self._after_producers(cols)
         ptrs = [_dev_ptr(c) for c in cols]
         b = L.FgPartials()
         keep = []

@@ -73,6 +73,9 @@ enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
 /* Aggregates over the single value column (SumAggFunction, Count1AggFunction,
  * CountAggFunction, AvgAggFunction of TP/functions/aggfunctions/). */
 enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3 };
+/* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
+ * producer before it (complete, or an event the stream waits on). They are fully read when
+ * fg_add_batch / fg_add_partials return. */
 enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
 enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1 };
 enum fg_flags {

@@ -5,7 +5,9 @@ mkdir -p gpurun_out
 K=$1; shift
 for v in "$@"; do
   echo "== $v"
-  FLINKGPU_LIB=$PWD/flink_amd/libflinkgpu_$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 240 \
+  LIB=$PWD/flink_amd/libflinkgpu_$v.so
+  [ "$v" = main ] && LIB=$PWD/flink_amd/libflinkgpu.so
+  FLINKGPU_LIB=$LIB timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 240 \
      --timeout-method thread -k "$K" > gpurun_out/tv_$v.log 2>&1
   tail -3 gpurun_out/tv_$v.log
 done

@@ -17,12 +17,12 @@ def window_of(cfg):
 
 
 class GpuOperator:
-    def __init__(self, cfg, expected_keys=1 << 12, buffer_records=1 << 20, _op=None):
+    def __init__(self, cfg, expected_keys=1 << 12, buffer_records=1 << 20, _op=None, kernel_timing=False):
         self.cfg = cfg
         self.op = _op or F.WindowAggOperator(
             window_of(cfg), aggs=("count_star", "count", "sum", "avg"), val_type=cfg["val_type"],
             mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
-            buffer_records=buffer_records)
+            buffer_records=buffer_records, kernel_timing=kernel_timing)
         self._rows = []
 
     def process_batch(self, key, ts, val=None, isnull=None):

@@ -15,15 +15,25 @@ def splitmix64(x: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
+def zipf_keys(u, keys, s):
+    """Zipf(s) ranks 0..keys-1 by inverse CDF of the uniform 53-bit fraction of u."""
+    w = np.arange(1, keys + 1, dtype=np.float64) ** -s
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    q = (u >> np.uint64(11)).astype(np.float64) * (1.0 / float(1 << 53))
+    return np.minimum(np.searchsorted(cdf, q), keys - 1).astype(np.int64)
+
+
 def make_stream(n, keys, val_type="f64", t0=1_600_000_000_000, rate_per_ms=100, jitter_ms=0, null_frac=0.0,
-                seed=SEED, key_spread=False, big_ints=False):
+                seed=SEED, key_spread=False, big_ints=False, zipf=0.0):
     """Returns (key, rowtime, val, isnull) numpy arrays.
 
-    rowtime = t0 + i / rate_per_ms (+ uniform jitter in [0, jitter_ms) when out of order)."""
+    rowtime = t0 + i / rate_per_ms (+ uniform jitter in [0, jitter_ms) when out of order);
+    keys uniform over [0, keys), or Zipf(zipf) ranks (hot keys) when zipf > 0."""
     i = np.arange(n, dtype=np.uint64)
     u = splitmix64(np.uint64(seed) ^ i)
     u2 = splitmix64(np.uint64(seed * 3 + 1) ^ i)
-    key = (u % np.uint64(keys)).astype(np.int64)
+    key = zipf_keys(u, keys, zipf) if zipf > 0 else (u % np.uint64(keys)).astype(np.int64)
     if key_spread:   # spread ids over the whole i64 range (incl. the sentinel Long.MIN_VALUE)
         key = splitmix64(key.astype(np.uint64) ^ np.uint64(77)).view(np.int64)
         key[key == key.min()] = np.iinfo(np.int64).min

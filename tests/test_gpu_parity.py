@@ -61,9 +61,10 @@ def assert_rows_equal(got, exp, vt, ctx=""):
 
 
 def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at=None, end_wm=JMAX,
-               expected_keys=None, **gen):
+               expected_keys=None, kstats=None, **gen):
     key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
-    g = gpu_mk(cfg, expected_keys=expected_keys or keys, buffer_records=max(batch * 4, 1 << 16))
+    g = gpu_mk(cfg, expected_keys=expected_keys or keys, buffer_records=max(batch * 4, 1 << 16),
+               kernel_timing=kstats is not None)
     o = oracle_mk(O, cfg)
     o_base = 0
     step = 0
@@ -88,6 +89,8 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
     o.process_watermark(end_wm)
     assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final")
     late = g.late_dropped
+    if kstats is not None:
+        kstats.update(g.op.kernel_stats())
     g.close()
     o.close()
     return late
@@ -127,12 +130,28 @@ STREAM_CASES = [
     ("big_units_i64_nulls_ooo", cfg_of("tumble", 1000, vt="i64"), dict(n=16_000_000, keys=500_000, batch=8_000_000,
                                                                        delay=600, jitter=500, null_frac=0.1,
                                                                        rate_per_ms=10_000)),
+    # Zipf(1.1) hot keys: regions over the skew threshold take the chunked heavy pass
+    ("zipf_tumble_f64", cfg_of("tumble", 1000), dict(n=3_000_000, keys=100_000, batch=1_000_000, delay=0, jitter=0,
+                                                      rate_per_ms=2_000, zipf=1.1)),
+    ("zipf_tumble_i64_nulls_late", cfg_of("tumble", 1000, vt="i64"), dict(n=3_000_000, keys=100_000, batch=1_000_000,
+                                                                          delay=200, jitter=600, null_frac=0.1,
+                                                                          rate_per_ms=2_000, zipf=1.1)),
+    ("zipf_hop_f64", cfg_of("hop", 3000, 1000), dict(n=3_000_000, keys=50_000, batch=1_000_000, delay=100, jitter=300,
+                                                      rate_per_ms=1_000, zipf=1.1)),
+    ("zipf_cumulate_i64", cfg_of("cumulate", 4000, 1000, vt="i64"), dict(n=3_000_000, keys=50_000, batch=1_000_000,
+                                                                         delay=0, jitter=0, rate_per_ms=1_000,
+                                                                         zipf=1.3)),
+    ("zipf_ds_tumble_i64", cfg_of("tumble", 2000, vt="i64", mode="datastream"),
+     dict(n=3_000_000, keys=100_000, batch=1_000_000, delay=0, jitter=0, rate_per_ms=1_000, zipf=1.1)),
 ]
 
 
 @pytest.mark.parametrize("name,cfg,kw", STREAM_CASES, ids=[c[0] for c in STREAM_CASES])
 def test_stream_parity(oracle_mod, name, cfg, kw):
-    drive_both(oracle_mod, cfg, **kw)
+    ks = {} if kw.get("zipf") else None
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    if ks is not None:   # the hot keys' regions did take the chunked heavy pass
+        assert ks.get("merge_heavy", {}).get("launches", 0) > 0, ks
 
 
 @pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
@@ -290,6 +309,9 @@ TWO_PHASE_CASES = [
     ("tumble_i64_ooo_late", cfg_of("tumble", 300, vt="i64"), dict(n=300_000, keys=20_000, batch=20_000, delay=100, jitter=600)),
     ("hop_f64_late", cfg_of("hop", 3000, 1000), dict(n=300_000, keys=30_000, batch=20_000, delay=200, jitter=1500)),
     ("cumulate_i64_late", cfg_of("cumulate", 4000, 500, vt="i64"), dict(n=300_000, keys=30_000, batch=15_000, delay=50, jitter=2500)),
+    # hot keys in the local phase: skewed regions take the heavy pass before the exchange
+    ("zipf_tumble_f64", cfg_of("tumble", 1000), dict(n=6_000_000, keys=100_000, batch=3_000_000, delay=0, jitter=0,
+                                                      rate_per_ms=3_000, zipf=1.1)),
 ]
 
 
@@ -304,7 +326,8 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     from tests.gpu_adapter import window_of
     S, R, MAXP = 3, 2, 128
     n, keys, batch, delay, jitter = kw["n"], kw["keys"], kw["batch"], kw["delay"], kw["jitter"]
-    key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter)
+    key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter,
+                                  **{k: kw[k] for k in ("rate_per_ms", "zipf") if k in kw})
     w = window_of(cfg)
     aggs = ("count_star", "count", "sum", "avg")
     local = [F.WindowAggOperator(w, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
