@@ -85,11 +85,11 @@ WORKLOADS = {
 
 
 def zipf_cdf(keys, s, device):
-    """CDF of Zipf(s) over ranks 1..keys (float64, on the device)."""
-    r = torch.arange(1, keys + 1, dtype=torch.float64, device=device)
-    w = r.pow(-s)
-    c = torch.cumsum(w, 0)
-    return c / c[-1]
+    """CDF of Zipf(s) over ranks 1..keys (float64), summed sequentially on the host so that
+    the generated keys are the same in every run (a device cumsum's order is not fixed)."""
+    w = np.arange(1, keys + 1, dtype=np.float64) ** -s
+    c = np.cumsum(w)
+    return torch.from_numpy(c / c[-1]).to(device)
 
 
 def gen_columns(n, keys, rate_s, base_index, device, chunk=1 << 26, jitter=0, zipf=0.0):
