@@ -209,6 +209,7 @@ struct fg_handle {
 
     // fired rows
     int64_t out_cap = 0, out_n = 0, pending_out = 0;
+    int64_t q_guess = kEmptyLane;   // first slice of the next batch's first ingest pass (kEmptyLane: all)
     DevBuf o_key, o_ws, o_we, o_null, o_rt;
     DevBuf o_agg[FG_MAX_AGGS];
     HostBuf h_key, h_ws, h_we, h_null, h_rt;
@@ -952,8 +953,11 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     }
     if (got.qmin > got.qmax) return FG_OK;   // nothing accepted
     h->anchor_start = jsub(slice_end_of(h, got.qmin), h->w.slice);
-    if ((uint64_t)(got.qmax - got.qmin) >= (uint64_t)h->lanes) return -1;   // more slices than lanes
-    for (int64_t q = got.qmin; q <= got.qmax; q++) {
+    // qmin/qmax span the batch's accepted records; the pass stages those inside the filter
+    const int64_t fq0 = std::max<int64_t>(got.qmin, flo), fq1 = std::min<int64_t>(got.qmax, fhi - 1);
+    if (fq0 > fq1) return FG_OK;                                            // none inside
+    if ((uint64_t)(fq1 - fq0) >= (uint64_t)h->lanes) return -1;              // more slices than lanes
+    for (int64_t q = fq0; q <= fq1; q++) {
         const int l = (int)(q & (h->lanes - 1));
         if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
     }
@@ -1121,8 +1125,10 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
         out->lane_total[l] = (long long)got.lane_total[l];
     }
     if (got.qmin > got.qmax) return FG_OK;
-    if ((uint64_t)(got.qmax - got.qmin) >= (uint64_t)h->lanes) return -1;
-    for (int64_t q = got.qmin; q <= got.qmax; q++) {
+    const int64_t fq0 = std::max<int64_t>(got.qmin, flo), fq1 = std::min<int64_t>(got.qmax, fhi - 1);
+    if (fq0 > fq1) return FG_OK;
+    if ((uint64_t)(fq1 - fq0) >= (uint64_t)h->lanes) return -1;
+    for (int64_t q = fq0; q <= fq1; q++) {
         const int l = (int)(q & (h->lanes - 1));
         if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
     }
@@ -1390,23 +1396,33 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
         int rc0 = b->location == FG_HOST ? seed_anchor(h, nullptr, b->rowtime) : seed_anchor(h, ts, nullptr);
         if (rc0) return rc0;
     }
+    // First pass: every slice -- or, while batches span more slices than the staged lanes
+    // (out-of-order jitter, long batches), the `lanes` slices from the previous batch's
+    // first one. Slices outside the pass's filter are staged by filtered passes of `lanes`
+    // slices each; a lane holding another slice is flushed to its table first (ingest_pass).
     Counters c{};
-    int rc = ingest_pass(h, n, key, ts, val, vnull, JMIN, JMAX, true, &c);
+    int64_t flo = JMIN, fhi = JMAX;
+    if (h->q_guess != kEmptyLane) {
+        flo = h->q_guess;
+        fhi = flo + h->lanes;
+    }
+    int rc = ingest_pass(h, n, key, ts, val, vnull, flo, fhi, true, &c);
     h->late_dropped += (int64_t)c.drops;
-    if (rc == FG_OK) return FG_OK;
-    if (rc != -1) return rc;
-    // Lane conflict: the batch spans slices that do not fit the staged lanes. Flush and
-    // ingest the batch in slice ranges of `lanes` slices.
-    const int64_t qlo = c.qmin, qhi = c.qmax;
-    rc = flush(h);
-    if (rc) return rc;
-    for (int64_t lo = qlo; lo <= qhi; lo += h->lanes) {
-        Counters c2{};
-        rc = ingest_pass(h, n, key, ts, val, vnull, lo, lo + h->lanes, false, &c2);
-        if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
-        if (rc) return rc;
-        if (lo + h->lanes <= qhi) {
-            rc = flush(h);
+    if (rc != FG_OK && rc != -1) return rc;
+    if (c.qmin > c.qmax) return FG_OK;   // nothing accepted
+    h->q_guess = (uint64_t)(c.qmax - c.qmin) >= (uint64_t)h->lanes ? c.qmin : kEmptyLane;
+    std::vector<std::pair<int64_t, int64_t>> rest;   // slice ranges [a, b) still to stage
+    if (rc == -1) {
+        rest.push_back({c.qmin, c.qmax + 1});
+    } else {
+        if (c.qmin < flo) rest.push_back({c.qmin, flo});
+        if (c.qmax >= fhi) rest.push_back({fhi, c.qmax + 1});
+    }
+    for (auto& r : rest) {
+        for (int64_t lo = r.first; lo < r.second; lo += h->lanes) {
+            Counters c2{};
+            rc = ingest_pass(h, n, key, ts, val, vnull, lo, std::min<int64_t>(lo + h->lanes, r.second), false, &c2);
+            if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
             if (rc) return rc;
         }
     }
@@ -1741,6 +1757,7 @@ int fg_reset(fg_handle* h) {
     for (int64_t e : ends) table_free(h, e);
     for (int l = 0; l < h->lanes; l++) release_lane(h, l);
     h->anchor_start = JMIN;
+    h->q_guess = kEmptyLane;
     h->current_progress = JMIN;
     h->next_trigger = JMIN;
     h->timer_wm = JMIN;

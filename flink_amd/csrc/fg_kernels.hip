@@ -27,6 +27,15 @@ namespace fg {
 #define FG_DIAG_PART2 0    // diagnostic builds only (wrong results): bit0 no writes, bit1 no loads, bit2 no map
 #endif
 
+typedef long long RecV2 __attribute__((ext_vector_type(2)));
+typedef const RecV2 __attribute__((address_space(1)))* GlobalRec;
+// a pointer that was itself loaded from memory is generic (flat) to the compiler: view it in
+// the global address space so its loads are global_load (see `load` below)
+template <class T>
+__device__ __forceinline__ const T __attribute__((address_space(1)))* gbl(const T* q) {
+    return (const T __attribute__((address_space(1)))*)q;
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's LDS ops, not for its
 // global loads/stores (a __syncthreads() also drains vmcnt, stalling on in-flight stores).
 __device__ __forceinline__ void lds_barrier() {
@@ -51,8 +60,8 @@ __device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int6
         if (!target_slice(p.w, ts, p.progress, &target)) return -1;
         q = floor_div_fast(target, p.w.slice, p.w.rslice);
     }
+    *q_out = q;   // also for records outside the filter: the batch's whole slice range is counted
     if (q < p.filter_lo || q >= p.filter_hi) return -2;
-    *q_out = q;
     const int lane = (int)(q & (int64_t)(p.lanes - 1));
     const uint32_t rb = p.region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.region_bits));
     return (lane << p.region_bits) | (int)rb;
@@ -137,6 +146,9 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
             mask |= 1u << ((int)q & lm);
         } else if (b == -1) {
             drops++;
+        } else {   // outside the slice filter: in the batch's slice range only
+            qmin = q < qmin ? q : qmin;
+            qmax = q > qmax ? q : qmax;
         }
     };
     constexpr int kU = 4;
@@ -470,7 +482,12 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
                 const uint32_t c = (uint32_t)b >> kFineBits;
                 return (atomicAdd(&s_cc[c], 1u) << 9) | c;
             }
-            if (b == -1) drops++;
+            if (b == -1) {
+                drops++;
+            } else {   // outside the slice filter: in the batch's slice range only
+                qmin = q < qmin ? q : qmin;
+                qmax = q > qmax ? q : qmax;
+            }
             return 0xffffffffu;
         };
         if (tn == kPart1Tile && p.vec) {
@@ -1080,6 +1097,34 @@ __device__ __forceinline__ int lds_find_or_insert(LdsTableT<C>& t, int64_t k, bo
     return lds_find_or_insert_from<C>(t, k, lds_home<C>(k), full);
 }
 
+// slot of key k given its home bucket's keys (read beforehand): a match, else a CAS on the
+// bucket's first empty slot, else (full bucket / lost CAS) the linear probe
+template <bool C>
+__device__ __forceinline__ int lds_bucket_slot(LdsTableT<C>& t, int64_t k, uint32_t home, RecV2 b01, RecV2 b23,
+                                               bool& full) {
+    constexpr uint32_t S_ = (uint32_t)MergeCfg<C>::kSlotsT;
+    if (k == JMIN) return (int)S_;
+    const int64_t q[kBucket] = {b01.x, b01.y, b23.x, b23.y};
+    int hit = -1, empty = -1;
+#pragma unroll
+    for (int j = kBucket - 1; j >= 0; j--) {
+        if (q[j] == k) hit = j;
+        if (q[j] == JMIN) empty = j;
+    }
+    if (hit >= 0 && (empty < 0 || hit < empty)) return (int)home + hit;
+    if (empty >= 0) {
+        const uint32_t e = home + (uint32_t)empty;
+        const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&t.key[e]),
+                                                 (unsigned long long)JMIN, (unsigned long long)k);
+        if (old == (unsigned long long)JMIN || old == (unsigned long long)k) return (int)e;
+        return lds_find_or_insert_from<C>(t, k, e + 1 >= S_ ? 0u : e + 1, full);
+    }
+    const uint32_t nx = home + kBucket;
+    return lds_find_or_insert_from<C>(t, k, nx >= S_ ? 0u : nx, full);
+}
+constexpr int kSrcU = 2;          // source-table entries per thread per round (wide merge)
+constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
+
 template <bool C>
 __device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long long cs, unsigned long long cn,
                                         int64_t sum_bits, int vt) {
@@ -1096,14 +1141,6 @@ __device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long
     }
 }
 
-typedef long long RecV2 __attribute__((ext_vector_type(2)));
-typedef const RecV2 __attribute__((address_space(1)))* GlobalRec;
-// a pointer that was itself loaded from memory is generic (flat) to the compiler: view it in
-// the global address space so its loads are global_load (see `load` below)
-template <class T>
-__device__ __forceinline__ const T __attribute__((address_space(1)))* gbl(const T* q) {
-    return (const T __attribute__((address_space(1)))*)q;
-}
 
 // Pipelined staged stream (every batch plain {key, value} AoS, <= kMaxMergeBatches): the
 // workgroup walks its regions r0, r0 + G, ... as one stream of chunks (chunks never span
@@ -1134,6 +1171,8 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     __shared__ unsigned long long s_out_base;
     __shared__ const longlong2* s_brec[kMaxMergeBatches];     // fast path: batch record bases
     __shared__ uint32_t s_rng[3][kMaxMergeBatches][2];         // fast path: [ri % 3][batch] = (beg, end)
+    __shared__ uint32_t s_soff[kMaxSrcFlat + 1];               // source tables: entry prefix of the region
+    __shared__ const int64_t* s_sbase[kMaxSrcFlat];            //   and each table's region base
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int cap = kRegionCap;
@@ -1295,6 +1334,20 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             t.sum[i] = 0;
         }
         if (tid == 0) s_flags = 0;
+        if constexpr (!C) if (tid < 64) {   // source tables: per-region entry counts -> flat prefix
+            const int nsrc = p.n_src <= kMaxSrcFlat ? p.n_src : 0;
+            const uint32_t v = tid < nsrc ? gbl(p.src[tid].counts)[r] : 0u;
+            uint32_t x = v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (tid >= off) x += y;
+            }
+            if (tid < nsrc) {
+                s_soff[tid + 1] = x;
+                s_sbase[tid] = p.src[tid].base + (int64_t)r * 4 * cap;
+            }
+            if (tid == 0) s_soff[0] = 0;
+        }
         // fast path: ranges of region ri + 2 (written to LDS after this region's inserts)
         uint32_t nbeg = 0, nend = 0;
         if (fast && tid < nb && ri + 2 < nreg) range_of(ri + 2, tid, nbeg, nend);
@@ -1303,28 +1356,62 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
 
         MSTAMP(0);   // clear + barrier
         // 1) resident slice regions (state) ------------------------------------------
-        for (int j = 0; !C && !skip && j < p.n_src; j++) {
-            const TableRef src = p.src[j];
-            const uint32_t n = gbl(src.counts)[r];
-            const auto base = gbl(src.base + (int64_t)r * 4 * cap);
-            for (uint32_t i0 = 0; i0 < n; i0 += 4 * T) {
-                int64_t k[4], cs[4], cn[4], sm[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {      // issue all loads first (latency hiding)
-                    const uint32_t i = i0 + u * T + tid;
-                    if (i < n) {
-                        k[u] = base[i];
-                        cs[u] = base[cap + i];
-                        cn[u] = base[2 * cap + i];
-                        sm[u] = base[3 * cap + i];
+        //    the entries of all source tables form one flat sequence (prefix of the
+        //    tables' counts in s_soff), loaded kSrcU per thread at a time and inserted with
+        //    the bucketed probe
+        if constexpr (!C) {
+            const uint32_t NT = skip ? 0u : s_soff[p.n_src <= kMaxSrcFlat ? p.n_src : 0];
+            for (uint32_t i0 = 0; i0 < NT; i0 += kSrcU * T) {
+                int64_t k[kSrcU], cs[kSrcU], cn[kSrcU], sm[kSrcU];
+                int j = 0;
+                {   // table of this thread's first entry (binary search), later ones advance
+                    const uint32_t f = i0 + tid;
+                    int lo = 0, hi = p.n_src;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_soff[mid] <= f) lo = mid;
+                        else hi = mid;
                     }
+                    j = lo;
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t i = i0 + u * T + tid;
-                    if (i >= n) continue;
-                    const int slot = lds_find_or_insert<C>(t, k[u], full);
+                for (int u = 0; u < kSrcU; u++) {
+                    const uint32_t f = i0 + u * T + tid;
+                    k[u] = JMIN;
+                    if (f >= NT) continue;
+                    while (s_soff[j + 1] <= f) j++;
+                    const uint32_t i = f - s_soff[j];
+                    const auto base = gbl(s_sbase[j]);
+                    k[u] = base[i];
+                    cs[u] = base[cap + i];
+                    cn[u] = base[2 * cap + i];
+                    sm[u] = base[3 * cap + i];
+                }
+                uint32_t home[kSrcU];
+                RecV2 b01[kSrcU], b23[kSrcU];
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    home[u] = lds_home<C>(k[u]);
+                    const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
+                    b01[u] = kb[0];
+                    b23[u] = kb[1];
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    if (i0 + u * T + tid >= NT) continue;
+                    const int slot = lds_bucket_slot<C>(t, k[u], home[u], b01[u], b23[u], full);
                     if (slot >= 0) lds_add<C>(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
+                }
+            }
+            for (int j = 0; !skip && p.n_src > kMaxSrcFlat && j < p.n_src; j++) {   // many tables: one by one
+                const TableRef src = p.src[j];
+                const uint32_t n = gbl(src.counts)[r];
+                const auto base = gbl(src.base + (int64_t)r * 4 * cap);
+                for (uint32_t i = tid; i < n; i += T) {
+                    const int slot = lds_find_or_insert<C>(t, base[i], full);
+                    if (slot >= 0)
+                        lds_add<C>(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
+                                   base[3 * cap + i], vt);
                 }
             }
         }
