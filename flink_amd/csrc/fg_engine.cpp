@@ -366,6 +366,7 @@ int check_overflow(fg_handle* h) {
 }
 
 int ensure_out(fg_handle* h, int64_t need);
+int fire_collect(fg_handle* h);
 
 // zero the overflow word and the fired-row counter once per advance
 int reset_out_count(fg_handle* h) {
@@ -663,14 +664,16 @@ int ensure_out(fg_handle* h, int64_t need) {
 }
 
 // Emit one window from the union of `srcs`; optionally write the merged state to `dst`.
-int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, SliceTable* dst) {
+// `defer`: no host synchronization -- the caller collects the row count (fire_collect)
+// after the advance's last fire (launches stay ordered on the handle's stream).
+int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, SliceTable* dst, bool defer = false) {
     int64_t ub = 0;
     for (auto* s : srcs) ub += s->upper;
     ub = std::min<int64_t>(ub, (int64_t)kRegionCap * h->P);
     if (ub == 0 && dst == nullptr) return FG_OK;
     int rc = reset_out_count(h);
     if (rc) return rc;
-    rc = ensure_out(h, h->out_n + ub);
+    rc = ensure_out(h, h->out_n + h->pending_out + ub);
     if (rc) return rc;
     std::vector<TableRef> refs;
     for (auto* s : srcs) refs.push_back(ref_of(s));
@@ -691,21 +694,38 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
         KTimer kt(h, K_FIRE, 0);
         HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
     }
+    if (dst) dst->upper = ub;
+    if (defer) {
+        h->pending_out += ub;
+        return FG_OK;
+    }
+    return fire_collect(h);
+}
+
+// after fires: overflow check and the fired-row count (one synchronization)
+int fire_collect(fg_handle* h) {
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
-    rc = sync(h);
+    int rc = sync(h);
     if (rc) return rc;
     rc = check_overflow(h);
     if (rc) return rc;
     const int64_t before = h->out_n;
     h->out_n = (int64_t)h->h_scalars.as<unsigned long long>()[1];
     h->kstat[K_FIRE].rows += h->out_n - before;
-    if (dst) dst->upper = ub;
+    h->pending_out = 0;
     return FG_OK;
 }
 
 // Fire every window whose timer time lies in (prev, wm] (InternalTimerServiceImpl.advanceWatermark
 // :294-304 -> SlicingWindowOperator.onTimer :230-237), in window order.
+int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired);
 int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
+    bool fired = false;
+    int rc = fire_windows_launch(h, prev, wm, &fired);
+    if (rc) return rc;
+    return fired ? fire_collect(h) : FG_OK;
+}
+int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired) {
     const WindowSpec& w = h->w;
     auto due = [&](int64_t wend) {
         int64_t t = trigger_time(w, wend);
@@ -719,7 +739,8 @@ int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
         for (auto& kv : h->tables) ends.push_back(kv.first);
         for (int64_t e : ends) {
             if (due(e)) {
-                rc = fire_one(h, e, {h->tables[e].get()}, nullptr);
+                rc = fire_one(h, e, {h->tables[e].get()}, nullptr, true);
+                *fired = true;
                 if (rc) return rc;
                 table_free(h, e);   // expiredSlices = [windowEnd]
             } else if (dead(e)) {
@@ -740,7 +761,8 @@ int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
                 for (auto it = h->tables.upper_bound(jsub(W, w.size)); it != h->tables.end() && it->first <= W; ++it)
                     srcs.push_back(it->second.get());
                 if (!srcs.empty()) {
-                    rc = fire_one(h, W, srcs, nullptr);
+                    rc = fire_one(h, W, srcs, nullptr, true);
+                    *fired = true;
                     if (rc) return rc;
                 }
             }
@@ -778,14 +800,15 @@ int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
                 if (F) srcs.push_back(F);
                 if (S) srcs.push_back(S);
                 SliceTable* dst = nullptr;
-                if (W != first && W != last) {
+                if (W != first && W != last && S) {
                     if (!F) {
                         rc = table_get(h, first, true, &F);
                         if (rc) return rc;
                     }
                     dst = F;   // merge the step slice into the first slice's state
                 }
-                rc = fire_one(h, W, srcs, dst);
+                rc = fire_one(h, W, srcs, dst, true);   // (no step slice: the state is unchanged)
+                *fired = true;
                 if (rc) return rc;
             } else if (S && F && W != first) {
                 // window already fired before: fold the slice into the first slice without emitting
