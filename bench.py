@@ -192,6 +192,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
+    ap.add_argument("--host-input", action="store_true",
+                    help="hand the engine pinned host columns (PCIe-inclusive rate; never the headline value)")
     ap.add_argument("--exchange", choices=("partials", "raw"), default="partials",
                     help="N > 1: exchange partial accumulators (two-phase) or raw records")
     args = ap.parse_args()
@@ -229,6 +231,8 @@ def main():
     n = args.records
     key, ts, val = gen_columns(n, args.keys, args.rate, rank * n, dev, jitter=wl["jitter"], zipf=wl["zipf"])
     torch.cuda.synchronize()
+    if args.host_input:   # FG_HOST columns: the engine copies each micro-batch H2D on its stream
+        key, ts, val = (x.cpu().pin_memory() for x in (key, ts, val))
 
     maxp = 128
     kg_lo, kg_hi = (rank * maxp + world - 1) // world, ((rank + 1) * maxp - 1) // world
@@ -360,7 +364,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (counter-based splitmix64 stream generated on the GPU, resident in HBM)",
+        "data": "synthetic (counter-based splitmix64 stream generated on the GPU, " + (
+            "handed over as pinned host columns: PCIe-inclusive)" if args.host_input else "resident in HBM)"),
         "config": {
             "workload": wl["desc"],
             "records_per_gpu": n, "keys": args.keys, "records_per_event_second": args.rate,
