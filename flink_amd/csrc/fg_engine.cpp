@@ -191,6 +191,7 @@ struct fg_handle {
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
     int64_t hv_max_chunks = 0;
     DevBuf hist, totals, scan_tmp, counters;
+    DevBuf sink;   // target of the stores of idle lanes (kernels keep their store counts static)
     HostBuf h_counters;
 
     // resident state
@@ -926,6 +927,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.grid = (int)std::max<int64_t>(1, std::min<int64_t>(h->grid, g));
     p.vec = ((uintptr_t)key % 16 == 0 && (uintptr_t)ts % 16 == 0 && (!val || (uintptr_t)val % 16 == 0)) ? 1 : 0;
     p.hist = h->hist.as<uint32_t>();
+    p.sink = h->sink.as<int64_t>();
     set_fast_path(h, &p);
     // two-pass partition when the regions split into 64-bucket coarse groups
     const bool two_pass = h->region_bits >= kFineBits && h->F <= kMaxPart1Fine;
@@ -1373,7 +1375,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
               chk(hp->totals.ensure(4 * ((size_t)hp->F + 1))) &&
               chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F))) &&
               chk(hp->counters.ensure(sizeof(Counters))) && chk(hp->h_counters.ensure(sizeof(Counters))) &&
-              chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) &&
+              chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) && chk(hp->sink.ensure(256)) &&
               chk(hp->h_scalars.ensure(64));
     if (!ok) {
         g_open_error = "device allocation failed";

@@ -100,6 +100,7 @@ struct IngestParams {
     uint16_t* dir;             // [grid * max_tiles][n_coarse + 1] coarse offsets within each tile
     int32_t max_tiles;         // tiles per workgroup segment (ceil(segment / kPart1Tile))
     int32_t n_coarse;          // lanes << (region_bits - kFineBits)
+    int64_t* sink;             // >= 32 B of scratch: idle lanes store here (static store counts)
 };
 
 constexpr int kMaxMergeBatches = 32;         // pipelined merge: staged batches held in LDS

@@ -628,6 +628,7 @@ int32_t part2_group(int32_t max_tiles) {
     return k < 1 ? 1 : (k > 8 ? 8 : k);
 }
 
+template <bool AOS>
 __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t group) {
     constexpr int NF = 1 << kFineBits;
     constexpr int R = kPart2Tile / kPart2Threads;   // 8
@@ -696,7 +697,6 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     }
     __syncthreads();
     const bool has_null = p.vnull != nullptr;
-    const bool aos = p.st_stride == 2;
     // records of a sub-tile: idx = base + u * T + tid; the next sub-tile's loads are issued
     // before this one is ranked, staged and written. The fragment of each idx comes from a
     // per-sub-tile map: every fragment marks its first record in the sub-tile, and an
@@ -732,41 +732,32 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
         s_map4[tid] = make_uint4(e[0] | (e[1] << 16), e[2] | (e[3] << 16), e[4] | (e[5] << 16), e[6] | (e[7] << 16));
         lds_barrier();
     };
-    longlong2 rr[R];
-    uint8_t rn[R];
-    auto load = [&](uint32_t base) {
+    // every lane issues all R loads (past the end: record 0, unused) and all R stores (idle
+    // lanes into p.sink), and the two record buffers alternate statically (the loop is
+    // unrolled by two): the number of memory operations between a prefetch and its use is
+    // then the same on every path, so the wait for it leaves the stores in flight
+    // NULL flags (rare) are gathered into a bit mask at load time
+    auto load = [&](longlong2 (&rr)[R], uint32_t& rn, uint32_t base) {
+        rn = 0;
 #pragma unroll
         for (int u = 0; u < R; u++) {
             const uint32_t idx = base + (uint32_t)(u * kPart2Threads + tid);
-            rn[u] = 0;
-            if (idx >= total) continue;
-            const int q = s_map[idx - base];
-            const uint32_t src = s_fsrc[q] + (idx - s_fstart[q]);
+            const bool ok = idx < total;
+            const int q = ok ? (int)s_map[idx - base] : 0;
+            const uint32_t src = ok ? s_fsrc[q] + (idx - s_fstart[q]) : 0u;
             if (FG_DIAG_PART2 & 2) {
                 rr[u] = make_longlong2((long long)src * 0x9E3779B97F4A7C15ll, src);
                 continue;
             }
             rr[u] = p.tmp[src];
-            if (has_null) rn[u] = p.tmp_null[src];
+            if (has_null && p.tmp_null[src] != 0) rn |= 1u << u;
         }
     };
-    if (total > 0) {
-        build_map(0);
-        load(0);
-        lds_barrier();   // every wave has read the map before build_map(kPart2Tile) clears it
-    }
-    for (uint32_t base = 0; base < total; base += kPart2Tile) {
-        longlong2 cr[R];
-        uint8_t cn[R];
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            cr[u] = rr[u];
-            cn[u] = rn[u];
-        }
-        if (base + kPart2Tile < total) {
-            if (!(FG_DIAG_PART2 & 4)) build_map(base + kPart2Tile);
-            load(base + kPart2Tile);
-        }
+    // sub-tile at `base` (records in cr, NULL bits cn); loads the next one into nr/nn
+    // first; cr is reused for the write-out once its records are staged in LDS
+    auto step = [&](longlong2 (&cr)[R], const uint32_t cn, longlong2 (&nr)[R], uint32_t& nn, uint32_t base) {
+        if (base + kPart2Tile < total && !(FG_DIAG_PART2 & 4)) build_map(base + kPart2Tile);
+        load(nr, nn, base + kPart2Tile);
         uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
 #pragma unroll
         for (int u = 0; u < R; u++) {
@@ -792,34 +783,43 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             if (rf[u] == 0xffffffffu) continue;
             const uint32_t slot = s_off[rf[u] & (NF - 1)] + (rf[u] >> 6);
             s_rec[slot] = cr[u];
-            s_fb[slot] = (uint8_t)((rf[u] & (NF - 1)) | (cn[u] ? 0x80u : 0u));
+            s_fb[slot] = (uint8_t)((rf[u] & (NF - 1)) | (((cn >> u) & 1u) << 7));
         }
         lds_barrier();
         // write-out: all of the thread's LDS reads first, then its stores back to back
         const uint32_t sub = s_off[NF];
         uint32_t wfb[R];
+        longlong2 (&wv)[R] = cr;
 #pragma unroll
         for (int u = 0; u < R; u++) {
             const uint32_t i = (uint32_t)(u * kPart2Threads + tid);
-            wfb[u] = 0xffffffffu;
-            if (i < sub) {
-                wfb[u] = s_fb[i];
-                cr[u] = s_rec[i];
-            }
+            const bool live = i < sub;
+            wfb[u] = live ? (uint32_t)s_fb[i] : 0xffffffffu;
+            wv[u] = s_rec[live ? i : 0];
         }
 #pragma unroll
         for (int u = 0; u < R; u++) {
-            if (wfb[u] == 0xffffffffu) continue;
+            const bool live = wfb[u] != 0xffffffffu;
             const uint32_t i = (uint32_t)(u * kPart2Threads + tid);
             const int f = (int)(wfb[u] & (NF - 1));
-            const int64_t pos = (int64_t)(s_cur[f] + (i - s_off[f]));
+            const int64_t pos = live ? (int64_t)(s_cur[f] + (i - s_off[f])) : 0;
             if (FG_DIAG_PART2 & 1) {
-                if (cr[u].x == 0x5555 && cr[u].y == 0x7777) p.st_rec[0] = pos;   // keep the reads alive
+                if (wv[u].x == 0x5555 && wv[u].y == 0x7777) p.st_rec[0] = pos;   // keep the reads alive
                 continue;
             }
-            if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * pos) = cr[u];
-            else p.st_rec[pos] = cr[u].x;
-            if (has_null) p.st_null[pos] = (uint8_t)(wfb[u] >> 7);
+            if constexpr (AOS) *reinterpret_cast<longlong2*>(live ? p.st_rec + 2 * pos : p.sink) = wv[u];
+            else *(live ? p.st_rec + pos : p.sink) = wv[u].x;
+        }
+        if (has_null) {
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                const bool live = wfb[u] != 0xffffffffu;
+                const uint32_t i = (uint32_t)(u * kPart2Threads + tid);
+                const int f = (int)(wfb[u] & (NF - 1));
+                uint8_t* dst = live ? p.st_null + (int64_t)(s_cur[f] + (i - s_off[f]))
+                                    : reinterpret_cast<uint8_t*>(p.sink);
+                *dst = (uint8_t)(wfb[u] >> 7);
+            }
         }
         lds_barrier();
         if (tid < NF) {
@@ -827,6 +827,18 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             s_cnt[tid] = 0;
         }
         lds_barrier();
+    };
+    longlong2 ra[R], rb[R];
+    uint32_t na = 0, nb = 0;
+    if (total > 0) {
+        build_map(0);
+        load(ra, na, 0);
+        lds_barrier();   // every wave has read the map before build_map(kPart2Tile) clears it
+    }
+    for (uint32_t base = 0; base < total; base += 2 * kPart2Tile) {
+        step(ra, na, rb, nb, base);
+        if (base + kPart2Tile >= total) break;
+        step(rb, nb, ra, na, base + kPart2Tile);
     }
 }
 
@@ -850,7 +862,8 @@ hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
     const int32_t group = part2_group(p.max_tiles);
     const int64_t units = (int64_t)nslots * (1 << (p.region_bits - kFineBits)) * ((p.grid + group - 1) / group);
     if (units == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_part2, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+    if (p.st_stride == 2) hipLaunchKernelGGL(k_part2<true>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+    else hipLaunchKernelGGL(k_part2<false>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
     return hipGetLastError();
 }
 
