@@ -130,6 +130,25 @@ def watermarks_for(lo, hi, rate_s, every, delay=0, jitter=0):
     return out
 
 
+def measure_copy_peak(dev, nbytes=2 << 30, reps=5):
+    """Device-to-device copy bandwidth (read + write bytes / time) on this GPU."""
+    try:
+        a = torch.empty(nbytes // 8, dtype=torch.int64, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+        del a, b
+        return gbs
+    except RuntimeError:
+        return None
+
+
 def cpu_baseline(args, rate):
     """The oracle (C restatement of the reference operator) on the host cores: one instance
     per core, records routed by key group, on a bounded prefix of the same stream."""
@@ -349,6 +368,7 @@ def main():
         except Exception:
             traffic = None
 
+    copy_gbs = measure_copy_peak(dev)
     total_records = world * n * args.steps
     value = total_records / el
     b_alg = 24 * total_records + 48 * tot_rows
@@ -377,7 +397,11 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom_name,
                      "avg_launch_ms": avg_s * 1e3,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     # SURVEY.md 8d second denominator: a device-to-device copy measured on this box
+                     "copy_peak_gbs": copy_gbs,
+                     "frac_of_copy_peak": achieved / copy_gbs if copy_gbs else None,
+                     "actual_gbs": traffic / avg_s / 1e9 if traffic else None},
         "job_roofline_frac": b_alg / el / (world * HBM_PEAK_GBS * 1e9),
         "rows_fired": tot_rows,
         "late_dropped": late,
