@@ -77,6 +77,7 @@ class FgKernelStat(C.Structure):
 
 FLAG_KERNEL_TIMING = 1
 FLAG_LOCAL_PARTIALS = 2
+FLAG_PROCTIME = 4
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (

@@ -180,6 +180,7 @@ struct fg_handle {
     DevBuf acc_key, acc_cs, acc_cn, acc_sum;
     DevBuf in_cs, in_cv, in_sum, in_slice;
     bool local = false;     // FG_FLAG_LOCAL_PARTIALS: fired slices emit partial accumulators
+    bool proctime = false;  // FG_FLAG_PROCTIME: processing-time windows, nothing is late
     std::vector<std::unique_ptr<Staged>> passes;       // live passes
     std::vector<std::unique_ptr<Staged>> pass_pool;
     int64_t anchor_start = JMIN;   // a recent slice start: base of the 32-bit rowtime fast path
@@ -869,7 +870,7 @@ void set_fast_path(fg_handle* h, IngestParams* p) {
     p->tbase = (int64_t)tb;
     p->div_m = ~0ull / (uint64_t)S + 1;
     p->qbase = floor_div(p->tbase, S) + 1;
-    __int128 lim = (__int128)(h->local ? JMIN : h->current_progress) + 1 + h->w.tz;
+    __int128 lim = (__int128)(h->local || h->proctime ? JMIN : h->current_progress) + 1 + h->w.tz;
     if (lim < (__int128)JMIN) lim = JMIN;
     if (lim > (__int128)JMAX) lim = JMAX;
     p->fired_lim = (int64_t)lim;
@@ -917,7 +918,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.ts = ts;
     p.val = val;
     p.vnull = vnull;
-    p.progress = h->local ? JMIN : h->current_progress;   // the local phase drops nothing
+    p.progress = h->local || h->proctime ? JMIN : h->current_progress;   // local phase / proctime: nothing is late
     p.lanes = h->lanes;
     p.region_bits = h->region_bits;
     p.filter_lo = flo;
@@ -1307,6 +1308,11 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         c.aggs[1] = FG_AGG_COUNT;
         c.aggs[2] = FG_AGG_SUM;
     }
+    const bool proctime = (c.flags & FG_FLAG_PROCTIME) != 0;
+    if (proctime && (c.mode != FG_MODE_SQL || local)) {
+        g_open_error = "FG_FLAG_PROCTIME is for SQL window aggregation (not DataStream or the local phase)";
+        return FG_EINVAL;
+    }
     std::string msg;
     int rc = validate(&c, &msg);
     if (rc) {
@@ -1325,6 +1331,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     std::unique_ptr<fg_handle> h(new fg_handle());
     h->cfg = c;
     h->local = local;
+    h->proctime = proctime;
     h->device = cfg->device_id;
     h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
     if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {

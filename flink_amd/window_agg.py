@@ -78,7 +78,8 @@ class WindowAggOperator:
     def __init__(self, window: Window, aggs=("count_star", "count", "sum", "avg"), val_type: str = "f64",
                  mode: str = "sql", shift_tz_offset_ms: int = 0, expected_keys: int = 1 << 16,
                  buffer_records: int = 1 << 22, device: int = 0, max_parallelism: int = 128,
-                 key_group_range=(0, 127), kernel_timing: bool = False, local_partials: bool = False):
+                 key_group_range=(0, 127), kernel_timing: bool = False, local_partials: bool = False,
+                 proctime: bool = False):
         """local_partials: the local phase of the two-phase aggregation
         (LocalSlicingWindowAggOperator + LocalAggCombiner): process_watermark returns one
         partial accumulator row per (key, fired slice) with columns count_star, count, sum
@@ -106,7 +107,8 @@ class WindowAggOperator:
         cfg.max_parallelism = int(max_parallelism)
         cfg.key_group_start, cfg.key_group_end = int(key_group_range[0]), int(key_group_range[1])
         cfg.device_id = int(device)
-        cfg.flags = (L.FLAG_KERNEL_TIMING if kernel_timing else 0) | (L.FLAG_LOCAL_PARTIALS if local_partials else 0)
+        cfg.flags = ((L.FLAG_KERNEL_TIMING if kernel_timing else 0) | (L.FLAG_LOCAL_PARTIALS if local_partials else 0)
+                     | (L.FLAG_PROCTIME if proctime else 0))
         cfg.expected_keys = int(expected_keys)
         cfg.buffer_records = int(buffer_records)
         self.cfg = cfg

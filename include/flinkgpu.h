@@ -87,7 +87,12 @@ enum fg_flags {
      * partial accumulator row per key instead of window rows: window_start/window_end = the
      * slice, agg[0] = COUNT(*), agg[1] = COUNT(v), agg[2] = SUM bits (0 when COUNT(v) = 0).
      * fg_config.aggs is ignored (the global operator's list applies). */
-    FG_FLAG_LOCAL_PARTIALS = 2
+    FG_FLAG_LOCAL_PARTIALS = 2,
+    /* SQL processing-time windows (SliceAssigner.isEventTime() == false,
+     * AbstractWindowAggProcessor.java:137-140): `rowtime` carries each record's processing
+     * time, nothing is late, fg_advance_progress takes the current processing time. Records
+     * are expected at or after the last progress (as processing time is). */
+    FG_FLAG_PROCTIME = 4
 };
 
 #define FG_MAX_AGGS 8

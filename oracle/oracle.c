@@ -465,7 +465,7 @@ static void buffer_flush(or_op* op) {
         or_acc* acc = state_put(op, key, window);        /* value(window) ?: createAccumulators */
         for (int64_t r = op->be_head[ei]; r >= 0; r = op->br_next[r])
             acc_accumulate(acc, vt, op->br_val[r], op->br_null[r]);   /* arrival order */
-        if (!is_window_fired(op, window, op->timer_wm))   /* step 5 (:101-110) */
+        if (!op->cfg.proctime && !is_window_fired(op, window, op->timer_wm))   /* step 5 (:101-110), event time */
             register_window_timer(op, key, window);
     }
     pmap_free(&op->buf_map);
@@ -479,6 +479,12 @@ static void buffer_flush(or_op* op) {
 /* AbstractWindowAggProcessor.processElement  TR/operators/aggregate/window/processors/AbstractWindowAggProcessor.java:135-165 */
 static int sql_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits, uint8_t isnull) {
     int64_t slice_end = or_assign_slice_end(op, ts);
+    if (op->cfg.proctime) {
+        /* :137-140 processing time: a timer per element at its slice, never late */
+        register_window_timer(op, key, slice_end);
+        buffer_add(op, key, slice_end, vbits, isnull);
+        return 0;
+    }
     if (is_window_fired(op, slice_end, op->current_progress)) {
         int64_t last = or_get_last_window_end(op, slice_end);
         if (is_window_fired(op, last, op->current_progress)) return 1;   /* dropped */

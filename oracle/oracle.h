@@ -39,6 +39,8 @@ typedef struct or_config {
     int64_t tz_offset_ms;     /* fixed-offset shift time zone (no DST); 0 = UTC */
     int32_t val_type;         /* OR_VAL_* */
     int32_t count_star_index; /* >= 0 when the agg list holds COUNT(*) (required for HOP) */
+    int32_t proctime;         /* SQL processing-time windows (assigner isEventTime() == false) */
+    int32_t reserved0;
 } or_config;
 
 /* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v). */

@@ -33,6 +33,8 @@ class Config(C.Structure):
         ("tz_offset_ms", C.c_int64),
         ("val_type", C.c_int32),
         ("count_star_index", C.c_int32),
+        ("proctime", C.c_int32),
+        ("reserved0", C.c_int32),
     ]
 
 
@@ -139,8 +141,9 @@ class OracleOperator:
     prepareSnapshotPreBarrier / snapshot-restore, with fired rows collected."""
 
     def __init__(self, mode=MODE_SQL, kind=TUMBLE, size=1000, slide=0, offset=0, tz_offset_ms=0,
-                 val_type=VAL_F64, count_star_index=0, _handle=None):
-        self.cfg = Config(mode, kind, size, slide, offset, tz_offset_ms, val_type, count_star_index)
+                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None):
+        self.cfg = Config(mode, kind, size, slide, offset, tz_offset_ms, val_type, count_star_index,
+                          1 if proctime else 0, 0)
         L = lib()
         if _handle is None:
             err = C.create_string_buffer(512)

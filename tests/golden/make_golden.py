@@ -117,6 +117,87 @@ def slicing_operator_fixtures():
                         val_type="i64", count_star_index=-1),
             columns=["key", "sum", "count", "window_start", "window_end"],
             events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=2))
+    out += proctime_fixtures()
+    return out
+
+
+# Processing-time variants (:224-343, :454-587, :690-767): a record's time is the harness's
+# processing time when it arrives (its rowtime field is ignored); setProcessingTime(t) fires
+# the processing-time timers <= t, i.e. advances progress to t. Processing times are
+# epochMills(shiftTimeZone, local) = utc_ms(local) - tz; window bounds are local times.
+def proctime_fixtures():
+    out = []
+    H = 3600 * 1000
+    for tzname, tz in (("UTC", 0), ("Asia/Shanghai", SHANGHAI)):
+        P = lambda s: utc_ms(s) - tz
+        U = utc_ms
+        # testProcessingTimeHoppingWindows :224-343 (hop 3h/1h, countStarIndex 1)
+        ev = []
+        steps = []
+        t = P("1970-01-01T00:00:00.003")
+        ev += [E(2, 1, t)]
+        ev.append(WM(P("1970-01-01T01:00:00"))); steps.append((len(ev) - 1, [[2, 1, 1, U("1969-12-31T22:00:00"), U("1970-01-01T01:00:00")]]))
+        t = P("1970-01-01T01:00:00")
+        ev += [E(2, 1, t), E(2, 1, t)]
+        ev.append(WM(P("1970-01-01T02:00:00"))); steps.append((len(ev) - 1, [[2, 3, 3, U("1969-12-31T23:00:00"), U("1970-01-01T02:00:00")]]))
+        t = P("1970-01-01T02:00:00")
+        ev += [E(1, 1, t), E(1, 1, t)]
+        ev.append(WM(P("1970-01-01T03:00:00"))); steps.append((len(ev) - 1, [[2, 3, 3, U("1970-01-01T00:00:00"), U("1970-01-01T03:00:00")],
+                                                                             [1, 2, 2, U("1970-01-01T00:00:00"), U("1970-01-01T03:00:00")]]))
+        t = P("1970-01-01T03:00:00")
+        ev += [E(1, 1, t), E(1, 1, t), E(1, 1, t)]
+        ev.append(WM(P("1970-01-01T07:00:00"))); steps.append((len(ev) - 1, [[2, 2, 2, U("1970-01-01T01:00:00"), U("1970-01-01T04:00:00")],
+                                                                             [1, 5, 5, U("1970-01-01T01:00:00"), U("1970-01-01T04:00:00")],
+                                                                             [1, 5, 5, U("1970-01-01T02:00:00"), U("1970-01-01T05:00:00")],
+                                                                             [1, 3, 3, U("1970-01-01T03:00:00"), U("1970-01-01T06:00:00")]]))
+        out.append(dict(
+            name=f"sql_proctime_hop_3h_1h_{tzname}", source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:224-343",
+            config=dict(mode="sql", kind="hop", size=3 * H, slide=H, offset=0, tz_offset_ms=tz,
+                        val_type="i64", count_star_index=1, proctime=True),
+            columns=["key", "sum", "count", "window_start", "window_end"],
+            events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
+
+        # testProcessingTimeCumulativeWindows :454-587 (cumulate 1 day / 8h)
+        ev = []
+        steps = []
+        ev += [E(2, 1, P("1970-01-01T00:00:00.003"))]
+        ev.append(WM(P("1970-01-01T08:00:00"))); steps.append((len(ev) - 1, [[2, 1, 1, U("1970-01-01T00:00:00"), U("1970-01-01T08:00:00")]]))
+        t = P("1970-01-01T08:00:00")
+        ev += [E(2, 1, t), E(2, 1, t)]
+        ev.append(WM(P("1970-01-01T16:00:00"))); steps.append((len(ev) - 1, [[2, 3, 3, U("1970-01-01T00:00:00"), U("1970-01-01T16:00:00")]]))
+        t = P("1970-01-01T16:00:00")
+        ev += [E(1, 1, t), E(1, 1, t)]
+        ev.append(WM(P("1970-01-02T00:00:00"))); steps.append((len(ev) - 1, [[2, 3, 3, U("1970-01-01T00:00:00"), U("1970-01-02T00:00:00")],
+                                                                             [1, 2, 2, U("1970-01-01T00:00:00"), U("1970-01-02T00:00:00")]]))
+        t = P("1970-01-02T00:00:00")
+        ev += [E(1, 1, t), E(2, 1, t), E(1, 1, t)]
+        ev.append(WM(P("1970-01-03T08:00:00"))); steps.append((len(ev) - 1, [
+            [1, 2, 2, U("1970-01-02T00:00:00"), U("1970-01-02T08:00:00")], [2, 1, 1, U("1970-01-02T00:00:00"), U("1970-01-02T08:00:00")],
+            [1, 2, 2, U("1970-01-02T00:00:00"), U("1970-01-02T16:00:00")], [2, 1, 1, U("1970-01-02T00:00:00"), U("1970-01-02T16:00:00")],
+            [1, 2, 2, U("1970-01-02T00:00:00"), U("1970-01-03T00:00:00")], [2, 1, 1, U("1970-01-02T00:00:00"), U("1970-01-03T00:00:00")]]))
+        out.append(dict(
+            name=f"sql_proctime_cumulate_1d_8h_{tzname}", source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:454-587",
+            config=dict(mode="sql", kind="cumulate", size=24 * H, slide=8 * H, offset=0, tz_offset_ms=tz,
+                        val_type="i64", count_star_index=-1, proctime=True),
+            columns=["key", "sum", "count", "window_start", "window_end"],
+            events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
+
+        # testProcessingTimeTumblingWindows :690-767 (tumble 5h)
+        ev = []
+        steps = []
+        t = P("1970-01-01T00:00:00.003")
+        ev += [E(2, 1, t), E(2, 1, t), E(2, 1, t), E(1, 1, t), E(1, 1, t)]
+        ev.append(WM(P("1970-01-01T05:00:00"))); steps.append((len(ev) - 1, [[2, 3, 3, U("1970-01-01T00:00:00"), U("1970-01-01T05:00:00")],
+                                                                             [1, 2, 2, U("1970-01-01T00:00:00"), U("1970-01-01T05:00:00")]]))
+        t = P("1970-01-01T05:00:00")
+        ev += [E(1, 1, t), E(1, 1, t), E(1, 1, t)]
+        ev.append(WM(P("1970-01-01T10:00:01"))); steps.append((len(ev) - 1, [[1, 3, 3, U("1970-01-01T05:00:00"), U("1970-01-01T10:00:00")]]))
+        out.append(dict(
+            name=f"sql_proctime_tumble_5h_{tzname}", source="TRT/operators/aggregate/window/SlicingWindowAggOperatorTest.java:690-767",
+            config=dict(mode="sql", kind="tumble", size=5 * H, slide=0, offset=0, tz_offset_ms=tz,
+                        val_type="i64", count_star_index=-1, proctime=True),
+            columns=["key", "sum", "count", "window_start", "window_end"],
+            events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
     return out
 
 

@@ -22,7 +22,7 @@ class GpuOperator:
         self.op = _op or F.WindowAggOperator(
             window_of(cfg), aggs=("count_star", "count", "sum", "avg"), val_type=cfg["val_type"],
             mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
-            buffer_records=buffer_records, kernel_timing=kernel_timing)
+            buffer_records=buffer_records, kernel_timing=kernel_timing, proctime=cfg.get("proctime", False))
         self._rows = []
 
     def process_batch(self, key, ts, val=None, isnull=None):
@@ -39,7 +39,7 @@ class GpuOperator:
         new = GpuOperator(self.cfg, _op=F.WindowAggOperator(
             self.op.window, aggs=self.op.aggs, val_type=self.cfg["val_type"], mode=self.cfg["mode"],
             shift_tz_offset_ms=self.cfg.get("tz_offset_ms", 0), expected_keys=self.op.cfg.expected_keys,
-            buffer_records=self.op.cfg.buffer_records))
+            buffer_records=self.op.cfg.buffer_records, proctime=self.cfg.get("proctime", False)))
         new.op.restore_state(img, wm)
         new._late_base = self.late_dropped
         return new

@@ -70,3 +70,10 @@ def test_no_device_is_loud():
     with pytest.raises(F.FlinkGpuError) as ei:
         F.WindowAggOperator(F.tumbling(1000))
     assert ei.value.code == L.FG_EDEVICE
+
+
+def test_proctime_only_for_sql():
+    """FG_FLAG_PROCTIME is validated before any device call."""
+    import flink_amd as F
+    with pytest.raises(F.WindowSpecError):
+        F.WindowAggOperator(F.tumbling(1000), mode="datastream", val_type="i64", proctime=True)

@@ -23,7 +23,7 @@ def gpu_mk(cfg, **kw):
 def oracle_mk(O, cfg):
     return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"], slide=cfg["slide"],
                             offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"], val_type=VT[cfg["val_type"]],
-                            count_star_index=cfg["count_star_index"])
+                            count_star_index=cfg["count_star_index"], proctime=cfg.get("proctime", False))
 
 
 @pytest.mark.parametrize("case", OP_CASES, ids=[c["name"] for c in OP_CASES])
@@ -130,6 +130,11 @@ STREAM_CASES = [
     ("big_units_i64_nulls_ooo", cfg_of("tumble", 1000, vt="i64"), dict(n=16_000_000, keys=500_000, batch=8_000_000,
                                                                        delay=600, jitter=500, null_frac=0.1,
                                                                        rate_per_ms=10_000)),
+    # processing-time windows (records carry their arrival time, nothing is late)
+    ("proctime_hop_f64", dict(cfg_of("hop", 3000, 1000), proctime=True), dict(n=600_000, keys=100_000, batch=50_000,
+                                                                              delay=0, jitter=0)),
+    ("proctime_cumulate_i64", dict(cfg_of("cumulate", 4000, 1000, vt="i64"), proctime=True),
+     dict(n=400_000, keys=20_000, batch=20_000, delay=0, jitter=0)),
     # Zipf(1.1) hot keys: regions over the skew threshold take the chunked heavy pass
     ("zipf_tumble_f64", cfg_of("tumble", 1000), dict(n=3_000_000, keys=100_000, batch=1_000_000, delay=0, jitter=0,
                                                       rate_per_ms=2_000, zipf=1.1)),

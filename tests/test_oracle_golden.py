@@ -11,7 +11,8 @@ def make_oracle(O):
     def mk(cfg):
         return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"],
                                 slide=cfg["slide"], offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"],
-                                val_type=VT[cfg["val_type"]], count_star_index=cfg["count_star_index"])
+                                val_type=VT[cfg["val_type"]], count_star_index=cfg["count_star_index"],
+                                proctime=cfg.get("proctime", False))
     return mk
 
 
