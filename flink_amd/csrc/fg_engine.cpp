@@ -694,7 +694,8 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     p.overflow = h->scalars.as<unsigned int>();
     {
         KTimer kt(h, K_FIRE, 0);
-        HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+        if (refs.size() == 1 && !dst) HIPCHK(h, launch_emit_table(p, refs[0], h->stream));
+        else HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
     }
     if (dst) dst->upper = ub;
     if (defer) {

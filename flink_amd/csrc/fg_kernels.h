@@ -217,6 +217,8 @@ hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int3
 // persistent merge over the P regions: `workgroups` <= P workgroups, each a strided set of
 // regions (p.compact: two workgroups fit a CU)
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s);
+// fire one window straight from a single slice table (no combine): p's emit fields
+hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
 hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s);
 hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s);

@@ -1135,6 +1135,38 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C>& t, int64_t k, uint3
     const uint32_t nx = home + kBucket;
     return lds_find_or_insert_from<C>(t, k, nx >= S_ ? 0u : nx, full);
 }
+// one fired row: key, window bounds, (DataStream) output timestamp and the aggregates of
+// the accumulator {COUNT(*), NULL count, sum} (a6: Count1/Count/Sum/AvgAggFunction)
+__device__ __forceinline__ void write_row(const MergeParams& p, unsigned long long o, int64_t key,
+                                          unsigned long long cs, unsigned long long cn, int64_t sum, int vt) {
+    p.out_key[o] = key;
+    p.out_ws[o] = p.wstart;
+    p.out_we[o] = p.wend;
+    if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
+    const int64_t cv = (int64_t)(cs - cn);
+    uint8_t nm = 0;
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; a++) {
+        if (a >= p.num_aggs) break;
+        int64_t v = 0;
+        switch (p.aggs[a]) {
+            case 0: v = (int64_t)cs; break;   // COUNT(*)
+            case 1: v = cv; break;            // COUNT(v)
+            case 2:                           // SUM(v): NULL when no non-null value
+                if (cv == 0) nm |= (uint8_t)(1u << a);
+                else v = sum;
+                break;
+            default:                          // AVG(v): count == 0 ? NULL : sum / count
+                if (cv == 0) nm |= (uint8_t)(1u << a);
+                else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
+                else v = sum / cv;
+                break;
+        }
+        p.out_agg[a][o] = v;
+    }
+    p.out_null[o] = nm;
+}
+
 constexpr int kSrcU = 2;          // source-table entries per thread per round (wide merge)
 constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
 
@@ -1571,35 +1603,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 dbase[2 * cap + at] = (int64_t)cn;
                 dbase[3 * cap + at] = sum;
             }
-            if (write_out) {
-                const unsigned long long o = obase + at;
-                p.out_key[o] = key;
-                p.out_ws[o] = p.wstart;
-                p.out_we[o] = p.wend;
-                if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
-                const int64_t cv = (int64_t)(cs - cn);
-                uint8_t nm = 0;
-#pragma unroll
-                for (int a = 0; a < kMaxAggs; a++) {
-                    if (a >= p.num_aggs) break;
-                    int64_t v = 0;
-                    switch (p.aggs[a]) {
-                        case 0: v = (int64_t)cs; break;   // COUNT(*)
-                        case 1: v = cv; break;            // COUNT(v)
-                        case 2:                           // SUM(v): NULL when no non-null value
-                            if (cv == 0) nm |= (uint8_t)(1u << a);
-                            else v = sum;
-                            break;
-                        default:                          // AVG(v): count == 0 ? NULL : sum / count
-                            if (cv == 0) nm |= (uint8_t)(1u << a);
-                            else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
-                            else v = sum / cv;
-                            break;
-                    }
-                    p.out_agg[a][o] = v;
-                }
-                p.out_null[o] = nm;
-            }
+            if (write_out) write_row(p, obase + at, key, cs, cn, sum, vt);
         }
         if (tid == 0 && write_dst) {
             const uint32_t total = s_total;
@@ -1614,6 +1618,34 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     if (p.stamps && (tid & 63) == 0)
         for (int i = 0; i < 4; i++) atomicAdd(&p.stamps[i], st_acc[i]);
 #endif
+}
+
+// Fire straight from one slice table (a window whose state is a single table and is not
+// written back: tumble windows flushed before their fire, cumulate windows re-fired with
+// no new step slice, hop windows of one slice): no LDS combine, one row per entry.
+constexpr int kEmitThreads = 256;
+__global__ __launch_bounds__(kEmitThreads) void k_emit_table(MergeParams p, TableRef t) {
+    __shared__ unsigned long long s_base;
+    const int r = blockIdx.x;
+    const uint32_t n = gbl(t.counts)[r];
+    if (n == 0) return;
+    if (threadIdx.x == 0) {
+        const unsigned long long b = atomicAdd(p.out_count, (unsigned long long)n);
+        s_base = b;
+        if ((int64_t)(b + n) > p.out_cap) atomicOr(p.overflow, 2u);
+    }
+    __syncthreads();
+    const unsigned long long b = s_base;
+    if ((int64_t)(b + n) > p.out_cap) return;
+    const auto base = gbl(t.base + (int64_t)r * 4 * kRegionCap);
+    for (uint32_t i = threadIdx.x; i < n; i += kEmitThreads)
+        write_row(p, b + i, base[i], (unsigned long long)base[kRegionCap + i], (unsigned long long)base[2 * kRegionCap + i],
+                  base[3 * kRegionCap + i], p.val_type);
+}
+
+hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_t s) {
+    hipLaunchKernelGGL(k_emit_table, dim3(1u << p.region_bits), dim3(kEmitThreads), 0, s, p, t);
+    return hipGetLastError();
 }
 
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {
