@@ -25,6 +25,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <set>
 #include <vector>
 
 #include "../../include/flinkgpu.h"
@@ -211,6 +212,7 @@ struct fg_handle {
 
     // fired rows
     int64_t out_cap = 0, out_n = 0, pending_out = 0;
+    std::set<int64_t> fused_fired;   // window ends fired by a fused flush in the current advance
     int64_t q_guess = kEmptyLane;   // first slice of the next batch's first ingest pass (kEmptyLane: all)
     DevBuf o_key, o_ws, o_we, o_null, o_rt;
     DevBuf o_agg[FG_MAX_AGGS];
@@ -492,8 +494,10 @@ int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, Heav
 // and fired in the same pass: its rows are emitted straight from LDS and the slice is
 // never written back (SliceUnsharedWindowAggProcessor.fireWindow + clearWindow, :46-54 /
 // AbstractWindowAggProcessor.java:200-206).
-int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire) {
-    if (sel.empty()) return FG_OK;
+int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* fire) {
+    if (sel_in.empty()) return FG_OK;
+    std::vector<int> sel = sel_in;   // slice order: windows fired by the flush fire in order
+    std::sort(sel.begin(), sel.end(), [&](int a, int b) { return h->lane[a].q < h->lane[b].q; });
     if (h->out_count_reset) HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
     else HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
     std::vector<int64_t> fired_tables;
@@ -528,21 +532,53 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         rc = table_get(h, se, true, &t);
         if (rc) return rc;
         const int64_t trig = trigger_time(h->w, se);
+        const bool due = fire && se != JMAX && trig > fire->prev && trig <= fire->wm;
         // local phase: every fired slice lane emits its partial accumulators
-        const bool fire_now =
-            fire && (h->local || (h->w.kind == TUMBLE && se != JMAX && trig > fire->prev && trig <= fire->wm));
-        if (fire_now) {
+        const bool fire_now = fire && (h->local || (h->w.kind == TUMBLE && due));
+        // CUMULATE: the step window W = se fires now -- combine the staged slice with the
+        // first slice's state, write the state back (unless W is the last window) and emit
+        // W in one pass, instead of a flush into the slice table and a fire re-reading it
+        // (CumulativeSliceAssigner.mergeSlices :359-370 + SliceSharedWindowAggProcessor.fireWindow)
+        // (only when every earlier step window of this cumulative window fired in an earlier
+        // advance, so that no earlier window still has to fire from the unextended state)
+        bool cum_fire = !h->local && h->w.kind == CUMULATE && due;
+        if (cum_fire) {
+            const int64_t ws0 = window_start(h->w, se);
+            const int64_t prev_w = jsub(se, h->w.slice);
+            cum_fire = se == jadd(ws0, h->w.slice) || trigger_time(h->w, prev_w) <= fire->prev;
+        }
+        SliceTable* F = nullptr;       // first slice's table of W's cumulative window
+        SliceTable* dstt = t;          // table written by this merge (null: none)
+        std::vector<TableRef> srcs;
+        if (t->upper > 0) srcs.push_back(ref_of(t));
+        int64_t cum_first = 0, cum_last = 0;
+        if (cum_fire) {
+            const int64_t ws = window_start(h->w, se);
+            cum_first = jadd(ws, h->w.slice);
+            cum_last = jadd(ws, h->w.size);
+            if (se != cum_first) {
+                rc = table_get(h, cum_first, se != cum_last, &F);
+                if (rc) return rc;
+                if (F && F->upper > 0) srcs.push_back(ref_of(F));
+            }
+            dstt = se == cum_last ? nullptr : (se == cum_first ? t : F);
+        } else if (fire_now) {
+            dstt = nullptr;
+        }
+        int64_t ub_in = ln.fill + ln.acc_fill;
+        for (const TableRef& r : srcs) ub_in += r.base == t->data.as<int64_t>() ? t->upper : (F ? F->upper : 0);
+        const int64_t ub = std::min<int64_t>(ub_in, (int64_t)kRegionCap * h->P);
+        if (fire_now || cum_fire) {
             rc = reset_out_count(h);
             if (rc) return rc;
-            const int64_t ub = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, (int64_t)kRegionCap * h->P);
             rc = ensure_out(h, h->out_n + h->pending_out + ub);
             if (rc) return rc;
             h->pending_out += ub;
         }
-        TableRef tr = ref_of(t);
+        const TableRef tr = dstt ? ref_of(dstt) : TableRef{};
         const TableRef* d_src = nullptr;
-        if (t->upper > 0) {
-            rc = arena_put(h, &tr, 1, &d_src);
+        if (!srcs.empty()) {
+            rc = arena_put(h, srcs.data(), srcs.size(), &d_src);
             if (rc) return rc;
         }
         bool plain = h->st_stride == 2 && !sb.empty() && sb.size() <= (size_t)kMaxMergeBatches;
@@ -550,7 +586,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         MergeParams p{};
         p.region_bits = h->region_bits;
         p.fast_stream = plain ? 1 : 0;
-        p.n_src = t->upper > 0 ? 1 : 0;
+        p.n_src = (int)srcs.size();
         // compact LDS table (two workgroups per CU) when no resident state is read and the
         // COUNT(*) of a key cannot reach 2^32
         p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) ? 1 : 0;
@@ -558,10 +594,10 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         p.n_batches = (int)sb.size();
         p.batches = d_sb;
         p.val_type = h->cfg.val_type;
-        p.has_dst = fire_now ? 0 : 1;
+        p.has_dst = dstt ? 1 : 0;
         p.dst = tr;
         p.emit = 0;
-        if (fire_now) fill_emit(h, p, se);
+        if (fire_now || cum_fire) fill_emit(h, p, se);
         p.overflow = h->scalars.as<unsigned int>();
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
 #ifdef FG_STAMPS
@@ -581,7 +617,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
             p.heavy = hp.heavy;
         }
         {
-            KTimer kt(h, fire_now ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
+            KTimer kt(h, fire_now || cum_fire ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
             HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
         }
         if (skew) {
@@ -619,6 +655,16 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel, const FireRange* fire
         if (fire_now) {
             fired_tables.push_back(se);
             any_emit = true;
+        } else if (cum_fire) {
+            any_emit = true;
+            h->fused_fired.insert(se);   // fire_windows must not fire W again
+            if (dstt) dstt->upper = ub;
+            if (se == cum_last) {        // the cumulative window is complete
+                fired_tables.push_back(se);
+                if (se != cum_first) fired_tables.push_back(cum_first);
+            } else if (se != cum_first) {
+                fired_tables.push_back(se);   // folded into the first slice
+            }
         } else {
             t->upper = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, (int64_t)kRegionCap * h->P);
         }
@@ -798,7 +844,7 @@ int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired) {
                 if (rc) return rc;
             }
             if (!F && !S) continue;
-            if (due(W)) {
+            if (due(W) && !h->fused_fired.count(W)) {
                 std::vector<SliceTable*> srcs;
                 if (F) srcs.push_back(F);
                 if (S) srcs.push_back(S);
@@ -1524,6 +1570,7 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     h->out_n = 0;
     h->pending_out = 0;
     h->out_count_reset = false;
+    h->fused_fired.clear();
     int rc;
     const int64_t prev = h->timer_wm;
     const FireRange fr{prev, wm};
