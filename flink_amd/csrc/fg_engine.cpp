@@ -1011,6 +1011,30 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         HIPCHK(h, launch_ingest_count(p, h->stream));
     }
     HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
+    // per-bucket prefix over workgroups and bucket bases: they depend on the histogram only,
+    // so they are queued before the host waits for the counters (no idle GPU across the
+    // round trip); a pass that stages nothing goes back to the pool
+    std::unique_ptr<Staged> s;
+    if (!h->pass_pool.empty()) {
+        s = std::move(h->pass_pool.back());
+        h->pass_pool.pop_back();
+    } else {
+        s.reset(new Staged());
+    }
+    struct PoolBack {
+        fg_handle* h;
+        std::unique_ptr<Staged>& s;
+        ~PoolBack() {
+            if (s) h->pass_pool.push_back(std::move(s));
+        }
+    } pool_back{h, s};
+    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
+    {
+        KTimer kt(h, K_SCAN, 0);
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), h->F, p.grid, h->stream));
+        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F,
+                                  h->scan_tmp.as<uint32_t>(), h->stream));
+    }
     int rc = sync(h);
     if (rc) return rc;
     DevCounters got;
@@ -1067,21 +1091,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         }
     }
 
-    // per-bucket prefix over workgroups, bucket bases, then scatter into the lane areas
-    std::unique_ptr<Staged> s;
-    if (!h->pass_pool.empty()) {
-        s = std::move(h->pass_pool.back());
-        h->pass_pool.pop_back();
-    } else {
-        s.reset(new Staged());
-    }
-    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
-    {
-        KTimer kt(h, K_SCAN, 0);
-        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), h->F, p.grid, h->stream));
-        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F,
-                                  h->scan_tmp.as<uint32_t>(), h->stream));
-    }
+    // scatter into the lane areas at the bucket bases scanned above
     p.bucket_base = s->bucket_off.as<uint32_t>();
     // staged position of bucket b (lane l) = bucket_base[b] - (records of lanes < l) + lane l's
     // area start + its fill
