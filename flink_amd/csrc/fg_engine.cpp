@@ -1327,7 +1327,7 @@ int validate(const fg_config* c, std::string* msg) {
         if (c->num_aggs < 1 || c->num_aggs > FG_MAX_AGGS)
             snprintf(buf, sizeof buf, "num_aggs must be in [1, %d]", FG_MAX_AGGS);
         for (int a = 0; a < c->num_aggs && !buf[0]; a++)
-            if (c->aggs[a] < FG_AGG_COUNT_STAR || c->aggs[a] > FG_AGG_AVG) snprintf(buf, sizeof buf, "bad agg %d", c->aggs[a]);
+            if (c->aggs[a] < FG_AGG_COUNT_STAR || c->aggs[a] > FG_AGG_SUM0) snprintf(buf, sizeof buf, "bad agg %d", c->aggs[a]);
         if (c->val_type < FG_VAL_NONE || c->val_type > FG_VAL_F64) snprintf(buf, sizeof buf, "bad val_type");
         if (c->val_type == FG_VAL_NONE)
             for (int a = 0; a < c->num_aggs && !buf[0]; a++)

@@ -1156,6 +1156,7 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
                 if (cv == 0) nm |= (uint8_t)(1u << a);
                 else v = sum;
                 break;
+            case 4: v = sum; break;           // SUM0(v): 0-initialised, never NULL
             default:                          // AVG(v): count == 0 ? NULL : sum / count
                 if (cv == 0) nm |= (uint8_t)(1u << a);
                 else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);

@@ -31,8 +31,10 @@ import numpy as np
 
 from . import _lib as L
 
-AGG_NAMES = {L.AGG_COUNT_STAR: "count_star", L.AGG_COUNT: "count", L.AGG_SUM: "sum", L.AGG_AVG: "avg"}
-AGGS = {"count_star": L.AGG_COUNT_STAR, "count": L.AGG_COUNT, "sum": L.AGG_SUM, "avg": L.AGG_AVG}
+AGG_NAMES = {L.AGG_COUNT_STAR: "count_star", L.AGG_COUNT: "count", L.AGG_SUM: "sum", L.AGG_AVG: "avg",
+             L.AGG_SUM0: "sum0"}
+AGGS = {"count_star": L.AGG_COUNT_STAR, "count": L.AGG_COUNT, "sum": L.AGG_SUM, "avg": L.AGG_AVG,
+        "sum0": L.AGG_SUM0}
 
 
 @dataclass(frozen=True)
@@ -220,7 +222,7 @@ class WindowAggOperator:
         fields = [("key", "<i8"), ("window_start", "<i8"), ("window_end", "<i8")]
         for a in self.aggs:
             nm = AGG_NAMES[a]
-            is_f = self.val_type == L.VAL_F64 and a in (L.AGG_SUM, L.AGG_AVG)
+            is_f = self.val_type == L.VAL_F64 and a in (L.AGG_SUM, L.AGG_AVG, L.AGG_SUM0)
             fields.append((nm, "<f8" if is_f else "<i8"))
             fields.append((nm + "_null", "?"))
         if self.mode == L.MODE_DATASTREAM:

@@ -71,8 +71,10 @@ enum fg_mode { FG_MODE_SQL = 0, FG_MODE_DATASTREAM = 1 };
 enum fg_window_kind { FG_TUMBLE = 0, FG_HOP = 1, FG_CUMULATE = 2 };   /* DataStream: TUMBLE, HOP=sliding */
 enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
 /* Aggregates over the single value column (SumAggFunction, Count1AggFunction,
- * CountAggFunction, AvgAggFunction of TP/functions/aggfunctions/). */
-enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3 };
+ * CountAggFunction, AvgAggFunction, Sum0AggFunction of TP/functions/aggfunctions/).
+ * SUM0 (Sum0AggFunction.java:60-63,75-76,97-98,136-137,162-163): 0-initialised, never NULL;
+ * its value is the AVG accumulator's sum. */
+enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3, FG_AGG_SUM0 = 4 };
 /* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
  * producer before it (complete, or an event the stream waits on). They are fully read when
  * fg_add_batch / fg_add_partials return. */

@@ -133,6 +133,9 @@ static int pmap_remove(pmap* m, int64_t a, int64_t b, int64_t* old) {
  *   COUNT(v)  -> CountAggFunction    TP/functions/aggfunctions/CountAggFunction.java:63-83
  *   SUM(v)    -> SumAggFunction      TP/functions/aggfunctions/SumAggFunction.java:58-96 (null init)
  *   AVG(v)    -> AvgAggFunction      TP/functions/aggfunctions/AvgAggFunction.java:64-103 (0 init)
+ *   SUM0(v)   -> Sum0AggFunction     TP/functions/aggfunctions/Sum0AggFunction.java:60-63,75-76
+ *                (0 init :97-98/:136-137/:162-163, sum0 + v for non-null v): the same
+ *                accumulator as AVG's sum, so it is read from avg_sum_* at emit
  * ---------------------------------------------------------------------------------- */
 typedef struct {
     int64_t cnt_star, cnt_val;
@@ -211,14 +214,60 @@ struct or_op {
 int64_t or_window_start_with_offset(int64_t ts, int64_t offset, int64_t size) {
     return jsub(ts, jmod(jadd(jsub(ts, offset), size), size));
 }
-/* toUtcTimestampMills  TimeWindowUtil.java:53-61 (fixed-offset zones only) */
+/* ZoneRules.getOffset(Instant): the offset in force at an epoch instant (zone with
+ * transitions: the offset after the last transition at or before it) */
+static int64_t zone_offset_at(const or_op* op, int64_t instant) {
+    int32_t lo = 0, hi = op->cfg.tz_n;   /* number of transitions <= instant */
+    while (lo < hi) {
+        int32_t mid = (lo + hi) / 2;
+        if (op->cfg.tz_trans[mid] <= instant) lo = mid + 1;
+        else hi = mid;
+    }
+    return op->cfg.tz_offs[lo];
+}
+/* LocalDateTime.atZone(zone).toInstant().toEpochMilli() (ZonedDateTime.ofLocal with no
+ * preferred offset): the unique valid offset; in an overlap the earlier one (the offset
+ * before the transition); in a gap the local time moves later by the gap length and takes
+ * the offset after, i.e. epoch = local - offset before. */
+static int64_t zone_local_to_epoch(const or_op* op, int64_t local) {
+    const int64_t W = 20LL * 3600 * 1000;   /* |offset| <= 18 h */
+    const int32_t n = op->cfg.tz_n;
+    const int64_t* T = op->cfg.tz_trans;
+    const int64_t* O = op->cfg.tz_offs;
+    int32_t k = 0;   /* first offset region that may hold local - offset: transitions <= local - W */
+    while (k < n && T[k] <= jsub(local, W)) k++;
+    for (; k <= n; k++) {
+        const int64_t e = jsub(local, O[k]);
+        const int lo_ok = k == 0 || T[k - 1] <= e;
+        const int hi_ok = k == n || e < T[k];
+        if (lo_ok && hi_ok) return e;                 /* first valid = earlier offset */
+        if (k < n && T[k] > jadd(local, W)) break;
+        if (k < n && e >= T[k] && jsub(local, O[k + 1]) < T[k]) return e;   /* gap at transition k */
+    }
+    return jsub(local, O[n]);
+}
+/* toUtcTimestampMills  TimeWindowUtil.java:53-61 */
 static inline int64_t to_utc(const or_op* op, int64_t epoch) {
-    if (op->cfg.tz_offset_ms == 0 || epoch == JMAX) return epoch;
+    if (epoch == JMAX) return epoch;
+    if (op->cfg.tz_n > 0) return jadd(epoch, zone_offset_at(op, epoch));
+    if (op->cfg.tz_offset_ms == 0) return epoch;
     return jadd(epoch, op->cfg.tz_offset_ms);
 }
-/* toEpochMillsForTimer  TimeWindowUtil.java:70-140 (zone without DST -> :137-139) */
+/* toEpochMillsForTimer  TimeWindowUtil.java:70-140: DST zones take the first skipped
+ * instant for a local time in a gap and the later instant for one in an overlap (:107-135);
+ * zones without DST -> toEpochMills (:137-139) */
 static inline int64_t to_epoch_for_timer(const or_op* op, int64_t utc) {
-    if (op->cfg.tz_offset_ms == 0 || utc == JMAX) return utc;
+    if (utc == JMAX) return utc;
+    if (op->cfg.tz_n > 0) {
+        if (!op->cfg.tz_use_dst) return zone_local_to_epoch(op, utc);
+        const int64_t HOUR = 3600LL * 1000;
+        int64_t t1 = zone_local_to_epoch(op, utc);
+        int64_t t2 = zone_local_to_epoch(op, jadd(utc, HOUR));
+        if (t1 == t2) return jsub(t1, t1 % HOUR);      /* hasNoEpoch */
+        if (jsub(t2, t1) > HOUR) return jadd(t1, HOUR); /* hasTwoEpochs */
+        return t1;
+    }
+    if (op->cfg.tz_offset_ms == 0) return utc;
     return jsub(utc, op->cfg.tz_offset_ms);
 }
 /* isWindowFired  TimeWindowUtil.java:176-184 */
@@ -233,6 +282,24 @@ int64_t or_next_trigger_watermark(int64_t wm, int64_t interval) {
     int64_t trig = jsub(jadd(start, interval), 1);
     return trig > wm ? trig : jadd(trig, interval);
 }
+/* the same with the operator's zone: the DST branch (:194-199) when useDayLightSaving */
+static int64_t next_trigger(const or_op* op, int64_t wm) {
+    if (!(op->cfg.tz_n > 0 && op->cfg.tz_use_dst)) return or_next_trigger_watermark(wm, op->interval);
+    if (wm == JMAX) return wm;
+    int64_t utc_start = or_window_start_with_offset(to_utc(op, wm), 0, op->interval);
+    int64_t trig = to_epoch_for_timer(op, jsub(jadd(utc_start, op->interval), 1));
+    return trig > wm ? trig : jadd(trig, op->interval);
+}
+
+int64_t or_to_utc(const or_op* op, int64_t epoch) { return to_utc(op, epoch); }
+int64_t or_to_epoch_for_timer(const or_op* op, int64_t local) { return to_epoch_for_timer(op, local); }
+/* toEpochMills  TimeWindowUtil.java:149-157 */
+int64_t or_to_epoch(const or_op* op, int64_t local) {
+    if (local == JMAX) return local;
+    if (op->cfg.tz_n > 0) return zone_local_to_epoch(op, local);
+    return jsub(local, op->cfg.tz_offset_ms);
+}
+int64_t or_next_trigger(const or_op* op, int64_t wm) { return next_trigger(op, wm); }
 
 /* ---------------- SliceAssigners.java ---------------------------------------------- */
 /* assignSliceEnd: Tumbling :164-167, Hopping :231-234, Cumulative :318-321, via
@@ -418,6 +485,8 @@ static void emit_row(or_op* op, int64_t key, int64_t wstart, int64_t wend, const
         r->avg_i = (a->cnt_val == -1 && a->avg_sum_i == JMIN) ? JMIN : a->avg_sum_i / a->cnt_val;
         r->avg_d = a->avg_sum_d / (double)a->cnt_val;
     }
+    r->sum0_i = a->avg_sum_i;   /* Sum0AggFunction.getValueExpression :85 */
+    r->sum0_d = a->avg_sum_d;
     r->out_ts = out_ts;
 }
 
@@ -615,6 +684,17 @@ or_op* or_open(const or_config* cfg, char* err, int errlen) {
     }
     or_op* op = (or_op*)calloc(1, sizeof(or_op));
     op->cfg = *cfg;
+    if (cfg->tz_n > 0) {   /* the operator keeps its own copy of the zone rules */
+        int64_t* tr = (int64_t*)malloc(sizeof(int64_t) * (size_t)cfg->tz_n);
+        int64_t* of = (int64_t*)malloc(sizeof(int64_t) * (size_t)(cfg->tz_n + 1));
+        memcpy(tr, cfg->tz_trans, sizeof(int64_t) * (size_t)cfg->tz_n);
+        memcpy(of, cfg->tz_offs, sizeof(int64_t) * (size_t)(cfg->tz_n + 1));
+        op->cfg.tz_trans = tr;
+        op->cfg.tz_offs = of;
+    } else {
+        op->cfg.tz_n = 0;
+        op->cfg.tz_trans = op->cfg.tz_offs = NULL;
+    }
     switch (cfg->kind) {
         case OR_TUMBLE: op->slice_size = size; op->num_slices = 1; break;
         case OR_HOP: op->slice_size = gcd64(size, slide); op->num_slices = size / op->slice_size; break;
@@ -638,6 +718,7 @@ void or_close(or_op* op) {
     free(op->be_slice); free(op->be_key); free(op->be_head); free(op->be_tail);
     free(op->br_val); free(op->br_null); free(op->br_next);
     free(op->accs); free(op->acc_free); free(op->heap); free(op->rows); free(op->merge_buf);
+    free((void*)op->cfg.tz_trans); free((void*)op->cfg.tz_offs);
     free(op);
 }
 
@@ -661,7 +742,7 @@ void or_process_watermark(or_op* op, int64_t wm) {
             if (op->current_progress >= op->next_trigger_progress) {
                 /* RecordsWindowBuffer.advanceProgress :100-105 */
                 if (is_window_fired(op, op->min_slice_end, wm)) buffer_flush(op);
-                op->next_trigger_progress = or_next_trigger_watermark(wm, op->interval);
+                op->next_trigger_progress = next_trigger(op, wm);
             }
         }
     }

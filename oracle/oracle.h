@@ -40,10 +40,14 @@ typedef struct or_config {
     int32_t val_type;         /* OR_VAL_* */
     int32_t count_star_index; /* >= 0 when the agg list holds COUNT(*) (required for HOP) */
     int32_t proctime;         /* SQL processing-time windows (assigner isEventTime() == false) */
-    int32_t reserved0;
+    int32_t tz_n;             /* > 0: a zone with transitions (DST); tz_offset_ms is then ignored */
+    const int64_t* tz_trans;  /* tz_n transition instants (epoch ms, ascending) */
+    const int64_t* tz_offs;   /* tz_n + 1 offsets (ms): [i] in force before transition i */
+    int32_t tz_use_dst;       /* TimeZone.getTimeZone(zone).useDaylightTime() */
+    int32_t reserved1;
 } or_config;
 
-/* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v). */
+/* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v), SUM0(v). */
 typedef struct or_row {
     int64_t key;
     int64_t window_start;
@@ -57,6 +61,8 @@ typedef struct or_row {
     int32_t sum_null;
     int32_t avg_null;
     int64_t out_ts;     /* DataStream: emitted StreamRecord timestamp (end - 1) */
+    int64_t sum0_i;     /* SUM0 for i64 values (Sum0AggFunction: 0-initialised, never NULL) */
+    double  sum0_d;     /* SUM0 for f64 values                                  */
 } or_row;
 
 typedef struct or_op or_op;
@@ -83,6 +89,12 @@ int64_t or_pending_timers(const or_op* op);
 
 /* --- slice assigner restatement (SliceAssigners.java) ------------------------- */
 int64_t or_assign_slice_end(const or_op* op, int64_t ts);
+/* TimeWindowUtil with the operator's zone: toUtcTimestampMills, toEpochMillsForTimer,
+ * toEpochMills, getNextTriggerWatermark(useDayLightSaving of the zone) */
+int64_t or_to_utc(const or_op* op, int64_t epoch);
+int64_t or_to_epoch_for_timer(const or_op* op, int64_t local);
+int64_t or_to_epoch(const or_op* op, int64_t local);
+int64_t or_next_trigger(const or_op* op, int64_t wm);
 int64_t or_get_window_start(const or_op* op, int64_t window_end);
 int64_t or_get_last_window_end(const or_op* op, int64_t slice_end);
 /* writes up to 2 slices, returns count */

@@ -34,7 +34,11 @@ class Config(C.Structure):
         ("val_type", C.c_int32),
         ("count_star_index", C.c_int32),
         ("proctime", C.c_int32),
-        ("reserved0", C.c_int32),
+        ("tz_n", C.c_int32),
+        ("tz_trans", C.c_void_p),
+        ("tz_offs", C.c_void_p),
+        ("tz_use_dst", C.c_int32),
+        ("reserved1", C.c_int32),
     ]
 
 
@@ -52,6 +56,8 @@ class Row(C.Structure):
         ("sum_null", C.c_int32),
         ("avg_null", C.c_int32),
         ("out_ts", C.c_int64),
+        ("sum0_i", C.c_int64),
+        ("sum0_d", C.c_double),
     ]
 
 
@@ -60,7 +66,7 @@ ROW_DTYPE = np.dtype(
         ("key", "<i8"), ("window_start", "<i8"), ("window_end", "<i8"),
         ("cnt_star", "<i8"), ("cnt_val", "<i8"), ("sum_i", "<i8"), ("sum_d", "<f8"),
         ("avg_i", "<i8"), ("avg_d", "<f8"), ("sum_null", "<i4"), ("avg_null", "<i4"),
-        ("out_ts", "<i8"),
+        ("out_ts", "<i8"), ("sum0_i", "<i8"), ("sum0_d", "<f8"),
     ]
 )
 assert ROW_DTYPE.itemsize == C.sizeof(Row)
@@ -98,7 +104,8 @@ def lib():
         for fn in ("or_late_dropped", "or_state_entries", "or_pending_timers"):
             getattr(L, fn).restype = C.c_int64
             getattr(L, fn).argtypes = [P]
-        for fn in ("or_assign_slice_end", "or_get_window_start", "or_get_last_window_end"):
+        for fn in ("or_assign_slice_end", "or_get_window_start", "or_get_last_window_end", "or_to_utc",
+                   "or_to_epoch_for_timer", "or_to_epoch", "or_next_trigger"):
             getattr(L, fn).restype = C.c_int64
             getattr(L, fn).argtypes = [P, C.c_int64]
         L.or_expired_slices.restype = C.c_int32
@@ -141,9 +148,22 @@ class OracleOperator:
     prepareSnapshotPreBarrier / snapshot-restore, with fired rows collected."""
 
     def __init__(self, mode=MODE_SQL, kind=TUMBLE, size=1000, slide=0, offset=0, tz_offset_ms=0,
-                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None):
+                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None, zone=None):
+        """zone: an IANA zone name whose rules (transitions, daylight saving) replace the fixed
+        tz_offset_ms (TimeWindowUtil with a ZoneId)."""
         self.cfg = Config(mode, kind, size, slide, offset, tz_offset_ms, val_type, count_star_index,
                           1 if proctime else 0, 0)
+        self.zone = zone
+        if zone is not None:
+            from flink_amd.tz import zone_rules
+            tr, of, dst = zone_rules(zone)
+            self._tz = (np.ascontiguousarray(tr), np.ascontiguousarray(of))
+            self.cfg.tz_n = len(tr)
+            self.cfg.tz_trans = self._tz[0].ctypes.data if len(tr) else None
+            self.cfg.tz_offs = self._tz[1].ctypes.data
+            self.cfg.tz_use_dst = 1 if dst else 0
+            if len(tr) == 0:   # a zone that never changed offset: the fixed-offset path
+                self.cfg.tz_offset_ms = int(of[0])
         L = lib()
         if _handle is None:
             err = C.create_string_buffer(512)
@@ -185,7 +205,7 @@ class OracleOperator:
         h = lib().or_restore_copy(self._h)
         c = self.cfg
         return OracleOperator(c.mode, c.kind, c.size, c.slide, c.offset, c.tz_offset_ms, c.val_type,
-                              c.count_star_index, _handle=h)
+                              c.count_star_index, _handle=h, zone=self.zone)
 
     def take_rows(self) -> np.ndarray:
         L = lib()
@@ -216,6 +236,19 @@ class OracleOperator:
 
     def window_start(self, w):
         return lib().or_get_window_start(self._h, w)
+
+    # TimeWindowUtil with this operator's zone
+    def to_utc(self, epoch):
+        return lib().or_to_utc(self._h, epoch)
+
+    def to_epoch_for_timer(self, local):
+        return lib().or_to_epoch_for_timer(self._h, local)
+
+    def to_epoch(self, local):
+        return lib().or_to_epoch(self._h, local)
+
+    def next_trigger(self, wm):
+        return lib().or_next_trigger(self._h, wm)
 
     def last_window_end(self, s):
         return lib().or_get_last_window_end(self._h, s)

@@ -118,6 +118,54 @@ def slicing_operator_fixtures():
             columns=["key", "sum", "count", "window_start", "window_end"],
             events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=2))
     out += proctime_fixtures()
+    out += dst_proctime_fixtures()
+    return out
+
+
+# WindowAggregateUseDaylightTimeHarnessTest.scala (TPT/runtime/harness/, :80-197): processing-
+# time CUMULATE(1 h step, 3 h max) over `name` in America/Los_Angeles (daylight saving) and
+# UTC; setProcessingTime(t) then processElement at t. COUNT(*) is the aggregate transcribed
+# (MAX(double) / COUNT(DISTINCT) are outside the engine's aggregate set); all rows are
+# compared at the end ("a" -> key 1). Window bounds are local (shifted) times.
+def dst_proctime_fixtures():
+    out = []
+    H = 3600 * 1000
+    U = utc_ms
+    times = [1615708800000, 1615712400000, 1615716000000, 1615719600000, 1615723200000,
+             1636268400000, 1636272000000, 1636275600000, 1636279200000, 1636282800000]
+    vals = [1.0, 2.0, 2.0, 5.0, 5.0, 3.0, 3.0, 3.0, 3.0, 3.0]
+    ev = []
+    for t, v in zip(times, vals):
+        ev.append(WM(t))
+        ev.append(E(1, v, t))
+    ev.append(WM(1636286400000))
+    rows = {
+        "America/Los_Angeles": [
+            (1, "2021-03-14T00:00:00", "2021-03-14T01:00:00"), (2, "2021-03-14T00:00:00", "2021-03-14T02:00:00"),
+            (2, "2021-03-14T00:00:00", "2021-03-14T03:00:00"), (1, "2021-03-14T03:00:00", "2021-03-14T04:00:00"),
+            (2, "2021-03-14T03:00:00", "2021-03-14T05:00:00"), (3, "2021-03-14T03:00:00", "2021-03-14T06:00:00"),
+            (1, "2021-11-07T00:00:00", "2021-11-07T01:00:00"), (3, "2021-11-07T00:00:00", "2021-11-07T02:00:00"),
+            (4, "2021-11-07T00:00:00", "2021-11-07T03:00:00"), (1, "2021-11-07T03:00:00", "2021-11-07T04:00:00")],
+        "UTC": [
+            (1, "2021-03-14T06:00:00", "2021-03-14T09:00:00"), (1, "2021-03-14T09:00:00", "2021-03-14T10:00:00"),
+            (2, "2021-03-14T09:00:00", "2021-03-14T11:00:00"), (3, "2021-03-14T09:00:00", "2021-03-14T12:00:00"),
+            (1, "2021-03-14T12:00:00", "2021-03-14T13:00:00"), (1, "2021-03-14T12:00:00", "2021-03-14T14:00:00"),
+            (1, "2021-03-14T12:00:00", "2021-03-14T15:00:00"),
+            (1, "2021-11-07T06:00:00", "2021-11-07T08:00:00"), (2, "2021-11-07T06:00:00", "2021-11-07T09:00:00"),
+            (1, "2021-11-07T09:00:00", "2021-11-07T10:00:00"), (2, "2021-11-07T09:00:00", "2021-11-07T11:00:00"),
+            (3, "2021-11-07T09:00:00", "2021-11-07T12:00:00")],
+    }
+    for zone, exp in rows.items():
+        cfg = dict(mode="sql", kind="cumulate", size=3 * H, slide=H, offset=0, tz_offset_ms=0, val_type="f64",
+                   count_star_index=0, proctime=True)
+        if zone != "UTC":
+            cfg["zone"] = zone
+        out.append(dict(
+            name=f"sql_proctime_cumulate_dst_{zone.replace('/', '_')}",
+            source="TPT/runtime/harness/WindowAggregateUseDaylightTimeHarnessTest.scala:80-197",
+            config=cfg, columns=["key", "cnt_star", "window_start", "window_end"], events=ev,
+            expected=[dict(after_event="end", rows=[[1, c, U(s), U(e)] for c, s, e in exp])],
+            expected_late_dropped=0))
     return out
 
 
@@ -328,8 +376,9 @@ def assigner_fixtures():
     H = 3600 * 1000
     U = lambda s: utc_ms(s)
     cases = []
-    for tzname, tz in (("UTC", 0), ("Asia/Shanghai", SHANGHAI)):
+    for tzname, tz in (("UTC", 0), ("Asia/Shanghai", SHANGHAI), ("America/Los_Angeles", -8 * H)):
         A = lambda s: U(s) - tz
+        n0 = len(cases)
         cases.append(dict(
             name=f"tumbling_{tzname}", source="TRT/operators/window/slicing/TumblingSliceAssignerTest.java:47-153",
             config=dict(kind="tumble", size=5 * H, slide=0, offset=0, tz_offset_ms=tz),
@@ -408,6 +457,11 @@ def assigner_fixtures():
             + [[c5("05:00:00"), False, None], [c5("06:00:00"), False, c5("07:00:00")], [c5("00:00:00"), True, None]]
             + [[c5(f"0{h}:00:00"), True, c5(f"0{h + 1}:00:00")] for h in (1, 2, 3, 4)]
             + [[c5("05:00:00"), True, None], [c5("06:00:00"), True, c5("07:00:00")]]))
+        if tzname == "America/Los_Angeles":   # the zone's rules (transitions), not a fixed offset
+            for c in cases[n0:]:
+                c["config"]["zone"] = tzname
+                c["config"]["tz_offset_ms"] = 0
+    cases += dst_assigner_fixtures()
     errors = [  # testInvalidParameters of each assigner test
         dict(config=dict(kind="tumble", size=-1000, slide=0, offset=0),
              message="Tumbling Window parameters must satisfy size > 0, but got size -1000ms.",
@@ -440,13 +494,85 @@ def assigner_fixtures():
     return cases, errors
 
 
+# testDstSaving of Tumbling/Hopping/CumulativeSliceAssignerTest (America/Los_Angeles, the
+# 2021-03-14 gap and the 2021-11-07 overlap): assertSliceStartEnd(start, end, epoch) checks
+# assignSliceEnd(epoch) == end and getWindowStart(end) == start (local times).
+DST_EPOCHS = [1615708800000, 1615712400000, 1615716000000, 1615719600000,
+              1636268400000, 1636272000000, 1636275600000, 1636279200000, 1636282800000, 1636286400000]
+
+
+def dst_assigner_fixtures():
+    H = 3600 * 1000
+    U = lambda s: utc_ms(s + ":00")
+    spec = [
+        ("tumbling_dst", "TRT/operators/window/slicing/TumblingSliceAssignerTest.java:79-114",
+         dict(kind="tumble", size=4 * H, slide=0),
+         [("2021-03-14T00:00", "2021-03-14T04:00")] * 3 + [("2021-03-14T04:00", "2021-03-14T08:00")]
+         + [("2021-11-07T00:00", "2021-11-07T04:00")] * 5 + [("2021-11-07T04:00", "2021-11-07T08:00")]),
+        ("hopping_dst", "TRT/operators/window/slicing/HoppingSliceAssignerTest.java:82-117",
+         dict(kind="hop", size=4 * H, slide=H),
+         [("2021-03-13T21:00", "2021-03-14T01:00"), ("2021-03-13T22:00", "2021-03-14T02:00"),
+          ("2021-03-14T00:00", "2021-03-14T04:00"), ("2021-03-14T01:00", "2021-03-14T05:00"),
+          ("2021-11-06T21:00", "2021-11-07T01:00"), ("2021-11-06T22:00", "2021-11-07T02:00"),
+          ("2021-11-06T22:00", "2021-11-07T02:00"), ("2021-11-06T23:00", "2021-11-07T03:00"),
+          ("2021-11-07T00:00", "2021-11-07T04:00"), ("2021-11-07T01:00", "2021-11-07T05:00")]),
+        ("cumulative_dst", "TRT/operators/window/slicing/CumulativeSliceAssignerTest.java:83-119",
+         dict(kind="cumulate", size=4 * H, slide=H),
+         [("2021-03-14T00:00", "2021-03-14T01:00"), ("2021-03-14T00:00", "2021-03-14T02:00"),
+          ("2021-03-14T00:00", "2021-03-14T04:00"), ("2021-03-14T04:00", "2021-03-14T05:00"),
+          ("2021-11-07T00:00", "2021-11-07T01:00"), ("2021-11-07T00:00", "2021-11-07T02:00"),
+          ("2021-11-07T00:00", "2021-11-07T02:00"), ("2021-11-07T00:00", "2021-11-07T03:00"),
+          ("2021-11-07T00:00", "2021-11-07T04:00"), ("2021-11-07T04:00", "2021-11-07T05:00")]),
+    ]
+    out = []
+    for name, src, cfg, exp in spec:
+        out.append(dict(
+            name=name + "_America/Los_Angeles", source=src,
+            config=dict(cfg, offset=0, tz_offset_ms=0, zone="America/Los_Angeles"),
+            assign=[[e, U(end)] for e, (start, end) in zip(DST_EPOCHS, exp)],
+            window_start=[[U(end), U(start)] for start, end in exp]))
+    return out
+
+
+# TimeWindowUtilTest (TRT/util/TimeWindowUtilTest.java:38-128): [zone, function, in, expected]
+def timeutil_fixtures():
+    U = utc_ms
+    SH, LA = "Asia/Shanghai", "America/Los_Angeles"
+    v = []
+    for s, e in (("1970-01-01T00:00:01", -28799000), ("1970-01-01T07:59:59.999", -1), ("1970-01-01T08:00:01", 1000),
+                 ("1970-01-01T08:00:00.001", 1)):
+        v += [[SH, "to_epoch_for_timer", U(s), e], [SH, "to_epoch", U(s), e]]
+    for s, e in (("2021-03-14T00:00:00", 1615708800000), ("2021-03-14T01:00:00", 1615712400000),
+                 ("2021-03-14T02:00:00", 1615716000000), ("2021-03-14T02:30:00", 1615716000000),
+                 ("2021-03-14T02:59:59", 1615716000000), ("2021-03-14T03:00:00", 1615716000000),
+                 ("2021-03-14T03:30:00", 1615717800000), ("2021-03-14T03:59:59", 1615719599000),
+                 ("2021-11-07T00:00:00", 1636268400000), ("2021-11-07T01:00:00", 1636275600000),
+                 ("2021-11-07T02:00:00", 1636279200000), ("2021-11-07T00:00:01", 1636268401000),
+                 ("2021-11-07T01:59:59", 1636279199000), ("2021-11-07T02:00:01", 1636279201000)):
+        v.append([LA, "to_epoch_for_timer", U(s), e])
+    for s, e in (("2021-03-14T00:00:00", 1615708800000), ("2021-03-14T01:00:00", 1615712400000),
+                 ("2021-03-14T02:00:00", 1615716000000), ("2021-03-14T02:30:00", 1615717800000),
+                 ("2021-03-14T02:59:59", 1615719599000), ("2021-03-14T03:30:00", 1615717800000),
+                 ("2021-03-14T03:00:00", 1615716000000),
+                 ("2021-11-07T00:00:00", 1636268400000), ("2021-11-07T01:00:00", 1636272000000),
+                 ("2021-11-07T02:00:00", 1636279200000), ("2021-11-07T00:00:01", 1636268401000),
+                 ("2021-11-07T01:59:59", 1636275599000), ("2021-11-07T02:00:01", 1636279201000)):
+        v.append([LA, "to_epoch", U(s), e])
+    for t, s in ((1636272000000, "2021-11-07T01:00:00"), (1636275600000, "2021-11-07T01:00:00"),
+                 (1636272001000, "2021-11-07T01:00:01"), (1636275599000, "2021-11-07T01:59:59")):
+        v.append([LA, "to_utc", t, U(s)])
+    for f in ("to_utc", "to_epoch_for_timer", "to_epoch"):   # testMaxWatermark
+        v.append([SH, f, JMAX, JMAX])
+    return v
+
+
 def main():
     ops = slicing_operator_fixtures() + datastream_fixtures() + itcase_fixtures()
     with open(os.path.join(HERE, "operator_cases.json"), "w") as f:
         json.dump(ops, f, indent=1)
     cases, errors = assigner_fixtures()
     with open(os.path.join(HERE, "assigner_cases.json"), "w") as f:
-        json.dump(dict(cases=cases, errors=errors), f, indent=1)
+        json.dump(dict(cases=cases, errors=errors, timeutil=timeutil_fixtures()), f, indent=1)
     print(f"wrote {len(ops)} operator cases, {len(cases)} assigner cases, {len(errors)} error cases")
 
 

@@ -20,7 +20,7 @@ class GpuOperator:
     def __init__(self, cfg, expected_keys=1 << 12, buffer_records=1 << 20, _op=None, kernel_timing=False):
         self.cfg = cfg
         self.op = _op or F.WindowAggOperator(
-            window_of(cfg), aggs=("count_star", "count", "sum", "avg"), val_type=cfg["val_type"],
+            window_of(cfg), aggs=("count_star", "count", "sum", "avg", "sum0"), val_type=cfg["val_type"],
             mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
             buffer_records=buffer_records, kernel_timing=kernel_timing, proctime=cfg.get("proctime", False))
         self._rows = []
@@ -64,12 +64,10 @@ class GpuOperator:
         out["cnt_val"] = r["count"]
         out["sum_null"] = r["sum_null"]
         out["avg_null"] = r["avg_null"]
-        if self.cfg["val_type"] == "f64":
-            out["sum_d"] = r["sum"]
-            out["avg_d"] = r["avg"]
-        else:
-            out["sum_i"] = r["sum"]
-            out["avg_i"] = r["avg"]
+        sfx = "_d" if self.cfg["val_type"] == "f64" else "_i"
+        for name in ("sum", "avg", "sum0"):
+            if name in r.dtype.names:
+                out[name + sfx] = r[name]
         if "rowtime" in r.dtype.names:
             out["out_ts"] = r["rowtime"]
         else:

@@ -39,7 +39,7 @@ def sort_rows(r):
     return r[np.lexsort((r["key"], r["window_end"]))]
 
 
-def assert_rows_equal(got, exp, vt, ctx=""):
+def assert_rows_equal(got, exp, vt, ctx="", sum0=True):
     assert len(got) == len(exp), f"{ctx}: {len(got)} rows vs {len(exp)} expected"
     if len(got) == 0:
         return
@@ -52,9 +52,13 @@ def assert_rows_equal(got, exp, vt, ctx=""):
         assert np.array_equal(g["sum_i"][ok], e["sum_i"][ok]), f"{ctx}: i64 SUM differs"
         ok = e["avg_null"] == 0
         assert np.array_equal(g["avg_i"][ok], e["avg_i"][ok]), f"{ctx}: i64 AVG differs"
+        if sum0:
+            assert np.array_equal(g["sum0_i"], e["sum0_i"]), f"{ctx}: i64 SUM0 differs"
     else:
-        for f, nf in (("sum_d", "sum_null"), ("avg_d", "avg_null")):
-            ok = e[nf] == 0
+        for f, nf in (("sum_d", "sum_null"), ("avg_d", "avg_null"), ("sum0_d", None)):
+            if f == "sum0_d" and not sum0:
+                continue
+            ok = e[nf] == 0 if nf else np.ones(len(e), dtype=bool)
             a, b = g[f][ok], e[f][ok]
             err = np.abs(a - b) <= REL_TOL * np.maximum(np.abs(a), np.abs(b)) + 1e-300
             assert err.all(), f"{ctx}: f64 {f} beyond 1e-9 rel: {a[~err][:5]} vs {b[~err][:5]}"
@@ -334,7 +338,7 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter,
                                   **{k: kw[k] for k in ("rate_per_ms", "zipf") if k in kw})
     w = window_of(cfg)
-    aggs = ("count_star", "count", "sum", "avg")
+    aggs = ("count_star", "count", "sum", "avg", "sum0")
     local = [F.WindowAggOperator(w, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
                                  local_partials=True) for _ in range(S)]
     glob = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys // R + 1,

@@ -12,7 +12,7 @@ def make_oracle(O):
         return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"],
                                 slide=cfg["slide"], offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"],
                                 val_type=VT[cfg["val_type"]], count_star_index=cfg["count_star_index"],
-                                proctime=cfg.get("proctime", False))
+                                proctime=cfg.get("proctime", False), zone=cfg.get("zone"))
     return mk
 
 
@@ -31,7 +31,7 @@ def test_assigner_golden(oracle_mod, case):
     c = case["config"]
     cs = 0 if c["kind"] == "hop" else -1
     op = oracle_mod.OracleOperator(kind=KIND[c["kind"]], size=c["size"], slide=c["slide"], offset=c["offset"],
-                                   tz_offset_ms=c["tz_offset_ms"], count_star_index=cs)
+                                   tz_offset_ms=c["tz_offset_ms"], count_star_index=cs, zone=c.get("zone"))
     for ts, exp in case.get("assign", []):
         assert op.assign_slice_end(ts) == exp
     for w, exp in case.get("window_start", []):
@@ -75,3 +75,53 @@ def test_window_start_java_remainder(oracle_mod):
     assert L.or_window_start_with_offset(-500, 0, 1000) == -1000
     assert L.or_window_start_with_offset(-1500, 0, 1000) == -1000
     assert L.or_window_start_with_offset(-2000, 0, 1000) == -2000
+
+
+def test_sum0_known_answers(oracle_mod):
+    """SUM0 (Sum0AggFunction.java:60-63,97-98,136-137): 0-initialised and never NULL, where
+    SUM (SumAggFunction) is NULL for a window without non-null values; BIGINT wraps as long."""
+    O = oracle_mod
+    import numpy as np
+    big = (1 << 63) - 1
+    for vt, vals in ((O.VAL_I64, [0, 0, 5, 0, 7, big, 1]), (O.VAL_F64, [0.0, 0.0, 5.0, 0.0, 7.0, 1.5, 2.5])):
+        o = O.OracleOperator(kind=O.TUMBLE, size=1000, val_type=vt)
+        key = np.array([1, 1, 2, 2, 2, 3, 3], dtype=np.int64)
+        ts = np.full(7, 10, dtype=np.int64)
+        isnull = np.array([1, 1, 0, 1, 0, 0, 0], dtype=np.uint8)
+        val = np.array(vals, dtype=np.int64 if vt == O.VAL_I64 else np.float64)
+        o.process_batch(key, ts, val, isnull)
+        o.process_watermark(big)
+        r = o.take_rows()
+        o.close()
+        r = r[np.argsort(r["key"])]
+        f = "sum0_i" if vt == O.VAL_I64 else "sum0_d"
+        assert list(r["sum_null"]) == [1, 0, 0]
+        if vt == O.VAL_I64:
+            assert list(r[f]) == [0, 12, -(1 << 63)]   # Long.MAX_VALUE + 1 wraps
+        else:
+            assert list(r[f]) == [0.0, 12.0, 4.0]
+
+
+@pytest.mark.parametrize("zone,fn,arg,exp", AS["timeutil"], ids=[f"{v[0]}-{v[1]}-{v[2]}" for v in AS["timeutil"]])
+def test_time_window_util(oracle_mod, zone, fn, arg, exp):
+    """TimeWindowUtilTest known answers (toUtcTimestampMills / toEpochMillsForTimer /
+    toEpochMills in Asia/Shanghai and in America/Los_Angeles across its 2021 transitions)."""
+    op = oracle_mod.OracleOperator(kind=oracle_mod.TUMBLE, size=1000, zone=zone)
+    assert getattr(op, fn)(arg) == exp
+    op.close()
+
+
+def test_dst_next_trigger_watermark(oracle_mod):
+    """getNextTriggerWatermark's daylight-saving branch (TimeWindowUtil.java:194-199): in
+    America/Los_Angeles the next trigger after a watermark in the 2021-03-14 gap hour is the
+    first skipped instant's hour, and zones without daylight saving take the plain branch."""
+    H = 3600 * 1000
+    la = oracle_mod.OracleOperator(kind=oracle_mod.TUMBLE, size=H, zone="America/Los_Angeles")
+    # 09:30 UTC = 01:30 PST -> window [01:00, 02:00) local ends in the gap: trigger 09:59:59.999 UTC
+    assert la.next_trigger(1615714200000) == 1615715999999
+    # 10:00 UTC = 03:00 PDT -> next local hour end 04:00 -> 10:59:59.999 UTC
+    assert la.next_trigger(1615716000000) == 1615719599999
+    la.close()
+    sh = oracle_mod.OracleOperator(kind=oracle_mod.TUMBLE, size=H, zone="Asia/Shanghai")
+    assert sh.next_trigger(1615714200000) == oracle_mod.next_trigger_watermark(1615714200000, H)
+    sh.close()
