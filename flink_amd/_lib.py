@@ -31,6 +31,8 @@ class FgConfig(C.Structure):
         ("max_parallelism", C.c_int32), ("key_group_start", C.c_int32), ("key_group_end", C.c_int32),
         ("device_id", C.c_int32), ("flags", C.c_int32),
         ("expected_keys", C.c_int64), ("buffer_records", C.c_int64),
+        ("tz_transition_ms", C.c_void_p), ("tz_offset_ms", C.c_void_p),
+        ("n_tz_transitions", C.c_int32), ("tz_use_daylight", C.c_int32),
     ]
 
 

@@ -182,6 +182,8 @@ struct fg_handle {
     DevBuf in_cs, in_cv, in_sum, in_slice;
     bool local = false;     // FG_FLAG_LOCAL_PARTIALS: fired slices emit partial accumulators
     bool proctime = false;  // FG_FLAG_PROCTIME: processing-time windows, nothing is late
+    std::vector<int64_t> tz_trans, tz_offs;   // zone rules (host copy); tz_dev: the HBM copy
+    DevBuf tz_dev;
     std::vector<std::unique_ptr<Staged>> passes;       // live passes
     std::vector<std::unique_ptr<Staged>> pass_pool;
     int64_t anchor_start = JMIN;   // a recent slice start: base of the 32-bit rowtime fast path
@@ -910,6 +912,7 @@ int copy_out_to_host(fg_handle* h, fg_rows* r) {
 void set_fast_path(fg_handle* h, IngestParams* p) {
     p->div_m = 0;
     const int64_t S = h->w.slice;
+    if (h->w.tz_n > 0) return;   // zone rules: the offset varies per record, exact path
     if (h->anchor_start == JMIN || S < 2 || S >= ((int64_t)1 << 32)) return;
     const __int128 margin = (__int128)S * (((int64_t)1 << 30) / S);
     const __int128 tb = (__int128)h->anchor_start - margin;
@@ -1370,6 +1373,26 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         g_open_error = "FG_FLAG_PROCTIME is for SQL window aggregation (not DataStream or the local phase)";
         return FG_EINVAL;
     }
+    if (c.n_tz_transitions < 0 || (c.n_tz_transitions > 0 && (!c.tz_transition_ms || !c.tz_offset_ms))) {
+        g_open_error = "zone rules need n_tz_transitions instants and n_tz_transitions + 1 offsets";
+        return FG_EINVAL;
+    }
+    if (c.n_tz_transitions > 0) {
+        if (c.mode != FG_MODE_SQL || local) {
+            g_open_error = "zone rules (daylight saving) are for SQL window aggregation, not DataStream or the local phase";
+            return FG_EINVAL;
+        }
+        for (int32_t i = 0; i + 1 < c.n_tz_transitions; i++)
+            if (c.tz_transition_ms[i] >= c.tz_transition_ms[i + 1]) {
+                g_open_error = "zone transitions must be ascending";
+                return FG_EINVAL;
+            }
+        for (int32_t i = 0; i <= c.n_tz_transitions; i++)
+            if (c.tz_offset_ms[i] < -18ll * 3600 * 1000 || c.tz_offset_ms[i] > 18ll * 3600 * 1000) {
+                g_open_error = "zone offsets must lie within +-18 h (ZoneOffset)";
+                return FG_EINVAL;
+            }
+    }
     std::string msg;
     int rc = validate(&c, &msg);
     if (rc) {
@@ -1406,6 +1429,24 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     w.nslices = w.size / w.slice;
     w.rslice = 1.0 / (double)w.slice;
     w.rsize = 1.0 / (double)w.size;
+    if (c.n_tz_transitions > 0) {   // zone rules: host copy + HBM copy for the kernels
+        const size_t n = (size_t)c.n_tz_transitions;
+        h->tz_trans.assign(c.tz_transition_ms, c.tz_transition_ms + n);
+        h->tz_offs.assign(c.tz_offset_ms, c.tz_offset_ms + n + 1);
+        if (h->tz_dev.ensure(8 * (2 * n + 1)) != hipSuccess ||
+            hipMemcpy(h->tz_dev.p, h->tz_trans.data(), 8 * n, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(h->tz_dev.as<int64_t>() + n, h->tz_offs.data(), 8 * (n + 1), hipMemcpyHostToDevice) != hipSuccess) {
+            g_open_error = "zone rules: device copy failed";
+            return FG_EDEVICE;
+        }
+        w.tz = 0;
+        w.tz_n = c.n_tz_transitions;
+        w.tz_dst = c.tz_use_daylight ? 1 : 0;
+        w.tz_trans_h = h->tz_trans.data();
+        w.tz_offs_h = h->tz_offs.data();
+        w.tz_trans_d = h->tz_dev.as<int64_t>();
+        w.tz_offs_d = h->tz_dev.as<int64_t>() + n;
+    }
     h->slice_phase = ((w.offset % w.slice) + w.slice) % w.slice;
 
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
@@ -1522,6 +1563,7 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     if (!h || !b) return FG_EINVAL;
     if (b->n <= 0) return FG_OK;
     if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
+    if (h->w.tz_n > 0) return h->fail(FG_EINVAL, "fg_add_partials with zone rules (daylight saving) is not supported");
     if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 rows");
     if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
         return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
@@ -1613,7 +1655,7 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
                     rc = flush(h, fuse, true);
                     if (rc) return rc;
                 }
-                h->next_trigger = next_trigger_watermark(wm, h->w.slice);
+                h->next_trigger = next_trigger_watermark(h->w, wm, h->w.slice);
             }
         }
     } else {

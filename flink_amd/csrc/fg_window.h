@@ -1,8 +1,9 @@
 // fg_window.h -- window / slice arithmetic shared by the HIP kernels and the host engine.
 //
 // Restates the reference's slice assigners and time utilities for the event-time path
-// (UTC or a fixed-offset shift time zone). Java long arithmetic wraps, so every add/sub
-// goes through unsigned arithmetic.
+// (UTC, a fixed-offset shift time zone, or a zone with transitions / daylight saving given
+// as its rules). Java long arithmetic wraps, so every add/sub goes through unsigned
+// arithmetic.
 //   TimeWindow.getWindowStartWithOffset  TR/operators/window/TimeWindow.java:222-224
 //   TimeWindowUtil.toUtcTimestampMills / toEpochMillsForTimer / isWindowFired /
 //     getNextTriggerWatermark            TR/util/TimeWindowUtil.java:53-61,137-139,176-210
@@ -53,21 +54,95 @@ struct WindowSpec {
     int64_t size;       // tumble size, hop size, cumulate max size
     int64_t slide;      // hop slide, cumulate step
     int64_t offset;
-    int64_t tz;         // fixed shift-zone offset in ms (0 = UTC)
+    int64_t tz;         // fixed shift-zone offset in ms (0 = UTC; unused when tz_n > 0)
     int64_t slice;      // getSliceEndInterval: tumble size, hop gcd(size, slide), cumulate step
     int64_t nslices;    // hop: size / slice
     double rslice;      // 1.0 / slice
     double rsize;       // 1.0 / size
+    // zone with transitions (ZoneRules as data): tz_n instants (epoch ms, ascending) and
+    // tz_n + 1 offsets ([i] in force before transition i), one copy in host memory for the
+    // engine and one in HBM for the kernels
+    const int64_t* tz_trans_h;
+    const int64_t* tz_offs_h;
+    const int64_t* tz_trans_d;
+    const int64_t* tz_offs_d;
+    int32_t tz_n;
+    int32_t tz_dst;     // TimeZone.useDaylightTime(): the DST branches of TimeWindowUtil
 };
+
+// the zone tables of the side this code runs on
+__host__ __device__ __forceinline__ const int64_t* zone_trans(const WindowSpec& w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return w.tz_trans_d;
+#else
+    return w.tz_trans_h;
+#endif
+}
+__host__ __device__ __forceinline__ const int64_t* zone_offs(const WindowSpec& w) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return w.tz_offs_d;
+#else
+    return w.tz_offs_h;
+#endif
+}
+// ZoneRules.getOffset(Instant): the offset after the last transition at or before `instant`
+__host__ __device__ __forceinline__ int64_t zone_offset_at(const WindowSpec& w, int64_t instant) {
+    const int64_t* T = zone_trans(w);
+    int32_t lo = 0, hi = w.tz_n;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (T[mid] <= instant) lo = mid + 1;
+        else hi = mid;
+    }
+    return zone_offs(w)[lo];
+}
+// LocalDateTime.atZone(zone).toInstant() for a local (UTC-shifted) time: the one valid
+// offset; in an overlap the earlier offset (the one before the transition); in a gap the
+// local time moves later by the gap and takes the offset after (= local - offset before).
+__host__ __device__ inline int64_t zone_local_to_epoch(const WindowSpec& w, int64_t local) {
+    const int64_t W = 20ll * 3600 * 1000;   // |offset| <= 18 h
+    const int32_t n = w.tz_n;
+    const int64_t* T = zone_trans(w);
+    const int64_t* O = zone_offs(w);
+    int32_t lo = 0, hi = n;                  // first offset region that can hold local - offset
+    const int64_t from = jsub(local, W);
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (T[mid] <= from) lo = mid + 1;
+        else hi = mid;
+    }
+    for (int32_t k = lo; k <= n; k++) {
+        const int64_t e = jsub(local, O[k]);
+        if ((k == 0 || T[k - 1] <= e) && (k == n || e < T[k])) return e;   // first valid: earlier offset
+        if (k == n || T[k] > jadd(local, W)) break;
+        if (e >= T[k] && jsub(local, O[k + 1]) < T[k]) return e;            // gap at transition k
+    }
+    return jsub(local, O[n]);
+}
 
 // TimeWindow.getWindowStartWithOffset (Java truncated remainder, kept bit for bit)
 __host__ __device__ __forceinline__ int64_t window_start_with_offset(int64_t ts, int64_t off, int64_t size) {
     return jsub(ts, jadd(jsub(ts, off), size) % size);
 }
+// TimeWindowUtil.toUtcTimestampMills (:53-61)
 __host__ __device__ __forceinline__ int64_t to_utc(const WindowSpec& w, int64_t epoch) {
+    if (w.tz_n > 0) return epoch == JMAX ? epoch : jadd(epoch, zone_offset_at(w, epoch));
     return (w.tz == 0 || epoch == JMAX) ? epoch : jadd(epoch, w.tz);
 }
+// TimeWindowUtil.toEpochMillsForTimer (:70-140): with daylight saving, a local time in a
+// gap takes the first skipped instant (hasNoEpoch) and one in an overlap the later instant
+// (hasTwoEpochs); without, toEpochMills (atZone)
 __host__ __device__ __forceinline__ int64_t to_epoch_for_timer(const WindowSpec& w, int64_t utc) {
+    if (w.tz_n > 0) {
+        if (utc == JMAX) return utc;
+        const int64_t t1 = zone_local_to_epoch(w, utc);
+        if (!w.tz_dst) return t1;
+        const int64_t HOUR = 3600ll * 1000;
+        const int64_t t2 = zone_local_to_epoch(w, jadd(utc, HOUR));
+        if (t1 == t2) return jsub(t1, t1 % HOUR);
+        if (jsub(t2, t1) > HOUR) return jadd(t1, HOUR);
+        return t1;
+    }
     return (w.tz == 0 || utc == JMAX) ? utc : jsub(utc, w.tz);
 }
 // trigger time of a window (the timer timestamp registered by WindowTimerServiceImpl:60-63)
@@ -106,6 +181,14 @@ __host__ __device__ __forceinline__ int64_t next_trigger_watermark(int64_t wm, i
     if (wm == JMAX) return wm;
     int64_t start = window_start_with_offset(wm, 0, interval);
     int64_t trig = jsub(jadd(start, interval), 1);
+    return trig > wm ? trig : jadd(trig, interval);
+}
+// the same with the window's zone: the daylight-saving branch (:194-199) when the zone
+// observes it (AbstractWindowAggProcessor's useDayLightSaving)
+__host__ __device__ __forceinline__ int64_t next_trigger_watermark(const WindowSpec& w, int64_t wm, int64_t interval) {
+    if (!(w.tz_n > 0 && w.tz_dst) || wm == JMAX) return next_trigger_watermark(wm, interval);
+    const int64_t start = window_start_with_offset(to_utc(w, wm), 0, interval);
+    const int64_t trig = to_epoch_for_timer(w, jsub(jadd(start, interval), 1));
     return trig > wm ? trig : jadd(trig, interval);
 }
 

@@ -81,8 +81,12 @@ class WindowAggOperator:
                  mode: str = "sql", shift_tz_offset_ms: int = 0, expected_keys: int = 1 << 16,
                  buffer_records: int = 1 << 22, device: int = 0, max_parallelism: int = 128,
                  key_group_range=(0, 127), kernel_timing: bool = False, local_partials: bool = False,
-                 proctime: bool = False):
-        """local_partials: the local phase of the two-phase aggregation
+                 proctime: bool = False, zone: str | None = None):
+        """zone: an IANA zone name (TableConfig.getLocalTimeZone() of a TIMESTAMP_LTZ window)
+        whose rules -- transitions and daylight saving -- replace shift_tz_offset_ms
+        (flink_amd.tz.zone_rules; a zone that never changed offset takes the fixed path).
+
+        local_partials: the local phase of the two-phase aggregation
         (LocalSlicingWindowAggOperator + LocalAggCombiner): process_watermark returns one
         partial accumulator row per (key, fired slice) with columns count_star, count, sum
         (window_start/window_end = the slice), to be exchanged by key group and merged by a
@@ -113,6 +117,18 @@ class WindowAggOperator:
                      | (L.FLAG_PROCTIME if proctime else 0))
         cfg.expected_keys = int(expected_keys)
         cfg.buffer_records = int(buffer_records)
+        self.zone = zone
+        if zone is not None:
+            from .tz import zone_rules
+            trans, offs, dst = zone_rules(zone)
+            if len(trans) == 0:
+                cfg.shift_tz_offset_ms = int(offs[0])
+            else:   # fg_open copies the rules
+                self._tz = (np.ascontiguousarray(trans), np.ascontiguousarray(offs))
+                cfg.tz_transition_ms = self._tz[0].ctypes.data
+                cfg.tz_offset_ms = self._tz[1].ctypes.data
+                cfg.n_tz_transitions = len(trans)
+                cfg.tz_use_daylight = 1 if dst else 0
         self.cfg = cfg
         h = C.c_void_p()
         L.check(lib.fg_open(C.byref(cfg), C.byref(h)), None)

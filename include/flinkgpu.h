@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 2
+#define FG_ABI_VERSION 3
 
 enum fg_status {
     FG_OK = 0,
@@ -116,6 +116,15 @@ typedef struct fg_config {
     int32_t flags;                /* FG_FLAG_* */
     int64_t expected_keys;        /* distinct keys per slice on this subtask (sizes HBM regions) */
     int64_t buffer_records;       /* staged records before an implicit flush (managed-memory analogue) */
+    /* Shift time zone with transitions (daylight saving): the ZoneRules of the ZoneId as data
+     * (ZoneRules.getTransitions() on the Java side). n_tz_transitions > 0 replaces
+     * shift_tz_offset_ms: toUtcTimestampMills / toEpochMillsForTimer / getNextTriggerWatermark
+     * follow TimeWindowUtil.java:53-61,70-140,187-210 with these rules. SQL mode only, and not
+     * for the two-phase operators (FG_FLAG_LOCAL_PARTIALS, fg_add_partials). Copied at fg_open. */
+    const int64_t* tz_transition_ms;   /* n_tz_transitions instants, epoch ms, ascending */
+    const int64_t* tz_offset_ms;       /* n_tz_transitions + 1 offsets (ms): [i] in force before transition i */
+    int32_t n_tz_transitions;
+    int32_t tz_use_daylight;           /* TimeZone.getTimeZone(zone).useDaylightTime() */
 } fg_config;
 
 typedef struct fg_batch {

@@ -22,7 +22,8 @@ class GpuOperator:
         self.op = _op or F.WindowAggOperator(
             window_of(cfg), aggs=("count_star", "count", "sum", "avg", "sum0"), val_type=cfg["val_type"],
             mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
-            buffer_records=buffer_records, kernel_timing=kernel_timing, proctime=cfg.get("proctime", False))
+            buffer_records=buffer_records, kernel_timing=kernel_timing, proctime=cfg.get("proctime", False),
+            zone=cfg.get("zone"))
         self._rows = []
 
     def process_batch(self, key, ts, val=None, isnull=None):
@@ -39,7 +40,8 @@ class GpuOperator:
         new = GpuOperator(self.cfg, _op=F.WindowAggOperator(
             self.op.window, aggs=self.op.aggs, val_type=self.cfg["val_type"], mode=self.cfg["mode"],
             shift_tz_offset_ms=self.cfg.get("tz_offset_ms", 0), expected_keys=self.op.cfg.expected_keys,
-            buffer_records=self.op.cfg.buffer_records, proctime=self.cfg.get("proctime", False)))
+            buffer_records=self.op.cfg.buffer_records, proctime=self.cfg.get("proctime", False),
+            zone=self.cfg.get("zone")))
         new.op.restore_state(img, wm)
         new._late_base = self.late_dropped
         return new

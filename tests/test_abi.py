@@ -28,12 +28,12 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 2
+    assert lib.fg_abi_version() == 3
 
 
 def test_struct_layouts_match_header_sizes():
-    # fg_config: 2*4 + 4*8 + 2*4 + 8*4 + 6*4 + 2*8
-    assert C.sizeof(L.FgConfig) == 8 + 32 + 8 + 32 + 24 + 16
+    # fg_config: 2*4 + 4*8 + 2*4 + 8*4 + 6*4 + 2*8 + zone rules (2 pointers + 2*4)
+    assert C.sizeof(L.FgConfig) == 8 + 32 + 8 + 32 + 24 + 16 + 16 + 8
     assert C.sizeof(L.FgBatch) == 8 + 8 + 4 * 8
     assert C.sizeof(L.FgRows) == 8 + 8 + 3 * 8 + 8 * 8 + 2 * 8
     assert C.sizeof(L.FgPartials) == 8 + 8 + 5 * 8
@@ -77,3 +77,12 @@ def test_proctime_only_for_sql():
     import flink_amd as F
     with pytest.raises(F.WindowSpecError):
         F.WindowAggOperator(F.tumbling(1000), mode="datastream", val_type="i64", proctime=True)
+
+
+def test_zone_rules_validated_before_device():
+    """Zone rules (daylight saving) are for SQL windows only, checked before any device call."""
+    import flink_amd as F
+    with pytest.raises(F.WindowSpecError):
+        F.WindowAggOperator(F.tumbling(1000), mode="datastream", val_type="i64", zone="America/Los_Angeles")
+    with pytest.raises(F.WindowSpecError):
+        F.WindowAggOperator(F.tumbling(1000), local_partials=True, zone="America/Los_Angeles")

@@ -23,7 +23,8 @@ def gpu_mk(cfg, **kw):
 def oracle_mk(O, cfg):
     return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"], slide=cfg["slide"],
                             offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"], val_type=VT[cfg["val_type"]],
-                            count_star_index=cfg["count_star_index"], proctime=cfg.get("proctime", False))
+                            count_star_index=cfg["count_star_index"], proctime=cfg.get("proctime", False),
+                            zone=cfg.get("zone"))
 
 
 @pytest.mark.parametrize("case", OP_CASES, ids=[c["name"] for c in OP_CASES])
@@ -100,9 +101,16 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
     return late
 
 
-def cfg_of(kind, size, slide=0, vt="f64", mode="sql", tz=0, offset=0):
-    return dict(mode=mode, kind=kind, size=size, slide=slide, offset=offset, tz_offset_ms=tz, val_type=vt,
-                count_star_index=0)
+def cfg_of(kind, size, slide=0, vt="f64", mode="sql", tz=0, offset=0, zone=None):
+    c = dict(mode=mode, kind=kind, size=size, slide=slide, offset=offset, tz_offset_ms=tz, val_type=vt,
+             count_star_index=0)
+    if zone:
+        c["zone"] = zone
+    return c
+
+
+LA = "America/Los_Angeles"
+SPRING, FALL = 1615708800000, 1636268400000   # 2021-03-14 / 2021-11-07 00:00 local, LA
 
 
 STREAM_CASES = [
@@ -152,6 +160,20 @@ STREAM_CASES = [
                                                                          zipf=1.3)),
     ("zipf_ds_tumble_i64", cfg_of("tumble", 2000, vt="i64", mode="datastream"),
      dict(n=3_000_000, keys=100_000, batch=1_000_000, delay=0, jitter=0, rate_per_ms=1_000, zipf=1.1)),
+    # America/Los_Angeles zone rules across the 2021 gap (spring) and overlap (fall):
+    # TIMESTAMP_LTZ windows in local time, DST trigger times, late records
+    ("dst_tumble_spring_f64", cfg_of("tumble", 3600_000, zone=LA),
+     dict(n=400_000, keys=3000, batch=20_000, delay=600_000, jitter=1_800_000, t0=SPRING, rate_per_ms=0.02)),
+    ("dst_hop_fall_i64", cfg_of("hop", 4 * 3600_000, 3600_000, vt="i64", zone=LA),
+     dict(n=400_000, keys=2000, batch=25_000, delay=300_000, jitter=2_400_000, t0=FALL, rate_per_ms=0.02)),
+    ("dst_cumulate_spring_f64", cfg_of("cumulate", 4 * 3600_000, 3600_000, zone=LA),
+     dict(n=300_000, keys=2000, batch=15_000, delay=900_000, jitter=3_000_000, t0=SPRING - 3600_000,
+          rate_per_ms=0.02, null_frac=0.1)),
+    ("dst_cumulate_fall_regions_i64", cfg_of("cumulate", 3 * 3600_000, 3600_000, vt="i64", zone=LA),
+     dict(n=1_200_000, keys=150_000, batch=100_000, delay=300_000, jitter=1_200_000, t0=FALL - 1800_000,
+          rate_per_ms=0.06)),
+    ("dst_proctime_cumulate_fall", dict(cfg_of("cumulate", 3 * 3600_000, 3600_000, zone=LA), proctime=True),
+     dict(n=300_000, keys=20_000, batch=20_000, delay=0, jitter=0, t0=FALL - 1800_000, rate_per_ms=0.02)),
 ]
 
 
