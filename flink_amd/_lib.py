@@ -80,6 +80,7 @@ class FgKernelStat(C.Structure):
 FLAG_KERNEL_TIMING = 1
 FLAG_LOCAL_PARTIALS = 2
 FLAG_PROCTIME = 4
+FLAG_WINDOWED = 8
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (

@@ -184,6 +184,9 @@ struct fg_handle {
     bool proctime = false;  // FG_FLAG_PROCTIME: processing-time windows, nothing is late
     std::vector<int64_t> tz_trans, tz_offs;   // zone rules (host copy); tz_dev: the HBM copy
     DevBuf tz_dev;
+    bool windowed = false;  // FG_FLAG_WINDOWED: rows carry window_end; `w` is a one-slice
+    WindowSpec inner{};     // window per slice, `inner` the TVF's assigner (getWindowStart)
+    DevBuf in_wts;          // windowed: pseudo rowtimes of a batch
     std::vector<std::unique_ptr<Staged>> passes;       // live passes
     std::vector<std::unique_ptr<Staged>> pass_pool;
     int64_t anchor_start = JMIN;   // a recent slice start: base of the 32-bit rowtime fast path
@@ -391,7 +394,7 @@ void fill_emit(fg_handle* h, MergeParams& p, int64_t wend) {
     p.emit = 1;
     // local phase: the emitted "window" is the slice itself (LocalAggCombiner emits
     // (key, acc, slice_end) rows)
-    p.wstart = h->local ? jsub(wend, h->w.slice) : window_start(h->w, wend);
+    p.wstart = h->local ? jsub(wend, h->w.slice) : window_start(h->windowed ? h->inner : h->w, wend);
     p.wend = wend;
     p.out_ts = jsub(wend, 1);
     p.num_aggs = h->cfg.num_aggs;
@@ -1310,7 +1313,7 @@ int validate(const fg_config* c, std::string* msg) {
             snprintf(buf, sizeof buf,
                      "Slicing Hopping Window requires size must be an integral multiple of slide, but got size %lldms and slide %lldms.",
                      size, slide);
-        else if (c->mode == FG_MODE_SQL && !has_star)
+        else if (c->mode == FG_MODE_SQL && !has_star && !(c->flags & FG_FLAG_WINDOWED))
             snprintf(buf, sizeof buf, "Hopping window requires a COUNT(*) in the aggregate functions.");
     } else if (c->window_kind == FG_CUMULATE) {
         if (size <= 0 || slide <= 0)
@@ -1371,6 +1374,13 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     const bool proctime = (c.flags & FG_FLAG_PROCTIME) != 0;
     if (proctime && (c.mode != FG_MODE_SQL || local)) {
         g_open_error = "FG_FLAG_PROCTIME is for SQL window aggregation (not DataStream or the local phase)";
+        return FG_EINVAL;
+    }
+    const bool windowed = (c.flags & FG_FLAG_WINDOWED) != 0;
+    if (windowed && (c.mode != FG_MODE_SQL || local || proctime || c.n_tz_transitions > 0)) {
+        // WindowedSliceAssigner.isEventTime() is always true (SliceAssigners.java:430-434)
+        g_open_error = "FG_FLAG_WINDOWED is for SQL event-time window aggregation (not DataStream, processing time, "
+                       "the local phase or zone rules)";
         return FG_EINVAL;
     }
     if (c.n_tz_transitions < 0 || (c.n_tz_transitions > 0 && (!c.tz_transition_ms || !c.tz_offset_ms))) {
@@ -1448,6 +1458,14 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         w.tz_offs_d = h->tz_dev.as<int64_t>() + n;
     }
     h->slice_phase = ((w.offset % w.slice) + w.slice) % w.slice;
+    if (windowed) {   // each window its own slice: a tumbling spec of the inner slice interval
+        h->windowed = true;
+        h->inner = w;
+        w.kind = TUMBLE;
+        w.size = w.slide = w.slice;
+        w.nslices = 1;
+        w.rsize = w.rslice;
+    }
 
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
     int64_t keys = std::max<int64_t>(cfg->expected_keys, 1);
@@ -1519,11 +1537,25 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
             vnull = h->in_null.as<uint8_t>();
         }
     }
+    if (h->windowed) {   // window_end -> pseudo rowtime (every end on the slice grid)
+        HIPCHK(h, h->in_wts.ensure(8 * n + 8));
+        unsigned long long* bad = reinterpret_cast<unsigned long long*>(h->in_wts.as<int64_t>() + n);
+        HIPCHK(h, hipMemsetAsync(bad, 0, 8, h->stream));
+        HIPCHK(h, launch_window_end_rowtime(ts, n, h->w.tz, h->w.slice, h->slice_phase, h->in_wts.as<int64_t>(), bad,
+                                            h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_counters.p, bad, 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        unsigned long long nbad = 0;
+        std::memcpy(&nbad, h->h_counters.p, 8);
+        if (nbad)
+            return h->fail(FG_EINVAL, "windowed input: %llu window_end values off the slice grid of the window", nbad);
+        ts = h->in_wts.as<int64_t>();
+    }
     // EOFException semantics (RecordsWindowBuffer.java:91-96) are applied per lane inside
     // ingest_pass: a lane without room is flushed into its slice table, then the pass stages
     h->records_in += n;
     {
-        int rc0 = b->location == FG_HOST ? seed_anchor(h, nullptr, b->rowtime) : seed_anchor(h, ts, nullptr);
+        int rc0 = b->location == FG_HOST && !h->windowed ? seed_anchor(h, nullptr, b->rowtime) : seed_anchor(h, ts, nullptr);
         if (rc0) return rc0;
     }
     // First pass: every slice -- or, while batches span more slices than the staged lanes

@@ -880,6 +880,30 @@ __global__ void k_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz
     }
 }
 
+// Windowed input (WindowedSliceAssigner): the attached window_end of a row is its slice,
+// classified like a record with rowtime window_end - 1 - tz; ends off the inner assigner's
+// slice grid are counted (the caller fails loudly on any)
+__global__ void k_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,
+                                     int64_t* out, unsigned long long* off_grid) {
+    unsigned long long bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = wend[i];
+        int64_t r = jsub(e, phase) % S;
+        if (r < 0) r += S;
+        bad += (r != 0 || e == JMAX) ? 1ull : 0ull;
+        out[i] = jsub(jsub(e, 1), tz);
+    }
+    if (bad) atomicAdd(off_grid, bad);
+}
+
+hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,
+                                     int64_t* out, unsigned long long* off_grid, hipStream_t s) {
+    int64_t blocks = (n + 255) / 256;
+    blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
+    hipLaunchKernelGGL(k_window_end_rowtime, dim3((unsigned)blocks), dim3(256), 0, s, wend, n, tz, S, phase, out, off_grid);
+    return hipGetLastError();
+}
+
 hipError_t launch_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out, hipStream_t s) {
     int64_t blocks = (n + 255) / 256;
     blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);

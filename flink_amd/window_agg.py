@@ -81,8 +81,11 @@ class WindowAggOperator:
                  mode: str = "sql", shift_tz_offset_ms: int = 0, expected_keys: int = 1 << 16,
                  buffer_records: int = 1 << 22, device: int = 0, max_parallelism: int = 128,
                  key_group_range=(0, 127), kernel_timing: bool = False, local_partials: bool = False,
-                 proctime: bool = False, zone: str | None = None):
-        """zone: an IANA zone name (TableConfig.getLocalTimeZone() of a TIMESTAMP_LTZ window)
+                 proctime: bool = False, zone: str | None = None, windowed: bool = False):
+        """windowed: rows carry their window (WindowedSliceAssigner, after a window TVF): the
+        `rowtime` column of process_batch holds each row's window_end; `window` is the TVF's.
+
+        zone: an IANA zone name (TableConfig.getLocalTimeZone() of a TIMESTAMP_LTZ window)
         whose rules -- transitions and daylight saving -- replace shift_tz_offset_ms
         (flink_amd.tz.zone_rules; a zone that never changed offset takes the fixed path).
 
@@ -114,7 +117,7 @@ class WindowAggOperator:
         cfg.key_group_start, cfg.key_group_end = int(key_group_range[0]), int(key_group_range[1])
         cfg.device_id = int(device)
         cfg.flags = ((L.FLAG_KERNEL_TIMING if kernel_timing else 0) | (L.FLAG_LOCAL_PARTIALS if local_partials else 0)
-                     | (L.FLAG_PROCTIME if proctime else 0))
+                     | (L.FLAG_PROCTIME if proctime else 0) | (L.FLAG_WINDOWED if windowed else 0))
         cfg.expected_keys = int(expected_keys)
         cfg.buffer_records = int(buffer_records)
         self.zone = zone

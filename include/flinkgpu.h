@@ -94,7 +94,16 @@ enum fg_flags {
      * AbstractWindowAggProcessor.java:137-140): `rowtime` carries each record's processing
      * time, nothing is late, fg_advance_progress takes the current processing time. Records
      * are expected at or after the last progress (as processing time is). */
-    FG_FLAG_PROCTIME = 4
+    FG_FLAG_PROCTIME = 4,
+    /* Input rows already carry their window (SliceAssigners.windowed / WindowedSliceAssigner,
+     * TR/operators/window/slicing/SliceAssigners.java:386-435, after a window TVF): `rowtime`
+     * carries each row's window_end; every window is its own slice (unshared, fired and
+     * expired alone, a late row is dropped once its window fired); window_start =
+     * the kind's getWindowStart(window_end). The window kind/size/slide/offset describe the
+     * inner assigner. window_end values must lie on the inner assigner's slice grid (as a
+     * window TVF emits them), else fg_add_batch fails with FG_EINVAL. SQL event time only;
+     * not with zone rules or the two-phase operators. */
+    FG_FLAG_WINDOWED = 8
 };
 
 #define FG_MAX_AGGS 8

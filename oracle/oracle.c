@@ -305,6 +305,8 @@ int64_t or_next_trigger(const or_op* op, int64_t wm) { return next_trigger(op, w
 /* assignSliceEnd: Tumbling :164-167, Hopping :231-234, Cumulative :318-321, via
  * AbstractSliceAssigner.assignSliceEnd :551-561 (rowtime path) */
 int64_t or_assign_slice_end(const or_op* op, int64_t ts) {
+    /* WindowedSliceAssigner.assignSliceEnd :402-404: the attached window end, as is */
+    if (op->cfg.windowed) return ts;
     int64_t t = to_utc(op, ts);
     return jadd(or_window_start_with_offset(t, op->cfg.offset, op->slice_size), op->slice_size);
 }
@@ -316,6 +318,7 @@ int64_t or_get_window_start(const or_op* op, int64_t window_end) {
 }
 /* getLastWindowEnd: Tumbling :170-172, Hopping :237-239, Cumulative :324-327 */
 int64_t or_get_last_window_end(const or_op* op, int64_t slice_end) {
+    if (op->cfg.windowed) return slice_end;   /* WindowedSliceAssigner :407-412: the window itself */
     switch (op->cfg.kind) {
         case OR_TUMBLE: return slice_end;
         case OR_HOP: return jadd(jsub(slice_end, op->slice_size), op->cfg.size);
@@ -324,6 +327,7 @@ int64_t or_get_last_window_end(const or_op* op, int64_t slice_end) {
 }
 /* expiredSlices: Tumbling :179-182, Hopping :247-253, Cumulative :335-351 */
 int32_t or_expired_slices(const or_op* op, int64_t w, int64_t* out) {
+    if (op->cfg.windowed) { out[0] = w; return 1; }   /* WindowedSliceAssigner :420-423 */
     switch (op->cfg.kind) {
         case OR_TUMBLE: out[0] = w; return 1;
         case OR_HOP: out[0] = jadd(or_get_window_start(op, w), op->slice_size); return 1;
@@ -373,7 +377,7 @@ int32_t or_next_trigger_window(const or_op* op, int64_t w, int32_t is_empty, int
 }
 /* SliceSharedWindowAggProcessor.sliceStateMergeTarget :120-131 (+ helper :172-190) */
 static int64_t slice_state_merge_target(const or_op* op, int64_t slice) {
-    if (op->cfg.kind == OR_CUMULATE) {
+    if (op->cfg.kind == OR_CUMULATE && !op->cfg.windowed) {
         int64_t mr, tmp[1];
         or_merge_slices(op, slice, &mr, tmp, 1);
         return mr;   /* never null for cumulate */
@@ -571,8 +575,8 @@ static int sql_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits
  * clearWindow: AbstractWindowAggProcessor.java:200-206; via SlicingWindowOperator.onTimer :230-237 */
 static void sql_on_timer(or_op* op, int64_t key, int64_t w) {
     int vt = op->cfg.val_type;
-    int64_t wstart = or_get_window_start(op, w);
-    if (op->cfg.kind == OR_TUMBLE) {
+    int64_t wstart = or_get_window_start(op, w);   /* windowed: innerAssigner.getWindowStart :415-417 */
+    if (op->cfg.kind == OR_TUMBLE || op->cfg.windowed) {   /* SliceUnsharedWindowAggProcessor */
         or_acc tmp;
         const or_acc* a = state_get(op, key, w);
         if (!a) { acc_create(&tmp); a = &tmp; }
@@ -661,7 +665,7 @@ or_op* or_open(const or_config* cfg, char* err, int errlen) {
             snprintf(buf, sizeof buf,
                      "Slicing Hopping Window requires size must be an integral multiple of slide, but got size %lldms and slide %lldms.",
                      (long long)size, (long long)slide);
-        else if (cfg->mode == OR_MODE_SQL && cfg->count_star_index < 0)
+        else if (cfg->mode == OR_MODE_SQL && cfg->count_star_index < 0 && !cfg->windowed)
             snprintf(buf, sizeof buf, "Hopping window requires a COUNT(*) in the aggregate functions.");
     } else if (cfg->kind == OR_CUMULATE) {
         /* SliceAssigners.java:299-310 */
@@ -678,6 +682,9 @@ or_op* or_open(const or_config* cfg, char* err, int errlen) {
     } else {
         snprintf(buf, sizeof buf, "unknown window kind %d", cfg->kind);
     }
+    if (!buf[0] && cfg->windowed && (cfg->mode != OR_MODE_SQL || cfg->proctime))
+        /* WindowedSliceAssigner.isEventTime() is always true (:430-434); SQL only */
+        snprintf(buf, sizeof buf, "a windowed slice assigner is an SQL event-time assigner");
     if (buf[0]) {
         if (err && errlen > 0) { strncpy(err, buf, (size_t)errlen - 1); err[errlen - 1] = 0; }
         return NULL;

@@ -44,7 +44,7 @@ typedef struct or_config {
     const int64_t* tz_trans;  /* tz_n transition instants (epoch ms, ascending) */
     const int64_t* tz_offs;   /* tz_n + 1 offsets (ms): [i] in force before transition i */
     int32_t tz_use_dst;       /* TimeZone.getTimeZone(zone).useDaylightTime() */
-    int32_t reserved1;
+    int32_t windowed;         /* WindowedSliceAssigner over the kind's assigner: ts = window_end */
 } or_config;
 
 /* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v), SUM0(v). */

@@ -38,7 +38,7 @@ class Config(C.Structure):
         ("tz_trans", C.c_void_p),
         ("tz_offs", C.c_void_p),
         ("tz_use_dst", C.c_int32),
-        ("reserved1", C.c_int32),
+        ("windowed", C.c_int32),
     ]
 
 
@@ -148,11 +148,12 @@ class OracleOperator:
     prepareSnapshotPreBarrier / snapshot-restore, with fired rows collected."""
 
     def __init__(self, mode=MODE_SQL, kind=TUMBLE, size=1000, slide=0, offset=0, tz_offset_ms=0,
-                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None, zone=None):
+                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None, zone=None, windowed=False):
         """zone: an IANA zone name whose rules (transitions, daylight saving) replace the fixed
         tz_offset_ms (TimeWindowUtil with a ZoneId)."""
         self.cfg = Config(mode, kind, size, slide, offset, tz_offset_ms, val_type, count_star_index,
                           1 if proctime else 0, 0)
+        self.cfg.windowed = 1 if windowed else 0
         self.zone = zone
         if zone is not None:
             from flink_amd.tz import zone_rules
@@ -205,7 +206,7 @@ class OracleOperator:
         h = lib().or_restore_copy(self._h)
         c = self.cfg
         return OracleOperator(c.mode, c.kind, c.size, c.slide, c.offset, c.tz_offset_ms, c.val_type,
-                              c.count_star_index, _handle=h, zone=self.zone)
+                              c.count_star_index, _handle=h, zone=self.zone, windowed=bool(c.windowed))
 
     def take_rows(self) -> np.ndarray:
         L = lib()

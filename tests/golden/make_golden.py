@@ -462,6 +462,7 @@ def assigner_fixtures():
                 c["config"]["zone"] = tzname
                 c["config"]["tz_offset_ms"] = 0
     cases += dst_assigner_fixtures()
+    cases += windowed_assigner_fixtures()
     errors = [  # testInvalidParameters of each assigner test
         dict(config=dict(kind="tumble", size=-1000, slide=0, offset=0),
              message="Tumbling Window parameters must satisfy size > 0, but got size -1000ms.",
@@ -531,6 +532,40 @@ def dst_assigner_fixtures():
             config=dict(cfg, offset=0, tz_offset_ms=0, zone="America/Los_Angeles"),
             assign=[[e, U(end)] for e, (start, end) in zip(DST_EPOCHS, exp)],
             window_start=[[U(end), U(start)] for start, end in exp]))
+    return out
+
+
+# WindowedSliceAssignerTest (TRT/operators/window/slicing/WindowedSliceAssignerTest.java:57-170):
+# SliceAssigners.windowed(0, inner) over tumbling(4 h), hopping(5 h, 1 h), cumulative(5 h, 1 h);
+# parameterized over America/Los_Angeles and Asia/Shanghai, with the same answers (the window
+# end attached to the row is taken as is; getWindowStart is the inner assigner's).
+def windowed_assigner_fixtures():
+    H = 3600 * 1000
+    U = utc_ms
+    d = lambda s: U("1970-01-01T" + s)
+    out = []
+    for zname, zcfg in (("America/Los_Angeles", dict(zone="America/Los_Angeles", tz_offset_ms=0)),
+                        ("Asia/Shanghai", dict(tz_offset_ms=SHANGHAI))):
+        src = "TRT/operators/window/slicing/WindowedSliceAssignerTest.java"
+        out.append(dict(
+            name=f"windowed_tumble_{zname}", source=src + ":57-84,152-163",
+            config=dict(kind="tumble", size=4 * H, slide=0, offset=0, windowed=True, **zcfg),
+            assign=[[d("00:00:00"), d("00:00:00")], [d("05:00:00"), d("05:00:00")], [d("10:00:00"), d("10:00:00")]],
+            window_start=[[d("00:00:00"), U("1969-12-31T20:00:00")], [d("04:00:00"), d("00:00:00")],
+                          [d("08:00:00"), d("04:00:00")]],
+            expired=[[d("00:00:00"), [d("00:00:00")]], [d("04:00:00"), [d("04:00:00")]],
+                     [d("10:00:00"), [d("10:00:00")]]]))
+        out.append(dict(
+            name=f"windowed_hop_{zname}", source=src + ":86-118",
+            config=dict(kind="hop", size=5 * H, slide=H, offset=0, windowed=True, **zcfg),
+            window_start=[[d(f"0{h}:00:00"), U(f"1969-12-31T{19 + h}:00:00")] for h in range(5)]
+            + [[d("05:00:00"), d("00:00:00")], [d("06:00:00"), d("01:00:00")], [d("10:00:00"), d("05:00:00")]]))
+        out.append(dict(
+            name=f"windowed_cumulate_{zname}", source=src + ":120-150",
+            config=dict(kind="cumulate", size=5 * H, slide=H, offset=0, windowed=True, **zcfg),
+            window_start=[[d("00:00:00"), U("1969-12-31T19:00:00")]]
+            + [[d(f"0{h}:00:00"), d("00:00:00")] for h in (1, 2, 3, 4, 5)]
+            + [[d("06:00:00"), d("05:00:00")], [d("10:00:00"), d("05:00:00")]]))
     return out
 
 

@@ -24,7 +24,7 @@ def oracle_mk(O, cfg):
     return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"], slide=cfg["slide"],
                             offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"], val_type=VT[cfg["val_type"]],
                             count_star_index=cfg["count_star_index"], proctime=cfg.get("proctime", False),
-                            zone=cfg.get("zone"))
+                            zone=cfg.get("zone"), windowed=cfg.get("windowed", False))
 
 
 @pytest.mark.parametrize("case", OP_CASES, ids=[c["name"] for c in OP_CASES])
@@ -402,3 +402,73 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     for x in local + glob:
         x.close()
     o.close()
+
+
+def windowed_rows(kind, size, slide, key, ts, val, isnull):
+    """A window TVF's output: every record once per window containing it (record-major),
+    with the window's end as its `window_end` column (offset 0)."""
+    S = size if kind == "tumble" else (np.gcd(size, slide) if kind == "hop" else slide)
+    se = (ts // S) * S + S
+    if kind == "tumble":
+        ends = [se]
+    elif kind == "hop":
+        ends = [se + j * S for j in range(size // S)]
+    else:
+        ws = (ts // size) * size
+        ends = [np.where(se + j * S <= ws + size, se + j * S, -1) for j in range(size // S)]
+    E = np.stack(ends, axis=1)
+    rep = (E >= 0).sum(axis=1)
+    keep = (E >= 0).ravel()
+    out = dict(key=np.repeat(key, rep), wend=E.ravel()[keep], val=np.repeat(val, rep), ts=np.repeat(ts, rep))
+    out["isnull"] = None if isnull is None else np.repeat(isnull, rep)
+    return out
+
+
+WINDOWED_CASES = [
+    ("windowed_tumble_f64", cfg_of("tumble", 1000), dict(n=200_000, keys=3000, batch=10_000, delay=300, jitter=900)),
+    ("windowed_hop_i64", cfg_of("hop", 3000, 1000, vt="i64"), dict(n=150_000, keys=2000, batch=12_000, delay=200, jitter=1500)),
+    ("windowed_cumulate_f64_nulls", cfg_of("cumulate", 4000, 1000), dict(n=150_000, keys=2000, batch=9_000, delay=100,
+                                                                        jitter=2500, null_frac=0.1)),
+    ("windowed_hop_regions_f64", cfg_of("hop", 4000, 1000), dict(n=600_000, keys=100_000, batch=60_000, delay=200,
+                                                                 jitter=800)),
+]
+
+
+@pytest.mark.parametrize("name,cfg,kw", WINDOWED_CASES, ids=[c[0] for c in WINDOWED_CASES])
+def test_windowed_input_parity(oracle_mod, name, cfg, kw):
+    """WindowedSliceAssigner (SliceAssigners.java:386-435): rows carrying their window_end;
+    late rows of fired windows dropped; window_start from the inner assigner."""
+    cfg = dict(cfg, windowed=True, count_star_index=-1 if cfg["kind"] == "hop" else 0)
+    key, ts, val, isnull = make_stream(kw["n"], kw["keys"], cfg["val_type"], jitter_ms=kw["jitter"],
+                                       null_frac=kw.get("null_frac", 0.0))
+    r = windowed_rows(cfg["kind"], cfg["size"], cfg["slide"], key, ts, val, isnull)
+    g = gpu_mk(cfg, expected_keys=kw["keys"], buffer_records=max(4 * kw["batch"], 1 << 16))
+    o = oracle_mk(oracle_mod, cfg)
+    n = len(r["key"])
+    mx = np.iinfo(np.int64).min
+    for step, lo in enumerate(range(0, n, kw["batch"])):
+        hi = min(n, lo + kw["batch"])
+        nl = None if r["isnull"] is None else r["isnull"][lo:hi]
+        for op in (g, o):
+            op.process_batch(r["key"][lo:hi], r["wend"][lo:hi], r["val"][lo:hi], nl)
+        mx = max(mx, int(r["ts"][lo:hi].max()))
+        g.process_watermark(mx - kw["delay"] - 1)
+        o.process_watermark(mx - kw["delay"] - 1)
+        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"{name} step {step}")
+        assert g.late_dropped == o.late_dropped, f"late drops differ at step {step}"
+    g.process_watermark(JMAX)
+    o.process_watermark(JMAX)
+    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"{name} final")
+    assert o.late_dropped > 0   # the jitter makes late rows of fired windows
+    g.close()
+    o.close()
+
+
+def test_windowed_input_off_grid_is_loud():
+    """A window_end off the window's slice grid is rejected, never silently re-sliced."""
+    import flink_amd as F
+    op = F.WindowAggOperator(F.tumbling(1000), windowed=True, expected_keys=100)
+    with pytest.raises(F.WindowSpecError, match="off the slice grid"):
+        op.process_batch(np.arange(4, dtype=np.int64), np.array([1000, 2000, 2500, 3000], dtype=np.int64),
+                         np.ones(4))
+    op.close()

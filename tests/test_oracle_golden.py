@@ -31,7 +31,8 @@ def test_assigner_golden(oracle_mod, case):
     c = case["config"]
     cs = 0 if c["kind"] == "hop" else -1
     op = oracle_mod.OracleOperator(kind=KIND[c["kind"]], size=c["size"], slide=c["slide"], offset=c["offset"],
-                                   tz_offset_ms=c["tz_offset_ms"], count_star_index=cs, zone=c.get("zone"))
+                                   tz_offset_ms=c["tz_offset_ms"], count_star_index=cs, zone=c.get("zone"),
+                                   windowed=c.get("windowed", False))
     for ts, exp in case.get("assign", []):
         assert op.assign_slice_end(ts) == exp
     for w, exp in case.get("window_start", []):
