@@ -16,7 +16,7 @@ FG_OK, FG_EINVAL, FG_EFULL, FG_EDEVICE, FG_ECAPACITY, FG_ESTATE = range(6)
 MODE_SQL, MODE_DATASTREAM = 0, 1
 TUMBLE, HOP, CUMULATE = 0, 1, 2
 VAL_NONE, VAL_I64, VAL_F64 = 0, 1, 2
-AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_AVG, AGG_SUM0 = 0, 1, 2, 3, 4
+AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_AVG, AGG_SUM0, AGG_MIN, AGG_MAX = 0, 1, 2, 3, 4, 5, 6
 HOST, DEVICE = 0, 1
 KEYHASH_BINARYROW_BIGINT, KEYHASH_JAVA_LONG = 0, 1
 MAX_AGGS = 8

@@ -157,6 +157,7 @@ struct PendingEv {
 }  // namespace
 
 struct fg_handle {
+    int32_t kvt = 0;   // kernel value op (val_type | op << 2)
     fg_config cfg{};
     WindowSpec w{};
     int device = 0;
@@ -472,7 +473,7 @@ int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, Heav
     hp->threshold = threshold;
     hp->chunk = kHeavyChunk;
     hp->max_chunks = (int32_t)std::min<int64_t>(h->hv_max_chunks, INT32_MAX);
-    hp->val_type = h->cfg.val_type;
+    hp->val_type = h->kvt;
     hp->heavy = h->hv_flags.as<uint8_t>();
     hp->region_list = h->hv_list.as<int32_t>();
     hp->n_list = h->hv_n.as<int32_t>();
@@ -598,7 +599,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         p.src = d_src;
         p.n_batches = (int)sb.size();
         p.batches = d_sb;
-        p.val_type = h->cfg.val_type;
+        p.val_type = h->kvt;
         p.has_dst = dstt ? 1 : 0;
         p.dst = tr;
         p.emit = 0;
@@ -737,7 +738,7 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     p.region_bits = h->region_bits;
     p.n_src = (int)refs.size();
     p.src = d_src;
-    p.val_type = h->cfg.val_type;
+    p.val_type = h->kvt;
     p.has_dst = dst != nullptr;
     if (dst) p.dst = ref_of(dst);
     fill_emit(h, p, wend);
@@ -1333,7 +1334,23 @@ int validate(const fg_config* c, std::string* msg) {
         if (c->num_aggs < 1 || c->num_aggs > FG_MAX_AGGS)
             snprintf(buf, sizeof buf, "num_aggs must be in [1, %d]", FG_MAX_AGGS);
         for (int a = 0; a < c->num_aggs && !buf[0]; a++)
-            if (c->aggs[a] < FG_AGG_COUNT_STAR || c->aggs[a] > FG_AGG_SUM0) snprintf(buf, sizeof buf, "bad agg %d", c->aggs[a]);
+            if (c->aggs[a] < FG_AGG_COUNT_STAR || c->aggs[a] > FG_AGG_MAX) snprintf(buf, sizeof buf, "bad agg %d", c->aggs[a]);
+        if (!buf[0]) {   // one value accumulator per (key, slice): SUM-family, MIN or MAX
+            int kinds = 0;
+            bool sum_family = false, has_min = false, has_max = false;
+            for (int a = 0; a < c->num_aggs; a++) {
+                sum_family |= c->aggs[a] == FG_AGG_SUM || c->aggs[a] == FG_AGG_AVG || c->aggs[a] == FG_AGG_SUM0;
+                has_min |= c->aggs[a] == FG_AGG_MIN;
+                has_max |= c->aggs[a] == FG_AGG_MAX;
+            }
+            kinds = (int)sum_family + (int)has_min + (int)has_max;
+            if (kinds > 1 && !(c->flags & FG_FLAG_LOCAL_PARTIALS))
+                snprintf(buf, sizeof buf,
+                         "MIN and MAX take an operator of their own (one value accumulator per key and slice); "
+                         "they do not mix with each other or with SUM/AVG/SUM0");
+            else if ((has_min || has_max) && c->mode != FG_MODE_SQL)
+                snprintf(buf, sizeof buf, "MIN/MAX are SQL aggregates (DataStream windows here reduce with SumAggregator)");
+        }
         if (c->val_type < FG_VAL_NONE || c->val_type > FG_VAL_F64) snprintf(buf, sizeof buf, "bad val_type");
         if (c->val_type == FG_VAL_NONE)
             for (int a = 0; a < c->num_aggs && !buf[0]; a++)
@@ -1366,10 +1383,14 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             g_open_error = "FG_FLAG_LOCAL_PARTIALS needs an SQL operator with a value column";
             return FG_EINVAL;
         }
+        // a MIN / MAX in the global operator's list makes the partial accumulator a MIN / MAX
+        int32_t vagg = FG_AGG_SUM;
+        for (int a = 0; a < c.num_aggs && a < FG_MAX_AGGS; a++)
+            if (c.aggs[a] == FG_AGG_MIN || c.aggs[a] == FG_AGG_MAX) vagg = c.aggs[a];
         c.num_aggs = 3;
         c.aggs[0] = FG_AGG_COUNT_STAR;
         c.aggs[1] = FG_AGG_COUNT;
-        c.aggs[2] = FG_AGG_SUM;
+        c.aggs[2] = vagg;
     }
     const bool proctime = (c.flags & FG_FLAG_PROCTIME) != 0;
     if (proctime && (c.mode != FG_MODE_SQL || local)) {
@@ -1420,6 +1441,11 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     }
     std::unique_ptr<fg_handle> h(new fg_handle());
     h->cfg = c;
+    h->kvt = c.val_type;   // kernel value op: val_type | op << 2 (op 1 MIN, 2 MAX; fg_kernels.hip lds_add)
+    for (int a = 0; a < c.num_aggs; a++) {
+        if (c.aggs[a] == FG_AGG_MIN) h->kvt = c.val_type | (1 << 2);
+        if (c.aggs[a] == FG_AGG_MAX) h->kvt = c.val_type | (2 << 2);
+    }
     h->local = local;
     h->proctime = proctime;
     h->device = cfg->device_id;
@@ -1863,7 +1889,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         p.src = d_src;
         p.n_batches = 1;
         p.batches = d_sb;
-        p.val_type = h->cfg.val_type;
+        p.val_type = h->kvt;
         p.has_dst = 1;
         p.dst = tr;
         p.overflow = h->scalars.as<unsigned int>();

@@ -1181,6 +1181,11 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
                 else v = sum;
                 break;
             case 4: v = sum; break;           // SUM0(v): 0-initialised, never NULL
+            case 5:                           // MIN(v) / MAX(v): NULL when no non-null value
+            case 6:
+                if (cv == 0) nm |= (uint8_t)(1u << a);
+                else v = sum;
+                break;
             default:                          // AVG(v): count == 0 ? NULL : sum / count
                 if (cv == 0) nm |= (uint8_t)(1u << a);
                 else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
@@ -1195,6 +1200,46 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
 constexpr int kSrcU = 2;          // source-table entries per thread per round (wide merge)
 constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
 
+// Value accumulator of an entry (kernel vt = val_type | op << 2; val_type 1 BIGINT, 2 DOUBLE;
+// op 0 SUM/AVG/SUM0, 1 MIN, 2 MAX). MIN/MAX restate Min/MaxAggFunction
+// (TP/functions/aggfunctions/MinAggFunction.java:61-90, MaxAggFunction.java:61-96):
+// the operand replaces the accumulator iff `operand < min` (`>` for MAX), Java primitive
+// comparison; a NULL accumulator is the identity (+inf / Long.MAX_VALUE for MIN), and an
+// entry without non-null values (COUNT(v) = 0) emits NULL, so the identity is never seen.
+constexpr int kOpShift = 2;
+__device__ __forceinline__ int64_t val_identity(int vt) {
+    switch (vt) {
+        case 1 | (1 << kOpShift): return INT64_MAX;
+        case 1 | (2 << kOpShift): return JMIN;
+        case 2 | (1 << kOpShift): return 0x7FF0000000000000ll;    // +inf
+        case 2 | (2 << kOpShift): return (int64_t)0xFFF0000000000000ull;   // -inf
+        default: return 0;
+    }
+}
+// a op b (wave pre-reduction of hot keys)
+__device__ __forceinline__ int64_t val_combine(int64_t a, int64_t b, int vt) {
+    switch (vt) {
+        case 1: return (int64_t)((uint64_t)a + (uint64_t)b);
+        case 2: return __double_as_longlong(__longlong_as_double(a) + __longlong_as_double(b));
+        case 1 | (1 << kOpShift): return b < a ? b : a;
+        case 1 | (2 << kOpShift): return b > a ? b : a;
+        case 2 | (1 << kOpShift): return __longlong_as_double(b) < __longlong_as_double(a) ? b : a;
+        case 2 | (2 << kOpShift): return __longlong_as_double(b) > __longlong_as_double(a) ? b : a;
+        default: return 0;
+    }
+}
+// DOUBLE MIN/MAX in LDS: compare-and-swap while the operand still wins (Java `<` / `>`)
+template <bool kMin>
+__device__ __forceinline__ void lds_minmax_f64(unsigned long long* a, int64_t bits) {
+    const double v = __longlong_as_double(bits);
+    unsigned long long cur = *a;
+    while (kMin ? v < __longlong_as_double((int64_t)cur) : v > __longlong_as_double((int64_t)cur)) {
+        const unsigned long long old = atomicCAS(a, cur, (unsigned long long)bits);
+        if (old == cur) break;
+        cur = old;
+    }
+}
+
 template <bool C>
 __device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long long cs, unsigned long long cn,
                                         int64_t sum_bits, int vt) {
@@ -1208,6 +1253,14 @@ __device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long
         atomicAdd(reinterpret_cast<double*>(&t.sum[slot]), __longlong_as_double(sum_bits));
     } else if (vt == 1) {
         atomicAdd(&t.sum[slot], (unsigned long long)sum_bits);
+    } else if (vt > 3 && cn < cs) {   // MIN / MAX; an accumulator with COUNT(v) = 0 holds no value
+        switch (vt) {
+            case 1 | (1 << kOpShift): atomicMin(reinterpret_cast<long long*>(&t.sum[slot]), (long long)sum_bits); break;
+            case 1 | (2 << kOpShift): atomicMax(reinterpret_cast<long long*>(&t.sum[slot]), (long long)sum_bits); break;
+            case 2 | (1 << kOpShift): lds_minmax_f64<true>(&t.sum[slot], sum_bits); break;
+            case 2 | (2 << kOpShift): lds_minmax_f64<false>(&t.sum[slot], sum_bits); break;
+            default: break;
+        }
     }
 }
 
@@ -1247,6 +1300,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     const int lane = tid & 63, wave = tid >> 6;
     const int cap = kRegionCap;
     const int vt = p.val_type;
+    const int64_t vinit = val_identity(vt);
     const int P = 1 << p.region_bits;
     const int G = gridDim.x;
     // regions: all P (strided over the grid), or the heavy pass's list
@@ -1401,7 +1455,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             t.key[i] = JMIN;
             t.cs[i] = 0;
             if constexpr (!C) t.cn[i] = 0;
-            t.sum[i] = 0;
+            t.sum[i] = (unsigned long long)vinit;
         }
         if (tid == 0) s_flags = 0;
         if constexpr (!C) if (tid < 64) {   // source tables: per-region entry counts -> flat prefix
@@ -1753,13 +1807,14 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
     __shared__ unsigned int s_full;
     const int tid = threadIdx.x, lane = tid & 63;
     const int vt = hp.val_type;
+    const int64_t vinit = val_identity(vt);
     const int nch = *gbl(hp.n_list + 1);
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
         for (int i = tid; i <= kSlots; i += T) {
             t.key[i] = JMIN;
             t.cs[i] = 0;
             t.cn[i] = 0;
-            t.sum[i] = 0;
+            t.sum[i] = (unsigned long long)vinit;
         }
         if (tid == 0) {
             s_n = 0;
@@ -1813,8 +1868,11 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
                         double d = in ? __longlong_as_double(sum) : 0.0;
                         for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
                         part = __double_as_longlong(d);
-                    } else {
+                    } else if (vt == 1) {
                         for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+                    } else if (vt > 3) {   // MIN / MAX: lanes outside the run hold the identity
+                        part = in ? sum : vinit;
+                        for (int off = 32; off > 0; off >>= 1) part = val_combine(part, __shfl_xor(part, off), vt);
                     }
                     if (in) {
                         done = true;

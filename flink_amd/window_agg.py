@@ -32,9 +32,11 @@ import numpy as np
 from . import _lib as L
 
 AGG_NAMES = {L.AGG_COUNT_STAR: "count_star", L.AGG_COUNT: "count", L.AGG_SUM: "sum", L.AGG_AVG: "avg",
-             L.AGG_SUM0: "sum0"}
+             L.AGG_SUM0: "sum0", L.AGG_MIN: "min", L.AGG_MAX: "max"}
 AGGS = {"count_star": L.AGG_COUNT_STAR, "count": L.AGG_COUNT, "sum": L.AGG_SUM, "avg": L.AGG_AVG,
-        "sum0": L.AGG_SUM0}
+        "sum0": L.AGG_SUM0, "min": L.AGG_MIN, "max": L.AGG_MAX}
+# aggregates whose column has the value's type (DOUBLE for f64 values)
+VALUE_TYPED = (L.AGG_SUM, L.AGG_AVG, L.AGG_SUM0, L.AGG_MIN, L.AGG_MAX)
 
 
 @dataclass(frozen=True)
@@ -92,7 +94,7 @@ class WindowAggOperator:
         local_partials: the local phase of the two-phase aggregation
         (LocalSlicingWindowAggOperator + LocalAggCombiner): process_watermark returns one
         partial accumulator row per (key, fired slice) with columns count_star, count, sum
-        (window_start/window_end = the slice), to be exchanged by key group and merged by a
+        (min / max for a MIN / MAX query; window_start/window_end = the slice), to be exchanged by key group and merged by a
         global operator's process_partials."""
         lib = L.load()
         self.window = window
@@ -100,7 +102,9 @@ class WindowAggOperator:
         self.val_type = {"none": L.VAL_NONE, "i64": L.VAL_I64, "f64": L.VAL_F64}[val_type]
         self.local_partials = bool(local_partials)
         if self.local_partials:
-            aggs = ("count_star", "count", "sum")
+            # the partial accumulator: SUM, or the MIN / MAX of a MIN / MAX query
+            vagg = next((a for a in aggs if a in ("min", "max", L.AGG_MIN, L.AGG_MAX)), "sum")
+            aggs = ("count_star", "count", AGG_NAMES.get(vagg, vagg))
         self.aggs = tuple(AGGS[a] if isinstance(a, str) else int(a) for a in aggs)
         cfg = L.FgConfig()
         cfg.mode = self.mode
@@ -241,7 +245,7 @@ class WindowAggOperator:
         fields = [("key", "<i8"), ("window_start", "<i8"), ("window_end", "<i8")]
         for a in self.aggs:
             nm = AGG_NAMES[a]
-            is_f = self.val_type == L.VAL_F64 and a in (L.AGG_SUM, L.AGG_AVG, L.AGG_SUM0)
+            is_f = self.val_type == L.VAL_F64 and a in VALUE_TYPED
             fields.append((nm, "<f8" if is_f else "<i8"))
             fields.append((nm + "_null", "?"))
         if self.mode == L.MODE_DATASTREAM:

@@ -74,7 +74,14 @@ enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
  * CountAggFunction, AvgAggFunction, Sum0AggFunction of TP/functions/aggfunctions/).
  * SUM0 (Sum0AggFunction.java:60-63,75-76,97-98,136-137,162-163): 0-initialised, never NULL;
  * its value is the AVG accumulator's sum. */
-enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3, FG_AGG_SUM0 = 4 };
+/* MIN / MAX (MinAggFunction.java:56-90, MaxAggFunction.java:56-96, TP/functions/aggfunctions/):
+ * NULL-initialised; a non-null operand replaces the accumulator iff operand < min (> max),
+ * Java primitive comparison; NULL when the window holds no non-null value. An operator keeps
+ * ONE value accumulator per (key, slice), so MIN and MAX each take an operator of their own
+ * and do not mix with SUM / AVG / SUM0 (COUNT(*) and COUNT do mix): FG_EINVAL otherwise. A
+ * query with several value aggregates opens one handle per accumulator kind. */
+enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3, FG_AGG_SUM0 = 4,
+              FG_AGG_MIN = 5, FG_AGG_MAX = 6 };
 /* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
  * producer before it (complete, or an event the stream waits on). They are fully read when
  * fg_add_batch / fg_add_partials return. */
@@ -88,7 +95,8 @@ enum fg_flags {
      * late handling, and fg_advance_progress emits, for every slice the watermark fires, one
      * partial accumulator row per key instead of window rows: window_start/window_end = the
      * slice, agg[0] = COUNT(*), agg[1] = COUNT(v), agg[2] = SUM bits (0 when COUNT(v) = 0).
-     * fg_config.aggs is ignored (the global operator's list applies). */
+     * fg_config.aggs is ignored (the global operator's list applies), except that a MIN or
+     * MAX in it makes agg[2] the partial MIN / MAX instead of the SUM. */
     FG_FLAG_LOCAL_PARTIALS = 2,
     /* SQL processing-time windows (SliceAssigner.isEventTime() == false,
      * AbstractWindowAggProcessor.java:137-140): `rowtime` carries each record's processing

@@ -136,12 +136,19 @@ static int pmap_remove(pmap* m, int64_t a, int64_t b, int64_t* old) {
  *   SUM0(v)   -> Sum0AggFunction     TP/functions/aggfunctions/Sum0AggFunction.java:60-63,75-76
  *                (0 init :97-98/:136-137/:162-163, sum0 + v for non-null v): the same
  *                accumulator as AVG's sum, so it is read from avg_sum_* at emit
+ *   MIN(v)    -> MinAggFunction      TP/functions/aggfunctions/MinAggFunction.java:56-90
+ *   MAX(v)    -> MaxAggFunction      TP/functions/aggfunctions/MaxAggFunction.java:56-96
+ *                null init; accumulate/merge: isNull(operand) ? acc : isNull(acc) ? operand :
+ *                lessThan(operand, acc) ? operand : acc (greaterThan for MAX), Java primitive
+ *                comparison. Null exactly when SUM is null, so sum_null serves all three.
  * ---------------------------------------------------------------------------------- */
 typedef struct {
     int64_t cnt_star, cnt_val;
     int64_t sum_i, avg_sum_i;
     double sum_d, avg_sum_d;
     int32_t sum_null;
+    int64_t min_i, max_i;
+    double min_d, max_d;
 } or_acc;
 
 static inline void acc_create(or_acc* a) {   /* initialValuesExpressions */
@@ -155,11 +162,15 @@ static inline void acc_accumulate(or_acc* a, int vt, int64_t vbits, int isnull) 
     if (vt == OR_VAL_I64) {
         a->sum_i = a->sum_null ? vbits : jadd(a->sum_i, vbits);   /* isNull(sum) ? v : sum + v */
         a->avg_sum_i = jadd(a->avg_sum_i, vbits);
+        a->min_i = a->sum_null ? vbits : (vbits < a->min_i ? vbits : a->min_i);
+        a->max_i = a->sum_null ? vbits : (vbits > a->max_i ? vbits : a->max_i);
     } else if (vt == OR_VAL_F64) {
         double d;
         memcpy(&d, &vbits, 8);
         a->sum_d = a->sum_null ? d : a->sum_d + d;
         a->avg_sum_d = a->avg_sum_d + d;
+        a->min_d = a->sum_null ? d : (d < a->min_d ? d : a->min_d);
+        a->max_d = a->sum_null ? d : (d > a->max_d ? d : a->max_d);
     }
     a->sum_null = 0;
 }
@@ -167,8 +178,15 @@ static inline void acc_merge(or_acc* a, const or_acc* o, int vt) {   /* mergeExp
     a->cnt_star = jadd(a->cnt_star, o->cnt_star);
     a->cnt_val = jadd(a->cnt_val, o->cnt_val);
     if (!o->sum_null) {
-        if (vt == OR_VAL_I64) a->sum_i = a->sum_null ? o->sum_i : jadd(a->sum_i, o->sum_i);
-        else a->sum_d = a->sum_null ? o->sum_d : a->sum_d + o->sum_d;
+        if (vt == OR_VAL_I64) {
+            a->sum_i = a->sum_null ? o->sum_i : jadd(a->sum_i, o->sum_i);
+            a->min_i = a->sum_null ? o->min_i : (o->min_i < a->min_i ? o->min_i : a->min_i);
+            a->max_i = a->sum_null ? o->max_i : (o->max_i > a->max_i ? o->max_i : a->max_i);
+        } else {
+            a->sum_d = a->sum_null ? o->sum_d : a->sum_d + o->sum_d;
+            a->min_d = a->sum_null ? o->min_d : (o->min_d < a->min_d ? o->min_d : a->min_d);
+            a->max_d = a->sum_null ? o->max_d : (o->max_d > a->max_d ? o->max_d : a->max_d);
+        }
         a->sum_null = 0;
     }
     a->avg_sum_i = jadd(a->avg_sum_i, o->avg_sum_i);
@@ -491,6 +509,10 @@ static void emit_row(or_op* op, int64_t key, int64_t wstart, int64_t wend, const
     }
     r->sum0_i = a->avg_sum_i;   /* Sum0AggFunction.getValueExpression :85 */
     r->sum0_d = a->avg_sum_d;
+    r->min_i = a->min_i;   /* Min/MaxAggFunction.getValueExpression: the accumulator (NULL iff sum_null) */
+    r->max_i = a->max_i;
+    r->min_d = a->min_d;
+    r->max_d = a->max_d;
     r->out_ts = out_ts;
 }
 

@@ -47,7 +47,7 @@ typedef struct or_config {
     int32_t windowed;         /* WindowedSliceAssigner over the kind's assigner: ts = window_end */
 } or_config;
 
-/* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v), SUM0(v). */
+/* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v), SUM0(v), MIN(v), MAX(v). */
 typedef struct or_row {
     int64_t key;
     int64_t window_start;
@@ -63,6 +63,10 @@ typedef struct or_row {
     int64_t out_ts;     /* DataStream: emitted StreamRecord timestamp (end - 1) */
     int64_t sum0_i;     /* SUM0 for i64 values (Sum0AggFunction: 0-initialised, never NULL) */
     double  sum0_d;     /* SUM0 for f64 values                                  */
+    int64_t min_i;      /* MIN / MAX (Min/MaxAggFunction; NULL exactly when sum_null) */
+    int64_t max_i;
+    double  min_d;
+    double  max_d;
 } or_row;
 
 typedef struct or_op or_op;

@@ -58,6 +58,10 @@ class Row(C.Structure):
         ("out_ts", C.c_int64),
         ("sum0_i", C.c_int64),
         ("sum0_d", C.c_double),
+        ("min_i", C.c_int64),
+        ("max_i", C.c_int64),
+        ("min_d", C.c_double),
+        ("max_d", C.c_double),
     ]
 
 
@@ -67,6 +71,7 @@ ROW_DTYPE = np.dtype(
         ("cnt_star", "<i8"), ("cnt_val", "<i8"), ("sum_i", "<i8"), ("sum_d", "<f8"),
         ("avg_i", "<i8"), ("avg_d", "<f8"), ("sum_null", "<i4"), ("avg_null", "<i4"),
         ("out_ts", "<i8"), ("sum0_i", "<i8"), ("sum0_d", "<f8"),
+        ("min_i", "<i8"), ("max_i", "<i8"), ("min_d", "<f8"), ("max_d", "<f8"),
     ]
 )
 assert ROW_DTYPE.itemsize == C.sizeof(Row)

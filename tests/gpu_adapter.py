@@ -20,7 +20,7 @@ class GpuOperator:
     def __init__(self, cfg, expected_keys=1 << 12, buffer_records=1 << 20, _op=None, kernel_timing=False):
         self.cfg = cfg
         self.op = _op or F.WindowAggOperator(
-            window_of(cfg), aggs=("count_star", "count", "sum", "avg", "sum0"), val_type=cfg["val_type"],
+            window_of(cfg), aggs=cfg.get("aggs", ("count_star", "count", "sum", "avg", "sum0")), val_type=cfg["val_type"],
             mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
             buffer_records=buffer_records, kernel_timing=kernel_timing, proctime=cfg.get("proctime", False),
             zone=cfg.get("zone"), windowed=cfg.get("windowed", False))
@@ -64,10 +64,12 @@ class GpuOperator:
         out["window_end"] = r["window_end"]
         out["cnt_star"] = r["count_star"]
         out["cnt_val"] = r["count"]
-        out["sum_null"] = r["sum_null"]
-        out["avg_null"] = r["avg_null"]
+        # a MIN / MAX operator has no SUM / AVG: its NULL mask is theirs (COUNT(v) = 0)
+        vnull = next(r[c + "_null"] for c in ("sum", "min", "max", "avg") if c in r.dtype.names)
+        out["sum_null"] = r["sum_null"] if "sum_null" in r.dtype.names else vnull
+        out["avg_null"] = r["avg_null"] if "avg_null" in r.dtype.names else vnull
         sfx = "_d" if self.cfg["val_type"] == "f64" else "_i"
-        for name in ("sum", "avg", "sum0"):
+        for name in ("sum", "avg", "sum0", "min", "max"):
             if name in r.dtype.names:
                 out[name + sfx] = r[name]
         if "rowtime" in r.dtype.names:

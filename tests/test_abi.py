@@ -86,3 +86,23 @@ def test_zone_rules_validated_before_device():
         F.WindowAggOperator(F.tumbling(1000), mode="datastream", val_type="i64", zone="America/Los_Angeles")
     with pytest.raises(F.WindowSpecError):
         F.WindowAggOperator(F.tumbling(1000), local_partials=True, zone="America/Los_Angeles")
+
+
+def test_min_max_accumulator_rules():
+    """MIN / MAX keep the operator's one value accumulator (include/flinkgpu.h fg_agg): they
+    take an operator of their own, SQL only; validated before any device call."""
+    import torch
+    import flink_amd as F
+    for aggs in (("sum", "min"), ("min", "max"), ("avg", "max"), ("sum0", "min")):
+        with pytest.raises(F.WindowSpecError):
+            F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="f64")
+    with pytest.raises(F.WindowSpecError):
+        F.WindowAggOperator(F.tumbling(1000), aggs=("max",), mode="datastream", val_type="i64")
+    with pytest.raises(F.WindowSpecError):
+        F.WindowAggOperator(F.tumbling(1000), aggs=("count_star", "min"), val_type="none")
+    if torch.cuda.is_available():
+        return
+    for aggs in (("count_star", "count", "min"), ("max",)):   # valid: fails only for want of a device
+        with pytest.raises(F.FlinkGpuError) as ei:
+            F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="i64")
+        assert ei.value.code == L.FG_EDEVICE

@@ -40,7 +40,7 @@ def sort_rows(r):
     return r[np.lexsort((r["key"], r["window_end"]))]
 
 
-def assert_rows_equal(got, exp, vt, ctx="", sum0=True):
+def assert_rows_equal(got, exp, vt, ctx="", sum0=True, minmax=()):
     assert len(got) == len(exp), f"{ctx}: {len(got)} rows vs {len(exp)} expected"
     if len(got) == 0:
         return
@@ -48,6 +48,14 @@ def assert_rows_equal(got, exp, vt, ctx="", sum0=True):
     for f in ("key", "window_start", "window_end", "cnt_star", "cnt_val", "sum_null", "avg_null", "out_ts"):
         bad = np.nonzero(g[f] != e[f])[0]
         assert len(bad) == 0, f"{ctx}: field {f} differs at {bad[:5]}: {g[f][bad[:5]]} vs {e[f][bad[:5]]}"
+    if minmax:   # MIN / MAX operator: bit-exact (order-independent), NULL exactly when SUM is
+        ok = e["sum_null"] == 0
+        for m in minmax:
+            f = m + ("_i" if vt == "i64" else "_d")
+            a, b = g[f][ok].view(np.int64), e[f][ok].view(np.int64)
+            bad = np.nonzero(a != b)[0]
+            assert len(bad) == 0, f"{ctx}: {m.upper()} differs at {bad[:5]}: {g[f][ok][bad[:5]]} vs {e[f][ok][bad[:5]]}"
+        return
     if vt == "i64":
         ok = e["sum_null"] == 0
         assert np.array_equal(g["sum_i"][ok], e["sum_i"][ok]), f"{ctx}: i64 SUM differs"
@@ -68,6 +76,7 @@ def assert_rows_equal(got, exp, vt, ctx="", sum0=True):
 def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at=None, end_wm=JMAX,
                expected_keys=None, kstats=None, **gen):
     key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
+    mm = tuple(a for a in cfg.get("aggs", ()) if a in ("min", "max"))
     g = gpu_mk(cfg, expected_keys=expected_keys or keys, buffer_records=max(batch * 4, 1 << 16),
                kernel_timing=kstats is not None)
     o = oracle_mk(O, cfg)
@@ -79,7 +88,7 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
         o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], nl)
         g.process_watermark(wm)
         o.process_watermark(wm)
-        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"step {step} wm {wm}")
+        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"step {step} wm {wm}", minmax=mm)
         assert g.late_dropped == o_base + o.late_dropped, f"late drops differ at step {step}"
         step += 1
         if snapshot_at is not None and step == snapshot_at:
@@ -92,7 +101,7 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
             g, o = g2, o2
     g.process_watermark(end_wm)
     o.process_watermark(end_wm)
-    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final")
+    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final", minmax=mm)
     late = g.late_dropped
     if kstats is not None:
         kstats.update(g.op.kernel_stats())
@@ -175,6 +184,38 @@ STREAM_CASES = [
     ("dst_proctime_cumulate_fall", dict(cfg_of("cumulate", 3 * 3600_000, 3600_000, zone=LA), proctime=True),
      dict(n=300_000, keys=20_000, batch=20_000, delay=0, jitter=0, t0=FALL - 1800_000, rate_per_ms=0.02)),
 ]
+
+
+MIN_AGGS = ("count_star", "count", "min")
+MAX_AGGS = ("count_star", "count", "max")
+# MIN / MAX (Min/MaxAggFunction): one operator per accumulator kind over the paths the SUM
+# family takes -- small-table and two-pass partitions, compact and wide merges, NULLs, late
+# records, hop/cumulate slice merges, Zipf heavy pass (wave pre-reduction by min/max),
+# processing time, daylight-saving zones, DataStream excluded (SumAggregator only)
+MINMAX_BASE = [c for c in STREAM_CASES if c[0] in (
+    "tumble_f64_inorder", "tumble_i64_ooo", "tumble_i64_wrap", "tumble_f64_nulls_late", "tumble_spread_keys",
+    "hop_f64", "hop_i64_late", "cumulate_f64", "cumulate_i64_late", "regions_f64_nulls_late",
+    "regions_i64_ooo_lanes", "regions_hop_f64", "regions_cumulate_i64_late", "big_units_i64_nulls_ooo",
+    "proctime_cumulate_i64", "zipf_tumble_f64", "zipf_tumble_i64_nulls_late", "zipf_hop_f64",
+    "dst_hop_fall_i64")]
+MINMAX_CASES = [(f"{m}_{name}", dict(cfg, aggs=aggs), kw) for name, cfg, kw in MINMAX_BASE
+                for m, aggs in (("min", MIN_AGGS), ("max", MAX_AGGS))]
+
+
+@pytest.mark.parametrize("name,cfg,kw", MINMAX_CASES, ids=[c[0] for c in MINMAX_CASES])
+def test_min_max_parity(oracle_mod, name, cfg, kw):
+    ks = {} if kw.get("zipf") else None
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    if ks is not None:
+        assert ks.get("merge_heavy", {}).get("launches", 0) > 0, ks
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_min_max_snapshot_restore(oracle_mod, kind):
+    for aggs in (MIN_AGGS, MAX_AGGS):
+        cfg = dict(cfg_of(kind, 4000, 0 if kind == "tumble" else 1000, vt="i64"), aggs=aggs)
+        drive_both(oracle_mod, cfg, n=120_000, keys=2000, batch=6_000, delay=100, jitter=500, snapshot_at=7,
+                   null_frac=0.1)
 
 
 @pytest.mark.parametrize("name,cfg,kw", STREAM_CASES, ids=[c[0] for c in STREAM_CASES])
@@ -343,6 +384,13 @@ TWO_PHASE_CASES = [
     # hot keys in the local phase: skewed regions take the heavy pass before the exchange
     ("zipf_tumble_f64", cfg_of("tumble", 1000), dict(n=6_000_000, keys=100_000, batch=3_000_000, delay=0, jitter=0,
                                                       rate_per_ms=3_000, zipf=1.1)),
+    # MIN / MAX partial accumulators (LocalAggCombiner merges with Min/MaxAggFunction.merge)
+    ("min_hop_f64_late", dict(cfg_of("hop", 3000, 1000), aggs=MIN_AGGS), dict(n=300_000, keys=30_000, batch=20_000,
+                                                                             delay=200, jitter=1500)),
+    ("max_cumulate_i64_late", dict(cfg_of("cumulate", 4000, 500, vt="i64"), aggs=MAX_AGGS),
+     dict(n=300_000, keys=30_000, batch=15_000, delay=50, jitter=2500)),
+    ("max_zipf_tumble_f64", dict(cfg_of("tumble", 1000), aggs=MAX_AGGS),
+     dict(n=6_000_000, keys=100_000, batch=3_000_000, delay=0, jitter=0, rate_per_ms=3_000, zipf=1.1)),
 ]
 
 
@@ -360,8 +408,10 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter,
                                   **{k: kw[k] for k in ("rate_per_ms", "zipf") if k in kw})
     w = window_of(cfg)
-    aggs = ("count_star", "count", "sum", "avg", "sum0")
-    local = [F.WindowAggOperator(w, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
+    aggs = cfg.get("aggs", ("count_star", "count", "sum", "avg", "sum0"))
+    mm = tuple(a for a in aggs if a in ("min", "max"))
+    vcol = mm[0] if mm else "sum"   # the partial accumulator column
+    local = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
                                  local_partials=True) for _ in range(S)]
     glob = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys // R + 1,
                                 buffer_records=1 << 18) for _ in range(R)]
@@ -373,7 +423,7 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
         if len(rows) == 0:
             return
         owner = F.key_groups(rows["key"], MAXP).astype(np.int64) * R // MAXP
-        sums = rows["sum"].view(np.int64) if rows["sum"].dtype == np.float64 else rows["sum"]
+        sums = rows[vcol].view(np.int64) if rows[vcol].dtype == np.float64 else rows[vcol]
         for r in range(R):
             m = owner == r
             glob[r].process_partials(rows["key"][m], rows["window_end"][m], rows["count_star"][m],
@@ -398,7 +448,7 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     adapter = GpuOperator.__new__(GpuOperator)
     adapter.cfg = cfg
     adapter._rows = [g]
-    assert_rows_equal(adapter.take_rows(), np.concatenate(exp), cfg["val_type"], name)
+    assert_rows_equal(adapter.take_rows(), np.concatenate(exp), cfg["val_type"], name, minmax=mm)
     for x in local + glob:
         x.close()
     o.close()
