@@ -275,8 +275,10 @@ class WindowAggOperator:
         """Flush the staged buffer into the GPU-resident state (RecordsWindowBuffer.flush)."""
         L.check(self._lib.fg_flush(self._h), self._h)
 
-    def snapshot_state(self):
-        """(state image dict of numpy arrays, timer watermark): the window-aggs ValueState."""
+    def snapshot_state(self, copy: bool = True):
+        """(state image dict of numpy arrays, timer watermark): the window-aggs ValueState.
+        copy=False returns views of the library-owned pinned host image (what a JNI shim hands
+        to the state backend), valid until the next call on this operator."""
         s = L.FgStateRows()
         wm = C.c_int64()
         L.check(self._lib.fg_snapshot_state(self._h, C.byref(s), C.byref(wm)), self._h)
@@ -285,7 +287,8 @@ class WindowAggOperator:
         def col(p):
             if n == 0:
                 return np.zeros(0, dtype=np.int64)
-            return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(n,)).copy()
+            a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int64)), shape=(n,))
+            return a.copy() if copy else a
 
         img = dict(key=col(s.key), slice_end=col(s.slice_end), cnt_star=col(s.cnt_star), cnt_val=col(s.cnt_val),
                    sum=col(s.sum))
