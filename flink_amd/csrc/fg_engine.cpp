@@ -1172,6 +1172,7 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
              const int64_t* sum, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
     IngestParams p{};
     p.w = h->w;
+    p.w.local_input = h->w.tz_n > 0 ? 1 : 0;   // partial rows carry local slice ends
     p.n = n;
     p.key = key;
     p.ts = ts;
@@ -1398,10 +1399,10 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         return FG_EINVAL;
     }
     const bool windowed = (c.flags & FG_FLAG_WINDOWED) != 0;
-    if (windowed && (c.mode != FG_MODE_SQL || local || proctime || c.n_tz_transitions > 0)) {
+    if (windowed && (c.mode != FG_MODE_SQL || local || proctime)) {
         // WindowedSliceAssigner.isEventTime() is always true (SliceAssigners.java:430-434)
-        g_open_error = "FG_FLAG_WINDOWED is for SQL event-time window aggregation (not DataStream, processing time, "
-                       "the local phase or zone rules)";
+        g_open_error = "FG_FLAG_WINDOWED is for SQL event-time window aggregation (not DataStream, processing time "
+                       "or the local phase)";
         return FG_EINVAL;
     }
     if (c.n_tz_transitions < 0 || (c.n_tz_transitions > 0 && (!c.tz_transition_ms || !c.tz_offset_ms))) {
@@ -1409,8 +1410,8 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         return FG_EINVAL;
     }
     if (c.n_tz_transitions > 0) {
-        if (c.mode != FG_MODE_SQL || local) {
-            g_open_error = "zone rules (daylight saving) are for SQL window aggregation, not DataStream or the local phase";
+        if (c.mode != FG_MODE_SQL) {
+            g_open_error = "zone rules (daylight saving) are for SQL window aggregation, not DataStream";
             return FG_EINVAL;
         }
         for (int32_t i = 0; i + 1 < c.n_tz_transitions; i++)
@@ -1491,6 +1492,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         w.size = w.slide = w.slice;
         w.nslices = 1;
         w.rsize = w.rslice;
+        if (w.tz_n > 0) w.local_input = 1;   // window ends are local times (zone rules)
     }
 
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
@@ -1621,7 +1623,6 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     if (!h || !b) return FG_EINVAL;
     if (b->n <= 0) return FG_OK;
     if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
-    if (h->w.tz_n > 0) return h->fail(FG_EINVAL, "fg_add_partials with zone rules (daylight saving) is not supported");
     if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 rows");
     if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
         return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
@@ -1643,7 +1644,9 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     }
     HIPCHK(h, h->in_ts.ensure(8 * n));
     int64_t* ts = h->in_ts.as<int64_t>();
-    HIPCHK(h, launch_pseudo_rowtime(se, n, h->w.tz, ts, h->stream));
+    // fixed offset: pseudo rowtime slice_end - 1 - tz; zone rules: slice_end - 1 in local
+    // time, assigned without the zone shift (WindowSpec::local_input, set in acc_pass)
+    HIPCHK(h, launch_pseudo_rowtime(se, n, h->w.tz_n > 0 ? 0 : h->w.tz, ts, h->stream));
     h->records_in += n;
     int rc0 = seed_anchor(h, ts, nullptr);
     if (rc0) return rc0;

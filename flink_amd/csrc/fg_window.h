@@ -68,6 +68,11 @@ struct WindowSpec {
     const int64_t* tz_offs_d;
     int32_t tz_n;
     int32_t tz_dst;     // TimeZone.useDaylightTime(): the DST branches of TimeWindowUtil
+    // the rowtime column already holds local (UTC-shifted) times: partial rows and windowed
+    // rows carry their slice / window end, which the `sliced` / `windowed` assigners take as
+    // is (SliceAssigners.java:407-412, :520-524) -- set for zone rules, whose local -> epoch
+    // mapping is not invertible (a fixed offset round-trips through slice_end - 1 - tz)
+    int32_t local_input;
 };
 
 // the zone tables of the side this code runs on
@@ -155,7 +160,7 @@ __host__ __device__ __forceinline__ bool is_window_fired(const WindowSpec& w, in
 }
 // AbstractSliceAssigner.assignSliceEnd (rowtime path)
 __host__ __device__ __forceinline__ int64_t assign_slice_end(const WindowSpec& w, int64_t ts) {
-    int64_t t = to_utc(w, ts);
+    int64_t t = w.local_input ? ts : to_utc(w, ts);
     int64_t start = jsub(t, jrem_fast(jadd(jsub(t, w.offset), w.slice), w.slice, w.rslice));
     return jadd(start, w.slice);
 }

@@ -84,8 +84,11 @@ def test_zone_rules_validated_before_device():
     import flink_amd as F
     with pytest.raises(F.WindowSpecError):
         F.WindowAggOperator(F.tumbling(1000), mode="datastream", val_type="i64", zone="America/Los_Angeles")
-    with pytest.raises(F.WindowSpecError):
-        F.WindowAggOperator(F.tumbling(1000), local_partials=True, zone="America/Los_Angeles")
+    import torch
+    if not torch.cuda.is_available():   # the local phase takes zone rules: valid, no device
+        with pytest.raises(F.FlinkGpuError) as ei:
+            F.WindowAggOperator(F.tumbling(1000), local_partials=True, zone="America/Los_Angeles")
+        assert ei.value.code == L.FG_EDEVICE
 
 
 def test_min_max_accumulator_rules():

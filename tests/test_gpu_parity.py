@@ -391,6 +391,15 @@ TWO_PHASE_CASES = [
      dict(n=300_000, keys=30_000, batch=15_000, delay=50, jitter=2500)),
     ("max_zipf_tumble_f64", dict(cfg_of("tumble", 1000), aggs=MAX_AGGS),
      dict(n=6_000_000, keys=100_000, batch=3_000_000, delay=0, jitter=0, rate_per_ms=3_000, zipf=1.1)),
+    # America/Los_Angeles zone rules: partial rows carry local slice ends across the 2021
+    # gap / overlap (the `sliced` assigner takes them as is)
+    ("dst_hop_fall_i64", cfg_of("hop", 4 * 3600_000, 3600_000, vt="i64", zone=LA),
+     dict(n=300_000, keys=2000, batch=25_000, delay=300_000, jitter=2_400_000, t0=FALL, rate_per_ms=0.02)),
+    ("dst_cumulate_spring_f64", cfg_of("cumulate", 4 * 3600_000, 3600_000, zone=LA),
+     dict(n=300_000, keys=2000, batch=15_000, delay=900_000, jitter=3_000_000, t0=SPRING - 3600_000,
+          rate_per_ms=0.02)),
+    ("dst_tumble_spring_f64", cfg_of("tumble", 3600_000, zone=LA),
+     dict(n=300_000, keys=3000, batch=20_000, delay=600_000, jitter=1_800_000, t0=SPRING, rate_per_ms=0.02)),
 ]
 
 
@@ -406,15 +415,16 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     S, R, MAXP = 3, 2, 128
     n, keys, batch, delay, jitter = kw["n"], kw["keys"], kw["batch"], kw["delay"], kw["jitter"]
     key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter,
-                                  **{k: kw[k] for k in ("rate_per_ms", "zipf") if k in kw})
+                                  **{k: kw[k] for k in ("rate_per_ms", "zipf", "t0") if k in kw})
     w = window_of(cfg)
     aggs = cfg.get("aggs", ("count_star", "count", "sum", "avg", "sum0"))
     mm = tuple(a for a in aggs if a in ("min", "max"))
     vcol = mm[0] if mm else "sum"   # the partial accumulator column
+    zone = cfg.get("zone")
     local = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
-                                 local_partials=True) for _ in range(S)]
+                                 local_partials=True, zone=zone) for _ in range(S)]
     glob = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys // R + 1,
-                                buffer_records=1 << 18) for _ in range(R)]
+                                buffer_records=1 << 18, zone=zone) for _ in range(R)]
     o = oracle_mk(oracle_mod, cfg)
     src = np.arange(n) % S
 
@@ -454,17 +464,24 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     o.close()
 
 
-def windowed_rows(kind, size, slide, key, ts, val, isnull):
+def windowed_rows(kind, size, slide, key, ts, val, isnull, zone=None):
     """A window TVF's output: every record once per window containing it (record-major),
-    with the window's end as its `window_end` column (offset 0)."""
+    with the window's end as its `window_end` column (offset 0); with a zone, windows of
+    the local (UTC-shifted) time toUtcTimestampMills gives (TimeWindowUtil.java:53-61)."""
     S = size if kind == "tumble" else (np.gcd(size, slide) if kind == "hop" else slide)
-    se = (ts // S) * S + S
+    if zone:
+        from flink_amd.tz import zone_rules
+        trans, offs, _ = zone_rules(zone)
+        lt = ts + np.asarray(offs, dtype=np.int64)[np.searchsorted(np.asarray(trans, dtype=np.int64), ts, side="right")]
+    else:
+        lt = ts   # watermarks stay epoch times (the `ts` column below)
+    se = (lt // S) * S + S
     if kind == "tumble":
         ends = [se]
     elif kind == "hop":
         ends = [se + j * S for j in range(size // S)]
     else:
-        ws = (ts // size) * size
+        ws = (lt // size) * size
         ends = [np.where(se + j * S <= ws + size, se + j * S, -1) for j in range(size // S)]
     E = np.stack(ends, axis=1)
     rep = (E >= 0).sum(axis=1)
@@ -481,6 +498,14 @@ WINDOWED_CASES = [
                                                                         jitter=2500, null_frac=0.1)),
     ("windowed_hop_regions_f64", cfg_of("hop", 4000, 1000), dict(n=600_000, keys=100_000, batch=60_000, delay=200,
                                                                  jitter=800)),
+    # zone rules: local window ends across the 2021 LA gap (spring) and overlap (fall)
+    ("windowed_dst_tumble_spring_f64", cfg_of("tumble", 3600_000, zone=LA),
+     dict(n=200_000, keys=2000, batch=10_000, delay=600_000, jitter=1_800_000, t0=SPRING, rate_per_ms=0.02)),
+    ("windowed_dst_hop_fall_i64", cfg_of("hop", 4 * 3600_000, 3600_000, vt="i64", zone=LA),
+     dict(n=150_000, keys=2000, batch=12_000, delay=300_000, jitter=2_400_000, t0=FALL, rate_per_ms=0.02)),
+    ("windowed_dst_cumulate_fall_f64", cfg_of("cumulate", 3 * 3600_000, 3600_000, zone=LA),
+     dict(n=150_000, keys=2000, batch=9_000, delay=900_000, jitter=3_000_000, t0=FALL - 1800_000, rate_per_ms=0.02,
+          null_frac=0.1)),
 ]
 
 
@@ -490,8 +515,9 @@ def test_windowed_input_parity(oracle_mod, name, cfg, kw):
     late rows of fired windows dropped; window_start from the inner assigner."""
     cfg = dict(cfg, windowed=True, count_star_index=-1 if cfg["kind"] == "hop" else 0)
     key, ts, val, isnull = make_stream(kw["n"], kw["keys"], cfg["val_type"], jitter_ms=kw["jitter"],
-                                       null_frac=kw.get("null_frac", 0.0))
-    r = windowed_rows(cfg["kind"], cfg["size"], cfg["slide"], key, ts, val, isnull)
+                                       null_frac=kw.get("null_frac", 0.0),
+                                       **{k: kw[k] for k in ("rate_per_ms", "t0") if k in kw})
+    r = windowed_rows(cfg["kind"], cfg["size"], cfg["slide"], key, ts, val, isnull, zone=cfg.get("zone"))
     g = gpu_mk(cfg, expected_keys=kw["keys"], buffer_records=max(4 * kw["batch"], 1 << 16))
     o = oracle_mk(oracle_mod, cfg)
     n = len(r["key"])
