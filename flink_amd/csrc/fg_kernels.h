@@ -200,6 +200,13 @@ struct ExportParams {
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s);
 // global phase: rowtime = slice_end - 1 - tz for partial rows; scatter of accumulator rows
 hipError_t launch_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out, hipStream_t s);
+// a few words stored by a kernel (scratch counters initialised in stream order: a small
+// host-to-device copy costs a blit plus ~20 us of queue latency before the next kernel)
+struct Words16 {
+    unsigned long long v[16];
+    int32_t n;
+};
+hipError_t launch_store_words(unsigned long long* dst, const Words16& w, hipStream_t s);
 hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,
                                      int64_t* out, unsigned long long* off_grid, hipStream_t s);
 hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStream_t s);

@@ -904,6 +904,16 @@ hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz,
     return hipGetLastError();
 }
 
+__global__ void k_store_words(unsigned long long* dst, Words16 w) {
+    if ((int)threadIdx.x < w.n) dst[threadIdx.x] = w.v[threadIdx.x];
+}
+
+hipError_t launch_store_words(unsigned long long* dst, const Words16& w, hipStream_t s) {
+    if (w.n < 0 || w.n > 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_store_words, dim3(1), dim3(64), 0, s, dst, w);
+    return hipGetLastError();
+}
+
 hipError_t launch_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out, hipStream_t s) {
     int64_t blocks = (n + 255) / 256;
     blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);

@@ -140,6 +140,8 @@ class WindowAggOperator:
         h = C.c_void_p()
         L.check(lib.fg_open(C.byref(cfg), C.byref(h)), None)
         self._h = h
+        self._dev_rows = L.FgRows()   # process_watermark(device_output=True) result
+        self._dev_rows_ref = C.byref(self._dev_rows)
         self._lib = lib
 
     # -- lifecycle -------------------------------------------------------------------------
@@ -168,7 +170,10 @@ class WindowAggOperator:
             if hasattr(c, "is_cuda") and c.is_cuda:
                 import torch
                 cur = torch.cuda.current_stream(c.device)
-                torch.cuda.ExternalStream(self.stream, device=c.device).wait_stream(cur)
+                ext = self.__dict__.get("_ext_stream")
+                if ext is None or ext.device != c.device:   # made once per operator
+                    ext = self._ext_stream = torch.cuda.ExternalStream(self.stream, device=c.device)
+                ext.wait_stream(cur)
                 return
 
     def process_batch(self, key, rowtime, val=None, val_null=None):
@@ -232,12 +237,18 @@ class WindowAggOperator:
 
     # -- processWatermark ---------------------------------------------------------------------
     def process_watermark(self, watermark: int, device_output: bool = False):
-        """Advance event time; returns the rows fired by this watermark (FiredRows)."""
-        r = L.FgRows()
-        loc = L.DEVICE if device_output else L.HOST
-        L.check(self._lib.fg_advance_progress(self._h, int(watermark), loc, C.byref(r)), self._h)
+        """Advance event time; returns the rows fired by this watermark: a structured numpy
+        array, or with device_output=True the operator's FgRows (device pointers, reused and
+        valid until the next call on this operator)."""
         if device_output:
-            return r
+            # one FgRows per operator: device rows are library-owned and valid until the next
+            # call on this handle anyway; no per-call allocation on the watermark path
+            rc = self._lib.fg_advance_progress(self._h, int(watermark), L.DEVICE, self._dev_rows_ref)
+            if rc:
+                L.check(rc, self._h)
+            return self._dev_rows
+        r = L.FgRows()
+        L.check(self._lib.fg_advance_progress(self._h, int(watermark), L.HOST, C.byref(r)), self._h)
         return self._host_rows(r)
 
     def _host_rows(self, r: L.FgRows) -> np.ndarray:
