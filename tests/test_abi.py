@@ -109,3 +109,17 @@ def test_min_max_accumulator_rules():
         with pytest.raises(F.FlinkGpuError) as ei:
             F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="i64")
         assert ei.value.code == L.FG_EDEVICE
+
+
+def test_accumulator_groups_split():
+    """A query with several value accumulators maps to one handle per kind, each with
+    COUNT(*) (flink_amd/composite.py)."""
+    from flink_amd import _lib as L
+    from flink_amd.composite import accumulator_groups
+    codes, groups = accumulator_groups(("count_star", "sum", "avg", "min", "max"))
+    assert groups == [(L.AGG_COUNT_STAR, L.AGG_SUM, L.AGG_AVG), (L.AGG_COUNT_STAR, L.AGG_MIN),
+                      (L.AGG_COUNT_STAR, L.AGG_MAX)]
+    _, groups = accumulator_groups(("count", "max"))
+    assert groups == [(L.AGG_COUNT_STAR, L.AGG_COUNT, L.AGG_MAX)]
+    _, groups = accumulator_groups(("sum",))
+    assert groups == [(L.AGG_COUNT_STAR, L.AGG_SUM)]

@@ -548,3 +548,51 @@ def test_windowed_input_off_grid_is_loud():
         op.process_batch(np.arange(4, dtype=np.int64), np.array([1000, 2000, 2500, 3000], dtype=np.int64),
                          np.ones(4))
     op.close()
+
+
+@pytest.mark.parametrize("kind,vt,device_output", [("tumble", "f64", False), ("hop", "i64", False),
+                                                   ("cumulate", "f64", True)])
+def test_composite_sum_min_max(oracle_mod, kind, vt, device_output):
+    """COUNT(*), COUNT, SUM, AVG, MIN, MAX of one column: one handle per accumulator kind,
+    rows joined on (window_end, key) (flink_amd/composite.py) vs the oracle's one row."""
+    import flink_amd as F
+    from tests.gpu_adapter import window_of
+    cfg = cfg_of(kind, 4000, 0 if kind == "tumble" else 1000, vt=vt)
+    key, ts, val, isnull = make_stream(150_000, 3000, vt, jitter_ms=900, null_frac=0.1)
+    aggs = ("count_star", "count", "sum", "avg", "min", "max")
+    op = F.window_agg_operator(window_of(cfg), aggs=aggs, val_type=vt, expected_keys=3000)
+    assert isinstance(op, F.CompositeWindowAggOperator) and len(op.ops) == 3
+    o = oracle_mk(oracle_mod, cfg)
+    sfx = "_i" if vt == "i64" else "_d"
+
+    def check(got, exp, ctx):
+        if device_output:
+            got = {k: v.cpu().numpy() for k, v in got.items()}
+        e = sort_rows(exp)
+        assert len(got["key"]) == len(e), ctx
+        for f, ef in (("key", "key"), ("window_start", "window_start"), ("window_end", "window_end"),
+                      ("count_star", "cnt_star"), ("count", "cnt_val")):
+            assert np.array_equal(got[f], e[ef]), (ctx, f)
+        ok = e["sum_null"] == 0
+        assert np.array_equal(got["sum_null"], ~ok) and np.array_equal(got["min_null"], ~ok), ctx
+        for f in ("min", "max"):
+            assert np.array_equal(got[f][ok], e[f + sfx][ok]), (ctx, f)
+        for f in ("sum", "avg"):
+            a, b = got[f][ok], e[f + sfx][ok]
+            if vt == "i64":
+                assert np.array_equal(a, b), (ctx, f)
+            else:
+                assert (np.abs(a - b) <= REL_TOL * np.maximum(np.abs(a), np.abs(b)) + 1e-300).all(), (ctx, f)
+
+    for step, (lo, hi, wm) in enumerate(batches_with_watermarks(len(key), 9_000, ts, 300)):
+        op.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], isnull[lo:hi])
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], isnull[lo:hi])
+        got = op.process_watermark(wm, device_output=device_output)
+        o.process_watermark(wm)
+        check(got, o.take_rows(), f"step {step}")
+    got = op.process_watermark(JMAX, device_output=device_output)
+    o.process_watermark(JMAX)
+    check(got, o.take_rows(), "final")
+    assert op.num_late_records_dropped == o.late_dropped
+    op.close()
+    o.close()
