@@ -77,6 +77,12 @@ WORKLOADS = {
                      jitter=0, delay=0, zipf=0.0, batch=12_500_000,
                      desc="SQL CUMULATE 1h/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 60 event-minutes, "
                           "uniform keys: 12.5M per GPU = the per-GPU key-group share of 100M (BASELINE configs[3])"),
+    # configs[0]: DataStream keyBy().window(TumblingEventTimeWindows 1s).sum on (long key,
+    # long val), 10M records, 10k keys, 1M records per event-second, watermark every 10k
+    "datastream": dict(window=("tumbling", 1000), keys=10_000, rate=1_000_000, jitter=0, delay=0, zipf=0.0,
+                       batch=1_000_000, records=10_000_000, wm_every=10_000, mode="datastream",
+                       desc="DataStream keyBy().window(TumblingEventTimeWindows 1s).sum (WindowOperator), "
+                            "10M (long, long) records, 10k keys (BASELINE configs[0])"),
     # configs[4]: TUMBLE 1s AVG(double), Zipf s = 1.1 keys, 2 s jitter, bounded out-of-orderness 2 s
     "zipf": dict(window=("tumbling", 1000), keys=10_000_000, rate=100_000_000, jitter=2000, delay=2000, zipf=1.1,
                  desc="SQL TUMBLE 1s AVG(double), 1B records per GPU, 10M Zipf(1.1) keys, rowtime jitter U[0,2s), "
@@ -199,7 +205,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--records", type=int, default=1_000_000_000, help="records per GPU per step")
+    ap.add_argument("--records", type=int, default=None, help="records per GPU per step (default: 1B; "
+                    "configs[0]: 10M)")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="tumble",
                     help="BASELINE config; `tumble` (configs[1]) is the bench's headline value")
     ap.add_argument("--keys", type=int, default=None, help="key space (default: the workload's)")
@@ -207,7 +214,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None,
                     help="micro-batch records (default 50M; hop 25M and cumulate 12.5M so that a micro-batch "
                          "spans at most two 1-minute slices, the staged lanes of a 10M-key operator)")
-    ap.add_argument("--wm-every", type=int, default=1_000_000)
+    ap.add_argument("--wm-every", type=int, default=None, help="records between watermarks (default 1M; "
+                    "configs[0]: 10k)")
     ap.add_argument("--checkpoint-every", type=int, default=None,
                     help="micro-batches between checkpoints (prepareSnapshotPreBarrier flush + state image to "
                          "host); default: the zipf workload (configs[4]) checkpoints once per step, others never")
@@ -226,6 +234,11 @@ def main():
         args.rate = wl["rate"]
     if args.batch is None:
         args.batch = wl.get("batch", 50_000_000)
+    if args.records is None:
+        args.records = wl.get("records", 1_000_000_000)
+    if args.wm_every is None:
+        args.wm_every = wl.get("wm_every", 1_000_000)
+    datastream = wl.get("mode") == "datastream"
     if args.workload != "tumble":
         args.no_cpu_baseline = True   # the CPU baseline is quoted on configs[1]
     if args.checkpoint_every is None:
@@ -257,17 +270,20 @@ def main():
 
     n = args.records
     key, ts, val = gen_columns(n, args.keys, args.rate, rank * n, dev, jitter=wl["jitter"], zipf=wl["zipf"])
+    if datastream:   # Tuple2<Long, Long>: long values in [0, 1000)
+        val = val.to(torch.int64)
     torch.cuda.synchronize()
     if args.host_input:   # FG_HOST columns: the engine copies each micro-batch H2D on its stream
         key, ts, val = (x.cpu().pin_memory() for x in (key, ts, val))
 
     maxp = 128
     kg_lo, kg_hi = (rank * maxp + world - 1) // world, ((rank + 1) * maxp - 1) // world
-    two_phase = world > 1 and args.exchange == "partials"
+    two_phase = world > 1 and args.exchange == "partials" and not datastream
     wname, *wargs = wl["window"]
     window = getattr(F, wname)(*wargs)
-    aggs = ("avg",) if args.workload == "zipf" else ("count_star", "sum", "avg")
-    op = F.WindowAggOperator(window, aggs=aggs, val_type="f64",
+    aggs = ("avg",) if args.workload == "zipf" else ("sum",) if datastream else ("count_star", "sum", "avg")
+    op = F.WindowAggOperator(window, aggs=aggs, val_type="i64" if datastream else "f64",
+                             mode="datastream" if datastream else "sql",
                              expected_keys=int(args.keys / world * 1.05) + 1,
                              buffer_records=max(4 * args.batch, 1 << 26) if not two_phase else 1 << 24,
                              device=local, key_group_range=(kg_lo, kg_hi), kernel_timing=True)
@@ -321,8 +337,8 @@ def main():
                     xgmi += sent
                 continue
             if world > 1:
-                k, t, v, sent = exchange(k, t, v.view(torch.int64), max_parallelism=maxp)
-                v = v.view(torch.float64)
+                k, t, v2, sent = exchange(k, t, v.view(torch.int64), max_parallelism=maxp)
+                v = v2.view(v.dtype)
                 xgmi += sent
                 torch.cuda.current_stream().synchronize()
             op.process_batch(k, t, v)
@@ -409,7 +425,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "int64" if datastream else "f64",
         "data": "synthetic (counter-based splitmix64 stream generated on the GPU, " + (
             "handed over as pinned host columns: PCIe-inclusive)" if args.host_input else "resident in HBM)"),
         "config": {
