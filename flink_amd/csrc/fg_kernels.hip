@@ -1069,7 +1069,7 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
 //
 // staged-stream chunk of the compact merge: 16-B loads per thread (overridable for experiments)
 #ifndef FG_MERGE_U
-#define FG_MERGE_U 3
+#define FG_MERGE_U 2
 #endif
 #ifndef FG_DIAG_MERGE
 #define FG_DIAG_MERGE 0    // diagnostic builds only (wrong results): bit0 no adds, bit1 no probe loop, bit2 no emit
