@@ -1071,6 +1071,9 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
 #ifndef FG_MERGE_U
 #define FG_MERGE_U 2
 #endif
+#ifndef FG_WIDE_U
+#define FG_WIDE_U 2        // the wide merge's staged records per thread per chunk
+#endif
 #ifndef FG_DIAG_MERGE
 #define FG_DIAG_MERGE 0    // diagnostic builds only (wrong results): bit0 no adds, bit1 no probe loop, bit2 no emit
 #endif
@@ -1081,7 +1084,7 @@ template <>
 struct MergeCfg<false> {
     static constexpr int kSlotsT = kSlots;
     static constexpr int kThreads = kMergeThreads;
-    static constexpr int kU = 2;      // 1,024 threads: 128 VGPRs
+    static constexpr int kU = FG_WIDE_U;   // 1,024 threads: 128 VGPRs
 };
 template <>
 struct MergeCfg<true> {
