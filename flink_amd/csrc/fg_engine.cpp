@@ -21,7 +21,6 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
-#include <chrono>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -158,7 +157,6 @@ struct PendingEv {
 }  // namespace
 
 struct fg_handle {
-    hipEvent_t sync_ev = nullptr;   // spin-wait event of sync()
     int32_t kvt = 0;   // kernel value op (val_type | op << 2)
     fg_config cfg{};
     WindowSpec w{};
@@ -323,22 +321,8 @@ hipError_t init_counters(fg_handle* h, const DevCounters& init) {
     return launch_store_words(h->counters.as<unsigned long long>(), w, h->stream);
 }
 
-// Wait for the stream: spin on an event for a short while (the common wait is one pass of
-// a micro-batch, ~0.1-0.5 ms; a blocking wait adds ~20-30 us of wake-up latency while the
-// GPU idles), then block.
 int sync(fg_handle* h, bool drain_timing = false) {
-    if (!h->sync_ev) HIPCHK(h, hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming));
-    HIPCHK(h, hipEventRecord(h->sync_ev, h->stream));
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-        const hipError_t q = hipEventQuery(h->sync_ev);
-        if (q == hipSuccess) break;
-        if (q != hipErrorNotReady) HIPCHK(h, q);
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
-            HIPCHK(h, hipStreamSynchronize(h->stream));
-            break;
-        }
-    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     h->arena_used = 0;
     // kernel-timing events are read off the critical path (they are complete here); only a
     // long backlog, and fg_kernel_stats / fg_synchronize, drain them
@@ -2031,7 +2015,6 @@ void fg_close(fg_handle* h) {
         h->ev_pool.push_back(p.b);
     }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-    if (h->sync_ev) (void)hipEventDestroy(h->sync_ev);
     hipStream_t s = h->stream;
     delete h;
     if (s) (void)hipStreamDestroy(s);
