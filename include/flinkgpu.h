@@ -109,8 +109,9 @@ enum fg_flags {
      * expired alone, a late row is dropped once its window fired); window_start =
      * the kind's getWindowStart(window_end). The window kind/size/slide/offset describe the
      * inner assigner. window_end values must lie on the inner assigner's slice grid (as a
-     * window TVF emits them), else fg_add_batch fails with FG_EINVAL. SQL event time only;
-     * not with zone rules or the two-phase operators. */
+     * window TVF emits them), else fg_add_batch fails with FG_EINVAL. SQL event time only,
+     * not the local phase. With zone rules the window_end values are local (UTC-shifted)
+     * times and are taken as is. */
     FG_FLAG_WINDOWED = 8
 };
 
