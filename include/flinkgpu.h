@@ -137,8 +137,8 @@ typedef struct fg_config {
     /* Shift time zone with transitions (daylight saving): the ZoneRules of the ZoneId as data
      * (ZoneRules.getTransitions() on the Java side). n_tz_transitions > 0 replaces
      * shift_tz_offset_ms: toUtcTimestampMills / toEpochMillsForTimer / getNextTriggerWatermark
-     * follow TimeWindowUtil.java:53-61,70-140,187-210 with these rules. SQL mode only, and not
-     * for the two-phase operators (FG_FLAG_LOCAL_PARTIALS, fg_add_partials). Copied at fg_open. */
+     * follow TimeWindowUtil.java:53-61,70-140,187-210 with these rules. SQL mode only (incl. the
+     * two-phase operators, whose partial rows carry local slice ends). Copied at fg_open. */
     const int64_t* tz_transition_ms;   /* n_tz_transitions instants, epoch ms, ascending */
     const int64_t* tz_offset_ms;       /* n_tz_transitions + 1 offsets (ms): [i] in force before transition i */
     int32_t n_tz_transitions;
