@@ -219,6 +219,8 @@ def main():
     ap.add_argument("--checkpoint-every", type=int, default=None,
                     help="micro-batches between checkpoints (prepareSnapshotPreBarrier flush + state image to "
                          "host); default: the zipf workload (configs[4]) checkpoints once per step, others never")
+    ap.add_argument("--aggs", default=None, help="comma-separated aggregate list (default: the workload's), "
+                    "e.g. count_star,min")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
@@ -282,6 +284,8 @@ def main():
     wname, *wargs = wl["window"]
     window = getattr(F, wname)(*wargs)
     aggs = ("avg",) if args.workload == "zipf" else ("sum",) if datastream else ("count_star", "sum", "avg")
+    if args.aggs:
+        aggs = tuple(args.aggs.split(","))
     op = F.WindowAggOperator(window, aggs=aggs, val_type="i64" if datastream else "f64",
                              mode="datastream" if datastream else "sql",
                              expected_keys=int(args.keys / world * 1.05) + 1,
