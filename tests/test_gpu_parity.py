@@ -596,3 +596,29 @@ def test_composite_sum_min_max(oracle_mod, kind, vt, device_output):
     assert op.num_late_records_dropped == o.late_dropped
     op.close()
     o.close()
+
+
+def test_batch_limits_are_loud_and_recoverable(oracle_mod):
+    """fg_add_batch rejects a batch over 2^31-1 records and missing columns with FG_EINVAL
+    before touching any buffer; the operator keeps working afterwards."""
+    import ctypes as C
+    import flink_amd as F
+    from flink_amd import _lib as L
+    op = F.WindowAggOperator(F.tumbling(1000), aggs=("count_star", "sum"), val_type="i64", expected_keys=100)
+    lib = L.load()
+    b = L.FgBatch()
+    b.location = L.DEVICE
+    b.n = 1 << 31
+    b.key, b.rowtime, b.val = 8, 8, 8    # never dereferenced: the size check comes first
+    assert lib.fg_add_batch(op._h, C.byref(b)) == L.FG_EINVAL
+    assert b"2^31" in lib.fg_last_error(op._h)
+    b.n = 10
+    b.key = 0
+    assert lib.fg_add_batch(op._h, C.byref(b)) == L.FG_EINVAL
+    key = np.arange(10, dtype=np.int64) % 3
+    ts = np.full(10, 1_000_500, dtype=np.int64)
+    op.process_batch(key, ts, np.arange(10, dtype=np.int64))
+    r = op.process_watermark(JMAX)
+    r = r[np.argsort(r["key"])]
+    assert list(r["count_star"]) == [4, 3, 3] and list(r["sum"]) == [18, 12, 15]
+    op.close()
