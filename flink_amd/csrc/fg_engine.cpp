@@ -1514,7 +1514,9 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     }
 
     // regions: average occupancy <= ~70 % of the per-region HBM capacity
-    int64_t keys = std::max<int64_t>(cfg->expected_keys, 1);
+    // expected_keys <= 0: unknown (a shim without a key-count hint) -> the largest table
+    // (2^13 regions, ~29M entries per slice); a hint sizes it down for speed
+    int64_t keys = cfg->expected_keys > 0 ? cfg->expected_keys : INT64_MAX;
     int bits = 0;
     // Keys per region ~35 % of the kSlots LDS slots: linear probes stay short (a wave's
     // probe loop runs at its lanes' probe counts); up to 2^13 regions, then denser.

@@ -132,7 +132,8 @@ typedef struct fg_config {
     int32_t key_group_end;
     int32_t device_id;            /* HIP device ordinal */
     int32_t flags;                /* FG_FLAG_* */
-    int64_t expected_keys;        /* distinct keys per slice on this subtask (sizes HBM regions) */
+    int64_t expected_keys;        /* distinct keys per slice on this subtask (sizes HBM regions);
+                                   * <= 0: unknown, the largest table (~29M entries per slice) */
     int64_t buffer_records;       /* staged records before an implicit flush (managed-memory analogue) */
     /* Shift time zone with transitions (daylight saving): the ZoneRules of the ZoneId as data
      * (ZoneRules.getTransitions() on the Java side). n_tz_transitions > 0 replaces

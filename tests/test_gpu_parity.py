@@ -77,7 +77,7 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
                expected_keys=None, kstats=None, **gen):
     key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
     mm = tuple(a for a in cfg.get("aggs", ()) if a in ("min", "max"))
-    g = gpu_mk(cfg, expected_keys=expected_keys or keys, buffer_records=max(batch * 4, 1 << 16),
+    g = gpu_mk(cfg, expected_keys=keys if expected_keys is None else expected_keys, buffer_records=max(batch * 4, 1 << 16),
                kernel_timing=kstats is not None)
     o = oracle_mk(O, cfg)
     o_base = 0
@@ -622,3 +622,10 @@ def test_batch_limits_are_loud_and_recoverable(oracle_mod):
     r = r[np.argsort(r["key"])]
     assert list(r["count_star"]) == [4, 3, 3] and list(r["sum"]) == [18, 12, 15]
     op.close()
+
+
+def test_unknown_key_count_takes_the_largest_table(oracle_mod):
+    """expected_keys = 0 (no key-count hint from the shim): sized for the maximum, so 200k
+    keys fit where a one-region table (3,584 entries) would overflow loudly."""
+    cfg = cfg_of("tumble", 1000)
+    drive_both(oracle_mod, cfg, n=400_000, keys=200_000, batch=100_000, delay=0, jitter=0, expected_keys=0)
