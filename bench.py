@@ -292,7 +292,7 @@ def main():
                              buffer_records=max(4 * args.batch, 1 << 26) if not two_phase else 1 << 24,
                              device=local, key_group_range=(kg_lo, kg_hi), kernel_timing=True)
     # two-phase: the local operator sees every key of its source partition
-    op_local = F.WindowAggOperator(window, val_type="f64", expected_keys=int(args.keys * 1.05) + 1,
+    op_local = F.WindowAggOperator(window, aggs=aggs, val_type="f64", expected_keys=int(args.keys * 1.05) + 1,
                                    buffer_records=max(4 * args.batch, 1 << 26), device=local,
                                    kernel_timing=True, local_partials=True) if two_phase else None
 
