@@ -90,6 +90,15 @@ WORKLOADS = {
 }
 
 
+def zipf_distinct_per_slice(keys, s, records):
+    """Expected distinct keys among `records` Zipf(s) draws over `keys` ranks:
+    sum_k 1 - (1 - p_k)^records -- the operator's sizing hint (fg_config.expected_keys is
+    the distinct keys per slice; the key space over-sizes the tables for skewed keys)."""
+    p = np.arange(1, keys + 1, dtype=np.float64) ** -s
+    p /= p.sum()
+    return float(np.sum(-np.expm1(records * np.log1p(-p))))
+
+
 def zipf_cdf(keys, s, device):
     """CDF of Zipf(s) over ranks 1..keys (float64), summed sequentially on the host so that
     the generated keys are the same in every run (a device cumsum's order is not fixed)."""
@@ -221,6 +230,8 @@ def main():
                          "host); default: the zipf workload (configs[4]) checkpoints once per step, others never")
     ap.add_argument("--aggs", default=None, help="comma-separated aggregate list (default: the workload's), "
                     "e.g. count_star,min")
+    ap.add_argument("--expected-keys", type=int, default=None,
+                    help="operator sizing hint: distinct keys per slice (default: the key space x 1.05)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
@@ -283,12 +294,15 @@ def main():
     two_phase = world > 1 and args.exchange == "partials" and not datastream
     wname, *wargs = wl["window"]
     window = getattr(F, wname)(*wargs)
+    expected_keys = args.expected_keys or int(args.keys / world * 1.05) + 1
+    if not args.expected_keys and wl["zipf"] > 0:   # distinct keys in one slice's records, +10 %
+        expected_keys = int(1.1 * zipf_distinct_per_slice(args.keys, wl["zipf"], args.rate) / world) + 1
     aggs = ("avg",) if args.workload == "zipf" else ("sum",) if datastream else ("count_star", "sum", "avg")
     if args.aggs:
         aggs = tuple(args.aggs.split(","))
     op = F.WindowAggOperator(window, aggs=aggs, val_type="i64" if datastream else "f64",
                              mode="datastream" if datastream else "sql",
-                             expected_keys=int(args.keys / world * 1.05) + 1,
+                             expected_keys=expected_keys,
                              buffer_records=max(4 * args.batch, 1 << 26) if not two_phase else 1 << 24,
                              device=local, key_group_range=(kg_lo, kg_hi), kernel_timing=True)
     # two-phase: the local operator sees every key of its source partition
@@ -435,7 +449,7 @@ def main():
         "config": {
             "workload": wl["desc"],
             "records_per_gpu": n, "keys": args.keys, "records_per_event_second": args.rate,
-            "micro_batch": args.batch, "watermark_every": args.wm_every,
+            "micro_batch": args.batch, "watermark_every": args.wm_every, "expected_keys": expected_keys,
             "parallelism": f"key-group sharded x{world}" + (
                 (" + RCCL all-to-all of partial accumulators (two-phase)" if two_phase else
                  " + RCCL all-to-all of records") if world > 1 else ""),
