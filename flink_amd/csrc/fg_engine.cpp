@@ -119,6 +119,7 @@ struct DevCounters {     // device scratch words read back after the count pass
     unsigned long long drops;
     unsigned long long lane_mask;
     long long qmin, qmax;
+    long long qnext;       // smallest occupied slice index >= the pass's filter (JMAX: none)
     unsigned long long lane_total[kMaxLanes];
     unsigned int max_bucket;   // largest per-workgroup bucket count (skew hint)
     unsigned int pad;
@@ -126,6 +127,7 @@ struct DevCounters {     // device scratch words read back after the count pass
 struct Counters {        // host view: per-lane slice index ranges (min > max: lane idle)
     unsigned long long drops;
     long long qmin, qmax;
+    long long qnext;       // smallest occupied slice index >= the pass's filter_hi (JMAX: none)
     long long lane_min[kMaxLanes];
     long long lane_max[kMaxLanes];
     long long lane_total[kMaxLanes];
@@ -1013,12 +1015,14 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     DevCounters init{};
     init.qmin = JMAX;
     init.qmax = JMIN;
+    init.qnext = JMAX;
     HIPCHK(h, init_counters(h, init));
     DevCounters* dc = h->counters.as<DevCounters>();
     p.drops = &dc->drops;
     p.lane_mask = &dc->lane_mask;
     p.qmin = &dc->qmin;
     p.qmax = &dc->qmax;
+    p.qnext = &dc->qnext;
     p.lane_total = dc->lane_total;
     p.max_bucket = &dc->max_bucket;
     if (two_pass) {
@@ -1060,6 +1064,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     out->drops = got.drops;
     out->qmin = got.qmin;
     out->qmax = got.qmax;
+    out->qnext = got.qnext;
     out->skew = (int64_t)got.max_bucket * p.grid > kHeavyMin;
     for (int l = 0; l < kMaxLanes; l++) {
         out->lane_min[l] = JMAX;
@@ -1201,12 +1206,14 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     DevCounters init{};
     init.qmin = JMAX;
     init.qmax = JMIN;
+    init.qnext = JMAX;
     HIPCHK(h, init_counters(h, init));
     DevCounters* dc = h->counters.as<DevCounters>();
     p.drops = &dc->drops;
     p.lane_mask = &dc->lane_mask;
     p.qmin = &dc->qmin;
     p.qmax = &dc->qmax;
+    p.qnext = &dc->qnext;
     p.lane_total = dc->lane_total;
     {
         KTimer kt(h, K_COUNT, n);
@@ -1220,6 +1227,7 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     out->drops = got.drops;
     out->qmin = got.qmin;
     out->qmax = got.qmax;
+    out->qnext = got.qnext;
     for (int l = 0; l < kMaxLanes; l++) {
         out->lane_min[l] = JMAX;
         out->lane_max[l] = JMIN;
@@ -1394,10 +1402,23 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             g_open_error = "FG_FLAG_LOCAL_PARTIALS needs an SQL operator with a value column";
             return FG_EINVAL;
         }
-        // a MIN / MAX in the global operator's list makes the partial accumulator a MIN / MAX
+        // a MIN / MAX in the global operator's list makes the partial accumulator a MIN / MAX;
+        // the partial row holds ONE value accumulator, so the list may name one kind only
         int32_t vagg = FG_AGG_SUM;
-        for (int a = 0; a < c.num_aggs && a < FG_MAX_AGGS; a++)
+        bool sum_family = false, has_min = false, has_max = false;
+        for (int a = 0; a < c.num_aggs && a < FG_MAX_AGGS; a++) {
             if (c.aggs[a] == FG_AGG_MIN || c.aggs[a] == FG_AGG_MAX) vagg = c.aggs[a];
+            has_min |= c.aggs[a] == FG_AGG_MIN;
+            has_max |= c.aggs[a] == FG_AGG_MAX;
+            sum_family |= c.aggs[a] == FG_AGG_SUM || c.aggs[a] == FG_AGG_AVG || c.aggs[a] == FG_AGG_SUM0;
+        }
+        if ((int)sum_family + (int)has_min + (int)has_max > 1) {
+            g_open_error = std::string("FG_FLAG_LOCAL_PARTIALS: the partial row holds one value accumulator, but the "
+                                       "aggregate list names ") +
+                           (sum_family ? "SUM/AVG/SUM0 " : "") + (has_min ? "MIN " : "") + (has_max ? "MAX " : "") +
+                           "(open one local operator per accumulator kind)";
+            return FG_EINVAL;
+        }
         c.num_aggs = 3;
         c.aggs[0] = FG_AGG_COUNT_STAR;
         c.aggs[1] = FG_AGG_COUNT;
@@ -1626,14 +1647,19 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
         rest.push_back({c.qmin, c.qmax + 1});
     } else {
         if (c.qmin < flo) rest.push_back({c.qmin, flo});
-        if (c.qmax >= fhi) rest.push_back({fhi, c.qmax + 1});
+        if (c.qmax >= fhi) rest.push_back({c.qnext, c.qmax + 1});   // qnext: first occupied slice >= fhi
     }
+    // Each filtered pass reports the next occupied slice above its filter, so empty
+    // stretches (a far-future or ancient outlier record) cost no passes.
     for (auto& r : rest) {
-        for (int64_t lo = r.first; lo < r.second; lo += h->lanes) {
+        int64_t lo = r.first;
+        while (lo < r.second) {
             Counters c2{};
-            rc = ingest_pass(h, n, key, ts, val, vnull, lo, std::min<int64_t>(lo + h->lanes, r.second), false, &c2);
+            const int64_t hi = std::min<int64_t>(lo + h->lanes, r.second);
+            rc = ingest_pass(h, n, key, ts, val, vnull, lo, hi, false, &c2);
             if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
             if (rc) return rc;
+            lo = c2.qnext;   // JMAX when nothing lies above hi
         }
     }
     return FG_OK;
@@ -1678,12 +1704,14 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     const int64_t qlo = c.qmin, qhi = c.qmax;
     rc = flush(h);
     if (rc) return rc;
-    for (int64_t lo = qlo; lo <= qhi; lo += h->lanes) {
+    // filtered passes over the occupied slices only (each pass reports the next one)
+    for (int64_t lo = qlo; lo <= qhi;) {
         Counters c2{};
         rc = acc_pass(h, n, key, ts, cs, cv, sum, lo, lo + h->lanes, false, &c2);
         if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
         if (rc) return rc;
-        if (lo + h->lanes <= qhi) {
+        lo = c2.qnext;
+        if (lo <= qhi) {
             rc = flush(h);
             if (rc) return rc;
         }

@@ -84,6 +84,7 @@ struct IngestParams {
     unsigned long long* drops;
     long long* qmin;           // min / max slice index of the accepted records
     long long* qmax;
+    long long* qnext;          // min slice index >= filter_hi of the accepted records (JMAX: none)
     unsigned long long* lane_mask;    // bit l: some record has slice index == l (mod lanes)
     unsigned long long* lane_total;   // [kMaxLanes] accepted records per lane
     unsigned int* max_bucket;  // max over workgroups and buckets of a workgroup's bucket count (skew hint)

@@ -118,20 +118,20 @@ constexpr int kMaxBuckets = kMaxStageBuckets;
 __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p) {
     __shared__ uint32_t s_hist[kMaxBuckets];
     __shared__ unsigned long long s_drop;
-    __shared__ long long s_qmin, s_qmax;
+    __shared__ long long s_qmin, s_qmax, s_qnext;
     __shared__ uint32_t s_mask;
     __shared__ uint32_t s_lane[kMaxLanes];
     const int F = p.lanes << p.region_bits;
     const int tid = threadIdx.x;
     for (int i = tid; i < F; i += kIngestThreads) s_hist[i] = 0;
-    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_mask = 0; }
+    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; }
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
 
     int64_t beg, end;
     seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
     uint32_t drops = 0, mask = 0;
-    long long qmin = JMAX, qmax = JMIN;
+    long long qmin = JMAX, qmax = JMIN, qnext = JMAX;
     const int lm = p.lanes - 1;
 
     // pairs of records per thread: 16-byte loads of key and rowtime, 4 pairs in flight
@@ -149,6 +149,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
         } else {   // outside the slice filter: in the batch's slice range only
             qmin = q < qmin ? q : qmin;
             qmax = q > qmax ? q : qmax;
+            if (q >= p.filter_hi) qnext = q < qnext ? q : qnext;   // next occupied slice above the filter
         }
     };
     constexpr int kU = 4;
@@ -180,15 +181,17 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
     for (int off = 32; off > 0; off >>= 1) {
         drops += __shfl_down(drops, off);
         mask |= __shfl_down(mask, off);
-        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off);
+        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off), on = __shfl_down(qnext, off);
         qmin = oa < qmin ? oa : qmin;
         qmax = oz > qmax ? oz : qmax;
+        qnext = on < qnext ? on : qnext;
     }
     if ((tid & 63) == 0) {
         if (drops) atomicAdd(&s_drop, (unsigned long long)drops);
         if (mask) atomicOr(&s_mask, mask);
         if (qmin != JMAX) atomicMin(&s_qmin, qmin);
         if (qmax != JMIN) atomicMax(&s_qmax, qmax);
+        if (qnext != JMAX) atomicMin(&s_qnext, qnext);
     }
     __syncthreads();
     // workgroup-major histogram: hist[g * F + b] (contiguous stores) + per-lane totals
@@ -219,6 +222,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_count(IngestParams p)
         if (s_mask) atomicOr(p.lane_mask, (unsigned long long)s_mask);
         if (s_qmin != JMAX) atomicMin(p.qmin, s_qmin);
         if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
+        if (s_qnext != JMAX) atomicMin(p.qnext, s_qnext);
     }
 }
 
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     __shared__ uint32_t s_cc[kMaxCoarse + 1];        // tile coarse counts, then offsets
     __shared__ uint32_t s_wave[kPart1Threads / 64];
     __shared__ unsigned long long s_drop;
-    __shared__ long long s_qmin, s_qmax;
+    __shared__ long long s_qmin, s_qmax, s_qnext;
     __shared__ uint32_t s_mask;
     __shared__ uint32_t s_lane[kMaxLanes];
     const int F = p.lanes << p.region_bits;
@@ -454,7 +458,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     const int tid = threadIdx.x;
     for (int i = tid; i < F; i += kPart1Threads) s_hist[i] = 0;
     for (int i = tid; i <= NC; i += kPart1Threads) s_cc[i] = 0;
-    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_mask = 0; }
+    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; }
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
     int64_t beg, end;
@@ -462,7 +466,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     const bool has_val = p.val != nullptr;
     const bool has_null = p.vnull != nullptr;
     uint32_t drops = 0, mask = 0;
-    long long qmin = JMAX, qmax = JMIN;
+    long long qmin = JMAX, qmax = JMIN, qnext = JMAX;
     const int lm = p.lanes - 1;
     constexpr int R = kPart1Tile / kPart1Threads;   // 8
 
@@ -487,6 +491,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
             } else {   // outside the slice filter: in the batch's slice range only
                 qmin = q < qmin ? q : qmin;
                 qmax = q > qmax ? q : qmax;
+                if (q >= p.filter_hi) qnext = q < qnext ? q : qnext;   // next occupied slice above the filter
             }
             return 0xffffffffu;
         };
@@ -574,15 +579,17 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     for (int off = 32; off > 0; off >>= 1) {
         drops += __shfl_down(drops, off);
         mask |= __shfl_down(mask, off);
-        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off);
+        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off), on = __shfl_down(qnext, off);
         qmin = oa < qmin ? oa : qmin;
         qmax = oz > qmax ? oz : qmax;
+        qnext = on < qnext ? on : qnext;
     }
     if ((tid & 63) == 0) {
         if (drops) atomicAdd(&s_drop, (unsigned long long)drops);
         if (mask) atomicOr(&s_mask, mask);
         if (qmin != JMAX) atomicMin(&s_qmin, qmin);
         if (qmax != JMIN) atomicMax(&s_qmax, qmax);
+        if (qnext != JMAX) atomicMin(&s_qnext, qnext);
     }
     __syncthreads();
     uint32_t lane_part = 0, bmax = 0;
@@ -612,6 +619,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
         if (s_mask) atomicOr(p.lane_mask, (unsigned long long)s_mask);
         if (s_qmin != JMAX) atomicMin(p.qmin, s_qmin);
         if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
+        if (s_qnext != JMAX) atomicMin(p.qnext, s_qnext);
     }
 }
 

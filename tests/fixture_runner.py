@@ -49,6 +49,11 @@ def project(rows: np.ndarray, columns, val_type: str):
                 t.append(int(r["cnt_star"]))
             elif c == "val_all_null":
                 t.append(1 if int(r["cnt_val"]) == 0 else 0)
+            elif c in ("min", "max"):   # MIN / MAX accumulator: NULL iff no non-null value
+                if int(r["cnt_val"]) == 0:
+                    t.append(None)
+                else:
+                    t.append(int(r[c + "_i"]) if val_type == "i64" else float(r[c + "_d"]))
             else:
                 t.append(int(r[c]))
         out.append(tuple(t))

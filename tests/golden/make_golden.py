@@ -367,6 +367,76 @@ def itcase_fixtures():
 
 
 # ----------------------------------------------------------------------------------------
+# The same three ITCase queries assert MAX(`double`) and MIN(`float`) per (name, window)
+# (WindowAggregateITCase.scala:176-207 tumble, :394-430 hop, :519-562 cumulate; the data's
+# `double` and `float` columns, TestData.scala:601-615, hold different NULLs: the 00:00:08
+# row has no `double`, the late 00:00:04 row no `float`). MIN / MAX keep one value column
+# per operator here, so each aggregate is a fixture of its own over its column; float
+# values are exact in f64. The expected rows are the asserted strings
+# "name,window_start,window_end,COUNT(*),SUM(bigdec),MAX(double),MIN(float),..." with
+# name a -> 1, b -> 2, null -> 3.
+# ----------------------------------------------------------------------------------------
+ITCASE_FLOAT = [1.0, 2.0, 2.0, 5.0, 3.0, 6.0, 3.0, None, 4.0, 7.0, 3.0]   # the `float` column, row order
+
+ITCASE_EXPECTED = {   # window -> [(name, start, end, COUNT(*), MAX(double), MIN(float))]
+    "tumble": [   # :199-205
+        ("a", "00:00", "00:00:05", 4, 5.0, 1.0), ("a", "00:00:05", "00:00:10", 1, None, 3.0),
+        ("b", "00:00:05", "00:00:10", 2, 6.0, 3.0), ("b", "00:00:15", "00:00:20", 1, 4.0, 4.0),
+        ("b", "00:00:30", "00:00:35", 1, 3.0, 3.0), ("null", "00:00:30", "00:00:35", 1, 7.0, 7.0)],
+    "hop": [   # :416-428
+        ("a", "-00:00:05", "00:00:05", 4, 5.0, 1.0), ("a", "00:00", "00:00:10", 6, 5.0, 1.0),
+        ("a", "00:00:05", "00:00:15", 1, None, 3.0), ("b", "00:00", "00:00:10", 2, 6.0, 3.0),
+        ("b", "00:00:05", "00:00:15", 2, 6.0, 3.0), ("b", "00:00:10", "00:00:20", 1, 4.0, 4.0),
+        ("b", "00:00:15", "00:00:25", 1, 4.0, 4.0), ("b", "00:00:25", "00:00:35", 1, 3.0, 3.0),
+        ("b", "00:00:30", "00:00:40", 1, 3.0, 3.0), ("null", "00:00:25", "00:00:35", 1, 7.0, 7.0),
+        ("null", "00:00:30", "00:00:40", 1, 7.0, 7.0)],
+    "cumulate": [   # :545-559
+        ("a", "00:00", "00:00:05", 4, 5.0, 1.0), ("a", "00:00", "00:00:10", 6, 5.0, 1.0),
+        ("a", "00:00", "00:00:15", 6, 5.0, 1.0), ("b", "00:00", "00:00:10", 2, 6.0, 3.0),
+        ("b", "00:00", "00:00:15", 2, 6.0, 3.0), ("b", "00:00:15", "00:00:20", 1, 4.0, 4.0),
+        ("b", "00:00:15", "00:00:25", 1, 4.0, 4.0), ("b", "00:00:15", "00:00:30", 1, 4.0, 4.0),
+        ("b", "00:00:30", "00:00:35", 1, 3.0, 3.0), ("b", "00:00:30", "00:00:40", 1, 3.0, 3.0),
+        ("b", "00:00:30", "00:00:45", 1, 3.0, 3.0), ("null", "00:00:30", "00:00:35", 1, 7.0, 7.0),
+        ("null", "00:00:30", "00:00:40", 1, 7.0, 7.0), ("null", "00:00:30", "00:00:45", 1, 7.0, 7.0)],
+}
+
+
+def itcase_minmax_fixtures():
+    NAME = {"a": 1, "b": 2, "null": 3}
+    base = "TPT/runtime/stream/sql/WindowAggregateITCase.scala"
+    src = {"tumble": ":176-207", "hop": ":394-430", "cumulate": ":519-562"}
+    spec = {"tumble": dict(size=5000, slide=0), "hop": dict(size=10000, slide=5000),
+            "cumulate": dict(size=15000, slide=5000)}
+
+    def T(s):   # "00:00:05" on 2020-10-10; "-00:00:05" = 2020-10-09T23:59:55
+        if s.startswith("-"):
+            return utc_ms("2020-10-10T00:00:00") - (utc_ms("2020-10-10T" + s[1:]) - utc_ms("2020-10-10T00:00:00"))
+        return utc_ms("2020-10-10T" + (s if s.count(":") == 2 else s + ":00"))
+
+    out = []
+    for agg, col in (("max", "double"), ("min", "float")):
+        ev = []
+        mx = -(1 << 63)
+        for i, (ts, d, name) in enumerate(ITCASE_ROWS):
+            v = d if col == "double" else ITCASE_FLOAT[i]
+            t = utc_ms(ts.replace(" ", "T"))
+            ev.append(E(name, 0.0 if v is None else v, t, 1 if v is None else 0))
+            mx = max(mx, t)
+            ev.append(WM(mx - 1000))
+        ev.append(WM(JMAX))
+        for kind in ("tumble", "hop", "cumulate"):
+            rows = [[NAME[n], T(a), T(b), c, mxv if agg == "max" else mnv]
+                    for n, a, b, c, mxv, mnv in ITCASE_EXPECTED[kind]]
+            out.append(dict(
+                name=f"itcase_{kind}_{agg}_{col}", source=base + src[kind] + "; data TPT/runtime/utils/TestData.scala:601-615",
+                config=dict(mode="sql", kind=kind, offset=0, tz_offset_ms=0, val_type="f64", count_star_index=0,
+                            aggs=["count_star", "count", agg], **spec[kind]),
+                columns=["key", "window_start", "window_end", "cnt_star", agg], events=ev,
+                expected=[dict(after_event="end", rows=rows)], expected_late_dropped=None))
+    return out
+
+
+# ----------------------------------------------------------------------------------------
 # Slice assigner known answers (TRT/operators/window/slicing/*SliceAssignerTest.java),
 # parameterized there over America/Los_Angeles and Asia/Shanghai; the fixed-offset zone
 # Asia/Shanghai (and UTC) are transcribed. Inputs to assignSliceEnd are localMills(str)
@@ -602,7 +672,7 @@ def timeutil_fixtures():
 
 
 def main():
-    ops = slicing_operator_fixtures() + datastream_fixtures() + itcase_fixtures()
+    ops = slicing_operator_fixtures() + datastream_fixtures() + itcase_fixtures() + itcase_minmax_fixtures()
     with open(os.path.join(HERE, "operator_cases.json"), "w") as f:
         json.dump(ops, f, indent=1)
     cases, errors = assigner_fixtures()

@@ -629,3 +629,44 @@ def test_unknown_key_count_takes_the_largest_table(oracle_mod):
     keys fit where a one-region table (3,584 entries) would overflow loudly."""
     cfg = cfg_of("tumble", 1000)
     drive_both(oracle_mod, cfg, n=400_000, keys=200_000, batch=100_000, delay=0, jitter=0, expected_keys=0)
+
+
+@pytest.mark.parametrize("kind,outliers", [("tumble", "future"), ("tumble", "epoch0"), ("hop", "both"),
+                                           ("cumulate", "future")])
+def test_outlier_slices_cost_no_empty_passes(oracle_mod, kind, outliers):
+    """A batch holding a record a day ahead (or at rowtime 0) spans ~86,400 (or ~1.6e9) empty
+    1-s slices: the filtered ingest passes jump from occupied slice to occupied slice
+    (each pass reports the next one), so the batch stages in a few passes and the rows and
+    late drops still match the oracle. Watermarks follow the regular records (the outliers
+    are held back by the source's watermark strategy)."""
+    import time
+    cfg = cfg_of(kind, 1000 if kind == "tumble" else 4000, 0 if kind == "tumble" else 1000)
+    n, keys, batch = 200_000, 3000, 20_000
+    key, ts, val, _ = make_stream(n, keys, "f64", jitter_ms=400)
+    ts = ts.copy()
+    if outliers in ("future", "both"):
+        ts[5] = ts[5] + 86_400_000          # a day ahead
+        ts[n // 2 + 7] = ts[n // 2 + 7] + 3 * 86_400_000
+    if outliers in ("epoch0", "both"):
+        ts[11] = 0                          # Long 0: an ancient record, before the first watermark
+    g = gpu_mk(cfg, expected_keys=keys, buffer_records=1 << 17)
+    o = oracle_mk(oracle_mod, cfg)
+    regular = np.ones(n, dtype=bool)
+    regular[[5, 11, n // 2 + 7]] = False
+    mx = np.iinfo(np.int64).min
+    t0 = time.time()
+    for lo in range(0, n, batch):
+        hi = min(n, lo + batch)
+        g.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        mx = max(mx, int(ts[lo:hi][regular[lo:hi]].max()))
+        g.process_watermark(mx - 300 - 1)
+        o.process_watermark(mx - 300 - 1)
+        assert_rows_equal(g.take_rows(), o.take_rows(), "f64", f"{kind} batch {lo}")
+        assert g.late_dropped == o.late_dropped
+    g.process_watermark(JMAX)
+    o.process_watermark(JMAX)
+    assert_rows_equal(g.take_rows(), o.take_rows(), "f64", "final")
+    assert time.time() - t0 < 60, "empty slice stretches were walked pass by pass"
+    g.close()
+    o.close()

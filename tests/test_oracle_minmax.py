@@ -1,7 +1,9 @@
-"""Oracle MIN / MAX (MinAggFunction.java:56-90, MaxAggFunction.java:56-96): the restatement
-against a direct numpy group-by of the same records. The reference's own tests hold no
-MIN / MAX window-aggregate golden vector for this path, so beyond the shared accumulator
-null rule (pinned with SUM by the golden cases) MIN / MAX are pinned by restatement."""
+"""Oracle MIN / MAX (MinAggFunction.java:56-90, MaxAggFunction.java:56-96) on randomized
+streams: the restatement against a direct numpy group-by of the same records. The literal
+values are pinned by the reference's own vectors -- WindowAggregateITCase's MAX(`double`)
+and MIN(`float`) per (name, window) for tumble / hop / cumulate (tests/golden,
+itcase_*_max_double / itcase_*_min_float, run on the oracle in test_oracle_golden.py and on
+the GPU in test_gpu_parity.py::test_golden_cases_on_gpu); this file adds coverage at scale."""
 import numpy as np
 import pytest
 
