@@ -879,6 +879,8 @@ typedef struct {
     int64_t* key; int64_t* ts; int64_t* val; int64_t* gidx;   /* records routed to this instance */
     int32_t n_wm; const int64_t* wm_at; const int64_t* wm_val;
     int64_t rows; uint64_t checksum; int64_t late;
+    int keep_rows; int32_t snapshot_after;          /* or_run_partitioned_rows */
+    or_row* out; int64_t out_n, out_cap;
 } part_job;
 
 static uint64_t row_digest(const or_row* r) {
@@ -899,10 +901,25 @@ static void* part_worker(void* arg) {
         if (i > s) or_process_batch(op, i - s, j->key + s, j->ts + s, j->val ? j->val + s : NULL, NULL);
         if (w < j->n_wm) or_process_watermark(op, j->wm_val[w]);
         for (int64_t r = 0; r < op->rows_n; r++) j->checksum += row_digest(&op->rows[r]);
+        if (j->keep_rows && op->rows_n > 0) {
+            if (j->out_n + op->rows_n > j->out_cap) {
+                j->out_cap = 2 * (j->out_n + op->rows_n);
+                j->out = (or_row*)realloc(j->out, sizeof(or_row) * (size_t)j->out_cap);
+            }
+            memcpy(j->out + j->out_n, op->rows, sizeof(or_row) * (size_t)op->rows_n);
+            j->out_n += op->rows_n;
+        }
         j->rows += op->rows_n;
         op->rows_n = 0;
+        if (w == j->snapshot_after) {   /* checkpoint + failover: continue as the restored copy */
+            or_prepare_snapshot(op);
+            or_op* r = or_restore_copy(op);
+            j->late += op->late_dropped;
+            or_close(op);
+            op = r;
+        }
     }
-    j->late = op->late_dropped;
+    j->late += op->late_dropped;
     or_close(op);
     return NULL;
 }
@@ -913,9 +930,10 @@ static double now_s(void) {
     return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
-double or_run_partitioned(const or_config* cfg, int32_t P, int32_t max_p, int64_t n, const int64_t* key,
-                          const int64_t* ts, const void* val, int32_t n_wm, const int64_t* wm_at,
-                          const int64_t* wm_val, int64_t* rows_out, uint64_t* checksum, int64_t* late_out) {
+static double run_partitioned(const or_config* cfg, int32_t P, int32_t max_p, int64_t n, const int64_t* key,
+                              const int64_t* ts, const void* val, int32_t n_wm, const int64_t* wm_at,
+                              const int64_t* wm_val, int64_t* rows_out, uint64_t* checksum, int64_t* late_out,
+                              int keep_rows, int32_t snapshot_after, or_row** rows_kept) {
     /* keyBy routing: KeyGroupStreamPartitioner.selectChannel (SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:55-65) */
     int32_t* dest = (int32_t*)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
     int64_t* cnt = (int64_t*)calloc((size_t)P, sizeof(int64_t));
@@ -933,6 +951,7 @@ double or_run_partitioned(const or_config* cfg, int32_t P, int32_t max_p, int64_
         jobs[p].val = v ? (int64_t*)malloc(sizeof(int64_t) * (size_t)(cnt[p] + 1)) : NULL;
         jobs[p].gidx = (int64_t*)malloc(sizeof(int64_t) * (size_t)(cnt[p] + 1));
         jobs[p].n_wm = n_wm; jobs[p].wm_at = wm_at; jobs[p].wm_val = wm_val;
+        jobs[p].keep_rows = keep_rows; jobs[p].snapshot_after = snapshot_after;
     }
     for (int64_t i = 0; i < n; i++) {
         part_job* j = &jobs[dest[i]];
@@ -953,7 +972,35 @@ double or_run_partitioned(const or_config* cfg, int32_t P, int32_t max_p, int64_
         rows += jobs[p].rows; cs += jobs[p].checksum; late += jobs[p].late;
         free(jobs[p].key); free(jobs[p].ts); free(jobs[p].val); free(jobs[p].gidx);
     }
+    if (keep_rows) {
+        or_row* all = (or_row*)malloc(sizeof(or_row) * (size_t)(rows > 0 ? rows : 1));
+        int64_t at = 0;
+        for (int32_t p = 0; p < P; p++) {
+            if (jobs[p].out_n) memcpy(all + at, jobs[p].out, sizeof(or_row) * (size_t)jobs[p].out_n);
+            at += jobs[p].out_n;
+            free(jobs[p].out);
+        }
+        *rows_kept = all;
+    }
     *rows_out = rows; *checksum = cs; *late_out = late;
     free(th); free(jobs); free(cnt); free(dest);
     return el;
 }
+
+double or_run_partitioned(const or_config* cfg, int32_t P, int32_t max_p, int64_t n, const int64_t* key,
+                          const int64_t* ts, const void* val, int32_t n_wm, const int64_t* wm_at,
+                          const int64_t* wm_val, int64_t* rows_out, uint64_t* checksum, int64_t* late_out) {
+    return run_partitioned(cfg, P, max_p, n, key, ts, val, n_wm, wm_at, wm_val, rows_out, checksum, late_out, 0, -1,
+                           NULL);
+}
+
+double or_run_partitioned_rows(const or_config* cfg, int32_t P, int32_t max_p, int64_t n, const int64_t* key,
+                               const int64_t* ts, const void* val, int32_t n_wm, const int64_t* wm_at,
+                               const int64_t* wm_val, int32_t snapshot_after, or_row** rows, int64_t* n_rows,
+                               int64_t* late_out) {
+    uint64_t cs = 0;
+    return run_partitioned(cfg, P, max_p, n, key, ts, val, n_wm, wm_at, wm_val, n_rows, &cs, late_out, 1,
+                           snapshot_after, rows);
+}
+
+void or_free(void* p) { free(p); }

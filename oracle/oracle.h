@@ -128,6 +128,17 @@ double  or_run_partitioned(const or_config* cfg, int32_t parallelism, int32_t ma
                            int32_t n_wm, const int64_t* wm_at, const int64_t* wm_val,
                            int64_t* rows_out, uint64_t* checksum, int64_t* late_out);
 
+/* --- The same, keeping every fired row (parity runs at BASELINE key spaces): the rows of
+ * all instances are concatenated into *rows (malloc'd; free with or_free), *n_rows their
+ * count. snapshot_after >= 0: after watermark snapshot_after every instance takes a
+ * checkpoint (prepareSnapshotPreBarrier) and continues as a restored copy (initializeState
+ * from that snapshot), as a failover would. Returns elapsed seconds. */
+double  or_run_partitioned_rows(const or_config* cfg, int32_t parallelism, int32_t max_parallelism,
+                                int64_t n, const int64_t* key, const int64_t* ts, const void* val,
+                                int32_t n_wm, const int64_t* wm_at, const int64_t* wm_val,
+                                int32_t snapshot_after, or_row** rows, int64_t* n_rows, int64_t* late_out);
+void    or_free(void* p);
+
 #ifdef __cplusplus
 }
 #endif

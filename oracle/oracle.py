@@ -140,6 +140,12 @@ def lib():
             C.POINTER(Config), C.c_int32, C.c_int32, C.c_int64, P, P, P, C.c_int32, P, P,
             i64p, C.POINTER(C.c_uint64), i64p,
         ]
+        L.or_run_partitioned_rows.restype = C.c_double
+        L.or_run_partitioned_rows.argtypes = [
+            C.POINTER(Config), C.c_int32, C.c_int32, C.c_int64, P, P, P, C.c_int32, P, P, C.c_int32,
+            C.POINTER(C.c_void_p), i64p, i64p,
+        ]
+        L.or_free.argtypes = [P]
         _lib = L
     return _lib
 
@@ -325,3 +331,31 @@ def run_partitioned(cfg: Config, parallelism, max_parallelism, key, ts, val, wm_
                                   _ptr(val), len(wm_at), _ptr(wm_at), _ptr(wm_val), C.byref(rows),
                                   C.byref(cs), C.byref(late))
     return el, rows.value, cs.value, late.value
+
+
+def run_partitioned_rows(cfg: Config, parallelism, max_parallelism, key, ts, val, wm_at, wm_val, snapshot_after=-1):
+    """Every fired row of `parallelism` key-group-routed operator instances (ROW_DTYPE), the
+    late-drop count and the elapsed seconds; snapshot_after >= 0 takes a checkpoint and
+    restores from it after that watermark (or_run_partitioned_rows)."""
+    key = np.ascontiguousarray(key, dtype=np.int64)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    val = None if val is None else np.ascontiguousarray(val)
+    wm_at = np.ascontiguousarray(wm_at, dtype=np.int64)
+    wm_val = np.ascontiguousarray(wm_val, dtype=np.int64)
+    rp = C.c_void_p()
+    nr = C.c_int64()
+    late = C.c_int64()
+    L = lib()
+    el = L.or_run_partitioned_rows(C.byref(cfg), parallelism, max_parallelism, len(key), _ptr(key), _ptr(ts),
+                                   _ptr(val), len(wm_at), _ptr(wm_at), _ptr(wm_val), int(snapshot_after),
+                                   C.byref(rp), C.byref(nr), C.byref(late))
+    n = nr.value
+    try:
+        if n == 0:
+            rows = np.zeros(0, dtype=ROW_DTYPE)
+        else:
+            buf = (C.c_char * (n * ROW_DTYPE.itemsize)).from_address(rp.value)
+            rows = np.frombuffer(buf, dtype=ROW_DTYPE).copy()
+    finally:
+        L.or_free(rp)
+    return rows, late.value, el

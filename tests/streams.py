@@ -25,11 +25,14 @@ def zipf_keys(u, keys, s):
 
 
 def make_stream(n, keys, val_type="f64", t0=1_600_000_000_000, rate_per_ms=100, jitter_ms=0, null_frac=0.0,
-                seed=SEED, key_spread=False, big_ints=False, zipf=0.0):
+                seed=SEED, key_spread=False, big_ints=False, zipf=0.0, signed=False, cancel=False):
     """Returns (key, rowtime, val, isnull) numpy arrays.
 
     rowtime = t0 + i / rate_per_ms (+ uniform jitter in [0, jitter_ms) when out of order);
-    keys uniform over [0, keys), or Zipf(zipf) ranks (hot keys) when zipf > 0."""
+    keys uniform over [0, keys), or Zipf(zipf) ranks (hot keys) when zipf > 0.
+    signed: DOUBLE values uniform in [-1000, 1000) instead of [0, 1000).
+    cancel: every odd record repeats the previous record's key and rowtime with the negated
+    value (plus a small perturbation), so (key, window) sums nearly cancel."""
     i = np.arange(n, dtype=np.uint64)
     u = splitmix64(np.uint64(seed) ^ i)
     u2 = splitmix64(np.uint64(seed * 3 + 1) ^ i)
@@ -42,11 +45,18 @@ def make_stream(n, keys, val_type="f64", t0=1_600_000_000_000, rate_per_ms=100, 
         ts = ts + (u2 % np.uint64(jitter_ms)).astype(np.int64)
     if val_type == "f64":
         val = (u2 >> np.uint64(11)).astype(np.float64) * (1000.0 / float(1 << 53))
+        if signed:
+            val = val * 2.0 - 1000.0
     else:
         if big_ints:
             val = (u2 ^ (u << np.uint64(7))).view(np.int64)   # full-range: exercises Java wrap-around
         else:
             val = (u2 % np.uint64(1000)).astype(np.int64) - 300
+    if cancel:
+        odd = np.arange(1, n, 2)
+        key[odd] = key[odd - 1]
+        ts[odd] = ts[odd - 1]
+        val[odd] = -val[odd - 1] + (val[odd] if val_type != "f64" else val[odd] * 1e-9)
     isnull = None
     if null_frac > 0:
         isnull = ((u2 >> np.uint64(40)) % np.uint64(1000) < np.uint64(int(null_frac * 1000))).astype(np.uint8)
