@@ -164,12 +164,31 @@ def measure_copy_peak(dev, nbytes=2 << 30, reps=5):
         return None
 
 
+def host_cores():
+    """CPUs this process may run on (its affinity mask; os.cpu_count() counts the machine)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants (cpu.max quota / period), or None."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else float(q) / float(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, rate):
     """The oracle (C restatement of the reference operator) on the host cores: one instance
-    per core, records routed by key group, on a bounded prefix of the same stream."""
+    per core (P = nproc, capped at 85 so that maxParallelism stays 128 by
+    KeyGroupRangeAssignment.computeDefaultMaxParallelism), records routed by key
+    group, on a bounded prefix of the same stream."""
     from oracle import oracle as O
     O.build()
-    cores = min(16, os.cpu_count() or 1)
+    cores = min(85, host_cores()) if args.cpu_threads is None else args.cpu_threads
 
     def gen(n):
         i = np.arange(n, dtype=np.uint64)
@@ -202,11 +221,95 @@ def cpu_baseline(args, rate):
     n = int(min(args.cpu_max_records, max(4_000_000, rate_est * args.cpu_seconds)))
     n -= n % args.wm_every
     el, rows = run(n)
-    return dict(value=n / el, unit="records/s", cores=cores, kind="port",
+    quota = cpu_quota()
+    return dict(value=n / el, unit="records/s", cores=cores, kind="port", cpu_quota=quota,
                 sample=f"first {n:,} records of the configs[1] stream (10M-key space), watermark every "
                        f"{args.wm_every:,} records + final Long.MAX_VALUE; C restatement of "
                        f"SlicingWindowOperator/RecordsWindowBuffer/AggCombiner, {cores} instances routed by "
-                       f"key group (maxParallelism 128); {el:.1f} s, {rows:,} rows fired")
+                       f"key group (maxParallelism 128); {el:.1f} s, {rows:,} rows fired" +
+                       (f"; the cgroup grants {quota:g} CPUs of time to the {cores} threads" if quota else ""))
+
+
+def lib_sha256():
+    import hashlib
+    h = hashlib.sha256()
+    with open(os.path.join(ROOT, "flink_amd", "libflinkgpu.so"), "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def pmc_traffic(kernel_class):
+    """HBM bytes per launch of `kernel_class` from the newest committed rocprofv3 PMC summary
+    (profiles/*/pmc_traffic.json, profiles/pmc_summary.py) -- only if it was counted on THIS
+    library build (same sha256 of libflinkgpu.so); otherwise None. Returns (bytes, source)."""
+    import glob
+    try:
+        sha = lib_sha256()
+    except OSError:
+        return None, None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("_provenance", {}).get("lib_sha256") != sha:
+            continue
+        v = d.get(kernel_class.replace("local_", ""), {}).get("hbm_bytes_per_launch")
+        if v is not None:
+            return v, os.path.relpath(path, ROOT) + f" (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, lib {sha[:12]})"
+    return None, f"no PMC summary of this build (lib {sha[:12]}) under profiles/"
+
+
+def h2d_link_peak(dev, nbytes=1 << 30, reps=4):
+    """Pinned host -> device copy rate (GB/s) of this box's link."""
+    try:
+        a = torch.empty(nbytes // 8, dtype=torch.int64).pin_memory()
+        b = torch.empty(nbytes // 8, dtype=torch.int64, device=dev)
+        b.copy_(a, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            b.copy_(a, non_blocking=True)
+        torch.cuda.synchronize()
+        return nbytes * reps / (time.perf_counter() - t0) / 1e9
+    except RuntimeError:
+        return None
+
+
+def h2d_leg(args, wl, window, aggs, expected_keys, dev):
+    """The bench workload's first `h2d_records` records as pinned host columns (FG_HOST):
+    whole-job rate including PCIe, the link bytes, and the link's measured pinned H2D rate."""
+    import flink_amd as F
+    n = args.h2d_records - args.h2d_records % args.batch or args.batch
+    key, ts, val = gen_columns(n, args.keys, args.rate, 0, dev, jitter=wl["jitter"], zipf=wl["zipf"])
+    hk, ht, hv = (x.cpu().pin_memory() for x in (key, ts, val))
+    del key, ts, val
+    torch.cuda.empty_cache()
+    op = F.WindowAggOperator(window, aggs=aggs, val_type="f64", expected_keys=expected_keys,
+                             buffer_records=max(4 * args.batch, 1 << 26), device=dev.index)
+
+    def run():
+        op.reset()
+        for lo in range(0, n, args.batch):
+            hi = min(n, lo + args.batch)
+            op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi])
+            for wm in watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"]):
+                op.process_watermark(wm, device_output=True)
+        op.process_watermark(JMAX, device_output=True)
+        op.synchronize()
+    run()   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run()
+    el = time.perf_counter() - t0
+    op.close()
+    link = h2d_link_peak(dev)
+    gbs = 24 * n / el / 1e9
+    return {"value": n / el, "unit": "records/s", "records": n, "seconds": el, "pcie_gbs": gbs,
+            "link_peak_gbs": link, "link_frac": gbs / link if link else None,
+            "note": "pinned host columns handed over as FG_HOST batches (double-buffered H2D on the engine's "
+                    "copy stream, overlapping the kernels); secondary -- `value` has the inputs resident in HBM"}
 
 
 def main():
@@ -239,6 +342,11 @@ def main():
                     help="hand the engine pinned host columns (PCIe-inclusive rate; never the headline value)")
     ap.add_argument("--exchange", choices=("partials", "raw"), default="partials",
                     help="N > 1: exchange partial accumulators (two-phase) or raw records")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="CPU baseline instances (default: min(85, CPUs in this process's affinity mask))")
+    ap.add_argument("--h2d-records", type=int, default=200_000_000,
+                    help="records of the secondary pinned-host leg (FG_HOST batches, double-buffered H2D "
+                         "overlapping the kernels); 0 skips it. Never the headline value")
     args = ap.parse_args()
     wl = WORKLOADS[args.workload]
     if args.keys is None:
@@ -420,13 +528,7 @@ def main():
     avg_s = dom["total_ms"] / dom["launches"] / 1e3
     alg_bytes = (24 * dom["records"] + 48 * dom["rows"]) / dom["launches"]
     achieved = alg_bytes / avg_s / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get(dom_name.replace("local_", ""), {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = pmc_traffic(dom_name)
 
     copy_gbs = measure_copy_peak(dev)
     total_records = world * n * args.steps
@@ -455,7 +557,8 @@ def main():
                  " + RCCL all-to-all of records") if world > 1 else ""),
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": dom_name,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": dom_name,
                      "avg_launch_ms": avg_s * 1e3,
                      "alg_bytes_per_launch": alg_bytes,
                      # SURVEY.md 8d second denominator: a device-to-device copy measured on this box
@@ -472,12 +575,19 @@ def main():
         "kernels": {k: dict(v, avg_ms=v["total_ms"] / v["launches"]) for k, v in ks.items()},
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and args.h2d_records > 0 and not args.host_input and args.workload == "tumble":
+        # secondary: the same workload handed over as pinned host columns (the FG_HOST
+        # boundary a JNI shim uses), H2D double-buffered on the engine's copy stream
+        op.close()
+        del key, ts, val
+        torch.cuda.empty_cache()
+        result["h2d"] = h2d_leg(args, wl, window, aggs, expected_keys, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args, args.rate // 1000)
         except Exception as e:  # reported, not fatal
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
-    op.close()
+    op.close()   # (idempotent)
     if op_local:
         op_local.close()
     if rank == 0:

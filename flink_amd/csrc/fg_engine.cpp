@@ -196,6 +196,13 @@ struct fg_handle {
 
     // ingest scratch
     DevBuf in_key, in_ts, in_val, in_null;
+    // FG_HOST batches: double-buffered H2D on a copy stream of its own, so that the copy of
+    // batch i + 1 overlaps the kernels of batch i (the engine stream waits for the copy's
+    // event; a buffer is rewritten only after the kernels that read it)
+    hipStream_t copy_stream = nullptr;
+    DevBuf hb_key[2], hb_ts[2], hb_val[2], hb_null[2];
+    hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+    int hslot = 0;
     DevBuf part_tmp, part_tmp_null, part_dir;   // two-pass partition: pass-1 tiles + directory
     // skewed-region plan and chunk partial tables
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
@@ -1588,24 +1595,51 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     const int64_t *key = b->key, *ts = b->rowtime;
     const int64_t* val = h->cfg.val_type != FG_VAL_NONE ? static_cast<const int64_t*>(b->val) : nullptr;
     const uint8_t* vnull = b->val_null;
+    int slot = -1;   // FG_HOST: the device buffer set this batch was copied into
     if (b->location == FG_HOST) {
-        HIPCHK(h, h->in_key.ensure(8 * n));
-        HIPCHK(h, h->in_ts.ensure(8 * n));
-        HIPCHK(h, hipMemcpyAsync(h->in_key.p, key, 8 * n, hipMemcpyHostToDevice, h->stream));
-        HIPCHK(h, hipMemcpyAsync(h->in_ts.p, ts, 8 * n, hipMemcpyHostToDevice, h->stream));
-        key = h->in_key.as<int64_t>();
-        ts = h->in_ts.as<int64_t>();
+        // double-buffered H2D (RecordsWindowBuffer.addElement receives the records from the
+        // JVM, :81-97; the shim hands a micro-batch of them): the copy runs on the copy stream
+        // while the previous batch's kernels run on the engine stream
+        if (!h->copy_stream) {
+            HIPCHK(h, hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking));
+            for (int i = 0; i < 2; i++) {
+                HIPCHK(h, hipEventCreateWithFlags(&h->ev_copied[i], hipEventDisableTiming));
+                HIPCHK(h, hipEventCreateWithFlags(&h->ev_free[i], hipEventDisableTiming));
+                HIPCHK(h, hipEventRecord(h->ev_free[i], h->stream));
+            }
+        }
+        slot = h->hslot;
+        h->hslot ^= 1;
+        const bool grow = h->hb_key[slot].bytes < (size_t)(8 * n) || (val && h->hb_val[slot].bytes < (size_t)(8 * n)) ||
+                          (vnull && h->hb_null[slot].bytes < (size_t)n);
+        if (grow) HIPCHK(h, hipEventSynchronize(h->ev_free[slot]));   // the old buffers are freed
+        HIPCHK(h, h->hb_key[slot].ensure(8 * n));
+        HIPCHK(h, h->hb_ts[slot].ensure(8 * n));
+        HIPCHK(h, hipStreamWaitEvent(h->copy_stream, h->ev_free[slot], 0));
+        HIPCHK(h, hipMemcpyAsync(h->hb_key[slot].p, key, 8 * n, hipMemcpyHostToDevice, h->copy_stream));
+        HIPCHK(h, hipMemcpyAsync(h->hb_ts[slot].p, ts, 8 * n, hipMemcpyHostToDevice, h->copy_stream));
+        key = h->hb_key[slot].as<int64_t>();
+        ts = h->hb_ts[slot].as<int64_t>();
         if (val) {
-            HIPCHK(h, h->in_val.ensure(8 * n));
-            HIPCHK(h, hipMemcpyAsync(h->in_val.p, val, 8 * n, hipMemcpyHostToDevice, h->stream));
-            val = h->in_val.as<int64_t>();
+            HIPCHK(h, h->hb_val[slot].ensure(8 * n));
+            HIPCHK(h, hipMemcpyAsync(h->hb_val[slot].p, val, 8 * n, hipMemcpyHostToDevice, h->copy_stream));
+            val = h->hb_val[slot].as<int64_t>();
         }
         if (vnull) {
-            HIPCHK(h, h->in_null.ensure(n));
-            HIPCHK(h, hipMemcpyAsync(h->in_null.p, vnull, n, hipMemcpyHostToDevice, h->stream));
-            vnull = h->in_null.as<uint8_t>();
+            HIPCHK(h, h->hb_null[slot].ensure(n));
+            HIPCHK(h, hipMemcpyAsync(h->hb_null[slot].p, vnull, n, hipMemcpyHostToDevice, h->copy_stream));
+            vnull = h->hb_null[slot].as<uint8_t>();
         }
+        HIPCHK(h, hipEventRecord(h->ev_copied[slot], h->copy_stream));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_copied[slot], 0));
     }
+    struct SlotFree {   // every kernel reading the slot's buffers is queued when this runs
+        fg_handle* h;
+        int slot;
+        ~SlotFree() {
+            if (slot >= 0) (void)hipEventRecord(h->ev_free[slot], h->stream);
+        }
+    } slot_free{h, slot};
     if (h->windowed) {   // window_end -> pseudo rowtime (every end on the slice grid)
         HIPCHK(h, h->in_wts.ensure(8 * n + 8));
         unsigned long long* bad = reinterpret_cast<unsigned long long*>(h->in_wts.as<int64_t>() + n);
@@ -2045,6 +2079,14 @@ void fg_close(fg_handle* h) {
         h->ev_pool.push_back(p.b);
     }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; i++) {
+        if (h->ev_copied[i]) (void)hipEventDestroy(h->ev_copied[i]);
+        if (h->ev_free[i]) (void)hipEventDestroy(h->ev_free[i]);
+    }
+    if (h->copy_stream) {
+        (void)hipStreamSynchronize(h->copy_stream);
+        (void)hipStreamDestroy(h->copy_stream);
+    }
     hipStream_t s = h->stream;
     delete h;
     if (s) (void)hipStreamDestroy(s);

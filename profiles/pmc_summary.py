@@ -59,6 +59,15 @@ def traffic(res):
     return t
 
 
+def lib_sha256(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 if __name__ == "__main__":
     res = summarize(glob.glob(sys.argv[1]))
     for k, cs in sorted(res.items()):
@@ -66,5 +75,10 @@ if __name__ == "__main__":
         for c, v in sorted(cs.items()):
             print(f"   {c:28s} {v:16.1f}")
     if len(sys.argv) > 2:
-        json.dump(traffic(res), open(sys.argv[2], "w"), indent=1)
+        t = traffic(res)
+        # provenance: bench.py reports these bytes only for the library build they were
+        # counted on (sha256 of libflinkgpu.so), never for another build
+        lib = sys.argv[3] if len(sys.argv) > 3 else None
+        t["_provenance"] = {"lib_sha256": lib_sha256(lib) if lib else None, "source": sys.argv[1]}
+        json.dump(t, open(sys.argv[2], "w"), indent=1)
         print("wrote", sys.argv[2])

@@ -18,6 +18,7 @@ of Zipf(1.1) keys with 2 s jitter, a bounded-out-of-orderness watermark and a ch
 failover -> restore mid-stream; configs[0] the whole 10M-record DataStream job.
 """
 import os
+import time
 
 import numpy as np
 import pytest
@@ -34,8 +35,12 @@ def _bench():
     return bench
 
 
+def log(msg):
+    print(f"[{time.strftime('%H:%M:%S')}] {msg}", flush=True)   # progress (long cases; run with -s)
+
+
 def gpu_rows_run(op, key, ts, val, n, batch, rate, wm_every, delay, jitter, snapshot_after_batch=None,
-                 reopen=None):
+                 reopen=None, final_wm=JMAX):
     """Drive the engine like bench.one_step; returns (rows, late drops, oracle watermark schedule,
     index of the snapshot watermark or -1)."""
     B = _bench()
@@ -60,9 +65,9 @@ def gpu_rows_run(op, key, ts, val, n, batch, rate, wm_every, delay, jitter, snap
             op = reopen()
             op.restore_state(img, twm)
             snap_idx = len(wm_at) - 1
-    parts.append(op.process_watermark(JMAX))
+    parts.append(op.process_watermark(final_wm))
     wm_at.append(n)
-    wm_val.append(JMAX)
+    wm_val.append(final_wm)
     late = late_base + op.num_late_records_dropped
     op.close()
     parts = [p for p in parts if len(p)]
@@ -96,7 +101,11 @@ def compare_rows(g, e, S, ctx, aggs):
         assert err.all(), f"{ctx}: {f} beyond 1e-9 relative: {a[~err][:5]} vs {b[~err][:5]}"
 
 
-def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch=None, keys=None):
+def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch=None, keys=None,
+               final_wm_after=None):
+    """final_wm_after: end with the watermark `final_wm_after` ms past the last regular one
+    instead of Long.MAX_VALUE (CUMULATE: MAX_VALUE would fire every remaining step window of
+    the hour for every key -- 60 x 12.5M rows)."""
     import torch
 
     import flink_amd as F
@@ -123,14 +132,20 @@ def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch
         return F.WindowAggOperator(window, aggs=aggs, val_type="i64" if datastream else "f64",
                                    mode="datastream" if datastream else "sql", expected_keys=expected,
                                    buffer_records=max(4 * batch, 1 << 26))
+    final_wm = JMAX
+    if final_wm_after is not None:
+        final_wm = B.watermarks_for(0, n, rate, wm_every, wl["delay"], wl["jitter"])[-1] + final_wm_after
+    log(f"{workload}: {n:,} records generated; GPU run")
     rows, late, wm_at, wm_val, snap = gpu_rows_run(mk(), key, ts, val, n, batch, rate, wm_every, wl["delay"],
-                                                   wl["jitter"], snapshot_after_batch, reopen=mk)
+                                                   wl["jitter"], snapshot_after_batch, reopen=mk, final_wm=final_wm)
+    log(f"{workload}: GPU fired {0 if rows is None else len(rows):,} rows; oracle run")
     kh, th, vh = key.cpu().numpy(), ts.cpu().numpy(), val.cpu().numpy()
     del key, ts, val
     torch.cuda.empty_cache()
     cfg = O.Config(O.MODE_DATASTREAM if datastream else O.MODE_SQL, oracle_kind, size, slide, 0, 0,
                    O.VAL_I64 if datastream else O.VAL_F64, 0)
     exp, olate, _ = O.run_partitioned_rows(cfg, ORACLE_THREADS, 128, kh, th, vh, wm_at, wm_val, snapshot_after=snap)
+    log(f"{workload}: oracle fired {len(exp):,} rows; comparing")
     assert rows is not None and len(rows) > 0
     ctx = f"{workload} n={n}"
     if datastream:
@@ -174,7 +189,8 @@ def test_config3_cumulate_1h_1min_per_gpu_share():
     records = 4+ one-minute steps of the hour window (each step window folds its slice into
     the first slice's state and emits every key seen so far)."""
     from oracle import oracle as O
-    nrows, _ = run_config("cumulate", 70_000_000, ("count_star", "sum", "avg"), O.CUMULATE, 3_600_000, 60_000)
+    nrows, _ = run_config("cumulate", 70_000_000, ("count_star", "sum", "avg"), O.CUMULATE, 3_600_000, 60_000,
+                          final_wm_after=60_000)
     assert nrows > 30_000_000
 
 
