@@ -1923,8 +1923,8 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         std::vector<uint32_t> off(NB + 1, 0);
         std::vector<uint32_t> reg(m);
         for (int64_t j = 0; j < m; j++) {
-            const int64_t k = in->key[idx[j]];
-            reg[j] = h->region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)k) >> (64 - h->region_bits));
+            const uint64_t hk = fmix64((uint64_t)in->key[idx[j]]);
+            reg[j] = h->region_bits == 0 ? 0u : (uint32_t)(hk >> (64 - h->region_bits));
             off[reg[j] + 1]++;
         }
         for (int r = 0; r < NB; r++) off[r + 1] += off[r];
@@ -1933,7 +1933,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         for (int64_t j = 0; j < m; j++) {
             const int64_t i = idx[j];
             const uint32_t at = cur[reg[j]]++;
-            k[at] = in->key[i];
+            k[at] = mix_of(in->key[i]);   // state keeps the key's mix (fg_window.h)
             cs[at] = in->cnt_star[i];
             cn[at] = in->cnt_star[i] - in->cnt_val[i];
             sm[at] = in->sum[i];

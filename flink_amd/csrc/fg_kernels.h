@@ -25,12 +25,21 @@ constexpr int kMaxAggs = 8;
 // into a tile-private buffer, pass 2 sorts each (coarse bucket, workgroup) unit by fine
 // bucket into the staged areas
 constexpr int kFineBits = 6;                  // fine buckets per coarse bucket = 64
-constexpr int kPart1Threads = 768;            // 12 waves: 168 VGPRs per lane, room for a prefetched tile
-constexpr int kPart1Tile = 8 * kPart1Threads;  // pass-1 records per tile (8 per thread)
+#ifndef FG_P1_T
+#define FG_P1_T 768
+#endif
+#ifndef FG_P1_R
+#define FG_P1_R 6
+#endif
+constexpr int kPart1Threads = FG_P1_T;        // one workgroup per CU (LDS: fine histogram + tile)
+constexpr int kPart1Tile = FG_P1_R * kPart1Threads;   // pass-1 records per tile (FG_P1_R per thread, one LDS round)
 constexpr int kMaxPart1Fine = 16384;          // lanes << region_bits for the two-pass path
 constexpr int kMaxCoarse = kMaxPart1Fine >> kFineBits;   // 256
-constexpr int kPart2Threads = 256;
-constexpr int kPart2Tile = 2048;              // pass-2 records per sub-tile (8 per thread)
+#ifndef FG_P2_T
+#define FG_P2_T 512
+#endif
+constexpr int kPart2Threads = FG_P2_T;
+constexpr int kPart2Tile = 8 * kPart2Threads;  // pass-2 records per sub-tile (8 per thread)
 
 // One slice table in HBM: P regions, each region an SoA block of kRegionCap entries:
 //   [key i64 x cap][cnt_star i64 x cap][cnt_null i64 x cap][sum (i64 | f64 bits) x cap]

@@ -36,6 +36,17 @@ __device__ __forceinline__ const T __attribute__((address_space(1)))* gbl(const 
     return (const T __attribute__((address_space(1)))*)q;
 }
 
+// A pointer every lane of the wave holds (loaded from LDS, so the compiler cannot tell):
+// moved to SGPRs, so loads off it take the scalar-base + 32-bit-offset form (no 64-bit
+// address arithmetic per lane).
+template <class T>
+__device__ __forceinline__ T* wave_uniform(T* q) {
+    const uint64_t v = (uint64_t)q;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's LDS ops, not for its
 // global loads/stores (a __syncthreads() also drains vmcnt, stalling on in-flight stores).
 __device__ __forceinline__ void lds_barrier() {
@@ -48,8 +59,10 @@ __device__ __forceinline__ void lds_barrier() {
 // ----------------------------------------------------------------------------------------
 // record classification shared by count and scatter (must agree exactly)
 // ----------------------------------------------------------------------------------------
-// returns bucket >= 0, -1 when the record is late-dropped, -2 when outside the slice filter
-__device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int64_t ts, int64_t* q_out) {
+// returns bucket >= 0, -1 when the record is late-dropped, -2 when outside the slice filter;
+// *h_out = fmix64(key), the form in which the key is staged and kept (fg_window.h)
+__device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int64_t ts, int64_t* q_out,
+                                        int64_t* h_out) {
     int64_t target, q;
     const uint64_t d = (uint64_t)ts + (uint64_t)p.w.tz - (uint64_t)p.tbase;
     const uint64_t qq = __umul64hi(d, p.div_m);
@@ -63,8 +76,14 @@ __device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int6
     *q_out = q;   // also for records outside the filter: the batch's whole slice range is counted
     if (q < p.filter_lo || q >= p.filter_hi) return -2;
     const int lane = (int)(q & (int64_t)(p.lanes - 1));
-    const uint32_t rb = p.region_bits == 0 ? 0u : (uint32_t)(fmix64((uint64_t)key) >> (64 - p.region_bits));
+    const uint64_t h = fmix64((uint64_t)key);
+    *h_out = (int64_t)h;
+    const uint32_t rb = p.region_bits == 0 ? 0u : (uint32_t)(h >> (64 - p.region_bits));
     return (lane << p.region_bits) | (int)rb;
+}
+__device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int64_t ts, int64_t* q_out) {
+    int64_t h;
+    return classify(p, key, ts, q_out, &h);
 }
 
 __device__ __forceinline__ void seg_bounds(int64_t n, int grid, int g, int64_t* b, int64_t* e) {
@@ -247,12 +266,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_direct(Ingest
     const bool aos = p.st_stride == 2;
     for (int64_t i = beg + tid; i < end; i += kIngestThreads) {
         const int64_t k = p.key[i];
-        int64_t q;
-        const int b = classify(p, k, p.ts[i], &q);
+        int64_t q, h;
+        const int b = classify(p, k, p.ts[i], &q, &h);
         if (b < 0) continue;
         const uint32_t pos = atomicAdd(&s_cur[b], 1u);
-        if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = make_longlong2(k, has_val ? p.val[i] : 0);
-        else p.st_rec[pos] = k;
+        if (aos) *reinterpret_cast<longlong2*>(p.st_rec + 2 * (int64_t)pos) = make_longlong2(h, has_val ? p.val[i] : 0);
+        else p.st_rec[pos] = h;
         if (has_null) p.st_null[pos] = p.vnull[i];
     }
 }
@@ -316,11 +335,9 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
             }
 #pragma unroll
             for (int j = 0; j < kPerThread / 2; j++) {
-                rk[2 * j] = k2[j].x;
-                rk[2 * j + 1] = k2[j].y;
                 int64_t q;
-                int b0 = classify(p, k2[j].x, t2[j].x, &q);
-                int b1 = classify(p, k2[j].y, t2[j].y, &q);
+                int b0 = classify(p, k2[j].x, t2[j].x, &q, &rk[2 * j]);
+                int b1 = classify(p, k2[j].y, t2[j].y, &q, &rk[2 * j + 1]);
                 if (b0 >= 0) b0 = p.lane_slot[b0 >> p.region_bits] * P + (b0 & (P - 1));
                 if (b1 >= 0) b1 = p.lane_slot[b1 >> p.region_bits] * P + (b1 & (P - 1));
                 rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
@@ -353,11 +370,10 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
                     k2.y = p.key[i + 1];
                     t2.y = p.ts[i + 1];
                 }
-                rk[2 * j] = k2.x;
-                rk[2 * j + 1] = k2.y;
+                rk[2 * j] = rk[2 * j + 1] = 0;
                 int64_t q;
-                int b0 = li < tn ? classify(p, k2.x, t2.x, &q) : -3;
-                int b1 = li + 1 < tn ? classify(p, k2.y, t2.y, &q) : -3;
+                int b0 = li < tn ? classify(p, k2.x, t2.x, &q, &rk[2 * j]) : -3;
+                int b1 = li + 1 < tn ? classify(p, k2.y, t2.y, &q, &rk[2 * j + 1]) : -3;
                 if (b0 >= 0) b0 = p.lane_slot[b0 >> p.region_bits] * P + (b0 & (P - 1));
                 if (b1 >= 0) b1 = p.lane_slot[b1 >> p.region_bits] * P + (b1 & (P - 1));
                 rbr[2 * j] = b0 >= 0 ? (atomicAdd(&s_off[b0], 1u) << 13) | (uint32_t)b0 : 0xffffffffu;
@@ -443,12 +459,19 @@ __global__ __launch_bounds__(kIngestThreads) void k_ingest_scatter_sorted(Ingest
 // Pass 1: the count pass's bookkeeping (drops, slice range, lane totals, fine histogram per
 // workgroup) plus a tile sort by coarse bucket (fine >> 6) written back to the tile's own
 // input offset in p.tmp (fully sequential stores); p.dir holds each tile's coarse offsets.
+// Software-pipelined: the next tile's key / rowtime / value loads are issued right after the
+// current tile is classified, so they are in flight across its scan, LDS staging and
+// write-out (barriers here order LDS only); one LDS staging round per tile.
 __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
+    constexpr int T = kPart1Threads;
+    constexpr int R = FG_P1_R;                       // records per thread per tile (even: 16-B pairs)
+    constexpr int TILE = kPart1Tile;
+    static_assert(R % 2 == 0, "pairs of records per thread");
     __shared__ uint32_t s_hist[kMaxPart1Fine];       // 64 KiB: fine histogram of this workgroup
-    __shared__ longlong2 s_rec[kRound];              // 64 KiB
-    __shared__ uint8_t s_nul[kRound];                // 4 KiB
+    __shared__ longlong2 s_rec[TILE];                // the tile, coarse-bucket sorted
+    __shared__ uint8_t s_nul[TILE];
     __shared__ uint32_t s_cc[kMaxCoarse + 1];        // tile coarse counts, then offsets
-    __shared__ uint32_t s_wave[kPart1Threads / 64];
+    __shared__ uint32_t s_wave[T / 64];
     __shared__ unsigned long long s_drop;
     __shared__ long long s_qmin, s_qmax, s_qnext;
     __shared__ uint32_t s_mask;
@@ -456,8 +479,8 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     const int F = p.lanes << p.region_bits;
     const int NC = p.n_coarse;
     const int tid = threadIdx.x;
-    for (int i = tid; i < F; i += kPart1Threads) s_hist[i] = 0;
-    for (int i = tid; i <= NC; i += kPart1Threads) s_cc[i] = 0;
+    for (int i = tid; i < F; i += T) s_hist[i] = 0;
+    for (int i = tid; i <= NC; i += T) s_cc[i] = 0;
     if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; }
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
@@ -468,77 +491,76 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     uint32_t drops = 0, mask = 0;
     long long qmin = JMAX, qmax = JMIN, qnext = JMAX;
     const int lm = p.lanes - 1;
-    constexpr int R = kPart1Tile / kPart1Threads;   // 8
 
+    // record u of this thread in a tile: pair u / 2 at 2 * (tid + (u / 2) * T), element u & 1
+    auto li_of = [&](int u) -> int64_t { return 2 * ((int64_t)tid + (int64_t)(u >> 1) * T) + (u & 1); };
+    // loads of the tile at t0 (records past the segment's end are not loaded: tn < TILE)
+    auto load = [&](int64_t t0, longlong2 (&k2)[R / 2], longlong2 (&t2)[R / 2], longlong2 (&v2)[R / 2]) {
+        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
+        if (tn == TILE && p.vec) {
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                const int64_t i = t0 + li_of(2 * u);
+                k2[u] = *reinterpret_cast<const longlong2*>(p.key + i);
+                t2[u] = *reinterpret_cast<const longlong2*>(p.ts + i);
+                v2[u] = has_val ? *reinterpret_cast<const longlong2*>(p.val + i) : make_longlong2(0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                const int64_t l0 = li_of(2 * u);
+                k2[u] = t2[u] = v2[u] = make_longlong2(0, 0);
+                if (l0 < tn) {
+                    k2[u].x = p.key[t0 + l0]; t2[u].x = p.ts[t0 + l0];
+                    if (has_val) v2[u].x = p.val[t0 + l0];
+                }
+                if (l0 + 1 < tn) {
+                    k2[u].y = p.key[t0 + l0 + 1]; t2[u].y = p.ts[t0 + l0 + 1];
+                    if (has_val) v2[u].y = p.val[t0 + l0 + 1];
+                }
+            }
+        }
+    };
+    longlong2 ka[R / 2], ta[R / 2], va[R / 2];
+    if (beg < end) load(beg, ka, ta, va);
     int j = 0;
-    for (int64_t t0 = beg; t0 < end; t0 += kPart1Tile, j++) {
-        const int64_t tn = end - t0 < kPart1Tile ? end - t0 : kPart1Tile;
-        int64_t rk[R], rv[R];
+    for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
+        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
+        // 1) classify + rank the current tile (LDS atomics); keys become their mixes
         uint32_t rcr[R];   // (rank << 9) | coarse, 0xffffffff = not staged
-        auto account = [&](int64_t k, int64_t ts) -> uint32_t {
+        int64_t hk[R];
+        uint32_t nb = 0;   // NULL flags of the thread's records
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const int64_t li = li_of(u);
+            rcr[u] = 0xffffffffu;
+            hk[u] = 0;
+            if (li >= tn) continue;
+            const int64_t k = (u & 1) ? ka[u >> 1].y : ka[u >> 1].x;
+            const int64_t ts = (u & 1) ? ta[u >> 1].y : ta[u >> 1].x;
             int64_t q;
-            const int b = classify(p, k, ts, &q);
+            const int b = classify(p, k, ts, &q, &hk[u]);
             if (b >= 0) {
                 atomicAdd(&s_hist[b], 1u);
                 qmin = q < qmin ? q : qmin;
                 qmax = q > qmax ? q : qmax;
                 mask |= 1u << ((int)q & lm);
                 const uint32_t c = (uint32_t)b >> kFineBits;
-                return (atomicAdd(&s_cc[c], 1u) << 9) | c;
-            }
-            if (b == -1) {
+                rcr[u] = (atomicAdd(&s_cc[c], 1u) << 9) | c;
+                if (has_null && p.vnull[t0 + li]) nb |= 1u << u;
+            } else if (b == -1) {
                 drops++;
             } else {   // outside the slice filter: in the batch's slice range only
                 qmin = q < qmin ? q : qmin;
                 qmax = q > qmax ? q : qmax;
                 if (q >= p.filter_hi) qnext = q < qnext ? q : qnext;   // next occupied slice above the filter
             }
-            return 0xffffffffu;
-        };
-        if (tn == kPart1Tile && p.vec) {
-            longlong2 k2[R / 2], t2[R / 2];
-#pragma unroll
-            for (int u = 0; u < R / 2; u++) {
-                const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kPart1Threads);
-                k2[u] = *reinterpret_cast<const longlong2*>(p.key + i);
-                t2[u] = *reinterpret_cast<const longlong2*>(p.ts + i);
-            }
-#pragma unroll
-            for (int u = 0; u < R / 2; u++) {
-                rk[2 * u] = k2[u].x;
-                rk[2 * u + 1] = k2[u].y;
-                rcr[2 * u] = account(k2[u].x, t2[u].x);
-                rcr[2 * u + 1] = account(k2[u].y, t2[u].y);
-            }
-            if (has_val) {   // values are not needed until staging: their latency hides behind the scan
-#pragma unroll
-                for (int u = 0; u < R / 2; u++) {
-                    const int64_t i = t0 + 2 * ((int64_t)tid + (int64_t)u * kPart1Threads);
-                    const longlong2 v2 = *reinterpret_cast<const longlong2*>(p.val + i);
-                    rv[2 * u] = v2.x;
-                    rv[2 * u + 1] = v2.y;
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < R; u++) rv[u] = 0;
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < R; u++) {
-                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kPart1Threads) + (u & 1);
-                rk[u] = 0;
-                rcr[u] = 0xffffffffu;
-                if (li < tn) {
-                    rk[u] = p.key[t0 + li];
-                    rcr[u] = account(rk[u], p.ts[t0 + li]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < R; u++) {
-                const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kPart1Threads) + (u & 1);
-                rv[u] = has_val && li < tn ? p.val[t0 + li] : 0;
-            }
         }
+        int64_t rv[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) rv[u] = (u & 1) ? va[u >> 1].y : va[u >> 1].x;
+        // 2) prefetch the next tile: in flight across this tile's scan, staging and write-out
+        if (t0 + TILE < end) load(t0 + TILE, ka, ta, va);
         lds_barrier();
         {   // exclusive scan of the tile's coarse counts; the offsets go to the directory
             const uint32_t c = tid < NC ? s_cc[tid] : 0u;
@@ -549,30 +571,23 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
         }
         lds_barrier();
         uint16_t* drow = p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * (NC + 1);
-        for (int c = tid; c <= NC; c += kPart1Threads) drow[c] = (uint16_t)s_cc[c];
+        for (int c = tid; c <= NC; c += T) drow[c] = (uint16_t)s_cc[c];
         const uint32_t tile_total = s_cc[NC];
-        for (uint32_t lo = 0; lo < tile_total; lo += kRound) {
+        // 3) stage the tile coarse-bucket sorted, then write it back sequentially
 #pragma unroll
-            for (int u = 0; u < R; u++) {
-                if (rcr[u] == 0xffffffffu) continue;
-                const uint32_t slot = s_cc[rcr[u] & 511u] + (rcr[u] >> 9);
-                if (slot - lo >= (uint32_t)kRound) continue;
-                s_rec[slot - lo] = make_longlong2(rk[u], rv[u]);
-                if (has_null) {
-                    const int64_t li = 2 * ((int64_t)tid + (int64_t)(u >> 1) * kPart1Threads) + (u & 1);
-                    s_nul[slot - lo] = p.vnull[t0 + li];
-                }
-            }
-            lds_barrier();
-            const uint32_t hi = tile_total - lo < (uint32_t)kRound ? tile_total - lo : (uint32_t)kRound;
-            for (uint32_t i = tid; i < hi; i += kPart1Threads) {
-                p.tmp[t0 + lo + i] = s_rec[i];
-                if (has_null) p.tmp_null[t0 + lo + i] = s_nul[i];
-            }
-            if (lo + kRound < tile_total) lds_barrier();
+        for (int u = 0; u < R; u++) {
+            if (rcr[u] == 0xffffffffu) continue;
+            const uint32_t slot = s_cc[rcr[u] & 511u] + (rcr[u] >> 9);
+            s_rec[slot] = make_longlong2(hk[u], rv[u]);
+            if (has_null) s_nul[slot] = (uint8_t)((nb >> u) & 1u);
+        }
+        lds_barrier();
+        for (uint32_t i = tid; i < tile_total; i += T) {
+            p.tmp[t0 + i] = s_rec[i];
+            if (has_null) p.tmp_null[t0 + i] = s_nul[i];
         }
         lds_barrier();   // staging and the directory row have read the offsets
-        for (int c = tid; c <= NC; c += kPart1Threads) s_cc[c] = 0;
+        for (int c = tid; c <= NC; c += T) s_cc[c] = 0;
         lds_barrier();
     }
     // bookkeeping as in k_ingest_count
@@ -594,7 +609,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     __syncthreads();
     uint32_t lane_part = 0, bmax = 0;
     int lane_of = -1;
-    for (int b = tid; b < F; b += kPart1Threads) {
+    for (int b = tid; b < F; b += T) {
         const uint32_t c = s_hist[b];
         p.hist[(int64_t)blockIdx.x * F + b] = c;
         bmax = c > bmax ? c : bmax;
@@ -771,7 +786,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
         for (int u = 0; u < R; u++) {
             rf[u] = 0xffffffffu;
             if (base + (uint32_t)(u * kPart2Threads + tid) >= total) continue;
-            const uint32_t f = (uint32_t)(fmix64((uint64_t)cr[u].x) >> (64 - p.region_bits)) & (NF - 1);
+            const uint32_t f = (uint32_t)((uint64_t)cr[u].x >> (64 - p.region_bits)) & (NF - 1);   // staged mix
             rf[u] = (atomicAdd(&s_cnt[f], 1u) << 6) | f;
         }
         lds_barrier();
@@ -943,12 +958,12 @@ __global__ __launch_bounds__(kIngestThreads) void k_acc_scatter(IngestParams p, 
     seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
     for (int64_t i = beg + tid; i < end; i += kIngestThreads) {
         const int64_t k = p.key[i];
-        int64_t q;
-        const int b = classify(p, k, p.ts[i], &q);
+        int64_t q, h;
+        const int b = classify(p, k, p.ts[i], &q, &h);
         if (b < 0) continue;
         const uint32_t pos = atomicAdd(&s_cur[b], 1u);
         const int64_t cs = a.in_cnt_star[i];
-        a.key[pos] = k;
+        a.key[pos] = h;
         a.cnt_star[pos] = cs;
         a.cnt_null[pos] = cs - a.in_cnt_val[i];
         a.sum[pos] = a.in_sum[i];
@@ -1117,17 +1132,17 @@ struct LdsTableT<true> {
     uint32_t cs[kCompactSlots + 1];
 };
 
-// Home bucket: a multiplicative hash of the key (the region already selects keys by the top
-// bits of fmix64, independent of these bits) picks an aligned bucket of kBucket slots, read
-// with one 32-byte LDS access; probing is linear, slot by slot, from the bucket's first slot.
-// At the regions' load factor (<= ~0.35) a key sits in its home bucket ~99 % of the time,
-// against ~84 % for a single home slot, so a wave's lanes rarely leave the fast path.
+// Home bucket: the low 32 bits of the key's mix h (the region is its top bits; the low
+// word is independent of them) pick an aligned bucket of kBucket slots -- one 32-bit
+// multiply-high, no hashing in the merge -- read with one 32-byte LDS access; probing is
+// linear, slot by slot, from the bucket's first slot. At the regions' load factor (<= ~0.35)
+// a key sits in its home bucket ~99 % of the time, against ~84 % for a single home slot, so
+// a wave's lanes rarely leave the fast path.
 constexpr int kBucket = 4;
 template <bool C>
-__device__ __forceinline__ uint32_t lds_home(int64_t k) {
+__device__ __forceinline__ uint32_t lds_home(int64_t h) {
     constexpr uint32_t NB = (uint32_t)(MergeCfg<C>::kSlotsT / kBucket);
-    const uint64_t m = (uint64_t)k * 0x9E3779B97F4A7C15ull;
-    return (uint32_t)(((m >> 32) * (uint64_t)NB) >> 32) * kBucket;
+    return __umulhi((uint32_t)(uint64_t)h, NB) * kBucket;
 }
 
 // linear probe from `slot` (keys never leave the table during a region, so a key is at the
@@ -1182,9 +1197,9 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C>& t, int64_t k, uint3
 }
 // one fired row: key, window bounds, (DataStream) output timestamp and the aggregates of
 // the accumulator {COUNT(*), NULL count, sum} (a6: Count1/Count/Sum/AvgAggFunction)
-__device__ __forceinline__ void write_row(const MergeParams& p, unsigned long long o, int64_t key,
+__device__ __forceinline__ void write_row(const MergeParams& p, unsigned long long o, int64_t h,
                                           unsigned long long cs, unsigned long long cn, int64_t sum, int vt) {
-    p.out_key[o] = key;
+    p.out_key[o] = key_of(h);   // state holds the key's mix
     p.out_ws[o] = p.wstart;
     p.out_we[o] = p.wend;
     if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
@@ -1299,7 +1314,9 @@ struct MergeCursor {
     bool ok;         // settled on a chunk (false: walked past the regions whose ranges are known)
 };
 
-template <bool C>
+// VTC >= 0: the value op compiled in (kernel vt = val_type | op << 2: the LDS adds, identity and
+// row arithmetic of that op only -- a small straight-line stream loop); -1: read p.val_type
+template <bool C, int VTC>
 // waves_per_eu(4): 128 VGPRs, so two compact workgroups (16 waves) fit a CU
 __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_merge(MergeParams p) {
     constexpr int S = MergeCfg<C>::kSlotsT;
@@ -1320,7 +1337,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int cap = kRegionCap;
-    const int vt = p.val_type;
+    const int vt = VTC >= 0 ? VTC : p.val_type;
     const int64_t vinit = val_identity(vt);
     const int P = 1 << p.region_bits;
     const int G = gridDim.x;
@@ -1333,7 +1350,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     };
     // heavy regions are left to the heavy pass (no state read, nothing emitted or written)
     auto skipped = [&](int r) -> bool { return p.heavy != nullptr && gbl(p.heavy)[r] != 0; };
-    const bool fast = p.fast_stream != 0;
+    const bool fast = C || p.fast_stream != 0;   // the compact merge always streams plain staged records
     const int nb = p.n_batches;
 
     // fast path state
@@ -1367,7 +1384,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
         // the base comes back from LDS: cast to the global address space so these are
         // global_load_dwordx4 (a flat load is waited for with vmcnt(0) AND lgkmcnt(0),
         // serializing every LDS probe behind the loads in flight)
-        const GlobalRec rec = (GlobalRec)s_brec[m.j];
+        const GlobalRec rec = (GlobalRec)wave_uniform(s_brec[m.j]);   // the cursor is workgroup-uniform
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             const uint32_t i = m.i0 + u * T + tid;
@@ -1751,9 +1768,15 @@ hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {
     if (p.compact) {
         if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_merge<true>, dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p);
+        // the compact merge (the TUMBLE fire of plain staged records) per value op
+        switch (p.val_type) {
+            case 0: hipLaunchKernelGGL((k_merge<true, 0>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            case 1: hipLaunchKernelGGL((k_merge<true, 1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            case 2: hipLaunchKernelGGL((k_merge<true, 2>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            default: hipLaunchKernelGGL((k_merge<true, -1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+        }
     } else {
-        hipLaunchKernelGGL(k_merge<false>, dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+        hipLaunchKernelGGL((k_merge<false, -1>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     }
     return hipGetLastError();
 }
@@ -1951,7 +1974,7 @@ __global__ __launch_bounds__(256) void k_export(ExportParams p) {
     const uint64_t o = p.region_off[r];
     for (uint32_t i = threadIdx.x; i < n; i += 256) {
         const int64_t cs = base[kRegionCap + i], cn = base[2 * kRegionCap + i];
-        p.out_key[o + i] = base[i];
+        p.out_key[o + i] = key_of(base[i]);
         p.out_slice[o + i] = p.slice_end;
         p.out_cnt_star[o + i] = cs;
         p.out_cnt_val[o + i] = cs - cn;

@@ -212,6 +212,9 @@ __host__ __device__ __forceinline__ bool target_slice(const WindowSpec& w, int64
 }
 
 // 64-bit finalizer (MurmurHash3 fmix64): bijective, spreads keys over state regions.
+// Device state keeps every key as its mix h = fmix64(key): the top region_bits of h pick
+// the state region, the low 32 bits the LDS home bucket, and no kernel past ingest hashes
+// a key again; rows and images leaving the engine carry fmix64_inv(h) = the key.
 __host__ __device__ __forceinline__ uint64_t fmix64(uint64_t h) {
     h ^= h >> 33;
     h *= 0xff51afd7ed558ccdULL;
@@ -220,6 +223,17 @@ __host__ __device__ __forceinline__ uint64_t fmix64(uint64_t h) {
     h ^= h >> 33;
     return h;
 }
+// inverse of fmix64 (x ^= x >> 33 is an involution; the multipliers' inverses mod 2^64)
+__host__ __device__ __forceinline__ uint64_t fmix64_inv(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0x9cb4b2f8129337dbULL;
+    h ^= h >> 33;
+    h *= 0x4f74430c22a54005ULL;
+    h ^= h >> 33;
+    return h;
+}
+__host__ __device__ __forceinline__ int64_t key_of(int64_t h) { return (int64_t)fmix64_inv((uint64_t)h); }
+__host__ __device__ __forceinline__ int64_t mix_of(int64_t key) { return (int64_t)fmix64((uint64_t)key); }
 
 // ---- Flink key groups (KeyGroupRangeAssignment.java:63-77, MathUtils.java:137-155,194-201,
 //      MurmurHashUtils.java hashBytes over the 16-byte BinaryRowData of one BIGINT) ----------
