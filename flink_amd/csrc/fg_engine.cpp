@@ -62,6 +62,10 @@ struct DevBuf {
     }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
+    void swap(DevBuf& o) {
+        std::swap(p, o.p);
+        std::swap(bytes, o.bytes);
+    }
 };
 
 struct HostBuf {   // pinned host memory
@@ -95,7 +99,8 @@ struct SliceTable {
 // One ingest pass: the bucket scan of its records over all lanes; lane l's records sit at
 // [lane_start[l], lane_start[l] + lane_n[l]) of lane l's staged area.
 struct Staged {
-    DevBuf bucket_off;    // F + 1 uint32 (lane-major)
+    DevBuf bucket_off;    // F + 1 uint32 (lane-major), F = lanes << bits
+    int bits = 0;         // region bits the pass was bucketed at (the regions may split later)
     bool is_acc = false;  // accumulator rows (global phase) in the lanes' accumulator areas
     int64_t lane_start[kMaxLanes] = {0, 0, 0, 0};
     int64_t lane_n[kMaxLanes] = {0, 0, 0, 0};
@@ -154,6 +159,33 @@ struct PendingEv {
     int cls;
     hipEvent_t a, b;
     int64_t records;
+};
+
+// Capacity growth (the BytesMap analogue: BytesMap.java:229-290 doubles its bucket area when
+// full; RecordsWindowBuffer.java:89-96 flushes and retries on EOFException). A state region
+// holds at most kRegionCap entries in HBM and its LDS table kSlots keys; a region that
+// overflows in a merge emits and writes nothing and is reported in the fail list. Every
+// merge launch is kept as a job (inputs by reference) until the synchronization that
+// follows it: then the regions split (2^b -> 2^(b+1), the slice tables re-laid by
+// k_split_table, staged passes read through their coarser buckets) and exactly the failed
+// regions' children are merged again, until none fails.
+constexpr int kMaxRegionBits = 13;
+constexpr int kFailCap = 1 << 16;
+struct JobBatch {
+    Staged* s = nullptr;   // a staged pass (lane `lane`) ...
+    int lane = 0;
+    StagedBatch ext{};     // ... or an explicit batch (restore image) bucketed at ext_bits
+    int ext_bits = 0;
+};
+struct SliceTable;
+struct MergeJob {
+    std::vector<JobBatch> batches;
+    std::vector<SliceTable*> srcs;
+    SliceTable* dst = nullptr;
+    bool emit = false;
+    int64_t wend = 0;
+    int bits = 0;          // region bits of its last launch
+    int kclass = 0;
 };
 
 }  // namespace
@@ -1990,11 +2022,21 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         if (rc) return rc;
         t->upper = std::min<int64_t>(t->upper + m, (int64_t)kRegionCap * h->P);
     }
-    // open(): processor progress restarts at Long.MIN_VALUE; windows whose timers fired
-    // before the checkpoint stay fired (restored timer set)
+    // open(): processor progress restarts at Long.MIN_VALUE, and so does the restored timer
+    // service's watermark (InternalTimerServiceImpl.currentWatermark is not part of the
+    // snapshot): a record older than the checkpoint's watermark is not late, its flush
+    // registers a timer (AggCombiner step 5 checks isWindowFired against the timer
+    // watermark) and the window fires again on the next watermark.
+    // Unshared slices (TUMBLE, windowed inputs): every restored (key, slice) entry holds a
+    // pending timer (a fired slice is cleared), so firing every window with state whose
+    // trigger is <= the watermark is exactly the timers that fire -- the timer watermark
+    // restarts at Long.MIN_VALUE here too.
+    // Shared slices (HOP, CUMULATE, DataStream sliding): restored slices may also belong to
+    // windows that fired before the checkpoint, for keys without pending timers, so the
+    // checkpoint's timer watermark is kept (divergence 2).
     h->current_progress = JMIN;
     h->next_trigger = JMIN;
-    h->timer_wm = timer_watermark;
+    h->timer_wm = h->w.kind == TUMBLE ? JMIN : timer_watermark;
     return FG_OK;
 }
 

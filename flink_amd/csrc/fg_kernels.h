@@ -63,6 +63,11 @@ struct StagedBatch {
     const uint32_t* bucket_off;
     int32_t is_acc;
     int32_t stride;            // int64 words per record (1 or 2)
+    // regions split since the batch was staged (MergeParams.region_bits - the batch's bits):
+    // region r's records are those of bucket r >> shift whose key mix lies in region r
+    // (general merge path only)
+    int32_t shift;
+    int32_t pad0;
 };
 
 struct IngestParams {
@@ -154,8 +159,21 @@ struct MergeParams {
     const int64_t* part_cs;
     const int64_t* part_cn;
     const int64_t* part_sum;
-    const uint32_t* part_n;    // entries per chunk
+    const uint32_t* part_n;    // entries per chunk (kChunkFailed: the chunk's table overflowed)
+    // Region overflow (LDS table full, or more than kRegionCap entries for a table write): the
+    // region emits and writes nothing, and (job << kFailJobShift | region) is appended to
+    // fail_list, so the host can split the regions and redo exactly the failed ones
+    // (BytesMap growth, BytesMap.java:229-290). A retry launch names its regions in retry_list.
+    uint32_t* fail_list;
+    uint32_t* fail_n;
+    int32_t fail_cap;
+    int32_t job;
+    const int32_t* retry_list;
+    int32_t n_retry;
+    int32_t pad2;
 };
+constexpr int kFailJobShift = 14;             // region < 2^13
+constexpr uint32_t kChunkFailed = 0xFFFFFFFFu;
 
 // Skewed regions (Zipf hot keys): a region whose staged records exceed `threshold` is
 // merged in chunks of `chunk` records by k_heavy_chunks (one LDS table per chunk, with a
@@ -239,6 +257,10 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
 // fire one window straight from a single slice table (no combine): p's emit fields
 hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_t s);
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
+// region split: the table `src` at old_bits -> `dst` at old_bits + shift (each region's
+// entries go to its 2^shift child regions by the next bits of their key mix)
+hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift,
+                              hipStream_t s);
 hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s);
 hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s);
 constexpr int kMaxOwnerCols = 8;

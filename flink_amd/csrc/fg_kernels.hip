@@ -1341,12 +1341,12 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     const int64_t vinit = val_identity(vt);
     const int P = 1 << p.region_bits;
     const int G = gridDim.x;
-    // regions: all P (strided over the grid), or the heavy pass's list
-    const int NR = p.region_list ? *gbl(p.n_list) : P;
+    // regions: all P (strided over the grid), the heavy pass's list, or a retry's list
+    const int NR = p.region_list ? *gbl(p.n_list) : p.retry_list ? p.n_retry : P;
     const int nreg = ((int)blockIdx.x < NR) ? (NR - 1 - (int)blockIdx.x) / G + 1 : 0;
     auto region_at = [&](int ri) -> int {
         const int x = (int)blockIdx.x + ri * G;
-        return p.region_list ? gbl(p.region_list)[x] : x;
+        return p.region_list ? gbl(p.region_list)[x] : p.retry_list ? gbl(p.retry_list)[x] : x;
     };
     // heavy regions are left to the heavy pass (no state read, nothing emitted or written)
     auto skipped = [&](int r) -> bool { return p.heavy != nullptr && gbl(p.heavy)[r] != 0; };
@@ -1605,6 +1605,10 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 const int c0 = gbl(p.chunk0)[li], c1 = gbl(p.chunk0)[li + 1];
                 for (int c = c0; c < c1; c++) {
                     const uint32_t n = gbl(p.part_n)[c];
+                    if (n == kChunkFailed) {   // the chunk's table overflowed: the region fails
+                        full = true;
+                        continue;
+                    }
                     const int64_t at = (int64_t)c * kPartStride;
                     for (uint32_t i = tid; i < n; i += T) {
                         const int slot = lds_find_or_insert<C>(t, gbl(p.part_key)[at + i], full);
@@ -1618,13 +1622,19 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 const StagedBatch sb = p.batches[j];
                 const auto bo = gbl(sb.bucket_off);
                 const uint32_t b0 = bo[0];
-                const uint32_t beg = bo[r] - b0;
-                const uint32_t end = bo[r + 1] - b0;
+                // a batch staged before the regions split: its bucket r >> shift holds region
+                // r's records among its siblings' (keys are staged as their mix, whose top
+                // region_bits are the region)
+                const int sh = sb.shift;
+                const uint32_t beg = bo[r >> sh] - b0;
+                const uint32_t end = bo[(r >> sh) + 1] - b0;
+                auto mine = [&](int64_t h) { return sh == 0 || (int)((uint64_t)h >> (64 - p.region_bits)) == r; };
                 const auto srec = gbl(sb.rec);
                 const auto vnull = sb.vnull != nullptr ? gbl(sb.vnull) : nullptr;
                 if (sb.is_acc) {
                     const auto cst = gbl(sb.cnt_star), cnl = gbl(sb.cnt_null), sval = gbl(sb.val);
                     for (uint32_t i = beg + tid; i < end; i += T) {
+                        if (!mine(srec[i])) continue;
                         const int slot = lds_find_or_insert<C>(t, srec[i], full);
                         if (slot >= 0)
                             lds_add<C>(t, slot, (unsigned long long)cst[i], (unsigned long long)cnl[i], sval[i], vt);
@@ -1633,6 +1643,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     const GlobalRec rec = (GlobalRec)sb.rec;
                     for (uint32_t i = beg + tid; i < end; i += T) {
                         const RecV2 rc = rec[i];
+                        if (!mine(rc.x)) continue;
                         const int slot = lds_find_or_insert<C>(t, rc.x, full);
                         if (slot < 0) continue;
                         const bool isnull = vnull != nullptr && vnull[i] != 0;
@@ -1640,6 +1651,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     }
                 } else {
                     for (uint32_t i = beg + tid; i < end; i += T) {
+                        if (!mine(srec[i])) continue;
                         const int slot = lds_find_or_insert<C>(t, srec[i], full);
                         if (slot < 0) continue;
                         const bool isnull = vnull != nullptr && vnull[i];
@@ -1685,7 +1697,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             if (lane == 0) {
                 unsigned int fl = s_flags;
                 if (p.has_dst && total > (uint32_t)cap) fl |= 1u;
-                if (p.emit) {
+                if (p.emit && !(fl & 5u)) {   // (a failed region reserves no rows)
                     const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
                     s_out_base = ob;
                     if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
@@ -1693,13 +1705,17 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 s_flags = fl;
                 s_total = total;
                 if (fl) atomicOr(p.overflow, fl);
+                if ((fl & 5u) && p.fail_list) {   // the region does nothing; the host redoes it split
+                    const uint32_t at = atomicAdd(p.fail_n, 1u);
+                    if (at < (uint32_t)p.fail_cap) p.fail_list[at] = ((uint32_t)p.job << kFailJobShift) | (uint32_t)r;
+                }
             }
         }
         lds_barrier();
         MSTAMP(2);   // compaction + scan + barriers
         const unsigned int fl = s_flags;
-        const bool write_dst = !skip && p.has_dst && !(fl & 1u) && !(fl & 4u);
-        const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 2u) && !(fl & 4u);
+        const bool write_dst = !skip && p.has_dst && !(fl & 5u);
+        const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 7u);
         int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
         const unsigned long long obase = s_out_base;
         // per round: the wave's occupied lanes below this lane give the rank within the group
@@ -1946,7 +1962,8 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
         }
         lds_barrier();
         if (tid == 0) {
-            hp.part_n[c] = s_n;
+            // an overflowed chunk fails its region in the heavy pass (which then redoes it split)
+            hp.part_n[c] = s_full ? kChunkFailed : s_n;
             if (s_full) atomicOr(hp.overflow, 4u);
         }
         lds_barrier();   // the table is cleared for the next chunk
@@ -1984,6 +2001,44 @@ __global__ __launch_bounds__(256) void k_export(ExportParams p) {
 
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s) {
     hipLaunchKernelGGL(k_export, dim3(regions), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------------
+// region split (capacity growth): one workgroup per old region appends each entry to the
+// child region named by the next `shift` bits of its key mix (a child holds a subset of its
+// parent, so it never exceeds kRegionCap); entry order inside a region is irrelevant (the
+// merge rebuilds its LDS table from the entries)
+// ----------------------------------------------------------------------------------------
+constexpr int kSplitThreads = 256;
+__global__ __launch_bounds__(kSplitThreads) void k_split_table(TableRef src, TableRef dst, int32_t old_bits,
+                                                               int32_t shift) {
+    __shared__ uint32_t s_cnt[1 << 13];
+    const int r = blockIdx.x;
+    const int nch = 1 << shift;
+    const int new_bits = old_bits + shift;
+    for (int c = threadIdx.x; c < nch; c += kSplitThreads) s_cnt[c] = 0;
+    __syncthreads();
+    const uint32_t n = gbl(src.counts)[r];
+    const auto sb = gbl(src.base + (int64_t)r * 4 * kRegionCap);
+    for (uint32_t i = threadIdx.x; i < n; i += kSplitThreads) {
+        const int64_t h = sb[i];
+        const int c = (int)(((uint64_t)h >> (64 - new_bits)) & (uint64_t)(nch - 1));
+        const uint32_t at = atomicAdd(&s_cnt[c], 1u);
+        int64_t* db = dst.base + ((int64_t)r * nch + c) * 4 * kRegionCap;
+        db[at] = h;
+        db[kRegionCap + at] = sb[kRegionCap + i];
+        db[2 * kRegionCap + at] = sb[2 * kRegionCap + i];
+        db[3 * kRegionCap + at] = sb[3 * kRegionCap + i];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nch; c += kSplitThreads) dst.counts[(int64_t)r * nch + c] = s_cnt[c];
+}
+
+hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift,
+                              hipStream_t s) {
+    if (shift < 1 || old_bits < 0 || old_bits + shift > 13) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_split_table, dim3(1u << old_bits), dim3(kSplitThreads), 0, s, src, dst, old_bits, shift);
     return hipGetLastError();
 }
 

@@ -272,10 +272,52 @@ def test_lane_conflict_slow_path_two_pass(oracle_mod):
 
 @pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
 def test_snapshot_restore_many_regions(oracle_mod, kind):
-    # jitter < watermark delay: no record older than the checkpoint's watermark arrives after
-    # the restore (that case re-fires windows in the reference -- DESIGN.md section 3, divergence 2)
+    # TUMBLE: jitter > watermark delay, so records older than the checkpoint's watermark arrive
+    # after the restore and re-fire their windows, as in the reference. HOP / CUMULATE keep
+    # jitter < delay: their re-fire is DESIGN.md section 3, divergence 2.
     cfg = cfg_of(kind, 4000, 0 if kind == "tumble" else 1000)
-    drive_both(oracle_mod, cfg, n=400_000, keys=100_000, batch=20_000, delay=100, jitter=80, snapshot_at=9)
+    drive_both(oracle_mod, cfg, n=400_000, keys=100_000, batch=20_000, delay=100,
+               jitter=1500 if kind == "tumble" else 80, snapshot_at=9)
+
+
+@pytest.mark.parametrize("mode", ["sql", "datastream"])
+def test_restore_refires_old_windows(oracle_mod, mode):
+    """After initializeState the timer service restarts at Long.MIN_VALUE: rows older than the
+    checkpoint's watermark are not late and fire their (already fired) window again on the next
+    watermark (SlicingWindowAggOperatorTest.java:173-184 restores mid-stream; the oracle replays
+    the restored timer heap, oracle.c or_restore_copy)."""
+    cfg = cfg_of("tumble", 1000, vt="i64", mode=mode)
+    g = gpu_mk(cfg, expected_keys=300, buffer_records=1 << 16)
+    o = oracle_mk(oracle_mod, cfg)
+    rng = np.random.default_rng(7)
+    k1 = rng.integers(0, 300, 5000).astype(np.int64)
+    t1 = rng.integers(0, 5000, 5000).astype(np.int64)
+    v1 = rng.integers(-50, 50, 5000).astype(np.int64)
+    for op in (g, o):
+        op.process_batch(k1, t1, v1)
+        op.process_watermark(2999)
+    assert_rows_equal(g.take_rows(), o.take_rows(), "i64", "before checkpoint")
+    for op in (g, o):
+        op.prepare_snapshot()
+    g2, o2 = g.restore_copy(), o.restore_copy()
+    g.close()
+    o.close()
+    # after the restore: rows of windows [0, 3000) that fired before the checkpoint, and newer ones
+    k2 = rng.integers(0, 300, 4000).astype(np.int64)
+    t2 = rng.integers(0, 7000, 4000).astype(np.int64)
+    v2 = rng.integers(-50, 50, 4000).astype(np.int64)
+    for op in (g2, o2):
+        op.process_batch(k2, t2, v2)
+        op.process_watermark(4999)
+    got, exp = g2.take_rows(), o2.take_rows()
+    assert (exp["window_end"] <= 3000).any()   # the old windows did fire again
+    assert_rows_equal(got, exp, "i64", "first watermark after restore")
+    assert g2.late_dropped == o2.late_dropped
+    for op in (g2, o2):
+        op.process_watermark(JMAX)
+    assert_rows_equal(g2.take_rows(), o2.take_rows(), "i64", "final")
+    g2.close()
+    o2.close()
 
 
 def test_count_star_only_many_regions(oracle_mod):
