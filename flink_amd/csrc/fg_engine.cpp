@@ -40,6 +40,9 @@ thread_local std::string g_open_error;
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;   // one owner per device allocation
+    DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
@@ -94,6 +97,7 @@ struct SliceTable {
     DevBuf data;          // P * 4 * kRegionCap int64
     DevBuf counts;        // P uint32
     int64_t upper = 0;    // host-side upper bound of entries
+    int bits = 0;         // region bits of its layout
 };
 
 // One ingest pass: the bucket scan of its records over all lanes; lane l's records sit at
@@ -171,13 +175,14 @@ struct PendingEv {
 // regions' children are merged again, until none fails.
 constexpr int kMaxRegionBits = 13;
 constexpr int kFailCap = 1 << 16;
+constexpr int64_t kStateCapMax = (int64_t)kRegionCap << kMaxRegionBits;   // entries of a slice at most
+constexpr int kDefaultRegionBits = 10;   // no key-count hint
 struct JobBatch {
     Staged* s = nullptr;   // a staged pass (lane `lane`) ...
     int lane = 0;
     StagedBatch ext{};     // ... or an explicit batch (restore image) bucketed at ext_bits
     int ext_bits = 0;
 };
-struct SliceTable;
 struct MergeJob {
     std::vector<JobBatch> batches;
     std::vector<SliceTable*> srcs;
@@ -246,6 +251,15 @@ struct fg_handle {
     // resident state
     std::map<int64_t, std::unique_ptr<SliceTable>> tables;
     std::vector<std::unique_ptr<SliceTable>> table_pool;
+    // capacity growth: merge launches since the last synchronization (job id = index),
+    // tables freed meanwhile (a job may still read them), the fail list of overflowed regions
+    std::vector<MergeJob> jobs;
+    std::vector<std::unique_ptr<SliceTable>> deferred;
+    bool defer_free = false;
+    DevBuf fail_list;
+    HostBuf h_fail;
+    int lanes_target = 0;   // lanes for the current region bits (reached once the upper lanes drain)
+    int64_t grows = 0;
 
     // descriptor arena (device + pinned mirror), reset at every sync point
     DevBuf arena;
@@ -402,6 +416,7 @@ int table_get(fg_handle* h, int64_t slice_end, bool create, SliceTable** out) {
     HIPCHK(h, hipMemsetAsync(t->counts.p, 0, sizeof(uint32_t) * h->P, h->stream));
     t->slice_end = slice_end;
     t->upper = 0;
+    t->bits = h->region_bits;
     *out = t.get();
     h->tables[slice_end] = std::move(t);
     return FG_OK;
@@ -410,22 +425,212 @@ int table_get(fg_handle* h, int64_t slice_end, bool create, SliceTable** out) {
 void table_free(fg_handle* h, int64_t slice_end) {
     auto it = h->tables.find(slice_end);
     if (it == h->tables.end()) return;
-    h->table_pool.push_back(std::move(it->second));
+    // a merge launched since the last synchronization may still need it (region retry)
+    if (h->defer_free) h->deferred.push_back(std::move(it->second));
+    else h->table_pool.push_back(std::move(it->second));
     h->tables.erase(it);
 }
 
 TableRef ref_of(SliceTable* t) { return TableRef{t->data.as<int64_t>(), t->counts.as<uint32_t>()}; }
 
+// device scalars: [0] overflow flags (u32), [8] fired-row counter (u64), [16] fail count (u32)
+constexpr size_t kScalarBytes = 24;
+uint32_t fail_count(const fg_handle* h) { return h->h_scalars.as<uint32_t>()[4]; }
+
 int check_overflow(fg_handle* h) {
+    // region overflows (bits 0 and 2) are handled by the fail list (settle_jobs)
     unsigned int fl = h->h_scalars.as<unsigned int>()[0];
-    if (fl & 4u)
-        return h->fail(FG_ECAPACITY, "state region hash table full (%d slots): raise fg_config.expected_keys",
-                       kSlots);
-    if (fl & 1u)
-        return h->fail(FG_ECAPACITY, "state region overflow (> %d entries per region): raise fg_config.expected_keys",
-                       kRegionCap);
     if (fl & 2u) return h->fail(FG_EDEVICE, "internal: fired-row buffer overflow");
     return FG_OK;
+}
+
+int lanes_for(int bits) {
+    // lanes x regions bounded by the count histogram and, for the two-pass partition, by
+    // pass 1's LDS histogram
+    int lanes = kMaxLanes;
+    while (lanes > 1 && (lanes << bits) > kMaxStageBuckets) lanes >>= 1;
+    while (lanes > 2 && bits >= kFineBits && (lanes << bits) > kMaxPart1Fine) lanes >>= 1;
+    return lanes;
+}
+
+// A new job set starts after every synchronization: zero its fail count.
+int job_add(fg_handle* h, MergeJob&& j, int* id) {
+    if (h->jobs.empty()) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 16, 0, 8, h->stream));
+    j.bits = h->region_bits;
+    h->jobs.push_back(std::move(j));
+    *id = (int)h->jobs.size() - 1;
+    return FG_OK;
+}
+
+StagedBatch batch_of(const fg_handle* h, const JobBatch& jb) {
+    StagedBatch b{};
+    if (!jb.s) {
+        b = jb.ext;
+        b.shift = h->region_bits - jb.ext_bits;
+        return b;
+    }
+    const Staged* s = jb.s;
+    const int l = jb.lane;
+    b.bucket_off = s->bucket_off.as<uint32_t>() + ((int64_t)l << s->bits);
+    if (s->is_acc) {
+        const int64_t at = (int64_t)l * h->acc_cap + s->lane_start[l];
+        b.is_acc = 1;
+        b.stride = 1;
+        b.rec = h->acc_key.as<int64_t>() + at;
+        b.cnt_star = h->acc_cs.as<int64_t>() + at;
+        b.cnt_null = h->acc_cn.as<int64_t>() + at;
+        b.val = h->acc_sum.as<int64_t>() + at;
+    } else {
+        b.rec = h->st_rec.as<int64_t>() + ((int64_t)l * h->lane_cap + s->lane_start[l]) * h->st_stride;
+        b.vnull = s->has_null ? h->st_null.as<uint8_t>() + (int64_t)l * h->lane_cap + s->lane_start[l] : nullptr;
+        b.stride = h->st_stride;
+    }
+    b.shift = h->region_bits - s->bits;
+    return b;
+}
+
+void fill_emit(fg_handle* h, MergeParams& p, int64_t wend);
+
+// MergeParams of job `ji` at the current region bits (the general path; callers pick the
+// fast variants on a first launch)
+int job_params(fg_handle* h, int ji, MergeParams* p) {
+    const MergeJob& j = h->jobs[(size_t)ji];
+    std::vector<StagedBatch> sb;
+    for (const JobBatch& jb : j.batches) sb.push_back(batch_of(h, jb));
+    std::vector<TableRef> srcs;
+    for (SliceTable* t : j.srcs) srcs.push_back(ref_of(t));
+    *p = MergeParams{};
+    p->region_bits = h->region_bits;
+    p->n_src = (int)srcs.size();
+    if (!srcs.empty()) {
+        int rc = arena_put(h, srcs.data(), srcs.size(), &p->src);
+        if (rc) return rc;
+    }
+    p->n_batches = (int)sb.size();
+    if (!sb.empty()) {
+        int rc = arena_put(h, sb.data(), sb.size(), &p->batches);
+        if (rc) return rc;
+    }
+    p->val_type = h->kvt;
+    p->has_dst = j.dst ? 1 : 0;
+    if (j.dst) p->dst = ref_of(j.dst);
+    if (j.emit) fill_emit(h, *p, j.wend);
+    p->overflow = h->scalars.as<unsigned int>();
+    p->out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+    p->fail_list = h->fail_list.as<uint32_t>();
+    p->fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 16);
+    p->fail_cap = kFailCap;
+    p->job = ji;
+    return FG_OK;
+}
+
+// Split every slice table's regions 2^b -> 2^nb (k_split_table). Staged passes keep their
+// bucketing (the merge reads a region's records through its parent bucket); new passes
+// bucket at nb. The slice lanes stay until the lanes above lanes_for(nb) drain.
+int grow(fg_handle* h, int nb) {
+    const int sh = nb - h->region_bits;
+    if (sh <= 0) return FG_OK;
+    if (nb > kMaxRegionBits) return h->fail(FG_ECAPACITY, "internal: region bits above %d", kMaxRegionBits);
+    const int64_t P2 = (int64_t)1 << nb;
+    std::vector<std::unique_ptr<DevBuf>> old;   // freed once the split kernels are done
+    auto split = [&](SliceTable* t) -> int {
+        std::unique_ptr<DevBuf> nd(new DevBuf()), nc(new DevBuf());
+        HIPCHK(h, nd->ensure(sizeof(int64_t) * 4 * (size_t)kRegionCap * P2));
+        HIPCHK(h, nc->ensure(sizeof(uint32_t) * P2));
+        HIPCHK(h, launch_split_table(ref_of(t), TableRef{nd->as<int64_t>(), nc->as<uint32_t>()}, t->bits,
+                                     nb - t->bits, h->stream));
+        t->data.swap(*nd);
+        t->counts.swap(*nc);
+        t->bits = nb;
+        old.push_back(std::move(nd));
+        old.push_back(std::move(nc));
+        return FG_OK;
+    };
+    int rc;
+    for (auto& kv : h->tables)
+        if ((rc = split(kv.second.get()))) return rc;
+    for (auto& t : h->deferred)
+        if ((rc = split(t.get()))) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    old.clear();
+    h->table_pool.clear();   // pooled tables have the old layout
+    h->region_bits = nb;
+    h->P = 1 << nb;
+    h->lanes_target = lanes_for(nb);
+    h->F = h->lanes << nb;
+    // (the ingest scratch grows at the next pass: a pass in progress keeps its buffers)
+    h->grows++;
+    return FG_OK;
+}
+
+int merge_grid(const fg_handle* h);
+
+// After the synchronization that follows a job set (h_scalars read back): while regions
+// failed, split the regions and redo exactly the failed ones' children. The jobs' inputs
+// (staged lanes, tables) are untouched until this returns.
+int retry_failed(fg_handle* h) {
+    while (!h->jobs.empty() && fail_count(h) > 0) {
+        const uint32_t nf = fail_count(h);
+        if (nf > (uint32_t)kFailCap) return h->fail(FG_ECAPACITY, "internal: %u failed regions in one merge set", nf);
+        if (h->region_bits >= kMaxRegionBits)
+            return h->fail(FG_ECAPACITY,
+                           "state region overflow at %d regions (> %d distinct keys of one region in a slice): "
+                           "more keys per subtask than one operator holds; raise the parallelism",
+                           1 << kMaxRegionBits, kRegionCap);
+        HIPCHK(h, h->h_fail.ensure(4 * (size_t)nf));
+        HIPCHK(h, hipMemcpyAsync(h->h_fail.p, h->fail_list.p, 4 * (size_t)nf, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        std::map<int, std::vector<int32_t>> per_job;
+        for (uint32_t i = 0; i < nf; i++) {
+            const uint32_t e = h->h_fail.as<uint32_t>()[i];
+            per_job[(int)(e >> kFailJobShift)].push_back((int32_t)(e & ((1u << kFailJobShift) - 1)));
+        }
+        int rc = grow(h, h->region_bits + 1);
+        if (rc) return rc;
+        h->arena_used = 0;
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 4, h->stream));                    // flags
+        HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 16, 0, 8, h->stream));     // fail count
+        for (auto& kv : per_job) {
+            MergeJob& j = h->jobs[(size_t)kv.first];
+            const int sh = h->region_bits - j.bits;
+            std::vector<int32_t> regs;
+            for (int32_t r : kv.second)
+                for (int c = 0; c < (1 << sh); c++) regs.push_back((r << sh) | c);
+            j.bits = h->region_bits;
+            MergeParams p{};
+            rc = job_params(h, kv.first, &p);
+            if (rc) return rc;
+            rc = arena_put(h, regs.data(), regs.size(), &p.retry_list);
+            if (rc) return rc;
+            p.n_retry = (int)regs.size();
+            KTimer kt(h, j.kclass, 0);
+            HIPCHK(h, launch_merge(p, std::min<int>((int)regs.size(), merge_grid(h)), h->stream));
+        }
+        HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, kScalarBytes, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->arena_used = 0;
+    }
+    return FG_OK;
+}
+int settle_jobs(fg_handle* h) {
+    const int rc = retry_failed(h);
+    h->jobs.clear();
+    // tables freed while the jobs ran go back to the pool (or away, after a split)
+    for (auto& t : h->deferred)
+        if (t->bits == h->region_bits) h->table_pool.push_back(std::move(t));
+    h->deferred.clear();
+    return rc;
+}
+
+// Reduce the slice lanes to lanes_for(region bits) once the lanes above it hold nothing
+// (after a split to 2^13 regions, two lanes keep the two-pass partition).
+void maybe_reduce_lanes(fg_handle* h) {
+    if (h->lanes_target <= 0 || h->lanes_target >= h->lanes) return;
+    for (int l = h->lanes_target; l < h->lanes; l++)
+        if (h->lane[l].q != kEmptyLane) return;
+    h->lanes = h->lanes_target;
+    h->F = h->lanes << h->region_bits;
+    h->q_guess = kEmptyLane;
 }
 
 int ensure_out(fg_handle* h, int64_t need);
@@ -480,8 +685,6 @@ int64_t min_staged_slice_end(const fg_handle* h) {
         if (h->lane[l].q != kEmptyLane) m = std::min(m, slice_end_of(h, h->lane[l].q));
     return m;
 }
-int64_t* lane_rec(const fg_handle* h, int l) { return h->st_rec.as<int64_t>() + (int64_t)l * h->lane_cap * h->st_stride; }
-uint8_t* lane_null(const fg_handle* h, int l) { return h->st_null.as<uint8_t>() + (int64_t)l * h->lane_cap; }
 
 // empty lane l; a pass returns to the pool once no lane holds its records
 void release_lane(fg_handle* h, int l) {
@@ -565,28 +768,6 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     for (int l : sel) {
         const Lane& ln = h->lane[l];
         const int64_t se = slice_end_of(h, ln.q);
-        std::vector<StagedBatch> sb;
-        for (Staged* s : ln.passes) {
-            StagedBatch b{};
-            b.bucket_off = s->bucket_off.as<uint32_t>() + ((int64_t)l << h->region_bits);
-            if (s->is_acc) {
-                const int64_t at = (int64_t)l * h->acc_cap + s->lane_start[l];
-                b.is_acc = 1;
-                b.stride = 1;
-                b.rec = h->acc_key.as<int64_t>() + at;
-                b.cnt_star = h->acc_cs.as<int64_t>() + at;
-                b.cnt_null = h->acc_cn.as<int64_t>() + at;
-                b.val = h->acc_sum.as<int64_t>() + at;
-            } else {
-                b.rec = lane_rec(h, l) + s->lane_start[l] * h->st_stride;
-                b.vnull = s->has_null ? lane_null(h, l) + s->lane_start[l] : nullptr;
-                b.stride = h->st_stride;
-            }
-            sb.push_back(b);
-        }
-        const StagedBatch* d_sb = nullptr;
-        rc = arena_put(h, sb.data(), sb.size(), &d_sb);
-        if (rc) return rc;
         SliceTable* t = nullptr;
         rc = table_get(h, se, true, &t);
         if (rc) return rc;
@@ -608,8 +789,9 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         }
         SliceTable* F = nullptr;       // first slice's table of W's cumulative window
         SliceTable* dstt = t;          // table written by this merge (null: none)
-        std::vector<TableRef> srcs;
-        if (t->upper > 0) srcs.push_back(ref_of(t));
+        MergeJob job;
+        for (Staged* s : ln.passes) job.batches.push_back(JobBatch{s, l, StagedBatch{}, 0});
+        if (t->upper > 0) job.srcs.push_back(t);
         int64_t cum_first = 0, cum_last = 0;
         if (cum_fire) {
             const int64_t ws = window_start(h->w, se);
@@ -618,15 +800,15 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             if (se != cum_first) {
                 rc = table_get(h, cum_first, se != cum_last, &F);
                 if (rc) return rc;
-                if (F && F->upper > 0) srcs.push_back(ref_of(F));
+                if (F && F->upper > 0) job.srcs.push_back(F);
             }
             dstt = se == cum_last ? nullptr : (se == cum_first ? t : F);
         } else if (fire_now) {
             dstt = nullptr;
         }
         int64_t ub_in = ln.fill + ln.acc_fill;
-        for (const TableRef& r : srcs) ub_in += r.base == t->data.as<int64_t>() ? t->upper : (F ? F->upper : 0);
-        const int64_t ub = std::min<int64_t>(ub_in, (int64_t)kRegionCap * h->P);
+        for (SliceTable* r : job.srcs) ub_in += r->upper;
+        const int64_t ub = std::min<int64_t>(ub_in, kStateCapMax);
         if (fire_now || cum_fire) {
             rc = reset_out_count(h);
             if (rc) return rc;
@@ -634,31 +816,23 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             if (rc) return rc;
             h->pending_out += ub;
         }
-        const TableRef tr = dstt ? ref_of(dstt) : TableRef{};
-        const TableRef* d_src = nullptr;
-        if (!srcs.empty()) {
-            rc = arena_put(h, srcs.data(), srcs.size(), &d_src);
-            if (rc) return rc;
-        }
-        bool plain = h->st_stride == 2 && !sb.empty() && sb.size() <= (size_t)kMaxMergeBatches;
-        for (Staged* s : ln.passes) plain = plain && !s->has_null && !s->is_acc;
+        job.dst = dstt;
+        job.emit = fire_now || cum_fire;
+        job.wend = se;
+        job.kclass = fire_now || cum_fire ? K_FLUSH_FIRE : K_FLUSH;
+        int ji = 0;
+        rc = job_add(h, std::move(job), &ji);
+        if (rc) return rc;
         MergeParams p{};
-        p.region_bits = h->region_bits;
+        rc = job_params(h, ji, &p);
+        if (rc) return rc;
+        // fast variants: plain staged {key, value} records bucketed at the current regions
+        bool plain = h->st_stride == 2 && !ln.passes.empty() && ln.passes.size() <= (size_t)kMaxMergeBatches;
+        for (Staged* s : ln.passes) plain = plain && !s->has_null && !s->is_acc && s->bits == h->region_bits;
         p.fast_stream = plain ? 1 : 0;
-        p.n_src = (int)srcs.size();
         // compact LDS table (two workgroups per CU) when no resident state is read and the
         // COUNT(*) of a key cannot reach 2^32
         p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) ? 1 : 0;
-        p.src = d_src;
-        p.n_batches = (int)sb.size();
-        p.batches = d_sb;
-        p.val_type = h->kvt;
-        p.has_dst = dstt ? 1 : 0;
-        p.dst = tr;
-        p.emit = 0;
-        if (fire_now || cum_fire) fill_emit(h, p, se);
-        p.overflow = h->scalars.as<unsigned int>();
-        p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
 #ifdef FG_STAMPS
         static DevBuf d_st;
         if (getenv("FG_STAMPS")) {
@@ -667,11 +841,16 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             p.stamps = d_st.as<unsigned long long>();
         }
 #endif
-        bool skew = false;
-        for (Staged* s : ln.passes) skew = skew || s->skew;
+        // skewed regions take the chunked heavy pass (passes bucketed at the current regions)
+        bool skew = false, same_bits = true;
+        for (Staged* s : ln.passes) {
+            skew = skew || s->skew;
+            same_bits = same_bits && s->bits == h->region_bits;
+        }
+        skew = skew && same_bits;
         HeavyPlan hp{};
         if (skew) {
-            rc = plan_heavy(h, d_sb, (int)sb.size(), ln.fill + ln.acc_fill, &hp);
+            rc = plan_heavy(h, p.batches, p.n_batches, ln.fill + ln.acc_fill, &hp);
             if (rc) return rc;
             p.heavy = hp.heavy;
         }
@@ -725,11 +904,13 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 fired_tables.push_back(se);   // folded into the first slice
             }
         } else {
-            t->upper = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, (int64_t)kRegionCap * h->P);
+            t->upper = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, kStateCapMax);
         }
     }
-    HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, kScalarBytes, hipMemcpyDeviceToHost, h->stream));
     rc = sync(h);
+    if (rc) return rc;
+    rc = settle_jobs(h);   // regions that overflowed: split and redone
     if (rc) return rc;
     rc = check_overflow(h);
     if (rc) return rc;
@@ -776,31 +957,36 @@ int ensure_out(fg_handle* h, int64_t need) {
 int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, SliceTable* dst, bool defer = false) {
     int64_t ub = 0;
     for (auto* s : srcs) ub += s->upper;
-    ub = std::min<int64_t>(ub, (int64_t)kRegionCap * h->P);
+    ub = std::min<int64_t>(ub, kStateCapMax);
     if (ub == 0 && dst == nullptr) return FG_OK;
     int rc = reset_out_count(h);
     if (rc) return rc;
     rc = ensure_out(h, h->out_n + h->pending_out + ub);
     if (rc) return rc;
-    std::vector<TableRef> refs;
-    for (auto* s : srcs) refs.push_back(ref_of(s));
-    const TableRef* d_src = nullptr;
-    rc = arena_put(h, refs.data(), refs.size(), &d_src);
-    if (rc) return rc;
-    MergeParams p{};
-    p.region_bits = h->region_bits;
-    p.n_src = (int)refs.size();
-    p.src = d_src;
-    p.val_type = h->kvt;
-    p.has_dst = dst != nullptr;
-    if (dst) p.dst = ref_of(dst);
-    fill_emit(h, p, wend);
-    p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
-    p.overflow = h->scalars.as<unsigned int>();
-    {
+    if (srcs.size() == 1 && !dst) {   // one table, nothing written: rows straight from it (cannot overflow)
+        MergeParams p{};
+        p.region_bits = h->region_bits;
+        p.val_type = h->kvt;
+        fill_emit(h, p, wend);
+        p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+        p.overflow = h->scalars.as<unsigned int>();
         KTimer kt(h, K_FIRE, 0);
-        if (refs.size() == 1 && !dst) HIPCHK(h, launch_emit_table(p, refs[0], h->stream));
-        else HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+        HIPCHK(h, launch_emit_table(p, ref_of(srcs[0]), h->stream));
+    } else {
+        MergeJob j;
+        j.srcs = srcs;
+        j.dst = dst;
+        j.emit = true;
+        j.wend = wend;
+        j.kclass = K_FIRE;
+        int ji = 0;
+        rc = job_add(h, std::move(j), &ji);
+        if (rc) return rc;
+        MergeParams p{};
+        rc = job_params(h, ji, &p);
+        if (rc) return rc;
+        KTimer kt(h, K_FIRE, 0);
+        HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
     }
     if (dst) dst->upper = ub;
     if (defer) {
@@ -810,10 +996,12 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     return fire_collect(h);
 }
 
-// after fires: overflow check and the fired-row count (one synchronization)
+// after fires: region retries, overflow check and the fired-row count (one synchronization)
 int fire_collect(fg_handle* h) {
-    HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, kScalarBytes, hipMemcpyDeviceToHost, h->stream));
     int rc = sync(h);
+    if (rc) return rc;
+    rc = settle_jobs(h);
     if (rc) return rc;
     rc = check_overflow(h);
     if (rc) return rc;
@@ -829,9 +1017,16 @@ int fire_collect(fg_handle* h) {
 int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired);
 int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
     bool fired = false;
+    // tables freed by the loop stay alive until the fires are collected (a failed region's
+    // retry reads them)
+    h->defer_free = true;
     int rc = fire_windows_launch(h, prev, wm, &fired);
+    h->defer_free = false;
     if (rc) return rc;
-    return fired ? fire_collect(h) : FG_OK;
+    if (fired) return fire_collect(h);
+    for (auto& t : h->deferred) h->table_pool.push_back(std::move(t));
+    h->deferred.clear();
+    return FG_OK;
 }
 int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired) {
     const WindowSpec& w = h->w;
@@ -1016,8 +1211,17 @@ int grow_lanes(fg_handle* h, int64_t need) {
 // (slice assignment, late rules, bucket histogram), then -- once the batch's slices are
 // known to fit the staged lanes -- bucket scan and scatter into the lanes' staged areas.
 // Returns -1 when the batch spans more slices than the lanes can hold.
+// ingest scratch for the current regions x lanes (after a split)
+int ensure_scratch(fg_handle* h) {
+    HIPCHK(h, h->hist.ensure(4 * (size_t)h->F * h->grid));
+    HIPCHK(h, h->totals.ensure(4 * ((size_t)h->F + 1)));
+    HIPCHK(h, h->scan_tmp.ensure(4 * scan_tmp_words((int64_t)h->F)));
+    return FG_OK;
+}
+
 int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
                 const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+    if (int rc0 = ensure_scratch(h)) return rc0;
     IngestParams p{};
     p.w = h->w;
     p.n = n;
@@ -1089,11 +1293,12 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
             if (s) h->pass_pool.push_back(std::move(s));
         }
     } pool_back{h, s};
-    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
+    const int Fp = p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
+    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (Fp + 1)));
     {
         KTimer kt(h, K_SCAN, 0);
-        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), h->F, p.grid, h->stream));
-        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F,
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), Fp, p.grid, h->stream));
+        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), Fp,
                                   h->scan_tmp.as<uint32_t>(), h->stream));
     }
     int rc = sync(h);
@@ -1172,7 +1377,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         for (int l = 0; l < kMaxLanes; l++) p.lane_slot[l] = -1;
         for (int l = 0; l < h->lanes; l++)
             if (out->lane_total[l] > 0) p.lane_slot[l] = nslots++;
-        p.sorted = (nslots >= 1 && nslots <= 2 && (nslots << h->region_bits) <= kMaxSortedBuckets) ? 1 : 0;
+        p.sorted = (nslots >= 1 && nslots <= 2 && (nslots << p.region_bits) <= kMaxSortedBuckets) ? 1 : 0;
     }
     p.st_stride = h->st_stride;
     p.st_rec = h->st_rec.as<int64_t>();
@@ -1186,6 +1391,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         HIPCHK(h, launch_ingest_scatter(p, h->stream));
     }
     s->has_null = vnull != nullptr;
+    s->bits = p.region_bits;   // (a flush above may have split the regions since the count)
     s->is_acc = false;
     s->skew = out->skew;
     s->refs = 0;
@@ -1225,6 +1431,7 @@ int grow_acc(fg_handle* h, int64_t need) {
 // rows span more slices than the lanes can hold.
 int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* cs, const int64_t* cv,
              const int64_t* sum, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+    if (int rc0 = ensure_scratch(h)) return rc0;
     IngestParams p{};
     p.w = h->w;
     p.w.local_input = h->w.tz_n > 0 ? 1 : 0;   // partial rows carry local slice ends
@@ -1302,11 +1509,12 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     } else {
         s.reset(new Staged());
     }
-    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (h->F + 1)));
+    const int Fp = p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
+    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (Fp + 1)));
     {
         KTimer kt(h, K_SCAN, 0);
-        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), h->F, p.grid, h->stream));
-        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), h->F,
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), Fp, p.grid, h->stream));
+        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), Fp,
                                   h->scan_tmp.as<uint32_t>(), h->stream));
     }
     p.bucket_base = s->bucket_off.as<uint32_t>();
@@ -1332,6 +1540,7 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
         HIPCHK(h, launch_acc_scatter(p, a, h->stream));
     }
     s->has_null = false;
+    s->bits = p.region_bits;
     s->is_acc = true;
     s->skew = false;
     s->refs = 0;
@@ -1573,22 +1782,22 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         if (w.tz_n > 0) w.local_input = 1;   // window ends are local times (zone rules)
     }
 
-    // regions: average occupancy <= ~70 % of the per-region HBM capacity
-    // expected_keys <= 0: unknown (a shim without a key-count hint) -> the largest table
-    // (2^13 regions, ~29M entries per slice); a hint sizes it down for speed
-    int64_t keys = cfg->expected_keys > 0 ? cfg->expected_keys : INT64_MAX;
+    // Regions: keys per region ~35 % of the kSlots LDS slots, so linear probes stay short (a
+    // wave's probe loop runs at its lanes' probe counts), up to 2^13 regions. A region that
+    // overflows later splits (settle_jobs / grow), so the hint sizes for speed, not for
+    // correctness. expected_keys <= 0 (a shim without a key-count hint): 2^10 regions
+    // (~1.4M keys per slice at that load, 117 MB per slice table), grown on demand.
     int bits = 0;
-    // Keys per region ~35 % of the kSlots LDS slots: linear probes stay short (a wave's
-    // probe loop runs at its lanes' probe counts); up to 2^13 regions, then denser.
-    while (bits < 13 && ((int64_t)1 << bits) * (int64_t)(kSlots * 0.35) < keys) bits++;
+    if (cfg->expected_keys > 0) {
+        while (bits < kMaxRegionBits && ((int64_t)1 << bits) * (int64_t)(kSlots * 0.35) < cfg->expected_keys) bits++;
+    } else {
+        bits = kDefaultRegionBits;
+    }
     h->region_bits = bits;
     h->P = 1 << bits;
     // the staging buckets are the state regions: one region per merge workgroup pass
-    h->lanes = kMaxLanes;
-    // lanes x regions bounded by the count histogram and, for the two-pass partition, by
-    // pass 1's LDS histogram
-    while (h->lanes > 1 && (h->lanes << h->region_bits) > kMaxStageBuckets) h->lanes >>= 1;
-    while (h->lanes > 2 && h->region_bits >= kFineBits && (h->lanes << h->region_bits) > kMaxPart1Fine) h->lanes >>= 1;
+    h->lanes = lanes_for(bits);
+    h->lanes_target = h->lanes;
     h->F = h->lanes << h->region_bits;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, h->device) == hipSuccess) {
@@ -1607,7 +1816,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
               chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F))) &&
               chk(hp->counters.ensure(sizeof(Counters))) && chk(hp->h_counters.ensure(sizeof(Counters))) &&
               chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) && chk(hp->sink.ensure(256)) &&
-              chk(hp->h_scalars.ensure(64));
+              chk(hp->h_scalars.ensure(64)) && chk(hp->fail_list.ensure(4 * (size_t)kFailCap));
     if (!ok) {
         g_open_error = "device allocation failed";
         return FG_EDEVICE;
@@ -1623,6 +1832,7 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     if (!b->key || !b->rowtime) return h->fail(FG_EINVAL, "batch key/rowtime columns are required");
     if (h->cfg.val_type != FG_VAL_NONE && !b->val) return h->fail(FG_EINVAL, "batch value column is required");
     HIPCHK(h, hipSetDevice(h->device));
+    maybe_reduce_lanes(h);
     const int64_t n = b->n;
     const int64_t *key = b->key, *ts = b->rowtime;
     const int64_t* val = h->cfg.val_type != FG_VAL_NONE ? static_cast<const int64_t*>(b->val) : nullptr;
@@ -1739,6 +1949,7 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
         return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
     HIPCHK(h, hipSetDevice(h->device));
+    maybe_reduce_lanes(h);
     const int64_t n = b->n;
     const int64_t *key = b->key, *se = b->slice_end, *cs = b->cnt_star, *cv = b->cnt_val, *sum = b->sum;
     if (b->location == FG_HOST) {
@@ -1948,6 +2159,28 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     // group entries by slice, bucket by region on the host (restore is off the hot path)
     std::map<int64_t, std::vector<int64_t>> by_slice;
     for (int64_t i = 0; i < in->n; i++) by_slice[in->slice_end[i]].push_back(i);
+    // regions sized for the image first: the smallest split whose fullest region keeps the
+    // LDS tables at most ~70 % full (a slice restored into a live table may still split more)
+    {
+        int need = h->region_bits;
+        for (auto& kv : by_slice) {
+            std::vector<uint32_t> c13((size_t)1 << kMaxRegionBits, 0);
+            for (int64_t i : kv.second) c13[fmix64((uint64_t)in->key[i]) >> (64 - kMaxRegionBits)]++;
+            for (int b = need; b <= kMaxRegionBits; b++) {
+                uint32_t mx = 0;
+                const int per = 1 << (kMaxRegionBits - b);
+                for (size_t r = 0; r < c13.size(); r += (size_t)per) {
+                    uint32_t sum = 0;
+                    for (int c = 0; c < per; c++) sum += c13[r + (size_t)c];
+                    mx = std::max(mx, sum);
+                }
+                need = b;
+                if (mx <= (uint32_t)(0.7 * kRegionCap)) break;
+            }
+        }
+        rc = grow(h, need);
+        if (rc) return rc;
+    }
     for (auto& kv : by_slice) {
         const auto& idx = kv.second;
         const int64_t m = (int64_t)idx.size();
@@ -1984,43 +2217,39 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         SliceTable* t = nullptr;
         rc = table_get(h, kv.first, true, &t);
         if (rc) return rc;
-        StagedBatch sb{};
-        sb.rec = dk.as<int64_t>();
-        sb.stride = 1;
-        sb.val = dsm.as<int64_t>();
-        sb.cnt_star = dcs.as<int64_t>();
-        sb.cnt_null = dcn.as<int64_t>();
-        sb.bucket_off = doff.as<uint32_t>();
-        sb.is_acc = 1;
-        const StagedBatch* d_sb = nullptr;
-        rc = arena_put(h, &sb, 1, &d_sb);
-        if (rc) return rc;
-        TableRef tr = ref_of(t);
-        const TableRef* d_src = nullptr;
-        rc = arena_put(h, &tr, 1, &d_src);
-        if (rc) return rc;
+        MergeJob j;
+        JobBatch jb;
+        jb.ext.rec = dk.as<int64_t>();
+        jb.ext.stride = 1;
+        jb.ext.val = dsm.as<int64_t>();
+        jb.ext.cnt_star = dcs.as<int64_t>();
+        jb.ext.cnt_null = dcn.as<int64_t>();
+        jb.ext.bucket_off = doff.as<uint32_t>();
+        jb.ext.is_acc = 1;
+        jb.ext_bits = h->region_bits;
+        j.batches.push_back(jb);
+        j.srcs.push_back(t);
+        j.dst = t;
+        j.kclass = K_RESTORE;
         HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+        int ji = 0;
+        rc = job_add(h, std::move(j), &ji);
+        if (rc) return rc;
         MergeParams p{};
-        p.region_bits = h->region_bits;
-        p.n_src = 1;
-        p.src = d_src;
-        p.n_batches = 1;
-        p.batches = d_sb;
-        p.val_type = h->kvt;
-        p.has_dst = 1;
-        p.dst = tr;
-        p.overflow = h->scalars.as<unsigned int>();
-        p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+        rc = job_params(h, ji, &p);
+        if (rc) return rc;
         {
             KTimer kt(h, K_RESTORE, m);
             HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
         }
-        HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, 16, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, kScalarBytes, hipMemcpyDeviceToHost, h->stream));
         rc = sync(h);
+        if (rc) return rc;
+        rc = settle_jobs(h);   // the device buffers above stay alive until this returns
         if (rc) return rc;
         rc = check_overflow(h);
         if (rc) return rc;
-        t->upper = std::min<int64_t>(t->upper + m, (int64_t)kRegionCap * h->P);
+        t->upper = std::min<int64_t>(t->upper + m, kStateCapMax);
     }
     // open(): processor progress restarts at Long.MIN_VALUE, and so does the restored timer
     // service's watermark (InternalTimerServiceImpl.currentWatermark is not part of the

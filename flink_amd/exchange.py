@@ -130,17 +130,26 @@ def exchange_partials(cols, group=None, max_parallelism: int = 128, key_hash: in
                                                                                        dtype=torch.int64, device=dev)
     if via_cpu:
         packed, counts = packed.cpu(), counts.cpu()
+    out, sent_bytes = exchange_grouped(packed, counts, group)
+    if via_cpu:
+        out = out.to(dev)
+    return [out[:, j].contiguous() for j in range(len(cols))], sent_bytes
+
+
+def exchange_grouped(packed, counts, group=None):
+    """The collective step of the partial-row exchange: `packed` [n, c] int64 rows grouped
+    by destination rank, counts[d] rows for rank d. One all-to-all of the counts, one of the
+    rows (RCCL on device tensors, gloo on host tensors). Returns the received rows and the
+    bytes sent to peers."""
+    import torch.distributed as dist
     recv_counts = torch.empty_like(counts)
     dist.all_to_all_single(recv_counts, counts, group=group)
     send = counts.cpu().tolist()
     recv = recv_counts.cpu().tolist()
-    out = torch.empty((sum(recv), len(cols)), dtype=packed.dtype, device=packed.device)
+    out = torch.empty((sum(recv), packed.shape[1]), dtype=packed.dtype, device=packed.device)
     dist.all_to_all_single(out, packed, output_split_sizes=recv, input_split_sizes=send, group=group)
-    if via_cpu:
-        out = out.to(dev)
     rank = dist.get_rank(group)
-    sent_bytes = 8 * len(cols) * (sum(send) - send[rank])
-    return [out[:, j].contiguous() for j in range(len(cols))], sent_bytes
+    return out, 8 * packed.shape[1] * (sum(send) - send[rank])
 
 
 def global_watermark(local_wm: int, group=None, device=None) -> int:

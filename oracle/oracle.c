@@ -213,6 +213,7 @@ struct or_op {
     int64_t* be_slice; int64_t* be_key; int64_t* be_head; int64_t* be_tail;
     int64_t be_n, be_cap;
     int64_t* br_val; uint8_t* br_null; int64_t* br_next;
+    or_acc* br_acc;                    /* global phase: the buffered partial accumulators */
     int64_t br_n, br_cap;
     /* WindowValueState: (key, ns) -> acc idx */
     pmap state;
@@ -517,7 +518,7 @@ static void emit_row(or_op* op, int64_t key, int64_t wstart, int64_t wend, const
 }
 
 /* ---------------- RecordsWindowBuffer ---------------------------------------------- */
-static void buffer_add(or_op* op, int64_t key, int64_t slice, int64_t vbits, uint8_t isnull) {
+static void buffer_add_any(or_op* op, int64_t key, int64_t slice, int64_t vbits, uint8_t isnull, const or_acc* acc) {
     /* RecordsWindowBuffer.addElement :81-97 */
     if (slice < op->min_slice_end) op->min_slice_end = slice;
     int ins;
@@ -527,11 +528,13 @@ static void buffer_add(or_op* op, int64_t key, int64_t slice, int64_t vbits, uin
         op->br_val = (int64_t*)realloc(op->br_val, sizeof(int64_t) * op->br_cap);
         op->br_null = (uint8_t*)realloc(op->br_null, op->br_cap);
         op->br_next = (int64_t*)realloc(op->br_next, sizeof(int64_t) * op->br_cap);
+        if (op->cfg.phase == OR_PHASE_GLOBAL) op->br_acc = (or_acc*)realloc(op->br_acc, sizeof(or_acc) * op->br_cap);
     }
     int64_t r = op->br_n++;
     op->br_val[r] = vbits;
     op->br_null[r] = isnull;
     op->br_next[r] = -1;
+    if (acc) op->br_acc[r] = *acc;
     if (ins) {
         /* AbstractBytesMultiMap.append :145-184 -- new key, insertion order kept */
         if (op->be_n == op->be_cap) {
@@ -551,15 +554,38 @@ static void buffer_add(or_op* op, int64_t key, int64_t slice, int64_t vbits, uin
         op->be_tail[*e] = r;
     }
 }
-/* RecordsWindowBuffer.flush :108-119 + AggCombiner.combine  TR/operators/aggregate/window/combines/AggCombiner.java:76-115 */
+static void buffer_add(or_op* op, int64_t key, int64_t slice, int64_t vbits, uint8_t isnull) {
+    buffer_add_any(op, key, slice, vbits, isnull, NULL);
+}
+/* RecordsWindowBuffer.flush :108-119 + AggCombiner.combine  TR/operators/aggregate/window/combines/AggCombiner.java:76-115
+ * (two-phase: LocalAggCombiner.combine  combines/LocalAggCombiner.java:69-106, GlobalAggCombiner.combine
+ *  combines/GlobalAggCombiner.java:77-110) */
 static void buffer_flush(or_op* op) {
     if (op->be_n == 0) return;
     int vt = op->cfg.val_type;
     for (int64_t ei = 0; ei < op->be_n; ei++) {
         int64_t key = op->be_key[ei], window = op->be_slice[ei];
+        if (op->cfg.phase == OR_PHASE_LOCAL) {
+            /* a fresh accumulator per (key, slice), emitted as (key, acc, slice end); no state */
+            or_acc acc;
+            acc_create(&acc);
+            for (int64_t r = op->be_head[ei]; r >= 0; r = op->br_next[r])
+                acc_accumulate(&acc, vt, op->br_val[r], op->br_null[r]);
+            emit_row(op, key, jsub(window, op->slice_size), window, &acc, JMIN);
+            continue;
+        }
         or_acc* acc = state_put(op, key, window);        /* value(window) ?: createAccumulators */
-        for (int64_t r = op->be_head[ei]; r >= 0; r = op->br_next[r])
-            acc_accumulate(acc, vt, op->br_val[r], op->br_null[r]);   /* arrival order */
+        if (op->cfg.phase == OR_PHASE_GLOBAL) {
+            /* localAggregator.merge of the partials into a fresh accumulator, then
+             * globalAggregator.merge into the state (:94-101) */
+            or_acc part;
+            acc_create(&part);
+            for (int64_t r = op->be_head[ei]; r >= 0; r = op->br_next[r]) acc_merge(&part, &op->br_acc[r], vt);
+            acc_merge(acc, &part, vt);
+        } else {
+            for (int64_t r = op->be_head[ei]; r >= 0; r = op->br_next[r])
+                acc_accumulate(acc, vt, op->br_val[r], op->br_null[r]);   /* arrival order */
+        }
         if (!op->cfg.proctime && !is_window_fired(op, window, op->timer_wm))   /* step 5 (:101-110), event time */
             register_window_timer(op, key, window);
     }
@@ -572,25 +598,34 @@ static void buffer_flush(or_op* op) {
 
 /* ---------------- processors ------------------------------------------------------- */
 /* AbstractWindowAggProcessor.processElement  TR/operators/aggregate/window/processors/AbstractWindowAggProcessor.java:135-165 */
-static int sql_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits, uint8_t isnull) {
-    int64_t slice_end = or_assign_slice_end(op, ts);
+static int sql_process_slice(or_op* op, int64_t key, int64_t slice_end, int64_t vbits, uint8_t isnull,
+                             const or_acc* acc) {
     if (op->cfg.proctime) {
         /* :137-140 processing time: a timer per element at its slice, never late */
         register_window_timer(op, key, slice_end);
-        buffer_add(op, key, slice_end, vbits, isnull);
+        buffer_add_any(op, key, slice_end, vbits, isnull, acc);
         return 0;
     }
     if (is_window_fired(op, slice_end, op->current_progress)) {
         int64_t last = or_get_last_window_end(op, slice_end);
         if (is_window_fired(op, last, op->current_progress)) return 1;   /* dropped */
-        buffer_add(op, key, slice_state_merge_target(op, slice_end), vbits, isnull);
+        buffer_add_any(op, key, slice_state_merge_target(op, slice_end), vbits, isnull, acc);
         int64_t unfired = slice_end;
         while (is_window_fired(op, unfired, op->current_progress)) unfired = jadd(unfired, op->interval);
         register_window_timer(op, key, unfired);
         return 0;
     }
-    buffer_add(op, key, slice_end, vbits, isnull);
+    buffer_add_any(op, key, slice_end, vbits, isnull, acc);
     return 0;
+}
+static int sql_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits, uint8_t isnull) {
+    int64_t slice_end = or_assign_slice_end(op, ts);
+    if (op->cfg.phase == OR_PHASE_LOCAL) {
+        /* LocalSlicingWindowAggOperator.processElement :113-119: its own slice, no late handling */
+        buffer_add(op, key, slice_end, vbits, isnull);
+        return 0;
+    }
+    return sql_process_slice(op, key, slice_end, vbits, isnull, NULL);
 }
 
 /* fireWindow: SliceUnsharedWindowAggProcessor.java:46-54 / SliceSharedWindowAggProcessor.java:64-118;
@@ -704,6 +739,9 @@ or_op* or_open(const or_config* cfg, char* err, int errlen) {
     } else {
         snprintf(buf, sizeof buf, "unknown window kind %d", cfg->kind);
     }
+    if (!buf[0] && cfg->phase != OR_PHASE_SINGLE &&
+        (cfg->mode != OR_MODE_SQL || cfg->windowed || cfg->proctime || cfg->phase > OR_PHASE_GLOBAL))
+        snprintf(buf, sizeof buf, "the two-phase operators are SQL event-time operators");
     if (!buf[0] && cfg->windowed && (cfg->mode != OR_MODE_SQL || cfg->proctime))
         /* WindowedSliceAssigner.isEventTime() is always true (:430-434); SQL only */
         snprintf(buf, sizeof buf, "a windowed slice assigner is an SQL event-time assigner");
@@ -745,7 +783,7 @@ void or_close(or_op* op) {
     if (!op) return;
     pmap_free(&op->buf_map); pmap_free(&op->state); pmap_free(&op->timer_set);
     free(op->be_slice); free(op->be_key); free(op->be_head); free(op->be_tail);
-    free(op->br_val); free(op->br_null); free(op->br_next);
+    free(op->br_val); free(op->br_null); free(op->br_next); free(op->br_acc);
     free(op->accs); free(op->acc_free); free(op->heap); free(op->rows); free(op->merge_buf);
     free((void*)op->cfg.tz_trans); free((void*)op->cfg.tz_offs);
     free(op);
@@ -763,7 +801,42 @@ void or_process_batch(or_op* op, int64_t n, const int64_t* key, const int64_t* t
     }
 }
 
+/* The global phase's input: the `sliced` assigner takes each partial row's slice end
+ * (SliceAssigners.java:494-533); late rules, buffer and timers as for records; the
+ * combiner merges accumulators (GlobalAggCombiner). A late row counts once. */
+void or_process_partials(or_op* op, int64_t n, const or_row* rows) {
+    for (int64_t i = 0; i < n; i++) {
+        const or_row* r = &rows[i];
+        or_acc a;
+        acc_create(&a);
+        a.cnt_star = r->cnt_star;
+        a.cnt_val = r->cnt_val;
+        a.sum_null = r->sum_null;
+        a.sum_i = r->sum_i;
+        a.sum_d = r->sum_d;
+        a.avg_sum_i = r->sum0_i;
+        a.avg_sum_d = r->sum0_d;
+        a.min_i = r->min_i;
+        a.max_i = r->max_i;
+        a.min_d = r->min_d;
+        a.max_d = r->max_d;
+        op->late_dropped += sql_process_slice(op, r->key, r->window_end, 0, 0, &a);
+    }
+}
+
 void or_process_watermark(or_op* op, int64_t wm) {
+    if (op->cfg.phase == OR_PHASE_LOCAL) {
+        /* LocalSlicingWindowAggOperator.processWatermark :121-134 (no timers) */
+        if (wm > op->current_progress) {
+            op->current_progress = wm;
+            if (op->current_progress >= op->next_trigger_progress) {
+                if (is_window_fired(op, op->min_slice_end, wm)) buffer_flush(op);   /* advanceProgress */
+                op->next_trigger_progress = next_trigger(op, wm);
+            }
+        }
+        op->timer_wm = wm;
+        return;
+    }
     if (op->cfg.mode == OR_MODE_SQL) {
         /* SlicingWindowOperator.processWatermark :207-210 -> AbstractWindowAggProcessor.advanceProgress :178-192 */
         if (wm > op->current_progress) {

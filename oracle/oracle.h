@@ -45,7 +45,10 @@ typedef struct or_config {
     const int64_t* tz_offs;   /* tz_n + 1 offsets (ms): [i] in force before transition i */
     int32_t tz_use_dst;       /* TimeZone.getTimeZone(zone).useDaylightTime() */
     int32_t windowed;         /* WindowedSliceAssigner over the kind's assigner: ts = window_end */
+    int32_t phase;            /* OR_PHASE_*: single operator, or the local / global half of the
+                               * two-phase plan (TwoStageOptimizedWindowAggregateRule) */
 } or_config;
+enum { OR_PHASE_SINGLE = 0, OR_PHASE_LOCAL = 1, OR_PHASE_GLOBAL = 2 };
 
 /* One fired row. The aggregate set is fixed: COUNT(*), COUNT(v), SUM(v), AVG(v), SUM0(v), MIN(v), MAX(v). */
 typedef struct or_row {
@@ -79,6 +82,10 @@ void    or_close(or_op* op);
 void    or_process_batch(or_op* op, int64_t n, const int64_t* key, const int64_t* ts,
                          const void* val, const uint8_t* isnull);
 void    or_process_watermark(or_op* op, int64_t wm);
+/* Global phase: n partial accumulator rows as the local phase emits them (key, window_end =
+ * the slice end, cnt_star, cnt_val, sum/sum0/min/max, sum_null), through the `sliced`
+ * assigner and GlobalAggCombiner. A local-phase operator's take_rows are such rows. */
+void    or_process_partials(or_op* op, int64_t n, const or_row* rows);
 /* prepareSnapshotPreBarrier: RecordsWindowBuffer.flush() (no-op for DataStream). */
 void    or_prepare_snapshot(or_op* op);
 /* snapshot -> close -> initializeState -> open: state and timers survive, the buffer

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 MODE_SQL, MODE_DATASTREAM = 0, 1
 TUMBLE, HOP, CUMULATE = 0, 1, 2
+PHASE_SINGLE, PHASE_LOCAL, PHASE_GLOBAL = 0, 1, 2
 VAL_NONE, VAL_I64, VAL_F64 = 0, 1, 2
 JMIN = -(1 << 63)
 JMAX = (1 << 63) - 1
@@ -39,6 +40,7 @@ class Config(C.Structure):
         ("tz_offs", C.c_void_p),
         ("tz_use_dst", C.c_int32),
         ("windowed", C.c_int32),
+        ("phase", C.c_int32),
     ]
 
 
@@ -98,6 +100,7 @@ def lib():
         L.or_close.argtypes = [P]
         L.or_process_batch.argtypes = [P, C.c_int64, P, P, P, P]
         L.or_process_watermark.argtypes = [P, C.c_int64]
+        L.or_process_partials.argtypes = [P, C.c_int64, P]
         L.or_prepare_snapshot.argtypes = [P]
         L.or_restore_copy.restype = P
         L.or_restore_copy.argtypes = [P]
@@ -159,12 +162,16 @@ class OracleOperator:
     prepareSnapshotPreBarrier / snapshot-restore, with fired rows collected."""
 
     def __init__(self, mode=MODE_SQL, kind=TUMBLE, size=1000, slide=0, offset=0, tz_offset_ms=0,
-                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None, zone=None, windowed=False):
+                 val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None, zone=None, windowed=False,
+                 phase=PHASE_SINGLE):
         """zone: an IANA zone name whose rules (transitions, daylight saving) replace the fixed
-        tz_offset_ms (TimeWindowUtil with a ZoneId)."""
+        tz_offset_ms (TimeWindowUtil with a ZoneId). phase: PHASE_LOCAL / PHASE_GLOBAL for the
+        two halves of the two-phase plan (LocalSlicingWindowAggOperator + LocalAggCombiner;
+        SlicingWindowOperator over the `sliced` assigner + GlobalAggCombiner)."""
         self.cfg = Config(mode, kind, size, slide, offset, tz_offset_ms, val_type, count_star_index,
                           1 if proctime else 0, 0)
         self.cfg.windowed = 1 if windowed else 0
+        self.cfg.phase = phase
         self.zone = zone
         if zone is not None:
             from flink_amd.tz import zone_rules
@@ -210,6 +217,11 @@ class OracleOperator:
     def process_watermark(self, wm: int):
         lib().or_process_watermark(self._h, int(wm))
 
+    def process_partials(self, rows):
+        """Global phase: partial accumulator rows (ROW_DTYPE) of local-phase operators."""
+        rows = np.ascontiguousarray(rows, dtype=ROW_DTYPE)
+        lib().or_process_partials(self._h, len(rows), rows.ctypes.data if len(rows) else None)
+
     def prepare_snapshot(self):
         lib().or_prepare_snapshot(self._h)
 
@@ -217,7 +229,8 @@ class OracleOperator:
         h = lib().or_restore_copy(self._h)
         c = self.cfg
         return OracleOperator(c.mode, c.kind, c.size, c.slide, c.offset, c.tz_offset_ms, c.val_type,
-                              c.count_star_index, _handle=h, zone=self.zone, windowed=bool(c.windowed))
+                              c.count_star_index, _handle=h, zone=self.zone, windowed=bool(c.windowed),
+                              phase=c.phase)
 
     def take_rows(self) -> np.ndarray:
         L = lib()

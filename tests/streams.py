@@ -71,3 +71,22 @@ def batches_with_watermarks(n, batch, ts, delay_ms):
         hi = min(n, lo + batch)
         mx = max(mx, int(ts[lo:hi].max()))
         yield lo, hi, mx - delay_ms - 1
+
+
+def fmix64_inv(h):
+    """Inverse of the MurmurHash3 fmix64 finalizer (numpy uint64; fg_window.h fmix64_inv)."""
+    h = np.asarray(h, dtype=np.uint64).copy()
+    with np.errstate(over="ignore"):
+        h ^= h >> np.uint64(33)
+        h *= np.uint64(0x9cb4b2f8129337db)
+        h ^= h >> np.uint64(33)
+        h *= np.uint64(0x4f74430c22a54005)
+        h ^= h >> np.uint64(33)
+    return h
+
+
+def keys_in_one_region(n, seed=SEED):
+    """n distinct BIGINT keys whose fmix64 mix has its top 16 bits zero: they share a state
+    region at every split the engine can make (at most 2^13 regions)."""
+    h = np.unique(splitmix64(np.uint64(seed) ^ np.arange(2 * n, dtype=np.uint64)) >> np.uint64(16))[:n]
+    return fmix64_inv(h).view(np.int64)

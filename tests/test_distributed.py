@@ -99,3 +99,107 @@ def test_two_rank_exchange_matches_single_operator(oracle_mod):
     for f in ("key", "window_end", "cnt_star", "sum_i"):
         assert np.array_equal(g[f], e[f]), f
     assert sum(l for _, _, l, _ in res) == op.late_dropped
+
+
+# ---- two-phase plan over the exchange (TwoStageOptimizedWindowAggregateRule) ---------------
+TP_N, TP_KEYS, TP_BATCH, TP_DELAY, TP_RATE = 60_000, 4000, 6_000, 100, 10
+# kind -> (oracle kind, size, slide, jitter): the jitter exceeds the window so rows are late
+TP_KINDS = {"tumble": (0, 500, 0, 900), "hop": (1, 1500, 500, 2500), "cumulate": (2, 2000, 500, 3000)}
+
+
+def _two_phase_rank(rank, world, port, kind, out_q):
+    import torch
+    import torch.distributed as dist
+
+    from flink_amd.exchange import exchange_grouped, global_watermark
+    from oracle import oracle as O
+    from tests.streams import make_stream
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    k_, size, slide, jitter = TP_KINDS[kind]
+    key, ts, val, isnull = make_stream(TP_N, TP_KEYS, "f64", seed=2000 + rank, jitter_ms=jitter, null_frac=0.1,
+                                       rate_per_ms=TP_RATE)
+    local = O.OracleOperator(kind=k_, size=size, slide=slide, phase=O.PHASE_LOCAL)
+    glob = O.OracleOperator(kind=k_, size=size, slide=slide, phase=O.PHASE_GLOBAL)
+    rows, sent_total = [], 0
+    mx = -(1 << 63)
+
+    def round_(local_wm):
+        nonlocal sent_total
+        # LocalSlicingWindowAggOperator.processWatermark: its flush emits partial accumulators
+        local.process_watermark(local_wm)
+        part = local.take_rows()
+        # key-group routing of the partial rows (KeyGroupStreamPartitioner.selectChannel)
+        owner = O.key_groups_binaryrow(part["key"], MAXP).astype(np.int64) * world // MAXP
+        part = part[np.argsort(owner, kind="stable")]
+        counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
+        packed = torch.from_numpy(part.view(np.int64).reshape(len(part), O.ROW_DTYPE.itemsize // 8).copy())
+        recv, sent = exchange_grouped(packed, counts)
+        sent_total += sent
+        got = np.ascontiguousarray(recv.numpy()).view(O.ROW_DTYPE).reshape(-1)
+        glob.process_partials(got)
+        # StatusWatermarkValve: the global operator's watermark is the min over its inputs
+        glob.process_watermark(global_watermark(local_wm))
+        rows.append(glob.take_rows())
+
+    for lo in range(0, TP_N, TP_BATCH):
+        hi = lo + TP_BATCH
+        local.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], isnull[lo:hi])
+        mx = max(mx, int(ts[lo:hi].max()))
+        round_(mx - TP_DELAY)
+    round_((1 << 63) - 1)
+    out_q.put((rank, np.concatenate(rows).tobytes(), glob.late_dropped, sent_total))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_two_phase_exchange_matches_single_operator(oracle_mod, kind):
+    """Two ranks run the local phase on their source partitions, exchange the partial
+    accumulator rows by key-group owner (flink_amd.exchange.exchange_grouped: the collective
+    step of exchange_partials, gloo here, RCCL on GPUs) and merge them in the owners' global
+    operators, which fire at the min-combined watermark. The union of the global rows equals
+    one single-phase operator over both partitions (late rows included: the jitter exceeds
+    the watermark delay); late partial rows are counted once each, as in the reference's
+    two-phase plan (LocalSlicingWindowAggOperator.java:113-134, GlobalAggCombiner.java:77-110)."""
+    import torch.multiprocessing as mp
+
+    from tests.streams import make_stream
+    O = oracle_mod
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_phase_rank, args=(r, WORLD, port, kind, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = np.concatenate([np.frombuffer(b, dtype=O.ROW_DTYPE) for _, b, _, _ in res])
+    assert all(sent > 0 for *_, sent in res)
+    k_, size, slide, jitter = TP_KINDS[kind]
+    streams = [make_stream(TP_N, TP_KEYS, "f64", seed=2000 + r, jitter_ms=jitter, null_frac=0.1, rate_per_ms=TP_RATE)
+               for r in range(WORLD)]
+    op = O.OracleOperator(kind=k_, size=size, slide=slide)
+    rows = []
+    mxs = [-(1 << 63)] * WORLD
+    for lo in range(0, TP_N, TP_BATCH):
+        for r in range(WORLD):
+            k, t, v, nl = streams[r]
+            op.process_batch(k[lo:lo + TP_BATCH], t[lo:lo + TP_BATCH], v[lo:lo + TP_BATCH], nl[lo:lo + TP_BATCH])
+            mxs[r] = max(mxs[r], int(t[lo:lo + TP_BATCH].max()))
+        op.process_watermark(min(mxs) - TP_DELAY)
+        rows.append(op.take_rows())
+    op.process_watermark((1 << 63) - 1)
+    rows.append(op.take_rows())
+    exp = np.concatenate(rows)
+    assert op.late_dropped > 0
+    srt = lambda a: a[np.lexsort((a["key"], a["window_end"]))]
+    g, e = srt(got), srt(exp)
+    assert len(g) == len(e)
+    for f in ("key", "window_start", "window_end", "cnt_star", "cnt_val", "sum_null"):
+        assert np.array_equal(g[f], e[f]), f
+    ok = e["sum_null"] == 0
+    assert np.allclose(g["sum_d"][ok], e["sum_d"][ok], rtol=1e-9, atol=0)
+    assert sum(late for _, _, late, _ in res) > 0

@@ -86,7 +86,7 @@ def assert_rows_equal(got, exp, vt, ctx="", sum0=True, minmax=(), vmax=None):
 
 
 def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at=None, end_wm=JMAX,
-               expected_keys=None, kstats=None, **gen):
+               expected_keys=None, kstats=None, stats=None, **gen):
     key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
     vmax = 1000.0 if gen.get("signed") and cfg["val_type"] == "f64" else None
     mm = tuple(a for a in cfg.get("aggs", ()) if a in ("min", "max"))
@@ -118,6 +118,8 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
     late = g.late_dropped
     if kstats is not None:
         kstats.update(g.op.kernel_stats())
+    if stats is not None:
+        stats.update(g.op.stats())
     g.close()
     o.close()
     return late
@@ -359,14 +361,39 @@ def test_empty_and_ragged_batches(oracle_mod):
     op.close()
 
 
-def test_capacity_overflow_is_loud():
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_regions_split_on_overflow(oracle_mod, kind):
+    """An under-estimated key count no longer fails the job: a region that overflows its LDS
+    table or its HBM capacity splits (BytesMap grows, BytesMap.java:229-290; the buffer flushes
+    and retries, RecordsWindowBuffer.java:89-96) and its records are merged again. 400k keys
+    into an operator sized for 1,000 (one region) give the oracle's rows."""
+    cfg = cfg_of(kind, 1000 if kind == "tumble" else 3000, 0 if kind == "tumble" else 1000)
+    st = {}
+    drive_both(oracle_mod, cfg, n=800_000, keys=400_000, batch=100_000, delay=100, jitter=300, expected_keys=1000,
+               stats=st)
+    assert st["state_regions"] >= 32, st   # split from 1 region: ~88k distinct keys per 1-s slice
+
+
+def test_regions_split_with_staged_lanes_and_restore(oracle_mod):
+    """Splits while other slice lanes hold staged records (read through their parent buckets),
+    a snapshot restored into a small operator (regions sized for the image), and the late
+    rows that follow."""
+    cfg = cfg_of("tumble", 200, vt="i64")
+    drive_both(oracle_mod, cfg, n=900_000, keys=150_000, batch=60_000, delay=150, jitter=450, expected_keys=500,
+               snapshot_at=6)
+
+
+def test_capacity_limit_is_loud():
+    """More distinct keys in one slice than 2^13 regions hold fails with FG_ECAPACITY."""
     import flink_amd as F
-    op = F.WindowAggOperator(F.tumbling(1000), expected_keys=1)   # one region
-    n = 8000
-    op.process_batch(np.arange(n, dtype=np.int64), np.full(n, 100, np.int64), np.ones(n))
+    op = F.WindowAggOperator(F.tumbling(1000), expected_keys=1)
+    # 8,000 keys whose mix shares the top 13 bits and more: they land in one region at any split
+    from tests.streams import keys_in_one_region
+    keys = keys_in_one_region(8000)
+    op.process_batch(keys, np.full(len(keys), 100, np.int64), np.ones(len(keys)))
     with pytest.raises(F.FlinkGpuError) as ei:
         op.process_watermark(JMAX)
-    assert "expected_keys" in str(ei.value)
+    assert "regions" in str(ei.value)
     op.close()
 
 
@@ -692,11 +719,15 @@ def test_batch_limits_are_loud_and_recoverable(oracle_mod):
     op.close()
 
 
-def test_unknown_key_count_takes_the_largest_table(oracle_mod):
-    """expected_keys = 0 (no key-count hint from the shim): sized for the maximum, so 200k
-    keys fit where a one-region table (3,584 entries) would overflow loudly."""
+def test_unknown_key_count_starts_small_and_grows(oracle_mod):
+    """expected_keys = 0 (no key-count hint from the shim): 2^10 regions (117 MB per slice
+    table instead of the largest table's 940 MB), split on demand: ~5.7M distinct keys in one
+    slice grow it to 2^11."""
     cfg = cfg_of("tumble", 1000)
-    drive_both(oracle_mod, cfg, n=400_000, keys=200_000, batch=100_000, delay=0, jitter=0, expected_keys=0)
+    st = {}
+    drive_both(oracle_mod, cfg, n=10_000_000, keys=8_000_000, batch=2_500_000, delay=0, jitter=0, expected_keys=0,
+               rate_per_ms=10_000, stats=st)
+    assert st["state_regions"] >= 2048, st
 
 
 @pytest.mark.parametrize("kind,outliers", [("tumble", "future"), ("tumble", "epoch0"), ("hop", "both"),
