@@ -63,7 +63,9 @@ enum fg_status {
     FG_EINVAL = 1,     /* invalid argument / window spec (IllegalArgumentException) */
     FG_EFULL = 2,      /* batch larger than the configured buffer (EOFException analogue) */
     FG_EDEVICE = 3,    /* HIP runtime error or no usable MI355X device */
-    FG_ECAPACITY = 4,  /* a state region overflowed its HBM capacity (raise expected_keys) */
+    FG_ECAPACITY = 4,  /* more distinct keys in one slice than 2^13 state regions hold (~29M):
+                        * raise the parallelism. Below that a region that overflows splits
+                        * (BytesMap growth, BytesMap.java:229-290) and the call succeeds. */
     FG_ESTATE = 5      /* API used out of order */
 };
 
@@ -132,8 +134,9 @@ typedef struct fg_config {
     int32_t key_group_end;
     int32_t device_id;            /* HIP device ordinal */
     int32_t flags;                /* FG_FLAG_* */
-    int64_t expected_keys;        /* distinct keys per slice on this subtask (sizes HBM regions);
-                                   * <= 0: unknown, the largest table (~29M entries per slice) */
+    int64_t expected_keys;        /* distinct keys per slice on this subtask: sizes the state regions
+                                   * (speed, not correctness: regions split on overflow, up to 2^13);
+                                   * <= 0: unknown, 2^10 regions (117 MB per slice table), grown on demand */
     int64_t buffer_records;       /* staged records before an implicit flush (managed-memory analogue) */
     /* Shift time zone with transitions (daylight saving): the ZoneRules of the ZoneId as data
      * (ZoneRules.getTransitions() on the Java side). n_tz_transitions > 0 replaces
