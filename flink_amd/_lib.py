@@ -43,6 +43,13 @@ class FgBatch(C.Structure):
     ]
 
 
+class FgRowBatch(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("location", C.c_int32), ("stride", C.c_int32), ("rows", C.c_void_p),
+        ("arity", C.c_int32), ("key_field", C.c_int32), ("rowtime_field", C.c_int32), ("val_field", C.c_int32),
+    ]
+
+
 class FgRows(C.Structure):
     _fields_ = [
         ("n", C.c_int64), ("location", C.c_int32), ("num_aggs", C.c_int32),
@@ -84,8 +91,9 @@ FLAG_WINDOWED = 8
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (
-    "fg_open", "fg_add_batch", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
-    "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_stream",
+    "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
+    "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
     "fg_abi_version",
 )
@@ -121,6 +129,7 @@ def load():
     P = C.c_void_p
     L.fg_open.argtypes = [C.POINTER(FgConfig), C.POINTER(P)]
     L.fg_add_batch.argtypes = [P, C.POINTER(FgBatch)]
+    L.fg_add_rows.argtypes = [P, C.POINTER(FgRowBatch)]
     L.fg_add_partials.argtypes = [P, C.POINTER(FgPartials)]
     L.fg_advance_progress.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(FgRows)]
     L.fg_flush.argtypes = [P]
@@ -131,6 +140,8 @@ def load():
     L.fg_synchronize.argtypes = [P]
     L.fg_reset.argtypes = [P]
     L.fg_kernel_stats.argtypes = [P, C.POINTER(FgKernelStat), C.c_int32, C.POINTER(C.c_int32)]
+    L.fg_set_kernel_timing.argtypes = [P, C.c_uint32]
+    L.fg_set_kernel_timing.restype = C.c_int
     L.fg_stream.argtypes = [P]
     L.fg_stream.restype = P
     L.fg_last_error.argtypes = [P]
@@ -143,7 +154,7 @@ def load():
     L.fg_partition_columns_by_owner.argtypes = [C.c_int32, P, C.c_int64, C.c_int32, P, C.c_int32, C.c_int32,
                                                 C.c_int32, P, P]
     L.fg_abi_version.restype = C.c_int
-    for fn in ("fg_open", "fg_add_batch", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
                "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int

@@ -77,11 +77,11 @@ struct HostBuf {   // pinned host memory
     ~HostBuf() {
         if (p) (void)hipHostFree(p);
     }
-    hipError_t ensure(size_t need) {
+    hipError_t ensure(size_t need, unsigned flags = hipHostMallocDefault) {
         if (need <= bytes) return hipSuccess;
         size_t nb = std::max(need, bytes + bytes / 2);
         void* q = nullptr;
-        hipError_t e = hipHostMalloc(&q, nb, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&q, nb, flags);
         if (e != hipSuccess) return e;
         if (p) (void)hipHostFree(p);
         p = q;
@@ -183,6 +183,15 @@ struct JobBatch {
     StagedBatch ext{};     // ... or an explicit batch (restore image) bucketed at ext_bits
     int ext_bits = 0;
 };
+struct PassState {
+    IngestParams p{};
+    std::unique_ptr<Staged> s;
+    bool two_pass = false, spec = false;
+    int64_t n = 0;
+    const uint8_t* vnull = nullptr;
+    int64_t flo = 0, fhi = 0;
+};
+
 struct MergeJob {
     std::vector<JobBatch> batches;
     std::vector<SliceTable*> srcs;
@@ -194,6 +203,17 @@ struct MergeJob {
 };
 
 }  // namespace
+
+// A batch whose first pass is queued but not yet finished on the host (deferred staging)
+struct PendingBatch {
+    bool active = false;
+    PassState ps;
+    int64_t n = 0;
+    const int64_t *key = nullptr, *ts = nullptr, *val = nullptr;
+    const uint8_t* vnull = nullptr;
+    int64_t flo = 0, fhi = 0;
+    int slot = -1;
+};
 
 struct fg_handle {
     int32_t kvt = 0;   // kernel value op (val_type | op << 2)
@@ -233,6 +253,7 @@ struct fg_handle {
 
     // ingest scratch
     DevBuf in_key, in_ts, in_val, in_null;
+    DevBuf in_rows, row_bad;   // fg_add_rows: host rows copied in; NULL key/rowtime + NULL value counts
     // FG_HOST batches: double-buffered H2D on a copy stream of its own, so that the copy of
     // batch i + 1 overlaps the kernels of batch i (the engine stream waits for the copy's
     // event; a buffer is rewritten only after the kernels that read it)
@@ -245,6 +266,13 @@ struct fg_handle {
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
     int64_t hv_max_chunks = 0;
     DevBuf hist, totals, scan_tmp, counters;
+    DevBuf plan_dev;          // k_scan_plan's lane plan (speculative pass 2)
+    HostBuf h_pass;           // coherent host memory k_scan_plan writes the pass's counters + plan to
+    unsigned long long pass_seq = 0;   // k_scan_plan's sequence word in h_pass
+    bool counters_clean = false;   // the device counters hold their initial values
+    bool speculate = true;    // FG_SPECULATE=0 turns the speculative pass 2 off (A/B)
+    PendingBatch pending;     // deferred first pass of the last batch
+    hipEvent_t ev_pending = nullptr;
     DevBuf sink;   // target of the stores of idle lanes (kernels keep their store counts static)
     HostBuf h_counters;
 
@@ -287,6 +315,7 @@ struct fg_handle {
     // stats
     int64_t records_in = 0, rows_fired = 0, flushes = 0;
     bool timing = false;
+    uint32_t timing_mask = ~0u;   // kernel classes bracketed with events (fg_set_kernel_timing)
     KStat kstat[K_NCLASS];
     std::vector<PendingEv> pend;
     std::vector<hipEvent_t> ev_pool;
@@ -354,13 +383,13 @@ struct KTimer {
     int64_t records;
     hipEvent_t a = nullptr;
     KTimer(fg_handle* hh, int c, int64_t r) : h(hh), cls(c), records(r) {
-        if (h->timing) {
+        if (h->timing && ((h->timing_mask >> cls) & 1u)) {
             a = ev_get(h);
             (void)hipEventRecord(a, h->stream);
         }
     }
     ~KTimer() {
-        if (!h->timing) return;
+        if (!a) return;
         hipEvent_t b = ev_get(h);
         (void)hipEventRecord(b, h->stream);
         h->pend.push_back(PendingEv{cls, a, b, records});
@@ -1219,10 +1248,19 @@ int ensure_scratch(fg_handle* h) {
     return FG_OK;
 }
 
-int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
-                const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+// One ingest pass in two halves: ingest_launch queues pass 1 (or the count pass), the bucket
+// scan and -- speculatively -- pass 2 with the device's lane plan, then the counters' copy to
+// the host; ingest_finish takes the host's decisions once the counters are there (flushes,
+// the regular pass 2 when the plan said no, the lanes' bookkeeping).
+
+int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                  const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, PassState& ps) {
     if (int rc0 = ensure_scratch(h)) return rc0;
-    IngestParams p{};
+    ps.n = n;
+    ps.vnull = vnull;
+    ps.flo = flo;
+    ps.fhi = fhi;
+    IngestParams& p = ps.p;
     p.w = h->w;
     p.n = n;
     p.key = key;
@@ -1243,6 +1281,7 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     set_fast_path(h, &p);
     // two-pass partition when the regions split into 64-bucket coarse groups
     const bool two_pass = h->region_bits >= kFineBits && h->F <= kMaxPart1Fine;
+    ps.two_pass = two_pass;
     if (two_pass) {
         p.max_tiles = part1_max_tiles(n, p.grid);
         p.n_coarse = h->F >> kFineBits;
@@ -1259,7 +1298,8 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     init.qmin = JMAX;
     init.qmax = JMIN;
     init.qnext = JMAX;
-    HIPCHK(h, init_counters(h, init));
+    if (!h->counters_clean) HIPCHK(h, init_counters(h, init));   // (else reset by the last scan)
+    h->counters_clean = false;
     DevCounters* dc = h->counters.as<DevCounters>();
     p.drops = &dc->drops;
     p.lane_mask = &dc->lane_mask;
@@ -1275,36 +1315,86 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         KTimer kt(h, K_COUNT, n);
         HIPCHK(h, launch_ingest_count(p, h->stream));
     }
-    HIPCHK(h, hipMemcpyAsync(h->h_counters.p, h->counters.p, sizeof(DevCounters), hipMemcpyDeviceToHost, h->stream));
     // per-bucket prefix over workgroups and bucket bases: they depend on the histogram only,
     // so they are queued before the host waits for the counters (no idle GPU across the
     // round trip); a pass that stages nothing goes back to the pool
-    std::unique_ptr<Staged> s;
+    std::unique_ptr<Staged>& s = ps.s;
     if (!h->pass_pool.empty()) {
         s = std::move(h->pass_pool.back());
         h->pass_pool.pop_back();
     } else {
         s.reset(new Staged());
     }
-    struct PoolBack {
+    const int Fp = p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
+    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (Fp + 1)));
+    // Speculative pass 2 (two-pass partition): the lane decision the host takes below is
+    // taken on the device from pass 1's counters (k_scan_plan), and pass 2 is queued at
+    // once, so the GPU does not idle across the counters' round trip. When the batch needs a
+    // flush first (another slice in a lane, no room) the plan says so and pass 2 does
+    // nothing; the host then takes the regular path below.
+    const bool spec = two_pass && h->speculate;
+    ps.spec = spec;
+    {
+        // per-bucket prefix over workgroups, then one workgroup: bucket bases, the counters
+        // to the host (reset for the next pass), the lane plan
+        KTimer kt(h, K_SCAN, 0);
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), Fp, p.grid, h->stream));
+        PlanParams pp{};
+        pp.lane_cap = h->lane_cap;
+        for (int l = 0; l < kMaxLanes; l++) {
+            pp.q[l] = l < h->lanes ? h->lane[l].q : kEmptyLane;
+            pp.fill[l] = l < h->lanes ? h->lane[l].fill : 0;
+        }
+        ScanPlanArgs sa{};
+        sa.totals = h->totals.as<uint32_t>();
+        sa.bucket_off = s->bucket_off.as<uint32_t>();
+        sa.F = Fp;
+        sa.n_words = (int32_t)(sizeof(DevCounters) / 8);
+        sa.counters = h->counters.as<unsigned long long>();
+        sa.host = h->h_pass.as<unsigned long long>();
+        sa.reset.n = sa.n_words;
+        std::memcpy(sa.reset.v, &init, sizeof init);
+        sa.do_plan = spec ? 1 : 0;
+        sa.plan = h->plan_dev.as<IngestPlan>();
+        sa.seq = ++h->pass_seq;   // settle_pending polls for it (no event between the kernels)
+        HIPCHK(h, launch_scan_plan(p, pp, sa, h->stream));
+        h->counters_clean = true;
+    }
+    if (spec) {
+        IngestParams q = p;
+        q.bucket_base = s->bucket_off.as<uint32_t>();
+        // one lane's units: each workgroup takes its unit of every lane the plan finds active
+        for (int l = 0; l < kMaxLanes; l++) q.lane_slot[l] = l == 0 ? 0 : -1;
+        q.st_stride = h->st_stride;
+        q.st_rec = h->st_rec.as<int64_t>();
+        q.st_null = vnull ? h->st_null.as<uint8_t>() : nullptr;
+        if (h->cfg.val_type == FG_VAL_NONE) q.val = nullptr;
+        q.plan = h->plan_dev.as<IngestPlan>();
+        KTimer kt(h, K_PART2, n);
+        HIPCHK(h, launch_part2(q, h->stream));
+    }
+    return FG_OK;
+}
+
+int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
+    IngestParams& p = ps.p;
+    std::unique_ptr<Staged>& s = ps.s;
+    struct PoolBack {   // a pass that stages nothing goes back to the pool
         fg_handle* h;
         std::unique_ptr<Staged>& s;
         ~PoolBack() {
             if (s) h->pass_pool.push_back(std::move(s));
         }
     } pool_back{h, s};
-    const int Fp = p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
-    HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (Fp + 1)));
-    {
-        KTimer kt(h, K_SCAN, 0);
-        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), Fp, p.grid, h->stream));
-        HIPCHK(h, launch_scan_u32(h->totals.as<uint32_t>(), s->bucket_off.as<uint32_t>(), Fp,
-                                  h->scan_tmp.as<uint32_t>(), h->stream));
-    }
-    int rc = sync(h);
-    if (rc) return rc;
-    DevCounters got;
-    std::memcpy(&got, h->h_counters.p, sizeof got);
+    const bool two_pass = ps.two_pass, spec = ps.spec;
+    const uint8_t* vnull = ps.vnull;
+    const int64_t n = ps.n, flo = ps.flo, fhi = ps.fhi;
+    int rc = FG_OK;
+    DevCounters got;   // written by k_scan_plan into host-visible memory
+    std::memcpy(&got, h->h_pass.p, sizeof got);
+    IngestPlan plan{};
+    if (spec) std::memcpy(&plan, h->h_pass.as<char>() + sizeof(DevCounters), sizeof plan);
+    const bool staged_by_plan = spec && plan.ok;
     out->drops = got.drops;
     out->qmin = got.qmin;
     out->qmax = got.qmax;
@@ -1326,6 +1416,15 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
         if (got.lane_mask >> l & 1) out->lane_min[l] = out->lane_max[l] = q;
     }
 
+    if (staged_by_plan) {   // pass 2 ran with the device's decision: the host's is the same
+        for (int l = 0; l < h->lanes; l++) {
+            if (out->lane_total[l] == 0) continue;
+            const Lane& ln = h->lane[l];
+            if (out->lane_total[l] > h->lane_cap ||
+                (ln.q != kEmptyLane && (ln.q != out->lane_min[l] || ln.fill + out->lane_total[l] > h->lane_cap)))
+                return h->fail(FG_ESTATE, "internal: device lane plan disagrees with the host (lane %d)", l);
+        }
+    }
     // make room: a lane holding another slice, or without space for the batch's records,
     // is flushed into its slice table first (the EOFException flush of RecordsWindowBuffer
     // :91-96, per lane)
@@ -1383,7 +1482,9 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     p.st_rec = h->st_rec.as<int64_t>();
     p.st_null = vnull ? h->st_null.as<uint8_t>() : nullptr;
     if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
-    if (two_pass) {
+    if (staged_by_plan) {
+        // (already staged by the speculative pass 2 at these positions)
+    } else if (two_pass) {
         KTimer kt(h, K_PART2, n);
         HIPCHK(h, launch_part2(p, h->stream));
     } else {
@@ -1408,6 +1509,16 @@ int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, 
     if (s->refs > 0) h->passes.push_back(std::move(s));
     else h->pass_pool.push_back(std::move(s));
     return FG_OK;
+}
+
+int ingest_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+    PassState ps;
+    int rc = ingest_launch(h, n, key, ts, val, vnull, flo, fhi, count_drops, ps);
+    if (rc) return rc;
+    rc = sync(h);
+    if (rc) return rc;
+    return ingest_finish(h, ps, out);
 }
 
 // grow the per-lane accumulator areas to `need` rows per lane (all lanes free of acc rows)
@@ -1454,6 +1565,7 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     init.qmax = JMIN;
     init.qnext = JMAX;
     HIPCHK(h, init_counters(h, init));
+    h->counters_clean = false;
     DevCounters* dc = h->counters.as<DevCounters>();
     p.drops = &dc->drops;
     p.lane_mask = &dc->lane_mask;
@@ -1630,6 +1742,72 @@ int validate(const fg_config* c, std::string* msg) {
     return FG_OK;
 }
 
+// The host half of fg_add_batch once the first pass's counters are on the host: its
+// decisions (the regular pass 2 when the device's plan said no), the filtered passes for
+// the slices outside the first pass's filter, the late-drop count.
+int finish_batch(fg_handle* h) {
+    PendingBatch& pb = h->pending;
+    struct SlotFree {   // every kernel reading the slot's buffers is queued when this runs
+        fg_handle* h;
+        int slot;
+        ~SlotFree() {
+            if (slot >= 0) (void)hipEventRecord(h->ev_free[slot], h->stream);
+        }
+    } slot_free{h, pb.slot};
+    pb.slot = -1;
+    const int64_t n = pb.n, flo = pb.flo, fhi = pb.fhi;
+    const int64_t *key = pb.key, *ts = pb.ts, *val = pb.val;
+    const uint8_t* vnull = pb.vnull;
+    Counters c{};
+    int rc = ingest_finish(h, pb.ps, &c);
+    pb.ps = PassState{};
+    h->late_dropped += (int64_t)c.drops;
+    if (rc != FG_OK && rc != -1) return rc;
+    if (c.qmin > c.qmax) return FG_OK;   // nothing accepted
+    h->q_guess = (uint64_t)(c.qmax - c.qmin) >= (uint64_t)h->lanes ? c.qmin : kEmptyLane;
+    std::vector<std::pair<int64_t, int64_t>> rest;   // slice ranges [a, b) still to stage
+    if (rc == -1) {
+        rest.push_back({c.qmin, c.qmax + 1});
+    } else {
+        if (c.qmin < flo) rest.push_back({c.qmin, flo});
+        if (c.qmax >= fhi) rest.push_back({c.qnext, c.qmax + 1});   // qnext: first occupied slice >= fhi
+    }
+    // Each filtered pass reports the next occupied slice above its filter, so empty
+    // stretches (a far-future or ancient outlier record) cost no passes.
+    for (auto& r : rest) {
+        int64_t lo = r.first;
+        while (lo < r.second) {
+            Counters c2{};
+            const int64_t hi = std::min<int64_t>(lo + h->lanes, r.second);
+            rc = ingest_pass(h, n, key, ts, val, vnull, lo, hi, false, &c2);
+            if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
+            if (rc) return rc;
+            lo = c2.qnext;   // JMAX when nothing lies above hi
+        }
+    }
+    return FG_OK;
+}
+
+// Every entry point first completes a deferred batch (its counters were copied behind
+// pass 1's plan, so the wait is usually over before pass 2 ends).
+int settle_pending(fg_handle* h) {
+    if (!h->pending.active) return FG_OK;
+    h->pending.active = false;
+    // k_scan_plan writes its sequence word into coherent host memory after the counters and
+    // the plan: poll for it (pass 1 is done by then; pass 2 still runs). A stream error or a
+    // lost write falls back to synchronizing the stream.
+    const volatile unsigned long long* sq = reinterpret_cast<const volatile unsigned long long*>(
+        h->h_pass.as<char>() + sizeof(DevCounters) + sizeof(IngestPlan));
+    for (int64_t spin = 0; *sq != h->pass_seq; spin++) {
+        if (spin > (1 << 12) && hipStreamQuery(h->stream) != hipErrorNotReady) {
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            if (*sq != h->pass_seq) return h->fail(FG_EDEVICE, "internal: pass counters never arrived");
+            break;
+        }
+    }
+    return finish_batch(h);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1730,6 +1908,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     h->proctime = proctime;
     h->device = cfg->device_id;
     h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
+    if (const char* e = getenv("FG_KERNEL_TIMING")) h->timing = h->timing && std::atoi(e) != 0;   // A/B of the events' cost
     if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         g_open_error = "hipSetDevice/hipStreamCreate failed";
         return FG_EDEVICE;
@@ -1814,11 +1993,19 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
               chk(hp->hist.ensure(4 * (size_t)hp->F * hp->grid)) &&
               chk(hp->totals.ensure(4 * ((size_t)hp->F + 1))) &&
               chk(hp->scan_tmp.ensure(4 * scan_tmp_words((int64_t)hp->F))) &&
-              chk(hp->counters.ensure(sizeof(Counters))) && chk(hp->h_counters.ensure(sizeof(Counters))) &&
+              chk(hp->counters.ensure(sizeof(Counters))) &&
+              chk(hp->h_counters.ensure(sizeof(Counters) + sizeof(IngestPlan))) &&
+              chk(hp->plan_dev.ensure(sizeof(IngestPlan))) && chk(hp->row_bad.ensure(16)) &&
+              chk(hp->h_pass.ensure(sizeof(DevCounters) + sizeof(IngestPlan) + 8, hipHostMallocCoherent)) &&
               chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) && chk(hp->sink.ensure(256)) &&
               chk(hp->h_scalars.ensure(64)) && chk(hp->fail_list.ensure(4 * (size_t)kFailCap));
     if (!ok) {
         g_open_error = "device allocation failed";
+        return FG_EDEVICE;
+    }
+    if (const char* e = getenv("FG_SPECULATE")) hp->speculate = std::atoi(e) != 0;
+    if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
+        g_open_error = "hipEventCreate failed";
         return FG_EDEVICE;
     }
     *out = h.release();
@@ -1832,6 +2019,7 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     if (!b->key || !b->rowtime) return h->fail(FG_EINVAL, "batch key/rowtime columns are required");
     if (h->cfg.val_type != FG_VAL_NONE && !b->val) return h->fail(FG_EINVAL, "batch value column is required");
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     maybe_reduce_lanes(h);
     const int64_t n = b->n;
     const int64_t *key = b->key, *ts = b->rowtime;
@@ -1907,38 +2095,98 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     // (out-of-order jitter, long batches), the `lanes` slices from the previous batch's
     // first one. Slices outside the pass's filter are staged by filtered passes of `lanes`
     // slices each; a lane holding another slice is flushed to its table first (ingest_pass).
-    Counters c{};
-    int64_t flo = JMIN, fhi = JMAX;
+    PendingBatch& pb = h->pending;
+    pb.ps = PassState{};
+    pb.n = n;
+    pb.key = key;
+    pb.ts = ts;
+    pb.val = val;
+    pb.vnull = vnull;
+    pb.slot = slot;
+    slot_free.slot = -1;   // recorded by finish_batch, after the last kernel reading the slot
+    pb.flo = JMIN;
+    pb.fhi = JMAX;
     if (h->q_guess != kEmptyLane) {
-        flo = h->q_guess;
-        fhi = flo + h->lanes;
+        pb.flo = h->q_guess;
+        pb.fhi = pb.flo + h->lanes;
     }
-    int rc = ingest_pass(h, n, key, ts, val, vnull, flo, fhi, true, &c);
-    h->late_dropped += (int64_t)c.drops;
-    if (rc != FG_OK && rc != -1) return rc;
-    if (c.qmin > c.qmax) return FG_OK;   // nothing accepted
-    h->q_guess = (uint64_t)(c.qmax - c.qmin) >= (uint64_t)h->lanes ? c.qmin : kEmptyLane;
-    std::vector<std::pair<int64_t, int64_t>> rest;   // slice ranges [a, b) still to stage
-    if (rc == -1) {
-        rest.push_back({c.qmin, c.qmax + 1});
-    } else {
-        if (c.qmin < flo) rest.push_back({c.qmin, flo});
-        if (c.qmax >= fhi) rest.push_back({c.qnext, c.qmax + 1});   // qnext: first occupied slice >= fhi
+    int rc = ingest_launch(h, n, key, ts, val, vnull, pb.flo, pb.fhi, true, pb.ps);
+    if (rc) {
+        if (slot >= 0) (void)hipEventRecord(h->ev_free[slot], h->stream);
+        return rc;
     }
-    // Each filtered pass reports the next occupied slice above its filter, so empty
-    // stretches (a far-future or ancient outlier record) cost no passes.
-    for (auto& r : rest) {
-        int64_t lo = r.first;
-        while (lo < r.second) {
-            Counters c2{};
-            const int64_t hi = std::min<int64_t>(lo + h->lanes, r.second);
-            rc = ingest_pass(h, n, key, ts, val, vnull, lo, hi, false, &c2);
-            if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
-            if (rc) return rc;
-            lo = c2.qnext;   // JMAX when nothing lies above hi
-        }
+    if (pb.ps.spec) {
+        // Deferred: pass 2 is queued with the device's lane plan; the host takes the
+        // counters at its next call on the handle (settle_pending: ev_pending follows the
+        // scan, so it waits for pass 1 only) while the GPU runs pass 2 -- no round trip inside
+        // the batch.
+        pb.active = true;
+        return FG_OK;
     }
-    return FG_OK;
+    rc = sync(h);
+    if (rc) return rc;
+    return finish_batch(h);
+}
+
+int fg_add_rows(fg_handle* h, const fg_row_batch* b) {
+    if (!h || !b) return FG_EINVAL;
+    if (b->n <= 0) return FG_OK;
+    if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 rows");
+    if (!b->rows) return h->fail(FG_EINVAL, "rows pointer is required");
+    // BinaryRowData.calculateBitSetWidthInBytes / calculateFixPartSizeInBytes (:70-76)
+    const int64_t bits_w = ((int64_t)b->arity + 63 + 8) / 64 * 8;
+    const int64_t fixed = bits_w + 8 * (int64_t)b->arity;
+    const bool has_val = h->cfg.val_type != FG_VAL_NONE;
+    auto field_ok = [&](int32_t f) { return f >= 0 && f < b->arity; };
+    if (b->arity < 1 || !field_ok(b->key_field) || !field_ok(b->rowtime_field))
+        return h->fail(FG_EINVAL, "row layout: arity %d, key field %d, rowtime field %d", b->arity, b->key_field,
+                       b->rowtime_field);
+    if (has_val ? !field_ok(b->val_field) : b->val_field != -1)
+        return h->fail(FG_EINVAL, "row layout: value field %d (val_type %d)", b->val_field, h->cfg.val_type);
+    if (b->stride < fixed || b->stride % 8 != 0)
+        return h->fail(FG_EINVAL, "row stride %d: at least the fixed-length part (%lld bytes), a multiple of 8",
+                       b->stride, (long long)fixed);
+    HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
+    const int64_t n = b->n;
+    const uint8_t* rows = b->rows;
+    if (b->location == FG_HOST) {
+        HIPCHK(h, h->in_rows.ensure((size_t)n * b->stride));
+        HIPCHK(h, hipMemcpyAsync(h->in_rows.p, rows, (size_t)n * b->stride, hipMemcpyHostToDevice, h->stream));
+        rows = h->in_rows.as<uint8_t>();
+    }
+    RowLayout L{};
+    L.stride = b->stride;
+    L.key_off = (int32_t)(bits_w + 8 * b->key_field);
+    L.ts_off = (int32_t)(bits_w + 8 * b->rowtime_field);
+    L.val_off = has_val ? (int32_t)(bits_w + 8 * b->val_field) : -1;
+    L.key_bit = 8 + b->key_field;   // HEADER_SIZE_IN_BITS + field (:155-157)
+    L.ts_bit = 8 + b->rowtime_field;
+    L.val_bit = has_val ? 8 + b->val_field : 0;
+    HIPCHK(h, h->in_key.ensure(8 * (size_t)n));
+    HIPCHK(h, h->in_ts.ensure(8 * (size_t)n));
+    if (has_val) {
+        HIPCHK(h, h->in_val.ensure(8 * (size_t)n));
+        HIPCHK(h, h->in_null.ensure((size_t)n));
+    }
+    unsigned long long* bad = h->row_bad.as<unsigned long long>();
+    HIPCHK(h, hipMemsetAsync(bad, 0, 16, h->stream));
+    HIPCHK(h, launch_rows_to_columns(rows, n, L, h->in_key.as<int64_t>(), h->in_ts.as<int64_t>(),
+                                     has_val ? h->in_val.as<int64_t>() : nullptr,
+                                     has_val ? h->in_null.as<uint8_t>() : nullptr, bad, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->h_counters.p, bad, 16, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    unsigned long long cnt[2];
+    std::memcpy(cnt, h->h_counters.p, sizeof cnt);
+    if (cnt[0]) return h->fail(FG_EINVAL, "%llu rows with a NULL key or rowtime", cnt[0]);
+    fg_batch cb{};
+    cb.n = n;
+    cb.location = FG_DEVICE;
+    cb.key = h->in_key.as<int64_t>();
+    cb.rowtime = h->in_ts.as<int64_t>();
+    cb.val = has_val ? h->in_val.as<int64_t>() : nullptr;
+    cb.val_null = has_val && cnt[1] ? h->in_null.as<uint8_t>() : nullptr;   // no NULLs: the plain path
+    return fg_add_batch(h, &cb);
 }
 
 int fg_add_partials(fg_handle* h, const fg_partials* b) {
@@ -1949,6 +2197,7 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
         return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     maybe_reduce_lanes(h);
     const int64_t n = b->n;
     const int64_t *key = b->key, *se = b->slice_end, *cs = b->cnt_star, *cv = b->cnt_val, *sum = b->sum;
@@ -1999,12 +2248,14 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
 int fg_flush(fg_handle* h) {
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     return flush(h);
 }
 
 int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows* fired) {
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     h->out_n = 0;
     h->pending_out = 0;
     h->out_count_reset = false;
@@ -2081,6 +2332,7 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
 int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark) {
     if (!h || !out) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     int rc = flush(h);
     if (rc) return rc;
     // region counts of every resident slice
@@ -2154,6 +2406,7 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
 int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     if (!h || !in) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     int rc = flush(h);
     if (rc) return rc;
     // group entries by slice, bucket by region on the host (restore is off the hot path)
@@ -2271,12 +2524,14 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
 
 int fg_late_dropped(fg_handle* h, int64_t* out) {
     if (!h || !out) return FG_EINVAL;
+    if (int rc0 = settle_pending(h)) return rc0;
     *out = h->late_dropped;
     return FG_OK;
 }
 
 int fg_get_stats(fg_handle* h, fg_stats* out) {
     if (!h || !out) return FG_EINVAL;
+    if (int rc0 = settle_pending(h)) return rc0;
     out->records_in = h->records_in;
     out->records_staged = staged_records(h);
     out->late_dropped = h->late_dropped;
@@ -2290,12 +2545,14 @@ int fg_get_stats(fg_handle* h, fg_stats* out) {
 
 int fg_synchronize(fg_handle* h) {
     if (!h) return FG_EINVAL;
+    if (int rc0 = settle_pending(h)) return rc0;
     return sync(h, true);
 }
 
 int fg_reset(fg_handle* h) {
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
+    if (int rc0 = settle_pending(h)) return rc0;
     int rc = sync(h);
     if (rc) return rc;
     std::vector<int64_t> ends;
@@ -2315,6 +2572,7 @@ int fg_reset(fg_handle* h) {
 
 int fg_kernel_stats(fg_handle* h, fg_kernel_stat* out, int32_t max, int32_t* count) {
     if (!h || !count) return FG_EINVAL;
+    if (int rc0 = settle_pending(h)) return rc0;
     int rc = sync(h, true);
     if (rc) return rc;
     *count = K_NCLASS;
@@ -2326,6 +2584,12 @@ int fg_kernel_stats(fg_handle* h, fg_kernel_stat* out, int32_t max, int32_t* cou
         out[c].records = h->kstat[c].records;
         out[c].rows = h->kstat[c].rows;
     }
+    return FG_OK;
+}
+
+int fg_set_kernel_timing(fg_handle* h, uint32_t class_mask) {
+    if (!h) return FG_EINVAL;
+    h->timing_mask = class_mask;
     return FG_OK;
 }
 
@@ -2350,6 +2614,7 @@ void fg_close(fg_handle* h) {
         h->ev_pool.push_back(p.b);
     }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->ev_pending) (void)hipEventDestroy(h->ev_pending);
     for (int i = 0; i < 2; i++) {
         if (h->ev_copied[i]) (void)hipEventDestroy(h->ev_copied[i]);
         if (h->ev_free[i]) (void)hipEventDestroy(h->ev_free[i]);

@@ -116,6 +116,23 @@ struct IngestParams {
     int32_t max_tiles;         // tiles per workgroup segment (ceil(segment / kPart1Tile))
     int32_t n_coarse;          // lanes << (region_bits - kFineBits)
     int64_t* sink;             // >= 32 B of scratch: idle lanes store here (static store counts)
+    // speculative pass 2 (launched right after pass 1, no host round trip): the staged
+    // positions come from k_ingest_plan's verdict instead of lane_shift; not ok -> no-op
+    const struct IngestPlan* plan;
+};
+
+// Lane decision of one ingest pass taken on the device (k_ingest_plan) from pass 1's
+// counters and the host's lane state, exactly as the host takes it (fg_engine.cpp
+// ingest_pass): ok iff the pass's slices fit the lanes without a flush.
+struct IngestPlan {
+    int32_t ok;
+    int32_t active;            // bit l: lane l receives records (the counters are reset by then)
+    int64_t lane_shift[kMaxLanes];
+};
+struct PlanParams {
+    int64_t lane_cap;
+    int64_t q[kMaxLanes];      // slice index a lane holds (INT64_MIN: empty)
+    int64_t fill[kMaxLanes];   // records staged in the lane
 };
 
 constexpr int kMaxMergeBatches = 32;         // pipelined merge: staged batches held in LDS
@@ -238,12 +255,39 @@ hipError_t launch_store_words(unsigned long long* dst, const Words16& w, hipStre
 hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,
                                      int64_t* out, unsigned long long* off_grid, hipStream_t s);
 hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStream_t s);
+// packed BinaryRowData fixed-length parts -> key / rowtime / value / NULL columns; bad[0]
+// counts rows whose key or rowtime is NULL, bad[1] NULL values
+struct RowLayout {
+    int32_t stride, key_off, ts_off, val_off;   // byte offsets of the fields (val_off < 0: none)
+    int32_t key_bit, ts_bit, val_bit;           // null-bit indices (8 + field)
+    int32_t pad;
+};
+hipError_t launch_rows_to_columns(const uint8_t* rows, int64_t n, const RowLayout& L, int64_t* key, int64_t* ts,
+                                  int64_t* val, uint8_t* vnull, unsigned long long* bad, hipStream_t s);
 // two-pass partition: pass 1 does the count pass's work (drops, slice range, lane totals,
 // fine histogram per workgroup) while sorting tiles by coarse bucket into p.tmp / p.dir
 hipError_t launch_part1(const IngestParams& p, hipStream_t s);
 // pass 2: one workgroup per (active coarse bucket, pass-1 workgroup); p.bucket_base, p.hist
 // (column prefixes), p.lane_shift and p.lane_slot as for the scatter
 hipError_t launch_part2(const IngestParams& p, hipStream_t s);
+// After pass 1 (or the count pass) and k_hist_columns, one workgroup: the exclusive scan of
+// the bucket totals into bucket_off[F + 1]; the pass's counter words (`counters`, n_words)
+// copied to host-visible memory `host` and reset to `reset` for the next pass; with `pp`,
+// the lane plan of the speculative pass 2 (into plan, and after the counters in `host`).
+struct ScanPlanArgs {
+    const uint32_t* totals;
+    uint32_t* bucket_off;
+    int32_t F;
+    int32_t n_words;
+    unsigned long long* counters;
+    unsigned long long* host;          // n_words counter words, then an IngestPlan
+    Words16 reset;
+    int32_t do_plan;
+    int32_t pad;
+    IngestPlan* plan;
+    unsigned long long seq;            // written after everything else: the host polls for it
+};
+hipError_t launch_scan_plan(const IngestParams& p, const PlanParams& pp, const ScanPlanArgs& a, hipStream_t s);
 int32_t part1_max_tiles(int64_t n, int32_t grid);
 hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s);   // picks the variant by p.sorted
 // exclusive scan of n u32 (n < 2^32 total); out has n + 1 entries; tmp >= scan_tmp_words(n)

@@ -677,12 +677,25 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     const int ca = blockIdx.x / ngroups;
     const int g0 = gi * group;
     const int g1 = g0 + group < p.grid ? g0 + group : p.grid;
+    // regular launch: one unit per workgroup, slot ca / cpl; speculative launch (p.plan): one
+    // lane's units, each workgroup taking its unit of every lane the plan found active
     int lane = 0;
-    {
+    uint32_t more = 0;   // further active lanes (speculative launch)
+    int64_t lane_shift;
+    if (p.plan) {
+        if (!gbl(&p.plan->ok)[0]) return;
+        more = (uint32_t)gbl(&p.plan->active)[0];
+        if (!more) return;
+        lane = __ffs(more) - 1;
+        more &= more - 1;
+        lane_shift = gbl(p.plan->lane_shift)[lane];
+    } else {
         const int sl = ca / cpl;
         for (int l = 0; l < kMaxLanes; l++)
             if (p.lane_slot[l] == sl) lane = l;
+        lane_shift = p.lane_shift[lane];
     }
+    for (;;) {   // (one iteration per lane; the body keeps its original indentation)
     const int cl = ca % cpl;
     const int c = lane * cpl + cl;
     // fragment q = (workgroup g0 + q / MT, tile q % MT); missing tiles are empty fragments
@@ -715,7 +728,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     }
     if (tid < NF) {
         const int b = lane * P + cl * NF + tid;
-        s_cur[tid] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)g0 * F + b] + p.lane_shift[lane]);
+        s_cur[tid] = (uint32_t)((int64_t)p.bucket_base[b] + p.hist[(int64_t)g0 * F + b] + lane_shift);
         s_cnt[tid] = 0;
     }
     __syncthreads();
@@ -863,6 +876,109 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
         if (base + kPart2Tile >= total) break;
         step(rb, nb, ra, na, base + kPart2Tile);
     }
+    if (!more) break;
+    lane = __ffs(more) - 1;   // the next active lane's unit (speculative launch)
+    more &= more - 1;
+    lane_shift = gbl(p.plan->lane_shift)[lane];
+    __syncthreads();
+    }
+}
+
+// The host's lane decision of ingest_pass, restated (pass 1's counters against the lane
+// state handed over in pp): ok iff the accepted slices inside the filter span fewer slices
+// than lanes and every active lane is empty or holds that slice with room left.
+__device__ void ingest_plan(const IngestParams& p, const PlanParams& pp, long long qmin, long long qmax,
+                            unsigned long long mask, const unsigned long long* lane_total, IngestPlan* out) {
+    int ok = 1;
+    if (qmin <= qmax) {
+        const long long fq0 = qmin > p.filter_lo ? qmin : p.filter_lo;
+        const long long fq1 = qmax < p.filter_hi - 1 ? qmax : p.filter_hi - 1;
+        if (fq0 <= fq1) {
+            if ((unsigned long long)(fq1 - fq0) >= (unsigned long long)p.lanes) {
+                ok = 0;
+            } else {
+                for (int l = 0; l < p.lanes; l++) {
+                    const long long tot = (long long)lane_total[l];
+                    if (tot == 0) continue;
+                    long long ql = JMAX;   // the lane's slice among [fq0, fq1]
+                    for (long long q = fq0; q <= fq1; q++)
+                        if ((int)(q & (p.lanes - 1)) == l && ((mask >> l) & 1)) ql = q;
+                    if (tot > pp.lane_cap) ok = 0;
+                    if (pp.q[l] != JMIN && (pp.q[l] != ql || pp.fill[l] + tot > pp.lane_cap)) ok = 0;
+                }
+            }
+        }
+    }
+    int64_t before = 0;
+    int active = 0;
+    for (int l = 0; l < kMaxLanes; l++) {
+        out->lane_shift[l] = l < p.lanes ? (int64_t)l * pp.lane_cap + pp.fill[l] - before : 0;
+        if (l < p.lanes) before += (int64_t)lane_total[l];
+        if (l < p.lanes && lane_total[l] > 0) active |= 1 << l;
+    }
+    out->active = active;
+    out->ok = ok;
+}
+
+constexpr int kScanPlanThreads = 1024;
+__global__ __launch_bounds__(kScanPlanThreads) void k_scan_plan(IngestParams p, PlanParams pp, ScanPlanArgs a) {
+    __shared__ uint32_t s_wave[kScanPlanThreads / 64];
+    __shared__ unsigned long long s_words[16];
+    const int tid = threadIdx.x;
+    // 1) bucket bases: thread t scans a run of consecutive totals (loaded at once)
+    constexpr int kPer = kMaxStageBuckets / kScanPlanThreads;
+    const int per = (a.F + kScanPlanThreads - 1) / kScanPlanThreads;
+    const int b0 = tid * per;
+    uint32_t v[kPer];
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        v[j] = (j < per && b0 + j < a.F) ? a.totals[b0 + j] : 0u;
+        run += v[j];
+    }
+    uint32_t total;
+    uint32_t ex = block_exclusive_scan(run, s_wave, &total);
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+        if (j < per && b0 + j < a.F) a.bucket_off[b0 + j] = ex;
+        ex += v[j];
+    }
+    if (tid == 0) a.bucket_off[a.F] = total;
+    // 2) the pass's counters to the host, reset for the next pass; the lane plan
+    if (tid < a.n_words) s_words[tid] = a.counters[tid];
+    __syncthreads();
+    if (tid < a.n_words) {
+        a.host[tid] = s_words[tid];
+        if (tid < a.reset.n) a.counters[tid] = a.reset.v[tid];
+    }
+    if (tid == 0 && a.do_plan) {
+        // the counter words hold DevCounters (fg_engine.cpp): read through the pass's pointers'
+        // offsets into the block
+        auto word = [&](const void* q) {
+            return s_words[(reinterpret_cast<const char*>(q) - reinterpret_cast<const char*>(a.counters)) / 8];
+        };
+        const long long qmin = (long long)word(p.qmin), qmax = (long long)word(p.qmax);
+        const unsigned long long mask = word(p.lane_mask);
+        unsigned long long lt[kMaxLanes];
+        for (int l = 0; l < kMaxLanes; l++) lt[l] = word(p.lane_total + l);
+        IngestPlan pl;
+        ingest_plan(p, pp, qmin, qmax, mask, lt, &pl);
+        *a.plan = pl;
+        IngestPlan* hp = reinterpret_cast<IngestPlan*>(a.host + a.n_words);
+        *hp = pl;
+    }
+    if (tid == 0) {   // the host polls the sequence word (after the counters and the plan)
+        __threadfence_system();
+        volatile unsigned long long* sq = a.host + a.n_words + sizeof(IngestPlan) / 8;
+        *sq = a.seq;
+        __threadfence_system();
+    }
+}
+
+hipError_t launch_scan_plan(const IngestParams& p, const PlanParams& pp, const ScanPlanArgs& a, hipStream_t s) {
+    if (a.n_words < 1 || a.n_words > 16 || a.reset.n > a.n_words) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_scan_plan, dim3(1), dim3(kScanPlanThreads), 0, s, p, pp, a);
+    return hipGetLastError();
 }
 
 int32_t part1_max_tiles(int64_t n, int32_t grid) {
@@ -901,6 +1017,42 @@ __global__ void k_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz
         const int64_t e = slice_end[i];
         out[i] = e == JMAX ? JMAX : jsub(jsub(e, 1), tz);
     }
+}
+
+// Packed BinaryRowData rows (BinaryRowData.java:68-76): the fixed-length part of row i at
+// rows + i * stride; field f's null bit is bit 8 + f of the row's leading bit set (:155-157,
+// BinarySegmentUtils.bitGet :459-463), its 8 bytes at the bit set's width + 8 f (:119-121).
+// One thread per row; the row's 8-byte words are read as aligned 8-B loads.
+__global__ void k_rows_to_columns(const uint8_t* rows, int64_t n, RowLayout L, int64_t* key, int64_t* ts,
+                                  int64_t* val, uint8_t* vnull, unsigned long long* bad) {
+    unsigned long long nbad = 0, nnull = 0;   // rows with a NULL key or rowtime; NULL values
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint8_t* r = rows + i * (int64_t)L.stride;
+        auto bit = [&](int b) { return (r[b >> 3] >> (b & 7)) & 1; };
+        key[i] = *reinterpret_cast<const int64_t*>(r + L.key_off);
+        ts[i] = *reinterpret_cast<const int64_t*>(r + L.ts_off);
+        if (bit(L.key_bit) | bit(L.ts_bit)) nbad++;
+        if (L.val_off >= 0) {
+            val[i] = *reinterpret_cast<const int64_t*>(r + L.val_off);
+            const int nl = bit(L.val_bit);
+            vnull[i] = (uint8_t)nl;
+            nnull += (unsigned long long)nl;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        nbad += __shfl_down(nbad, off);
+        nnull += __shfl_down(nnull, off);
+    }
+    if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
+    if ((threadIdx.x & 63) == 0 && nnull) atomicAdd(bad + 1, nnull);
+}
+
+hipError_t launch_rows_to_columns(const uint8_t* rows, int64_t n, const RowLayout& L, int64_t* key, int64_t* ts,
+                                  int64_t* val, uint8_t* vnull, unsigned long long* bad, hipStream_t s) {
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(k_rows_to_columns, dim3((unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096)), dim3(256),
+                       0, s, rows, n, L, key, ts, val, vnull, bad);
+    return hipGetLastError();
 }
 
 // Windowed input (WindowedSliceAssigner): the attached window_end of a row is its slice,
@@ -976,31 +1128,42 @@ hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStr
 }
 
 // per bucket: exclusive prefix over workgroups (column of the workgroup-major histogram)
+// 64 buckets per workgroup, four threads per bucket: each sums a quarter of the workgroup
+// rows (held in registers), the quarter sums are scanned in LDS, then each thread writes its
+// rows' prefixes. F / 64 workgroups keep the chip's memory pipes busy (one thread per bucket
+// over all rows left three quarters of the CUs idle and serialized the loads).
+constexpr int kHcRows = 64;   // rows per thread held in registers (grid <= 4 * kHcRows)
 __global__ __launch_bounds__(256) void k_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= F) return;
+    __shared__ uint32_t s_q[4][64];
+    const int j = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int b = blockIdx.x * 64 + j;
+    const int per = (grid + 3) / 4;
+    const int g0 = q * per;
+    uint32_t v[kHcRows];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kHcRows; k++) {
+        const int g = g0 + k;
+        v[k] = (b < F && k < per && g < grid) ? hist[(int64_t)g * F + b] : 0u;
+        sum += v[k];
+    }
+    s_q[q][j] = sum;
+    __syncthreads();
     uint32_t run = 0;
-    int g = 0;
-    for (; g + 8 <= grid; g += 8) {
-        uint32_t c[8];
+    for (int k = 0; k < q; k++) run += s_q[k][j];
+    if (b >= F) return;
 #pragma unroll
-        for (int j = 0; j < 8; j++) c[j] = hist[(int64_t)(g + j) * F + b];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            hist[(int64_t)(g + j) * F + b] = run;
-            run += c[j];
-        }
+    for (int k = 0; k < kHcRows; k++) {
+        const int g = g0 + k;
+        if (k < per && g < grid) hist[(int64_t)g * F + b] = run;
+        run += v[k];
     }
-    for (; g < grid; g++) {
-        const uint32_t c = hist[(int64_t)g * F + b];
-        hist[(int64_t)g * F + b] = run;
-        run += c;
-    }
-    totals[b] = run;
+    if (q == 3) totals[b] = run;
 }
 
 hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(k_hist_columns, dim3((F + 255) / 256), dim3(256), 0, s, hist, totals, F, grid);
+    if (grid > 4 * kHcRows) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hist_columns, dim3((F + 63) / 64), dim3(256), 0, s, hist, totals, F, grid);
     return hipGetLastError();
 }
 

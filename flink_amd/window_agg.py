@@ -204,6 +204,36 @@ class WindowAggOperator:
                 b.val_null = val_null.ctypes.data
             keep = [key, rowtime, val, val_null]
         L.check(self._lib.fg_add_batch(self._h, C.byref(b)), self._h)
+        # device columns stay in use until the next call on the handle (the engine may finish
+        # a batch's staging there): hold them until then
+        self._inflight = (key, rowtime, val, val_null) if kdev else None
+        del keep
+
+    def process_rows(self, rows, stride: int, arity: int, key_field: int = 0, rowtime_field: int = 1,
+                     val_field: int = 2):
+        """processElement for packed BinaryRowData rows (the fixed-length parts, `stride` bytes
+        apart: flink_amd.rows.pack_rows writes them as BinaryRowWriter does): a uint8 numpy
+        array / bytes on the host, or a uint8 device tensor."""
+        self._after_producers((rows,))
+        b = L.FgRowBatch()
+        rp, rdev, rows = _dev_ptr(rows)
+        keep = None
+        if rdev:
+            b.location = L.DEVICE
+            b.rows = rp
+            nbytes = int(rows.numel())
+        else:
+            keep = np.ascontiguousarray(np.frombuffer(rows, dtype=np.uint8) if isinstance(rows, (bytes, bytearray))
+                                        else rows, dtype=np.uint8)
+            b.location = L.HOST
+            b.rows = keep.ctypes.data
+            nbytes = keep.size
+        b.stride = int(stride)
+        b.n = nbytes // int(stride)
+        b.arity, b.key_field, b.rowtime_field = int(arity), int(key_field), int(rowtime_field)
+        b.val_field = int(val_field) if self.val_type != L.VAL_NONE else -1
+        L.check(self._lib.fg_add_rows(self._h, C.byref(b)), self._h)
+        self._inflight = rows if rdev else None
         del keep
 
     # -- global phase ----------------------------------------------------------------------------
@@ -337,6 +367,16 @@ class WindowAggOperator:
         L.check(self._lib.fg_kernel_stats(self._h, arr, 16, C.byref(n)), self._h)
         return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms,
                                            records=arr[i].records, rows=arr[i].rows) for i in range(n.value)}
+
+    def set_kernel_timing(self, classes=None):
+        """Time only the named kernel classes (names of kernel_stats); None: all."""
+        mask = 0xFFFFFFFF
+        if classes is not None:
+            names = list(self.kernel_stats())
+            mask = 0
+            for c in classes:
+                mask |= 1 << names.index(c)
+        L.check(self._lib.fg_set_kernel_timing(self._h, mask), self._h)
 
     def synchronize(self):
         L.check(self._lib.fg_synchronize(self._h), self._h)

@@ -12,6 +12,7 @@
  *     + SlicingWindowAggOperatorBuilder.build  .../SlicingWindowAggOperatorBuilder.java:127-170
  *   SlicingWindowOperator.processElement -> WindowProcessor.processElement
  *     TR/operators/window/slicing/SlicingWindowOperator.java:196-204     fg_add_batch
+ *     (packed BinaryRowData rows, TC/data/binary/BinaryRowData.java:68-76) fg_add_rows
  *     TR/operators/aggregate/window/processors/AbstractWindowAggProcessor.java:135-165
  *     (+ RecordsWindowBuffer.addElement  .../buffers/RecordsWindowBuffer.java:81-97)
  *   SlicingWindowOperator.processWatermark + onEventTime/onTimer
@@ -56,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 3
+#define FG_ABI_VERSION 4
 
 enum fg_status {
     FG_OK = 0,
@@ -85,8 +86,11 @@ enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
 enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3, FG_AGG_SUM0 = 4,
               FG_AGG_MIN = 5, FG_AGG_MAX = 6 };
 /* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
- * producer before it (complete, or an event the stream waits on). They are fully read when
- * fg_add_batch / fg_add_partials return. */
+ * producer before it (complete, or an event the stream waits on). fg_add_partials and
+ * fg_add_rows have read them when they return; fg_add_batch's columns stay in use until the
+ * next call on the handle returns (the engine finishes a batch's staging there, so that its
+ * two partition passes run back to back on the GPU); fg_synchronize releases them. FG_HOST
+ * buffers are copied before the call returns. */
 enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
 enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1 };
 enum fg_flags {
@@ -171,6 +175,26 @@ typedef struct fg_rows {
     const int64_t* rowtime;            /* DataStream: window.maxTimestamp() (end - 1); SQL: NULL */
 } fg_rows;
 
+/* Packed BinaryRowData input: the records as Flink holds them (BinaryRowData.java:68-76): row i
+ * is the fixed-length part of a BinaryRowData of `arity` fields at rows + i * stride -- a
+ * header byte (RowKind) and the null bits (bit 8 + f of the little-endian bit set marks field f
+ * NULL, :155-157) in calculateBitSetWidthInBytes(arity) = ((arity + 71) / 64) * 8 bytes, then
+ * 8 bytes per field (:119-121): BIGINT / DOUBLE as is (:306-320), TIMESTAMP(3) as its compact
+ * epoch millis (:347-352). A shim hands a MemorySegment of such rows (e.g. the serialized
+ * records of a network buffer or the RecordsWindowBuffer's pages) without building columns.
+ * A NULL value field is a NULL value; a NULL key or rowtime is FG_EINVAL (the columnar boundary
+ * has no NULL key either: the shim maps a nullable key to a BIGINT id). */
+typedef struct fg_row_batch {
+    int64_t n;
+    int32_t location;             /* fg_location of `rows` */
+    int32_t stride;               /* bytes between rows: >= the fixed-length part, a multiple of 8 */
+    const uint8_t* rows;
+    int32_t arity;                /* fields per row */
+    int32_t key_field;            /* BIGINT grouping key */
+    int32_t rowtime_field;        /* TIMESTAMP(3) event time */
+    int32_t val_field;            /* BIGINT or DOUBLE per fg_config.val_type; -1: none (FG_VAL_NONE) */
+} fg_row_batch;
+
 /* Partial accumulator rows entering the global phase (GlobalAggCombiner.combine,
  * combines/GlobalAggCombiner.java:77-110, fed through the `sliced` assigner,
  * SliceAssigners.java:494-533): the rows of a FG_FLAG_LOCAL_PARTIALS operator after the
@@ -222,6 +246,8 @@ typedef struct fg_handle fg_handle;
 
 int  fg_open(const fg_config* cfg, fg_handle** out);
 int  fg_add_batch(fg_handle* h, const fg_batch* batch);
+/* fg_add_batch for packed BinaryRowData rows (same semantics, same processElement per row). */
+int  fg_add_rows(fg_handle* h, const fg_row_batch* rows);
 /* Global phase: merge partial accumulators (late rules of the global operator apply to
  * the partial's slice). */
 int  fg_add_partials(fg_handle* h, const fg_partials* partials);
@@ -237,6 +263,10 @@ int  fg_synchronize(fg_handle* h);
 int  fg_reset(fg_handle* h);
 /* Copies up to `max` kernel statistics into out; *count receives the number available. */
 int  fg_kernel_stats(fg_handle* h, fg_kernel_stat* out, int32_t max, int32_t* count);
+/* With FG_FLAG_KERNEL_TIMING: bracket only the kernel classes whose bit is set (bit i = entry
+ * i of fg_kernel_stats' list); each bracket costs two events on the stream, so a measurement
+ * times the kernel it reports and leaves the others unperturbed. Default: all classes. */
+int  fg_set_kernel_timing(fg_handle* h, uint32_t class_mask);
 /* Device stream of the handle (hipStream_t), for callers that overlap their own work. */
 void* fg_stream(fg_handle* h);
 const char* fg_last_error(fg_handle* h);   /* h may be NULL: last error of fg_open */

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 3
+    assert lib.fg_abi_version() == 4
 
 
 def test_struct_layouts_match_header_sizes():
@@ -38,6 +38,24 @@ def test_struct_layouts_match_header_sizes():
     assert C.sizeof(L.FgRows) == 8 + 8 + 3 * 8 + 8 * 8 + 2 * 8
     assert C.sizeof(L.FgPartials) == 8 + 8 + 5 * 8
     assert C.sizeof(L.FgStateRows) == 8 + 5 * 8
+    assert C.sizeof(L.FgRowBatch) == 8 + 4 + 4 + 8 + 4 * 4
+
+
+def test_binary_row_layout():
+    """flink_amd.rows writes BinaryRowData fixed-length parts: the bit-set width of
+    calculateBitSetWidthInBytes (BinaryRowData.java:70-72: 8 bytes up to 56 fields, 16 from 57),
+    the null bit of field f at bit 8 + f (:155-157), 8 bytes per field after the bit set."""
+    import numpy as np
+
+    from flink_amd import rows as R
+    assert [R.bit_set_width(a) for a in (1, 3, 56, 57, 120, 121)] == [8, 8, 8, 16, 16, 24]
+    assert R.fixed_part_size(3) == 32
+    r = R.pack_rows([np.array([5, -1], dtype=np.int64), np.array([100, 200], dtype=np.int64),
+                     np.array([1.5, 2.5])], [None, None, np.array([False, True])], stride=40)
+    r = r.reshape(2, 40)
+    assert r[0, 0] == 0 and r[1, 1] == 1 << 2                       # field 2 NULL in row 1
+    assert r[0, 8:16].view(np.int64)[0] == 5 and r[1, 8:16].view(np.int64)[0] == -1
+    assert r[0, 24:32].view(np.float64)[0] == 1.5 and r[1, 24:32].view(np.int64)[0] == 0   # NULL: zero bytes
 
 
 AS = load_assigner_cases()

@@ -769,3 +769,46 @@ def test_outlier_slices_cost_no_empty_passes(oracle_mod, kind, outliers):
     assert time.time() - t0 < 60, "empty slice stretches were walked pass by pass"
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("case", ["tumble_f64_nulls", "hop_i64_padded", "cumulate_f64_device"])
+def test_binary_rows_parity(oracle_mod, case):
+    """fg_add_rows: the stream handed over as packed BinaryRowData rows (flink_amd.rows.pack_rows,
+    BinaryRowData.java:68-76) gives the oracle's rows -- NULL values through the null bits, wider
+    rows with the fields at other positions and padding, host and device rows."""
+    import torch
+
+    import flink_amd as F
+    from flink_amd.rows import pack_rows
+    kind, vt = {"tumble_f64_nulls": ("tumble", "f64"), "hop_i64_padded": ("hop", "i64"),
+                "cumulate_f64_device": ("cumulate", "f64")}[case]
+    cfg = cfg_of(kind, 1000 if kind == "tumble" else 3000, 0 if kind == "tumble" else 1000, vt=vt)
+    n, keys, batch = 200_000, 20_000, 20_000
+    key, ts, val, isnull = make_stream(n, keys, vt, jitter_ms=800, null_frac=0.15)
+    g = gpu_mk(cfg, expected_keys=keys, buffer_records=1 << 18)
+    o = oracle_mk(oracle_mod, cfg)
+    for lo, hi, wm in batches_with_watermarks(n, batch, ts, 100):
+        k, t, v, nl = key[lo:hi], ts[lo:hi], val[lo:hi], isnull[lo:hi]
+        if case == "hop_i64_padded":   # (pad, value, pad, rowtime, key) + 16 bytes of padding
+            z = np.zeros(hi - lo, dtype=np.int64)
+            rows = pack_rows([z, v, z, t, k], [None, nl, None, None, None], stride=72)
+            g.op.process_rows(rows, 72, 5, key_field=4, rowtime_field=3, val_field=1)
+        else:
+            rows = pack_rows([k, t, v], [None, None, nl])
+            if case == "cumulate_f64_device":
+                rows = torch.from_numpy(rows).cuda()
+            g.op.process_rows(rows, 32, 3)
+        o.process_batch(k, t, v, nl)
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), vt, f"wm {wm}")
+        assert g.late_dropped == o.late_dropped
+    g.process_watermark(JMAX)
+    o.process_watermark(JMAX)
+    assert_rows_equal(g.take_rows(), o.take_rows(), vt, "final")
+    # a NULL key is refused before any record is staged
+    bad = pack_rows([key[:10], ts[:10], val[:10]], [np.arange(10) == 3, None, None])
+    with pytest.raises(F.WindowSpecError):
+        g.op.process_rows(bad, 32, 3)
+    g.close()
+    o.close()
