@@ -200,6 +200,9 @@ struct MergeJob {
     int64_t wend = 0;
     int bits = 0;          // region bits of its last launch
     int kclass = 0;
+    // restore re-fire (MergeParams): marking / mark-only sources, marked emission, chain dst
+    uint64_t mark_mask = 0, markonly_mask = 0;
+    int emit_marked = 0, dst_mode = 0;
 };
 
 }  // namespace
@@ -288,6 +291,17 @@ struct fg_handle {
     HostBuf h_fail;
     int lanes_target = 0;   // lanes for the current region bits (reached once the upper lanes drain)
     int64_t grows = 0;
+    // Restore re-fire of shared windows (HOP / CUMULATE, refire()): records flushed after a
+    // restore into slices whose windows fired before the checkpoint are kept apart -- re_new
+    // their state, re_delta their keys since the last watermark -- and re-fire those windows
+    // for their keys only, chained as nextTriggerWindow chains the reference's timers.
+    int64_t refire_hi = JMIN;   // the checkpoint's timer watermark (JMIN: nothing to re-fire)
+    int64_t arrival_progress = JMIN;   // progress the staged records arrived under (set per advance)
+    int64_t refire_wm = JMIN;   // the watermark the re-fire ran at last
+    std::map<int64_t, std::unique_ptr<SliceTable>> re_new, re_delta;
+    std::unique_ptr<SliceTable> re_chain;   // keys whose chain continues at window re_chain_w
+    int64_t re_chain_w = JMIN;
+    std::vector<std::unique_ptr<SliceTable>> re_tmp;   // chain tables of the running re-fire
 
     // descriptor arena (device + pinned mirror), reset at every sync point
     DevBuf arena;
@@ -423,17 +437,9 @@ int sync(fg_handle* h, bool drain_timing = false) {
     return FG_OK;
 }
 
-int table_get(fg_handle* h, int64_t slice_end, bool create, SliceTable** out) {
-    auto it = h->tables.find(slice_end);
-    if (it != h->tables.end()) {
-        *out = it->second.get();
-        return FG_OK;
-    }
-    if (!create) {
-        *out = nullptr;
-        return FG_OK;
-    }
-    std::unique_ptr<SliceTable> t;
+// an empty slice table of the current layout (from the pool when one is free)
+int table_new(fg_handle* h, int64_t slice_end, std::unique_ptr<SliceTable>* out) {
+    std::unique_ptr<SliceTable>& t = *out;
     if (!h->table_pool.empty()) {
         t = std::move(h->table_pool.back());
         h->table_pool.pop_back();
@@ -446,6 +452,22 @@ int table_get(fg_handle* h, int64_t slice_end, bool create, SliceTable** out) {
     t->slice_end = slice_end;
     t->upper = 0;
     t->bits = h->region_bits;
+    return FG_OK;
+}
+
+int table_get(fg_handle* h, int64_t slice_end, bool create, SliceTable** out) {
+    auto it = h->tables.find(slice_end);
+    if (it != h->tables.end()) {
+        *out = it->second.get();
+        return FG_OK;
+    }
+    if (!create) {
+        *out = nullptr;
+        return FG_OK;
+    }
+    std::unique_ptr<SliceTable> t;
+    int rc = table_new(h, slice_end, &t);
+    if (rc) return rc;
     *out = t.get();
     h->tables[slice_end] = std::move(t);
     return FG_OK;
@@ -458,6 +480,25 @@ void table_free(fg_handle* h, int64_t slice_end) {
     if (h->defer_free) h->deferred.push_back(std::move(it->second));
     else h->table_pool.push_back(std::move(it->second));
     h->tables.erase(it);
+}
+
+bool refire_slice(const fg_handle* h, int64_t se) {
+    return h->refire_hi != JMIN && !h->local && se != JMAX && trigger_time(h->w, se) <= h->refire_hi;
+}
+
+SliceTable* side_get(std::map<int64_t, std::unique_ptr<SliceTable>>& m, int64_t se) {
+    auto it = m.find(se);
+    return it == m.end() ? nullptr : it->second.get();
+}
+
+int side_create(fg_handle* h, std::map<int64_t, std::unique_ptr<SliceTable>>& m, int64_t se, SliceTable** out) {
+    if ((*out = side_get(m, se))) return FG_OK;
+    std::unique_ptr<SliceTable> t;
+    int rc = table_new(h, se, &t);
+    if (rc) return rc;
+    *out = t.get();
+    m[se] = std::move(t);
+    return FG_OK;
 }
 
 TableRef ref_of(SliceTable* t) { return TableRef{t->data.as<int64_t>(), t->counts.as<uint32_t>()}; }
@@ -550,6 +591,10 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     p->fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 16);
     p->fail_cap = kFailCap;
     p->job = ji;
+    p->mark_mask = j.mark_mask;
+    p->markonly_mask = j.markonly_mask;
+    p->emit_marked = j.emit_marked;
+    p->dst_mode = j.dst_mode;
     return FG_OK;
 }
 
@@ -580,6 +625,12 @@ int grow(fg_handle* h, int nb) {
         if ((rc = split(kv.second.get()))) return rc;
     for (auto& t : h->deferred)
         if ((rc = split(t.get()))) return rc;
+    for (auto* m : {&h->re_new, &h->re_delta})
+        for (auto& kv : *m)
+            if ((rc = split(kv.second.get()))) return rc;
+    if (h->re_chain && (rc = split(h->re_chain.get()))) return rc;
+    for (auto& t : h->re_tmp)
+        if (t && (rc = split(t.get()))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     old.clear();
     h->table_pool.clear();   // pooled tables have the old layout
@@ -797,6 +848,36 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     for (int l : sel) {
         const Lane& ln = h->lane[l];
         const int64_t se = slice_end_of(h, ln.q);
+        if (refire_slice(h, se)) {
+            // after a restore, records of a slice whose windows fired before the checkpoint:
+            // their state (re_new) and their keys (re_delta, at the window their timer chain
+            // starts from: the slice's own, or for a record accepted late the first window not
+            // fired at its arrival, AbstractWindowAggProcessor.java:148-156)
+            SliceTable *T = nullptr, *D = nullptr;
+            rc = side_create(h, h->re_new, se, &T);
+            if (rc) return rc;
+            int64_t U = se;
+            while (U != JMAX && trigger_time(h->w, U) <= h->arrival_progress) U = jadd(U, h->w.slice);
+            rc = side_create(h, h->re_delta, U, &D);
+            if (rc) return rc;
+            for (SliceTable* x : {T, D}) {
+                MergeJob job;
+                for (Staged* st : ln.passes) job.batches.push_back(JobBatch{st, l, StagedBatch{}, 0});
+                if (x->upper > 0) job.srcs.push_back(x);
+                job.dst = x;
+                job.kclass = K_FLUSH;
+                int ji = 0;
+                rc = job_add(h, std::move(job), &ji);
+                if (rc) return rc;
+                MergeParams p{};
+                rc = job_params(h, ji, &p);
+                if (rc) return rc;
+                KTimer kt(h, K_FLUSH, ln.fill);
+                HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+                x->upper = std::min<int64_t>(x->upper + ln.fill + ln.acc_fill, kStateCapMax);
+            }
+            continue;
+        }
         SliceTable* t = nullptr;
         rc = table_get(h, se, true, &t);
         if (rc) return rc;
@@ -1152,6 +1233,232 @@ int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired) {
             }
         }
     }
+    return FG_OK;
+}
+
+// ---- restore re-fire of shared windows (HOP, CUMULATE) -------------------------------
+// After initializeState the reference's timer service restarts at Long.MIN_VALUE: a record
+// older than the checkpoint's watermark is not late, its flush registers the timer of its
+// slice's window (AggCombiner step 5), and onTimer chains the key on through
+// nextTriggerWindow -- HOP while the window is non-empty, CUMULATE to the cumulative window's
+// end (SliceSharedWindowAggProcessor.java:64-118) -- so those old windows fire again for the
+// keys of such records only. Here those records are flushed apart (re_new: their state,
+// re_delta: the keys flushed since the last watermark) and, per re-fired window W in
+// ascending order, one merge emits exactly the chained keys: the keys of W's own new slice
+// plus the running chain (a table of keys with zero accumulators, the merge's mark-only
+// sources), with their whole state over W's slices (restored + new); the merge writes the
+// chain on (HOP: the marked keys holding state in W; CUMULATE: every marked key). CUMULATE
+// folds each step slice into the first slice's state as it fires (mergeSlices).
+// one re-fire merge as a job (retried by region like every merge)
+int refire_job(fg_handle* h, const std::vector<SliceTable*>& vals, const std::vector<SliceTable*>& marks,
+               SliceTable* dst, int dst_mode, bool emit, int64_t wend) {
+    MergeJob j;
+    for (SliceTable* t : vals)
+        if (t && t->upper > 0) j.srcs.push_back(t);
+    int64_t ub = 0;
+    for (SliceTable* t : j.srcs) ub += t->upper;
+    for (SliceTable* t : marks) {
+        if (!t || t->upper == 0) continue;
+        if (j.srcs.size() >= 64) return h->fail(FG_ESTATE, "internal: re-fire merge over 64 sources");
+        const uint64_t bit = 1ull << j.srcs.size();
+        j.mark_mask |= bit;
+        j.markonly_mask |= bit;
+        j.srcs.push_back(t);
+    }
+    if (j.mark_mask == 0 && dst_mode != 0) return FG_OK;   // nothing chained
+    int rc;
+    if (emit) {
+        if (j.mark_mask == 0) return FG_OK;
+        rc = reset_out_count(h);
+        if (rc) return rc;
+        ub = std::min<int64_t>(ub, kStateCapMax);
+        rc = ensure_out(h, h->out_n + h->pending_out + ub);
+        if (rc) return rc;
+        h->pending_out += ub;
+        j.emit = true;
+        j.emit_marked = 1;
+        j.wend = wend;
+    }
+    j.dst = dst;
+    j.dst_mode = dst_mode;
+    j.kclass = K_FIRE;
+    int ji = 0;
+    rc = job_add(h, std::move(j), &ji);
+    if (rc) return rc;
+    MergeParams p{};
+    rc = job_params(h, ji, &p);
+    if (rc) return rc;
+    KTimer kt(h, K_FIRE, 0);
+    HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+    if (dst) {
+        int64_t u = 0;
+        for (SliceTable* t : h->jobs.back().srcs) u += t->upper;
+        dst->upper = std::min<int64_t>(u, kStateCapMax);
+    }
+    return FG_OK;
+}
+
+// the re-fire is over (the watermark passed the checkpoint's): new state of slices that
+// later windows still read joins the resident state, the rest is dropped
+int refire_finish(fg_handle* h) {
+    int rc;
+    const WindowSpec& w = h->w;
+    std::vector<std::pair<int64_t, std::unique_ptr<SliceTable>>> moved;
+    for (auto& kv : h->re_new) {
+        const int64_t se = kv.first;
+        // the last window containing the slice (HOP: se + size - slice; CUMULATE: its window's end)
+        const int64_t last = w.kind == HOP ? jadd(jsub(se, w.slice), w.size) : jadd(window_start(w, se), w.size);
+        if (trigger_time(w, last) <= h->refire_hi) continue;
+        // HOP: the slice's own table; CUMULATE: the first slice's state it folds into
+        const int64_t into = w.kind == HOP ? se : jadd(window_start(w, se), w.slice);
+        SliceTable* m = nullptr;
+        rc = table_get(h, into, w.kind == CUMULATE, &m);
+        if (rc) return rc;
+        if (m) {
+            rc = refire_job(h, {m, kv.second.get()}, {}, m, 0, false, 0);
+            if (rc) return rc;
+        } else {
+            moved.emplace_back(se, std::move(kv.second));
+        }
+    }
+    rc = fire_collect(h);
+    if (rc) return rc;
+    for (auto& mv : moved) h->tables[mv.first] = std::move(mv.second);
+    auto pool = [&](std::unique_ptr<SliceTable>& t) {
+        if (t && t->bits == h->region_bits) h->table_pool.push_back(std::move(t));
+        t.reset();
+    };
+    for (auto& kv : h->re_new) pool(kv.second);
+    for (auto& kv : h->re_delta) pool(kv.second);
+    for (auto& t : h->re_tmp) pool(t);
+    pool(h->re_chain);
+    h->re_new.clear();
+    h->re_delta.clear();
+    h->re_tmp.clear();
+    h->re_chain_w = JMIN;
+    h->refire_hi = JMIN;
+    return FG_OK;
+}
+
+int refire(fg_handle* h, int64_t wm) {
+    const WindowSpec& w = h->w;
+    const int64_t S = w.slice;
+    const int64_t lim = std::min(wm, h->refire_hi);
+    h->refire_wm = wm;
+    int64_t W = JMAX;
+    if (!h->re_delta.empty()) W = h->re_delta.begin()->first;
+    if (h->re_chain) W = std::min(W, h->re_chain_w);
+    const int64_t last_delta = h->re_delta.empty() ? JMIN : h->re_delta.rbegin()->first;
+    SliceTable* R = nullptr;   // running chain (in re_tmp)
+    int64_t R_ws = JMIN;       // CUMULATE: the cumulative window of R
+    std::vector<int64_t> done_delta, folded, expired_first;
+    bool any = false;
+    int rc;
+    auto new_chain = [&](SliceTable** out) -> int {
+        std::unique_ptr<SliceTable> t;
+        int r = table_new(h, JMIN, &t);
+        if (r) return r;
+        *out = t.get();
+        h->re_tmp.push_back(std::move(t));
+        return FG_OK;
+    };
+    for (; W != JMAX && trigger_time(w, W) <= lim; W = jadd(W, S)) {
+        SliceTable* D = side_get(h->re_delta, W);
+        SliceTable* Cold = h->re_chain && W == h->re_chain_w ? h->re_chain.get() : nullptr;
+        if (w.kind == CUMULATE && R && window_start(w, W) != R_ws) R = nullptr;   // a new cumulative window
+        if (!D && !R && !Cold) {
+            if (W >= last_delta && (!h->re_chain || W >= h->re_chain_w)) break;
+            continue;
+        }
+        if (D) done_delta.push_back(W);
+        SliceTable* R2 = nullptr;
+        rc = new_chain(&R2);
+        if (rc) return rc;
+        if (w.kind == HOP) {
+            std::vector<SliceTable*> vals;   // W's slices (W - size, W]: resident and new state
+            for (auto it = h->tables.upper_bound(jsub(W, w.size)); it != h->tables.end() && it->first <= W; ++it)
+                vals.push_back(it->second.get());
+            for (auto it = h->re_new.upper_bound(jsub(W, w.size)); it != h->re_new.end() && it->first <= W; ++it)
+                vals.push_back(it->second.get());
+            rc = refire_job(h, vals, {D, R, Cold}, R2, 1, true, W);   // emit + chain on (marked, non-empty)
+            if (rc) return rc;
+            expired_first.push_back(jadd(jsub(W, w.size), S));          // expiredSlices: W's first slice
+        } else {   // CUMULATE
+            const int64_t ws = window_start(w, W), first = jadd(ws, S), last = jadd(ws, w.size);
+            SliceTable* F = nullptr;
+            rc = table_get(h, first, true, &F);
+            if (rc) return rc;
+            // fold the new state of this cumulative window's slices up to W into the first
+            // slice's state (mergeSlices; a late-accepted record's slice is the first one)
+            std::vector<SliceTable*> fold{F};
+            for (auto it = h->re_new.lower_bound(first); it != h->re_new.end() && it->first <= W; ++it) {
+                if (std::find(folded.begin(), folded.end(), it->first) != folded.end()) continue;
+                fold.push_back(it->second.get());
+                folded.push_back(it->first);
+            }
+            if (fold.size() > 1) {
+                rc = refire_job(h, fold, {}, F, 0, false, 0);
+                if (rc) return rc;
+            }
+            rc = refire_job(h, {F}, {D, R, Cold}, nullptr, 0, true, W);   // emit the chained keys
+            if (rc) return rc;
+            rc = refire_job(h, {}, {D, R, Cold}, R2, 2, false, 0);        // the chain goes on regardless
+            if (rc) return rc;
+            R_ws = ws;
+            if (W == last) {   // the cumulative window is complete: its state expires
+                table_free(h, first);
+                R2 = nullptr;
+            }
+        }
+        R = R2;
+        any = true;
+    }
+    if (any) {
+        h->defer_free = true;   // (table_free above: held until the fires are collected)
+        rc = fire_collect(h);
+        h->defer_free = false;
+        if (rc) return rc;
+    }
+    for (int64_t e : done_delta) {
+        auto it = h->re_delta.find(e);
+        if (it != h->re_delta.end()) {
+            h->table_pool.push_back(std::move(it->second));
+            h->re_delta.erase(it);
+        }
+    }
+    for (int64_t e : folded) {
+        auto it = h->re_new.find(e);
+        if (it != h->re_new.end()) {
+            h->table_pool.push_back(std::move(it->second));
+            h->re_new.erase(it);
+        }
+    }
+    for (int64_t e : expired_first) {
+        auto it = h->re_new.find(e);
+        if (it != h->re_new.end()) {
+            h->table_pool.push_back(std::move(it->second));
+            h->re_new.erase(it);
+        }
+    }
+    // the chain that goes on past this watermark
+    std::unique_ptr<SliceTable> keep;
+    for (auto& t : h->re_tmp)
+        if (t && t.get() == R) keep = std::move(t);
+    for (auto& t : h->re_tmp)
+        if (t && t->bits == h->region_bits) h->table_pool.push_back(std::move(t));
+    h->re_tmp.clear();
+    if (h->re_chain && h->re_chain.get() != R) {
+        if (h->re_chain->bits == h->region_bits) h->table_pool.push_back(std::move(h->re_chain));
+        h->re_chain.reset();
+    }
+    if (keep) {
+        h->re_chain = std::move(keep);
+        h->re_chain_w = W;
+    } else if (!h->re_chain || h->re_chain.get() != R) {
+        h->re_chain.reset();
+        h->re_chain_w = JMIN;
+    }
+    if (wm >= h->refire_hi) return refire_finish(h);
     return FG_OK;
 }
 
@@ -2286,6 +2593,7 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     } else if (h->cfg.mode == FG_MODE_SQL) {
         // AbstractWindowAggProcessor.advanceProgress :178-192
         if (wm > h->current_progress) {
+            h->arrival_progress = h->current_progress;   // the staged records arrived under it
             h->current_progress = wm;
             if (h->current_progress >= h->next_trigger) {
                 if (staged_any(h) && is_window_fired(h->w, min_staged_slice_end(h), wm)) {
@@ -2302,6 +2610,11 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
             rc = flush(h, fuse, true);
             if (rc) return rc;
         }
+    }
+    h->arrival_progress = h->current_progress;
+    if (h->refire_hi != JMIN && wm > h->refire_wm) {   // restore re-fire (timers below prev)
+        rc = refire(h, wm);
+        if (rc) return rc;
     }
     if (wm > prev && !h->local) {
         rc = fire_windows(h, prev, wm);
@@ -2335,6 +2648,12 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
     if (int rc0 = settle_pending(h)) return rc0;
     int rc = flush(h);
     if (rc) return rc;
+    // a restore re-fire still pending: its new state joins the image (the chained timers
+    // of its keys are not part of it)
+    if (h->refire_hi != JMIN) {
+        rc = refire_finish(h);
+        if (rc) return rc;
+    }
     // region counts of every resident slice
     const size_t nt = h->tables.size();
     HIPCHK(h, h->hs_counts.ensure(sizeof(uint32_t) * h->P * std::max<size_t>(nt, 1)));
@@ -2517,8 +2836,14 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     // windows that fired before the checkpoint, for keys without pending timers, so the
     // checkpoint's timer watermark is kept (divergence 2).
     h->current_progress = JMIN;
+    h->arrival_progress = JMIN;
     h->next_trigger = JMIN;
     h->timer_wm = h->w.kind == TUMBLE ? JMIN : timer_watermark;
+    // shared slices: windows at or below the checkpoint's watermark re-fire for the keys of
+    // records that arrive for them (refire)
+    h->refire_hi = h->w.kind != TUMBLE && h->cfg.mode == FG_MODE_SQL && !h->local && !h->proctime
+                       ? timer_watermark : JMIN;
+    h->refire_wm = JMIN;
     return FG_OK;
 }
 
@@ -2562,11 +2887,19 @@ int fg_reset(fg_handle* h) {
     h->anchor_start = JMIN;
     h->q_guess = kEmptyLane;
     h->current_progress = JMIN;
+    h->arrival_progress = JMIN;
     h->next_trigger = JMIN;
     h->timer_wm = JMIN;
     h->late_dropped = 0;
     h->out_n = 0;
     h->pending_out = 0;
+    h->re_new.clear();
+    h->re_delta.clear();
+    h->re_tmp.clear();
+    h->re_chain.reset();
+    h->re_chain_w = JMIN;
+    h->refire_hi = JMIN;
+    h->refire_wm = JMIN;
     return FG_OK;
 }
 

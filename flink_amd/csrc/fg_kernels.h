@@ -187,7 +187,15 @@ struct MergeParams {
     int32_t job;
     const int32_t* retry_list;
     int32_t n_retry;
-    int32_t pad2;
+    // restore re-fire of shared windows (wide merge only): entries of source j with bit j of
+    // mark_mask set are marked; emit_marked emits marked entries holding state only; dst_mode
+    // 1 writes the marked entries holding state, 2 every marked entry, both as keys with zero
+    // accumulators (a chain table of the keys whose timers chain on)
+    int32_t emit_marked;
+    unsigned long long mark_mask;
+    unsigned long long markonly_mask;   // sources that only mark (their accumulators are not added)
+    int32_t dst_mode;
+    int32_t pad3;
 };
 constexpr int kFailJobShift = 14;             // region < 2^13
 constexpr uint32_t kChunkFailed = 0xFFFFFFFFu;

@@ -1397,6 +1397,7 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
 }
 
 constexpr int kSrcU = 2;          // source-table entries per thread per round (wide merge)
+constexpr unsigned long long kMarkBit = 1ull << 63;   // wide table: entry touched by a marking source (NULL-count word)
 constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
 
 // Value accumulator of an entry (kernel vt = val_type | op << 2; val_type 1 BIGINT, 2 DOUBLE;
@@ -1699,10 +1700,12 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     }
                     j = lo;
                 }
+                bool mk[kSrcU];
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
                     const uint32_t f = i0 + u * T + tid;
                     k[u] = JMIN;
+                    mk[u] = false;
                     if (f >= NT) continue;
                     while (s_soff[j + 1] <= f) j++;
                     const uint32_t i = f - s_soff[j];
@@ -1711,6 +1714,8 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     cs[u] = base[cap + i];
                     cn[u] = base[2 * cap + i];
                     sm[u] = base[3 * cap + i];
+                    mk[u] = ((p.mark_mask >> j) & 1ull) != 0;
+                    if ((p.markonly_mask >> j) & 1ull) cs[u] = 0;   // a mark-only source adds nothing
                 }
                 uint32_t home[kSrcU];
                 RecV2 b01[kSrcU], b23[kSrcU];
@@ -1725,18 +1730,25 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 for (int u = 0; u < kSrcU; u++) {
                     if (i0 + u * T + tid >= NT) continue;
                     const int slot = lds_bucket_slot<C>(t, k[u], home[u], b01[u], b23[u], full);
-                    if (slot >= 0) lds_add<C>(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
+                    if (slot < 0) continue;
+                    // (a zero accumulator -- a chain table's key -- adds nothing, only its mark)
+                    if (cs[u]) lds_add<C>(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
+                    if constexpr (!C) if (mk[u]) atomicOr(&t.cn[slot], kMarkBit);
                 }
             }
             for (int j = 0; !skip && p.n_src > kMaxSrcFlat && j < p.n_src; j++) {   // many tables: one by one
                 const TableRef src = p.src[j];
                 const uint32_t n = gbl(src.counts)[r];
                 const auto base = gbl(src.base + (int64_t)r * 4 * cap);
+                const bool mkj = j < 64 && ((p.mark_mask >> j) & 1ull) != 0;
+                const bool moj = j < 64 && ((p.markonly_mask >> j) & 1ull) != 0;
                 for (uint32_t i = tid; i < n; i += T) {
                     const int slot = lds_find_or_insert<C>(t, base[i], full);
-                    if (slot >= 0)
+                    if (slot < 0) continue;
+                    if (base[cap + i] && !moj)
                         lds_add<C>(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
                                    base[3 * cap + i], vt);
+                    if constexpr (!C) if (mkj) atomicOr(&t.cn[slot], kMarkBit);
                 }
             }
         }
@@ -1835,10 +1847,18 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
         //    sentinel slot, thread 0); rows of one (round, wave) are consecutive lanes, so the
         //    row stores of a wave are contiguous
         uint64_t occ_mask = 0;   // bit k: this thread's slot of round k is occupied
+        // occupied: holds state (COUNT(*) > 0); marked modes (restore re-fire): marked and
+        // holding state, or marked at all for a chain table of every marked key
+        const int omode = C ? 0 : (p.dst_mode == 2 ? 2 : (p.dst_mode == 1 || p.emit_marked) ? 1 : 0);
 #pragma unroll
         for (int k = 0; k < kRounds; k++) {
             const int slot = k < kRounds - 1 ? k * T + tid : S;
-            const bool occ = (k < kRounds - 1 ? slot < S : tid == 0) && t.cs[slot] != 0;
+            bool occ = (k < kRounds - 1 ? slot < S : tid == 0);
+            if (occ) {
+                bool marked = false;
+                if constexpr (!C) marked = (t.cn[slot] & kMarkBit) != 0;
+                occ = omode == 2 ? marked : (t.cs[slot] != 0 && (omode == 0 || marked));
+            }
             const uint64_t bal = __ballot(occ);
             if (occ) occ_mask |= 1ull << k;
             if (lane == 0) s_grp[k * kWaves + wave] = (uint32_t)__popcll(bal);
@@ -1891,13 +1911,14 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             const uint32_t at = s_grp[k * kWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
             const int64_t key = slot == S ? JMIN : t.key[slot];
             unsigned long long cs = t.cs[slot], cn = 0;
-            if constexpr (!C) cn = t.cn[slot];
+            if constexpr (!C) cn = t.cn[slot] & ~kMarkBit;
             const int64_t sum = (int64_t)t.sum[slot];
             if (write_dst) {
+                const bool chain = !C && p.dst_mode != 0;   // a chain table holds keys with zero accumulators
                 dbase[at] = key;
-                dbase[cap + at] = (int64_t)cs;
-                dbase[2 * cap + at] = (int64_t)cn;
-                dbase[3 * cap + at] = sum;
+                dbase[cap + at] = chain ? 0 : (int64_t)cs;
+                dbase[2 * cap + at] = chain ? 0 : (int64_t)cn;
+                dbase[3 * cap + at] = chain ? vinit : sum;
             }
             if (write_out) write_row(p, obase + at, key, cs, cn, sum, vt);
         }

@@ -274,21 +274,23 @@ def test_lane_conflict_slow_path_two_pass(oracle_mod):
 
 @pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
 def test_snapshot_restore_many_regions(oracle_mod, kind):
-    # TUMBLE: jitter > watermark delay, so records older than the checkpoint's watermark arrive
-    # after the restore and re-fire their windows, as in the reference. HOP / CUMULATE keep
-    # jitter < delay: their re-fire is DESIGN.md section 3, divergence 2.
+    # jitter > watermark delay: records older than the checkpoint's watermark arrive after the
+    # restore and re-fire their windows for their keys, as in the reference
     cfg = cfg_of(kind, 4000, 0 if kind == "tumble" else 1000)
-    drive_both(oracle_mod, cfg, n=400_000, keys=100_000, batch=20_000, delay=100,
-               jitter=1500 if kind == "tumble" else 80, snapshot_at=9)
+    drive_both(oracle_mod, cfg, n=400_000, keys=100_000, batch=20_000, delay=100, jitter=1500, snapshot_at=9)
 
 
-@pytest.mark.parametrize("mode", ["sql", "datastream"])
-def test_restore_refires_old_windows(oracle_mod, mode):
+@pytest.mark.parametrize("mode,kind,wm1", [("sql", "tumble", 4999), ("datastream", "tumble", 4999),
+                                           ("sql", "hop", 4999), ("sql", "cumulate", 4999),
+                                           ("sql", "hop", 1999), ("sql", "cumulate", 1999)])
+def test_restore_refires_old_windows(oracle_mod, mode, kind, wm1):
     """After initializeState the timer service restarts at Long.MIN_VALUE: rows older than the
     checkpoint's watermark are not late and fire their (already fired) window again on the next
-    watermark (SlicingWindowAggOperatorTest.java:173-184 restores mid-stream; the oracle replays
-    the restored timer heap, oracle.c or_restore_copy)."""
-    cfg = cfg_of("tumble", 1000, vt="i64", mode=mode)
+    watermark -- HOP / CUMULATE for their keys only, chained on by nextTriggerWindow
+    (SlicingWindowAggOperatorTest.java:173-184 restores mid-stream; the oracle replays the
+    restored timer heap, oracle.c or_restore_copy). wm1 = 1999: the first watermark after the
+    restore is below the checkpoint's, so the re-fire spans two watermarks."""
+    cfg = cfg_of(kind, 1000 if kind == "tumble" else 2000, 0 if kind == "tumble" else 500, vt="i64", mode=mode)
     g = gpu_mk(cfg, expected_keys=300, buffer_records=1 << 16)
     o = oracle_mk(oracle_mod, cfg)
     rng = np.random.default_rng(7)
@@ -310,10 +312,18 @@ def test_restore_refires_old_windows(oracle_mod, mode):
     v2 = rng.integers(-50, 50, 4000).astype(np.int64)
     for op in (g2, o2):
         op.process_batch(k2, t2, v2)
-        op.process_watermark(4999)
+        op.process_watermark(wm1)
     got, exp = g2.take_rows(), o2.take_rows()
     assert (exp["window_end"] <= 3000).any()   # the old windows did fire again
     assert_rows_equal(got, exp, "i64", "first watermark after restore")
+    assert g2.late_dropped == o2.late_dropped
+    k3 = rng.integers(0, 300, 3000).astype(np.int64)
+    t3 = rng.integers(1000, 8000, 3000).astype(np.int64)
+    v3 = rng.integers(-50, 50, 3000).astype(np.int64)
+    for op in (g2, o2):
+        op.process_batch(k3, t3, v3)
+        op.process_watermark(5999)
+    assert_rows_equal(g2.take_rows(), o2.take_rows(), "i64", "second watermark after restore")
     assert g2.late_dropped == o2.late_dropped
     for op in (g2, o2):
         op.process_watermark(JMAX)
