@@ -858,9 +858,13 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             if (rc) return rc;
             int64_t U = se;
             while (U != JMAX && trigger_time(h->w, U) <= h->arrival_progress) U = jadd(U, h->w.slice);
-            rc = side_create(h, h->re_delta, U, &D);
-            if (rc) return rc;
+            const bool ds = h->cfg.mode == FG_MODE_DATASTREAM;   // (per-window state: no chains)
+            if (!ds) {
+                rc = side_create(h, h->re_delta, U, &D);
+                if (rc) return rc;
+            }
             for (SliceTable* x : {T, D}) {
+                if (!x) continue;
                 MergeJob job;
                 for (Staged* st : ln.passes) job.batches.push_back(JobBatch{st, l, StagedBatch{}, 0});
                 if (x->upper > 0) job.srcs.push_back(x);
@@ -1340,7 +1344,42 @@ int refire_finish(fg_handle* h) {
     return FG_OK;
 }
 
+// DataStream sliding windows (WindowOperator): a restored window that fired was purged
+// (clearAllState at its cleanup time), so an element that arrives for it after the restore
+// (isWindowLate against the restarted timer watermark) builds a new window state of the
+// post-restore elements only, whose timer fires it again: re-fire every window up to the
+// horizon from the new slices alone, for every key in them.
+int refire_datastream(fg_handle* h, int64_t wm) {
+    const WindowSpec& w = h->w;
+    const int64_t lim = std::min(wm, h->refire_hi);
+    const int64_t from = h->refire_wm;   // windows up to the last run's limit are final
+    h->refire_wm = lim;
+    bool fired = false;
+    int rc;
+    if (!h->re_new.empty()) {
+        int64_t W = h->re_new.begin()->first;
+        const int64_t hi = jadd(jsub(h->re_new.rbegin()->first, w.slice), w.size);
+        for (; W <= hi && trigger_time(w, W) <= lim; W = jadd(W, w.slice)) {
+            if (trigger_time(w, W) <= from) continue;
+            std::vector<SliceTable*> srcs;
+            for (auto it = h->re_new.upper_bound(jsub(W, w.size)); it != h->re_new.end() && it->first <= W; ++it)
+                srcs.push_back(it->second.get());
+            if (srcs.empty()) continue;
+            rc = fire_one(h, W, srcs, nullptr, true);
+            if (rc) return rc;
+            fired = true;
+        }
+    }
+    if (fired) {
+        rc = fire_collect(h);
+        if (rc) return rc;
+    }
+    if (wm >= h->refire_hi) return refire_finish(h);
+    return FG_OK;
+}
+
 int refire(fg_handle* h, int64_t wm) {
+    if (h->cfg.mode == FG_MODE_DATASTREAM) return refire_datastream(h, wm);
     const WindowSpec& w = h->w;
     const int64_t S = w.slice;
     const int64_t lim = std::min(wm, h->refire_hi);
@@ -2841,8 +2880,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     h->timer_wm = h->w.kind == TUMBLE ? JMIN : timer_watermark;
     // shared slices: windows at or below the checkpoint's watermark re-fire for the keys of
     // records that arrive for them (refire)
-    h->refire_hi = h->w.kind != TUMBLE && h->cfg.mode == FG_MODE_SQL && !h->local && !h->proctime
-                       ? timer_watermark : JMIN;
+    h->refire_hi = h->w.kind != TUMBLE && !h->local && !h->proctime ? timer_watermark : JMIN;
     h->refire_wm = JMIN;
     return FG_OK;
 }

@@ -282,7 +282,8 @@ def test_snapshot_restore_many_regions(oracle_mod, kind):
 
 @pytest.mark.parametrize("mode,kind,wm1", [("sql", "tumble", 4999), ("datastream", "tumble", 4999),
                                            ("sql", "hop", 4999), ("sql", "cumulate", 4999),
-                                           ("sql", "hop", 1999), ("sql", "cumulate", 1999)])
+                                           ("sql", "hop", 1999), ("sql", "cumulate", 1999),
+                                           ("datastream", "hop", 4999), ("datastream", "hop", 1999)])
 def test_restore_refires_old_windows(oracle_mod, mode, kind, wm1):
     """After initializeState the timer service restarts at Long.MIN_VALUE: rows older than the
     checkpoint's watermark are not late and fire their (already fired) window again on the next
