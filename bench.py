@@ -404,7 +404,9 @@ def main():
     window = getattr(F, wname)(*wargs)
     expected_keys = args.expected_keys or int(args.keys / world * 1.05) + 1
     if not args.expected_keys and wl["zipf"] > 0:   # distinct keys in one slice's records, +10 %
-        expected_keys = int(1.1 * zipf_distinct_per_slice(args.keys, wl["zipf"], args.rate) / world) + 1
+        # each rank draws `rate` records per event-second, so an owner's slice holds the keys
+        # of world * rate draws, split over the world owners
+        expected_keys = int(1.1 * zipf_distinct_per_slice(args.keys, wl["zipf"], args.rate * world) / world) + 1
     aggs = ("avg",) if args.workload == "zipf" else ("sum",) if datastream else ("count_star", "sum", "avg")
     if args.aggs:
         aggs = tuple(args.aggs.split(","))
