@@ -61,7 +61,7 @@ class FgRows(C.Structure):
 class FgStateRows(C.Structure):
     _fields_ = [
         ("n", C.c_int64), ("key", C.c_void_p), ("slice_end", C.c_void_p), ("cnt_star", C.c_void_p),
-        ("cnt_val", C.c_void_p), ("sum", C.c_void_p),
+        ("cnt_val", C.c_void_p), ("sum", C.c_void_p), ("min", C.c_void_p), ("max", C.c_void_p),
     ]
 
 

@@ -1,10 +1,11 @@
 """Queries with several value accumulators (e.g. SUM, MIN and MAX of one column).
 
-An engine handle keeps one value accumulator per (key, slice) -- the SUM family (SUM, AVG,
-SUM0), MIN or MAX (include/flinkgpu.h, fg_agg) -- so a query such as
-``SELECT COUNT(*), SUM(v), MIN(v), MAX(v) ... GROUP BY TUMBLE(...)`` runs one handle per
-accumulator kind, each fed the same batches, and the fired rows are joined on
-(window_end, key). Every handle fires the same (key, window) set: emission is decided by
+An engine handle keeps the SUM-family, MIN and MAX accumulators of one (key, slice) side by
+side (value slots), so ``SELECT COUNT(*), SUM(v), MIN(v), MAX(v) ... GROUP BY TUMBLE(...)`` is
+one handle and one staging pass (window_agg_operator). CompositeWindowAggOperator is the
+split form: one handle per accumulator kind, each fed the same batches, the fired rows joined
+on (window_end, key) -- what the local phase of a two-phase plan needs (one partial
+accumulator per row), and a cross-check of the value slots in the tests. Every handle fires the same (key, window) set: emission is decided by
 COUNT(*) / the presence of state, which all of them keep (the reference's generated
 NamespaceAggsHandleFunction holds all accumulators of one (key, window) in one row,
 AggsHandlerCodeGenerator.scala:578-700; the join restores that row). This is the
@@ -36,12 +37,11 @@ def accumulator_groups(aggs):
 
 
 def window_agg_operator(window, aggs=("count_star", "count", "sum", "avg"), **kw):
-    """A WindowAggOperator when one value accumulator serves `aggs`, else a
-    CompositeWindowAggOperator over one handle per accumulator kind."""
-    codes, groups = accumulator_groups(aggs)
-    if len(groups) <= 1:
-        return WindowAggOperator(window, aggs=aggs, **kw)
-    return CompositeWindowAggOperator(window, aggs=aggs, **kw)
+    """One WindowAggOperator: a handle keeps the SUM-family, MIN and MAX accumulators side by
+    side (value slots, include/flinkgpu.h fg_agg). Only the local phase of a two-phase plan,
+    whose partial row holds one value accumulator, needs a handle per kind (open those with
+    accumulator_groups)."""
+    return WindowAggOperator(window, aggs=aggs, **kw)
 
 
 class CompositeWindowAggOperator:

@@ -219,7 +219,12 @@ struct PendingBatch {
 };
 
 struct fg_handle {
-    int32_t kvt = 0;   // kernel value op (val_type | op << 2)
+    int32_t kvt = 0;   // kernel value op (val_type | op << 2); multi-value: the value type
+    // several value accumulators (SUM family + MIN + MAX): value slots 0 SUM, 1 MIN, 2 MAX
+    int mv = 0;
+    int32_t vop[kNV] = {3, 3, 3};          // op per slot (0 SUM, 1 MIN, 2 MAX, 3 none)
+    int32_t agg_slot[FG_MAX_AGGS] = {};    // value slot of each output aggregate
+    int tcap = kRegionCap;                 // entries per region of its tables
     fg_config cfg{};
     WindowSpec w{};
     int device = 0;
@@ -323,8 +328,8 @@ struct fg_handle {
     HostBuf h_agg[FG_MAX_AGGS];
 
     // snapshot image
-    DevBuf s_key, s_slice, s_cs, s_cv, s_sum, s_off;
-    HostBuf hs_key, hs_slice, hs_cs, hs_cv, hs_sum, hs_counts, hs_off;
+    DevBuf s_key, s_slice, s_cs, s_cv, s_sum, s_off, s_v1, s_v2;
+    HostBuf hs_key, hs_slice, hs_cs, hs_cv, hs_sum, hs_counts, hs_off, hs_v1, hs_v2;
 
     // stats
     int64_t records_in = 0, rows_fired = 0, flushes = 0;
@@ -445,7 +450,7 @@ int table_new(fg_handle* h, int64_t slice_end, std::unique_ptr<SliceTable>* out)
         h->table_pool.pop_back();
     } else {
         t.reset(new SliceTable());
-        HIPCHK(h, t->data.ensure(sizeof(int64_t) * 4 * (size_t)kRegionCap * h->P));
+        HIPCHK(h, t->data.ensure(sizeof(int64_t) * table_cols(h->mv) * (size_t)table_cap(h->mv) * h->P));
         HIPCHK(h, t->counts.ensure(sizeof(uint32_t) * h->P));
     }
     HIPCHK(h, hipMemsetAsync(t->counts.p, 0, sizeof(uint32_t) * h->P, h->stream));
@@ -561,6 +566,14 @@ StagedBatch batch_of(const fg_handle* h, const JobBatch& jb) {
 
 void fill_emit(fg_handle* h, MergeParams& p, int64_t wend);
 
+// the operator's value accumulators in a merge's parameters
+void set_values(const fg_handle* h, MergeParams* p) {
+    p->val_type = h->kvt;
+    p->mv = h->mv;
+    for (int k = 0; k < kNV; k++) p->vop[k] = h->vop[k];
+    for (int a = 0; a < FG_MAX_AGGS; a++) p->agg_slot[a] = h->agg_slot[a];
+}
+
 // MergeParams of job `ji` at the current region bits (the general path; callers pick the
 // fast variants on a first launch)
 int job_params(fg_handle* h, int ji, MergeParams* p) {
@@ -581,7 +594,7 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
         int rc = arena_put(h, sb.data(), sb.size(), &p->batches);
         if (rc) return rc;
     }
-    p->val_type = h->kvt;
+    set_values(h, p);
     p->has_dst = j.dst ? 1 : 0;
     if (j.dst) p->dst = ref_of(j.dst);
     if (j.emit) fill_emit(h, *p, j.wend);
@@ -609,10 +622,10 @@ int grow(fg_handle* h, int nb) {
     std::vector<std::unique_ptr<DevBuf>> old;   // freed once the split kernels are done
     auto split = [&](SliceTable* t) -> int {
         std::unique_ptr<DevBuf> nd(new DevBuf()), nc(new DevBuf());
-        HIPCHK(h, nd->ensure(sizeof(int64_t) * 4 * (size_t)kRegionCap * P2));
+        HIPCHK(h, nd->ensure(sizeof(int64_t) * table_cols(h->mv) * (size_t)table_cap(h->mv) * P2));
         HIPCHK(h, nc->ensure(sizeof(uint32_t) * P2));
         HIPCHK(h, launch_split_table(ref_of(t), TableRef{nd->as<int64_t>(), nc->as<uint32_t>()}, t->bits,
-                                     nb - t->bits, h->stream));
+                                     nb - t->bits, h->mv, h->stream));
         t->data.swap(*nd);
         t->counts.swap(*nc);
         t->bits = nb;
@@ -961,7 +974,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             skew = skew || s->skew;
             same_bits = same_bits && s->bits == h->region_bits;
         }
-        skew = skew && same_bits;
+        skew = skew && same_bits && !h->mv;   // (a multi-value operator takes no heavy pass)
         HeavyPlan hp{};
         if (skew) {
             rc = plan_heavy(h, p.batches, p.n_batches, ln.fill + ln.acc_fill, &hp);
@@ -1080,7 +1093,7 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
     if (srcs.size() == 1 && !dst) {   // one table, nothing written: rows straight from it (cannot overflow)
         MergeParams p{};
         p.region_bits = h->region_bits;
-        p.val_type = h->kvt;
+        set_values(h, &p);
         fill_emit(h, p, wend);
         p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
         p.overflow = h->scalars.as<unsigned int>();
@@ -2069,11 +2082,8 @@ int validate(const fg_config* c, std::string* msg) {
                 has_max |= c->aggs[a] == FG_AGG_MAX;
             }
             kinds = (int)sum_family + (int)has_min + (int)has_max;
-            if (kinds > 1 && !(c->flags & FG_FLAG_LOCAL_PARTIALS))
-                snprintf(buf, sizeof buf,
-                         "MIN and MAX take an operator of their own (one value accumulator per key and slice); "
-                         "they do not mix with each other or with SUM/AVG/SUM0");
-            else if ((has_min || has_max) && c->mode != FG_MODE_SQL)
+            (void)kinds;   // several kinds: a multi-value operator (value slots SUM, MIN, MAX)
+            if ((has_min || has_max) && c->mode != FG_MODE_SQL)
                 snprintf(buf, sizeof buf, "MIN/MAX are SQL aggregates (DataStream windows here reduce with SumAggregator)");
         }
         if (c->val_type < FG_VAL_NONE || c->val_type > FG_VAL_F64) snprintf(buf, sizeof buf, "bad val_type");
@@ -2246,9 +2256,30 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     std::unique_ptr<fg_handle> h(new fg_handle());
     h->cfg = c;
     h->kvt = c.val_type;   // kernel value op: val_type | op << 2 (op 1 MIN, 2 MAX; fg_kernels.hip lds_add)
-    for (int a = 0; a < c.num_aggs; a++) {
-        if (c.aggs[a] == FG_AGG_MIN) h->kvt = c.val_type | (1 << 2);
-        if (c.aggs[a] == FG_AGG_MAX) h->kvt = c.val_type | (2 << 2);
+    {
+        bool sum_family = false, has_min = false, has_max = false;
+        for (int a = 0; a < c.num_aggs; a++) {
+            sum_family |= c.aggs[a] == FG_AGG_SUM || c.aggs[a] == FG_AGG_AVG || c.aggs[a] == FG_AGG_SUM0;
+            has_min |= c.aggs[a] == FG_AGG_MIN;
+            has_max |= c.aggs[a] == FG_AGG_MAX;
+        }
+        if ((int)sum_family + (int)has_min + (int)has_max > 1 && !local) {
+            // the reference's generated accumulator row holds every aggregate's accumulator
+            // (AggsHandlerCodeGenerator.scala:578-700): one operator, one staging, value slots
+            // 0 SUM (SUM / AVG / SUM0), 1 MIN, 2 MAX
+            h->mv = 1;
+            h->tcap = kRegionCapMV;
+            h->vop[0] = sum_family ? 0 : 3;
+            h->vop[1] = has_min ? 1 : 3;
+            h->vop[2] = has_max ? 2 : 3;
+            for (int a = 0; a < c.num_aggs; a++)
+                h->agg_slot[a] = c.aggs[a] == FG_AGG_MIN ? 1 : c.aggs[a] == FG_AGG_MAX ? 2 : 0;
+        } else {
+            for (int a = 0; a < c.num_aggs; a++) {
+                if (c.aggs[a] == FG_AGG_MIN) h->kvt = c.val_type | (1 << 2);
+                if (c.aggs[a] == FG_AGG_MAX) h->kvt = c.val_type | (2 << 2);
+            }
+        }
     }
     h->local = local;
     h->proctime = proctime;
@@ -2314,7 +2345,8 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     // (~1.4M keys per slice at that load, 117 MB per slice table), grown on demand.
     int bits = 0;
     if (cfg->expected_keys > 0) {
-        while (bits < kMaxRegionBits && ((int64_t)1 << bits) * (int64_t)(kSlots * 0.35) < cfg->expected_keys) bits++;
+        const int slots = h->mv ? kSlotsMV : kSlots;
+        while (bits < kMaxRegionBits && ((int64_t)1 << bits) * (int64_t)(slots * 0.35) < cfg->expected_keys) bits++;
     } else {
         bits = kDefaultRegionBits;
     }
@@ -2539,6 +2571,9 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     if (!h || !b) return FG_EINVAL;
     if (b->n <= 0) return FG_OK;
     if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
+    if (h->mv)
+        return h->fail(FG_EINVAL, "partial rows carry one value accumulator: a global operator takes one value "
+                                  "accumulator kind (SUM family, MIN or MAX)");
     if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 rows");
     if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
         return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
@@ -2718,6 +2753,10 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
     HIPCHK(h, h->s_cs.ensure(b8));
     HIPCHK(h, h->s_cv.ensure(b8));
     HIPCHK(h, h->s_sum.ensure(b8));
+    if (h->mv) {
+        HIPCHK(h, h->s_v1.ensure(b8));
+        HIPCHK(h, h->s_v2.ensure(b8));
+    }
     HIPCHK(h, h->s_off.ensure(sizeof(uint64_t) * h->P * std::max<size_t>(nt, 1)));
     HIPCHK(h, hipMemcpyAsync(h->s_off.p, h->hs_off.p, sizeof(uint64_t) * h->P * nt, hipMemcpyHostToDevice, h->stream));
     ti = 0;
@@ -2731,6 +2770,9 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
         p.out_cnt_star = h->s_cs.as<int64_t>();
         p.out_cnt_val = h->s_cv.as<int64_t>();
         p.out_sum = h->s_sum.as<int64_t>();
+        p.mv = h->mv;
+        p.out_v1 = h->s_v1.as<int64_t>();
+        p.out_v2 = h->s_v2.as<int64_t>();
         {
             KTimer kt(h, K_EXPORT, 0);
             HIPCHK(h, launch_export(p, h->P, h->stream));
@@ -2742,7 +2784,15 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
     HIPCHK(h, h->hs_cs.ensure(b8));
     HIPCHK(h, h->hs_cv.ensure(b8));
     HIPCHK(h, h->hs_sum.ensure(b8));
+    if (h->mv) {
+        HIPCHK(h, h->hs_v1.ensure(b8));
+        HIPCHK(h, h->hs_v2.ensure(b8));
+    }
     if (total > 0) {
+        if (h->mv) {
+            HIPCHK(h, hipMemcpyAsync(h->hs_v1.p, h->s_v1.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipMemcpyAsync(h->hs_v2.p, h->s_v2.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        }
         HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
@@ -2757,6 +2807,8 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
     out->cnt_star = h->hs_cs.as<int64_t>();
     out->cnt_val = h->hs_cv.as<int64_t>();
     out->sum = h->hs_sum.as<int64_t>();
+    out->min = h->mv ? h->hs_v1.as<int64_t>() : nullptr;   // multi-value operators: the MIN / MAX slots
+    out->max = h->mv ? h->hs_v2.as<int64_t>() : nullptr;
     if (timer_watermark) *timer_watermark = h->timer_wm;
     return FG_OK;
 }
@@ -2786,7 +2838,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
                     mx = std::max(mx, sum);
                 }
                 need = b;
-                if (mx <= (uint32_t)(0.7 * kRegionCap)) break;
+                if (mx <= (uint32_t)(0.7 * h->tcap)) break;
             }
         }
         rc = grow(h, need);
@@ -2804,7 +2856,9 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
             off[reg[j] + 1]++;
         }
         for (int r = 0; r < NB; r++) off[r + 1] += off[r];
-        std::vector<int64_t> k(m), cs(m), cn(m), sm(m);
+        if (h->mv && (!in->min || !in->max))
+            return h->fail(FG_EINVAL, "a multi-value operator's image needs the min and max columns");
+        std::vector<int64_t> k(m), cs(m), cn(m), sm(m), v1(h->mv ? m : 0), v2(h->mv ? m : 0);
         std::vector<uint32_t> cur(off.begin(), off.end() - 1);
         for (int64_t j = 0; j < m; j++) {
             const int64_t i = idx[j];
@@ -2813,8 +2867,18 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
             cs[at] = in->cnt_star[i];
             cn[at] = in->cnt_star[i] - in->cnt_val[i];
             sm[at] = in->sum[i];
+            if (h->mv) {
+                v1[at] = in->min[i];
+                v2[at] = in->max[i];
+            }
         }
-        DevBuf dk, dcs, dcn, dsm, doff;
+        DevBuf dk, dcs, dcn, dsm, doff, dv1, dv2;
+        if (h->mv) {
+            HIPCHK(h, dv1.ensure(8 * std::max<int64_t>(m, 1)));
+            HIPCHK(h, dv2.ensure(8 * std::max<int64_t>(m, 1)));
+            HIPCHK(h, hipMemcpy(dv1.p, v1.data(), 8 * m, hipMemcpyHostToDevice));
+            HIPCHK(h, hipMemcpy(dv2.p, v2.data(), 8 * m, hipMemcpyHostToDevice));
+        }
         HIPCHK(h, dk.ensure(8 * std::max<int64_t>(m, 1)));
         HIPCHK(h, dcs.ensure(8 * std::max<int64_t>(m, 1)));
         HIPCHK(h, dcn.ensure(8 * std::max<int64_t>(m, 1)));
@@ -2837,6 +2901,8 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         jb.ext.cnt_null = dcn.as<int64_t>();
         jb.ext.bucket_off = doff.as<uint32_t>();
         jb.ext.is_acc = 1;
+        jb.ext.val1 = dv1.as<int64_t>();
+        jb.ext.val2 = dv2.as<int64_t>();
         jb.ext_bits = h->region_bits;
         j.batches.push_back(jb);
         j.srcs.push_back(t);
@@ -2902,7 +2968,7 @@ int fg_get_stats(fg_handle* h, fg_stats* out) {
     out->flushes = h->flushes;
     out->live_slices = (int64_t)h->tables.size();
     out->state_regions = h->P;
-    out->region_capacity = kRegionCap;
+    out->region_capacity = h->tcap;
     return FG_OK;
 }
 

@@ -15,6 +15,13 @@ constexpr int kRegionCap = 3584;              // max entries per region in HBM (
 constexpr int kMergeThreads = 1024;           // persistent merge: one 1024-thread workgroup per CU
 constexpr int kCompactSlots = 3584;           // compact merge table: 3,584 x 20 B = 70 KiB of LDS
 constexpr int kCompactMergeThreads = 512;     // compact merge: two 512-thread workgroups per CU
+// Several value accumulators over the one value column (SUM family + MIN + MAX in one
+// operator, the reference's generated accumulator row, AggsHandlerCodeGenerator.scala:578-700):
+// three value slots per entry, so the LDS tables hold fewer slots and regions fewer entries
+constexpr int kNV = 3;                        // value slots per entry of a multi-value operator
+constexpr int kSlotsMV = 3072;                // wide LDS table: 3,072 x 48 B = 144 KiB
+constexpr int kCompactSlotsMV = 3072;         // compact LDS table: 3,072 x 36 B = 108 KiB
+constexpr int kRegionCapMV = 2688;            // entries per region in HBM (87.5 % of kSlotsMV)
 constexpr int kIngestThreads = 1024;
 constexpr int kMaxLanes = 4;
 constexpr int kMaxStageBuckets = 32768;       // lanes << region_bits (count / direct scatter LDS)
@@ -43,7 +50,8 @@ constexpr int kPart2Tile = 8 * kPart2Threads;  // pass-2 records per sub-tile (8
 
 // One slice table in HBM: P regions, each region an SoA block of kRegionCap entries:
 //   [key i64 x cap][cnt_star i64 x cap][cnt_null i64 x cap][sum (i64 | f64 bits) x cap]
-// cnt_val = cnt_star - cnt_null.
+// cnt_val = cnt_star - cnt_null. A multi-value operator's regions hold kRegionCapMV entries
+// and kNV value columns: [key][cnt_star][cnt_null][v0][v1][v2].
 struct TableRef {
     int64_t* base;
     uint32_t* counts;   // entries per region
@@ -68,6 +76,8 @@ struct StagedBatch {
     // (general merge path only)
     int32_t shift;
     int32_t pad0;
+    const int64_t* val1;       // is_acc of a multi-value operator: value slots 1 and 2
+    const int64_t* val2;
 };
 
 struct IngestParams {
@@ -195,8 +205,16 @@ struct MergeParams {
     unsigned long long mark_mask;
     unsigned long long markonly_mask;   // sources that only mark (their accumulators are not added)
     int32_t dst_mode;
-    int32_t pad3;
+    // multi-value operator (mv): value slot k accumulates with op vop[k] (0 SUM, 1 MIN,
+    // 2 MAX, 3 none) over the value type in val_type; output aggregate a reads slot agg_slot[a];
+    // tables have kNV value columns and kRegionCapMV entries per region
+    int32_t mv;
+    int32_t vop[kNV];
+    int32_t agg_slot[kMaxAggs];
 };
+// region capacity and 8-byte words per entry of an operator's tables
+__host__ __device__ __forceinline__ int table_cap(int mv) { return mv ? kRegionCapMV : kRegionCap; }
+__host__ __device__ __forceinline__ int table_cols(int mv) { return mv ? 3 + kNV : 4; }
 constexpr int kFailJobShift = 14;             // region < 2^13
 constexpr uint32_t kChunkFailed = 0xFFFFFFFFu;
 
@@ -248,6 +266,10 @@ struct ExportParams {
     int64_t* out_cnt_star;
     int64_t* out_cnt_val;
     int64_t* out_sum;
+    int64_t* out_v1;             // multi-value operator: value slots 1 and 2
+    int64_t* out_v2;
+    int32_t mv;
+    int32_t pad;
 };
 
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s);
@@ -311,7 +333,7 @@ hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
 // region split: the table `src` at old_bits -> `dst` at old_bits + shift (each region's
 // entries go to its 2^shift child regions by the next bits of their key mix)
-hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift,
+hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift, int32_t mv,
                               hipStream_t s);
 hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s);
 hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s);

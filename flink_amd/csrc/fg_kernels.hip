@@ -1264,35 +1264,61 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
 #define FG_DIAG_MERGE 0    // diagnostic builds only (wrong results): bit0 no adds, bit1 no probe loop, bit2 no emit
 #endif
 
-template <bool C>
+template <bool C, bool MV = false>
 struct MergeCfg;
 template <>
-struct MergeCfg<false> {
+struct MergeCfg<false, false> {
     static constexpr int kSlotsT = kSlots;
     static constexpr int kThreads = kMergeThreads;
     static constexpr int kU = FG_WIDE_U;   // 1,024 threads: 128 VGPRs
 };
 template <>
-struct MergeCfg<true> {
+struct MergeCfg<true, false> {
     static constexpr int kSlotsT = kCompactSlots;
     static constexpr int kThreads = kCompactMergeThreads;
     static constexpr int kU = FG_MERGE_U;
 };
+template <>
+struct MergeCfg<false, true> {   // multi-value: one 1,024-thread workgroup per CU
+    static constexpr int kSlotsT = kSlotsMV;
+    static constexpr int kThreads = kMergeThreads;
+    static constexpr int kU = FG_WIDE_U;
+};
+template <>
+struct MergeCfg<true, true> {    // multi-value compact: 108 KiB, one workgroup per CU
+    static constexpr int kSlotsT = kCompactSlotsMV;
+    static constexpr int kThreads = kCompactMergeThreads;
+    static constexpr int kU = FG_MERGE_U;
+};
 
-template <bool C>
+// v[k][slot]: value slot k (one slot; kNV for a multi-value operator)
+template <bool C, bool MV = false>
 struct LdsTableT;
 template <>
-struct LdsTableT<false> {
+struct LdsTableT<false, false> {
     alignas(16) int64_t key[kSlots + 1];      // slot kSlots: the key equal to the sentinel
     unsigned long long cs[kSlots + 1];        // COUNT(*)
     unsigned long long cn[kSlots + 1];        // records whose value was NULL
-    unsigned long long sum[kSlots + 1];       // SUM / AVG sum (i64, or f64 bits)
+    unsigned long long v[1][kSlots + 1];      // SUM / AVG sum (i64, or f64 bits) or MIN / MAX
 };
 template <>
-struct LdsTableT<true> {
+struct LdsTableT<true, false> {
     alignas(16) int64_t key[kCompactSlots + 1];
-    unsigned long long sum[kCompactSlots + 1];
+    unsigned long long v[1][kCompactSlots + 1];
     uint32_t cs[kCompactSlots + 1];
+};
+template <>
+struct LdsTableT<false, true> {
+    alignas(16) int64_t key[kSlotsMV + 1];
+    unsigned long long cs[kSlotsMV + 1];
+    unsigned long long cn[kSlotsMV + 1];
+    unsigned long long v[kNV][kSlotsMV + 1];
+};
+template <>
+struct LdsTableT<true, true> {
+    alignas(16) int64_t key[kCompactSlotsMV + 1];
+    unsigned long long v[kNV][kCompactSlotsMV + 1];
+    uint32_t cs[kCompactSlotsMV + 1];
 };
 
 // Home bucket: the low 32 bits of the key's mix h (the region is its top bits; the low
@@ -1302,17 +1328,17 @@ struct LdsTableT<true> {
 // a key sits in its home bucket ~99 % of the time, against ~84 % for a single home slot, so
 // a wave's lanes rarely leave the fast path.
 constexpr int kBucket = 4;
-template <bool C>
+template <bool C, bool MV>
 __device__ __forceinline__ uint32_t lds_home(int64_t h) {
-    constexpr uint32_t NB = (uint32_t)(MergeCfg<C>::kSlotsT / kBucket);
+    constexpr uint32_t NB = (uint32_t)(MergeCfg<C, MV>::kSlotsT / kBucket);
     return __umulhi((uint32_t)(uint64_t)h, NB) * kBucket;
 }
 
 // linear probe from `slot` (keys never leave the table during a region, so a key is at the
 // first slot from its home that was empty or held it when it was inserted)
-template <bool C>
-__device__ __forceinline__ int lds_find_or_insert_from(LdsTableT<C>& t, int64_t k, uint32_t slot, bool& full) {
-    constexpr int S = MergeCfg<C>::kSlotsT;
+template <bool C, bool MV>
+__device__ __forceinline__ int lds_find_or_insert_from(LdsTableT<C, MV>& t, int64_t k, uint32_t slot, bool& full) {
+    constexpr int S = MergeCfg<C, MV>::kSlotsT;
     for (int probe = 0; probe < S; probe++) {
         const int64_t cur = t.key[slot];
         if (cur == k) return (int)slot;
@@ -1327,18 +1353,18 @@ __device__ __forceinline__ int lds_find_or_insert_from(LdsTableT<C>& t, int64_t 
     return -1;
 }
 
-template <bool C>
-__device__ __forceinline__ int lds_find_or_insert(LdsTableT<C>& t, int64_t k, bool& full) {
-    if (k == JMIN) return MergeCfg<C>::kSlotsT;
-    return lds_find_or_insert_from<C>(t, k, lds_home<C>(k), full);
+template <bool C, bool MV>
+__device__ __forceinline__ int lds_find_or_insert(LdsTableT<C, MV>& t, int64_t k, bool& full) {
+    if (k == JMIN) return MergeCfg<C, MV>::kSlotsT;
+    return lds_find_or_insert_from<C, MV>(t, k, lds_home<C, MV>(k), full);
 }
 
 // slot of key k given its home bucket's keys (read beforehand): a match, else a CAS on the
 // bucket's first empty slot, else (full bucket / lost CAS) the linear probe
-template <bool C>
-__device__ __forceinline__ int lds_bucket_slot(LdsTableT<C>& t, int64_t k, uint32_t home, RecV2 b01, RecV2 b23,
+template <bool C, bool MV>
+__device__ __forceinline__ int lds_bucket_slot(LdsTableT<C, MV>& t, int64_t k, uint32_t home, RecV2 b01, RecV2 b23,
                                                bool& full) {
-    constexpr uint32_t S_ = (uint32_t)MergeCfg<C>::kSlotsT;
+    constexpr uint32_t S_ = (uint32_t)MergeCfg<C, MV>::kSlotsT;
     if (k == JMIN) return (int)S_;
     const int64_t q[kBucket] = {b01.x, b01.y, b23.x, b23.y};
     int hit = -1, empty = -1;
@@ -1353,15 +1379,17 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C>& t, int64_t k, uint3
         const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&t.key[e]),
                                                  (unsigned long long)JMIN, (unsigned long long)k);
         if (old == (unsigned long long)JMIN || old == (unsigned long long)k) return (int)e;
-        return lds_find_or_insert_from<C>(t, k, e + 1 >= S_ ? 0u : e + 1, full);
+        return lds_find_or_insert_from<C, MV>(t, k, e + 1 >= S_ ? 0u : e + 1, full);
     }
     const uint32_t nx = home + kBucket;
-    return lds_find_or_insert_from<C>(t, k, nx >= S_ ? 0u : nx, full);
+    return lds_find_or_insert_from<C, MV>(t, k, nx >= S_ ? 0u : nx, full);
 }
 // one fired row: key, window bounds, (DataStream) output timestamp and the aggregates of
 // the accumulator {COUNT(*), NULL count, sum} (a6: Count1/Count/Sum/AvgAggFunction)
+// v: the entry's value slots (one; kNV for a multi-value operator, aggregate a reading slot
+// p.agg_slot[a]); vt: the kernel value op (its low bits the value type)
 __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long long o, int64_t h,
-                                          unsigned long long cs, unsigned long long cn, int64_t sum, int vt) {
+                                          unsigned long long cs, unsigned long long cn, const int64_t* vals, int vt) {
     p.out_key[o] = key_of(h);   // state holds the key's mix
     p.out_ws[o] = p.wstart;
     p.out_we[o] = p.wend;
@@ -1372,6 +1400,7 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
     for (int a = 0; a < kMaxAggs; a++) {
         if (a >= p.num_aggs) break;
         int64_t v = 0;
+        const int64_t sum = vals[p.mv ? p.agg_slot[a] : 0];
         switch (p.aggs[a]) {
             case 0: v = (int64_t)cs; break;   // COUNT(*)
             case 1: v = cv; break;            // COUNT(v)
@@ -1387,7 +1416,7 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
                 break;
             default:                          // AVG(v): count == 0 ? NULL : sum / count
                 if (cv == 0) nm |= (uint8_t)(1u << a);
-                else if (vt == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
+                else if ((vt & 3) == 2) v = __double_as_longlong(__longlong_as_double(sum) / (double)cv);
                 else v = sum / cv;
                 break;
         }
@@ -1440,28 +1469,50 @@ __device__ __forceinline__ void lds_minmax_f64(unsigned long long* a, int64_t bi
     }
 }
 
-template <bool C>
-__device__ __forceinline__ void lds_add(LdsTableT<C>& t, int slot, unsigned long long cs, unsigned long long cn,
-                                        int64_t sum_bits, int vt) {
+// one value slot: `bits` into *a with the kernel value op vtk (val_type | op << 2; 0: none).
+// MIN / MAX skip an accumulator with COUNT(v) = 0 (it holds no value: has_value false).
+__device__ __forceinline__ void lds_val(unsigned long long* a, int64_t bits, int vtk, bool has_value) {
+    if (vtk == 2) {
+        atomicAdd(reinterpret_cast<double*>(a), __longlong_as_double(bits));
+    } else if (vtk == 1) {
+        atomicAdd(a, (unsigned long long)bits);
+    } else if (vtk > 3 && has_value) {
+        switch (vtk) {
+            case 1 | (1 << kOpShift): atomicMin(reinterpret_cast<long long*>(a), (long long)bits); break;
+            case 1 | (2 << kOpShift): atomicMax(reinterpret_cast<long long*>(a), (long long)bits); break;
+            case 2 | (1 << kOpShift): lds_minmax_f64<true>(a, bits); break;
+            case 2 | (2 << kOpShift): lds_minmax_f64<false>(a, bits); break;
+            default: break;
+        }
+    }
+}
+
+// Accumulate {COUNT(*), NULL count, values} into a slot. vt: the kernel value op for a
+// single-value table; for a multi-value table the value type (0: a NULL record, no value),
+// slot k taking op p.vop[k]. vals: one value per slot (a record's value repeated).
+template <bool C, bool MV>
+__device__ __forceinline__ void lds_add(LdsTableT<C, MV>& t, int slot, unsigned long long cs, unsigned long long cn,
+                                        const int64_t* vals, int vt, const MergeParams& p) {
     if constexpr (C) {
         atomicAdd(&t.cs[slot], (uint32_t)cs);
     } else {
         atomicAdd(&t.cs[slot], cs);
         if (cn) atomicAdd(&t.cn[slot], cn);
     }
-    if (vt == 2) {
-        atomicAdd(reinterpret_cast<double*>(&t.sum[slot]), __longlong_as_double(sum_bits));
-    } else if (vt == 1) {
-        atomicAdd(&t.sum[slot], (unsigned long long)sum_bits);
-    } else if (vt > 3 && cn < cs) {   // MIN / MAX; an accumulator with COUNT(v) = 0 holds no value
-        switch (vt) {
-            case 1 | (1 << kOpShift): atomicMin(reinterpret_cast<long long*>(&t.sum[slot]), (long long)sum_bits); break;
-            case 1 | (2 << kOpShift): atomicMax(reinterpret_cast<long long*>(&t.sum[slot]), (long long)sum_bits); break;
-            case 2 | (1 << kOpShift): lds_minmax_f64<true>(&t.sum[slot], sum_bits); break;
-            case 2 | (2 << kOpShift): lds_minmax_f64<false>(&t.sum[slot], sum_bits); break;
-            default: break;
-        }
+    if constexpr (!MV) {
+        lds_val(&t.v[0][slot], vals[0], vt, cn < cs);
+    } else if (vt) {
+#pragma unroll
+        for (int k = 0; k < kNV; k++)
+            if (p.vop[k] < 3) lds_val(&t.v[k][slot], vals[k], (vt & 3) | (p.vop[k] << kOpShift), cn < cs);
     }
+}
+// the same with one value for every slot (a staged record)
+template <bool C, bool MV>
+__device__ __forceinline__ void lds_add1(LdsTableT<C, MV>& t, int slot, unsigned long long cs, unsigned long long cn,
+                                         int64_t bits, int vt, const MergeParams& p) {
+    const int64_t vals[kNV] = {bits, bits, bits};
+    lds_add<C, MV>(t, slot, cs, cn, vals, vt, p);
 }
 
 
@@ -1480,16 +1531,16 @@ struct MergeCursor {
 
 // VTC >= 0: the value op compiled in (kernel vt = val_type | op << 2: the LDS adds, identity and
 // row arithmetic of that op only -- a small straight-line stream loop); -1: read p.val_type
-template <bool C, int VTC>
+template <bool C, int VTC, bool MV = false>
 // waves_per_eu(4): 128 VGPRs, so two compact workgroups (16 waves) fit a CU
-__global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_merge(MergeParams p) {
-    constexpr int S = MergeCfg<C>::kSlotsT;
-    constexpr int T = MergeCfg<C>::kThreads;
+__global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_waves_per_eu(4))) void k_merge(MergeParams p) {
+    constexpr int S = MergeCfg<C, MV>::kSlotsT;
+    constexpr int T = MergeCfg<C, MV>::kThreads;
     constexpr int kWaves = T / 64;
     constexpr int kRounds = (S + T - 1) / T + 1;    // + 1: the sentinel slot (thread 0)
-    constexpr int kMergeU = MergeCfg<C>::kU;
+    constexpr int kMergeU = MergeCfg<C, MV>::kU;
     constexpr uint32_t kChunk = kMergeU * T;
-    __shared__ LdsTableT<C> t;
+    __shared__ LdsTableT<C, MV> t;
     __shared__ uint32_t s_grp[kRounds * kWaves];   // per (round, wave) row counts -> offsets
     __shared__ unsigned int s_flags;
     __shared__ uint32_t s_total;
@@ -1500,9 +1551,13 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
     __shared__ const int64_t* s_sbase[kMaxSrcFlat];            //   and each table's region base
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
-    const int cap = kRegionCap;
-    const int vt = VTC >= 0 ? VTC : p.val_type;
-    const int64_t vinit = val_identity(vt);
+    constexpr int cap = MV ? kRegionCapMV : kRegionCap;   // table entries per region
+    constexpr int cols = MV ? 3 + kNV : 4;               // 8-byte words per table entry
+    constexpr int NVS = MV ? kNV : 1;                    // value slots
+    const int vt = VTC >= 0 ? VTC : p.val_type;          // (MV: the value type; slot k has op p.vop[k])
+    int64_t vinit[NVS];
+#pragma unroll
+    for (int k = 0; k < NVS; k++) vinit[k] = MV ? val_identity((vt & 3) | (p.vop[k] << kOpShift)) : val_identity(vt);
     const int P = 1 << p.region_bits;
     const int G = gridDim.x;
     // regions: all P (strided over the grid), the heavy pass's list, or a retry's list
@@ -1564,7 +1619,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
         RecV2 b01[kMergeU], b23[kMergeU];
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
-            home[u] = lds_home<C>(c[u].x);
+            home[u] = lds_home<C, MV>(c[u].x);
             const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
             b01[u] = kb[0];
             b23[u] = kb[1];
@@ -1580,7 +1635,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 if (q[j] == k) hit = j;
                 if (q[j] == JMIN) empty = j;
             }
-            constexpr uint32_t S_ = (uint32_t)MergeCfg<C>::kSlotsT;
+            constexpr uint32_t S_ = (uint32_t)MergeCfg<C, MV>::kSlotsT;
             int slot;
             if (FG_DIAG_MERGE & 2) {
                 slot = (int)home[u] + (hit >= 0 ? hit : 0);
@@ -1594,12 +1649,12 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&t.key[e]),
                                                          (unsigned long long)JMIN, (unsigned long long)k);
                 if (old == (unsigned long long)JMIN || old == (unsigned long long)k) slot = (int)e;
-                else slot = lds_find_or_insert_from<C>(t, k, e + 1 >= S_ ? 0u : e + 1, full);
+                else slot = lds_find_or_insert_from<C, MV>(t, k, e + 1 >= S_ ? 0u : e + 1, full);
             } else {                   // full bucket: probe on from the next one
                 const uint32_t nx = home[u] + kBucket;
-                slot = lds_find_or_insert_from<C>(t, k, nx >= S_ ? 0u : nx, full);
+                slot = lds_find_or_insert_from<C, MV>(t, k, nx >= S_ ? 0u : nx, full);
             }
-            if (!(FG_DIAG_MERGE & 1) && slot >= 0) lds_add<C>(t, slot, 1ull, 0ull, c[u].y, vt);
+            if (!(FG_DIAG_MERGE & 1) && slot >= 0) lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
             if ((FG_DIAG_MERGE & 1) && slot >= 0) t.cs[slot] = 1;
         }
     };
@@ -1657,7 +1712,8 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             t.key[i] = JMIN;
             t.cs[i] = 0;
             if constexpr (!C) t.cn[i] = 0;
-            t.sum[i] = (unsigned long long)vinit;
+#pragma unroll
+            for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)vinit[k];
         }
         if (tid == 0) s_flags = 0;
         if constexpr (!C) if (tid < 64) {   // source tables: per-region entry counts -> flat prefix
@@ -1670,7 +1726,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             }
             if (tid < nsrc) {
                 s_soff[tid + 1] = x;
-                s_sbase[tid] = p.src[tid].base + (int64_t)r * 4 * cap;
+                s_sbase[tid] = p.src[tid].base + (int64_t)r * cols * cap;
             }
             if (tid == 0) s_soff[0] = 0;
         }
@@ -1688,7 +1744,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
         if constexpr (!C) {
             const uint32_t NT = skip ? 0u : s_soff[p.n_src <= kMaxSrcFlat ? p.n_src : 0];
             for (uint32_t i0 = 0; i0 < NT; i0 += kSrcU * T) {
-                int64_t k[kSrcU], cs[kSrcU], cn[kSrcU], sm[kSrcU];
+                int64_t k[kSrcU], cs[kSrcU], cn[kSrcU], sm[kSrcU][NVS];
                 int j = 0;
                 {   // table of this thread's first entry (binary search), later ones advance
                     const uint32_t f = i0 + tid;
@@ -1713,7 +1769,8 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     k[u] = base[i];
                     cs[u] = base[cap + i];
                     cn[u] = base[2 * cap + i];
-                    sm[u] = base[3 * cap + i];
+#pragma unroll
+                    for (int q = 0; q < NVS; q++) sm[u][q] = base[(3 + q) * cap + i];
                     mk[u] = ((p.mark_mask >> j) & 1ull) != 0;
                     if ((p.markonly_mask >> j) & 1ull) cs[u] = 0;   // a mark-only source adds nothing
                 }
@@ -1721,7 +1778,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                 RecV2 b01[kSrcU], b23[kSrcU];
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
-                    home[u] = lds_home<C>(k[u]);
+                    home[u] = lds_home<C, MV>(k[u]);
                     const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
                     b01[u] = kb[0];
                     b23[u] = kb[1];
@@ -1729,25 +1786,29 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
                     if (i0 + u * T + tid >= NT) continue;
-                    const int slot = lds_bucket_slot<C>(t, k[u], home[u], b01[u], b23[u], full);
+                    const int slot = lds_bucket_slot<C, MV>(t, k[u], home[u], b01[u], b23[u], full);
                     if (slot < 0) continue;
                     // (a zero accumulator -- a chain table's key -- adds nothing, only its mark)
-                    if (cs[u]) lds_add<C>(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt);
+                    if (cs[u]) lds_add<C, MV>(t, slot, (unsigned long long)cs[u], (unsigned long long)cn[u], sm[u], vt, p);
                     if constexpr (!C) if (mk[u]) atomicOr(&t.cn[slot], kMarkBit);
                 }
             }
             for (int j = 0; !skip && p.n_src > kMaxSrcFlat && j < p.n_src; j++) {   // many tables: one by one
                 const TableRef src = p.src[j];
                 const uint32_t n = gbl(src.counts)[r];
-                const auto base = gbl(src.base + (int64_t)r * 4 * cap);
+                const auto base = gbl(src.base + (int64_t)r * cols * cap);
                 const bool mkj = j < 64 && ((p.mark_mask >> j) & 1ull) != 0;
                 const bool moj = j < 64 && ((p.markonly_mask >> j) & 1ull) != 0;
                 for (uint32_t i = tid; i < n; i += T) {
-                    const int slot = lds_find_or_insert<C>(t, base[i], full);
+                    const int slot = lds_find_or_insert<C, MV>(t, base[i], full);
                     if (slot < 0) continue;
-                    if (base[cap + i] && !moj)
-                        lds_add<C>(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
-                                   base[3 * cap + i], vt);
+                    if (base[cap + i] && !moj) {
+                        int64_t vv[NVS];
+#pragma unroll
+                        for (int q = 0; q < NVS; q++) vv[q] = base[(3 + q) * cap + i];
+                        lds_add<C, MV>(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
+                                       vv, vt, p);
+                    }
                     if constexpr (!C) if (mkj) atomicOr(&t.cn[slot], kMarkBit);
                 }
             }
@@ -1786,10 +1847,10 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     }
                     const int64_t at = (int64_t)c * kPartStride;
                     for (uint32_t i = tid; i < n; i += T) {
-                        const int slot = lds_find_or_insert<C>(t, gbl(p.part_key)[at + i], full);
-                        if (slot >= 0)
-                            lds_add<C>(t, slot, (unsigned long long)gbl(p.part_cs)[at + i],
-                                       (unsigned long long)gbl(p.part_cn)[at + i], gbl(p.part_sum)[at + i], vt);
+                        const int slot = lds_find_or_insert<C, MV>(t, gbl(p.part_key)[at + i], full);
+                        if (slot >= 0)   // (a multi-value operator takes no heavy pass)
+                            lds_add1<C, MV>(t, slot, (unsigned long long)gbl(p.part_cs)[at + i],
+                                            (unsigned long long)gbl(p.part_cn)[at + i], gbl(p.part_sum)[at + i], vt, p);
                     }
                 }
             }
@@ -1810,27 +1871,33 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
                     const auto cst = gbl(sb.cnt_star), cnl = gbl(sb.cnt_null), sval = gbl(sb.val);
                     for (uint32_t i = beg + tid; i < end; i += T) {
                         if (!mine(srec[i])) continue;
-                        const int slot = lds_find_or_insert<C>(t, srec[i], full);
-                        if (slot >= 0)
-                            lds_add<C>(t, slot, (unsigned long long)cst[i], (unsigned long long)cnl[i], sval[i], vt);
+                        const int slot = lds_find_or_insert<C, MV>(t, srec[i], full);
+                        if (slot < 0) continue;
+                        int64_t vv[NVS];
+                        vv[0] = sval[i];
+                        if constexpr (MV) {
+                            vv[1] = gbl(sb.val1)[i];
+                            vv[2] = gbl(sb.val2)[i];
+                        }
+                        lds_add<C, MV>(t, slot, (unsigned long long)cst[i], (unsigned long long)cnl[i], vv, vt, p);
                     }
                 } else if (sb.stride == 2) {
                     const GlobalRec rec = (GlobalRec)sb.rec;
                     for (uint32_t i = beg + tid; i < end; i += T) {
                         const RecV2 rc = rec[i];
                         if (!mine(rc.x)) continue;
-                        const int slot = lds_find_or_insert<C>(t, rc.x, full);
+                        const int slot = lds_find_or_insert<C, MV>(t, rc.x, full);
                         if (slot < 0) continue;
                         const bool isnull = vnull != nullptr && vnull[i] != 0;
-                        lds_add<C>(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt);
+                        lds_add1<C, MV>(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt, p);
                     }
                 } else {
                     for (uint32_t i = beg + tid; i < end; i += T) {
                         if (!mine(srec[i])) continue;
-                        const int slot = lds_find_or_insert<C>(t, srec[i], full);
+                        const int slot = lds_find_or_insert<C, MV>(t, srec[i], full);
                         if (slot < 0) continue;
                         const bool isnull = vnull != nullptr && vnull[i];
-                        lds_add<C>(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0);
+                        lds_add1<C, MV>(t, slot, 1ull, isnull ? 1ull : 0ull, 0, 0, p);
                     }
                 }
             }
@@ -1899,7 +1966,7 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
         const unsigned int fl = s_flags;
         const bool write_dst = !skip && p.has_dst && !(fl & 5u);
         const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 7u);
-        int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * 4 * cap : nullptr;
+        int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * cols * cap : nullptr;
         const unsigned long long obase = s_out_base;
         // per round: the wave's occupied lanes below this lane give the rank within the group
 #pragma unroll
@@ -1912,15 +1979,18 @@ __global__ __launch_bounds__(MergeCfg<C>::kThreads) __attribute__((amdgpu_waves_
             const int64_t key = slot == S ? JMIN : t.key[slot];
             unsigned long long cs = t.cs[slot], cn = 0;
             if constexpr (!C) cn = t.cn[slot] & ~kMarkBit;
-            const int64_t sum = (int64_t)t.sum[slot];
+            int64_t vv[NVS];
+#pragma unroll
+            for (int q = 0; q < NVS; q++) vv[q] = (int64_t)t.v[q][slot];
             if (write_dst) {
                 const bool chain = !C && p.dst_mode != 0;   // a chain table holds keys with zero accumulators
                 dbase[at] = key;
                 dbase[cap + at] = chain ? 0 : (int64_t)cs;
                 dbase[2 * cap + at] = chain ? 0 : (int64_t)cn;
-                dbase[3 * cap + at] = chain ? vinit : sum;
+#pragma unroll
+                for (int q = 0; q < NVS; q++) dbase[(3 + q) * cap + at] = chain ? vinit[q] : vv[q];
             }
-            if (write_out) write_row(p, obase + at, key, cs, cn, sum, vt);
+            if (write_out) write_row(p, obase + at, key, cs, cn, vv, vt);
         }
         if (tid == 0 && write_dst) {
             const uint32_t total = s_total;
@@ -1954,10 +2024,14 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit_table(MergeParams p, Tabl
     __syncthreads();
     const unsigned long long b = s_base;
     if ((int64_t)(b + n) > p.out_cap) return;
-    const auto base = gbl(t.base + (int64_t)r * 4 * kRegionCap);
-    for (uint32_t i = threadIdx.x; i < n; i += kEmitThreads)
-        write_row(p, b + i, base[i], (unsigned long long)base[kRegionCap + i], (unsigned long long)base[2 * kRegionCap + i],
-                  base[3 * kRegionCap + i], p.val_type);
+    const int cap = table_cap(p.mv);
+    const auto base = gbl(t.base + (int64_t)r * table_cols(p.mv) * cap);
+    for (uint32_t i = threadIdx.x; i < n; i += kEmitThreads) {
+        int64_t vv[kNV];
+        for (int q = 0; q < (p.mv ? kNV : 1); q++) vv[q] = base[(3 + q) * cap + i];
+        write_row(p, b + i, base[i], (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i], vv,
+                  p.val_type);
+    }
 }
 
 hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_t s) {
@@ -1966,6 +2040,16 @@ hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_
 }
 
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {
+    if (p.mv) {   // multi-value operator (no heavy pass)
+        if (p.heavy || p.region_list) return hipErrorInvalidValue;
+        if (p.compact) {
+            if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
+            hipLaunchKernelGGL((k_merge<true, -1, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p);
+        } else {
+            hipLaunchKernelGGL((k_merge<false, -1, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+        }
+        return hipGetLastError();
+    }
     if (p.compact) {
         if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
         // the compact merge (the TUMBLE fire of plain staged records) per value op
@@ -2046,7 +2130,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_heavy_plan(HeavyPlan hp) {
 // LDS atomics of a hot slot drop from one per record to one per wave.
 __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
     constexpr int T = kMergeThreads;
-    __shared__ LdsTableT<false> t;
+    __shared__ LdsTableT<false, false> t;   // (single-value operators only)
     __shared__ uint32_t s_n;
     __shared__ unsigned int s_full;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2058,7 +2142,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
             t.key[i] = JMIN;
             t.cs[i] = 0;
             t.cn[i] = 0;
-            t.sum[i] = (unsigned long long)vinit;
+            t.v[0][i] = (unsigned long long)vinit;
         }
         if (tid == 0) {
             s_n = 0;
@@ -2121,14 +2205,18 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
                     if (in) {
                         done = true;
                         if (lane == __ffsll((long long)m) - 1) {
-                            const int slot = lds_find_or_insert<false>(t, k0, full);
-                            if (slot >= 0) lds_add<false>(t, slot, (unsigned long long)__popcll(m), 0ull, part, vt);
+                            const int slot = lds_find_or_insert<false, false>(t, k0, full);
+                            if (slot >= 0) lds_val(&t.v[0][slot], part, vt, true), atomicAdd(&t.cs[slot], (unsigned long long)__popcll(m));
                         }
                     }
                 }
                 if (!done) {
-                    const int slot = lds_find_or_insert<false>(t, k, full);
-                    if (slot >= 0) lds_add<false>(t, slot, cs, cn, sum, cn == 1 && !sb.is_acc ? 0 : vt);
+                    const int slot = lds_find_or_insert<false, false>(t, k, full);
+                    if (slot >= 0) {
+                        atomicAdd(&t.cs[slot], cs);
+                        if (cn) atomicAdd(&t.cn[slot], cn);
+                        lds_val(&t.v[0][slot], sum, cn == 1 && !sb.is_acc ? 0 : vt, cn < cs);
+                    }
                 }
             }
             acc += len;
@@ -2142,7 +2230,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
             hp.part_key[at + o] = i == kSlots ? JMIN : t.key[i];
             hp.part_cs[at + o] = (int64_t)t.cs[i];
             hp.part_cn[at + o] = (int64_t)t.cn[i];
-            hp.part_sum[at + o] = (int64_t)t.sum[i];
+            hp.part_sum[at + o] = (int64_t)t.v[0][i];
         }
         lds_barrier();
         if (tid == 0) {
@@ -2171,15 +2259,20 @@ hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStrea
 __global__ __launch_bounds__(256) void k_export(ExportParams p) {
     const int r = blockIdx.x;
     const uint32_t n = p.t.counts[r];
-    const int64_t* base = p.t.base + (int64_t)r * 4 * kRegionCap;
+    const int cap = table_cap(p.mv);
+    const int64_t* base = p.t.base + (int64_t)r * table_cols(p.mv) * cap;
     const uint64_t o = p.region_off[r];
     for (uint32_t i = threadIdx.x; i < n; i += 256) {
-        const int64_t cs = base[kRegionCap + i], cn = base[2 * kRegionCap + i];
+        const int64_t cs = base[cap + i], cn = base[2 * cap + i];
         p.out_key[o + i] = key_of(base[i]);
         p.out_slice[o + i] = p.slice_end;
         p.out_cnt_star[o + i] = cs;
         p.out_cnt_val[o + i] = cs - cn;
-        p.out_sum[o + i] = base[3 * kRegionCap + i];
+        p.out_sum[o + i] = base[3 * cap + i];
+        if (p.mv) {
+            p.out_v1[o + i] = base[4 * cap + i];
+            p.out_v2[o + i] = base[5 * cap + i];
+        }
     }
 }
 
@@ -2196,7 +2289,7 @@ hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s) 
 // ----------------------------------------------------------------------------------------
 constexpr int kSplitThreads = 256;
 __global__ __launch_bounds__(kSplitThreads) void k_split_table(TableRef src, TableRef dst, int32_t old_bits,
-                                                               int32_t shift) {
+                                                               int32_t shift, int32_t mv) {
     __shared__ uint32_t s_cnt[1 << 13];
     const int r = blockIdx.x;
     const int nch = 1 << shift;
@@ -2204,25 +2297,23 @@ __global__ __launch_bounds__(kSplitThreads) void k_split_table(TableRef src, Tab
     for (int c = threadIdx.x; c < nch; c += kSplitThreads) s_cnt[c] = 0;
     __syncthreads();
     const uint32_t n = gbl(src.counts)[r];
-    const auto sb = gbl(src.base + (int64_t)r * 4 * kRegionCap);
+    const int cap = table_cap(mv), cols = table_cols(mv);
+    const auto sb = gbl(src.base + (int64_t)r * cols * cap);
     for (uint32_t i = threadIdx.x; i < n; i += kSplitThreads) {
         const int64_t h = sb[i];
         const int c = (int)(((uint64_t)h >> (64 - new_bits)) & (uint64_t)(nch - 1));
         const uint32_t at = atomicAdd(&s_cnt[c], 1u);
-        int64_t* db = dst.base + ((int64_t)r * nch + c) * 4 * kRegionCap;
-        db[at] = h;
-        db[kRegionCap + at] = sb[kRegionCap + i];
-        db[2 * kRegionCap + at] = sb[2 * kRegionCap + i];
-        db[3 * kRegionCap + at] = sb[3 * kRegionCap + i];
+        int64_t* db = dst.base + ((int64_t)r * nch + c) * cols * cap;
+        for (int w = 0; w < cols; w++) db[w * cap + at] = sb[w * cap + i];
     }
     __syncthreads();
     for (int c = threadIdx.x; c < nch; c += kSplitThreads) dst.counts[(int64_t)r * nch + c] = s_cnt[c];
 }
 
-hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift,
+hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift, int32_t mv,
                               hipStream_t s) {
     if (shift < 1 || old_bits < 0 || old_bits + shift > 13) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_table, dim3(1u << old_bits), dim3(kSplitThreads), 0, s, src, dst, old_bits, shift);
+    hipLaunchKernelGGL(k_split_table, dim3(1u << old_bits), dim3(kSplitThreads), 0, s, src, dst, old_bits, shift, mv);
     return hipGetLastError();
 }
 

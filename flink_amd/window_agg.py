@@ -102,7 +102,14 @@ class WindowAggOperator:
         self.val_type = {"none": L.VAL_NONE, "i64": L.VAL_I64, "f64": L.VAL_F64}[val_type]
         self.local_partials = bool(local_partials)
         if self.local_partials:
-            # the partial accumulator: SUM, or the MIN / MAX of a MIN / MAX query
+            # the partial accumulator: SUM, or the MIN / MAX of a MIN / MAX query (one kind: the
+            # partial row holds one value accumulator, as the engine checks for the C-ABI)
+            kinds = {("min" if a in ("min", L.AGG_MIN) else "max" if a in ("max", L.AGG_MAX) else
+                      "sum" if a in ("sum", "avg", "sum0", L.AGG_SUM, L.AGG_AVG, L.AGG_SUM0) else None)
+                     for a in aggs} - {None}
+            if len(kinds) > 1:
+                raise L.WindowSpecError("FG_FLAG_LOCAL_PARTIALS: the partial row holds one value accumulator, "
+                                        f"but the aggregate list names {sorted(kinds)}")
             vagg = next((a for a in aggs if a in ("min", "max", L.AGG_MIN, L.AGG_MAX)), "sum")
             aggs = ("count_star", "count", AGG_NAMES.get(vagg, vagg))
         self.aggs = tuple(AGGS[a] if isinstance(a, str) else int(a) for a in aggs)
@@ -333,15 +340,17 @@ class WindowAggOperator:
 
         img = dict(key=col(s.key), slice_end=col(s.slice_end), cnt_star=col(s.cnt_star), cnt_val=col(s.cnt_val),
                    sum=col(s.sum))
+        if s.min:   # several value accumulators: the MIN and MAX slots too
+            img["min"], img["max"] = col(s.min), col(s.max)
         return img, wm.value
 
     def restore_state(self, image, timer_watermark: int):
-        cols = {k: np.ascontiguousarray(image[k], dtype=np.int64) for k in
-                ("key", "slice_end", "cnt_star", "cnt_val", "sum")}
+        names = ("key", "slice_end", "cnt_star", "cnt_val", "sum") + (("min", "max") if "min" in image else ())
+        cols = {k: np.ascontiguousarray(image[k], dtype=np.int64) for k in names}
         s = L.FgStateRows()
         s.n = len(cols["key"])
-        s.key, s.slice_end, s.cnt_star, s.cnt_val, s.sum = (cols[k].ctypes.data for k in
-                                                            ("key", "slice_end", "cnt_star", "cnt_val", "sum"))
+        for k in names:
+            setattr(s, k, cols[k].ctypes.data)
         L.check(self._lib.fg_restore(self._h, C.byref(s), int(timer_watermark)), self._h)
 
     # -- metrics ------------------------------------------------------------------------------------

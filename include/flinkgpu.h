@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 4
+#define FG_ABI_VERSION 5
 
 enum fg_status {
     FG_OK = 0,
@@ -79,10 +79,11 @@ enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
  * its value is the AVG accumulator's sum. */
 /* MIN / MAX (MinAggFunction.java:56-90, MaxAggFunction.java:56-96, TP/functions/aggfunctions/):
  * NULL-initialised; a non-null operand replaces the accumulator iff operand < min (> max),
- * Java primitive comparison; NULL when the window holds no non-null value. An operator keeps
- * ONE value accumulator per (key, slice), so MIN and MAX each take an operator of their own
- * and do not mix with SUM / AVG / SUM0 (COUNT(*) and COUNT do mix): FG_EINVAL otherwise. A
- * query with several value aggregates opens one handle per accumulator kind. */
+ * Java primitive comparison; NULL when the window holds no non-null value. An aggregate list
+ * may mix SUM / AVG / SUM0, MIN and MAX over the value column: the operator then keeps all three
+ * value accumulators per (key, slice), as the reference's generated accumulator row does
+ * (AggsHandlerCodeGenerator.scala:578-700), staging each record once. The two-phase operators
+ * (FG_FLAG_LOCAL_PARTIALS / fg_add_partials) carry one value accumulator per partial row. */
 enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3, FG_AGG_SUM0 = 4,
               FG_AGG_MIN = 5, FG_AGG_MAX = 6 };
 /* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
@@ -218,7 +219,12 @@ typedef struct fg_state_rows {
     const int64_t* slice_end;     /* namespace of WindowValueState */
     const int64_t* cnt_star;      /* COUNT(*) accumulator */
     const int64_t* cnt_val;       /* COUNT(v) accumulator */
-    const int64_t* sum;           /* SUM/AVG sum accumulator (i64 or f64 bits) */
+    const int64_t* sum;           /* SUM/AVG sum accumulator (i64 or f64 bits); a MIN- or MAX-only
+                                   * operator: its MIN / MAX accumulator */
+    const int64_t* min;           /* an operator with several value accumulators (SUM family, MIN,
+                                   * MAX in one aggregate list): the MIN and MAX accumulators (the
+                                   * identity where absent); NULL for other operators */
+    const int64_t* max;
 } fg_state_rows;
 
 typedef struct fg_stats {

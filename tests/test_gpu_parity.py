@@ -43,7 +43,7 @@ def sort_rows(r):
 F64_EPS = float(np.finfo(np.float64).eps)
 
 
-def assert_rows_equal(got, exp, vt, ctx="", sum0=True, minmax=(), vmax=None):
+def assert_rows_equal(got, exp, vt, ctx="", sum0=True, minmax=(), vmax=None, sums=None):
     """vmax (mixed-sign DOUBLE streams): besides the 1e-9 relative bar, a row passes when
     |a - b| <= 2 (n - 1) eps n vmax -- the worst-case difference of two summation orders of
     n values with |x| <= vmax (each within (n - 1) eps sum|x| of the exact sum); a near-
@@ -62,7 +62,8 @@ def assert_rows_equal(got, exp, vt, ctx="", sum0=True, minmax=(), vmax=None):
             a, b = g[f][ok].view(np.int64), e[f][ok].view(np.int64)
             bad = np.nonzero(a != b)[0]
             assert len(bad) == 0, f"{ctx}: {m.upper()} differs at {bad[:5]}: {g[f][ok][bad[:5]]} vs {e[f][ok][bad[:5]]}"
-        return
+        if not sums:   # a MIN / MAX-only operator; several accumulators check the SUM family too
+            return
     if vt == "i64":
         ok = e["sum_null"] == 0
         assert np.array_equal(g["sum_i"][ok], e["sum_i"][ok]), f"{ctx}: i64 SUM differs"
@@ -90,6 +91,9 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
     key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
     vmax = 1000.0 if gen.get("signed") and cfg["val_type"] == "f64" else None
     mm = tuple(a for a in cfg.get("aggs", ()) if a in ("min", "max"))
+    aggs = cfg.get("aggs")
+    chk = dict(minmax=mm, vmax=vmax, sums=aggs is None or any(a in ("sum", "avg", "sum0") for a in aggs),
+               sum0=aggs is None or "sum0" in aggs)
     g = gpu_mk(cfg, expected_keys=keys if expected_keys is None else expected_keys, buffer_records=max(batch * 4, 1 << 16),
                kernel_timing=kstats is not None)
     o = oracle_mk(O, cfg)
@@ -101,7 +105,7 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
         o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], nl)
         g.process_watermark(wm)
         o.process_watermark(wm)
-        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"step {step} wm {wm}", minmax=mm, vmax=vmax)
+        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"step {step} wm {wm}", **chk)
         assert g.late_dropped == o_base + o.late_dropped, f"late drops differ at step {step}"
         step += 1
         if snapshot_at is not None and step == snapshot_at:
@@ -114,7 +118,7 @@ def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at
             g, o = g2, o2
     g.process_watermark(end_wm)
     o.process_watermark(end_wm)
-    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final", minmax=mm, vmax=vmax)
+    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final", **chk)
     late = g.late_dropped
     if kstats is not None:
         kstats.update(g.op.kernel_stats())
@@ -244,6 +248,49 @@ def test_min_max_snapshot_restore(oracle_mod, kind):
         cfg = dict(cfg_of(kind, 4000, 0 if kind == "tumble" else 1000, vt="i64"), aggs=aggs)
         drive_both(oracle_mod, cfg, n=120_000, keys=2000, batch=6_000, delay=100, jitter=500, snapshot_at=7,
                    null_frac=0.1)
+
+
+ALL_AGGS = ("count_star", "count", "sum", "avg", "sum0", "min", "max")
+# several value accumulators in one handle (value slots: SUM family, MIN, MAX): one staging
+# pass feeds all of them, the row holds every aggregate as the reference's generated
+# NamespaceAggsHandleFunction does (AggsHandlerCodeGenerator.scala:578-700)
+MV_BASE = [c for c in STREAM_CASES if c[0] in (
+    "tumble_f64_inorder", "tumble_i64_ooo", "tumble_i64_wrap", "tumble_f64_nulls_late", "hop_f64", "hop_i64_late",
+    "cumulate_f64", "cumulate_i64_late", "regions_f64_nulls_late", "regions_i64_ooo_lanes", "regions_hop_f64",
+    "regions_cumulate_i64_late", "big_units_i64_nulls_ooo", "proctime_hop_f64", "zipf_tumble_f64",
+    "zipf_tumble_i64_nulls_late", "zipf_hop_f64", "signed_tumble_f64", "dst_cumulate_spring_f64")]
+MV_CASES = [(f"mv_{name}", dict(cfg, aggs=ALL_AGGS), kw) for name, cfg, kw in MV_BASE] + [
+    ("mv_avg_min_i64_ooo", dict(cfg_of("tumble", 1000, vt="i64"), aggs=("count_star", "avg", "min")),
+     dict(n=200_000, keys=3000, batch=7_000, delay=300, jitter=900, null_frac=0.1)),
+    ("mv_max_sum_hop_regions", dict(cfg_of("hop", 3000, 1000), aggs=("max", "count_star", "sum")),
+     dict(n=600_000, keys=100_000, batch=40_000, delay=200, jitter=800, null_frac=0.1))]
+
+
+@pytest.mark.parametrize("name,cfg,kw", MV_CASES, ids=[c[0] for c in MV_CASES])
+def test_multi_accumulator_parity(oracle_mod, name, cfg, kw):
+    ks = {} if kw.get("zipf") else None
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    if ks is not None:
+        assert ks.get("merge_heavy", {}).get("launches", 0) > 0, ks
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_multi_accumulator_snapshot_restore(oracle_mod, kind):
+    """The state image carries the MIN / MAX slots (fg_state_rows.min / max); late records
+    after the restore re-fire old windows through the marked merges with every slot."""
+    for vt in ("i64", "f64"):
+        cfg = dict(cfg_of(kind, 4000, 0 if kind == "tumble" else 1000, vt=vt), aggs=ALL_AGGS)
+        drive_both(oracle_mod, cfg, n=400_000, keys=100_000, batch=20_000, delay=100, jitter=1500, snapshot_at=9,
+                   null_frac=0.1)
+
+
+def test_multi_accumulator_grows(oracle_mod):
+    """Far more keys than expected_keys: regions split with every value slot."""
+    cfg = dict(cfg_of("hop", 3000, 1000, vt="i64"), aggs=ALL_AGGS)
+    st = {}
+    drive_both(oracle_mod, cfg, n=600_000, keys=200_000, batch=60_000, delay=100, jitter=300, expected_keys=1000,
+               stats=st, null_frac=0.05)
+    assert st["state_regions"] >= 8, st
 
 
 @pytest.mark.parametrize("name,cfg,kw", STREAM_CASES, ids=[c[0] for c in STREAM_CASES])
@@ -666,8 +713,8 @@ def test_composite_sum_min_max(oracle_mod, kind, vt, device_output):
     cfg = cfg_of(kind, 4000, 0 if kind == "tumble" else 1000, vt=vt)
     key, ts, val, isnull = make_stream(150_000, 3000, vt, jitter_ms=900, null_frac=0.1)
     aggs = ("count_star", "count", "sum", "avg", "min", "max")
-    op = F.window_agg_operator(window_of(cfg), aggs=aggs, val_type=vt, expected_keys=3000)
-    assert isinstance(op, F.CompositeWindowAggOperator) and len(op.ops) == 3
+    op = F.CompositeWindowAggOperator(window_of(cfg), aggs=aggs, val_type=vt, expected_keys=3000)
+    assert len(op.ops) == 3
     o = oracle_mk(oracle_mod, cfg)
     sfx = "_i" if vt == "i64" else "_d"
 
