@@ -18,7 +18,7 @@ TUMBLE, HOP, CUMULATE = 0, 1, 2
 VAL_NONE, VAL_I64, VAL_F64 = 0, 1, 2
 AGG_COUNT_STAR, AGG_COUNT, AGG_SUM, AGG_AVG, AGG_SUM0, AGG_MIN, AGG_MAX = 0, 1, 2, 3, 4, 5, 6
 HOST, DEVICE = 0, 1
-KEYHASH_BINARYROW_BIGINT, KEYHASH_JAVA_LONG = 0, 1
+KEYHASH_BINARYROW_BIGINT, KEYHASH_JAVA_LONG, KEYHASH_DICT_ID = 0, 1, 2
 MAX_AGGS = 8
 
 
@@ -95,7 +95,8 @@ EXPORTS = (
     "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
-    "fg_abi_version",
+    "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
+    "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_last_error", "fg_key_dict_close", "fg_binaryrow_hash",
 )
 
 _lib = None
@@ -154,6 +155,22 @@ def load():
     L.fg_partition_columns_by_owner.argtypes = [C.c_int32, P, C.c_int64, C.c_int32, P, C.c_int32, C.c_int32,
                                                 C.c_int32, P, P]
     L.fg_abi_version.restype = C.c_int
+    L.fg_key_dict_open.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.POINTER(P)]
+    L.fg_key_dict_intern.argtypes = [P, C.c_int32, C.c_int64, P, C.c_int64, P, P, P, P]
+    L.fg_key_dict_lookup.argtypes = [P, C.c_int32, C.c_int64, P, P, P]
+    L.fg_key_dict_arena.argtypes = [P, C.POINTER(P), C.POINTER(C.c_int64)]
+    L.fg_key_dict_copy_arena.argtypes = [P, C.c_int64, C.c_int64, P]
+    L.fg_key_dict_size.argtypes = [P]
+    L.fg_key_dict_size.restype = C.c_int64
+    L.fg_key_dict_last_error.argtypes = [P]
+    L.fg_key_dict_last_error.restype = C.c_char_p
+    L.fg_key_dict_close.argtypes = [P]
+    L.fg_key_dict_close.restype = None
+    L.fg_binaryrow_hash.argtypes = [P, C.c_int32]
+    L.fg_binaryrow_hash.restype = C.c_int32
+    for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
+               "fg_key_dict_copy_arena"):
+        getattr(L, fn).restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
                "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):

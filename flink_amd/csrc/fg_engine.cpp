@@ -272,6 +272,7 @@ struct fg_handle {
     DevBuf part_tmp, part_tmp_null, part_dir;   // two-pass partition: pass-1 tiles + directory
     // skewed-region plan and chunk partial tables
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
+    DevBuf hv_mv1, hv_mv2;   // multi-value operator: value slots 1 and 2 of the chunks' partial rows
     int64_t hv_max_chunks = 0;
     DevBuf hist, totals, scan_tmp, counters;
     DevBuf plan_dev;          // k_scan_plan's lane plan (speculative pass 2)
@@ -812,6 +813,11 @@ int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, Heav
         HIPCHK(h, h->hv_sum.ensure(8 * e));
         h->hv_max_chunks = max_chunks;
     }
+    if (h->mv) {
+        const size_t e = (size_t)h->hv_max_chunks * kPartStride;
+        HIPCHK(h, h->hv_mv1.ensure(8 * e));
+        HIPCHK(h, h->hv_mv2.ensure(8 * e));
+    }
     HIPCHK(h, h->hv_flags.ensure((size_t)h->P));
     HIPCHK(h, h->hv_list.ensure(4 * (size_t)h->P));
     HIPCHK(h, h->hv_chunk0.ensure(4 * ((size_t)h->P + 1)));
@@ -834,6 +840,10 @@ int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, Heav
     hp->part_cs = h->hv_cs.as<int64_t>();
     hp->part_cn = h->hv_cn.as<int64_t>();
     hp->part_sum = h->hv_sum.as<int64_t>();
+    hp->part_v1 = h->mv ? h->hv_mv1.as<int64_t>() : nullptr;
+    hp->part_v2 = h->mv ? h->hv_mv2.as<int64_t>() : nullptr;
+    hp->mv = h->mv ? 1 : 0;
+    for (int k = 0; k < kNV; k++) hp->vop[k] = h->vop[k];
     hp->part_n = h->hv_pn.as<uint32_t>();
     hp->overflow = h->scalars.as<unsigned int>();
     KTimer kt(h, K_HEAVY, 0);
@@ -974,7 +984,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             skew = skew || s->skew;
             same_bits = same_bits && s->bits == h->region_bits;
         }
-        skew = skew && same_bits && !h->mv;   // (a multi-value operator takes no heavy pass)
+        skew = skew && same_bits;
         HeavyPlan hp{};
         if (skew) {
             rc = plan_heavy(h, p.batches, p.n_batches, ln.fill + ln.acc_fill, &hp);
@@ -1002,6 +1012,8 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             q.part_cs = hp.part_cs;
             q.part_cn = hp.part_cn;
             q.part_sum = hp.part_sum;
+            q.part_v1 = hp.part_v1;
+            q.part_v2 = hp.part_v2;
             q.part_n = hp.part_n;
             HIPCHK(h, launch_merge(q, merge_grid(h), h->stream));
         }

@@ -186,6 +186,8 @@ struct MergeParams {
     const int64_t* part_cs;
     const int64_t* part_cn;
     const int64_t* part_sum;
+    const int64_t* part_v1;    // multi-value operator: value slots 1 and 2 of the partial rows
+    const int64_t* part_v2;
     const uint32_t* part_n;    // entries per chunk (kChunkFailed: the chunk's table overflowed)
     // Region overflow (LDS table full, or more than kRegionCap entries for a table write): the
     // region emits and writes nothing, and (job << kFailJobShift | region) is appended to
@@ -242,8 +244,13 @@ struct HeavyPlan {
     int64_t* part_cs;
     int64_t* part_cn;
     int64_t* part_sum;
+    int64_t* part_v1;          // multi-value operator: value slots 1 and 2
+    int64_t* part_v2;
     uint32_t* part_n;          // [max_chunks]
     unsigned int* overflow;
+    // multi-value operator: val_type is the value type, slot k folds with op vop[k] (as MergeParams)
+    int32_t mv;
+    int32_t vop[kNV];
 };
 
 // Accumulator rows of the global phase: input columns and the SoA staged area (all lanes)

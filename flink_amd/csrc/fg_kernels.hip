@@ -1490,9 +1490,9 @@ __device__ __forceinline__ void lds_val(unsigned long long* a, int64_t bits, int
 // Accumulate {COUNT(*), NULL count, values} into a slot. vt: the kernel value op for a
 // single-value table; for a multi-value table the value type (0: a NULL record, no value),
 // slot k taking op p.vop[k]. vals: one value per slot (a record's value repeated).
-template <bool C, bool MV>
+template <bool C, bool MV, class PV>   // PV: MergeParams or HeavyPlan (vop)
 __device__ __forceinline__ void lds_add(LdsTableT<C, MV>& t, int slot, unsigned long long cs, unsigned long long cn,
-                                        const int64_t* vals, int vt, const MergeParams& p) {
+                                        const int64_t* vals, int vt, const PV& p) {
     if constexpr (C) {
         atomicAdd(&t.cs[slot], (uint32_t)cs);
     } else {
@@ -1848,9 +1848,15 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     const int64_t at = (int64_t)c * kPartStride;
                     for (uint32_t i = tid; i < n; i += T) {
                         const int slot = lds_find_or_insert<C, MV>(t, gbl(p.part_key)[at + i], full);
-                        if (slot >= 0)   // (a multi-value operator takes no heavy pass)
-                            lds_add1<C, MV>(t, slot, (unsigned long long)gbl(p.part_cs)[at + i],
-                                            (unsigned long long)gbl(p.part_cn)[at + i], gbl(p.part_sum)[at + i], vt, p);
+                        if (slot < 0) continue;
+                        int64_t vv[NVS];
+                        vv[0] = gbl(p.part_sum)[at + i];
+                        if constexpr (MV) {
+                            vv[1] = gbl(p.part_v1)[at + i];
+                            vv[2] = gbl(p.part_v2)[at + i];
+                        }
+                        lds_add<C, MV>(t, slot, (unsigned long long)gbl(p.part_cs)[at + i],
+                                       (unsigned long long)gbl(p.part_cn)[at + i], vv, vt, p);
                     }
                 }
             }
@@ -2040,8 +2046,7 @@ hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_
 }
 
 hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s) {
-    if (p.mv) {   // multi-value operator (no heavy pass)
-        if (p.heavy || p.region_list) return hipErrorInvalidValue;
+    if (p.mv) {   // multi-value operator
         if (p.compact) {
             if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
             hipLaunchKernelGGL((k_merge<true, -1, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p);
@@ -2125,24 +2130,35 @@ __global__ __launch_bounds__(kPlanThreads) void k_heavy_plan(HeavyPlan hp) {
 
 // Persistent over the chunks: each chunk's records (its slice of the region's records,
 // batches in order) are combined in a wide LDS table and the table is written out as the
-// chunk's partial rows {key, COUNT(*), NULL count, sum}. Equal keys within a wave (the hot
-// key of a Zipf region fills most lanes) are reduced with cross-lane adds first, so the
-// LDS atomics of a hot slot drop from one per record to one per wave.
+// chunk's partial rows {key, COUNT(*), NULL count, value slots}. Equal keys within a wave (the
+// hot key of a Zipf region fills most lanes) are reduced with cross-lane adds (min / max) first,
+// so the LDS atomics of a hot slot drop from one per record to one per wave. MV: a multi-value
+// operator's table (kNV value slots, slot k folding with op vop[k]).
+template <bool MV>
 __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
     constexpr int T = kMergeThreads;
-    __shared__ LdsTableT<false, false> t;   // (single-value operators only)
+    constexpr int S = MergeCfg<false, MV>::kSlotsT;
+    constexpr int NVS = MV ? kNV : 1;
+    __shared__ LdsTableT<false, MV> t;
     __shared__ uint32_t s_n;
     __shared__ unsigned int s_full;
     const int tid = threadIdx.x, lane = tid & 63;
-    const int vt = hp.val_type;
-    const int64_t vinit = val_identity(vt);
+    const int vt = hp.val_type;   // MV: the value type; else the kernel value op
+    int vops[NVS];                // the op of each slot (kernel value op form)
+    int64_t vinit[NVS];
+#pragma unroll
+    for (int k = 0; k < NVS; k++) {
+        vops[k] = MV ? (hp.vop[k] < 3 ? (vt & 3) | (hp.vop[k] << kOpShift) : 0) : vt;
+        vinit[k] = val_identity(vops[k]);
+    }
     const int nch = *gbl(hp.n_list + 1);
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
-        for (int i = tid; i <= kSlots; i += T) {
+        for (int i = tid; i <= S; i += T) {
             t.key[i] = JMIN;
             t.cs[i] = 0;
             t.cn[i] = 0;
-            t.v[0][i] = (unsigned long long)vinit;
+#pragma unroll
+            for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)vinit[k];
         }
         if (tid == 0) {
             s_n = 0;
@@ -2164,59 +2180,69 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
                 const int64_t x = xb + tid;
                 const bool valid = x < hi;
                 const int64_t i = beg + (x - acc);
-                int64_t k = JMIN, sum = 0;
+                int64_t k = JMIN;
+                int64_t vals[NVS];
+#pragma unroll
+                for (int q = 0; q < NVS; q++) vals[q] = 0;
                 unsigned long long cs = 1, cn = 0;
                 if (valid) {
                     if (sb.is_acc) {
                         k = gbl(sb.rec)[i];
                         cs = (unsigned long long)gbl(sb.cnt_star)[i];
                         cn = (unsigned long long)gbl(sb.cnt_null)[i];
-                        sum = gbl(sb.val)[i];
+                        vals[0] = gbl(sb.val)[i];
+                        if constexpr (MV) {
+                            vals[1] = gbl(sb.val1)[i];
+                            vals[2] = gbl(sb.val2)[i];
+                        }
                     } else if (sb.stride == 2) {
                         const RecV2 rc = ((GlobalRec)sb.rec)[i];
                         k = rc.x;
-                        sum = rc.y;
+#pragma unroll
+                        for (int q = 0; q < NVS; q++) vals[q] = rc.y;
                     } else {
                         k = gbl(sb.rec)[i];
                     }
                     if (!sb.is_acc && sb.vnull != nullptr && gbl(sb.vnull)[i] != 0) {
                         cn = 1;
-                        sum = 0;
+#pragma unroll
+                        for (int q = 0; q < NVS; q++) vals[q] = 0;
                     }
                 }
-                if (!sb.is_acc && sb.stride != 2) sum = 0;
+                // a record without a value column or a NULL record adds no value
+                const bool novalue = !sb.is_acc && (sb.stride != 2 || cn == 1);
                 // wave pre-reduction of the records equal to the first lane's key (no NULLs)
                 bool done = !valid;
                 const int64_t k0 = __builtin_amdgcn_readfirstlane(k);
                 const uint64_t m = __ballot(valid && cn == 0 && k == k0 && !sb.is_acc);
                 if (__popcll(m) > 1) {
                     const bool in = (m >> lane) & 1;
-                    int64_t part = in ? sum : 0;
-                    if (vt == 2) {
-                        double d = in ? __longlong_as_double(sum) : 0.0;
-                        for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
-                        part = __double_as_longlong(d);
-                    } else if (vt == 1) {
-                        for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-                    } else if (vt > 3) {   // MIN / MAX: lanes outside the run hold the identity
-                        part = in ? sum : vinit;
-                        for (int off = 32; off > 0; off >>= 1) part = val_combine(part, __shfl_xor(part, off), vt);
+                    int64_t part[NVS];
+#pragma unroll
+                    for (int q = 0; q < NVS; q++) {
+                        const int op = vops[q];
+                        part[q] = in && sb.stride == 2 ? vals[q] : vinit[q];
+                        if (op == 2) {
+                            double d = __longlong_as_double(part[q]);
+                            for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);
+                            part[q] = __double_as_longlong(d);
+                        } else if (op != 0) {
+                            for (int off = 32; off > 0; off >>= 1) part[q] = val_combine(part[q], __shfl_xor(part[q], off), op);
+                        }
                     }
                     if (in) {
                         done = true;
                         if (lane == __ffsll((long long)m) - 1) {
-                            const int slot = lds_find_or_insert<false, false>(t, k0, full);
-                            if (slot >= 0) lds_val(&t.v[0][slot], part, vt, true), atomicAdd(&t.cs[slot], (unsigned long long)__popcll(m));
+                            const int slot = lds_find_or_insert<false, MV>(t, k0, full);
+                            if (slot >= 0)
+                                lds_add<false, MV>(t, slot, (unsigned long long)__popcll(m), 0ull, part,
+                                                   sb.stride == 2 ? vt : 0, hp);
                         }
                     }
                 }
                 if (!done) {
-                    const int slot = lds_find_or_insert<false, false>(t, k, full);
-                    if (slot >= 0) {
-                        atomicAdd(&t.cs[slot], cs);
-                        if (cn) atomicAdd(&t.cn[slot], cn);
-                        lds_val(&t.v[0][slot], sum, cn == 1 && !sb.is_acc ? 0 : vt, cn < cs);
-                    }
+                    const int slot = lds_find_or_insert<false, MV>(t, k, full);
+                    if (slot >= 0) lds_add<false, MV>(t, slot, cs, cn, vals, novalue ? 0 : vt, hp);
                 }
             }
             acc += len;
@@ -2224,13 +2250,17 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
         if (full) atomicOr(&s_full, 1u);
         lds_barrier();
         const int64_t at = (int64_t)c * kPartStride;
-        for (int i = tid; i <= kSlots; i += T) {
+        for (int i = tid; i <= S; i += T) {
             if (t.cs[i] == 0) continue;
             const uint32_t o = atomicAdd(&s_n, 1u);
-            hp.part_key[at + o] = i == kSlots ? JMIN : t.key[i];
+            hp.part_key[at + o] = i == S ? JMIN : t.key[i];
             hp.part_cs[at + o] = (int64_t)t.cs[i];
             hp.part_cn[at + o] = (int64_t)t.cn[i];
             hp.part_sum[at + o] = (int64_t)t.v[0][i];
+            if constexpr (MV) {
+                hp.part_v1[at + o] = (int64_t)t.v[1][i];
+                hp.part_v2[at + o] = (int64_t)t.v[2][i];
+            }
         }
         lds_barrier();
         if (tid == 0) {
@@ -2249,7 +2279,8 @@ hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s) {
 }
 
 hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s) {
-    hipLaunchKernelGGL(k_heavy_chunks, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
+    if (hp.mv) hipLaunchKernelGGL(k_heavy_chunks<true>, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
+    else hipLaunchKernelGGL(k_heavy_chunks<false>, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
     return hipGetLastError();
 }
 

@@ -281,6 +281,7 @@ __host__ __device__ __forceinline__ int32_t murmur_hash(int32_t code) {
     return 0;
 }
 __host__ __device__ __forceinline__ int32_t key_group_of(int64_t key, int32_t key_hash, int32_t max_p) {
+    if (key_hash == 2) return (int32_t)((uint64_t)key >> 40) % max_p;   // an fg_key_dict id carries it
     int32_t h = key_hash == 0 ? binaryrow_hash_i64(key) : java_long_hash(key);
     return murmur_hash(h) % max_p;
 }

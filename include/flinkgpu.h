@@ -34,6 +34,9 @@
  *   KeyGroupRangeAssignment.assignToKeyGroup  RT/state/KeyGroupRangeAssignment.java:63-77
  *     + KeyGroupStreamPartitioner.selectChannel SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:55-65
  *                                                                        fg_key_groups
+ *   BinaryRowDataKeySelector.getKey (any key type: STRING, several columns)
+ *     TR/keyselector/BinaryRowDataKeySelector.java:43-50, key identity BinarySection.equals /
+ *     hashCode TC/data/binary/BinarySection.java:62-78                   fg_key_dict_intern
  *
  * Conventions
  *  - Return 0 (FG_OK) on success, a positive FG_E* code otherwise; fg_last_error()
@@ -57,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 5
+#define FG_ABI_VERSION 6
 
 enum fg_status {
     FG_OK = 0,
@@ -93,7 +96,9 @@ enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AV
  * two partition passes run back to back on the GPU); fg_synchronize releases them. FG_HOST
  * buffers are copied before the call returns. */
 enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
-enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1 };
+/* FG_KEYHASH_DICT_ID: the key is an id of an fg_key_dict (any key type); its key group, computed
+ * from the key row's bytes when it was interned, is carried in the id (id >> 40). */
+enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1, FG_KEYHASH_DICT_ID = 2 };
 enum fg_flags {
     FG_FLAG_KERNEL_TIMING = 1,    /* HIP-event timing of every launch (fg_kernel_stats) */
     /* Local phase of the two-phase window aggregation (LocalSlicingWindowAggOperator +
@@ -298,6 +303,38 @@ int  fg_partition_by_owner(int32_t device_id, void* stream, int64_t n, const int
 int  fg_partition_columns_by_owner(int32_t device_id, void* stream, int64_t n, int32_t ncols,
                                    const int64_t* const* cols, int32_t key_hash, int32_t max_parallelism,
                                    int32_t parallelism, int64_t* const* out_cols, int64_t* counts);
+
+/* Grouping keys of any type (STRING, several key columns ...): a GPU-resident dictionary of the
+ * serialized key rows. The reference groups by the BinaryRowData key row the key selector
+ * projects (BinaryRowDataKeySelector.java:43-50); two keys are equal iff their rows' bytes are
+ * (BinarySection.equals, BinarySection.java:62-73), and the key group comes from
+ * MurmurHashUtils.hashBytesByWords over those bytes, seed 42 (BinarySection.hashCode :76-78,
+ * MurmurHashUtils.java:92-96,131-170) -> KeyGroupRangeAssignment. fg_key_dict_intern maps each row
+ * to a 64-bit id: equal rows -> equal ids, distinct rows -> distinct ids (exact: a hash collision
+ * is resolved by comparing the bytes), id = key group << 40 | ordinal. The ids are the BIGINT key
+ * column of fg_add_batch / the key field of fg_add_rows; FG_KEYHASH_DICT_ID routes them by the
+ * carried key group; fired rows' ids map back to their rows with fg_key_dict_lookup. A handle is
+ * single-threaded like fg_handle; ids are stable for the dictionary's life (a restored operator
+ * re-interns the key rows of its state image first). */
+typedef struct fg_key_dict fg_key_dict;
+int  fg_key_dict_open(int32_t device_id, int32_t max_parallelism, int64_t expected_keys, fg_key_dict** out);
+/* n key rows: row i = bytes[offsets[i], offsets[i] + lengths[i]) (nbytes = the buffer's size),
+ * each length and offset a multiple of 4 (BinaryRowData rows are multiples of 8). out_id[n]
+ * receives the ids, out_kg[n] (optional) the rows' key groups under the dictionary's max
+ * parallelism. All pointers FG_HOST or all FG_DEVICE (location). */
+int  fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_t* bytes, int64_t nbytes,
+                        const int64_t* offsets, const int32_t* lengths, int64_t* out_id, int32_t* out_kg);
+/* For each id: its row's offset and length in the dictionary's arena (-1 / -1 for an unknown id). */
+int  fg_key_dict_lookup(fg_key_dict* d, int32_t location, int64_t n, const int64_t* ids, int64_t* out_offsets,
+                        int32_t* out_lengths);
+/* The arena (device memory, rows padded to 8 bytes) and its used size; valid until the next intern. */
+int  fg_key_dict_arena(fg_key_dict* d, const uint8_t** dev_bytes, int64_t* size);
+int  fg_key_dict_copy_arena(fg_key_dict* d, int64_t begin, int64_t nbytes, uint8_t* host);
+int64_t fg_key_dict_size(fg_key_dict* d);   /* distinct key rows interned */
+const char* fg_key_dict_last_error(fg_key_dict* d);
+void fg_key_dict_close(fg_key_dict* d);
+/* BinarySection.hashCode of one row (MurmurHashUtils.hashBytesByWords, seed 42); len % 4 == 0. */
+int32_t fg_binaryrow_hash(const uint8_t* row, int32_t len);
 
 int  fg_abi_version(void);
 

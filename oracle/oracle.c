@@ -914,6 +914,19 @@ int32_t or_binaryrow_hash_i64(int64_t key) {
     h1 = mix_h1(h1, mix_k1((int32_t)(uint32_t)((uint64_t)key >> 32)));
     return fmix32(h1 ^ 16);
 }
+/* BinarySection.hashCode of any row (TC/data/binary/BinarySection.java:76-78 ->
+ * BinarySegmentUtils.hash -> MurmurHashUtils.hashBytesByWords, MurmurHashUtils.java:92-96,
+ * 131-141): the row's little-endian 4-byte words (MemorySegment.getInt, native order), seed 42,
+ * fmix(h1 ^ length); len % 4 == 0 (BinaryRowData sizes are multiples of 8) */
+int32_t or_binaryrow_hash_bytes(const uint8_t* row, int32_t len) {
+    int32_t h1 = 42;
+    for (int32_t i = 0; i < len; i += 4) {
+        const uint32_t w = (uint32_t)row[i] | (uint32_t)row[i + 1] << 8 | (uint32_t)row[i + 2] << 16 |
+                           (uint32_t)row[i + 3] << 24;
+        h1 = mix_h1(h1, mix_k1((int32_t)w));
+    }
+    return fmix32(h1 ^ len);
+}
 int32_t or_long_hash(int64_t key) { return (int32_t)(uint32_t)((uint64_t)key ^ ((uint64_t)key >> 32)); }
 /* MathUtils.murmurHash  CO/util/MathUtils.java:137-155 */
 int32_t or_murmur_hash(int32_t code) {

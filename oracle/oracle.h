@@ -118,7 +118,8 @@ int64_t or_next_trigger_watermark(int64_t wm, int64_t interval);
 int64_t or_window_start_with_offset(int64_t ts, int64_t offset, int64_t size);
 
 /* --- key groups (KeyGroupRangeAssignment / MathUtils / MurmurHashUtils) ------- */
-int32_t or_binaryrow_hash_i64(int64_t key);          /* BinaryRowData(BIGINT).hashCode() */
+int32_t or_binaryrow_hash_i64(int64_t key);
+int32_t or_binaryrow_hash_bytes(const uint8_t* row, int32_t len);          /* BinaryRowData(BIGINT).hashCode() */
 int32_t or_long_hash(int64_t key);                    /* java.lang.Long.hashCode() */
 int32_t or_murmur_hash(int32_t code);                 /* MathUtils.murmurHash */
 int32_t or_key_group(int32_t key_hash, int32_t max_parallelism);

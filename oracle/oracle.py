@@ -129,6 +129,8 @@ def lib():
         for fn in ("or_binaryrow_hash_i64", "or_long_hash"):
             getattr(L, fn).restype = C.c_int32
             getattr(L, fn).argtypes = [C.c_int64]
+        L.or_binaryrow_hash_bytes.restype = C.c_int32
+        L.or_binaryrow_hash_bytes.argtypes = [P, C.c_int32]
         L.or_murmur_hash.restype = C.c_int32
         L.or_murmur_hash.argtypes = [C.c_int32]
         L.or_key_group.restype = C.c_int32
@@ -301,6 +303,17 @@ def next_trigger_watermark(wm, interval):
 
 def binaryrow_hash_i64(key: int) -> int:
     return lib().or_binaryrow_hash_i64(key)
+
+
+def binaryrow_hash_bytes(row: bytes) -> int:
+    """BinarySection.hashCode of a serialized row (any key type)."""
+    buf = (C.c_uint8 * max(len(row), 1)).from_buffer_copy(row or b"\0")
+    return lib().or_binaryrow_hash_bytes(buf, len(row))
+
+
+def key_group_of_row(row: bytes, max_parallelism: int) -> int:
+    """KeyGroupRangeAssignment.assignToKeyGroup(keyRow, maxP) for a BinaryRowData key row."""
+    return key_group(binaryrow_hash_bytes(row), max_parallelism)
 
 
 def long_hash(key: int) -> int:

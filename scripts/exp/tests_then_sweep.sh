@@ -1,0 +1,9 @@
+# All GPU tests (no -x: every failure listed), then -- unless the test run crashed or timed
+# out -- the micro-batch sweep.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+tail -15 gpurun_out/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests ended with $rc: stopping"; exit $rc; fi
+bash scripts/exp/batch_sweep.sh

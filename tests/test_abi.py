@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "flinkgpu.h")
 
 def declared_symbols():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void\*?|const char\*|void)\s+\*?(fg_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int32_t|int64_t|void\*?|const char\*|void)\s+\*?(fg_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_expected_api():
@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 5
+    assert lib.fg_abi_version() == 6
 
 
 def test_struct_layouts_match_header_sizes():

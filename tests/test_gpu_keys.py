@@ -1,0 +1,211 @@
+"""GPU tests of the key dictionary (fg_key_dict_*): grouping keys of any type (STRING, several
+key columns, NULL keys) interned as BinaryRowData key rows, with exact ids, Flink key groups
+(BinarySection.hashCode -> KeyGroupRangeAssignment), and the reference's own operator tests run
+with their literal STRING keys through the dictionary + the window engine."""
+
+import numpy as np
+import pytest
+
+import flink_amd as F
+from flink_amd import keys as K
+from oracle import oracle as O
+from tests.fixture_runner import load_operator_cases, run_case
+
+pytestmark = pytest.mark.gpu
+
+MAXP = 128
+TYPES = ["string", "bigint"]
+
+
+def random_keys(rng, n_distinct):
+    out = set()
+    while len(out) < n_distinct:
+        n = int(rng.integers(0, 41))
+        s = "".join(chr(c) for c in rng.integers(0x20, 0x7f, n))
+        out.add((s if rng.random() > 0.02 else None, int(rng.integers(-5, 5))))
+    return sorted(out, key=lambda t: (t[0] is None, t[0] or "", t[1]))
+
+
+def check_interned(d, rows, ids, kgs):
+    ids = np.asarray(ids)
+    first = {}
+    for r, i in zip(rows, ids.tolist()):
+        assert first.setdefault(r, i) == i, "equal key rows got different ids"
+    assert len(set(first.values())) == len(first), "distinct key rows share an id"
+    exp_kg = np.array([O.key_group_of_row(r, MAXP) for r in rows], dtype=np.int32)
+    assert np.array_equal(np.asarray(kgs), exp_kg)
+    assert np.array_equal(K.key_group_of_id(ids, MAXP), exp_kg)
+    assert d.lookup(ids) == list(rows)
+    return first
+
+
+def test_intern_exact_ids_key_groups_and_lookup():
+    rng = np.random.default_rng(3)
+    keys = random_keys(rng, 40_000)
+    rows_all = [K.key_row(list(k), TYPES) for k in keys]
+    d = F.KeyDictionary(max_parallelism=MAXP, expected_keys=1000)   # grows several times
+    seen = {}
+    for b in range(5):
+        pick = rng.integers(0, len(rows_all), 60_000)
+        rows = [rows_all[i] for i in pick]
+        ids, kgs = d.intern(rows)
+        m = check_interned(d, rows, ids, kgs)
+        for r, i in m.items():
+            assert seen.setdefault(r, i) == i, "an id changed across calls"
+    assert len(d) == len(seen)
+    # device input: the same rows as torch tensors on the GPU get the same ids
+    import torch
+    rows = [rows_all[i] for i in rng.integers(0, len(rows_all), 30_000)]
+    buf, off, ln = K.pack_key_rows(rows)
+    dev = torch.device("cuda", 0)
+    ids_t, kg_t = d.intern(packed=(torch.from_numpy(buf.copy()).to(dev), torch.from_numpy(off).to(dev),
+                                   torch.from_numpy(ln).to(dev)))
+    ids = ids_t.cpu().numpy()
+    for r, i in zip(rows, ids.tolist()):
+        if r in seen:
+            assert seen[r] == i
+    check_interned(d, rows, ids, kg_t.cpu().numpy())
+    d.close()
+
+
+def test_intern_forced_hash_collisions_stay_exact(monkeypatch):
+    """A 6-bit table tag (diagnostic knob): nearly every distinct row collides with another's
+    tag; the byte comparison sends them to the host map and the ids stay exact."""
+    monkeypatch.setenv("FG_DICT_TAG_BITS", "6")
+    rng = np.random.default_rng(11)
+    keys = random_keys(rng, 3000)
+    rows_all = [K.key_row(list(k), TYPES) for k in keys]
+    d = F.KeyDictionary(max_parallelism=MAXP, expected_keys=16)
+    seen = {}
+    for _ in range(3):
+        rows = [rows_all[i] for i in rng.integers(0, len(rows_all), 8000)]
+        ids, kgs = d.intern(rows)
+        for r, i in check_interned(d, rows, ids, kgs).items():
+            assert seen.setdefault(r, i) == i
+    assert len(d) == len(seen)
+    d.close()
+
+
+def test_intern_rejects_bad_rows_and_keeps_working():
+    d = F.KeyDictionary(max_parallelism=MAXP)
+    buf = np.zeros(64, dtype=np.uint8)
+    with pytest.raises(F.WindowSpecError):
+        d.intern(packed=(buf, np.array([0, 8], dtype=np.int64), np.array([16, 6], dtype=np.int32)))
+    with pytest.raises(F.WindowSpecError):
+        d.intern(packed=(buf, np.array([56], dtype=np.int64), np.array([16], dtype=np.int32)))
+    import torch
+    dev = torch.device("cuda", 0)
+    with pytest.raises(F.WindowSpecError):
+        d.intern(packed=(torch.zeros(64, dtype=torch.uint8, device=dev), torch.tensor([4, 60], device=dev),
+                         torch.tensor([16, 8], dtype=torch.int32, device=dev)))
+    rows = [K.key_row(["k%d" % i], ["string"]) for i in range(100)]
+    ids, kgs = d.intern(rows)
+    check_interned(d, rows, ids, kgs)
+    assert len(d) == 100
+    d.close()
+
+
+# the reference's operator tests with their literal STRING keys (the fixtures number them)
+SLICING_NAMES = {1: "key1", 2: "key2"}
+ITCASE_NAMES = {1: "a", 2: "b", 3: None}   # TestData.windowDataWithTimestamp: a NULL name
+STRING_CASES = [c for c in load_operator_cases() if c["config"]["mode"] == "sql"]
+
+
+def names_of(case):
+    if case["name"].startswith("itcase"):
+        return ITCASE_NAMES
+    if "dst" in case["name"]:
+        return {1: "a"}
+    return SLICING_NAMES
+
+
+class StringKeyOperator:
+    """GpuOperator whose keys enter as BinaryRowData STRING key rows interned by the dictionary
+    (the shim's path for non-BIGINT keys) and leave as the rows' strings (back to the fixture's
+    numbering for the comparison)."""
+
+    def __init__(self, inner, d, names):
+        self.inner, self.d, self.names = inner, d, names
+        self.back = {v: k for k, v in names.items()}
+
+    def process_batch(self, key, ts, val=None, isnull=None):
+        rows = [K.key_row([self.names[int(k)]], ["string"]) for k in key]
+        ids, _ = self.d.intern(rows)
+        self.inner.process_batch(ids, ts, val, isnull)
+
+    def process_watermark(self, wm):
+        self.inner.process_watermark(wm)
+
+    def prepare_snapshot(self):
+        self.inner.prepare_snapshot()
+
+    def restore_copy(self):
+        return StringKeyOperator(self.inner.restore_copy(), self.d, self.names)
+
+    @property
+    def late_dropped(self):
+        return self.inner.late_dropped
+
+    def take_rows(self):
+        r = self.inner.take_rows()
+        if len(r):
+            rows = self.d.lookup(r["key"])
+            r["key"] = [self.back[K.decode_key_row(x, ["string"])[0]] for x in rows]
+        return r
+
+    def close(self):
+        self.inner.close()
+
+
+@pytest.mark.parametrize("case", STRING_CASES, ids=[c["name"] for c in STRING_CASES])
+def test_golden_cases_with_string_keys(case):
+    from tests.test_gpu_parity import gpu_mk
+    d = F.KeyDictionary(max_parallelism=MAXP)
+    results, late = run_case(case, lambda cfg: StringKeyOperator(gpu_mk(cfg), d, names_of(case)))
+    for step, got, exp in results:
+        assert got == exp, f"{case['name']} step {step}: got {got} expected {exp}"
+    if case["expected_late_dropped"] is not None:
+        assert late == case["expected_late_dropped"]
+    d.close()
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop"])
+def test_string_keys_stream_vs_oracle(oracle_mod, kind):
+    """A randomized out-of-order stream over 20k (STRING, BIGINT) keys: the GPU path (dictionary
+    ids -> engine) against the oracle run on the same keys numbered by position."""
+    from tests.test_gpu_parity import assert_rows_equal, cfg_of, gpu_mk, oracle_mk
+    rng = np.random.default_rng(5)
+    keys = random_keys(rng, 20_000)
+    rows_all = [K.key_row(list(k), TYPES) for k in keys]
+    index = {r: i for i, r in enumerate(rows_all)}
+    n = 300_000
+    pick = rng.integers(0, len(rows_all), n)
+    ts = (1_000_000 + np.arange(n) // 100 + rng.integers(0, 300, n)).astype(np.int64)
+    val = rng.random(n) * 1000.0
+    cfg = cfg_of(kind, 3000 if kind == "hop" else 1000, 1000 if kind == "hop" else 0)
+    d = F.KeyDictionary(max_parallelism=MAXP, expected_keys=len(rows_all))
+    g = gpu_mk(cfg, expected_keys=len(rows_all))
+    o = oracle_mk(oracle_mod, cfg)
+
+    def check(ctx):
+        r = g.take_rows()
+        if len(r):
+            r["key"] = [index[x] for x in d.lookup(r["key"])]
+        assert_rows_equal(r, o.take_rows(), "f64", ctx)
+
+    for lo in range(0, n, 50_000):
+        hi = lo + 50_000
+        ids, _ = d.intern([rows_all[i] for i in pick[lo:hi]])
+        g.process_batch(ids, ts[lo:hi], val[lo:hi])
+        o.process_batch(pick[lo:hi].astype(np.int64), ts[lo:hi], val[lo:hi])
+        wm = int(ts[hi - 1]) - 400
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        check(f"wm {wm}")
+    assert g.late_dropped == o.late_dropped
+    g.process_watermark((1 << 63) - 1)
+    o.process_watermark((1 << 63) - 1)
+    check("final")
+    g.close()
+    o.close()
+    d.close()
