@@ -993,7 +993,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         }
         {
             KTimer kt(h, fire_now || cum_fire ? K_FLUSH_FIRE : K_FLUSH, ln.fill);
-            HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
+            HIPCHK(h, launch_merge(p, p.compact && !h->mv ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
         }
         if (skew) {
             // the heavy regions: chunk tables, then their merge with the region's state

@@ -29,6 +29,30 @@ namespace fg {
 
 typedef long long RecV2 __attribute__((ext_vector_type(2)));
 typedef const RecV2 __attribute__((address_space(1)))* GlobalRec;
+
+// Non-temporal (streaming) forms of the record streams, by FG_NT bit (experiment knob):
+// 1 pass-1 input loads, 2 pass-1 tile stores, 4 pass-2 tile loads, 8 pass-2 staged stores,
+// 16 merge staged loads
+#ifndef FG_NT
+#define FG_NT 0
+#endif
+template <int BIT>
+__device__ __forceinline__ longlong2 ld2(const void* q) {
+    const RecV2* r = static_cast<const RecV2*>(q);
+    RecV2 v;
+    if constexpr ((FG_NT & BIT) != 0) v = __builtin_nontemporal_load(r);
+    else v = *r;
+    return make_longlong2(v.x, v.y);
+}
+template <int BIT>
+__device__ __forceinline__ void st2(void* q, longlong2 a) {
+    RecV2 v;
+    v.x = a.x;
+    v.y = a.y;
+    RecV2* r = static_cast<RecV2*>(q);
+    if constexpr ((FG_NT & BIT) != 0) __builtin_nontemporal_store(v, r);
+    else *r = v;
+}
 // a pointer that was itself loaded from memory is generic (flat) to the compiler: view it in
 // the global address space so its loads are global_load (see `load` below)
 template <class T>
@@ -501,9 +525,9 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
 #pragma unroll
             for (int u = 0; u < R / 2; u++) {
                 const int64_t i = t0 + li_of(2 * u);
-                k2[u] = *reinterpret_cast<const longlong2*>(p.key + i);
-                t2[u] = *reinterpret_cast<const longlong2*>(p.ts + i);
-                v2[u] = has_val ? *reinterpret_cast<const longlong2*>(p.val + i) : make_longlong2(0, 0);
+                k2[u] = ld2<1>(p.key + i);
+                t2[u] = ld2<1>(p.ts + i);
+                v2[u] = has_val ? ld2<1>(p.val + i) : make_longlong2(0, 0);
             }
         } else {
 #pragma unroll
@@ -583,7 +607,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
         }
         lds_barrier();
         for (uint32_t i = tid; i < tile_total; i += T) {
-            p.tmp[t0 + i] = s_rec[i];
+            st2<2>(&p.tmp[t0 + i], s_rec[i]);
             if (has_null) p.tmp_null[t0 + i] = s_nul[i];
         }
         lds_barrier();   // staging and the directory row have read the offsets
@@ -785,7 +809,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
                 rr[u] = make_longlong2((long long)src * 0x9E3779B97F4A7C15ll, src);
                 continue;
             }
-            rr[u] = p.tmp[src];
+            rr[u] = ld2<4>(&p.tmp[src]);
             if (has_null && p.tmp_null[src] != 0) rn |= 1u << u;
         }
     };
@@ -843,7 +867,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
                 if (wv[u].x == 0x5555 && wv[u].y == 0x7777) p.st_rec[0] = pos;   // keep the reads alive
                 continue;
             }
-            if constexpr (AOS) *reinterpret_cast<longlong2*>(live ? p.st_rec + 2 * pos : p.sink) = wv[u];
+            if constexpr (AOS) st2<8>(live ? p.st_rec + 2 * pos : p.sink, wv[u]);
             else *(live ? p.st_rec + pos : p.sink) = wv[u].x;
         }
         if (has_null) {
@@ -1285,9 +1309,9 @@ struct MergeCfg<false, true> {   // multi-value: one 1,024-thread workgroup per 
     static constexpr int kU = FG_WIDE_U;
 };
 template <>
-struct MergeCfg<true, true> {    // multi-value compact: 108 KiB, one workgroup per CU
+struct MergeCfg<true, true> {    // multi-value compact: 108 KiB, one 1,024-thread workgroup per CU
     static constexpr int kSlotsT = kCompactSlotsMV;
-    static constexpr int kThreads = kCompactMergeThreads;
+    static constexpr int kThreads = kMergeThreads;
     static constexpr int kU = FG_MERGE_U;
 };
 
@@ -1457,16 +1481,23 @@ __device__ __forceinline__ int64_t val_combine(int64_t a, int64_t b, int vt) {
         default: return 0;
     }
 }
-// DOUBLE MIN/MAX in LDS: compare-and-swap while the operand still wins (Java `<` / `>`)
+// DOUBLE MIN/MAX in LDS: an LDS slot of a DOUBLE MIN / MAX holds the value's bits mapped to an
+// order-preserving int64 (f64_ord: non-negative doubles as they are, negative ones with the
+// magnitude bits flipped; an involution), so one ds_min_i64 / ds_max_i64 replaces a
+// compare-and-swap loop. The operand replaces the accumulator iff operand < min (> max) as
+// Java's primitive comparison, except that a NaN operand never wins (Java keeps a NaN that
+// arrived first) and -0.0 < +0.0 (Java keeps whichever zero came first): DESIGN.md section 3.
+__device__ __forceinline__ int64_t f64_ord(int64_t b) { return b >= 0 ? b : b ^ 0x7FFFFFFFFFFFFFFFll; }
+__device__ __forceinline__ bool is_f64_minmax(int op) {
+    return op == (2 | (1 << kOpShift)) || op == (2 | (2 << kOpShift));
+}
+// the LDS form of a value slot's bits (and back: f64_ord is its own inverse)
+__device__ __forceinline__ int64_t lds_repr(int op, int64_t b) { return is_f64_minmax(op) ? f64_ord(b) : b; }
 template <bool kMin>
 __device__ __forceinline__ void lds_minmax_f64(unsigned long long* a, int64_t bits) {
-    const double v = __longlong_as_double(bits);
-    unsigned long long cur = *a;
-    while (kMin ? v < __longlong_as_double((int64_t)cur) : v > __longlong_as_double((int64_t)cur)) {
-        const unsigned long long old = atomicCAS(a, cur, (unsigned long long)bits);
-        if (old == cur) break;
-        cur = old;
-    }
+    if ((bits & 0x7FFFFFFFFFFFFFFFll) > 0x7FF0000000000000ll) return;   // NaN: never wins
+    if (kMin) atomicMin(reinterpret_cast<long long*>(a), (long long)f64_ord(bits));
+    else atomicMax(reinterpret_cast<long long*>(a), (long long)f64_ord(bits));
 }
 
 // one value slot: `bits` into *a with the kernel value op vtk (val_type | op << 2; 0: none).
@@ -1556,8 +1587,13 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     constexpr int NVS = MV ? kNV : 1;                    // value slots
     const int vt = VTC >= 0 ? VTC : p.val_type;          // (MV: the value type; slot k has op p.vop[k])
     int64_t vinit[NVS];
+    int vops[NVS];   // the op of each value slot (kernel value op form)
 #pragma unroll
-    for (int k = 0; k < NVS; k++) vinit[k] = MV ? val_identity((vt & 3) | (p.vop[k] << kOpShift)) : val_identity(vt);
+    for (int k = 0; k < NVS; k++) {
+        // MV with VTC >= 0: the slots' ops compiled in as SUM, MIN, MAX (launch_merge)
+        vops[k] = MV ? (VTC >= 0 ? (VTC | (k << kOpShift)) : p.vop[k] < 3 ? (vt & 3) | (p.vop[k] << kOpShift) : 0) : vt;
+        vinit[k] = val_identity(vops[k]);
+    }
     const int P = 1 << p.region_bits;
     const int G = gridDim.x;
     // regions: all P (strided over the grid), the heavy pass's list, or a retry's list
@@ -1607,7 +1643,9 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             const uint32_t i = m.i0 + u * T + tid;
-            const RecV2 v = rec[i < m.end ? i : m.end - 1];
+            RecV2 v;
+            if constexpr ((FG_NT & 16) != 0) v = __builtin_nontemporal_load(&rec[i < m.end ? i : m.end - 1]);
+            else v = rec[i < m.end ? i : m.end - 1];
             c[u] = make_longlong2(v.x, v.y);
         }
     };
@@ -1654,7 +1692,16 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 const uint32_t nx = home[u] + kBucket;
                 slot = lds_find_or_insert_from<C, MV>(t, k, nx >= S_ ? 0u : nx, full);
             }
-            if (!(FG_DIAG_MERGE & 1) && slot >= 0) lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
+            if constexpr (MV && VTC >= 0) {   // SUM, MIN, MAX slots, straight-line
+                if (slot >= 0) {
+                    if constexpr (C) atomicAdd(&t.cs[slot], 1u);
+                    else atomicAdd(&t.cs[slot], 1ull);
+#pragma unroll
+                    for (int k = 0; k < NVS; k++) lds_val(&t.v[k][slot], c[u].y, vops[k], true);
+                }
+            } else if (!(FG_DIAG_MERGE & 1) && slot >= 0) {
+                lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
+            }
             if ((FG_DIAG_MERGE & 1) && slot >= 0) t.cs[slot] = 1;
         }
     };
@@ -1713,7 +1760,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             t.cs[i] = 0;
             if constexpr (!C) t.cn[i] = 0;
 #pragma unroll
-            for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)vinit[k];
+            for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)lds_repr(vops[k], vinit[k]);
         }
         if (tid == 0) s_flags = 0;
         if constexpr (!C) if (tid < 64) {   // source tables: per-region entry counts -> flat prefix
@@ -1987,7 +2034,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             if constexpr (!C) cn = t.cn[slot] & ~kMarkBit;
             int64_t vv[NVS];
 #pragma unroll
-            for (int q = 0; q < NVS; q++) vv[q] = (int64_t)t.v[q][slot];
+            for (int q = 0; q < NVS; q++) vv[q] = lds_repr(vops[q], (int64_t)t.v[q][slot]);
             if (write_dst) {
                 const bool chain = !C && p.dst_mode != 0;   // a chain table holds keys with zero accumulators
                 dbase[at] = key;
@@ -2049,7 +2096,12 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
     if (p.mv) {   // multi-value operator
         if (p.compact) {
             if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
-            hipLaunchKernelGGL((k_merge<true, -1, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p);
+            // the common list (SUM family, MIN and MAX) over BIGINT / DOUBLE: ops compiled in
+            const bool all3 = p.vop[0] == 0 && p.vop[1] == 1 && p.vop[2] == 2;
+            constexpr int MT = MergeCfg<true, true>::kThreads;
+            if (all3 && p.val_type == 2) hipLaunchKernelGGL((k_merge<true, 2, true>), dim3(workgroups), dim3(MT), 0, s, p);
+            else if (all3 && p.val_type == 1) hipLaunchKernelGGL((k_merge<true, 1, true>), dim3(workgroups), dim3(MT), 0, s, p);
+            else hipLaunchKernelGGL((k_merge<true, -1, true>), dim3(workgroups), dim3(MT), 0, s, p);
         } else {
             hipLaunchKernelGGL((k_merge<false, -1, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
         }
@@ -2158,7 +2210,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
             t.cs[i] = 0;
             t.cn[i] = 0;
 #pragma unroll
-            for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)vinit[k];
+            for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)lds_repr(vops[k], vinit[k]);
         }
         if (tid == 0) {
             s_n = 0;
@@ -2256,10 +2308,10 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
             hp.part_key[at + o] = i == S ? JMIN : t.key[i];
             hp.part_cs[at + o] = (int64_t)t.cs[i];
             hp.part_cn[at + o] = (int64_t)t.cn[i];
-            hp.part_sum[at + o] = (int64_t)t.v[0][i];
+            hp.part_sum[at + o] = lds_repr(vops[0], (int64_t)t.v[0][i]);
             if constexpr (MV) {
-                hp.part_v1[at + o] = (int64_t)t.v[1][i];
-                hp.part_v2[at + o] = (int64_t)t.v[2][i];
+                hp.part_v1[at + o] = lds_repr(vops[1], (int64_t)t.v[1][i]);
+                hp.part_v2[at + o] = lds_repr(vops[2], (int64_t)t.v[2][i]);
             }
         }
         lds_barrier();
