@@ -1449,7 +1449,13 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
     p.out_null[o] = nm;
 }
 
-constexpr int kSrcU = 2;          // source-table entries per thread per round (wide merge)
+#ifndef FG_DENSE_EMIT
+#define FG_DENSE_EMIT 1
+#endif
+#ifndef FG_SRC_U
+#define FG_SRC_U 2
+#endif
+constexpr int kSrcU = FG_SRC_U;   // source-table entries per thread per round (wide merge)
 constexpr unsigned long long kMarkBit = 1ull << 63;   // wide table: entry touched by a marking source (NULL-count word)
 constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
 
@@ -1573,6 +1579,9 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     constexpr uint32_t kChunk = kMergeU * T;
     __shared__ LdsTableT<C, MV> t;
     __shared__ uint32_t s_grp[kRounds * kWaves];   // per (round, wave) row counts -> offsets
+#if FG_DENSE_EMIT
+    __shared__ uint16_t s_map[S + 1];              // rank -> slot of the region's emitted entries
+#endif
     __shared__ unsigned int s_flags;
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
@@ -2021,14 +2030,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 7u);
         int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * cols * cap : nullptr;
         const unsigned long long obase = s_out_base;
-        // per round: the wave's occupied lanes below this lane give the rank within the group
-#pragma unroll
-        for (int k = 0; k < kRounds; k++) {
-            const bool occ = (occ_mask >> k) & 1;
-            const uint64_t bal = __ballot(occ);
-            if (!occ) continue;
-            const int slot = k < kRounds - 1 ? k * T + tid : S;
-            const uint32_t at = s_grp[k * kWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        // one entry out: its table write-back and / or its fired row, at rank `at`
+        auto emit_one = [&](int slot, uint32_t at) {
             const int64_t key = slot == S ? JMIN : t.key[slot];
             unsigned long long cs = t.cs[slot], cn = 0;
             if constexpr (!C) cn = t.cn[slot] & ~kMarkBit;
@@ -2044,7 +2047,35 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 for (int q = 0; q < NVS; q++) dbase[(3 + q) * cap + at] = chain ? vinit[q] : vv[q];
             }
             if (write_out) write_row(p, obase + at, key, cs, cn, vv, vt);
+        };
+        // per round: the wave's occupied lanes below this lane give the rank within the group
+#if FG_DENSE_EMIT
+        // the ranks are gathered into a rank -> slot map first, then every lane writes one
+        // entry at consecutive ranks (full-width stores instead of the ~1/3 of a wave that a
+        // round's occupied lanes fill)
+#pragma unroll
+        for (int k = 0; k < kRounds; k++) {
+            const bool occ = (occ_mask >> k) & 1;
+            const uint64_t bal = __ballot(occ);
+            if (!occ) continue;
+            const int slot = k < kRounds - 1 ? k * T + tid : S;
+            s_map[s_grp[k * kWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] = (uint16_t)slot;
         }
+        lds_barrier();
+        if (write_dst || write_out) {
+            const uint32_t total = s_total;
+            for (uint32_t i = tid; i < total; i += T) emit_one(s_map[i], i);
+        }
+#else
+#pragma unroll
+        for (int k = 0; k < kRounds; k++) {
+            const bool occ = (occ_mask >> k) & 1;
+            const uint64_t bal = __ballot(occ);
+            if (!occ) continue;
+            const int slot = k < kRounds - 1 ? k * T + tid : S;
+            emit_one(slot, s_grp[k * kWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1)));
+        }
+#endif
         if (tid == 0 && write_dst) {
             const uint32_t total = s_total;
             const uint32_t old = p.dst.counts[r];

@@ -209,3 +209,30 @@ def test_string_keys_stream_vs_oracle(oracle_mod, kind):
     g.close()
     o.close()
     d.close()
+
+
+def test_dictionary_ids_route_by_the_rows_key_group():
+    """FG_KEYHASH_DICT_ID: owner partitioning of partial rows keyed by dictionary ids sends
+    each row to the subtask of its key row's Flink key group (kg * P / maxP)."""
+    import torch
+
+    from flink_amd import _lib as L
+    from flink_amd.exchange import partition_columns_by_owner
+    rng = np.random.default_rng(9)
+    keys = random_keys(rng, 5000)
+    rows_all = [K.key_row(list(k), TYPES) for k in keys]
+    d = F.KeyDictionary(max_parallelism=MAXP)
+    pick = rng.integers(0, len(rows_all), 50_000)
+    ids, kgs = d.intern([rows_all[i] for i in pick])
+    assert np.array_equal(F.key_groups(ids, MAXP, key_hash=L.KEYHASH_DICT_ID), kgs)
+    par = 8
+    dev = torch.device("cuda", 0)
+    cols = [torch.from_numpy(ids).to(dev), torch.arange(len(ids), dtype=torch.int64, device=dev)]
+    outs, counts = partition_columns_by_owner(cols, par, MAXP, key_hash=L.KEYHASH_DICT_ID)
+    owner = kgs.astype(np.int64) * par // MAXP
+    assert np.array_equal(counts.cpu().numpy(), np.bincount(owner, minlength=par))
+    pos = outs[1].cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(counts.cpu().numpy())])
+    for r in range(par):
+        assert (owner[pos[off[r]:off[r + 1]]] == r).all()
+    d.close()
