@@ -98,6 +98,7 @@ struct SliceTable {
     DevBuf counts;        // P uint32
     int64_t upper = 0;    // host-side upper bound of entries
     int bits = 0;         // region bits of its layout
+    bool has_null = false;   // some entry may count NULL values (else its cnt_null column is all 0)
 };
 
 // One ingest pass: the bucket scan of its records over all lanes; lane l's records sit at
@@ -458,6 +459,7 @@ int table_new(fg_handle* h, int64_t slice_end, std::unique_ptr<SliceTable>* out)
     t->slice_end = slice_end;
     t->upper = 0;
     t->bits = h->region_bits;
+    t->has_null = false;
     return FG_OK;
 }
 
@@ -582,7 +584,21 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     std::vector<StagedBatch> sb;
     for (const JobBatch& jb : j.batches) sb.push_back(batch_of(h, jb));
     std::vector<TableRef> srcs;
-    for (SliceTable* t : j.srcs) srcs.push_back(ref_of(t));
+    // sources known free of NULL counts are read without their cnt_null column; a destination
+    // may hold NULL counts iff something merged into it may
+    unsigned long long null_mask = 0;
+    bool dst_null = false;
+    for (size_t i = 0; i < j.srcs.size(); i++) {
+        srcs.push_back(ref_of(j.srcs[i]));
+        if (j.srcs[i]->has_null) {
+            if (i < 64) null_mask |= 1ull << i;
+            dst_null = true;
+        }
+    }
+    if (j.srcs.size() > 64) null_mask = ~0ull;
+    for (const JobBatch& jb : j.batches)
+        dst_null = dst_null || !jb.s || jb.s->has_null || jb.s->is_acc;   // (restore images, partials)
+    if (j.dst) j.dst->has_null = j.dst->has_null || dst_null;
     *p = MergeParams{};
     p->region_bits = h->region_bits;
     p->n_src = (int)srcs.size();
@@ -609,6 +625,7 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     p->markonly_mask = j.markonly_mask;
     p->emit_marked = j.emit_marked;
     p->dst_mode = j.dst_mode;
+    p->src_null_mask = null_mask;
     return FG_OK;
 }
 

@@ -204,6 +204,7 @@ struct MergeParams {
     // 1 writes the marked entries holding state, 2 every marked entry, both as keys with zero
     // accumulators (a chain table of the keys whose timers chain on)
     int32_t emit_marked;
+    unsigned long long src_null_mask;   // source j (< 64) may hold NULL counts (else its cnt_null column is 0)
     unsigned long long mark_mask;
     unsigned long long markonly_mask;   // sources that only mark (their accumulators are not added)
     int32_t dst_mode;

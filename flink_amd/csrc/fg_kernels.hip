@@ -1824,7 +1824,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     const auto base = gbl(s_sbase[j]);
                     k[u] = base[i];
                     cs[u] = base[cap + i];
-                    cn[u] = base[2 * cap + i];
+                    cn[u] = ((p.src_null_mask >> j) & 1ull) ? base[2 * cap + i] : 0;
 #pragma unroll
                     for (int q = 0; q < NVS; q++) sm[u][q] = base[(3 + q) * cap + i];
                     mk[u] = ((p.mark_mask >> j) & 1ull) != 0;

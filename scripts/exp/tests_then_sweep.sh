@@ -6,4 +6,4 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 rc=$?
 tail -15 gpurun_out/gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests ended with $rc: stopping"; exit $rc; fi
-bash scripts/exp/batch_sweep.sh
+bash scripts/exp/wl_variants.sh base
