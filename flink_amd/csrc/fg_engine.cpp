@@ -1141,8 +1141,29 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
         MergeParams p{};
         rc = job_params(h, ji, &p);
         if (rc) return rc;
-        KTimer kt(h, K_FIRE, 0);
-        HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+#ifdef FG_STAMPS
+        static DevBuf d_fst;
+        if (getenv("FG_STAMPS")) {
+            HIPCHK(h, d_fst.ensure(64));
+            HIPCHK(h, hipMemsetAsync(d_fst.p, 0, 64, h->stream));
+            p.stamps = d_fst.as<unsigned long long>();
+        }
+#endif
+        {
+            KTimer kt(h, K_FIRE, 0);
+            HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+        }
+#ifdef FG_STAMPS
+        if (p.stamps) {
+            unsigned long long st[4];
+            HIPCHK(h, hipMemcpyAsync(st, d_fst.p, 32, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            const int waves = merge_grid(h) * kMergeThreads / 64;
+            fprintf(stderr, "[fg stamps] fire srcs=%zu dst=%d: clear %.0f stream %.0f compact %.0f emit %.0f (cycles/wave)\n",
+                    srcs.size(), dst ? 1 : 0, (double)st[0] / waves, (double)st[1] / waves, (double)st[2] / waves,
+                    (double)st[3] / waves);
+        }
+#endif
     }
     if (dst) dst->upper = ub;
     if (defer) {

@@ -15,6 +15,6 @@ i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc$i -o run -- \
-      python3 $R/bench.py --records $REC --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+      python3 $R/bench.py --records $REC --steps 1 --warmup 0 --no-cpu-baseline --h2d-records 0 > $OUT/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
 echo profile-done

@@ -294,6 +294,41 @@ def datastream_fixtures():
                     val_type="i64", count_star_index=-1),
         columns=["key", "sum", "out_ts"],
         events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
+    # testSideOutputDueToLatenessTumbling :1975-2053 (2 s tumbling, allowedLateness 0,
+    # EventTimeTrigger): the element at 1998 arrives after WM 1999 fired its window -> late (the
+    # reference side-outputs it; here it is counted in numLateRecordsDropped)
+    ev, steps = [], []
+    ev.append(E(2, 1, 1000)); ev.append(WM(1985)); steps.append((len(ev) - 1, []))
+    ev.append(E(2, 1, 1980)); ev.append(WM(1999)); steps.append((len(ev) - 1, [[2, 2, 1999]]))
+    ev.append(E(2, 1, 1998)); ev.append(E(2, 1, 2001))
+    ev.append(WM(2999)); steps.append((len(ev) - 1, []))
+    ev.append(WM(3999)); steps.append((len(ev) - 1, [[2, 1, 3999]]))
+    out.append(dict(
+        name="ds_tumble_2s_lateness0_side_output",
+        source="SJT/runtime/operators/windowing/WindowOperatorTest.java:1975-2053",
+        config=dict(mode="datastream", kind="tumble", size=2000, slide=0, offset=0, tz_offset_ms=0,
+                    val_type="i64", count_star_index=-1),
+        columns=["key", "sum", "out_ts"],
+        events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=1))
+    # testSideOutputDueToLatenessSliding :2055-2151 (3 s / 1 s sliding, allowedLateness 0): the
+    # elements at 2400 are late for the window ending 2999 only and stay in 3999 / 4999; the last
+    # 3001 is late for all three of its windows -> late
+    ev, steps = [], []
+    ev.append(E(2, 1, 1000)); ev.append(WM(1999)); steps.append((len(ev) - 1, [[2, 1, 1999]]))
+    ev.append(E(2, 1, 2000)); ev.append(WM(3000)); steps.append((len(ev) - 1, [[2, 2, 2999]]))
+    for e in (E(1, 1, 3001), E(2, 1, 2400), E(2, 1, 2400), E(1, 1, 3001), E(2, 1, 3900)):
+        ev.append(e)
+    ev.append(WM(6000)); steps.append((len(ev) - 1, [[2, 5, 3999], [1, 2, 3999], [2, 4, 4999], [1, 2, 4999],
+                                                     [2, 1, 5999], [1, 2, 5999]]))
+    ev.append(E(1, 1, 3001))
+    ev.append(WM(25000)); steps.append((len(ev) - 1, []))
+    out.append(dict(
+        name="ds_sliding_3s_1s_lateness0_side_output",
+        source="SJT/runtime/operators/windowing/WindowOperatorTest.java:2055-2151",
+        config=dict(mode="datastream", kind="hop", size=3000, slide=1000, offset=0, tz_offset_ms=0,
+                    val_type="i64", count_star_index=-1),
+        columns=["key", "sum", "out_ts"],
+        events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=1))
     return out
 
 
