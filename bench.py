@@ -423,7 +423,8 @@ def main():
     def partials_round(wm):
         """local fire -> exchange of partial accumulators -> global merge + fire"""
         r = op_local.process_watermark(wm, device_output=True)
-        cols = device_columns(r, device=dev)
+        # key, slice end, COUNT(*), COUNT(v), SUM (+ MIN, MAX for several value accumulators)
+        cols = device_columns(r, aggs=tuple(range(len(op_local.aggs))), device=dev)
         recv, sent = exchange_partials(cols, max_parallelism=maxp, via_cpu=via_cpu)
         torch.cuda.current_stream().synchronize()
         op.process_partials(*recv)

@@ -69,7 +69,7 @@ class FgPartials(C.Structure):
     _fields_ = [
         ("n", C.c_int64), ("location", C.c_int32), ("reserved0", C.c_int32),
         ("key", C.c_void_p), ("slice_end", C.c_void_p), ("cnt_star", C.c_void_p), ("cnt_val", C.c_void_p),
-        ("sum", C.c_void_p),
+        ("sum", C.c_void_p), ("min", C.c_void_p), ("max", C.c_void_p),
     ]
 
 

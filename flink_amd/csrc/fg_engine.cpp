@@ -248,7 +248,8 @@ struct fg_handle {
     // accumulator areas (global phase, fg_add_partials): SoA, acc_cap rows per lane
     int64_t acc_cap = 0;
     DevBuf acc_key, acc_cs, acc_cn, acc_sum;
-    DevBuf in_cs, in_cv, in_sum, in_slice;
+    DevBuf acc_v1, acc_v2;   // multi-value operator: the partial rows' MIN / MAX
+    DevBuf in_cs, in_cv, in_sum, in_slice, in_v1, in_v2;
     bool local = false;     // FG_FLAG_LOCAL_PARTIALS: fired slices emit partial accumulators
     bool proctime = false;  // FG_FLAG_PROCTIME: processing-time windows, nothing is late
     std::vector<int64_t> tz_trans, tz_offs;   // zone rules (host copy); tz_dev: the HBM copy
@@ -558,6 +559,10 @@ StagedBatch batch_of(const fg_handle* h, const JobBatch& jb) {
         b.cnt_star = h->acc_cs.as<int64_t>() + at;
         b.cnt_null = h->acc_cn.as<int64_t>() + at;
         b.val = h->acc_sum.as<int64_t>() + at;
+        if (h->mv) {
+            b.val1 = h->acc_v1.as<int64_t>() + at;
+            b.val2 = h->acc_v2.as<int64_t>() + at;
+        }
     } else {
         b.rec = h->st_rec.as<int64_t>() + ((int64_t)l * h->lane_cap + s->lane_start[l]) * h->st_stride;
         b.vnull = s->has_null ? h->st_null.as<uint8_t>() + (int64_t)l * h->lane_cap + s->lane_start[l] : nullptr;
@@ -1941,6 +1946,10 @@ int grow_acc(fg_handle* h, int64_t need) {
     HIPCHK(h, h->acc_cs.ensure(b));
     HIPCHK(h, h->acc_cn.ensure(b));
     HIPCHK(h, h->acc_sum.ensure(b));
+    if (h->mv) {
+        HIPCHK(h, h->acc_v1.ensure(b));
+        HIPCHK(h, h->acc_v2.ensure(b));
+    }
     h->acc_cap = cap;
     return FG_OK;
 }
@@ -1950,7 +1959,8 @@ int grow_acc(fg_handle* h, int64_t need) {
 // the rows are scattered into their slice lanes' accumulator areas. Returns -1 when the
 // rows span more slices than the lanes can hold.
 int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* cs, const int64_t* cv,
-             const int64_t* sum, int64_t flo, int64_t fhi, bool count_drops, Counters* out) {
+             const int64_t* sum, const int64_t* v1, const int64_t* v2, int64_t flo, int64_t fhi, bool count_drops,
+             Counters* out) {
     if (int rc0 = ensure_scratch(h)) return rc0;
     IngestParams p{};
     p.w = h->w;
@@ -2056,6 +2066,12 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     a.cnt_star = h->acc_cs.as<int64_t>();
     a.cnt_null = h->acc_cn.as<int64_t>();
     a.sum = h->acc_sum.as<int64_t>();
+    if (h->mv) {
+        a.in_v1 = v1;
+        a.in_v2 = v2;
+        a.v1 = h->acc_v1.as<int64_t>();
+        a.v2 = h->acc_v2.as<int64_t>();
+    }
     {
         KTimer kt(h, K_SCATTER, n);
         HIPCHK(h, launch_acc_scatter(p, a, h->stream));
@@ -2244,17 +2260,18 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             has_max |= c.aggs[a] == FG_AGG_MAX;
             sum_family |= c.aggs[a] == FG_AGG_SUM || c.aggs[a] == FG_AGG_AVG || c.aggs[a] == FG_AGG_SUM0;
         }
-        if ((int)sum_family + (int)has_min + (int)has_max > 1) {
-            g_open_error = std::string("FG_FLAG_LOCAL_PARTIALS: the partial row holds one value accumulator, but the "
-                                       "aggregate list names ") +
-                           (sum_family ? "SUM/AVG/SUM0 " : "") + (has_min ? "MIN " : "") + (has_max ? "MAX " : "") +
-                           "(open one local operator per accumulator kind)";
-            return FG_EINVAL;
-        }
         c.num_aggs = 3;
         c.aggs[0] = FG_AGG_COUNT_STAR;
         c.aggs[1] = FG_AGG_COUNT;
         c.aggs[2] = vagg;
+        if ((int)sum_family + (int)has_min + (int)has_max > 1) {
+            // several value accumulators: the partial row carries SUM, MIN and MAX
+            // (agg[2..4]; a kind absent from the list travels as its identity)
+            c.num_aggs = 5;
+            c.aggs[2] = FG_AGG_SUM;
+            c.aggs[3] = FG_AGG_MIN;
+            c.aggs[4] = FG_AGG_MAX;
+        }
     }
     const bool proctime = (c.flags & FG_FLAG_PROCTIME) != 0;
     if (proctime && (c.mode != FG_MODE_SQL || local)) {
@@ -2313,7 +2330,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             has_min |= c.aggs[a] == FG_AGG_MIN;
             has_max |= c.aggs[a] == FG_AGG_MAX;
         }
-        if ((int)sum_family + (int)has_min + (int)has_max > 1 && !local) {
+        if ((int)sum_family + (int)has_min + (int)has_max > 1) {
             // the reference's generated accumulator row holds every aggregate's accumulator
             // (AggsHandlerCodeGenerator.scala:578-700): one operator, one staging, value slots
             // 0 SUM (SUM / AVG / SUM0), 1 MIN, 2 MAX
@@ -2621,21 +2638,22 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     if (!h || !b) return FG_EINVAL;
     if (b->n <= 0) return FG_OK;
     if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
-    if (h->mv)
-        return h->fail(FG_EINVAL, "partial rows carry one value accumulator: a global operator takes one value "
-                                  "accumulator kind (SUM family, MIN or MAX)");
     if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 rows");
     if (!b->key || !b->slice_end || !b->cnt_star || !b->cnt_val || !b->sum)
         return h->fail(FG_EINVAL, "partials need key, slice_end, cnt_star, cnt_val and sum columns");
+    if (h->mv && (!b->min || !b->max))
+        return h->fail(FG_EINVAL, "a global operator with several value accumulators (SUM family, MIN, MAX) needs "
+                                  "the partial rows' min and max columns");
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc0 = settle_pending(h)) return rc0;
     maybe_reduce_lanes(h);
     const int64_t n = b->n;
     const int64_t *key = b->key, *se = b->slice_end, *cs = b->cnt_star, *cv = b->cnt_val, *sum = b->sum;
+    const int64_t *v1 = h->mv ? b->min : nullptr, *v2 = h->mv ? b->max : nullptr;
     if (b->location == FG_HOST) {
-        DevBuf* bufs[5] = {&h->in_key, &h->in_slice, &h->in_cs, &h->in_cv, &h->in_sum};
-        const int64_t* src[5] = {key, se, cs, cv, sum};
-        for (int i = 0; i < 5; i++) {
+        DevBuf* bufs[7] = {&h->in_key, &h->in_slice, &h->in_cs, &h->in_cv, &h->in_sum, &h->in_v1, &h->in_v2};
+        const int64_t* src[7] = {key, se, cs, cv, sum, v1, v2};
+        for (int i = 0; i < (h->mv ? 7 : 5); i++) {
             HIPCHK(h, bufs[i]->ensure(8 * n));
             HIPCHK(h, hipMemcpyAsync(bufs[i]->p, src[i], 8 * n, hipMemcpyHostToDevice, h->stream));
         }
@@ -2644,6 +2662,10 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
         cs = h->in_cs.as<int64_t>();
         cv = h->in_cv.as<int64_t>();
         sum = h->in_sum.as<int64_t>();
+        if (h->mv) {
+            v1 = h->in_v1.as<int64_t>();
+            v2 = h->in_v2.as<int64_t>();
+        }
     }
     HIPCHK(h, h->in_ts.ensure(8 * n));
     int64_t* ts = h->in_ts.as<int64_t>();
@@ -2654,7 +2676,7 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     int rc0 = seed_anchor(h, ts, nullptr);
     if (rc0) return rc0;
     Counters c{};
-    int rc = acc_pass(h, n, key, ts, cs, cv, sum, JMIN, JMAX, true, &c);
+    int rc = acc_pass(h, n, key, ts, cs, cv, sum, v1, v2, JMIN, JMAX, true, &c);
     h->late_dropped += (int64_t)c.drops;
     if (rc == FG_OK) return FG_OK;
     if (rc != -1) return rc;
@@ -2664,7 +2686,7 @@ int fg_add_partials(fg_handle* h, const fg_partials* b) {
     // filtered passes over the occupied slices only (each pass reports the next one)
     for (int64_t lo = qlo; lo <= qhi;) {
         Counters c2{};
-        rc = acc_pass(h, n, key, ts, cs, cv, sum, lo, lo + h->lanes, false, &c2);
+        rc = acc_pass(h, n, key, ts, cs, cv, sum, v1, v2, lo, lo + h->lanes, false, &c2);
         if (rc == -1) return h->fail(FG_ESTATE, "internal: slice lanes conflict inside a filtered pass");
         if (rc) return rc;
         lo = c2.qnext;

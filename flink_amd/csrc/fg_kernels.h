@@ -263,6 +263,10 @@ struct AccColumns {
     int64_t* cnt_star;
     int64_t* cnt_null;
     int64_t* sum;
+    const int64_t* in_v1;      // multi-value operator: the partial MIN / MAX (else null)
+    const int64_t* in_v2;
+    int64_t* v1;
+    int64_t* v2;
 };
 
 struct ExportParams {

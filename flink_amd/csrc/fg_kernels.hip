@@ -1143,6 +1143,10 @@ __global__ __launch_bounds__(kIngestThreads) void k_acc_scatter(IngestParams p, 
         a.cnt_star[pos] = cs;
         a.cnt_null[pos] = cs - a.in_cnt_val[i];
         a.sum[pos] = a.in_sum[i];
+        if (a.v1) {
+            a.v1[pos] = a.in_v1[i];
+            a.v2[pos] = a.in_v2[i];
+        }
     }
 }
 

@@ -94,7 +94,8 @@ class WindowAggOperator:
         local_partials: the local phase of the two-phase aggregation
         (LocalSlicingWindowAggOperator + LocalAggCombiner): process_watermark returns one
         partial accumulator row per (key, fired slice) with columns count_star, count, sum
-        (min / max for a MIN / MAX query; window_start/window_end = the slice), to be exchanged by key group and merged by a
+        (min / max for a MIN / MAX query; sum, min and max for a list mixing them;
+        window_start/window_end = the slice), to be exchanged by key group and merged by a
         global operator's process_partials."""
         lib = L.load()
         self.window = window
@@ -102,16 +103,16 @@ class WindowAggOperator:
         self.val_type = {"none": L.VAL_NONE, "i64": L.VAL_I64, "f64": L.VAL_F64}[val_type]
         self.local_partials = bool(local_partials)
         if self.local_partials:
-            # the partial accumulator: SUM, or the MIN / MAX of a MIN / MAX query (one kind: the
-            # partial row holds one value accumulator, as the engine checks for the C-ABI)
+            # the partial accumulator: SUM, or the MIN / MAX of a MIN / MAX query; a list mixing
+            # them carries SUM, MIN and MAX (the engine's layout for the C-ABI)
             kinds = {("min" if a in ("min", L.AGG_MIN) else "max" if a in ("max", L.AGG_MAX) else
                       "sum" if a in ("sum", "avg", "sum0", L.AGG_SUM, L.AGG_AVG, L.AGG_SUM0) else None)
                      for a in aggs} - {None}
-            if len(kinds) > 1:
-                raise L.WindowSpecError("FG_FLAG_LOCAL_PARTIALS: the partial row holds one value accumulator, "
-                                        f"but the aggregate list names {sorted(kinds)}")
-            vagg = next((a for a in aggs if a in ("min", "max", L.AGG_MIN, L.AGG_MAX)), "sum")
-            aggs = ("count_star", "count", AGG_NAMES.get(vagg, vagg))
+            if len(kinds) > 1:   # several value accumulators: the partial row carries all three
+                aggs = ("count_star", "count", "sum", "min", "max")
+            else:
+                vagg = next((a for a in aggs if a in ("min", "max", L.AGG_MIN, L.AGG_MAX)), "sum")
+                aggs = ("count_star", "count", AGG_NAMES.get(vagg, vagg))
         self.aggs = tuple(AGGS[a] if isinstance(a, str) else int(a) for a in aggs)
         cfg = L.FgConfig()
         cfg.mode = self.mode
@@ -244,10 +245,14 @@ class WindowAggOperator:
         del keep
 
     # -- global phase ----------------------------------------------------------------------------
-    def process_partials(self, key, slice_end, cnt_star, cnt_val, sum_bits):
+    def process_partials(self, key, slice_end, cnt_star, cnt_val, sum_bits, min_bits=None, max_bits=None):
         """GlobalAggCombiner.combine for partial accumulator rows (after the exchange): numpy
-        arrays or device tensors; `sum_bits` holds i64 sums or the bits of f64 sums."""
+        arrays or device tensors; `sum_bits` holds i64 sums or the bits of f64 sums. An operator
+        with several value accumulators (SUM family, MIN, MAX) also takes the partial MIN / MAX
+        (the local phase's agg[3] / agg[4])."""
         cols = [key, slice_end, cnt_star, cnt_val, sum_bits]
+        if min_bits is not None:
+            cols += [min_bits, max_bits]
         self._after_producers(cols)
         ptrs = [_dev_ptr(c) for c in cols]
         b = L.FgPartials()
@@ -257,7 +262,9 @@ class WindowAggOperator:
             b.location = L.DEVICE
             x = ptrs[0][2]
             b.n = int(x.numel() if hasattr(x, "numel") else x.shape[0])
-            b.key, b.slice_end, b.cnt_star, b.cnt_val, b.sum = (p[0] for p in ptrs)
+            b.key, b.slice_end, b.cnt_star, b.cnt_val, b.sum = (p[0] for p in ptrs[:5])
+            if len(ptrs) > 5:
+                b.min, b.max = ptrs[5][0], ptrs[6][0]
         else:
             arrs = []
             for c in cols:
@@ -267,7 +274,9 @@ class WindowAggOperator:
                 arrs.append(np.ascontiguousarray(a, dtype=np.int64))
             b.location = L.HOST
             b.n = len(arrs[0])
-            b.key, b.slice_end, b.cnt_star, b.cnt_val, b.sum = (a.ctypes.data for a in arrs)
+            b.key, b.slice_end, b.cnt_star, b.cnt_val, b.sum = (a.ctypes.data for a in arrs[:5])
+            if len(arrs) > 5:
+                b.min, b.max = arrs[5].ctypes.data, arrs[6].ctypes.data
             keep = arrs
         L.check(self._lib.fg_add_partials(self._h, C.byref(b)), self._h)
         del keep

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 6
+#define FG_ABI_VERSION 7
 
 enum fg_status {
     FG_OK = 0,
@@ -85,8 +85,8 @@ enum fg_val_type { FG_VAL_NONE = 0, FG_VAL_I64 = 1, FG_VAL_F64 = 2 };
  * Java primitive comparison; NULL when the window holds no non-null value. An aggregate list
  * may mix SUM / AVG / SUM0, MIN and MAX over the value column: the operator then keeps all three
  * value accumulators per (key, slice), as the reference's generated accumulator row does
- * (AggsHandlerCodeGenerator.scala:578-700), staging each record once. The two-phase operators
- * (FG_FLAG_LOCAL_PARTIALS / fg_add_partials) carry one value accumulator per partial row. */
+ * (AggsHandlerCodeGenerator.scala:578-700), staging each record once; the two-phase operators'
+ * partial rows then carry the three value accumulators too (FG_FLAG_LOCAL_PARTIALS, fg_partials). */
 enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AVG = 3, FG_AGG_SUM0 = 4,
               FG_AGG_MIN = 5, FG_AGG_MAX = 6 };
 /* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
@@ -108,7 +108,9 @@ enum fg_flags {
      * partial accumulator row per key instead of window rows: window_start/window_end = the
      * slice, agg[0] = COUNT(*), agg[1] = COUNT(v), agg[2] = SUM bits (0 when COUNT(v) = 0).
      * fg_config.aggs is ignored (the global operator's list applies), except that a MIN or
-     * MAX in it makes agg[2] the partial MIN / MAX instead of the SUM. */
+     * MAX in it makes agg[2] the partial MIN / MAX instead of the SUM; a list mixing the SUM
+     * family, MIN and MAX makes the partial row carry all three value accumulators: agg[2] =
+     * SUM, agg[3] = MIN, agg[4] = MAX (fg_partials.min / max of the global operator). */
     FG_FLAG_LOCAL_PARTIALS = 2,
     /* SQL processing-time windows (SliceAssigner.isEventTime() == false,
      * AbstractWindowAggProcessor.java:137-140): `rowtime` carries each record's processing
@@ -214,6 +216,10 @@ typedef struct fg_partials {
     const int64_t* cnt_star;
     const int64_t* cnt_val;
     const int64_t* sum;           /* i64 or f64 bits per fg_config.val_type */
+    /* a global operator whose list mixes the SUM family, MIN and MAX (several value
+     * accumulators): the partial MIN and MAX (the local phase's agg[3] / agg[4]); else NULL */
+    const int64_t* min;
+    const int64_t* max;
 } fg_partials;
 
 /* Checkpoint image of the GPU-resident keyed state: one entry per (key, slice) accumulator,

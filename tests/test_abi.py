@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 6
+    assert lib.fg_abi_version() == 7
 
 
 def test_struct_layouts_match_header_sizes():
@@ -36,7 +36,7 @@ def test_struct_layouts_match_header_sizes():
     assert C.sizeof(L.FgConfig) == 8 + 32 + 8 + 32 + 24 + 16 + 16 + 8
     assert C.sizeof(L.FgBatch) == 8 + 8 + 4 * 8
     assert C.sizeof(L.FgRows) == 8 + 8 + 3 * 8 + 8 * 8 + 2 * 8
-    assert C.sizeof(L.FgPartials) == 8 + 8 + 5 * 8
+    assert C.sizeof(L.FgPartials) == 8 + 8 + 7 * 8
     assert C.sizeof(L.FgStateRows) == 8 + 7 * 8
     assert C.sizeof(L.FgRowBatch) == 8 + 4 + 4 + 8 + 4 * 4
 
@@ -111,13 +111,10 @@ def test_zone_rules_validated_before_device():
 
 def test_min_max_accumulator_rules():
     """MIN / MAX are SQL aggregates over the value column; they mix with the SUM family in one
-    operator (value slots, include/flinkgpu.h fg_agg) except in the local phase, whose partial
-    row holds one value accumulator; validated before any device call."""
+    operator (value slots, include/flinkgpu.h fg_agg), the local phase included (its partial rows
+    then carry SUM, MIN and MAX); validated before any device call."""
     import torch
     import flink_amd as F
-    for aggs in (("sum", "min"), ("min", "max"), ("avg", "max")):
-        with pytest.raises(F.WindowSpecError):
-            F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="f64", local_partials=True)
     with pytest.raises(F.WindowSpecError):
         F.WindowAggOperator(F.tumbling(1000), aggs=("max",), mode="datastream", val_type="i64")
     with pytest.raises(F.WindowSpecError):
@@ -128,6 +125,10 @@ def test_min_max_accumulator_rules():
         # valid: fails only for want of a device
         with pytest.raises(F.FlinkGpuError) as ei:
             F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="i64")
+        assert ei.value.code == L.FG_EDEVICE
+    for aggs in (("sum", "min"), ("min", "max"), ("avg", "max")):   # local phase, several accumulators
+        with pytest.raises(F.FlinkGpuError) as ei:
+            F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="f64", local_partials=True)
         assert ei.value.code == L.FG_EDEVICE
 
 

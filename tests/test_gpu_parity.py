@@ -559,6 +559,13 @@ TWO_PHASE_CASES = [
           rate_per_ms=0.02)),
     ("dst_tumble_spring_f64", cfg_of("tumble", 3600_000, zone=LA),
      dict(n=300_000, keys=3000, batch=20_000, delay=600_000, jitter=1_800_000, t0=SPRING, rate_per_ms=0.02)),
+    # several value accumulators (SUM family, MIN, MAX): the partial rows carry all three
+    ("mv_hop_f64_late", dict(cfg_of("hop", 3000, 1000), aggs=ALL_AGGS), dict(n=300_000, keys=30_000, batch=20_000,
+                                                                           delay=200, jitter=1500)),
+    ("mv_cumulate_i64_late", dict(cfg_of("cumulate", 4000, 500, vt="i64"), aggs=ALL_AGGS),
+     dict(n=300_000, keys=30_000, batch=15_000, delay=50, jitter=2500)),
+    ("mv_zipf_tumble_f64", dict(cfg_of("tumble", 1000), aggs=("count_star", "avg", "min", "max")),
+     dict(n=6_000_000, keys=100_000, batch=3_000_000, delay=0, jitter=0, rate_per_ms=3_000, zipf=1.1)),
 ]
 
 
@@ -578,7 +585,9 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     w = window_of(cfg)
     aggs = cfg.get("aggs", ("count_star", "count", "sum", "avg", "sum0"))
     mm = tuple(a for a in aggs if a in ("min", "max"))
-    vcol = mm[0] if mm else "sum"   # the partial accumulator column
+    has_sum = any(a in ("sum", "avg", "sum0") for a in aggs)
+    mv = len(mm) + int(has_sum) > 1   # several value accumulators: SUM, MIN, MAX travel together
+    vcol = "sum" if mv or not mm else mm[0]   # the partial accumulator column
     zone = cfg.get("zone")
     local = [F.WindowAggOperator(w, aggs=aggs, val_type=cfg["val_type"], expected_keys=keys, buffer_records=1 << 18,
                                  local_partials=True, zone=zone) for _ in range(S)]
@@ -592,11 +601,13 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
         if len(rows) == 0:
             return
         owner = F.key_groups(rows["key"], MAXP).astype(np.int64) * R // MAXP
-        sums = rows[vcol].view(np.int64) if rows[vcol].dtype == np.float64 else rows[vcol]
+        bits = lambda c: rows[c].view(np.int64) if rows[c].dtype == np.float64 else rows[c]
+        sums = bits(vcol)
         for r in range(R):
             m = owner == r
+            extra = (bits("min")[m], bits("max")[m]) if mv else ()
             glob[r].process_partials(rows["key"][m], rows["window_end"][m], rows["count_star"][m],
-                                     rows["count"][m], sums[m])
+                                     rows["count"][m], sums[m], *extra)
 
     got, exp = [], []
     for lo, hi, wm in batches_with_watermarks(n, batch, ts, delay):
@@ -617,7 +628,8 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
     adapter = GpuOperator.__new__(GpuOperator)
     adapter.cfg = cfg
     adapter._rows = [g]
-    assert_rows_equal(adapter.take_rows(), np.concatenate(exp), cfg["val_type"], name, minmax=mm)
+    chk = dict(sums=True, aggs=aggs, sum0="sum0" in aggs) if mv else {}
+    assert_rows_equal(adapter.take_rows(), np.concatenate(exp), cfg["val_type"], name, minmax=mm, **chk)
     for x in local + glob:
         x.close()
     o.close()
