@@ -83,6 +83,12 @@ WORKLOADS = {
                        batch=1_000_000, records=10_000_000, wm_every=10_000, mode="datastream",
                        desc="DataStream keyBy().window(TumblingEventTimeWindows 1s).sum (WindowOperator), "
                             "10M (long, long) records, 10k keys (BASELINE configs[0])"),
+    # configs[1] with a STRING grouping key: every record's key is a 32-B BinaryRowData key row
+    # ("user" + 8 hex digits) interned by the GPU key dictionary inside the timed region
+    "strings": dict(window=("tumbling", 1000), keys=10_000_000, rate=100_000_000, jitter=0, delay=0, zipf=0.0,
+                    desc="SQL TUMBLE 1s COUNT(*)/SUM/AVG(double) GROUP BY a STRING key ('user' + 8 hex digits, "
+                         "32-B BinaryRowData key rows interned by the GPU key dictionary each micro-batch), "
+                         "1B records per GPU, 10M distinct keys (BASELINE configs[1] with a STRING key)"),
     # configs[4]: TUMBLE 1s AVG(double), Zipf s = 1.1 keys, 2 s jitter, bounded out-of-orderness 2 s
     "zipf": dict(window=("tumbling", 1000), keys=10_000_000, rate=100_000_000, jitter=2000, delay=2000, zipf=1.1,
                  desc="SQL TUMBLE 1s AVG(double), 1B records per GPU, 10M Zipf(1.1) keys, rowtime jitter U[0,2s), "
@@ -131,6 +137,23 @@ def gen_columns(n, keys, rate_s, base_index, device, chunk=1 << 26, jitter=0, zi
             ts[lo:hi] += lsr(u2, 1) % jitter
         del i, u, u2
     return key, ts, val
+
+
+def string_key_rows(key):
+    """32-B BinaryRowData key rows of one STRING field "user%08x" (flink_amd.keys.key_row
+    layout: bit set, the slot holding offset 16 << 32 | length 12, the 12 bytes padded to 8),
+    as an int64 [n, 4] device tensor."""
+    k = key & 0xFFFFFFFF
+    hexc = []
+    for i in range(8):
+        nib = (k >> (28 - 4 * i)) & 15
+        hexc.append(torch.where(nib < 10, nib + 48, nib + 87))
+    rows = torch.zeros((key.numel(), 4), dtype=torch.int64, device=key.device)
+    rows[:, 1] = (16 << 32) | 12
+    w2 = ord("u") | ord("s") << 8 | ord("e") << 16 | ord("r") << 24
+    rows[:, 2] = w2 | hexc[0] << 32 | hexc[1] << 40 | hexc[2] << 48 | hexc[3] << 56
+    rows[:, 3] = hexc[4] | hexc[5] << 8 | hexc[6] << 16 | hexc[7] << 24
+    return rows
 
 
 def watermarks_for(lo, hi, rate_s, every, delay=0, jitter=0):
@@ -393,6 +416,17 @@ def main():
     key, ts, val = gen_columns(n, args.keys, args.rate, rank * n, dev, jitter=wl["jitter"], zipf=wl["zipf"])
     if datastream:   # Tuple2<Long, Long>: long values in [0, 1000)
         val = val.to(torch.int64)
+    strings = args.workload == "strings"
+    kdict = None
+    if strings:   # key rows instead of BIGINT keys; the dictionary outlives the steps (as in a job)
+        rows_u8 = string_key_rows(key).view(torch.uint8).reshape(-1)
+        del key
+        key = None
+        row_off = torch.arange(args.batch, dtype=torch.int64, device=dev) * 32
+        row_len = torch.full((args.batch,), 32, dtype=torch.int32, device=dev)
+        kdict = F.KeyDictionary(max_parallelism=128, expected_keys=int(args.keys * 1.05), device=local)
+    from flink_amd import _lib as FL
+    key_hash = FL.KEYHASH_DICT_ID if strings else FL.KEYHASH_BINARYROW_BIGINT
     torch.cuda.synchronize()
     if args.host_input:   # FG_HOST columns: the engine copies each micro-batch H2D on its stream
         key, ts, val = (x.cpu().pin_memory() for x in (key, ts, val))
@@ -425,7 +459,7 @@ def main():
         r = op_local.process_watermark(wm, device_output=True)
         # key, slice end, COUNT(*), COUNT(v), SUM (+ MIN, MAX for several value accumulators)
         cols = device_columns(r, aggs=tuple(range(len(op_local.aggs))), device=dev)
-        recv, sent = exchange_partials(cols, max_parallelism=maxp, via_cpu=via_cpu)
+        recv, sent = exchange_partials(cols, max_parallelism=maxp, key_hash=key_hash, via_cpu=via_cpu)
         torch.cuda.current_stream().synchronize()
         op.process_partials(*recv)
         g = op.process_watermark(global_watermark(wm, device=dev), device_output=True)
@@ -456,7 +490,11 @@ def main():
             if args.checkpoint_every and bi > 0 and bi % args.checkpoint_every == 0:
                 checkpoint()
             hi = min(n, lo + args.batch)
-            k, t, v = key[lo:hi], ts[lo:hi], val[lo:hi]
+            if strings:   # BinaryRowDataKeySelector.getKey rows -> dictionary ids (on the GPU)
+                k, _ = kdict.intern(packed=(rows_u8[32 * lo:32 * hi], row_off[:hi - lo], row_len[:hi - lo]))
+            else:
+                k = key[lo:hi]
+            t, v = ts[lo:hi], val[lo:hi]
             wms = watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"])
             if two_phase:
                 op_local.process_batch(k, t, v)
@@ -466,7 +504,7 @@ def main():
                     xgmi += sent
                 continue
             if world > 1:
-                k, t, v2, sent = exchange(k, t, v.view(torch.int64), max_parallelism=maxp)
+                k, t, v2, sent = exchange(k, t, v.view(torch.int64), max_parallelism=maxp, key_hash=key_hash)
                 v = v2.view(v.dtype)
                 xgmi += sent
                 torch.cuda.current_stream().synchronize()
@@ -607,6 +645,9 @@ def main():
     op.close()   # (idempotent)
     if op_local:
         op_local.close()
+    if kdict is not None:
+        result["key_dictionary"] = {"distinct_keys": len(kdict), "row_bytes": 32}
+        kdict.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -12,13 +12,17 @@
 // aggregation by id is the aggregation by key row, and the id carries the row's key group
 // (FG_KEYHASH_DICT_ID routes by it).
 //
-// Layout in HBM: an open-addressing table of `cap` slots {tag u64 (a 64-bit hash of the row,
-// 0 = empty), id i64, claiming row u32}; per id its row's offset and length in a byte arena
-// (rows padded to 8 bytes). One intern call: k_dict_hash (both hashes per row), k_dict_claim
-// (a CAS per new tag), k_dict_assign (the first claimer of a new slot allocates the id and
-// copies its bytes), k_dict_verify (every row compares its bytes with its slot's row: a 64-bit
-// hash collision between distinct rows is caught here and resolved on the host, so ids stay
-// exact whatever the hash).
+// Layout in HBM: an open-addressing table of `cap` 16-B slots {tag u64 (a 64-bit hash of the
+// row, 0 = empty), loc u64 (where the row's entry lives in the arena, and its length)} plus the
+// claiming row of a new slot; the arena holds one entry per id, [id i64][row bytes padded to 8],
+// so a probe takes two random accesses (slot, entry). One intern call: k_dict_probe (per row
+// both hashes in one pass over its words, the slot of its tag or a CAS claiming an empty one,
+// and for a slot whose entry an earlier call wrote the byte comparison with that entry), then
+// over the rows whose slot is new in this call only: k_dict_assign (the first claimer allocates
+// the id and writes the entry) and k_dict_verify (the byte comparison). Reservations (pending
+// list, ids, arena bytes) take one atomic per wave. A 64-bit tag shared by distinct rows fails
+// the comparison and is
+// resolved on the host, so ids stay exact whatever the hash.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,35 +56,29 @@ __host__ __device__ __forceinline__ int32_t binaryrow_hash_bytes(const uint8_t* 
     return (int32_t)fmix32(h1 ^ (uint32_t)len);
 }
 
-// the table's own 64-bit hash of the row (independent of the Flink hash: two keys with equal
-// Flink hashes are common at 10M keys; equal 64-bit tags are ~1e-5 there, and exact anyway)
-__host__ __device__ __forceinline__ uint64_t table_hash(const uint8_t* p, int32_t len, int tag_bits) {
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)len * 0xff51afd7ed558ccdull;
-    int32_t i = 0;
-    for (; i + 8 <= len; i += 8) {
-        const uint64_t w = (uint64_t)load_u32(p + i) | (uint64_t)load_u32(p + i + 4) << 32;
-        h = fmix64(h ^ w) + 0x632BE59BD9B4E019ull;
-    }
-    if (i < len) h = fmix64(h ^ (uint64_t)load_u32(p + i) ^ 0xA0761D6478BD642Full);
-    h = fmix64(h);
-    if (tag_bits < 64) h &= (1ull << tag_bits) - 1;   // diagnostic: force collisions (tests)
-    return h ? h : 1;
-}
+constexpr uint64_t kNoLoc = ~0ull;   // a slot whose entry is not written yet
+
+// Table slot: the row's 64-bit tag and where its entry lives in the arena (entry offset << 24 |
+// row length); one 16-B access finds both. An arena entry is [id i64][row bytes, padded to 8].
+struct alignas(16) Slot {
+    unsigned long long tag;   // 0: empty
+    unsigned long long loc;   // kNoLoc until the entry is written
+};
+__host__ __device__ __forceinline__ uint64_t loc_of(uint64_t entry, int32_t len) { return entry << 24 | (uint32_t)len; }
 
 struct DictDev {
-    uint64_t* tag;       // [cap]
-    int64_t* slot_id;    // [cap] -1: no id yet
+    Slot* slots;         // [cap]
     uint32_t* slot_row;  // [cap] first claimer of a new slot in this call
-    int64_t* ent_off;    // [ids] arena offset of the id's row
+    int64_t* ent_off;    // [ids] arena offset of the id's row bytes (its entry + 8)
     int32_t* ent_len;    // [ids]
     uint64_t* ent_tag;   // [ids] tag (0: resolved on the host, not in the table)
     uint8_t* arena;
-    unsigned long long* counters;   // [0] ids, [1] arena bytes, [2] collisions, [3] bad rows
+    unsigned long long* counters;   // [0] ids, [1] arena bytes, [2] collisions, [3] bad rows, [4] pending rows
     uint64_t mask;       // cap - 1
 };
 
 struct RowsIn {
-    const uint8_t* bytes;
+    const uint8_t* bytes;   // 4-byte aligned; every row at a multiple of 4, of 4-byte words
     const int64_t* off;
     const int32_t* len;
     int64_t n;
@@ -89,36 +87,87 @@ struct RowsIn {
     int32_t tag_bits;
 };
 
-__global__ __launch_bounds__(kDictThreads) void k_dict_hash(RowsIn in, uint64_t* tag_out, int32_t* kg_out,
-                                                            unsigned long long* counters) {
+// device rows: offsets / lengths checked before anything is inserted (counters[3])
+__global__ __launch_bounds__(kDictThreads) void k_dict_check(RowsIn in, unsigned long long* counters) {
     const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
     if (i >= in.n) return;
     const int32_t len = in.len[i];
     const int64_t off = in.off[i];
-    if (len < 0 || (len & 3) != 0 || off < 0 || (off & 3) != 0 || off + len > in.nbytes) {
+    if (len < 0 || len >= (1 << 24) || (len & 3) != 0 || off < 0 || (off & 3) != 0 || off + len > in.nbytes)
         atomicAdd(&counters[3], 1ull);   // (BinaryRowData rows are 8-byte multiples)
-        tag_out[i] = 1;
-        kg_out[i] = 0;
-        return;
-    }
-    const uint8_t* p = in.bytes + off;
-    tag_out[i] = table_hash(p, len, in.tag_bits);
-    kg_out[i] = murmur_hash(binaryrow_hash_bytes(p, len)) % in.max_p;
 }
 
-// a slot for every row: the slot holding its tag, or an empty slot it claimed (CAS)
-__global__ __launch_bounds__(kDictThreads) void k_dict_claim(DictDev d, int64_t n, const uint64_t* tag_in,
-                                                             uint64_t* slot_out) {
-    const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t t = tag_in[i];
+// Both hashes of a row in one pass over its 4-byte words: the Flink hash (hashBytesByWords,
+// seed 42) and the table's own 64-bit tag (independent of it: equal Flink hashes are common at
+// 10M keys; equal tags are ~1e-5 there, and resolved exactly anyway).
+__device__ __forceinline__ void row_hashes(const uint32_t* w, int32_t len, int tag_bits, uint64_t* tag, int32_t* fh) {
+    uint32_t h1 = 42u;
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)len * 0xff51afd7ed558ccdull;
+    const int32_t nw = len >> 2;
+    int32_t k = 0;
+    for (; k + 2 <= nw; k += 2) {
+        const uint32_t a = w[k], b = w[k + 1];
+        h1 = mix_h1(mix_h1(h1, mix_k1(a)), mix_k1(b));
+        h = fmix64(h ^ ((uint64_t)a | (uint64_t)b << 32)) + 0x632BE59BD9B4E019ull;
+    }
+    if (k < nw) {
+        const uint32_t a = w[k];
+        h1 = mix_h1(h1, mix_k1(a));
+        h = fmix64(h ^ (uint64_t)a ^ 0xA0761D6478BD642Full);
+    }
+    h = fmix64(h);
+    if (tag_bits < 64) h &= (1ull << tag_bits) - 1;   // diagnostic: force collisions (tests)
+    *tag = h ? h : 1;
+    *fh = (int32_t)fmix32(h1 ^ (uint32_t)len);
+}
+
+// one atomic per wave: lane-exclusive offsets of `amount` (0 for a lane that takes nothing)
+// reserved from *ctr; every lane of the wave must call it (inactive lanes count as 0)
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* ctr, uint32_t amount) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = amount;   // inclusive scan over the wave
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    const uint32_t total = __shfl(x, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && total) base = atomicAdd(ctr, (unsigned long long)total);
+    base = __shfl(base, 63);
+    return base + x - amount;
+}
+
+// the id of the entry at `loc` if its row equals the row at w, else -1
+__device__ __forceinline__ int64_t entry_id_if_equal(const DictDev& d, uint64_t loc, const uint32_t* w, int32_t len) {
+    if ((int32_t)(loc & 0xFFFFFF) != len) return -1;
+    const uint8_t* e = d.arena + (loc >> 24);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(e + 8);
+    bool eq = true;
+    for (int32_t k = 0; eq && k < (len >> 2); k++) eq = w[k] == q[k];
+    return eq ? *reinterpret_cast<const int64_t*>(e) : -1;
+}
+
+// One pass per row: both hashes, the slot holding the row's tag or an empty one claimed with a
+// CAS, and -- when the slot's entry was written by an earlier call -- the byte comparison with
+// that entry (its id, or -1: a distinct row with an equal tag, left to the host). Rows whose
+// slot is new in this call (claimed by them or by an equal-tagged row) join the pending list for
+// k_dict_assign / k_dict_verify (none in a steady state).
+__global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn in, int32_t* kg_out, uint64_t* slot_out,
+                                                             int64_t* id_out, uint32_t* pending) {
+    const int64_t i0 = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
+    const bool valid = i0 < in.n;   // (every lane stays for the wave-wide reservation below)
+    const int64_t i = valid ? i0 : 0;
+    const int32_t len = in.len[i];
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]);
+    uint64_t t;
+    int32_t fh;
+    row_hashes(w, len, in.tag_bits, &t, &fh);
     uint64_t s = fmix64(t) & d.mask;
-    for (;;) {
-        const uint64_t cur = d.tag[s];
+    for (; valid;) {
+        const uint64_t cur = d.slots[s].tag;
         if (cur == t) break;
         if (cur == 0) {
-            const unsigned long long old =
-                atomicCAS(reinterpret_cast<unsigned long long*>(&d.tag[s]), 0ull, (unsigned long long)t);
+            const unsigned long long old = atomicCAS(&d.slots[s].tag, 0ull, (unsigned long long)t);
             if (old == 0) {   // claimed: this row owns the new slot (no other row can claim it)
                 d.slot_row[s] = (uint32_t)i;
                 break;
@@ -127,60 +176,76 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_claim(DictDev d, int64_t 
         }
         s = (s + 1) & d.mask;
     }
-    slot_out[i] = s;
+    const uint64_t loc = valid ? d.slots[s].loc : 0;   // written by an earlier call (this call's in k_dict_assign)
+    if (valid) {
+        kg_out[i] = murmur_hash(fh) % in.max_p;
+        slot_out[i] = s;
+        if (loc != kNoLoc) {
+            const int64_t id = entry_id_if_equal(d, loc, w, len);
+            if (id < 0) atomicAdd(&d.counters[2], 1ull);
+            id_out[i] = id;
+        }
+    }
+    const bool pend = valid && loc == kNoLoc;
+    const unsigned long long at = wave_reserve(&d.counters[4], pend ? 1u : 0u);
+    if (pend) pending[at] = (uint32_t)i;
 }
 
-// the claimer of a new slot allocates its id and copies its row into the arena
+// pending rows: the claimer of a new slot allocates its id and writes its entry
 __global__ __launch_bounds__(kDictThreads) void k_dict_assign(DictDev d, RowsIn in, const uint64_t* slot_in,
-                                                              const uint64_t* tag_in, const int32_t* kg_in) {
-    const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (i >= in.n) return;
-    const uint64_t s = slot_in[i];
-    if (d.slot_id[s] >= 0 || d.slot_row[s] != (uint32_t)i) return;
-    const int32_t len = in.len[i];
-    const unsigned long long ord = atomicAdd(&d.counters[0], 1ull);
-    const unsigned long long at = atomicAdd(&d.counters[1], (unsigned long long)((len + 7) & ~7));
-    const uint8_t* p = in.bytes + in.off[i];
-    uint32_t* dst = reinterpret_cast<uint32_t*>(d.arena + at);
-    for (int32_t b = 0; b < len; b += 4) dst[b >> 2] = load_u32(p + b);
-    if (len & 4) dst[len >> 2] = 0;   // (zero padding to 8 bytes)
-    d.ent_off[ord] = (int64_t)at;
-    d.ent_len[ord] = len;
-    d.ent_tag[ord] = tag_in[i];
-    d.slot_id[s] = (int64_t)((uint64_t)kg_in[i] << kIdShift | ord);
+                                                              const int32_t* kg_in, const uint32_t* pending) {
+    const uint64_t np = d.counters[4];
+    const int lane = threadIdx.x & 63;
+    // wave-uniform trip count (the reservations are wave-wide)
+    for (uint64_t wb = (uint64_t)blockIdx.x * kDictThreads + (threadIdx.x & ~63u); wb < np;
+         wb += (uint64_t)gridDim.x * kDictThreads) {
+        const uint64_t j = wb + lane;
+        const int64_t i = j < np ? pending[j] : 0;
+        const uint64_t s = j < np ? slot_in[i] : 0;
+        const bool own = j < np && d.slot_row[s] == (uint32_t)i;
+        const int32_t len = own ? in.len[i] : 0;
+        const unsigned long long ord = wave_reserve(&d.counters[0], own ? 1u : 0u);
+        const unsigned long long at = wave_reserve(&d.counters[1], own ? (uint32_t)(8 + ((len + 7) & ~7)) : 0u);
+        if (!own) continue;
+        const int64_t id = (int64_t)((uint64_t)kg_in[i] << kIdShift | ord);
+        *reinterpret_cast<int64_t*>(d.arena + at) = id;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(d.arena + at + 8);
+        for (int32_t k = 0; k < (len >> 2); k++) dst[k] = src[k];
+        if (len & 4) dst[len >> 2] = 0;   // (zero padding to 8 bytes)
+        d.ent_off[ord] = (int64_t)at + 8;
+        d.ent_len[ord] = len;
+        d.ent_tag[ord] = d.slots[s].tag;
+        d.slots[s].loc = loc_of(at, len);
+    }
 }
 
-// every row compares its bytes with its slot's row; a mismatch (distinct rows, equal tags) is
-// left to the host (-1)
+// pending rows compare their bytes with their slot's (new) entry; a mismatch is left to the host
 __global__ __launch_bounds__(kDictThreads) void k_dict_verify(DictDev d, RowsIn in, const uint64_t* slot_in,
-                                                              int64_t* id_out) {
-    const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (i >= in.n) return;
-    const int32_t len = in.len[i];
-    const int64_t id = d.slot_id[slot_in[i]];
-    const uint64_t ord = (uint64_t)id & kOrdMask;
-    bool eq = d.ent_len[ord] == len;
-    const uint8_t* p = in.bytes + in.off[i];
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(d.arena + d.ent_off[ord]);
-    for (int32_t b = 0; eq && b < len; b += 4) eq = load_u32(p + b) == q[b >> 2];
-    if (!eq) atomicAdd(&d.counters[2], 1ull);
-    id_out[i] = eq ? id : -1;
+                                                              const uint32_t* pending, int64_t* id_out) {
+    const uint64_t np = d.counters[4];
+    for (uint64_t j = (uint64_t)blockIdx.x * kDictThreads + threadIdx.x; j < np; j += (uint64_t)gridDim.x * kDictThreads) {
+        const int64_t i = pending[j];
+        const int64_t id = entry_id_if_equal(d, d.slots[slot_in[i]].loc,
+                                             reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]), in.len[i]);
+        if (id < 0) atomicAdd(&d.counters[2], 1ull);
+        id_out[i] = id;
+    }
 }
 
 // rebuild the table at a larger capacity from the entries (ids keep their values)
-__global__ __launch_bounds__(kDictThreads) void k_dict_rehash(DictDev d, int64_t nids, const int64_t* ids_kg) {
+__global__ __launch_bounds__(kDictThreads) void k_dict_rehash(DictDev d, int64_t nids) {
     const int64_t o = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
     if (o >= nids) return;
     const uint64_t t = d.ent_tag[o];
     if (t == 0) return;   // a host-resolved row: not in the table
     uint64_t s = fmix64(t) & d.mask;
     for (;;) {
-        const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long*>(&d.tag[s]), 0ull,
-                                                 (unsigned long long)t);
+        const unsigned long long old = atomicCAS(&d.slots[s].tag, 0ull, (unsigned long long)t);
         if (old == 0) break;
         s = (s + 1) & d.mask;
     }
-    d.slot_id[s] = ids_kg[o];
+    d.slots[s].loc = loc_of((uint64_t)(d.ent_off[o] - 8), d.ent_len[o]);
 }
 
 __global__ __launch_bounds__(kDictThreads) void k_dict_gather(DictDev d, int64_t n, const int64_t* ids, int64_t nids,
@@ -193,9 +258,9 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_gather(DictDev d, int64_t
     len_out[i] = ok ? d.ent_len[ord] : -1;
 }
 
-__global__ __launch_bounds__(kDictThreads) void k_fill_u64(uint64_t* p, int64_t n, uint64_t v) {
+__global__ __launch_bounds__(kDictThreads) void k_slots_clear(Slot* p, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (i < n) p[i] = v;
+    if (i < n) p[i] = Slot{0ull, kNoLoc};
 }
 
 inline unsigned grid_of(int64_t n) { return (unsigned)((n + kDictThreads - 1) / kDictThreads); }
@@ -243,7 +308,7 @@ struct fg_key_dict {
     uint64_t cap = 0;   // table slots (power of two)
     int64_t nids = 0;   // ids handed out (host mirror of counters[0])
     int64_t arena_used = 0;
-    Buf tag, slot_id, slot_row, ent_off, ent_len, ent_tag, ent_id, arena, counters;
+    Buf slots, slot_row, ent_off, ent_len, ent_tag, arena, counters;
     Buf in_bytes, in_off, in_len, row_tag, row_kg, row_slot, row_id;   // per-call scratch
     std::unordered_map<std::string, int64_t> side;   // rows whose tag another row holds
     std::string err;
@@ -254,8 +319,7 @@ struct fg_key_dict {
     }
     DictDev dev() const {
         DictDev d;
-        d.tag = tag.as<uint64_t>();
-        d.slot_id = slot_id.as<int64_t>();
+        d.slots = slots.as<Slot>();
         d.slot_row = slot_row.as<uint32_t>();
         d.ent_off = ent_off.as<int64_t>();
         d.ent_len = ent_len.as<int32_t>();
@@ -275,41 +339,22 @@ struct fg_key_dict {
 
 namespace {
 
-// ids of every entry (key group bits included), for a rebuild
-__global__ __launch_bounds__(kDictThreads) void k_dict_ids(DictDev d, uint64_t cap, int64_t* ids_kg) {
-    const int64_t s = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (s >= (int64_t)cap) return;
-    const int64_t id = d.slot_id[s];
-    if (id >= 0) ids_kg[(uint64_t)id & kOrdMask] = id;
-}
-
 // table at `ncap` slots (power of two) holding every entry
 int rebuild(fg_key_dict* d, uint64_t ncap) {
     hipStream_t s = d->stream;
-    // the ids' key-group bits: from the old table (host-resolved ids are kept in ent_id)
-    DCHK(d, d->ent_id.ensure(8 * (size_t)std::max<int64_t>(d->nids, 1), s, 8 * (size_t)d->nids));
-    if (d->cap && d->nids)
-        hipLaunchKernelGGL(k_dict_ids, dim3(grid_of((int64_t)d->cap)), dim3(kDictThreads), 0, s, d->dev(), d->cap,
-                           d->ent_id.as<int64_t>());
-    DCHK(d, hipGetLastError());
-    Buf ntag, nid, nrow;
-    DCHK(d, ntag.ensure(8 * ncap, s));
-    DCHK(d, nid.ensure(8 * ncap, s));
+    Buf nslots, nrow;
+    DCHK(d, nslots.ensure(sizeof(Slot) * ncap, s));
     DCHK(d, nrow.ensure(4 * ncap, s));
-    DCHK(d, hipMemsetAsync(ntag.p, 0, 8 * ncap, s));
-    hipLaunchKernelGGL(k_fill_u64, dim3(grid_of((int64_t)ncap)), dim3(kDictThreads), 0, s, nid.as<uint64_t>(),
-                       (int64_t)ncap, ~0ull);
+    hipLaunchKernelGGL(k_slots_clear, dim3(grid_of((int64_t)ncap)), dim3(kDictThreads), 0, s, nslots.as<Slot>(),
+                       (int64_t)ncap);
     DCHK(d, hipGetLastError());
-    std::swap(d->tag.p, ntag.p);
-    std::swap(d->tag.bytes, ntag.bytes);
-    std::swap(d->slot_id.p, nid.p);
-    std::swap(d->slot_id.bytes, nid.bytes);
+    std::swap(d->slots.p, nslots.p);
+    std::swap(d->slots.bytes, nslots.bytes);
     std::swap(d->slot_row.p, nrow.p);
     std::swap(d->slot_row.bytes, nrow.bytes);
     d->cap = ncap;
     if (d->nids)
-        hipLaunchKernelGGL(k_dict_rehash, dim3(grid_of(d->nids)), dim3(kDictThreads), 0, s, d->dev(), d->nids,
-                           d->ent_id.as<int64_t>());
+        hipLaunchKernelGGL(k_dict_rehash, dim3(grid_of(d->nids)), dim3(kDictThreads), 0, s, d->dev(), d->nids);
     DCHK(d, hipGetLastError());
     DCHK(d, hipStreamSynchronize(s));
     return FG_OK;
@@ -352,9 +397,11 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     if (hipSetDevice(d->device) != hipSuccess) return d->fail(FG_EDEVICE, "hipSetDevice failed");
     hipStream_t s = d->stream;
     const bool host = location == FG_HOST;
+    if (!host && (uintptr_t)bytes % 4 != 0)
+        return d->fail(FG_EINVAL, "fg_key_dict_intern: the row buffer must be 4-byte aligned");
     if (host) {   // validate on the host: every row inside the buffer, 4-byte words
         for (int64_t i = 0; i < n; i++) {
-            if (lengths[i] < 0 || (lengths[i] & 3) || (offsets[i] & 3) || offsets[i] < 0 ||
+            if (lengths[i] < 0 || lengths[i] >= (1 << 24) || (lengths[i] & 3) || (offsets[i] & 3) || offsets[i] < 0 ||
                 offsets[i] + lengths[i] > nbytes)
                 return d->fail(FG_EINVAL, "key row " + std::to_string(i) +
                                               ": offset/length outside the buffer or not a multiple of 4 bytes");
@@ -367,7 +414,7 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     DCHK(d, d->ent_off.ensure(8 * ents, s, 8 * (size_t)d->nids));
     DCHK(d, d->ent_len.ensure(4 * ents, s, 4 * (size_t)d->nids));
     DCHK(d, d->ent_tag.ensure(8 * ents, s, 8 * (size_t)d->nids));
-    DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)nbytes + 8 * (size_t)n + 8, s, (size_t)d->arena_used));
+    DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)nbytes + 16 * (size_t)n + 16, s, (size_t)d->arena_used));
     RowsIn in{};
     in.n = n;
     in.nbytes = nbytes;
@@ -388,7 +435,7 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
         in.off = offsets;
         in.len = lengths;
     }
-    DCHK(d, d->row_tag.ensure(8 * (size_t)n, s));
+    DCHK(d, d->row_tag.ensure(4 * (size_t)n, s));   // the pending list (row indices)
     DCHK(d, d->row_kg.ensure(4 * (size_t)n, s));
     DCHK(d, d->row_slot.ensure(8 * (size_t)n, s));
     int64_t* ids = out_id;
@@ -398,10 +445,9 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     }
     const DictDev dv = d->dev();
     const unsigned g = grid_of(n);
-    hipLaunchKernelGGL(k_dict_hash, dim3(g), dim3(kDictThreads), 0, s, in, d->row_tag.as<uint64_t>(),
-                       d->row_kg.as<int32_t>(), dv.counters);
-    DCHK(d, hipGetLastError());
     if (!host) {   // device rows are checked on the device before anything is inserted
+        hipLaunchKernelGGL(k_dict_check, dim3(g), dim3(kDictThreads), 0, s, in, dv.counters);
+        DCHK(d, hipGetLastError());
         unsigned long long bad = 0;
         DCHK(d, hipMemcpyAsync(&bad, dv.counters + 3, 8, hipMemcpyDeviceToHost, s));
         DCHK(d, hipStreamSynchronize(s));
@@ -412,13 +458,17 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
                                           " key rows outside the buffer or not a multiple of 4 bytes");
         }
     }
-    hipLaunchKernelGGL(k_dict_claim, dim3(g), dim3(kDictThreads), 0, s, dv, n, d->row_tag.as<uint64_t>(),
-                       d->row_slot.as<uint64_t>());
-    hipLaunchKernelGGL(k_dict_assign, dim3(g), dim3(kDictThreads), 0, s, dv, in, d->row_slot.as<uint64_t>(),
-                       d->row_tag.as<uint64_t>(), d->row_kg.as<int32_t>());
-    hipLaunchKernelGGL(k_dict_verify, dim3(g), dim3(kDictThreads), 0, s, dv, in, d->row_slot.as<uint64_t>(), ids);
+    DCHK(d, hipMemsetAsync(dv.counters + 4, 0, 8, s));
+    uint32_t* pending = d->row_tag.as<uint32_t>();
+    hipLaunchKernelGGL(k_dict_probe, dim3(g), dim3(kDictThreads), 0, s, dv, in, d->row_kg.as<int32_t>(),
+                       d->row_slot.as<uint64_t>(), ids, pending);
+    const unsigned gp = std::min(g, 1024u);   // the pending list is short in a steady state
+    hipLaunchKernelGGL(k_dict_assign, dim3(gp), dim3(kDictThreads), 0, s, dv, in, d->row_slot.as<uint64_t>(),
+                       d->row_kg.as<int32_t>(), pending);
+    hipLaunchKernelGGL(k_dict_verify, dim3(gp), dim3(kDictThreads), 0, s, dv, in, d->row_slot.as<uint64_t>(),
+                       pending, ids);
     DCHK(d, hipGetLastError());
-    unsigned long long cnt[4];
+    unsigned long long cnt[5];
     DCHK(d, hipMemcpyAsync(cnt, d->counters.p, sizeof cnt, hipMemcpyDeviceToHost, s));
     DCHK(d, hipStreamSynchronize(s));
     d->nids = (int64_t)cnt[0];
@@ -451,21 +501,24 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
             if (it != d->side.end()) {
                 id = it->second;
             } else {
+                // its entry ([id][row bytes, padded]) appended to the arena, out of the table
                 const int64_t ord = d->nids++;
                 const int64_t at = d->arena_used;
-                d->arena_used += (l + 7) & ~7;
+                d->arena_used += 8 + ((l + 7) & ~7);
                 DCHK(d, d->ent_off.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
                 DCHK(d, d->ent_len.ensure(4 * (size_t)d->nids, s, 4 * (size_t)ord));
                 DCHK(d, d->ent_tag.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
                 DCHK(d, d->arena.ensure((size_t)d->arena_used, s, (size_t)at));
-                std::vector<uint8_t> padded((l + 7) & ~7, 0);
-                std::copy(row.begin(), row.end(), padded.begin());
+                id = (int64_t)((uint64_t)hkg[i] << kIdShift | (uint64_t)ord);
+                std::vector<uint8_t> entry(8 + ((l + 7) & ~7), 0);
+                std::memcpy(entry.data(), &id, 8);
+                std::copy(row.begin(), row.end(), entry.begin() + 8);
                 const uint64_t zero = 0;
-                if (!padded.empty()) DCHK(d, hipMemcpy(d->arena.as<uint8_t>() + at, padded.data(), padded.size(), hipMemcpyHostToDevice));
-                DCHK(d, hipMemcpy(d->ent_off.as<int64_t>() + ord, &at, 8, hipMemcpyHostToDevice));
+                const int64_t row_off = at + 8;
+                DCHK(d, hipMemcpy(d->arena.as<uint8_t>() + at, entry.data(), entry.size(), hipMemcpyHostToDevice));
+                DCHK(d, hipMemcpy(d->ent_off.as<int64_t>() + ord, &row_off, 8, hipMemcpyHostToDevice));
                 DCHK(d, hipMemcpy(d->ent_len.as<int32_t>() + ord, &l, 4, hipMemcpyHostToDevice));
                 DCHK(d, hipMemcpy(d->ent_tag.as<uint64_t>() + ord, &zero, 8, hipMemcpyHostToDevice));
-                id = (int64_t)((uint64_t)hkg[i] << kIdShift | (uint64_t)ord);
                 d->side.emplace(std::move(k), id);
             }
             hid[i] = id;
