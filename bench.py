@@ -74,7 +74,7 @@ WORKLOADS = {
     # configs[3]: CUMULATE 1h/1min over 60 event-minutes; 100M keys sharded over 8 GPUs ->
     # the per-GPU share (12.5M) at N = 1, the whole 100M space at N = 8
     "cumulate": dict(window=("cumulative", 3_600_000, 60_000), keys=12_500_000, rate=1_000_000_000 // 3600,
-                     jitter=0, delay=0, zipf=0.0, batch=12_500_000,
+                     jitter=0, delay=0, zipf=0.0, batch=16_666_667,
                      desc="SQL CUMULATE 1h/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 60 event-minutes, "
                           "uniform keys: 12.5M per GPU = the per-GPU key-group share of 100M (BASELINE configs[3])"),
     # configs[0]: DataStream keyBy().window(TumblingEventTimeWindows 1s).sum on (long key,
@@ -347,8 +347,8 @@ def main():
     ap.add_argument("--keys", type=int, default=None, help="key space (default: the workload's)")
     ap.add_argument("--rate", type=int, default=None, help="records per event-second (default: the workload's)")
     ap.add_argument("--batch", type=int, default=None,
-                    help="micro-batch records (default 50M; hop 25M and cumulate 12.5M so that a micro-batch "
-                         "spans at most two 1-minute slices, the staged lanes of a 10M-key operator)")
+                    help="micro-batch records (default 50M; hop 25M and cumulate one event-minute (16.7M) so that a "
+                         "micro-batch spans at most two 1-minute slices, the staged lanes of a 10M-key operator)")
     ap.add_argument("--wm-every", type=int, default=None, help="records between watermarks (default 1M; "
                     "configs[0]: 10k)")
     ap.add_argument("--checkpoint-every", type=int, default=None,

@@ -480,21 +480,26 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
         std::vector<int32_t> hkg(n);
         DCHK(d, hipMemcpy(hid.data(), ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
         DCHK(d, hipMemcpy(hkg.data(), d->row_kg.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        // device rows: one copy of the buffer and its offsets / lengths, not one per row
+        std::vector<uint8_t> hbytes;
+        std::vector<int64_t> hoff;
+        std::vector<int32_t> hlen;
+        if (!host) {
+            hbytes.resize((size_t)nbytes);
+            hoff.resize(n);
+            hlen.resize(n);
+            if (nbytes) DCHK(d, hipMemcpy(hbytes.data(), bytes, (size_t)nbytes, hipMemcpyDeviceToHost));
+            DCHK(d, hipMemcpy(hoff.data(), offsets, 8 * (size_t)n, hipMemcpyDeviceToHost));
+            DCHK(d, hipMemcpy(hlen.data(), lengths, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        }
+        const uint8_t* rb = host ? bytes : hbytes.data();
+        const int64_t* ro = host ? offsets : hoff.data();
+        const int32_t* rl = host ? lengths : hlen.data();
         std::vector<uint8_t> row;
         for (int64_t i = 0; i < n; i++) {
             if (hid[i] >= 0) continue;
-            const int32_t len = host ? lengths[i] : 0;
-            int64_t off = 0;
-            int32_t l = len;
-            if (host) {
-                off = offsets[i];
-                row.assign(bytes + off, bytes + off + len);
-            } else {
-                DCHK(d, hipMemcpy(&off, offsets + i, 8, hipMemcpyDeviceToHost));
-                DCHK(d, hipMemcpy(&l, lengths + i, 4, hipMemcpyDeviceToHost));
-                row.resize(l);
-                if (l) DCHK(d, hipMemcpy(row.data(), bytes + off, (size_t)l, hipMemcpyDeviceToHost));
-            }
+            const int32_t l = rl[i];
+            row.assign(rb + ro[i], rb + ro[i] + l);
             std::string k(row.begin(), row.end());
             auto it = d->side.find(k);
             int64_t id;

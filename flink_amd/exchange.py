@@ -126,14 +126,33 @@ def exchange_partials(cols, group=None, max_parallelism: int = 128, key_hash: in
     if world == 1:
         return outs, 0
     dev = cols[0].device
-    packed = torch.stack(outs, dim=1).contiguous() if outs[0].numel() else torch.empty((0, len(cols)),
-                                                                                       dtype=torch.int64, device=dev)
+    if via_cpu:   # gloo rehearsal: staged through host memory
+        outs, counts = [o.cpu() for o in outs], counts.cpu()
+    # one all-to-all per column, straight from the partitioned columns into the received ones
+    # (no [n, c] packing copy before the collective, no column split after it)
+    recv, sent_bytes = exchange_columns(outs, counts, group)
     if via_cpu:
-        packed, counts = packed.cpu(), counts.cpu()
-    out, sent_bytes = exchange_grouped(packed, counts, group)
-    if via_cpu:
-        out = out.to(dev)
-    return [out[:, j].contiguous() for j in range(len(cols))], sent_bytes
+        recv = [r.to(dev) for r in recv]
+    return recv, sent_bytes
+
+
+def exchange_columns(cols, counts, group=None):
+    """The collective step of the partial-row exchange on separate columns: `cols` (int64, the
+    same length) grouped by destination rank, counts[d] rows for rank d. One all-to-all of the
+    counts, then one per column. Returns the received columns and the bytes sent to peers."""
+    import torch.distributed as dist
+    recv_counts = torch.empty_like(counts)
+    dist.all_to_all_single(recv_counts, counts, group=group)
+    send = counts.cpu().tolist()
+    recv = recv_counts.cpu().tolist()
+    total = sum(recv)
+    out = []
+    for c in cols:
+        r = torch.empty(total, dtype=c.dtype, device=c.device)
+        dist.all_to_all_single(r, c, output_split_sizes=recv, input_split_sizes=send, group=group)
+        out.append(r)
+    rank = dist.get_rank(group)
+    return out, 8 * len(cols) * (sum(send) - send[rank])
 
 
 def exchange_grouped(packed, counts, group=None):

@@ -107,11 +107,11 @@ TP_N, TP_KEYS, TP_BATCH, TP_DELAY, TP_RATE = 60_000, 4000, 6_000, 100, 10
 TP_KINDS = {"tumble": (0, 500, 0, 900), "hop": (1, 1500, 500, 2500), "cumulate": (2, 2000, 500, 3000)}
 
 
-def _two_phase_rank(rank, world, port, kind, out_q):
+def _two_phase_rank(rank, world, port, kind, out_q, columns=False):
     import torch
     import torch.distributed as dist
 
-    from flink_amd.exchange import exchange_grouped, global_watermark
+    from flink_amd.exchange import exchange_columns, exchange_grouped, global_watermark
     from oracle import oracle as O
     from tests.streams import make_stream
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -135,7 +135,11 @@ def _two_phase_rank(rank, world, port, kind, out_q):
         part = part[np.argsort(owner, kind="stable")]
         counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
         packed = torch.from_numpy(part.view(np.int64).reshape(len(part), O.ROW_DTYPE.itemsize // 8).copy())
-        recv, sent = exchange_grouped(packed, counts)
+        if columns:   # exchange_partials' form: one all-to-all per column
+            rc, sent = exchange_columns([packed[:, j].contiguous() for j in range(packed.shape[1])], counts)
+            recv = torch.stack(rc, dim=1) if rc else packed[:0]
+        else:
+            recv, sent = exchange_grouped(packed, counts)
         sent_total += sent
         got = np.ascontiguousarray(recv.numpy()).view(O.ROW_DTYPE).reshape(-1)
         glob.process_partials(got)
@@ -153,11 +157,13 @@ def _two_phase_rank(rank, world, port, kind, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
-def test_two_phase_exchange_matches_single_operator(oracle_mod, kind):
+@pytest.mark.parametrize("kind,columns", [("tumble", False), ("hop", False), ("cumulate", False),
+                                          ("tumble", True), ("hop", True)])
+def test_two_phase_exchange_matches_single_operator(oracle_mod, kind, columns):
     """Two ranks run the local phase on their source partitions, exchange the partial
-    accumulator rows by key-group owner (flink_amd.exchange.exchange_grouped: the collective
-    step of exchange_partials, gloo here, RCCL on GPUs) and merge them in the owners' global
+    accumulator rows by key-group owner (flink_amd.exchange.exchange_grouped, or exchange_columns:
+    the collective step of exchange_partials, one all-to-all per column; gloo here, RCCL on
+    GPUs) and merge them in the owners' global
     operators, which fire at the min-combined watermark. The union of the global rows equals
     one single-phase operator over both partitions (late rows included: the jitter exceeds
     the watermark delay); late partial rows are counted once each, as in the reference's
@@ -169,7 +175,7 @@ def test_two_phase_exchange_matches_single_operator(oracle_mod, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_two_phase_rank, args=(r, WORLD, port, kind, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_two_phase_rank, args=(r, WORLD, port, kind, q, columns)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(WORLD)]

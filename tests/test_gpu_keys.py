@@ -82,6 +82,16 @@ def test_intern_forced_hash_collisions_stay_exact(monkeypatch):
         ids, kgs = d.intern(rows)
         for r, i in check_interned(d, rows, ids, kgs).items():
             assert seen.setdefault(r, i) == i
+    # the same from device buffers (the host resolves the colliding rows from one copy)
+    import torch
+    dev = torch.device("cuda", 0)
+    for _ in range(2):
+        rows = [rows_all[i] for i in rng.integers(0, len(rows_all), 8000)]
+        buf, off, ln = K.pack_key_rows(rows)
+        ids_t, kg_t = d.intern(packed=(torch.from_numpy(buf.copy()).to(dev), torch.from_numpy(off).to(dev),
+                                       torch.from_numpy(ln).to(dev)))
+        for r, i in check_interned(d, rows, ids_t.cpu().numpy(), kg_t.cpu().numpy()).items():
+            assert seen.setdefault(r, i) == i
     assert len(d) == len(seen)
     d.close()
 
