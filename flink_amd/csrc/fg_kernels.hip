@@ -1355,7 +1355,15 @@ struct LdsTableT<true, true> {
 // linear, slot by slot, from the bucket's first slot. At the regions' load factor (<= ~0.35)
 // a key sits in its home bucket ~99 % of the time, against ~84 % for a single home slot, so
 // a wave's lanes rarely leave the fast path.
-constexpr int kBucket = 4;
+#ifndef FG_BUCKET
+#define FG_BUCKET 4
+#endif
+constexpr int kBucket = FG_BUCKET;   // 4 (two 16-B reads) or 2 (one): slots per home bucket
+#if FG_BUCKET == 4
+#define FG_BUCKET_KEYS(b01, b23) {(b01).x, (b01).y, (b23).x, (b23).y}
+#else
+#define FG_BUCKET_KEYS(b01, b23) {(b01).x, (b01).y}
+#endif
 template <bool C, bool MV>
 __device__ __forceinline__ uint32_t lds_home(int64_t h) {
     constexpr uint32_t NB = (uint32_t)(MergeCfg<C, MV>::kSlotsT / kBucket);
@@ -1394,7 +1402,7 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C, MV>& t, int64_t k, u
                                                bool& full) {
     constexpr uint32_t S_ = (uint32_t)MergeCfg<C, MV>::kSlotsT;
     if (k == JMIN) return (int)S_;
-    const int64_t q[kBucket] = {b01.x, b01.y, b23.x, b23.y};
+    const int64_t q[kBucket] = FG_BUCKET_KEYS(b01, b23);
     int hit = -1, empty = -1;
 #pragma unroll
     for (int j = kBucket - 1; j >= 0; j--) {
@@ -1673,13 +1681,13 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             home[u] = lds_home<C, MV>(c[u].x);
             const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
             b01[u] = kb[0];
-            b23[u] = kb[1];
+            b23[u] = kBucket == 4 ? kb[1] : b01[u];
         }
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             if (m.i0 + u * T + tid >= m.end) continue;
             const int64_t k = c[u].x;
-            const int64_t q[kBucket] = {b01[u].x, b01[u].y, b23[u].x, b23[u].y};
+            const int64_t q[kBucket] = FG_BUCKET_KEYS(b01[u], b23[u]);
             int hit = -1, empty = -1;
 #pragma unroll
             for (int j = kBucket - 1; j >= 0; j--) {   // the first match / first empty slot
@@ -1841,7 +1849,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     home[u] = lds_home<C, MV>(k[u]);
                     const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
                     b01[u] = kb[0];
-                    b23[u] = kb[1];
+                    b23[u] = kBucket == 4 ? kb[1] : b01[u];
                 }
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
