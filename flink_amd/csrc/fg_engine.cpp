@@ -1006,6 +1006,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             skew = skew || s->skew;
             same_bits = same_bits && s->bits == h->region_bits;
         }
+        p.hot_keys = skew ? 1 : 0;
         skew = skew && same_bits;
         HeavyPlan hp{};
         if (skew) {

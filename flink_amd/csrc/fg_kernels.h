@@ -205,6 +205,7 @@ struct MergeParams {
     // accumulators (a chain table of the keys whose timers chain on)
     int32_t emit_marked;
     unsigned long long src_null_mask;   // source j (< 64) may hold NULL counts (else its cnt_null column is 0)
+    int32_t hot_keys;          // skewed staging (Zipf): compact merges pre-combine a wave's equal keys
     unsigned long long mark_mask;
     unsigned long long markonly_mask;   // sources that only mark (their accumulators are not added)
     int32_t dst_mode;

@@ -1355,6 +1355,12 @@ struct LdsTableT<true, true> {
 // linear, slot by slot, from the bucket's first slot. At the regions' load factor (<= ~0.35)
 // a key sits in its home bucket ~99 % of the time, against ~84 % for a single home slot, so
 // a wave's lanes rarely leave the fast path.
+#ifndef FG_WAVE_PRE
+#define FG_WAVE_PRE 1
+#endif
+#ifndef FG_SWZ
+#define FG_SWZ 0
+#endif
 #ifndef FG_BUCKET
 #define FG_BUCKET 4
 #endif
@@ -1680,12 +1686,55 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         for (int u = 0; u < kMergeU; u++) {
             home[u] = lds_home<C, MV>(c[u].x);
             const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
+#if FG_SWZ
+            // odd buckets read their second half first: the first read of every lane then
+            // spans all 16 four-bank groups instead of the even ones only (32-B buckets)
+            const uint32_t sw = kBucket == 4 ? (home[u] >> 2) & 1u : 0u;
+            const RecV2 x0 = kb[sw];
+            const RecV2 x1 = kBucket == 4 ? kb[sw ^ 1u] : x0;
+            b01[u] = sw ? x1 : x0;
+            b23[u] = sw ? x0 : x1;
+#else
             b01[u] = kb[0];
             b23[u] = kBucket == 4 ? kb[1] : b01[u];
+#endif
+        }
+        // Hot keys (Zipf regions below the heavy threshold: one key can fill most of a wave):
+        // the wave's records equal to its first lane's key are combined with cross-lane
+        // reductions and inserted once, by the first of them, instead of serializing a
+        // wave's worth of LDS atomics on one slot. Wave-uniform: every lane takes part.
+        uint32_t pcnt[kMergeU];        // records this lane inserts (0: combined into another lane)
+        int64_t pval[kMergeU][NVS];    // their combined value per value slot
+#pragma unroll
+        for (int u = 0; u < kMergeU; u++) {
+            const bool valid = m.i0 + u * T + tid < m.end;
+            pcnt[u] = valid ? 1u : 0u;
+#pragma unroll
+            for (int q = 0; q < NVS; q++) pval[u][q] = C ? c[u].y : 0;
+#if FG_WAVE_PRE
+            if (C && p.hot_keys) {   // (compact merges only, and only over skewed staging: a
+                                     // uniform stream has no equal keys in a wave to combine)
+            const int64_t k0 = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)c[u].x) |
+                                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)c[u].x >> 32)) << 32));
+            const uint64_t msk = __ballot(valid && c[u].x == k0);
+            if (__popcll(msk) > 1) {
+                const bool in = (msk >> lane) & 1;
+#pragma unroll
+                for (int q = 0; q < NVS; q++) {
+                    const int op = vops[q];
+                    if (op == 0) continue;
+                    int64_t x = in ? c[u].y : val_identity(op);
+                    for (int off = 32; off > 0; off >>= 1) x = val_combine(x, __shfl_xor(x, off), op);
+                    if (in) pval[u][q] = x;   // (the others keep their own value)
+                }
+                if (in) pcnt[u] = lane == __ffsll((long long)msk) - 1 ? (uint32_t)__popcll(msk) : 0u;
+            }
+            }
+#endif
         }
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
-            if (m.i0 + u * T + tid >= m.end) continue;
+            if (pcnt[u] == 0) continue;
             const int64_t k = c[u].x;
             const int64_t q[kBucket] = FG_BUCKET_KEYS(b01[u], b23[u]);
             int hit = -1, empty = -1;
@@ -1715,13 +1764,14 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             }
             if constexpr (MV && VTC >= 0) {   // SUM, MIN, MAX slots, straight-line
                 if (slot >= 0) {
-                    if constexpr (C) atomicAdd(&t.cs[slot], 1u);
+                    if constexpr (C) atomicAdd(&t.cs[slot], pcnt[u]);
                     else atomicAdd(&t.cs[slot], 1ull);
 #pragma unroll
-                    for (int k = 0; k < NVS; k++) lds_val(&t.v[k][slot], c[u].y, vops[k], true);
+                    for (int k = 0; k < NVS; k++) lds_val(&t.v[k][slot], C ? pval[u][k] : c[u].y, vops[k], true);
                 }
             } else if (!(FG_DIAG_MERGE & 1) && slot >= 0) {
-                lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
+                if constexpr (C && FG_WAVE_PRE) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
+                else lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
             }
             if ((FG_DIAG_MERGE & 1) && slot >= 0) t.cs[slot] = 1;
         }
