@@ -491,7 +491,8 @@ def main():
                 checkpoint()
             hi = min(n, lo + args.batch)
             if strings:   # BinaryRowDataKeySelector.getKey rows -> dictionary ids (on the GPU)
-                k, _ = kdict.intern(packed=(rows_u8[32 * lo:32 * hi], row_off[:hi - lo], row_len[:hi - lo]))
+                k, _ = kdict.intern(packed=(rows_u8[32 * lo:32 * hi], row_off[:hi - lo], row_len[:hi - lo]),
+                                    key_groups=False)
             else:
                 k = key[lo:hi]
             t, v = ts[lo:hi], val[lo:hi]

@@ -147,67 +147,150 @@ __device__ __forceinline__ int64_t entry_id_if_equal(const DictDev& d, uint64_t 
     return eq ? *reinterpret_cast<const int64_t*>(e) : -1;
 }
 
+// Rows of up to kRegWords words (BinaryRowData key rows of one or two fixed fields and a short
+// string: 16-32 bytes) are read once into registers -- 8-byte loads when the row is 8-byte
+// aligned -- and hashed and compared from there; longer rows take the word loops above.
+constexpr int kRegWords = 8;
+__device__ __forceinline__ void row_words(const uint8_t* p, int32_t len, uint32_t (&r)[kRegWords]) {
+    const int32_t nw = len >> 2;
+    const bool a8 = ((uintptr_t)p & 7) == 0;
+#pragma unroll
+    for (int k = 0; k < kRegWords; k += 2) {
+        r[k] = r[k + 1] = 0;
+        if (a8 && k + 2 <= nw) {
+            const uint2 v = *reinterpret_cast<const uint2*>(p + 4 * k);
+            r[k] = v.x;
+            r[k + 1] = v.y;
+        } else {
+            if (k < nw) r[k] = *reinterpret_cast<const uint32_t*>(p + 4 * k);
+            if (k + 1 < nw) r[k + 1] = *reinterpret_cast<const uint32_t*>(p + 4 * k + 4);
+        }
+    }
+}
+// row_hashes over register words (the same arithmetic, unrolled)
+__device__ __forceinline__ void row_hashes_reg(const uint32_t (&r)[kRegWords], int32_t len, int tag_bits, uint64_t* tag,
+                                               int32_t* fh) {
+    uint32_t h1 = 42u;
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)(uint32_t)len * 0xff51afd7ed558ccdull;
+    const int32_t nw = len >> 2;
+#pragma unroll
+    for (int k = 0; k < kRegWords; k += 2) {
+        if (k + 2 <= nw) {
+            h1 = mix_h1(mix_h1(h1, mix_k1(r[k])), mix_k1(r[k + 1]));
+            h = fmix64(h ^ ((uint64_t)r[k] | (uint64_t)r[k + 1] << 32)) + 0x632BE59BD9B4E019ull;
+        } else if (k < nw) {
+            h1 = mix_h1(h1, mix_k1(r[k]));
+            h = fmix64(h ^ (uint64_t)r[k] ^ 0xA0761D6478BD642Full);
+        }
+    }
+    h = fmix64(h);
+    if (tag_bits < 64) h &= (1ull << tag_bits) - 1;
+    *tag = h ? h : 1;
+    *fh = (int32_t)fmix32(h1 ^ (uint32_t)len);
+}
+// entry_id_if_equal against register words (entries are 8-byte aligned: 8-byte loads)
+__device__ __forceinline__ int64_t entry_id_if_equal_reg(const DictDev& d, uint64_t loc, const uint32_t (&r)[kRegWords],
+                                                         int32_t len) {
+    if ((int32_t)(loc & 0xFFFFFF) != len) return -1;
+    const uint8_t* e = d.arena + (loc >> 24);
+    const int32_t nw = len >> 2;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int k = 0; k < kRegWords; k += 2) {
+        if (k + 2 <= nw) {
+            const uint2 v = *reinterpret_cast<const uint2*>(e + 8 + 4 * k);
+            diff |= (v.x ^ r[k]) | (v.y ^ r[k + 1]);
+        } else if (k < nw) {
+            diff |= *reinterpret_cast<const uint32_t*>(e + 8 + 4 * k) ^ r[k];
+        }
+    }
+    return diff == 0 ? *reinterpret_cast<const int64_t*>(e) : -1;
+}
+
+// Pending rows (their slot is new in this call): row index, slot and key group, for
+// k_dict_assign / k_dict_verify.
+struct Pending {
+    uint32_t* row;
+    uint64_t* slot;
+    int32_t* kg;
+};
+
 // One pass per row: both hashes, the slot holding the row's tag or an empty one claimed with a
-// CAS, and -- when the slot's entry was written by an earlier call -- the byte comparison with
-// that entry (its id, or -1: a distinct row with an equal tag, left to the host). Rows whose
-// slot is new in this call (claimed by them or by an equal-tagged row) join the pending list for
-// k_dict_assign / k_dict_verify (none in a steady state).
-__global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn in, int32_t* kg_out, uint64_t* slot_out,
-                                                             int64_t* id_out, uint32_t* pending) {
+// CAS (one 16-B load reads a slot's tag and entry location together), and -- when the slot's
+// entry was written by an earlier call -- the byte comparison with that entry (its id, or -1: a
+// distinct row with an equal tag, left to the host). Rows whose slot is new in this call (claimed
+// by them or by an equal-tagged row) join the pending list (none in a steady state). kg_out
+// (optional) takes every row's key group.
+__global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn in, int32_t* kg_out, int64_t* id_out,
+                                                             Pending pend_out) {
     const int64_t i0 = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
     const bool valid = i0 < in.n;   // (every lane stays for the wave-wide reservation below)
     const int64_t i = valid ? i0 : 0;
     const int32_t len = in.len[i];
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]);
+    const uint8_t* rp = in.bytes + in.off[i];
+    const bool small = len <= 4 * kRegWords;
+    uint32_t r[kRegWords];
     uint64_t t;
     int32_t fh;
-    row_hashes(w, len, in.tag_bits, &t, &fh);
+    if (small) {
+        row_words(rp, len, r);
+        row_hashes_reg(r, len, in.tag_bits, &t, &fh);
+    } else {
+        row_hashes(reinterpret_cast<const uint32_t*>(rp), len, in.tag_bits, &t, &fh);
+    }
     uint64_t s = fmix64(t) & d.mask;
+    uint64_t loc = kNoLoc;
     for (; valid;) {
-        const uint64_t cur = d.slots[s].tag;
-        if (cur == t) break;
-        if (cur == 0) {
+        const Slot cur = d.slots[s];
+        if (cur.tag == t) {   // (a slot claimed earlier in this call still has no entry: kNoLoc)
+            loc = cur.loc;
+            break;
+        }
+        if (cur.tag == 0) {
             const unsigned long long old = atomicCAS(&d.slots[s].tag, 0ull, (unsigned long long)t);
             if (old == 0) {   // claimed: this row owns the new slot (no other row can claim it)
                 d.slot_row[s] = (uint32_t)i;
                 break;
             }
-            if (old == t) break;
+            if (old == t) break;   // claimed in this call by an equal-tagged row
         }
         s = (s + 1) & d.mask;
     }
-    const uint64_t loc = valid ? d.slots[s].loc : 0;   // written by an earlier call (this call's in k_dict_assign)
+    const int32_t kg = murmur_hash(fh) % in.max_p;
     if (valid) {
-        kg_out[i] = murmur_hash(fh) % in.max_p;
-        slot_out[i] = s;
+        if (kg_out) kg_out[i] = kg;
         if (loc != kNoLoc) {
-            const int64_t id = entry_id_if_equal(d, loc, w, len);
+            const int64_t id = small ? entry_id_if_equal_reg(d, loc, r, len)
+                                     : entry_id_if_equal(d, loc, reinterpret_cast<const uint32_t*>(rp), len);
             if (id < 0) atomicAdd(&d.counters[2], 1ull);
             id_out[i] = id;
         }
     }
     const bool pend = valid && loc == kNoLoc;
     const unsigned long long at = wave_reserve(&d.counters[4], pend ? 1u : 0u);
-    if (pend) pending[at] = (uint32_t)i;
+    if (pend) {
+        pend_out.row[at] = (uint32_t)i;
+        pend_out.slot[at] = s;
+        pend_out.kg[at] = kg;
+    }
 }
 
 // pending rows: the claimer of a new slot allocates its id and writes its entry
-__global__ __launch_bounds__(kDictThreads) void k_dict_assign(DictDev d, RowsIn in, const uint64_t* slot_in,
-                                                              const int32_t* kg_in, const uint32_t* pending) {
+__global__ __launch_bounds__(kDictThreads) void k_dict_assign(DictDev d, RowsIn in, Pending pend) {
     const uint64_t np = d.counters[4];
     const int lane = threadIdx.x & 63;
     // wave-uniform trip count (the reservations are wave-wide)
     for (uint64_t wb = (uint64_t)blockIdx.x * kDictThreads + (threadIdx.x & ~63u); wb < np;
          wb += (uint64_t)gridDim.x * kDictThreads) {
         const uint64_t j = wb + lane;
-        const int64_t i = j < np ? pending[j] : 0;
-        const uint64_t s = j < np ? slot_in[i] : 0;
+        const int64_t i = j < np ? pend.row[j] : 0;
+        const uint64_t s = j < np ? pend.slot[j] : 0;
         const bool own = j < np && d.slot_row[s] == (uint32_t)i;
         const int32_t len = own ? in.len[i] : 0;
         const unsigned long long ord = wave_reserve(&d.counters[0], own ? 1u : 0u);
         const unsigned long long at = wave_reserve(&d.counters[1], own ? (uint32_t)(8 + ((len + 7) & ~7)) : 0u);
         if (!own) continue;
-        const int64_t id = (int64_t)((uint64_t)kg_in[i] << kIdShift | ord);
+        const int64_t id = (int64_t)((uint64_t)pend.kg[j] << kIdShift | ord);
         *reinterpret_cast<int64_t*>(d.arena + at) = id;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]);
         uint32_t* dst = reinterpret_cast<uint32_t*>(d.arena + at + 8);
@@ -221,12 +304,11 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_assign(DictDev d, RowsIn 
 }
 
 // pending rows compare their bytes with their slot's (new) entry; a mismatch is left to the host
-__global__ __launch_bounds__(kDictThreads) void k_dict_verify(DictDev d, RowsIn in, const uint64_t* slot_in,
-                                                              const uint32_t* pending, int64_t* id_out) {
+__global__ __launch_bounds__(kDictThreads) void k_dict_verify(DictDev d, RowsIn in, Pending pend, int64_t* id_out) {
     const uint64_t np = d.counters[4];
     for (uint64_t j = (uint64_t)blockIdx.x * kDictThreads + threadIdx.x; j < np; j += (uint64_t)gridDim.x * kDictThreads) {
-        const int64_t i = pending[j];
-        const int64_t id = entry_id_if_equal(d, d.slots[slot_in[i]].loc,
+        const int64_t i = pend.row[j];
+        const int64_t id = entry_id_if_equal(d, d.slots[pend.slot[j]].loc,
                                              reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]), in.len[i]);
         if (id < 0) atomicAdd(&d.counters[2], 1ull);
         id_out[i] = id;
@@ -309,7 +391,7 @@ struct fg_key_dict {
     int64_t nids = 0;   // ids handed out (host mirror of counters[0])
     int64_t arena_used = 0;
     Buf slots, slot_row, ent_off, ent_len, ent_tag, arena, counters;
-    Buf in_bytes, in_off, in_len, row_tag, row_kg, row_slot, row_id;   // per-call scratch
+    Buf in_bytes, in_off, in_len, row_tag, row_kg, row_slot, row_pkg, row_id;   // per-call scratch
     std::unordered_map<std::string, int64_t> side;   // rows whose tag another row holds
     std::string err;
 
@@ -360,6 +442,68 @@ int rebuild(fg_key_dict* d, uint64_t ncap) {
     return FG_OK;
 }
 
+// Rows of one chunk whose 64-bit tag another row holds (ids -1): exact ids from the host-side
+// map, new rows appended to the arena (ent_tag 0: never rehashed into the table). `bytes`,
+// `offsets`, `lengths` are the caller's (host or device) arrays for the chunk's rows.
+int resolve_collisions(fg_key_dict* d, bool host, int64_t n, const uint8_t* bytes, int64_t nbytes,
+                       const int64_t* offsets, const int32_t* lengths, int64_t* ids) {
+    hipStream_t s = d->stream;
+    std::vector<int64_t> hid(n);
+    DCHK(d, hipMemcpy(hid.data(), ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
+    // device rows: one copy of the buffer and the chunk's offsets / lengths, not one per row
+    std::vector<uint8_t> hbytes;
+    std::vector<int64_t> hoff;
+    std::vector<int32_t> hlen;
+    if (!host) {
+        hbytes.resize((size_t)nbytes);
+        hoff.resize(n);
+        hlen.resize(n);
+        if (nbytes) DCHK(d, hipMemcpy(hbytes.data(), bytes, (size_t)nbytes, hipMemcpyDeviceToHost));
+        DCHK(d, hipMemcpy(hoff.data(), offsets, 8 * (size_t)n, hipMemcpyDeviceToHost));
+        DCHK(d, hipMemcpy(hlen.data(), lengths, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    const uint8_t* rb = host ? bytes : hbytes.data();
+    const int64_t* ro = host ? offsets : hoff.data();
+    const int32_t* rl = host ? lengths : hlen.data();
+    for (int64_t i = 0; i < n; i++) {
+        if (hid[i] >= 0) continue;
+        const int32_t l = rl[i];
+        const uint8_t* row = rb + ro[i];
+        std::string k(row, row + l);
+        auto it = d->side.find(k);
+        int64_t id;
+        if (it != d->side.end()) {
+            id = it->second;
+        } else {
+            // its entry ([id][row bytes, padded]) appended to the arena, out of the table
+            const int64_t ord = d->nids++;
+            const int64_t at = d->arena_used;
+            d->arena_used += 8 + ((l + 7) & ~7);
+            DCHK(d, d->ent_off.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
+            DCHK(d, d->ent_len.ensure(4 * (size_t)d->nids, s, 4 * (size_t)ord));
+            DCHK(d, d->ent_tag.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
+            DCHK(d, d->arena.ensure((size_t)d->arena_used, s, (size_t)at));
+            const int32_t kg = murmur_hash(binaryrow_hash_bytes(row, l)) % d->max_p;
+            id = (int64_t)((uint64_t)kg << kIdShift | (uint64_t)ord);
+            std::vector<uint8_t> entry(8 + ((l + 7) & ~7), 0);
+            std::memcpy(entry.data(), &id, 8);
+            std::memcpy(entry.data() + 8, row, (size_t)l);
+            const uint64_t zero = 0;
+            const int64_t row_off = at + 8;
+            DCHK(d, hipMemcpy(d->arena.as<uint8_t>() + at, entry.data(), entry.size(), hipMemcpyHostToDevice));
+            DCHK(d, hipMemcpy(d->ent_off.as<int64_t>() + ord, &row_off, 8, hipMemcpyHostToDevice));
+            DCHK(d, hipMemcpy(d->ent_len.as<int32_t>() + ord, &l, 4, hipMemcpyHostToDevice));
+            DCHK(d, hipMemcpy(d->ent_tag.as<uint64_t>() + ord, &zero, 8, hipMemcpyHostToDevice));
+            d->side.emplace(std::move(k), id);
+        }
+        hid[i] = id;
+    }
+    DCHK(d, hipMemcpy(ids, hid.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
+    const unsigned long long c2[3] = {(unsigned long long)d->nids, (unsigned long long)d->arena_used, 0ull};
+    DCHK(d, hipMemcpy(d->counters.p, c2, sizeof c2, hipMemcpyHostToDevice));
+    return FG_OK;
+}
+
 uint64_t pow2_at_least(uint64_t x) {
     uint64_t c = 1024;
     while (c < x) c <<= 1;
@@ -407,9 +551,6 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
                                               ": offset/length outside the buffer or not a multiple of 4 bytes");
         }
     }
-    // room: the table stays at most half full, the arena takes every row of the call
-    if ((uint64_t)(d->nids + n) * 2 > d->cap)
-        if (int rc = rebuild(d, pow2_at_least(4 * (uint64_t)(d->nids + n)))) return rc;
     const size_t ents = (size_t)(d->nids + n);
     DCHK(d, d->ent_off.ensure(8 * ents, s, 8 * (size_t)d->nids));
     DCHK(d, d->ent_len.ensure(4 * ents, s, 4 * (size_t)d->nids));
@@ -435,107 +576,73 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
         in.off = offsets;
         in.len = lengths;
     }
-    DCHK(d, d->row_tag.ensure(4 * (size_t)n, s));   // the pending list (row indices)
-    DCHK(d, d->row_kg.ensure(4 * (size_t)n, s));
-    DCHK(d, d->row_slot.ensure(8 * (size_t)n, s));
     int64_t* ids = out_id;
     if (host) {
         DCHK(d, d->row_id.ensure(8 * (size_t)n, s));
         ids = d->row_id.as<int64_t>();
     }
-    const DictDev dv = d->dev();
     const unsigned g = grid_of(n);
     if (!host) {   // device rows are checked on the device before anything is inserted
-        hipLaunchKernelGGL(k_dict_check, dim3(g), dim3(kDictThreads), 0, s, in, dv.counters);
+        hipLaunchKernelGGL(k_dict_check, dim3(g), dim3(kDictThreads), 0, s, in, d->counters.as<unsigned long long>());
         DCHK(d, hipGetLastError());
         unsigned long long bad = 0;
-        DCHK(d, hipMemcpyAsync(&bad, dv.counters + 3, 8, hipMemcpyDeviceToHost, s));
+        DCHK(d, hipMemcpyAsync(&bad, d->counters.as<unsigned long long>() + 3, 8, hipMemcpyDeviceToHost, s));
         DCHK(d, hipStreamSynchronize(s));
         if (bad) {
-            DCHK(d, hipMemsetAsync(dv.counters + 3, 0, 8, s));
+            DCHK(d, hipMemsetAsync(d->counters.as<unsigned long long>() + 3, 0, 8, s));
             DCHK(d, hipStreamSynchronize(s));
             return d->fail(FG_EINVAL, "fg_key_dict_intern: " + std::to_string(bad) +
                                           " key rows outside the buffer or not a multiple of 4 bytes");
         }
     }
-    DCHK(d, hipMemsetAsync(dv.counters + 4, 0, 8, s));
-    uint32_t* pending = d->row_tag.as<uint32_t>();
-    hipLaunchKernelGGL(k_dict_probe, dim3(g), dim3(kDictThreads), 0, s, dv, in, d->row_kg.as<int32_t>(),
-                       d->row_slot.as<uint64_t>(), ids, pending);
-    const unsigned gp = std::min(g, 1024u);   // the pending list is short in a steady state
-    hipLaunchKernelGGL(k_dict_assign, dim3(gp), dim3(kDictThreads), 0, s, dv, in, d->row_slot.as<uint64_t>(),
-                       d->row_kg.as<int32_t>(), pending);
-    hipLaunchKernelGGL(k_dict_verify, dim3(gp), dim3(kDictThreads), 0, s, dv, in, d->row_slot.as<uint64_t>(),
-                       pending, ids);
-    DCHK(d, hipGetLastError());
-    unsigned long long cnt[5];
-    DCHK(d, hipMemcpyAsync(cnt, d->counters.p, sizeof cnt, hipMemcpyDeviceToHost, s));
-    DCHK(d, hipStreamSynchronize(s));
-    d->nids = (int64_t)cnt[0];
-    d->arena_used = (int64_t)cnt[1];
-    if (cnt[2]) {
-        // rows whose 64-bit tag another row holds: exact ids from the host-side map, their rows
-        // appended to the arena (ent_tag 0: never rehashed into the table)
-        std::vector<int64_t> hid(n);
-        std::vector<int32_t> hkg(n);
-        DCHK(d, hipMemcpy(hid.data(), ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
-        DCHK(d, hipMemcpy(hkg.data(), d->row_kg.p, 4 * (size_t)n, hipMemcpyDeviceToHost));
-        // device rows: one copy of the buffer and its offsets / lengths, not one per row
-        std::vector<uint8_t> hbytes;
-        std::vector<int64_t> hoff;
-        std::vector<int32_t> hlen;
-        if (!host) {
-            hbytes.resize((size_t)nbytes);
-            hoff.resize(n);
-            hlen.resize(n);
-            if (nbytes) DCHK(d, hipMemcpy(hbytes.data(), bytes, (size_t)nbytes, hipMemcpyDeviceToHost));
-            DCHK(d, hipMemcpy(hoff.data(), offsets, 8 * (size_t)n, hipMemcpyDeviceToHost));
-            DCHK(d, hipMemcpy(hlen.data(), lengths, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    // Chunks: the table stays at most half full against every row of a chunk being new, so a
+    // chunk takes at most the table's headroom; the table grows with the ids (at least
+    // kDictChunkMin rows, or as many rows as there are ids, per chunk), not with the call's size
+    // -- a 50M-row micro-batch over 10M keys probes a 64M-slot table (1 GiB), not a 256M one.
+    constexpr int64_t kDictChunkMin = 1 << 22;
+    int32_t* kg_dev = nullptr;   // every row's key group, when asked for
+    if (out_kg) {
+        if (host) {
+            DCHK(d, d->row_kg.ensure(4 * (size_t)n, s));
+            kg_dev = d->row_kg.as<int32_t>();
+        } else {
+            kg_dev = out_kg;
         }
-        const uint8_t* rb = host ? bytes : hbytes.data();
-        const int64_t* ro = host ? offsets : hoff.data();
-        const int32_t* rl = host ? lengths : hlen.data();
-        std::vector<uint8_t> row;
-        for (int64_t i = 0; i < n; i++) {
-            if (hid[i] >= 0) continue;
-            const int32_t l = rl[i];
-            row.assign(rb + ro[i], rb + ro[i] + l);
-            std::string k(row.begin(), row.end());
-            auto it = d->side.find(k);
-            int64_t id;
-            if (it != d->side.end()) {
-                id = it->second;
-            } else {
-                // its entry ([id][row bytes, padded]) appended to the arena, out of the table
-                const int64_t ord = d->nids++;
-                const int64_t at = d->arena_used;
-                d->arena_used += 8 + ((l + 7) & ~7);
-                DCHK(d, d->ent_off.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
-                DCHK(d, d->ent_len.ensure(4 * (size_t)d->nids, s, 4 * (size_t)ord));
-                DCHK(d, d->ent_tag.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
-                DCHK(d, d->arena.ensure((size_t)d->arena_used, s, (size_t)at));
-                id = (int64_t)((uint64_t)hkg[i] << kIdShift | (uint64_t)ord);
-                std::vector<uint8_t> entry(8 + ((l + 7) & ~7), 0);
-                std::memcpy(entry.data(), &id, 8);
-                std::copy(row.begin(), row.end(), entry.begin() + 8);
-                const uint64_t zero = 0;
-                const int64_t row_off = at + 8;
-                DCHK(d, hipMemcpy(d->arena.as<uint8_t>() + at, entry.data(), entry.size(), hipMemcpyHostToDevice));
-                DCHK(d, hipMemcpy(d->ent_off.as<int64_t>() + ord, &row_off, 8, hipMemcpyHostToDevice));
-                DCHK(d, hipMemcpy(d->ent_len.as<int32_t>() + ord, &l, 4, hipMemcpyHostToDevice));
-                DCHK(d, hipMemcpy(d->ent_tag.as<uint64_t>() + ord, &zero, 8, hipMemcpyHostToDevice));
-                d->side.emplace(std::move(k), id);
-            }
-            hid[i] = id;
-        }
-        DCHK(d, hipMemcpy(ids, hid.data(), 8 * (size_t)n, hipMemcpyHostToDevice));
-        const unsigned long long c2[3] = {(unsigned long long)d->nids, (unsigned long long)d->arena_used, 0ull};
-        DCHK(d, hipMemcpy(d->counters.p, c2, sizeof c2, hipMemcpyHostToDevice));
+    }
+    for (int64_t pos = 0; pos < n;) {
+        const int64_t want = std::min<int64_t>(n - pos, std::max<int64_t>(kDictChunkMin, d->nids));
+        if ((uint64_t)(d->nids + want) * 2 > d->cap)
+            if (int rc = rebuild(d, pow2_at_least(4 * (uint64_t)(d->nids + want)))) return rc;
+        const int64_t m = std::min<int64_t>(n - pos, (int64_t)(d->cap / 2) - d->nids);
+        DCHK(d, d->row_tag.ensure(4 * (size_t)m, s));   // the pending list
+        DCHK(d, d->row_slot.ensure(8 * (size_t)m, s));
+        DCHK(d, d->row_pkg.ensure(4 * (size_t)m, s));
+        RowsIn c = in;
+        c.off = in.off + pos;
+        c.len = in.len + pos;
+        c.n = m;
+        int64_t* cids = ids + pos;
+        const Pending pend{d->row_tag.as<uint32_t>(), d->row_slot.as<uint64_t>(), d->row_pkg.as<int32_t>()};
+        const DictDev dv = d->dev();
+        const unsigned gm = grid_of(m);
+        DCHK(d, hipMemsetAsync(dv.counters + 4, 0, 8, s));
+        hipLaunchKernelGGL(k_dict_probe, dim3(gm), dim3(kDictThreads), 0, s, dv, c, kg_dev ? kg_dev + pos : nullptr,
+                           cids, pend);
+        const unsigned gp = std::min(gm, 1024u);   // the pending list is short in a steady state
+        hipLaunchKernelGGL(k_dict_assign, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend);
+        hipLaunchKernelGGL(k_dict_verify, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend, cids);
+        DCHK(d, hipGetLastError());
+        unsigned long long cnt[5];
+        DCHK(d, hipMemcpyAsync(cnt, d->counters.p, sizeof cnt, hipMemcpyDeviceToHost, s));
+        DCHK(d, hipStreamSynchronize(s));
+        d->nids = (int64_t)cnt[0];
+        d->arena_used = (int64_t)cnt[1];
+        if (cnt[2])
+            if (int rc = resolve_collisions(d, host, m, bytes, nbytes, offsets + pos, lengths + pos, cids)) return rc;
+        pos += m;
     }
     if (host) DCHK(d, hipMemcpy(out_id, ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
-    if (out_kg) {
-        DCHK(d, hipMemcpy(out_kg, d->row_kg.p, 4 * (size_t)n, host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice));
-    }
+    if (out_kg && host) DCHK(d, hipMemcpy(out_kg, kg_dev, 4 * (size_t)n, hipMemcpyDeviceToHost));
     return FG_OK;
 }
 

@@ -137,9 +137,10 @@ class KeyDictionary:
             raise L.WindowSpecError(msg)
         raise L.FlinkGpuError(rc, msg)
 
-    def intern(self, rows=None, packed=None):
+    def intern(self, rows=None, packed=None, key_groups=True):
         """rows: list of key-row bytes, or packed=(bytes u8[], offsets i64[], lengths i32[]) on the
-        host (numpy) or the device (torch tensors). Returns (ids, key_groups) of the same kind."""
+        host (numpy) or the device (torch tensors). Returns (ids, key_groups) of the same kind
+        (key_groups None when not asked for: an id carries its key group, FG_KEYHASH_DICT_ID)."""
         if packed is None:
             packed = pack_key_rows(rows)
         buf, off, ln = packed
@@ -147,18 +148,20 @@ class KeyDictionary:
         if hasattr(buf, "data_ptr"):   # torch device tensors
             import torch
             ids = torch.empty(n, dtype=torch.int64, device=buf.device)
-            kg = torch.empty(n, dtype=torch.int32, device=buf.device)
+            kg = torch.empty(n, dtype=torch.int32, device=buf.device) if key_groups else None
             self._check(self._lib.fg_key_dict_intern(self._h, L.DEVICE, n, C.c_void_p(buf.data_ptr()), buf.numel(),
                                                      C.c_void_p(off.data_ptr()), C.c_void_p(ln.data_ptr()),
-                                                     C.c_void_p(ids.data_ptr()), C.c_void_p(kg.data_ptr())))
+                                                     C.c_void_p(ids.data_ptr()),
+                                                     C.c_void_p(kg.data_ptr() if key_groups else None)))
             return ids, kg
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.int64)
         ln = np.ascontiguousarray(ln, dtype=np.int32)
         ids = np.empty(n, dtype=np.int64)
-        kg = np.empty(n, dtype=np.int32)
+        kg = np.empty(n, dtype=np.int32) if key_groups else None
         self._check(self._lib.fg_key_dict_intern(self._h, L.HOST, n, buf.ctypes.data, buf.size, off.ctypes.data,
-                                                 ln.ctypes.data, ids.ctypes.data, kg.ctypes.data))
+                                                 ln.ctypes.data, ids.ctypes.data,
+                                                 C.c_void_p(kg.ctypes.data if key_groups else None)))
         return ids, kg
 
     def lookup(self, ids):

@@ -246,3 +246,38 @@ def test_dictionary_ids_route_by_the_rows_key_group():
     for r in range(par):
         assert (owner[pos[off[r]:off[r + 1]]] == r).all()
     d.close()
+
+
+def test_intern_chunked_call_unaligned_rows_and_no_key_groups():
+    """One call larger than a chunk (the table grows with the ids, the call is split into chunks
+    of at most the table's headroom), BIGINT key rows read from 8-byte-aligned and from only
+    4-byte-aligned offsets (register path, 8- and 4-byte loads), and the call without key groups:
+    the same exact ids everywhere."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    distinct = rng.choice(np.arange(-(1 << 40), 1 << 40, 7919, dtype=np.int64), 50_000, replace=False)
+    keys = distinct[rng.integers(0, len(distinct), 9_000_000)]
+    n = len(keys)
+    rows = np.zeros((n, 2), dtype=np.int64)   # BinaryRowData of one BIGINT field: null bits, value
+    rows[:, 1] = keys
+    buf = torch.from_numpy(rows.view(np.uint8).reshape(-1)).to(dev)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * 16
+    ln = torch.full((n,), 16, dtype=torch.int32, device=dev)
+    d = F.KeyDictionary(max_parallelism=MAXP, expected_keys=1000)
+    ids_t, kg_t = d.intern(packed=(buf, off, ln))
+    ids = ids_t.cpu().numpy()
+    assert len(d) == len(distinct)
+    pairs = np.unique(np.stack([keys, ids]), axis=1)
+    assert pairs.shape[1] == len(distinct) and len(np.unique(ids)) == len(distinct)   # a bijection
+    _, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    kg_u = np.array([O.key_group_of_row(rows[i].tobytes(), MAXP) for i in first], dtype=np.int32)
+    assert np.array_equal(kg_t.cpu().numpy(), kg_u[inv])
+    assert np.array_equal(K.key_group_of_id(ids, MAXP), kg_t.cpu().numpy())
+    # the same rows at 4-byte-aligned offsets (a 4-byte pad in front), without key groups
+    buf4 = torch.cat([torch.zeros(4, dtype=torch.uint8, device=dev), buf])
+    ids4, kg4 = d.intern(packed=(buf4, off + 4, ln), key_groups=False)
+    assert kg4 is None
+    assert np.array_equal(ids4.cpu().numpy(), ids)
+    assert len(d) == len(distinct)
+    d.close()
