@@ -41,6 +41,9 @@ using namespace fg;
 namespace {
 
 constexpr int kDictThreads = 256;
+#ifndef FG_DICT_GROW
+#define FG_DICT_GROW 4   // table rebuilt at FG_DICT_GROW x (ids + chunk) slots (>= 2: at most half full)
+#endif
 constexpr int kIdShift = 40;   // id = key group << kIdShift | ordinal
 constexpr uint64_t kOrdMask = (1ull << kIdShift) - 1;
 
@@ -612,7 +615,7 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     for (int64_t pos = 0; pos < n;) {
         const int64_t want = std::min<int64_t>(n - pos, std::max<int64_t>(kDictChunkMin, d->nids));
         if ((uint64_t)(d->nids + want) * 2 > d->cap)
-            if (int rc = rebuild(d, pow2_at_least(4 * (uint64_t)(d->nids + want)))) return rc;
+            if (int rc = rebuild(d, pow2_at_least(FG_DICT_GROW * (uint64_t)(d->nids + want)))) return rc;
         const int64_t m = std::min<int64_t>(n - pos, (int64_t)(d->cap / 2) - d->nids);
         DCHK(d, d->row_tag.ensure(4 * (size_t)m, s));   // the pending list
         DCHK(d, d->row_slot.ensure(8 * (size_t)m, s));
