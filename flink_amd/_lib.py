@@ -96,7 +96,8 @@ EXPORTS = (
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
     "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
-    "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_last_error", "fg_key_dict_close", "fg_binaryrow_hash",
+    "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_stream", "fg_key_dict_last_error", "fg_key_dict_close",
+    "fg_binaryrow_hash",
 )
 
 _lib = None
@@ -162,6 +163,8 @@ def load():
     L.fg_key_dict_copy_arena.argtypes = [P, C.c_int64, C.c_int64, P]
     L.fg_key_dict_size.argtypes = [P]
     L.fg_key_dict_size.restype = C.c_int64
+    L.fg_key_dict_stream.argtypes = [P]
+    L.fg_key_dict_stream.restype = P
     L.fg_key_dict_last_error.argtypes = [P]
     L.fg_key_dict_last_error.restype = C.c_char_p
     L.fg_key_dict_close.argtypes = [P]

@@ -2516,6 +2516,17 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
             if (slot >= 0) (void)hipEventRecord(h->ev_free[slot], h->stream);
         }
     } slot_free{h, slot};
+    // The caller's host columns are read by the DMA until ev_copied: the call returns only
+    // after it (the header's contract -- a shim recycles its pinned staging ring right away,
+    // as RecordsWindowBuffer's callers reuse their row objects, RecordsWindowBuffer.java:81-97).
+    // The kernels of this batch are queued first, so the GPU keeps working on the engine
+    // stream while the host waits for the copy.
+    struct CopyWait {
+        hipEvent_t e;
+        ~CopyWait() {
+            if (e) (void)hipEventSynchronize(e);
+        }
+    } copy_wait{slot >= 0 ? h->ev_copied[slot] : nullptr};
     if (h->windowed) {   // window_end -> pseudo rowtime (every end on the slice grid)
         HIPCHK(h, h->in_wts.ensure(8 * n + 8));
         unsigned long long* bad = reinterpret_cast<unsigned long long*>(h->in_wts.as<int64_t>() + n);

@@ -44,6 +44,7 @@ constexpr int kDictThreads = 256;
 #ifndef FG_DICT_GROW
 #define FG_DICT_GROW 4   // table rebuilt at FG_DICT_GROW x (ids + chunk) slots (>= 2: at most half full)
 #endif
+static_assert(FG_DICT_GROW >= 2, "FG_DICT_GROW: the table must stay at most half full after a rebuild");
 constexpr int kIdShift = 40;   // id = key group << kIdShift | ordinal
 constexpr uint64_t kOrdMask = (1ull << kIdShift) - 1;
 
@@ -80,6 +81,22 @@ struct DictDev {
     uint64_t mask;       // cap - 1
 };
 
+// one atomic per wave: lane-exclusive offsets of `amount` (0 for a lane that takes nothing)
+// reserved from *ctr; every lane of the wave must call it (inactive lanes count as 0)
+__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* ctr, uint32_t amount) {
+    const int lane = threadIdx.x & 63;
+    uint32_t x = amount;   // inclusive scan over the wave
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    const uint32_t total = __shfl(x, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && total) base = atomicAdd(ctr, (unsigned long long)total);
+    base = __shfl(base, 63);
+    return base + x - amount;
+}
+
 struct RowsIn {
     const uint8_t* bytes;   // 4-byte aligned; every row at a multiple of 4, of 4-byte words
     const int64_t* off;
@@ -90,14 +107,21 @@ struct RowsIn {
     int32_t tag_bits;
 };
 
-// device rows: offsets / lengths checked before anything is inserted (counters[3])
+// arena bytes an entry of a row of `len` bytes takes: [id i64][row bytes, padded to 8]
+__host__ __device__ __forceinline__ uint64_t entry_bytes(int32_t len) { return 8 + (((uint64_t)len + 7) & ~7ull); }
+
+// device rows: offsets / lengths checked before anything is inserted (counters[3]), and the
+// arena bytes the call may take if every row is new (counters[5]: rows may overlap in the
+// caller's buffer, so this is not bounded by its size)
 __global__ __launch_bounds__(kDictThreads) void k_dict_check(RowsIn in, unsigned long long* counters) {
     const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (i >= in.n) return;
-    const int32_t len = in.len[i];
-    const int64_t off = in.off[i];
-    if (len < 0 || len >= (1 << 24) || (len & 3) != 0 || off < 0 || (off & 3) != 0 || off + len > in.nbytes)
-        atomicAdd(&counters[3], 1ull);   // (BinaryRowData rows are 8-byte multiples)
+    const bool valid = i < in.n;
+    const int32_t len = valid ? in.len[i] : 0;
+    const int64_t off = valid ? in.off[i] : 0;
+    const bool bad = valid && (len < 0 || len >= (1 << 24) || (len & 3) != 0 || off < 0 || (off & 3) != 0 ||
+                               off + len > in.nbytes);
+    if (bad) atomicAdd(&counters[3], 1ull);   // (BinaryRowData rows are 8-byte multiples)
+    (void)wave_reserve(&counters[5], valid && !bad ? (uint32_t)entry_bytes(len) : 0u);
 }
 
 // Both hashes of a row in one pass over its 4-byte words: the Flink hash (hashBytesByWords,
@@ -122,22 +146,6 @@ __device__ __forceinline__ void row_hashes(const uint32_t* w, int32_t len, int t
     if (tag_bits < 64) h &= (1ull << tag_bits) - 1;   // diagnostic: force collisions (tests)
     *tag = h ? h : 1;
     *fh = (int32_t)fmix32(h1 ^ (uint32_t)len);
-}
-
-// one atomic per wave: lane-exclusive offsets of `amount` (0 for a lane that takes nothing)
-// reserved from *ctr; every lane of the wave must call it (inactive lanes count as 0)
-__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* ctr, uint32_t amount) {
-    const int lane = threadIdx.x & 63;
-    uint32_t x = amount;   // inclusive scan over the wave
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= off) x += y;
-    }
-    const uint32_t total = __shfl(x, 63);
-    unsigned long long base = 0;
-    if (lane == 63 && total) base = atomicAdd(ctr, (unsigned long long)total);
-    base = __shfl(base, 63);
-    return base + x - amount;
 }
 
 // the id of the entry at `loc` if its row equals the row at w, else -1
@@ -546,19 +554,20 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     const bool host = location == FG_HOST;
     if (!host && (uintptr_t)bytes % 4 != 0)
         return d->fail(FG_EINVAL, "fg_key_dict_intern: the row buffer must be 4-byte aligned");
+    uint64_t entry_need = 0;   // arena bytes if every row is new (rows may overlap in the buffer)
     if (host) {   // validate on the host: every row inside the buffer, 4-byte words
         for (int64_t i = 0; i < n; i++) {
             if (lengths[i] < 0 || lengths[i] >= (1 << 24) || (lengths[i] & 3) || (offsets[i] & 3) || offsets[i] < 0 ||
                 offsets[i] + lengths[i] > nbytes)
                 return d->fail(FG_EINVAL, "key row " + std::to_string(i) +
                                               ": offset/length outside the buffer or not a multiple of 4 bytes");
+            entry_need += entry_bytes(lengths[i]);
         }
     }
     const size_t ents = (size_t)(d->nids + n);
     DCHK(d, d->ent_off.ensure(8 * ents, s, 8 * (size_t)d->nids));
     DCHK(d, d->ent_len.ensure(4 * ents, s, 4 * (size_t)d->nids));
     DCHK(d, d->ent_tag.ensure(8 * ents, s, 8 * (size_t)d->nids));
-    DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)nbytes + 16 * (size_t)n + 16, s, (size_t)d->arena_used));
     RowsIn in{};
     in.n = n;
     in.nbytes = nbytes;
@@ -588,16 +597,19 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     if (!host) {   // device rows are checked on the device before anything is inserted
         hipLaunchKernelGGL(k_dict_check, dim3(g), dim3(kDictThreads), 0, s, in, d->counters.as<unsigned long long>());
         DCHK(d, hipGetLastError());
-        unsigned long long bad = 0;
-        DCHK(d, hipMemcpyAsync(&bad, d->counters.as<unsigned long long>() + 3, 8, hipMemcpyDeviceToHost, s));
+        unsigned long long chk[3] = {0, 0, 0};   // counters[3..5]: bad rows, (pending), entry bytes
+        DCHK(d, hipMemcpyAsync(chk, d->counters.as<unsigned long long>() + 3, sizeof chk, hipMemcpyDeviceToHost, s));
+        DCHK(d, hipMemsetAsync(d->counters.as<unsigned long long>() + 5, 0, 8, s));
+        if (chk[0]) DCHK(d, hipMemsetAsync(d->counters.as<unsigned long long>() + 3, 0, 8, s));
         DCHK(d, hipStreamSynchronize(s));
-        if (bad) {
-            DCHK(d, hipMemsetAsync(d->counters.as<unsigned long long>() + 3, 0, 8, s));
-            DCHK(d, hipStreamSynchronize(s));
-            return d->fail(FG_EINVAL, "fg_key_dict_intern: " + std::to_string(bad) +
+        if (chk[0])
+            return d->fail(FG_EINVAL, "fg_key_dict_intern: " + std::to_string(chk[0]) +
                                           " key rows outside the buffer or not a multiple of 4 bytes");
-        }
+        entry_need = chk[2];
     }
+    // k_dict_assign writes a new row's entry at a reserved arena offset without a bound check:
+    // the arena holds every row of the call as a new entry
+    DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)entry_need + 16, s, (size_t)d->arena_used));
     // Chunks: the table stays at most half full against every row of a chunk being new, so a
     // chunk takes at most the table's headroom; the table grows with the ids (at least
     // kDictChunkMin rows, or as many rows as there are ids, per chunk), not with the call's size
@@ -697,6 +709,8 @@ int fg_key_dict_copy_arena(fg_key_dict* d, int64_t begin, int64_t nbytes, uint8_
 }
 
 int64_t fg_key_dict_size(fg_key_dict* d) { return d ? d->nids : -1; }
+
+void* fg_key_dict_stream(fg_key_dict* d) { return d ? (void*)d->stream : nullptr; }
 
 const char* fg_key_dict_last_error(fg_key_dict* d) { return d ? d->err.c_str() : "null dictionary"; }
 

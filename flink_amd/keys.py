@@ -147,6 +147,12 @@ class KeyDictionary:
         n = len(off)
         if hasattr(buf, "data_ptr"):   # torch device tensors
             import torch
+            # the dictionary reads them on its own stream: order it after their producers
+            ext = self.__dict__.get("_ext_stream")
+            if ext is None or ext.device != buf.device:
+                ext = self._ext_stream = torch.cuda.ExternalStream(self._lib.fg_key_dict_stream(self._h),
+                                                                   device=buf.device)
+            ext.wait_stream(torch.cuda.current_stream(buf.device))
             ids = torch.empty(n, dtype=torch.int64, device=buf.device)
             kg = torch.empty(n, dtype=torch.int32, device=buf.device) if key_groups else None
             self._check(self._lib.fg_key_dict_intern(self._h, L.DEVICE, n, C.c_void_p(buf.data_ptr()), buf.numel(),

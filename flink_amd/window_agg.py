@@ -212,10 +212,22 @@ class WindowAggOperator:
                 b.val_null = val_null.ctypes.data
             keep = [key, rowtime, val, val_null]
         L.check(self._lib.fg_add_batch(self._h, C.byref(b)), self._h)
-        # device columns stay in use until the next call on the handle (the engine may finish
-        # a batch's staging there): hold them until then
+        # device columns stay in use until the work the NEXT call queues on the engine stream
+        # has run (the engine finishes a batch's staging there): hold them until that call, and
+        # tell torch's caching allocator they are used on the engine stream, so that a block
+        # freed afterwards is reused only once the engine stream has passed that point
+        if kdev:
+            self._record_on_engine_stream((key, rowtime, val, val_null))
         self._inflight = (key, rowtime, val, val_null) if kdev else None
         del keep
+
+    def _record_on_engine_stream(self, cols):
+        ext = self.__dict__.get("_ext_stream")
+        if ext is None:
+            return   # not torch tensors (CUDA-array-interface objects): the caller keeps them
+        for c in cols:
+            if c is not None and hasattr(c, "record_stream") and getattr(c, "is_cuda", False):
+                c.record_stream(ext)
 
     def process_rows(self, rows, stride: int, arity: int, key_field: int = 0, rowtime_field: int = 1,
                      val_field: int = 2):

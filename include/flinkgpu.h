@@ -92,9 +92,13 @@ enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AV
 /* FG_DEVICE columns are read on the handle's stream (fg_stream): the caller orders their
  * producer before it (complete, or an event the stream waits on). fg_add_partials and
  * fg_add_rows have read them when they return; fg_add_batch's columns stay in use until the
- * next call on the handle returns (the engine finishes a batch's staging there, so that its
- * two partition passes run back to back on the GPU); fg_synchronize releases them. FG_HOST
- * buffers are copied before the call returns. */
+ * work queued on the handle's stream by the NEXT call on the handle has completed (the engine
+ * finishes a batch's staging in that call, so that its two partition passes run back to back
+ * on the GPU): a caller that frees or reuses them orders that after the handle's stream (an
+ * event recorded on fg_stream after the next call, or fg_synchronize, which releases them).
+ * FG_HOST buffers (pageable or pinned) have been read completely when the call returns: the
+ * caller may overwrite them at once (the H2D copy is complete; the batch's kernels may still
+ * be running on the handle's stream). */
 enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
 /* FG_KEYHASH_DICT_ID: the key is an id of an fg_key_dict (any key type); its key group, computed
  * from the key row's bytes when it was interned, is carried in the id (id >> 40). */
@@ -325,9 +329,11 @@ int  fg_partition_columns_by_owner(int32_t device_id, void* stream, int64_t n, i
 typedef struct fg_key_dict fg_key_dict;
 int  fg_key_dict_open(int32_t device_id, int32_t max_parallelism, int64_t expected_keys, fg_key_dict** out);
 /* n key rows: row i = bytes[offsets[i], offsets[i] + lengths[i]) (nbytes = the buffer's size),
- * each length and offset a multiple of 4 (BinaryRowData rows are multiples of 8). out_id[n]
- * receives the ids, out_kg[n] (optional) the rows' key groups under the dictionary's max
- * parallelism. All pointers FG_HOST or all FG_DEVICE (location). */
+ * each length and offset a multiple of 4 (BinaryRowData rows are multiples of 8; rows may
+ * overlap). out_id[n] receives the ids, out_kg[n] (optional) the rows' key groups under the
+ * dictionary's max parallelism. All pointers FG_HOST or all FG_DEVICE (location). FG_DEVICE
+ * inputs are read on the dictionary's stream (fg_key_dict_stream): the caller orders their
+ * producer before it; the outputs are complete when the call returns. */
 int  fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_t* bytes, int64_t nbytes,
                         const int64_t* offsets, const int32_t* lengths, int64_t* out_id, int32_t* out_kg);
 /* For each id: its row's offset and length in the dictionary's arena (-1 / -1 for an unknown id). */
@@ -337,6 +343,7 @@ int  fg_key_dict_lookup(fg_key_dict* d, int32_t location, int64_t n, const int64
 int  fg_key_dict_arena(fg_key_dict* d, const uint8_t** dev_bytes, int64_t* size);
 int  fg_key_dict_copy_arena(fg_key_dict* d, int64_t begin, int64_t nbytes, uint8_t* host);
 int64_t fg_key_dict_size(fg_key_dict* d);   /* distinct key rows interned */
+void* fg_key_dict_stream(fg_key_dict* d);   /* the dictionary's device stream (hipStream_t) */
 const char* fg_key_dict_last_error(fg_key_dict* d);
 void fg_key_dict_close(fg_key_dict* d);
 /* BinarySection.hashCode of one row (MurmurHashUtils.hashBytesByWords, seed 42); len % 4 == 0. */

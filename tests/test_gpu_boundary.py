@@ -1,0 +1,115 @@
+"""Buffer-ownership contract of the C-ABI (include/flinkgpu.h, fg_location), on the GPU.
+
+The reference's callers reuse their input objects as soon as addElement returns
+(RecordsWindowBuffer.java:81-97 copies each row: `requiresCopy`), and a JNI shim recycles its
+pinned staging ring the same way. These tests overwrite (or free and reallocate) every input
+buffer immediately after the call that consumed it and require the fired rows to still equal
+the oracle's on the original data:
+  * FG_HOST from PINNED host memory (the DMA reads the caller's buffer directly);
+  * FG_DEVICE torch columns dropped right after process_batch (torch's caching allocator
+    hands the blocks to the next allocation on the current stream);
+  * device key rows interned through the key dictionary straight after a producer kernel on
+    torch's stream (the dictionary reads them on its own stream).
+"""
+import numpy as np
+import pytest
+
+from tests.streams import batches_with_watermarks, make_stream
+from tests.test_gpu_parity import assert_rows_equal, oracle_mk
+
+pytestmark = pytest.mark.gpu
+
+CFG = dict(mode="sql", kind="tumble", size=1000, slide=0, offset=0, tz_offset_ms=0, val_type="f64",
+           count_star_index=0)
+
+
+def _drive(O, feed, n=1_200_000, keys=20_000, batch=100_000, jitter=1500, delay=500, cfg=CFG):
+    """feed(g, lo, hi, key, ts, val) hands one batch to the GPU operator g however the test
+    wants; the oracle gets the plain arrays."""
+    from tests.gpu_adapter import GpuOperator
+    key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter)
+    g = GpuOperator(cfg, expected_keys=keys, buffer_records=batch * 4)
+    o = oracle_mk(O, cfg)
+    for step, (lo, hi, wm) in enumerate(batches_with_watermarks(n, batch, ts, delay)):
+        feed(g, lo, hi, key, ts, val)
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], f"step {step}")
+        assert g.late_dropped == o.late_dropped
+    g.process_watermark((1 << 63) - 1)
+    o.process_watermark((1 << 63) - 1)
+    assert_rows_equal(g.take_rows(), o.take_rows(), cfg["val_type"], "final")
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop"])
+def test_pinned_host_batches_overwritten_after_call(oracle_mod, kind):
+    """One pinned buffer set reused for every batch and scribbled over the moment
+    process_batch returns: FG_HOST buffers must have been read completely by then."""
+    import torch
+    cfg = dict(CFG, kind=kind, size=1000 if kind == "tumble" else 4000, slide=0 if kind == "tumble" else 1000)
+    cap = 100_000
+    pk = torch.empty(cap, dtype=torch.int64).pin_memory()
+    pt = torch.empty(cap, dtype=torch.int64).pin_memory()
+    pv = torch.empty(cap, dtype=torch.float64).pin_memory()
+    nk, nt, nv = pk.numpy(), pt.numpy(), pv.numpy()
+    garbage = np.random.default_rng(7)
+
+    def feed(g, lo, hi, key, ts, val):
+        m = hi - lo
+        nk[:m], nt[:m], nv[:m] = key[lo:hi], ts[lo:hi], val[lo:hi]
+        g.process_batch(nk[:m], nt[:m], nv[:m])          # FG_HOST from pinned memory
+        nk[:m] = garbage.integers(0, 1 << 40, m)          # the shim refills its staging slot
+        nt[:m] = garbage.integers(0, 1 << 42, m)
+        nv[:m] = np.nan
+
+    _drive(oracle_mod, feed, cfg=cfg)
+
+
+def test_device_columns_freed_after_call(oracle_mod):
+    """Device columns dropped right after process_batch; the next allocations on torch's
+    stream (same sizes, so the caching allocator offers the same blocks) are filled with
+    garbage at once. record_stream on the engine's stream keeps the blocks until the engine
+    has read them (fg_add_batch finishes a batch's staging in the next call)."""
+    import torch
+
+    def feed(g, lo, hi, key, ts, val):
+        k = torch.from_numpy(key[lo:hi]).cuda()
+        t = torch.from_numpy(ts[lo:hi]).cuda()
+        v = torch.from_numpy(val[lo:hi]).cuda()
+        g.process_batch(k, t, v)
+        del k, t, v
+        junk = [torch.full((hi - lo,), -7, dtype=torch.int64, device="cuda") for _ in range(3)]
+        del junk
+
+    _drive(oracle_mod, feed)
+
+
+def test_dictionary_reads_device_rows_after_their_producer():
+    """Key rows written by a torch kernel and interned at once: the dictionary's stream must
+    wait for torch's stream (fg_key_dict_stream), or it hashes unwritten bytes."""
+    import torch
+
+    from flink_amd.keys import KeyDictionary, key_row, pack_key_rows
+    rows = [key_row([f"user-{i:07d}"], ["string"]) for i in range(50_000)]
+    buf, off, ln = pack_key_rows(rows)
+    from oracle import oracle as O
+    exp_kg = np.array([O.key_group_of_row(r, 128) for r in rows[:2000]], dtype=np.int32)
+    d = KeyDictionary(expected_keys=1 << 16)
+    first = None
+    for rep in range(3):
+        src = torch.from_numpy(buf.copy()).cuda()
+        dst = torch.zeros_like(src)
+        torch.cuda._sleep(20_000_000)   # keep torch's stream busy so an unordered read sees zeros
+        dst.copy_(src)
+        ids, kg = d.intern(packed=(dst, torch.from_numpy(off).cuda(), torch.from_numpy(ln).cuda()))
+        ids, kg = ids.cpu().numpy(), kg.cpu().numpy()
+        assert np.array_equal(kg[:2000], exp_kg), f"rep {rep}: key groups differ"
+        assert len(np.unique(ids)) == len(rows), f"rep {rep}: distinct rows share ids"
+        if first is None:
+            first = ids
+        assert np.array_equal(ids, first), f"rep {rep}: ids not stable"
+    assert len(d) == len(rows)
+    d.close()
