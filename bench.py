@@ -72,11 +72,14 @@ WORKLOADS = {
                 zipf=0.0, batch=25_000_000, desc="SQL HOP 5min/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 30 event-minutes, "
                                "10M uniform keys (BASELINE configs[2])"),
     # configs[3]: CUMULATE 1h/1min over 60 event-minutes; 100M keys sharded over 8 GPUs ->
-    # the per-GPU share (12.5M) at N = 1, the whole 100M space at N = 8
-    "cumulate": dict(window=("cumulative", 3_600_000, 60_000), keys=12_500_000, rate=1_000_000_000 // 3600,
+    # the key space is 12.5M per GPU: the per-GPU share at N = 1, the whole 100M space at N = 8
+    # (keys_per_gpu: main() multiplies by the world size)
+    "cumulate": dict(window=("cumulative", 3_600_000, 60_000), keys=12_500_000, keys_per_gpu=True,
+                     rate=1_000_000_000 // 3600,
                      jitter=0, delay=0, zipf=0.0, batch=16_666_667,
                      desc="SQL CUMULATE 1h/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 60 event-minutes, "
-                          "uniform keys: 12.5M per GPU = the per-GPU key-group share of 100M (BASELINE configs[3])"),
+                          "uniform keys: 12.5M x N GPUs (100M at N = 8, each GPU owning a 12.5M key-group share; "
+                          "BASELINE configs[3])"),
     # configs[0]: DataStream keyBy().window(TumblingEventTimeWindows 1s).sum on (long key,
     # long val), 10M records, 10k keys, 1M records per event-second, watermark every 10k
     "datastream": dict(window=("tumbling", 1000), keys=10_000, rate=1_000_000, jitter=0, delay=0, zipf=0.0,
@@ -113,9 +116,12 @@ def zipf_cdf(keys, s, device):
     return torch.from_numpy(c / c[-1]).to(device)
 
 
-def gen_columns(n, keys, rate_s, base_index, device, chunk=1 << 26, jitter=0, zipf=0.0):
+def gen_columns(n, keys, rate_s, base_index, device, chunk=1 << 26, jitter=0, zipf=0.0, t_base=None):
     """key = u % keys (or Zipf(zipf) rank - 1 by inverse CDF), val = uniform [0, 1000) f64,
-    rowtime = T0 + i * 1000 // rate_s (+ U[0, jitter) ms) (tests/streams.py)."""
+    rowtime = T0 + (i - t_base) * 1000 // rate_s (+ U[0, jitter) ms) for the records
+    i = base_index .. base_index + n - 1 of the stream (t_base: base_index) (tests/streams.py)."""
+    if t_base is None:
+        t_base = base_index
     key = torch.empty(n, dtype=torch.int64, device=device)
     ts = torch.empty(n, dtype=torch.int64, device=device)
     val = torch.empty(n, dtype=torch.float64, device=device)
@@ -132,7 +138,7 @@ def gen_columns(n, keys, rate_s, base_index, device, chunk=1 << 26, jitter=0, zi
         else:
             key[lo:hi] = (lsr(u, 1) % keys * 2 + (u & 1)) % keys        # unsigned u % keys
         val[lo:hi] = lsr(u2, 11).to(torch.float64) * (1000.0 / float(1 << 53))
-        ts[lo:hi] = T0 + (i - base_index) * 1000 // rate_s
+        ts[lo:hi] = T0 + (i - t_base) * 1000 // rate_s
         if jitter:
             ts[lo:hi] += lsr(u2, 1) % jitter
         del i, u, u2
@@ -264,14 +270,15 @@ def lib_sha256():
 
 def pmc_traffic(kernel_class):
     """HBM bytes per launch of `kernel_class` from the newest committed rocprofv3 PMC summary
-    (profiles/*/pmc_traffic.json, profiles/pmc_summary.py) -- only if it was counted on THIS
+    (profiles/**/pmc_traffic.json, profiles/pmc_summary.py) -- only if it was counted on THIS
     library build (same sha256 of libflinkgpu.so); otherwise None. Returns (bytes, source)."""
     import glob
     try:
         sha = lib_sha256()
     except OSError:
         return None, None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True),
+                       reverse=True):
         try:
             d = json.load(open(path))
         except Exception:
@@ -301,38 +308,55 @@ def h2d_link_peak(dev, nbytes=1 << 30, reps=4):
 
 
 def h2d_leg(args, wl, window, aggs, expected_keys, dev):
-    """The bench workload's first `h2d_records` records as pinned host columns (FG_HOST):
-    whole-job rate including PCIe, the link bytes, and the link's measured pinned H2D rate."""
+    """SURVEY.md 8(d)'s contract timing: the kernels PLUS the H2D of columnar batches from
+    pinned host memory. The whole configs[1] job (`h2d_records`, default all 1B records) as
+    pinned host columns handed over as FG_HOST batches: whole-job rate including PCIe, the link
+    bytes, and the link's measured pinned H2D rate."""
     import flink_amd as F
     n = args.h2d_records - args.h2d_records % args.batch or args.batch
-    key, ts, val = gen_columns(n, args.keys, args.rate, 0, dev, jitter=wl["jitter"], zipf=wl["zipf"])
-    hk, ht, hv = (x.cpu().pin_memory() for x in (key, ts, val))
-    del key, ts, val
+    hk = torch.empty(n, dtype=torch.int64).pin_memory()
+    ht = torch.empty(n, dtype=torch.int64).pin_memory()
+    hv = torch.empty(n, dtype=torch.float64).pin_memory()
+    chunk = 1 << 27
+    for lo in range(0, n, chunk):   # generated on the GPU, copied into the pinned columns
+        hi = min(n, lo + chunk)
+        k, t, v = gen_columns(hi - lo, args.keys, args.rate, lo, dev, jitter=wl["jitter"], zipf=wl["zipf"], t_base=0)
+        hk[lo:hi].copy_(k)
+        ht[lo:hi].copy_(t)
+        hv[lo:hi].copy_(v)
+        del k, t, v
+    torch.cuda.synchronize()
     torch.cuda.empty_cache()
     op = F.WindowAggOperator(window, aggs=aggs, val_type="f64", expected_keys=expected_keys,
                              buffer_records=max(4 * args.batch, 1 << 26), device=dev.index)
 
     def run():
         op.reset()
+        rows = 0
         for lo in range(0, n, args.batch):
             hi = min(n, lo + args.batch)
             op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi])
             for wm in watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"]):
-                op.process_watermark(wm, device_output=True)
-        op.process_watermark(JMAX, device_output=True)
+                rows += op.process_watermark(wm, device_output=True).n
+        rows += op.process_watermark(JMAX, device_output=True).n
         op.synchronize()
+        return rows
     run()   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run()
+    rows = run()
     el = time.perf_counter() - t0
     op.close()
+    del hk, ht, hv
     link = h2d_link_peak(dev)
     gbs = 24 * n / el / 1e9
-    return {"value": n / el, "unit": "records/s", "records": n, "seconds": el, "pcie_gbs": gbs,
-            "link_peak_gbs": link, "link_frac": gbs / link if link else None,
-            "note": "pinned host columns handed over as FG_HOST batches (double-buffered H2D on the engine's "
-                    "copy stream, overlapping the kernels); secondary -- `value` has the inputs resident in HBM"}
+    return {"value": n / el, "unit": "records/s", "records": n, "rows_fired": rows, "seconds": el,
+            "pcie_gbs": gbs, "link_peak_gbs": link, "link_frac": gbs / link if link else None,
+            "job_roofline_frac": (24 * n + 48 * rows) / el / (HBM_PEAK_GBS * 1e9),
+            "note": "SURVEY 8(d) contract timing (kernels + H2D of columnar batches from pinned host memory): the "
+                    "configs[1] job as FG_HOST batches (double-buffered H2D on the engine's copy stream, "
+                    "overlapping the kernels; each call returns once its batch is copied). `value` is the "
+                    "kernel pipeline with the inputs resident in HBM"}
 
 
 def main():
@@ -367,11 +391,12 @@ def main():
                     help="N > 1: exchange partial accumulators (two-phase) or raw records")
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="CPU baseline instances (default: min(85, CPUs in this process's affinity mask))")
-    ap.add_argument("--h2d-records", type=int, default=200_000_000,
-                    help="records of the secondary pinned-host leg (FG_HOST batches, double-buffered H2D "
-                         "overlapping the kernels); 0 skips it. Never the headline value")
+    ap.add_argument("--h2d-records", type=int, default=1_000_000_000,
+                    help="records of the pinned-host leg (SURVEY 8(d) contract timing: FG_HOST batches, "
+                         "double-buffered H2D overlapping the kernels); 0 skips it. Never the headline value")
     args = ap.parse_args()
     wl = WORKLOADS[args.workload]
+    keys_default = args.keys is None
     if args.keys is None:
         args.keys = wl["keys"]
     if args.rate is None:
@@ -393,6 +418,8 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if keys_default and wl.get("keys_per_gpu"):   # configs[3]: 12.5M keys per GPU, 100M at N = 8
+        args.keys *= world
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = int(os.environ.get("BENCH_DEVICE", local))   # rehearsal: every rank on one device
     torch.cuda.set_device(local)
@@ -425,6 +452,11 @@ def main():
         row_off = torch.arange(args.batch, dtype=torch.int64, device=dev) * 32
         row_len = torch.full((args.batch,), 32, dtype=torch.int32, device=dev)
         kdict = F.KeyDictionary(max_parallelism=128, expected_keys=int(args.keys * 1.05), device=local)
+        kdict.set_timing(True)   # the dictionary's kernels are timed on its own stream
+        if world > 1 and args.exchange == "raw":
+            # a rank's dictionary ids are its own: records would have to carry their key rows;
+            # the two-phase plan ships each partial row's key row (exchange_partials key_rows)
+            raise SystemExit("--workload strings at N > 1 runs the two-phase plan (--exchange partials)")
     from flink_amd import _lib as FL
     key_hash = FL.KEYHASH_DICT_ID if strings else FL.KEYHASH_BINARYROW_BIGINT
     torch.cuda.synchronize()
@@ -454,13 +486,19 @@ def main():
                                    buffer_records=max(4 * args.batch, 1 << 26), device=local,
                                    kernel_timing=True, local_partials=True) if two_phase else None
 
+    # STRING keys over the exchange: the owner's dictionary interns the key rows the partial
+    # rows carry (a rank's local ids mean nothing elsewhere)
+    kdict_owner = F.KeyDictionary(max_parallelism=128, expected_keys=int(args.keys / world * 1.05) + 1,
+                                  device=local) if strings and two_phase else None
+
     def partials_round(wm):
         """local fire -> exchange of partial accumulators -> global merge + fire"""
         r = op_local.process_watermark(wm, device_output=True)
         # key, slice end, COUNT(*), COUNT(v), SUM (+ MIN, MAX for several value accumulators)
         cols = device_columns(r, aggs=tuple(range(len(op_local.aggs))), device=dev)
-        recv, sent = exchange_partials(cols, max_parallelism=maxp, key_hash=key_hash, via_cpu=via_cpu)
-        torch.cuda.current_stream().synchronize()
+        recv, sent = exchange_partials(cols, max_parallelism=maxp, key_hash=key_hash, via_cpu=via_cpu,
+                                       key_rows=(kdict, kdict_owner) if kdict_owner else None)
+        # (process_partials orders the engine's stream after torch's: no host synchronization)
         op.process_partials(*recv)
         g = op.process_watermark(global_watermark(wm, device=dev), device_output=True)
         return g.n, sent
@@ -527,6 +565,8 @@ def main():
         if op_local:   # local-phase kernels under their own names
             for name, d in op_local.kernel_stats().items():
                 ks["local_" + name] = d
+        if kdict is not None:   # the dictionary's kernels, timed on its stream
+            ks.update(kdict.kernel_stats())
         return ks
 
     for _ in range(args.warmup):
@@ -539,7 +579,8 @@ def main():
     dom_class = max(warm.items(), key=lambda kv: kv[1]["total_ms"])[0] if warm else None
     if dom_class and args.warmup > 0:
         is_local = dom_class.startswith("local_")
-        op.set_kernel_timing([] if is_local else [dom_class])
+        is_dict = dom_class.startswith("dict_")   # the dictionary keeps its own (per-chunk) events
+        op.set_kernel_timing([] if is_local or is_dict else [dom_class])
         if op_local is not None:
             op_local.set_kernel_timing([dom_class[len("local_"):]] if is_local else [])
     before = kstats()
@@ -580,7 +621,9 @@ def main():
         ks = {"untimed": dict(launches=1, total_ms=float("nan"), records=0, rows=0)}
     dom_name, dom = max(ks.items(), key=lambda kv: kv[1]["total_ms"])
     avg_s = dom["total_ms"] / dom["launches"] / 1e3
-    alg_bytes = (24 * dom["records"] + 48 * dom["rows"]) / dom["launches"]
+    # algorithmic bytes: 24 B per input record + 48 B per fired row; the key
+    # dictionary's probe: the 32-B key row read + the 8-B id written per row
+    alg_bytes = ((40 if dom_name.startswith("dict_") else 24) * dom["records"] + 48 * dom["rows"]) / dom["launches"]
     achieved = alg_bytes / avg_s / 1e9
     traffic, traffic_src = pmc_traffic(dom_name)
 
@@ -649,6 +692,8 @@ def main():
     if kdict is not None:
         result["key_dictionary"] = {"distinct_keys": len(kdict), "row_bytes": 32}
         kdict.close()
+    if kdict_owner is not None:
+        kdict_owner.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -96,7 +96,8 @@ EXPORTS = (
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
     "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
-    "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_stream", "fg_key_dict_last_error", "fg_key_dict_close",
+    "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_stream", "fg_key_dict_set_timing",
+    "fg_key_dict_kernel_stats", "fg_key_dict_last_error", "fg_key_dict_close",
     "fg_binaryrow_hash",
 )
 
@@ -163,6 +164,10 @@ def load():
     L.fg_key_dict_copy_arena.argtypes = [P, C.c_int64, C.c_int64, P]
     L.fg_key_dict_size.argtypes = [P]
     L.fg_key_dict_size.restype = C.c_int64
+    L.fg_key_dict_set_timing.argtypes = [P, C.c_int32]
+    L.fg_key_dict_set_timing.restype = C.c_int
+    L.fg_key_dict_kernel_stats.argtypes = [P, C.POINTER(FgKernelStat), C.c_int32, C.POINTER(C.c_int32)]
+    L.fg_key_dict_kernel_stats.restype = C.c_int
     L.fg_key_dict_stream.argtypes = [P]
     L.fg_key_dict_stream.restype = P
     L.fg_key_dict_last_error.argtypes = [P]

@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -405,6 +406,11 @@ struct fg_key_dict {
     Buf in_bytes, in_off, in_len, row_tag, row_kg, row_slot, row_pkg, row_id;   // per-call scratch
     std::unordered_map<std::string, int64_t> side;   // rows whose tag another row holds
     std::string err;
+    // kernel timing (fg_key_dict_set_timing): HIP events around each chunk's probe and its
+    // assign + verify, on the dictionary's stream; summed into the two classes below
+    bool timing = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    fg_kernel_stat kstat[2] = {};
 
     int fail(int rc, const std::string& m) {
         err = m;
@@ -641,15 +647,29 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
         const DictDev dv = d->dev();
         const unsigned gm = grid_of(m);
         DCHK(d, hipMemsetAsync(dv.counters + 4, 0, 8, s));
+        if (d->timing) DCHK(d, hipEventRecord(d->ev[0], s));
         hipLaunchKernelGGL(k_dict_probe, dim3(gm), dim3(kDictThreads), 0, s, dv, c, kg_dev ? kg_dev + pos : nullptr,
                            cids, pend);
+        if (d->timing) DCHK(d, hipEventRecord(d->ev[1], s));
         const unsigned gp = std::min(gm, 1024u);   // the pending list is short in a steady state
         hipLaunchKernelGGL(k_dict_assign, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend);
         hipLaunchKernelGGL(k_dict_verify, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend, cids);
+        if (d->timing) DCHK(d, hipEventRecord(d->ev[2], s));
         DCHK(d, hipGetLastError());
         unsigned long long cnt[5];
         DCHK(d, hipMemcpyAsync(cnt, d->counters.p, sizeof cnt, hipMemcpyDeviceToHost, s));
         DCHK(d, hipStreamSynchronize(s));
+        if (d->timing) {
+            float ms0 = 0.f, ms1 = 0.f;
+            DCHK(d, hipEventElapsedTime(&ms0, d->ev[0], d->ev[1]));
+            DCHK(d, hipEventElapsedTime(&ms1, d->ev[1], d->ev[2]));
+            d->kstat[0].launches++;
+            d->kstat[0].total_ms += ms0;
+            d->kstat[0].records += m;
+            d->kstat[1].launches++;
+            d->kstat[1].total_ms += ms1;
+            d->kstat[1].records += (int64_t)cnt[4];   // pending rows
+        }
         d->nids = (int64_t)cnt[0];
         d->arena_used = (int64_t)cnt[1];
         if (cnt[2])
@@ -712,6 +732,25 @@ int64_t fg_key_dict_size(fg_key_dict* d) { return d ? d->nids : -1; }
 
 void* fg_key_dict_stream(fg_key_dict* d) { return d ? (void*)d->stream : nullptr; }
 
+int fg_key_dict_set_timing(fg_key_dict* d, int32_t on) {
+    if (!d) return FG_EINVAL;
+    if (on && !d->ev[0]) {
+        if (hipSetDevice(d->device) != hipSuccess) return d->fail(FG_EDEVICE, "hipSetDevice failed");
+        for (auto& e : d->ev) DCHK(d, hipEventCreate(&e));
+        std::snprintf(d->kstat[0].name, sizeof d->kstat[0].name, "dict_probe");
+        std::snprintf(d->kstat[1].name, sizeof d->kstat[1].name, "dict_assign");
+    }
+    d->timing = on != 0;
+    return FG_OK;
+}
+
+int fg_key_dict_kernel_stats(fg_key_dict* d, fg_kernel_stat* out, int32_t max, int32_t* count) {
+    if (!d || !count || (max > 0 && !out)) return FG_EINVAL;
+    *count = d->ev[0] ? 2 : 0;
+    for (int i = 0; i < *count && i < max; i++) out[i] = d->kstat[i];
+    return FG_OK;
+}
+
 const char* fg_key_dict_last_error(fg_key_dict* d) { return d ? d->err.c_str() : "null dictionary"; }
 
 void fg_key_dict_close(fg_key_dict* d) {
@@ -719,6 +758,8 @@ void fg_key_dict_close(fg_key_dict* d) {
     (void)hipSetDevice(d->device);
     hipStream_t s = d->stream;
     if (s) (void)hipStreamSynchronize(s);
+    for (auto e : d->ev)
+        if (e) (void)hipEventDestroy(e);
     delete d;
     if (s) (void)hipStreamDestroy(s);
 }

@@ -116,24 +116,88 @@ def partition_columns_by_owner(cols, parallelism: int, max_parallelism: int = 12
 
 
 def exchange_partials(cols, group=None, max_parallelism: int = 128, key_hash: int = L.KEYHASH_BINARYROW_BIGINT,
-                      via_cpu: bool = False):
+                      via_cpu: bool = False, key_rows=None):
     """Key-group exchange of partial accumulator rows (int64 device columns, key first).
-    Returns the received columns and the bytes this rank sent to peers. via_cpu stages the
-    collective through host memory (gloo; for rehearsing N > 1 on one device)."""
+    Returns the received columns and the bytes this rank sent to peers.
+
+    Per call: the owner partition (a device counting sort), ONE all-to-all of the per-peer
+    counts, one host read of them (the split sizes of the next collective), ONE all-to-all of
+    the rows packed [n, c] (and, with key_rows, one of the key rows' words).
+
+    key_rows = (local, owner) dictionaries (flink_amd.keys.KeyDictionary, or any objects with
+    the same `locate` / `intern_rows` methods): the key column holds ids of this rank's `local`
+    dictionary, which mean nothing on another rank, so each partial row travels with its key
+    row's bytes -- as the reference's LocalAggCombiner emits the key BinaryRowData itself
+    (LocalAggCombiner.java:100-106) -- and the owner interns them into its `owner` dictionary:
+    the received key column holds owner ids. Routing is by the id's key group, which is the key
+    row's (FG_KEYHASH_DICT_ID: computed from the bytes, the same on every rank).
+
+    via_cpu stages the collectives through host memory (gloo; for rehearsing N > 1 on one
+    device, and the CPU tests)."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    if key_rows is not None:
+        key_hash = L.KEYHASH_DICT_ID
     outs, counts = partition_columns_by_owner(cols, world, max_parallelism, key_hash)
-    if world == 1:
+    if world == 1 and key_rows is None:
         return outs, 0
-    dev = cols[0].device
-    if via_cpu:   # gloo rehearsal: staged through host memory
-        outs, counts = [o.cpu() for o in outs], counts.cpu()
-    # one all-to-all per column, straight from the partitioned columns into the received ones
-    # (no [n, c] packing copy before the collective, no column split after it)
-    recv, sent_bytes = exchange_columns(outs, counts, group)
+    return exchange_grouped_columns(outs, counts, group, via_cpu=via_cpu, key_rows=key_rows)
+
+
+def exchange_grouped_columns(outs, counts, group=None, via_cpu: bool = False, key_rows=None):
+    """The collective step of exchange_partials: int64 columns already grouped by destination
+    rank (counts[d] rows for rank d; device tensors, or host tensors with gloo)."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    cols = outs
+    words = None
+    if key_rows is not None:
+        local, owner = key_rows
+        woff, nw, arena = local.locate(outs[0])          # the key rows of the local ids
+        ends = torch.cumsum(counts, 0)
+        cw = torch.cumsum(nw, 0)
+        at = torch.cat([torch.zeros(1, dtype=cw.dtype, device=cw.device), cw])
+        wcounts = at[ends] - at[torch.cat([torch.zeros(1, dtype=ends.dtype, device=ends.device), ends[:-1]])]
+        outs = outs + [nw]                                # row lengths (words) travel as a column
+        counts_all = torch.stack([counts, wcounts], dim=1)
+    else:
+        counts_all = counts.view(world, 1)
+    packed = torch.stack(outs, dim=1)                     # [n, c]: one collective for every column
     if via_cpu:
-        recv = [r.to(dev) for r in recv]
-    return recv, sent_bytes
+        packed, counts_all = packed.cpu(), counts_all.cpu()
+    recv_counts = torch.empty_like(counts_all)
+    dist.all_to_all_single(recv_counts, counts_all, group=group)
+    sc, rc = counts_all.cpu(), recv_counts.cpu()          # the one host read per exchange
+    send, recv = sc[:, 0].tolist(), rc[:, 0].tolist()
+    out = torch.empty((sum(recv), packed.shape[1]), dtype=packed.dtype, device=packed.device)
+    dist.all_to_all_single(out, packed, output_split_sizes=recv, input_split_sizes=send, group=group)
+    rank = dist.get_rank(group)
+    sent_bytes = 8 * packed.shape[1] * (sum(send) - send[rank])
+    if key_rows is not None:
+        wsend, wrecv = sc[:, 1].tolist(), rc[:, 1].tolist()
+        total = sum(wsend)
+        # word index of every row's bytes in the arena: row i's words woff[i] .. woff[i] + nw[i]
+        rep = torch.repeat_interleave(torch.arange(len(nw), device=nw.device), nw, output_size=total)
+        first = torch.cumsum(nw, 0) - nw
+        idx = woff[rep] + (torch.arange(total, device=nw.device) - first[rep])
+        words = arena[idx]
+        if via_cpu:
+            words = words.cpu()
+        rwords = torch.empty(sum(wrecv), dtype=words.dtype, device=words.device)
+        dist.all_to_all_single(rwords, words, output_split_sizes=wrecv, input_split_sizes=wsend, group=group)
+        sent_bytes += 4 * (total - wsend[rank])
+    cols_out = list(out.unbind(1))
+    if via_cpu:
+        dev = cols[0].device
+        cols_out = [c.to(dev) for c in cols_out]
+        if words is not None:
+            rwords = rwords.to(dev)
+    cols_out = [c.contiguous() for c in cols_out]
+    if key_rows is not None:
+        rlen = cols_out.pop() * 4                          # bytes per received row
+        roff = torch.cumsum(rlen, 0) - rlen
+        cols_out[0] = owner.intern_rows(rwords.view(torch.uint8), roff, rlen.to(torch.int32))
+    return cols_out, sent_bytes
 
 
 def exchange_columns(cols, counts, group=None):

@@ -170,6 +170,40 @@ class KeyDictionary:
                                                  C.c_void_p(kg.ctypes.data if key_groups else None)))
         return ids, kg
 
+    def intern_rows(self, data, offsets, lengths):
+        """ids (device int64 tensor) of the key rows in device tensors: data uint8, offsets
+        int64, lengths int32 (flink_amd.exchange's receiving side of key rows)."""
+        ids, _ = self.intern(packed=(data, offsets, lengths), key_groups=False)
+        return ids
+
+    def locate(self, ids):
+        """Where the key rows of device ids live: (word offsets int64, words int64, arena) with
+        arena an int32 device tensor view of the dictionary's arena (valid until the next
+        intern on this dictionary); row i = arena[woff[i] : woff[i] + nw[i]]."""
+        import torch
+        n = ids.numel()
+        off = torch.empty(n, dtype=torch.int64, device=ids.device)
+        ln = torch.empty(n, dtype=torch.int32, device=ids.device)
+        if n:
+            ext = self.__dict__.get("_ext_stream")
+            if ext is None or ext.device != ids.device:
+                ext = self._ext_stream = torch.cuda.ExternalStream(self._lib.fg_key_dict_stream(self._h),
+                                                                   device=ids.device)
+            ext.wait_stream(torch.cuda.current_stream(ids.device))
+            self._check(self._lib.fg_key_dict_lookup(self._h, L.DEVICE, n, C.c_void_p(ids.data_ptr()),
+                                                     C.c_void_p(off.data_ptr()), C.c_void_p(ln.data_ptr())))
+            if bool((ln < 0).any()):
+                raise KeyError("unknown dictionary id in locate()")
+        p = C.c_void_p()
+        size = C.c_int64()
+        self._check(self._lib.fg_key_dict_arena(self._h, C.byref(p), C.byref(size)))
+
+        class _Arena:   # zero-copy view for torch.as_tensor
+            __cuda_array_interface__ = {"shape": (max(int(size.value) // 4, 1),), "typestr": "<i4",
+                                        "data": (int(p.value or 0), False), "version": 2}
+        arena = torch.as_tensor(_Arena(), device=ids.device)
+        return off // 4, (ln // 4).to(torch.int64), arena
+
     def lookup(self, ids):
         """Key rows (bytes) of the ids (host)."""
         ids = np.ascontiguousarray(ids, dtype=np.int64)
@@ -186,6 +220,18 @@ class KeyDictionary:
         self._check(self._lib.fg_key_dict_copy_arena(self._h, lo, hi - lo, arena.ctypes.data))
         raw = arena.tobytes()
         return [raw[o - lo:o - lo + n_] for o, n_ in zip(off.tolist(), ln.tolist())]
+
+    def set_timing(self, on: bool = True):
+        """HIP-event timing of the dictionary's kernels (kernel_stats)."""
+        self._check(self._lib.fg_key_dict_set_timing(self._h, 1 if on else 0))
+
+    def kernel_stats(self) -> dict:
+        """{"dict_probe" | "dict_assign": dict(launches, total_ms, records, rows)}."""
+        arr = (L.FgKernelStat * 4)()
+        n = C.c_int32()
+        self._check(self._lib.fg_key_dict_kernel_stats(self._h, arr, 4, C.byref(n)))
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms,
+                                           records=arr[i].records, rows=arr[i].rows) for i in range(n.value)}
 
     def __len__(self):
         return int(self._lib.fg_key_dict_size(self._h))

@@ -344,6 +344,10 @@ int  fg_key_dict_arena(fg_key_dict* d, const uint8_t** dev_bytes, int64_t* size)
 int  fg_key_dict_copy_arena(fg_key_dict* d, int64_t begin, int64_t nbytes, uint8_t* host);
 int64_t fg_key_dict_size(fg_key_dict* d);   /* distinct key rows interned */
 void* fg_key_dict_stream(fg_key_dict* d);   /* the dictionary's device stream (hipStream_t) */
+/* HIP-event timing of the dictionary's kernels (per chunk: "dict_probe", then "dict_assign" =
+ * assign + verify of the rows new in the chunk); fg_key_dict_kernel_stats copies them. */
+int  fg_key_dict_set_timing(fg_key_dict* d, int32_t on);
+int  fg_key_dict_kernel_stats(fg_key_dict* d, fg_kernel_stat* out, int32_t max, int32_t* count);
 const char* fg_key_dict_last_error(fg_key_dict* d);
 void fg_key_dict_close(fg_key_dict* d);
 /* BinarySection.hashCode of one row (MurmurHashUtils.hashBytesByWords, seed 42); len % 4 == 0. */

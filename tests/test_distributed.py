@@ -209,3 +209,145 @@ def test_two_phase_exchange_matches_single_operator(oracle_mod, kind, columns):
     ok = e["sum_null"] == 0
     assert np.allclose(g["sum_d"][ok], e["sum_d"][ok], rtol=1e-9, atol=0)
     assert sum(late for _, _, late, _ in res) > 0
+
+
+# ---- STRING keys over the two-phase exchange -------------------------------------------------
+class HostKeyDict:
+    """A dictionary of key rows with the KeyDictionary interface exchange_partials uses
+    (locate / intern_rows), on the host: ids = key group << 40 | ordinal in THIS dictionary's
+    first-seen order, so two ranks' ids for one key differ, as the GPU dictionaries' do."""
+
+    def __init__(self, max_parallelism=MAXP):
+        self.maxp = max_parallelism
+        self.rows, self.ids = [], {}
+
+    def intern_bytes(self, row: bytes) -> int:
+        from oracle import oracle as O
+        i = self.ids.get(row)
+        if i is None:
+            i = O.key_group_of_row(row, self.maxp) << 40 | len(self.rows)
+            self.ids[row] = i
+            self.rows.append(row)
+        return i
+
+    def row_of(self, i: int) -> bytes:
+        return self.rows[i & ((1 << 40) - 1)]
+
+    def locate(self, ids):
+        import torch
+        blob = b"".join(self.rows)
+        starts = np.cumsum([0] + [len(r) for r in self.rows])
+        ords = ids.numpy() & ((1 << 40) - 1)
+        woff = torch.from_numpy((starts[ords] // 4).astype(np.int64))
+        nw = torch.from_numpy(np.array([len(self.rows[o]) // 4 for o in ords], dtype=np.int64))
+        return woff, nw, torch.from_numpy(np.frombuffer(blob or b"\0" * 4, dtype=np.int32).copy())
+
+    def intern_rows(self, data, offsets, lengths):
+        import torch
+        b = data.numpy().tobytes()
+        return torch.from_numpy(np.array([self.intern_bytes(b[o:o + n]) for o, n in
+                                          zip(offsets.tolist(), lengths.tolist())], dtype=np.int64))
+
+
+def _string_rows(key):
+    from flink_amd.keys import key_row
+    return [key_row([f"name-{int(k):05d}" + "x" * (int(k) % 13)], ["string"]) for k in key]
+
+
+def _two_phase_strings_rank(rank, world, port, out_q):
+    import torch
+    import torch.distributed as dist
+
+    from flink_amd.exchange import exchange_grouped_columns, global_watermark
+    from oracle import oracle as O
+    from tests.streams import make_stream
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    k_, size, slide, jitter = TP_KINDS["hop"]
+    n = TP_N // 3
+    key, ts, val, isnull = make_stream(n, 1500, "f64", seed=3000 + rank, jitter_ms=jitter, null_frac=0.1,
+                                       rate_per_ms=TP_RATE)
+    local_d, owner_d = HostKeyDict(), HostKeyDict()
+    if rank == 1:   # first-seen order differs between the ranks: their local ids disagree
+        for r in _string_rows(np.arange(1499, -1, -7)):
+            local_d.intern_bytes(r)
+    ids = np.array([local_d.intern_bytes(r) for r in _string_rows(key)], dtype=np.int64)
+    local = O.OracleOperator(kind=k_, size=size, slide=slide, phase=O.PHASE_LOCAL)
+    glob = O.OracleOperator(kind=k_, size=size, slide=slide, phase=O.PHASE_GLOBAL)
+    rows = []
+    mx = -(1 << 63)
+
+    def round_(local_wm):
+        local.process_watermark(local_wm)
+        part = local.take_rows()
+        kg = (part["key"].view(np.uint64) >> np.uint64(40)).astype(np.int64) % MAXP   # FG_KEYHASH_DICT_ID
+        owner = kg * world // MAXP
+        part = part[np.argsort(owner, kind="stable")]
+        counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
+        words = part.view(np.int64).reshape(len(part), O.ROW_DTYPE.itemsize // 8)
+        cols = [torch.from_numpy(np.ascontiguousarray(words[:, j])) for j in range(words.shape[1])]
+        recv, _ = exchange_grouped_columns(cols, counts, key_rows=(local_d, owner_d))
+        got = np.ascontiguousarray(torch.stack(recv, dim=1).numpy()).view(O.ROW_DTYPE).reshape(-1)
+        glob.process_partials(got)
+        glob.process_watermark(global_watermark(local_wm))
+        r = glob.take_rows()
+        rows.append([(owner_d.row_of(int(x["key"])), int(x["window_end"]), int(x["cnt_star"]), int(x["cnt_val"]),
+                      float(x["sum_d"]), int(x["sum_null"])) for x in r])
+
+    for lo in range(0, n, TP_BATCH):
+        hi = lo + TP_BATCH
+        local.process_batch(ids[lo:hi], ts[lo:hi], val[lo:hi], isnull[lo:hi])
+        mx = max(mx, int(ts[lo:hi].max()))
+        round_(mx - TP_DELAY)
+    round_((1 << 63) - 1)
+    out_q.put((rank, [x for r in rows for x in r], glob.late_dropped))
+    dist.destroy_process_group()
+
+
+def test_two_phase_string_keys_travel_as_key_rows(oracle_mod):
+    """STRING keys (BinaryRowData key rows) over the two-phase exchange: each rank's local
+    dictionary ids are its own (different first-seen orders), so partial rows carry their key
+    rows' bytes and the owner interns them (exchange_partials' key_rows). The owners' fired rows,
+    mapped back to key rows, equal one single-phase operator over both partitions."""
+    import torch.multiprocessing as mp
+
+    from tests.streams import make_stream
+    O = oracle_mod
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_phase_strings_rank, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = sorted(x for _, rows, _ in res for x in rows)
+    k_, size, slide, jitter = TP_KINDS["hop"]
+    n = TP_N // 3
+    streams = [make_stream(n, 1500, "f64", seed=3000 + r, jitter_ms=jitter, null_frac=0.1, rate_per_ms=TP_RATE)
+               for r in range(WORLD)]
+    d = HostKeyDict()
+    op = O.OracleOperator(kind=k_, size=size, slide=slide)
+    rows, mxs = [], [-(1 << 63)] * WORLD
+    for lo in range(0, n, TP_BATCH):
+        for r in range(WORLD):
+            k, t, v, nl = streams[r]
+            ids = np.array([d.intern_bytes(x) for x in _string_rows(k[lo:lo + TP_BATCH])], dtype=np.int64)
+            op.process_batch(ids, t[lo:lo + TP_BATCH], v[lo:lo + TP_BATCH], nl[lo:lo + TP_BATCH])
+            mxs[r] = max(mxs[r], int(t[lo:lo + TP_BATCH].max()))
+        op.process_watermark(min(mxs) - TP_DELAY)
+        rows.append(op.take_rows())
+    op.process_watermark((1 << 63) - 1)
+    rows.append(op.take_rows())
+    exp = sorted((d.row_of(int(x["key"])), int(x["window_end"]), int(x["cnt_star"]), int(x["cnt_val"]),
+                  float(x["sum_d"]), int(x["sum_null"])) for x in np.concatenate(rows))
+    assert len(got) == len(exp)
+    for a, b in zip(got, exp):
+        assert a[:4] == b[:4] and a[5] == b[5], (a, b)
+        assert a[5] or abs(a[4] - b[4]) <= 1e-9 * max(abs(a[4]), abs(b[4])), (a, b)
+    # the global phase counts late PARTIAL rows (one per key and slice), as the reference's
+    # two-phase plan does; the single-phase operator counts records
+    assert op.late_dropped > 0 and sum(late for *_, late in res) > 0
