@@ -33,6 +33,7 @@ class FgConfig(C.Structure):
         ("expected_keys", C.c_int64), ("buffer_records", C.c_int64),
         ("tz_transition_ms", C.c_void_p), ("tz_offset_ms", C.c_void_p),
         ("n_tz_transitions", C.c_int32), ("tz_use_daylight", C.c_int32),
+        ("allowed_lateness_ms", C.c_int64),
     ]
 
 

@@ -2274,6 +2274,18 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             c.aggs[4] = FG_AGG_MAX;
         }
     }
+    if (c.allowed_lateness_ms < 0) {   // WindowedStream.allowedLateness: "The allowed lateness cannot be negative."
+        g_open_error = "The allowed lateness cannot be negative.";
+        return FG_EINVAL;
+    }
+    if (c.allowed_lateness_ms > 0 && c.mode != FG_MODE_DATASTREAM) {
+        g_open_error = "allowed_lateness_ms is a DataStream WindowOperator setting (SQL window operators have none)";
+        return FG_EINVAL;
+    }
+    if (c.allowed_lateness_ms > 0) {
+        g_open_error = "allowed_lateness_ms > 0 is not supported by this build";
+        return FG_EINVAL;
+    }
     const bool proctime = (c.flags & FG_FLAG_PROCTIME) != 0;
     if (proctime && (c.mode != FG_MODE_SQL || local)) {
         g_open_error = "FG_FLAG_PROCTIME is for SQL window aggregation (not DataStream or the local phase)";

@@ -155,6 +155,10 @@ class WindowAggOperator:
     # -- lifecycle -------------------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
+            # the in-flight device columns were recorded on the engine's stream: release them
+            # while that stream exists (the caching allocator records an event on it when a
+            # block is freed), then close the handle (fg_close drains and destroys the stream)
+            self._inflight = None
             self._lib.fg_close(self._h)
             self._h = None
 

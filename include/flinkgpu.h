@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 7
+#define FG_ABI_VERSION 8
 
 enum fg_status {
     FG_OK = 0,
@@ -163,6 +163,11 @@ typedef struct fg_config {
     const int64_t* tz_offset_ms;       /* n_tz_transitions + 1 offsets (ms): [i] in force before transition i */
     int32_t n_tz_transitions;
     int32_t tz_use_daylight;           /* TimeZone.getTimeZone(zone).useDaylightTime() */
+    /* DataStream WindowOperator.allowedLateness (WindowedStream.allowedLateness, WindowOperator.java:
+     * 608-622,630-681): a window's state is kept until cleanupTime = maxTimestamp + lateness
+     * (Long.MAX_VALUE on overflow); an element of a fired window not yet cleaned re-fires it
+     * (EventTimeTrigger.onElement :37-46). 0 for SQL operators. */
+    int64_t allowed_lateness_ms;
 } fg_config;
 
 typedef struct fg_batch {

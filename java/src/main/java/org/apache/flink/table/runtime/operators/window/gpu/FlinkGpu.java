@@ -1,0 +1,106 @@
+/*
+ * Natives of libflinkgpu_jni.so (jni/flink_gpu_jni.c), one per C-ABI entry point of
+ * include/flinkgpu.h. Every ByteBuffer is a direct buffer in native byte order (a wrapped
+ * off-heap MemorySegment, MemorySegment.java:288,307, or ByteBuffer.allocateDirect).
+ */
+package org.apache.flink.table.runtime.operators.window.gpu;
+
+import java.nio.ByteBuffer;
+
+/** JNI entry points of the MI355X window-aggregation engine. */
+public final class FlinkGpu {
+
+    static {
+        System.loadLibrary("flinkgpu_jni");
+    }
+
+    private FlinkGpu() {}
+
+    /** fg_open: config is an fg_config image (FgConfig); zone rules as arrays (may be null). */
+    public static native long open(ByteBuffer config, long[] tzTransitions, long[] tzOffsets);
+
+    /** fg_add_batch (FG_HOST): the buffers may be refilled as soon as the call returns. */
+    public static native void addBatch(
+            long h, ByteBuffer key, ByteBuffer rowtime, ByteBuffer val, ByteBuffer valNull, int n);
+
+    /** fg_add_rows: n packed BinaryRowData fixed-length parts, stride bytes apart. */
+    public static native void addRows(
+            long h,
+            ByteBuffer rows,
+            int n,
+            int stride,
+            int arity,
+            int keyField,
+            int rowtimeField,
+            int valField);
+
+    /** fg_add_partials (GlobalAggCombiner.combine); min / max null unless several accumulators. */
+    public static native void addPartials(
+            long h,
+            int n,
+            ByteBuffer key,
+            ByteBuffer sliceEnd,
+            ByteBuffer cntStar,
+            ByteBuffer cntVal,
+            ByteBuffer sum,
+            ByteBuffer min,
+            ByteBuffer max);
+
+    /**
+     * fg_advance_progress: fills cols with key, window_start, window_end, agg[0..numAggs),
+     * null_mask, rowtime (library-owned, valid until the next call); returns the row count.
+     */
+    public static native long advanceProgress(long h, long watermark, ByteBuffer[] cols);
+
+    /** fg_flush (prepareSnapshotPreBarrier). */
+    public static native void flush(long h);
+
+    /**
+     * fg_snapshot_state: cols (length 7) receives key, slice_end, cnt_star, cnt_val, sum, min, max;
+     * timerWatermark[0] the timer watermark; returns the entry count.
+     */
+    public static native long snapshotState(long h, ByteBuffer[] cols, long[] timerWatermark);
+
+    /** fg_restore. */
+    public static native void restore(
+            long h,
+            int n,
+            ByteBuffer key,
+            ByteBuffer sliceEnd,
+            ByteBuffer cntStar,
+            ByteBuffer cntVal,
+            ByteBuffer sum,
+            ByteBuffer min,
+            ByteBuffer max,
+            long timerWatermark);
+
+    /** fg_late_dropped (numLateRecordsDropped). */
+    public static native long lateDropped(long h);
+
+    /** fg_close. */
+    public static native void close(long h);
+
+    /** fg_key_dict_open. */
+    public static native long dictOpen(int device, int maxParallelism, long expectedKeys);
+
+    /** fg_key_dict_intern (FG_HOST); outKeyGroups may be null. */
+    public static native void dictIntern(
+            long d,
+            ByteBuffer rows,
+            long nbytes,
+            ByteBuffer offsets,
+            ByteBuffer lengths,
+            int n,
+            ByteBuffer outIds,
+            ByteBuffer outKeyGroups);
+
+    /** fg_key_dict_lookup (FG_HOST). */
+    public static native void dictLookup(
+            long d, ByteBuffer ids, int n, ByteBuffer outOffsets, ByteBuffer outLengths);
+
+    /** fg_key_dict_copy_arena. */
+    public static native void dictCopyArena(long d, long begin, long nbytes, ByteBuffer out);
+
+    /** fg_key_dict_close. */
+    public static native void dictClose(long d);
+}

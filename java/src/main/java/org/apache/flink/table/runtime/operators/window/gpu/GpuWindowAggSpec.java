@@ -1,0 +1,45 @@
+/*
+ * What the planner knows about one window aggregation, in the engine's terms: the window
+ * (SliceAssigners.tumbling/hopping/cumulative, SliceAssigners.java:59-96), the aggregate list
+ * (Count1/Count/Sum/Avg/Sum0/Min/MaxAggFunction over one value column), the input row's
+ * rowtime and value fields, and the grouping key's kind (one BIGINT column, or any key row
+ * through the GPU key dictionary).
+ */
+package org.apache.flink.table.runtime.operators.window.gpu;
+
+import java.io.Serializable;
+
+/** Serializable description of a GPU window aggregation (shipped with the operator). */
+public final class GpuWindowAggSpec implements Serializable {
+    private static final long serialVersionUID = 1L;
+
+    public int mode = FgConfig.MODE_SQL;
+    public int windowKind = FgConfig.TUMBLE;
+    public long sizeMs;
+    public long slideMs;
+    public long offsetMs;
+    /** fixed-offset shift zone (TIMESTAMP_LTZ); zones with transitions pass their rules. */
+    public long shiftTzOffsetMs;
+    public long[] tzTransitionsMs;
+    public long[] tzOffsetsMs;
+    public boolean tzUseDaylight;
+    public int valType = FgConfig.VAL_F64;
+    public int[] aggs = {FgConfig.AGG_COUNT_STAR, FgConfig.AGG_SUM, FgConfig.AGG_AVG};
+    public int flags;
+    public long expectedKeys;
+    public long bufferRecords = 1 << 24;
+    public int device;
+    public long allowedLatenessMs;
+
+    /** input row layout */
+    public int rowtimeIndex;
+    public int valueIndex = -1;
+
+    /** the key row is one BIGINT column (else: interned by the key dictionary) */
+    public boolean bigintKey = true;
+    /** fields of the key row (BinaryRowData arity) when it is interned */
+    public int keyArity = 1;
+
+    /** records gathered before one engine call (one micro-batch) */
+    public int batchRecords = 1 << 20;
+}

@@ -1,0 +1,296 @@
+/*
+ * flink_gpu_jni.c -- JNI glue between the Java shim (java/, org.apache.flink...gpu.FlinkGpu)
+ * and libflinkgpu.so (include/flinkgpu.h). Built by jni/Makefile when $JAVA_HOME is set; not
+ * part of __graft_entry__.build() (this image has no JDK).
+ *
+ * Every native of FlinkGpu.java maps one-for-one onto a C-ABI entry point:
+ *   open            fg_open              (WindowBuffer.Factory.create / SlicingWindowAggOperatorBuilder.build)
+ *   addBatch        fg_add_batch         (SlicingWindowOperator.processElement, batched)
+ *   addRows         fg_add_rows          (packed BinaryRowData of a MemorySegment)
+ *   addPartials     fg_add_partials      (GlobalAggCombiner.combine)
+ *   advanceProgress fg_advance_progress  (processWatermark -> advanceProgress + fireWindow)
+ *   flush           fg_flush             (prepareSnapshotPreBarrier)
+ *   snapshotState   fg_snapshot_state    (snapshotState: the window-aggs image)
+ *   restore         fg_restore           (initializeState)
+ *   lateDropped     fg_late_dropped      (numLateRecordsDropped)
+ *   close           fg_close
+ *   dict*           fg_key_dict_*        (BinaryRowDataKeySelector rows of any key type)
+ *
+ * Buffers: every ByteBuffer argument is a DIRECT buffer (MemorySegment.wrap of an off-heap
+ * segment, MemorySegment.java:288,307, or ByteBuffer.allocateDirect) in native byte order;
+ * its address is handed to the engine as FG_HOST memory, which fg_add_batch has finished
+ * reading when it returns (the shim may refill the buffer at once). Output columns are
+ * library-owned and wrapped with NewDirectByteBuffer: valid until the next call on the handle.
+ *
+ * Errors: a non-zero return code throws -- FG_EINVAL as IllegalArgumentException (the
+ * reference's message, e.g. SliceAssigners' window-spec checks), FG_EFULL as EOFException
+ * (RecordsWindowBuffer's "buffer full" signal), anything else as RuntimeException -- carrying
+ * fg_last_error / fg_key_dict_last_error.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "flinkgpu.h"
+
+static void throw_code(JNIEnv* env, int rc, const char* msg) {
+    const char* cls = rc == FG_EINVAL ? "java/lang/IllegalArgumentException"
+                    : rc == FG_EFULL  ? "java/io/EOFException"
+                                      : "java/lang/RuntimeException";
+    jclass c = (*env)->FindClass(env, cls);
+    if (c) (*env)->ThrowNew(env, c, msg ? msg : "libflinkgpu error");
+}
+
+static int check(JNIEnv* env, fg_handle* h, int rc) {
+    if (rc != FG_OK) throw_code(env, rc, fg_last_error(h));
+    return rc;
+}
+
+/* address of a direct buffer (NULL for a null reference); throws for a heap buffer */
+static void* addr(JNIEnv* env, jobject buf) {
+    if (!buf) return NULL;
+    void* p = (*env)->GetDirectBufferAddress(env, buf);
+    if (!p) throw_code(env, FG_EINVAL, "libflinkgpu takes direct ByteBuffers only");
+    return p;
+}
+
+static jobject wrap(JNIEnv* env, const void* p, jlong bytes) {
+    return (*env)->NewDirectByteBuffer(env, (void*)p, bytes > 0 ? bytes : 0);
+}
+
+#define FN(name) Java_org_apache_flink_table_runtime_operators_window_gpu_FlinkGpu_##name
+
+/* long open(ByteBuffer config, long[] tzTransitions, long[] tzOffsets)
+ * config: an fg_config image written by FgConfig.java (its pointer fields are ignored: the
+ * zone rules come as the two arrays, copied by fg_open). */
+JNIEXPORT jlong JNICALL FN(open)(JNIEnv* env, jclass cls, jobject config, jlongArray tzTrans, jlongArray tzOffs) {
+    (void)cls;
+    const fg_config* img = (const fg_config*)addr(env, config);
+    if (!img) return 0;
+    fg_config c = *img;
+    jlong* tr = NULL;
+    jlong* of = NULL;
+    c.tz_transition_ms = NULL;
+    c.tz_offset_ms = NULL;
+    if (c.n_tz_transitions > 0) {
+        if (!tzTrans || !tzOffs || (*env)->GetArrayLength(env, tzTrans) != c.n_tz_transitions ||
+            (*env)->GetArrayLength(env, tzOffs) != c.n_tz_transitions + 1) {
+            throw_code(env, FG_EINVAL, "zone rules need n_tz_transitions instants and n_tz_transitions + 1 offsets");
+            return 0;
+        }
+        tr = (*env)->GetLongArrayElements(env, tzTrans, NULL);
+        of = (*env)->GetLongArrayElements(env, tzOffs, NULL);
+        c.tz_transition_ms = (const int64_t*)tr;
+        c.tz_offset_ms = (const int64_t*)of;
+    }
+    fg_handle* h = NULL;
+    int rc = fg_open(&c, &h);
+    if (tr) (*env)->ReleaseLongArrayElements(env, tzTrans, tr, JNI_ABORT);
+    if (of) (*env)->ReleaseLongArrayElements(env, tzOffs, of, JNI_ABORT);
+    if (rc != FG_OK) {
+        throw_code(env, rc, fg_last_error(NULL));
+        return 0;
+    }
+    return (jlong)(intptr_t)h;
+}
+
+/* void addBatch(long h, ByteBuffer key, ByteBuffer rowtime, ByteBuffer val, ByteBuffer valNull, int n) */
+JNIEXPORT void JNICALL FN(addBatch)(JNIEnv* env, jclass cls, jlong hp, jobject key, jobject rowtime, jobject val,
+                                    jobject valNull, jint n) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_batch b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.location = FG_HOST;
+    b.key = (const int64_t*)addr(env, key);
+    b.rowtime = (const int64_t*)addr(env, rowtime);
+    b.val = addr(env, val);
+    b.val_null = (const uint8_t*)addr(env, valNull);
+    if ((*env)->ExceptionCheck(env)) return;
+    check(env, h, fg_add_batch(h, &b));
+}
+
+/* void addRows(long h, ByteBuffer rows, int n, int stride, int arity, int keyField, int rowtimeField, int valField)
+ * rows: the fixed-length parts of n BinaryRowData (a MemorySegment of serialized records) */
+JNIEXPORT void JNICALL FN(addRows)(JNIEnv* env, jclass cls, jlong hp, jobject rows, jint n, jint stride, jint arity,
+                                   jint keyField, jint rowtimeField, jint valField) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_row_batch b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.location = FG_HOST;
+    b.stride = stride;
+    b.rows = (const uint8_t*)addr(env, rows);
+    b.arity = arity;
+    b.key_field = keyField;
+    b.rowtime_field = rowtimeField;
+    b.val_field = valField;
+    if ((*env)->ExceptionCheck(env)) return;
+    check(env, h, fg_add_rows(h, &b));
+}
+
+/* void addPartials(long h, int n, ByteBuffer key, ByteBuffer sliceEnd, ByteBuffer cntStar,
+ *                  ByteBuffer cntVal, ByteBuffer sum, ByteBuffer min, ByteBuffer max) */
+JNIEXPORT void JNICALL FN(addPartials)(JNIEnv* env, jclass cls, jlong hp, jint n, jobject key, jobject sliceEnd,
+                                       jobject cntStar, jobject cntVal, jobject sum, jobject min, jobject max) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_partials p;
+    memset(&p, 0, sizeof p);
+    p.n = n;
+    p.location = FG_HOST;
+    p.key = (const int64_t*)addr(env, key);
+    p.slice_end = (const int64_t*)addr(env, sliceEnd);
+    p.cnt_star = (const int64_t*)addr(env, cntStar);
+    p.cnt_val = (const int64_t*)addr(env, cntVal);
+    p.sum = (const int64_t*)addr(env, sum);
+    p.min = (const int64_t*)addr(env, min);
+    p.max = (const int64_t*)addr(env, max);
+    if ((*env)->ExceptionCheck(env)) return;
+    check(env, h, fg_add_partials(h, &p));
+}
+
+/* long advanceProgress(long h, long watermark, ByteBuffer[] cols)
+ * cols (length >= 5 + numAggs) receives: key, window_start, window_end, agg[0..numAggs), null_mask,
+ * rowtime (DataStream; else null). Returns the number of fired rows. */
+JNIEXPORT jlong JNICALL FN(advanceProgress)(JNIEnv* env, jclass cls, jlong hp, jlong wm, jobjectArray cols) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_rows r;
+    if (check(env, h, fg_advance_progress(h, wm, FG_HOST, &r))) return 0;
+    const jlong n = r.n, bytes = 8 * n;
+    if ((*env)->GetArrayLength(env, cols) < 5 + r.num_aggs) {
+        throw_code(env, FG_EINVAL, "advanceProgress: column array too short");
+        return 0;
+    }
+    int i = 0;
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.key, bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_start, bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_end, bytes));
+    for (int a = 0; a < r.num_aggs; a++) (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.agg[a], bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.null_mask, n));
+    (*env)->SetObjectArrayElement(env, cols, i++, r.rowtime ? wrap(env, r.rowtime, bytes) : NULL);
+    return n;
+}
+
+/* void flush(long h) */
+JNIEXPORT void JNICALL FN(flush)(JNIEnv* env, jclass cls, jlong hp) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    check(env, h, fg_flush(h));
+}
+
+/* long snapshotState(long h, ByteBuffer[] cols, long[] timerWatermark)
+ * cols (length 7) receives key, slice_end, cnt_star, cnt_val, sum, min, max (min/max null for a
+ * single-accumulator operator); timerWatermark[0] the timer service's watermark. Returns n. */
+JNIEXPORT jlong JNICALL FN(snapshotState)(JNIEnv* env, jclass cls, jlong hp, jobjectArray cols, jlongArray timerWm) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_state_rows s;
+    int64_t wm = 0;
+    if (check(env, h, fg_snapshot_state(h, &s, &wm))) return 0;
+    const jlong bytes = 8 * s.n;
+    const int64_t* c[7] = {s.key, s.slice_end, s.cnt_star, s.cnt_val, s.sum, s.min, s.max};
+    for (int i = 0; i < 7; i++) (*env)->SetObjectArrayElement(env, cols, i, c[i] ? wrap(env, c[i], bytes) : NULL);
+    jlong w = wm;
+    (*env)->SetLongArrayRegion(env, timerWm, 0, 1, &w);
+    return s.n;
+}
+
+/* void restore(long h, int n, ByteBuffer key, ByteBuffer sliceEnd, ByteBuffer cntStar, ByteBuffer cntVal,
+ *              ByteBuffer sum, ByteBuffer min, ByteBuffer max, long timerWatermark) */
+JNIEXPORT void JNICALL FN(restore)(JNIEnv* env, jclass cls, jlong hp, jint n, jobject key, jobject sliceEnd,
+                                   jobject cntStar, jobject cntVal, jobject sum, jobject min, jobject max,
+                                   jlong timerWm) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_state_rows s;
+    memset(&s, 0, sizeof s);
+    s.n = n;
+    s.key = (const int64_t*)addr(env, key);
+    s.slice_end = (const int64_t*)addr(env, sliceEnd);
+    s.cnt_star = (const int64_t*)addr(env, cntStar);
+    s.cnt_val = (const int64_t*)addr(env, cntVal);
+    s.sum = (const int64_t*)addr(env, sum);
+    s.min = (const int64_t*)addr(env, min);
+    s.max = (const int64_t*)addr(env, max);
+    if ((*env)->ExceptionCheck(env)) return;
+    check(env, h, fg_restore(h, &s, timerWm));
+}
+
+/* long lateDropped(long h) */
+JNIEXPORT jlong JNICALL FN(lateDropped)(JNIEnv* env, jclass cls, jlong hp) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    int64_t v = 0;
+    check(env, h, fg_late_dropped(h, &v));
+    return v;
+}
+
+/* void close(long h) */
+JNIEXPORT void JNICALL FN(close)(JNIEnv* env, jclass cls, jlong hp) {
+    (void)env;
+    (void)cls;
+    fg_close((fg_handle*)(intptr_t)hp);
+}
+
+/* ---- key dictionary (keys of any type) ------------------------------------------------------ */
+
+static int dcheck(JNIEnv* env, fg_key_dict* d, int rc) {
+    if (rc != FG_OK) throw_code(env, rc, d ? fg_key_dict_last_error(d) : "fg_key_dict_open failed");
+    return rc;
+}
+
+/* long dictOpen(int device, int maxParallelism, long expectedKeys) */
+JNIEXPORT jlong JNICALL FN(dictOpen)(JNIEnv* env, jclass cls, jint device, jint maxP, jlong expected) {
+    (void)cls;
+    fg_key_dict* d = NULL;
+    if (dcheck(env, NULL, fg_key_dict_open(device, maxP, expected, &d))) return 0;
+    return (jlong)(intptr_t)d;
+}
+
+/* void dictIntern(long d, ByteBuffer rows, long nbytes, ByteBuffer offsets, ByteBuffer lengths, int n,
+ *                 ByteBuffer outIds, ByteBuffer outKeyGroups) -- outKeyGroups may be null */
+JNIEXPORT void JNICALL FN(dictIntern)(JNIEnv* env, jclass cls, jlong dp, jobject rows, jlong nbytes, jobject offsets,
+                                      jobject lengths, jint n, jobject outIds, jobject outKg) {
+    (void)cls;
+    fg_key_dict* d = (fg_key_dict*)(intptr_t)dp;
+    const uint8_t* r = (const uint8_t*)addr(env, rows);
+    const int64_t* o = (const int64_t*)addr(env, offsets);
+    const int32_t* l = (const int32_t*)addr(env, lengths);
+    int64_t* ids = (int64_t*)addr(env, outIds);
+    int32_t* kg = (int32_t*)addr(env, outKg);
+    if ((*env)->ExceptionCheck(env)) return;
+    dcheck(env, d, fg_key_dict_intern(d, FG_HOST, n, r, nbytes, o, l, ids, kg));
+}
+
+/* void dictLookup(long d, ByteBuffer ids, int n, ByteBuffer outOffsets, ByteBuffer outLengths) */
+JNIEXPORT void JNICALL FN(dictLookup)(JNIEnv* env, jclass cls, jlong dp, jobject ids, jint n, jobject outOffsets,
+                                      jobject outLengths) {
+    (void)cls;
+    fg_key_dict* d = (fg_key_dict*)(intptr_t)dp;
+    const int64_t* i = (const int64_t*)addr(env, ids);
+    int64_t* o = (int64_t*)addr(env, outOffsets);
+    int32_t* l = (int32_t*)addr(env, outLengths);
+    if ((*env)->ExceptionCheck(env)) return;
+    dcheck(env, d, fg_key_dict_lookup(d, FG_HOST, n, i, o, l));
+}
+
+/* void dictCopyArena(long d, long begin, long nbytes, ByteBuffer out) */
+JNIEXPORT void JNICALL FN(dictCopyArena)(JNIEnv* env, jclass cls, jlong dp, jlong begin, jlong nbytes, jobject out) {
+    (void)cls;
+    fg_key_dict* d = (fg_key_dict*)(intptr_t)dp;
+    uint8_t* o = (uint8_t*)addr(env, out);
+    if ((*env)->ExceptionCheck(env)) return;
+    dcheck(env, d, fg_key_dict_copy_arena(d, begin, nbytes, o));
+}
+
+/* void dictClose(long d) */
+JNIEXPORT void JNICALL FN(dictClose)(JNIEnv* env, jclass cls, jlong dp) {
+    (void)env;
+    (void)cls;
+    fg_key_dict_close((fg_key_dict*)(intptr_t)dp);
+}
