@@ -89,6 +89,7 @@ FLAG_KERNEL_TIMING = 1
 FLAG_LOCAL_PARTIALS = 2
 FLAG_PROCTIME = 4
 FLAG_WINDOWED = 8
+FLAG_PURGING_TRIGGER = 16
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (

@@ -30,6 +30,7 @@
 
 #include "../../include/flinkgpu.h"
 #include "fg_kernels.h"
+#include "fg_late.h"
 
 using namespace fg;
 
@@ -333,6 +334,20 @@ struct fg_handle {
     // snapshot image
     DevBuf s_key, s_slice, s_cs, s_cv, s_sum, s_off, s_v1, s_v2;
     HostBuf hs_key, hs_slice, hs_cs, hs_cv, hs_sum, hs_counts, hs_off, hs_v1, hs_v2;
+
+    // DataStream allowed lateness (WindowOperator.allowedLateness, fg_late.hip): a fired window's
+    // slices stay resident until its cleanup time (retire_at: slice end -> the cleanup time of
+    // the slice's last window); rows fired by late elements in fg_add_batch wait in the output
+    // buffers for the next fg_advance_progress (late_rows of them)
+    int64_t lateness = 0;
+    bool purging = false;                  // FG_FLAG_PURGING_TRIGGER
+    bool retain = false;                   // lateness > 0 and not purging: fired windows keep state
+    std::map<int64_t, int64_t> retire_at;
+    int64_t late_rows = 0;
+    int64_t late_horizon = JMIN;           // after fg_restore: the checkpoint's watermark (fired windows)
+    DevBuf lt_mix, lt_se, lt_val, lt_null, lt_idx, lt_done, lt_sel, lt_slot, lt_found, lt_ckey, lt_cidx, lt_need;
+    DevBuf lt_dir_se, lt_dir_t, lt_words, lt_r_key, lt_r_ts, lt_r_val, lt_r_null;
+    HostBuf lt_h;
 
     // stats
     int64_t records_in = 0, rows_fired = 0, flushes = 0;
@@ -756,9 +771,27 @@ int fire_collect(fg_handle* h);
 int reset_out_count(fg_handle* h) {
     if (!h->out_count_reset) {
         HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+        if (h->late_rows > 0) {   // rows fired by late elements lead the advance's rows
+            Words16 w{};
+            w.v[0] = (unsigned long long)h->late_rows;
+            w.n = 1;
+            HIPCHK(h, launch_store_words(reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8), w, h->stream));
+        }
         h->out_count_reset = true;
     }
     return FG_OK;
+}
+
+// A slice whose windows all fired: freed now, or -- with allowed lateness -- kept until the
+// cleanup time of its last window (WindowOperator.registerCleanupTimer :630-642).
+void retire(fg_handle* h, int64_t se, int64_t last_window_end) {
+    if (!h->retain) {
+        table_free(h, se);
+        return;
+    }
+    const int64_t at = ds_cleanup(last_window_end, h->lateness);
+    if (at <= h->current_progress) table_free(h, se);
+    else h->retire_at[se] = at;
 }
 
 struct FireRange {   // windows whose timers fire in (prev, wm]
@@ -887,7 +920,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     std::sort(sel.begin(), sel.end(), [&](int a, int b) { return h->lane[a].q < h->lane[b].q; });
     if (h->out_count_reset) HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
     else HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
-    std::vector<int64_t> fired_tables;
+    std::vector<int64_t> fired_tables, retained;
     bool any_emit = false;
     int rc;
     for (int l : sel) {
@@ -963,7 +996,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             }
             dstt = se == cum_last ? nullptr : (se == cum_first ? t : F);
         } else if (fire_now) {
-            dstt = nullptr;
+            dstt = h->retain && !h->local ? t : nullptr;   // allowed lateness: the fired window keeps its state
         }
         int64_t ub_in = ln.fill + ln.acc_fill;
         for (SliceTable* r : job.srcs) ub_in += r->upper;
@@ -991,7 +1024,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         p.fast_stream = plain ? 1 : 0;
         // compact LDS table (two workgroups per CU) when no resident state is read and the
         // COUNT(*) of a key cannot reach 2^32
-        p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) ? 1 : 0;
+        p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) && !(p.emit && p.has_dst) ? 1 : 0;
 #ifdef FG_STAMPS
         static DevBuf d_st;
         if (getenv("FG_STAMPS")) {
@@ -1053,7 +1086,12 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         }
 #endif
         if (fire_now) {
-            fired_tables.push_back(se);
+            if (h->retain && !h->local) {
+                t->upper = ub;
+                retained.push_back(se);
+            } else {
+                fired_tables.push_back(se);
+            }
             any_emit = true;
         } else if (cum_fire) {
             any_emit = true;
@@ -1083,6 +1121,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         h->pending_out = 0;
     }
     for (int64_t se : fired_tables) table_free(h, se);
+    for (int64_t se : retained) retire(h, se, se);
     for (int l : sel) release_lane(h, l);
     h->flushes++;
     return FG_OK;
@@ -1224,13 +1263,14 @@ int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired) {
         std::vector<int64_t> ends;
         for (auto& kv : h->tables) ends.push_back(kv.first);
         for (int64_t e : ends) {
+            if (h->retire_at.count(e)) continue;   // fired before, kept for its late elements
             if (due(e)) {
                 rc = fire_one(h, e, {h->tables[e].get()}, nullptr, true);
                 *fired = true;
                 if (rc) return rc;
-                table_free(h, e);   // expiredSlices = [windowEnd]
+                retire(h, e, e);    // expiredSlices = [windowEnd] (with allowed lateness: at cleanup)
             } else if (dead(e)) {
-                table_free(h, e);   // no timer can fire for this slice any more
+                retire(h, e, e);    // no timer can fire for this slice any more
             }
         }
         return FG_OK;
@@ -1252,7 +1292,10 @@ int fire_windows_launch(fg_handle* h, int64_t prev, int64_t wm, bool* fired) {
                     if (rc) return rc;
                 }
             }
-            if (due(W) || dead(W)) table_free(h, jadd(jsub(W, w.size), w.slice));   // expiredSlices
+            if (due(W) || dead(W)) {   // expiredSlices: W was the last window of its first slice
+                const int64_t first = jadd(jsub(W, w.size), w.slice);
+                if (!h->retire_at.count(first)) retire(h, first, W);
+            }
             // skip empty stretches
             auto nx = h->tables.upper_bound(jsub(W, w.size));
             if (nx == h->tables.end()) break;
@@ -2211,6 +2254,206 @@ int finish_batch(fg_handle* h) {
     return FG_OK;
 }
 
+// ---- DataStream allowed lateness (fg_late.hip) ------------------------------------------------
+// The watermark the late rules compare with: the timer service's (the operator's progress); after
+// fg_restore, until the watermark passes it, the checkpoint's -- windows fired before the
+// checkpoint keep only their cleanup timers, and their state is resident.
+int64_t late_wm(const fg_handle* h) { return std::max(h->current_progress, h->late_horizon); }
+
+// The late elements of a batch (late-allowed: a fired window not yet cleaned), in rounds of one
+// element per key, oldest first: each updates its (key, slice) state and FIREs its fired, not
+// cleaned windows at once (EventTimeTrigger.onElement :37-46) -- rows appended to the output
+// buffers, returned by the next fg_advance_progress ahead of its own rows.
+int late_fire(fg_handle* h, int64_t nl) {
+    const WindowSpec& w = h->w;
+    const int64_t wm = late_wm(h);
+    const int64_t nwin = w.kind == TUMBLE ? 1 : w.size / w.slide;
+    std::vector<int64_t> ses(nl);
+    HIPCHK(h, hipMemcpyAsync(ses.data(), h->lt_se.p, 8 * (size_t)nl, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::sort(ses.begin(), ses.end());
+    ses.erase(std::unique(ses.begin(), ses.end()), ses.end());
+    int rc;
+    if (!h->purging) {   // every slice a late element updates holds a table (its windows' state)
+        for (int64_t se : ses) {
+            SliceTable* t = nullptr;
+            rc = table_get(h, se, true, &t);
+            if (rc) return rc;
+            if (!h->retire_at.count(se) && ds_fired(jadd(se, (nwin - 1) * w.slide), wm))
+                h->retire_at[se] = ds_cleanup(jadd(se, (nwin - 1) * w.slide), h->lateness);   // all its windows fired
+        }
+    }
+    // rounds
+    uint64_t cap = 1024;
+    while (cap < 2 * (uint64_t)nl) cap <<= 1;
+    HIPCHK(h, h->lt_done.ensure(nl));
+    HIPCHK(h, h->lt_sel.ensure(nl));
+    HIPCHK(h, h->lt_slot.ensure(4 * (size_t)nl));
+    HIPCHK(h, h->lt_found.ensure(4 * (size_t)nl));
+    HIPCHK(h, h->lt_ckey.ensure(8 * (size_t)(cap + 2)));
+    HIPCHK(h, h->lt_cidx.ensure(4 * (size_t)(cap + 2)));
+    HIPCHK(h, h->lt_h.ensure(64));
+    HIPCHK(h, hipMemsetAsync(h->lt_done.p, 0, (size_t)nl, h->stream));
+    rc = ensure_out(h, h->late_rows + nl * nwin + 1);
+    if (rc) return rc;
+    {   // the fired-row counter continues after the rows fired earlier since the last advance
+        Words16 wd{};
+        wd.v[0] = (unsigned long long)h->late_rows;
+        wd.n = 1;
+        HIPCHK(h, launch_store_words(reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8), wd, h->stream));
+    }
+    h->out_count_reset = false;   // (the next advance re-bases the counter on late_rows)
+    int64_t pending = nl;
+    int guard = 0;
+    while (pending > 0) {
+        if (++guard > 64 + 4 * nl) return h->fail(FG_ESTATE, "internal: late-element rounds do not progress");
+        // directory of the slice tables (sorted by slice end), rebuilt per round (a split moves them)
+        std::vector<int64_t> dse;
+        std::vector<TableRef> dt;
+        for (auto& kv : h->tables) {
+            dse.push_back(kv.first);
+            dt.push_back(ref_of(kv.second.get()));
+        }
+        const int nd = (int)dse.size();
+        HIPCHK(h, h->lt_dir_se.ensure(8 * (size_t)std::max(nd, 1)));
+        HIPCHK(h, h->lt_dir_t.ensure(sizeof(TableRef) * (size_t)std::max(nd, 1)));
+        HIPCHK(h, h->lt_need.ensure(4 * (size_t)std::max(nd, 1) * h->P));
+        if (nd) {
+            HIPCHK(h, hipMemcpyAsync(h->lt_dir_se.p, dse.data(), 8 * (size_t)nd, hipMemcpyHostToDevice, h->stream));
+            HIPCHK(h, hipMemcpyAsync(h->lt_dir_t.p, dt.data(), sizeof(TableRef) * (size_t)nd, hipMemcpyHostToDevice,
+                                     h->stream));
+            HIPCHK(h, hipMemsetAsync(h->lt_need.p, 0, 4 * (size_t)nd * h->P, h->stream));
+        }
+        LateRound p{};
+        p.w = w;
+        p.wm = wm;
+        p.lateness = h->lateness;
+        p.purging = h->purging ? 1 : 0;
+        p.vt = h->cfg.val_type;
+        p.region_bits = h->region_bits;
+        p.P = h->P;
+        p.cap = table_cap(h->mv);
+        p.cols = table_cols(h->mv);
+        p.n = nl;
+        p.mix = h->lt_mix.as<int64_t>();
+        p.se = h->lt_se.as<int64_t>();
+        p.val = h->lt_val.as<int64_t>();
+        p.vnull = h->lt_null.as<uint8_t>();
+        p.idx = h->lt_idx.as<uint32_t>();
+        p.done = h->lt_done.as<uint8_t>();
+        p.sel = h->lt_sel.as<uint8_t>();
+        p.slot = h->lt_slot.as<uint32_t>();
+        p.found = h->lt_found.as<int32_t>();
+        p.claim_key = h->lt_ckey.as<unsigned long long>();
+        p.claim_idx = h->lt_cidx.as<uint32_t>();
+        p.claim_mask = cap - 1;
+        p.need = h->lt_need.as<uint32_t>();
+        p.flags = reinterpret_cast<unsigned int*>(h->lt_words.as<char>());
+        p.nsel = reinterpret_cast<unsigned long long*>(h->lt_words.as<char>() + 8);
+        p.dir = LateDir{h->lt_dir_se.as<int64_t>(), h->lt_dir_t.as<TableRef>(), nd, 0};
+        p.num_aggs = h->cfg.num_aggs;
+        for (int a = 0; a < h->cfg.num_aggs; a++) {
+            p.aggs[a] = h->cfg.aggs[a];
+            p.out_agg[a] = h->o_agg[a].as<int64_t>();
+        }
+        p.out_key = h->o_key.as<int64_t>();
+        p.out_ws = h->o_ws.as<int64_t>();
+        p.out_we = h->o_we.as<int64_t>();
+        p.out_null = h->o_null.as<uint8_t>();
+        p.out_rowtime = h->o_rt.as<int64_t>();
+        p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+        p.out_cap = h->out_cap;
+        HIPCHK(h, launch_late_reset(p, h->stream));
+        HIPCHK(h, launch_late_claim(p, h->stream));
+        HIPCHK(h, launch_late_lookup(p, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->lt_h.p, h->lt_words.p, 16, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        const unsigned flags = h->lt_h.as<unsigned int>()[0];
+        if (flags & 2u) return h->fail(FG_ESTATE, "internal: a late element's slice table is missing");
+        if (flags & 1u) {   // a region cannot take the round's new entries: split and redo the round
+            rc = grow(h, h->region_bits + 1);
+            if (rc) return rc;
+            continue;
+        }
+        const int64_t nsel = (int64_t)h->lt_h.as<unsigned long long>()[1];
+        HIPCHK(h, launch_late_update(p, h->stream));
+        HIPCHK(h, launch_late_emit(p, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->lt_h.p, h->lt_words.p, 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->lt_h.as<char>() + 16, h->scalars.as<char>() + 8, 8, hipMemcpyDeviceToHost,
+                                 h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (h->lt_h.as<unsigned int>()[0] & 4u) return h->fail(FG_EDEVICE, "internal: late-row buffer overflow");
+        h->late_rows = (int64_t)h->lt_h.as<unsigned long long>()[2];
+        pending -= nsel;
+    }
+    if (!h->purging)
+        for (int64_t se : ses) {
+            SliceTable* t = nullptr;
+            table_get(h, se, false, &t);
+            if (t) t->upper = std::min<int64_t>(t->upper + nl, kStateCapMax);
+        }
+    return FG_OK;
+}
+
+// The batch's late-allowed elements (k_late_split) are fired here; the others replace the batch
+// (compacted into engine buffers). Returns the remaining record count in *n_regular.
+int late_split(fg_handle* h, int64_t n, const int64_t** key, const int64_t** ts, const int64_t** val,
+               const uint8_t** vnull, int64_t* n_regular) {
+    // the previous batch's remainder may still be read by its queued passes: no reallocation under them
+    if (h->lt_r_key.bytes < 8 * (size_t)n) HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, h->lt_mix.ensure(8 * (size_t)n));
+    HIPCHK(h, h->lt_se.ensure(8 * (size_t)n));
+    HIPCHK(h, h->lt_val.ensure(8 * (size_t)n));
+    HIPCHK(h, h->lt_null.ensure((size_t)n));
+    HIPCHK(h, h->lt_idx.ensure(4 * (size_t)n));
+    HIPCHK(h, h->lt_words.ensure(64));
+    HIPCHK(h, h->lt_r_key.ensure(8 * (size_t)n));
+    HIPCHK(h, h->lt_r_ts.ensure(8 * (size_t)n));
+    if (*val) HIPCHK(h, h->lt_r_val.ensure(8 * (size_t)n));
+    if (*vnull) HIPCHK(h, h->lt_r_null.ensure((size_t)n));
+    HIPCHK(h, h->lt_h.ensure(64));
+    unsigned long long* counts = reinterpret_cast<unsigned long long*>(h->lt_words.as<char>() + 32);
+    HIPCHK(h, hipMemsetAsync(counts, 0, 16, h->stream));
+    LateSplit p{};
+    p.w = h->w;
+    p.wm = late_wm(h);
+    p.lateness = h->lateness;
+    p.purging = h->purging ? 1 : 0;
+    p.n = n;
+    p.key = *key;
+    p.ts = *ts;
+    p.val = *val;
+    p.vnull = *vnull;
+    p.counts = counts;
+    p.l_mix = h->lt_mix.as<int64_t>();
+    p.l_se = h->lt_se.as<int64_t>();
+    p.l_val = h->lt_val.as<int64_t>();
+    p.l_null = h->lt_null.as<uint8_t>();
+    p.l_idx = h->lt_idx.as<uint32_t>();
+    p.r_key = h->lt_r_key.as<int64_t>();
+    p.r_ts = h->lt_r_ts.as<int64_t>();
+    p.r_val = *val ? h->lt_r_val.as<int64_t>() : nullptr;
+    p.r_null = *vnull ? h->lt_r_null.as<uint8_t>() : nullptr;
+    HIPCHK(h, launch_late_split(p, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->lt_h.p, counts, 16, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const int64_t nl = (int64_t)h->lt_h.as<unsigned long long>()[0];
+    const int64_t nr = (int64_t)h->lt_h.as<unsigned long long>()[1];
+    *n_regular = n;
+    if (nl == 0) return FG_OK;   // nothing late: the batch as it is
+    if (!*vnull) {   // (the late list's NULL flags are all 0)
+        HIPCHK(h, hipMemsetAsync(h->lt_null.p, 0, (size_t)nl, h->stream));
+    }
+    int rc = late_fire(h, nl);
+    if (rc) return rc;
+    *n_regular = nr;
+    *key = h->lt_r_key.as<int64_t>();
+    *ts = h->lt_r_ts.as<int64_t>();
+    if (*val) *val = h->lt_r_val.as<int64_t>();
+    if (*vnull) *vnull = h->lt_r_null.as<uint8_t>();
+    return FG_OK;
+}
+
 // Every entry point first completes a deferred batch (its counters were copied behind
 // pass 1's plan, so the wait is usually over before pass 2 ends).
 int settle_pending(fg_handle* h) {
@@ -2282,8 +2525,8 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         g_open_error = "allowed_lateness_ms is a DataStream WindowOperator setting (SQL window operators have none)";
         return FG_EINVAL;
     }
-    if (c.allowed_lateness_ms > 0) {
-        g_open_error = "allowed_lateness_ms > 0 is not supported by this build";
+    if ((c.flags & FG_FLAG_PURGING_TRIGGER) && c.mode != FG_MODE_DATASTREAM) {
+        g_open_error = "FG_FLAG_PURGING_TRIGGER is a DataStream WindowOperator trigger";
         return FG_EINVAL;
     }
     const bool proctime = (c.flags & FG_FLAG_PROCTIME) != 0;
@@ -2363,6 +2606,13 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     }
     h->local = local;
     h->proctime = proctime;
+    h->lateness = c.mode == FG_MODE_DATASTREAM ? c.allowed_lateness_ms : 0;
+    h->purging = c.mode == FG_MODE_DATASTREAM && (c.flags & FG_FLAG_PURGING_TRIGGER) != 0;
+    h->retain = h->lateness > 0 && !h->purging;
+    if (h->lateness > 0 && h->mv) {
+        g_open_error = "allowed lateness: one value accumulator (DataStream SumAggregator)";
+        return FG_EINVAL;
+    }
     h->device = cfg->device_id;
     h->timing = (cfg->flags & FG_FLAG_KERNEL_TIMING) != 0;
     if (const char* e = getenv("FG_KERNEL_TIMING")) h->timing = h->timing && std::atoi(e) != 0;   // A/B of the events' cost
@@ -2479,7 +2729,7 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc0 = settle_pending(h)) return rc0;
     maybe_reduce_lanes(h);
-    const int64_t n = b->n;
+    int64_t n = b->n;
     const int64_t *key = b->key, *ts = b->rowtime;
     const int64_t* val = h->cfg.val_type != FG_VAL_NONE ? static_cast<const int64_t*>(b->val) : nullptr;
     const uint8_t* vnull = b->val_null;
@@ -2552,6 +2802,17 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
         if (nbad)
             return h->fail(FG_EINVAL, "windowed input: %llu window_end values off the slice grid of the window", nbad);
         ts = h->in_wts.as<int64_t>();
+    }
+    // DataStream allowed lateness: elements of fired, not yet cleaned windows FIRE them now
+    // (late_split / late_fire); the rest go on as the batch
+    if (h->lateness > 0) {
+        h->records_in += n;
+        int64_t nr = n;
+        int rcl = late_split(h, n, &key, &ts, &val, &vnull, &nr);
+        if (rcl) return rcl;
+        if (nr == 0) return FG_OK;
+        h->records_in -= nr;   // (counted below)
+        n = nr;
     }
     // EOFException semantics (RecordsWindowBuffer.java:91-96) are applied per lane inside
     // ingest_pass: a lane without room is flushed into its slice table, then the pass stages
@@ -2733,10 +2994,14 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc0 = settle_pending(h)) return rc0;
-    h->out_n = 0;
+    h->out_n = h->late_rows;   // rows fired by late elements since the last advance come first
     h->pending_out = 0;
     h->out_count_reset = false;
     h->fused_fired.clear();
+    if (h->late_rows > 0) {
+        int rcr = reset_out_count(h);
+        if (rcr) return rcr;
+    }
     int rc;
     const int64_t prev = h->timer_wm;
     const FireRange fr{prev, wm};
@@ -2791,6 +3056,18 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
         if (rc) return rc;
     }
     if (wm > h->timer_wm) h->timer_wm = wm;
+    if (!h->retire_at.empty()) {   // cleanup timers (WindowOperator.onEventTime :493-496 -> clearAllState)
+        for (auto it = h->retire_at.begin(); it != h->retire_at.end();) {
+            if (it->second <= h->current_progress) {
+                table_free(h, it->first);
+                it = h->retire_at.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+    if (h->late_horizon != JMIN && h->current_progress >= h->late_horizon) h->late_horizon = JMIN;
+    h->late_rows = 0;
     h->rows_fired += h->out_n;
     if (fired) {
         std::memset(fired, 0, sizeof *fired);
@@ -3044,6 +3321,18 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     // records that arrive for them (refire)
     h->refire_hi = h->w.kind != TUMBLE && !h->local && !h->proctime ? timer_watermark : JMIN;
     h->refire_wm = JMIN;
+    if (h->lateness > 0) {
+        // allowed lateness: windows that fired before the checkpoint keep only their cleanup
+        // timers (WindowOperator.onEventTime fired their trigger timers); their slices stay
+        // resident until then and fire again only for elements that reach them (the late path,
+        // against the checkpoint's watermark until the watermark passes it)
+        h->late_horizon = timer_watermark;
+        const int64_t nwin = h->w.kind == TUMBLE ? 1 : h->w.size / h->w.slide;
+        for (auto& kv : h->tables) {
+            const int64_t last = jadd(kv.first, (nwin - 1) * h->w.slide);
+            if (ds_fired(last, timer_watermark)) h->retire_at[kv.first] = ds_cleanup(last, h->lateness);
+        }
+    }
     return FG_OK;
 }
 
@@ -3100,6 +3389,9 @@ int fg_reset(fg_handle* h) {
     h->re_chain_w = JMIN;
     h->refire_hi = JMIN;
     h->refire_wm = JMIN;
+    h->retire_at.clear();
+    h->late_rows = 0;
+    h->late_horizon = JMIN;
     return FG_OK;
 }
 

@@ -83,8 +83,15 @@ class WindowAggOperator:
                  mode: str = "sql", shift_tz_offset_ms: int = 0, expected_keys: int = 1 << 16,
                  buffer_records: int = 1 << 22, device: int = 0, max_parallelism: int = 128,
                  key_group_range=(0, 127), kernel_timing: bool = False, local_partials: bool = False,
-                 proctime: bool = False, zone: str | None = None, windowed: bool = False):
-        """windowed: rows carry their window (WindowedSliceAssigner, after a window TVF): the
+                 proctime: bool = False, zone: str | None = None, windowed: bool = False,
+                 allowed_lateness: int = 0, purging_trigger: bool = False):
+        """allowed_lateness (DataStream): WindowedStream.allowedLateness -- a fired window keeps
+        its state until maxTimestamp + allowed_lateness, and an element reaching it meanwhile
+        fires it again at once; those rows are returned by the next process_watermark, ahead of
+        the rows its watermark fires. purging_trigger: PurgingTrigger.of(EventTimeTrigger) (a
+        firing window's state is cleared).
+
+        windowed: rows carry their window (WindowedSliceAssigner, after a window TVF): the
         `rowtime` column of process_batch holds each row's window_end; `window` is the TVF's.
 
         zone: an IANA zone name (TableConfig.getLocalTimeZone() of a TIMESTAMP_LTZ window)
@@ -129,7 +136,9 @@ class WindowAggOperator:
         cfg.key_group_start, cfg.key_group_end = int(key_group_range[0]), int(key_group_range[1])
         cfg.device_id = int(device)
         cfg.flags = ((L.FLAG_KERNEL_TIMING if kernel_timing else 0) | (L.FLAG_LOCAL_PARTIALS if local_partials else 0)
-                     | (L.FLAG_PROCTIME if proctime else 0) | (L.FLAG_WINDOWED if windowed else 0))
+                     | (L.FLAG_PROCTIME if proctime else 0) | (L.FLAG_WINDOWED if windowed else 0)
+                     | (L.FLAG_PURGING_TRIGGER if purging_trigger else 0))
+        cfg.allowed_lateness_ms = int(allowed_lateness)
         cfg.expected_keys = int(expected_keys)
         cfg.buffer_records = int(buffer_records)
         self.zone = zone

@@ -130,7 +130,11 @@ enum fg_flags {
      * window TVF emits them), else fg_add_batch fails with FG_EINVAL. SQL event time only,
      * not the local phase. With zone rules the window_end values are local (UTC-shifted)
      * times and are taken as is. */
-    FG_FLAG_WINDOWED = 8
+    FG_FLAG_WINDOWED = 8,
+    /* DataStream: PurgingTrigger.of(EventTimeTrigger) -- a firing window's state is cleared
+     * (FIRE_AND_PURGE), so an element of a fired, not yet cleaned window (allowed lateness)
+     * fires it with itself alone (WindowOperatorTest.testLateness :1805-1886). */
+    FG_FLAG_PURGING_TRIGGER = 16
 };
 
 #define FG_MAX_AGGS 8

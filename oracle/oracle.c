@@ -222,6 +222,8 @@ struct or_op {
     int64_t timer_wm;
     or_timer* heap; int64_t heap_n, heap_cap, seq;
     pmap timer_set;                    /* (key, ns) dedup (ts is a function of ns) */
+    pmap cleanup_set;                  /* DataStream with allowed lateness: the (key, window) cleanup
+                                        * timers at maxTimestamp + lateness (a second timer per window) */
     /* output */
     or_row* rows; int64_t rows_n, rows_cap;
     int64_t late_dropped;
@@ -440,9 +442,13 @@ static or_timer heap_pop(or_op* op) {
     return top;
 }
 /* registerEventTimeTimer  InternalTimerServiceImpl.java (queue add with dedup) */
+/* HeapPriorityQueueSet dedups timers by (timestamp, key, namespace) (TimerHeapInternalTimer
+ * .equals): a window's trigger timer and its cleanup timer (WindowOperator.registerCleanupTimer
+ * :630-642, at cleanupTime :669-673) are distinct timers when the allowed lateness is > 0 */
+static int is_cleanup_timer(const or_op* op, int64_t ns, int64_t ts);
 static void register_timer(or_op* op, int64_t key, int64_t ns, int64_t ts) {
     int ins;
-    int64_t* v = pmap_upsert(&op->timer_set, key, ns, &ins);
+    int64_t* v = pmap_upsert(is_cleanup_timer(op, ns, ts) ? &op->cleanup_set : &op->timer_set, key, ns, &ins);
     if (!ins) return;           /* HeapPriorityQueueSet.add: already contained */
     *v = ts;
     or_timer t = {ts, op->seq++, key, ns};
@@ -668,6 +674,16 @@ static void sql_on_timer(or_op* op, int64_t key, int64_t w) {
  * (SJ/api/windowing/assigners/TumblingEventTimeWindows.java:70-88) or
  * SlidingEventTimeWindows.assignWindows (:70-85); EventTimeTrigger.onElement :37-46;
  * HeapReducingState.add -> SumAggregator.reduce (SJ/api/functions/aggregation/SumAggregator.java:66-76) */
+/* WindowOperator.cleanupTime :669-673: maxTimestamp + allowedLateness, Long.MAX_VALUE on overflow */
+static int64_t ds_cleanup_time(const or_op* op, int64_t end) {
+    int64_t max_ts = jsub(end, 1);
+    int64_t c = jadd(max_ts, op->cfg.allowed_lateness);
+    return c >= max_ts ? c : JMAX;
+}
+static int is_cleanup_timer(const or_op* op, int64_t ns, int64_t ts) {
+    return op->cfg.mode == OR_MODE_DATASTREAM && op->cfg.allowed_lateness > 0 && ts == ds_cleanup_time(op, ns) &&
+           ts != jsub(ns, 1);
+}
 static int ds_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits, uint8_t isnull) {
     (void)isnull;
     int64_t size = op->cfg.size;
@@ -677,21 +693,35 @@ static int ds_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits,
     for (int64_t start = last_start; start > jsub(ts, size); start = jsub(start, slide)) {
         int64_t end = jadd(start, size);
         int64_t max_ts = jsub(end, 1);
-        if (max_ts <= op->timer_wm) continue;        /* isWindowLate :608-611 (lateness 0) */
+        int64_t cleanup = ds_cleanup_time(op, end);
+        if (cleanup <= op->timer_wm) continue;       /* isWindowLate :608-611 */
         skipped = 0;
-        or_acc* a = state_put(op, key, end);
+        or_acc* a = state_put(op, key, end);         /* windowState.add -> SumAggregator.reduce */
         acc_accumulate(a, op->cfg.val_type, vbits, 0);
-        register_timer(op, key, end, max_ts);        /* EventTimeTrigger.onElement + cleanup timer (dedup) */
+        /* EventTimeTrigger.onElement :37-46 (PurgingTrigger.onElement: FIRE -> FIRE_AND_PURGE) */
+        if (max_ts <= op->timer_wm) {
+            emit_row(op, key, start, end, a, max_ts);  /* emitWindowContents :574-579 */
+            if (op->cfg.purging) state_clear(op, key, end);
+        } else {
+            register_timer(op, key, end, max_ts);
+        }
+        if (cleanup != JMAX) register_timer(op, key, end, cleanup);   /* registerCleanupTimer :630-642 */
         if (op->cfg.kind == OR_TUMBLE) break;
     }
-    /* :448-456: isSkippedElement && isElementLate */
-    return skipped && ts <= op->timer_wm;
+    /* :448-456: isSkippedElement && isElementLate (:620-622: timestamp + allowedLateness <= watermark) */
+    return skipped && jadd(ts, op->cfg.allowed_lateness) <= op->timer_wm;
 }
-/* onEventTime :459-503 -> emitWindowContents :574-579 (timestamp = window.maxTimestamp()) */
-static void ds_on_timer(or_op* op, int64_t key, int64_t end) {
-    const or_acc* a = state_get(op, key, end);
-    if (a) emit_row(op, key, jsub(end, op->cfg.size), end, a, jsub(end, 1));
-    state_clear(op, key, end);                       /* isCleanupTime -> clearAllState :559-570 */
+/* onEventTime :459-503: EventTimeTrigger.onEventTime FIREs at maxTimestamp (:49-51) ->
+ * emitWindowContents :574-579 (timestamp = window.maxTimestamp()); PurgingTrigger purges;
+ * at cleanupTime clearAllState :559-570 */
+static void ds_on_timer(or_op* op, int64_t key, int64_t end, int64_t time) {
+    int64_t max_ts = jsub(end, 1);
+    if (time == max_ts) {
+        const or_acc* a = state_get(op, key, end);
+        if (a) emit_row(op, key, jsub(end, op->cfg.size), end, a, max_ts);
+        if (op->cfg.purging) state_clear(op, key, end);
+    }
+    if (time == ds_cleanup_time(op, end)) state_clear(op, key, end);
 }
 
 /* ---------------- public API --------------------------------------------------------- */
@@ -742,6 +772,10 @@ or_op* or_open(const or_config* cfg, char* err, int errlen) {
     if (!buf[0] && cfg->phase != OR_PHASE_SINGLE &&
         (cfg->mode != OR_MODE_SQL || cfg->windowed || cfg->proctime || cfg->phase > OR_PHASE_GLOBAL))
         snprintf(buf, sizeof buf, "the two-phase operators are SQL event-time operators");
+    if (!buf[0] && cfg->allowed_lateness < 0)   /* WindowOperatorBuilder.allowedLateness :128 */
+        snprintf(buf, sizeof buf, "The allowed lateness cannot be negative.");
+    if (!buf[0] && (cfg->allowed_lateness > 0 || cfg->purging) && cfg->mode != OR_MODE_DATASTREAM)
+        snprintf(buf, sizeof buf, "allowed lateness and triggers are DataStream WindowOperator settings");
     if (!buf[0] && cfg->windowed && (cfg->mode != OR_MODE_SQL || cfg->proctime))
         /* WindowedSliceAssigner.isEventTime() is always true (:430-434); SQL only */
         snprintf(buf, sizeof buf, "a windowed slice assigner is an SQL event-time assigner");
@@ -776,12 +810,13 @@ or_op* or_open(const or_config* cfg, char* err, int errlen) {
     pmap_init(&op->buf_map, 1024);
     pmap_init(&op->state, 1024);
     pmap_init(&op->timer_set, 1024);
+    pmap_init(&op->cleanup_set, 1024);
     return op;
 }
 
 void or_close(or_op* op) {
     if (!op) return;
-    pmap_free(&op->buf_map); pmap_free(&op->state); pmap_free(&op->timer_set);
+    pmap_free(&op->buf_map); pmap_free(&op->state); pmap_free(&op->timer_set); pmap_free(&op->cleanup_set);
     free(op->be_slice); free(op->be_key); free(op->be_head); free(op->be_tail);
     free(op->br_val); free(op->br_null); free(op->br_next); free(op->br_acc);
     free(op->accs); free(op->acc_free); free(op->heap); free(op->rows); free(op->merge_buf);
@@ -852,9 +887,9 @@ void or_process_watermark(or_op* op, int64_t wm) {
     op->timer_wm = wm;
     while (op->heap_n > 0 && op->heap[0].ts <= wm) {
         or_timer t = heap_pop(op);
-        pmap_remove(&op->timer_set, t.key, t.ns, NULL);
+        pmap_remove(is_cleanup_timer(op, t.ns, t.ts) ? &op->cleanup_set : &op->timer_set, t.key, t.ns, NULL);
         if (op->cfg.mode == OR_MODE_SQL) sql_on_timer(op, t.key, t.ns);
-        else ds_on_timer(op, t.key, t.ns);
+        else ds_on_timer(op, t.key, t.ns, t.ts);
     }
 }
 

@@ -47,6 +47,8 @@ typedef struct or_config {
     int32_t windowed;         /* WindowedSliceAssigner over the kind's assigner: ts = window_end */
     int32_t phase;            /* OR_PHASE_*: single operator, or the local / global half of the
                                * two-phase plan (TwoStageOptimizedWindowAggregateRule) */
+    int32_t purging;          /* DataStream: PurgingTrigger.of(EventTimeTrigger) (FIRE -> FIRE_AND_PURGE) */
+    int64_t allowed_lateness; /* DataStream WindowOperator.allowedLateness (ms, >= 0) */
 } or_config;
 enum { OR_PHASE_SINGLE = 0, OR_PHASE_LOCAL = 1, OR_PHASE_GLOBAL = 2 };
 

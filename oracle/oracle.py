@@ -41,6 +41,8 @@ class Config(C.Structure):
         ("tz_use_dst", C.c_int32),
         ("windowed", C.c_int32),
         ("phase", C.c_int32),
+        ("purging", C.c_int32),
+        ("allowed_lateness", C.c_int64),
     ]
 
 
@@ -165,7 +167,7 @@ class OracleOperator:
 
     def __init__(self, mode=MODE_SQL, kind=TUMBLE, size=1000, slide=0, offset=0, tz_offset_ms=0,
                  val_type=VAL_F64, count_star_index=0, proctime=False, _handle=None, zone=None, windowed=False,
-                 phase=PHASE_SINGLE):
+                 phase=PHASE_SINGLE, allowed_lateness=0, purging=False):
         """zone: an IANA zone name whose rules (transitions, daylight saving) replace the fixed
         tz_offset_ms (TimeWindowUtil with a ZoneId). phase: PHASE_LOCAL / PHASE_GLOBAL for the
         two halves of the two-phase plan (LocalSlicingWindowAggOperator + LocalAggCombiner;
@@ -174,6 +176,8 @@ class OracleOperator:
                           1 if proctime else 0, 0)
         self.cfg.windowed = 1 if windowed else 0
         self.cfg.phase = phase
+        self.cfg.allowed_lateness = int(allowed_lateness)   # DataStream WindowOperator.allowedLateness
+        self.cfg.purging = 1 if purging else 0              # PurgingTrigger.of(EventTimeTrigger)
         self.zone = zone
         if zone is not None:
             from flink_amd.tz import zone_rules

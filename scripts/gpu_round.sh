@@ -5,7 +5,7 @@ set -o pipefail
 OUT=${OUT:-gpurun_out/r03}
 mkdir -p "$OUT"
 TESTS=${TESTS:-tests}
-timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread \
+timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread ${K:+-k "$K"} \
     > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
 tail -3 "$OUT/gpu_tests.log"
 if [ -n "$BENCH" ]; then

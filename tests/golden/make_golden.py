@@ -329,6 +329,41 @@ def datastream_fixtures():
                     val_type="i64", count_star_index=-1),
         columns=["key", "sum", "out_ts"],
         events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=1))
+    # testLateness :1805-1886 (2 s tumbling, allowedLateness 500, PurgingTrigger.of(EventTimeTrigger)):
+    # the element at 1997 arrives after WM 2300 fired and purged its window but before its cleanup
+    # time 1999 + 500 -> it re-fires the window at once with only itself ("this is 1 and not 3
+    # because the trigger fires and purges"); the element at 1998 after WM 6000 is late (the
+    # reference side-outputs it; here it is counted in numLateRecordsDropped)
+    ev, steps = [], []
+    ev.append(E(2, 1, 500)); ev.append(WM(1500)); steps.append((len(ev) - 1, []))
+    ev.append(E(2, 1, 1300)); ev.append(WM(2300)); steps.append((len(ev) - 1, [[2, 2, 1999]]))
+    ev.append(E(2, 1, 1997)); ev.append(WM(6000)); steps.append((len(ev) - 1, [[2, 1, 1999]]))
+    ev.append(E(2, 1, 1998)); ev.append(WM(7000)); steps.append((len(ev) - 1, []))
+    out.append(dict(
+        name="ds_tumble_2s_lateness500_purging",
+        source="SJT/runtime/operators/windowing/WindowOperatorTest.java:1805-1886",
+        config=dict(mode="datastream", kind="tumble", size=2000, slide=0, offset=0, tz_offset_ms=0,
+                    val_type="i64", count_star_index=-1, allowed_lateness=500, purging=True),
+        columns=["key", "sum", "out_ts"],
+        events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=1))
+    # testCleanupTimeOverflow :1888-1971 (1 s tumbling, allowedLateness 2000, EventTimeTrigger):
+    # the window of Long.MAX_VALUE - 1750 has maxTimestamp + lateness past Long.MAX_VALUE -> its
+    # cleanup time is Long.MAX_VALUE (no wrapped-around timer cleans it at MAX - 1500); it fires at
+    # its maxTimestamp
+    jmax = (1 << 63) - 1
+    ts = jmax - 1750
+    start = jmax - 1807   # getWindowStartWithOffset(ts, 0, 1000): (ts + 1000) wraps, Java % keeps its sign
+    max_ts = start + 1000 - 1
+    ev, steps = [], []
+    ev.append(E(2, 1, ts)); ev.append(WM(jmax - 1500)); steps.append((len(ev) - 1, []))
+    ev.append(WM(max_ts)); steps.append((len(ev) - 1, [[2, 1, max_ts]]))
+    out.append(dict(
+        name="ds_tumble_1s_lateness2000_cleanup_overflow",
+        source="SJT/runtime/operators/windowing/WindowOperatorTest.java:1888-1971",
+        config=dict(mode="datastream", kind="tumble", size=1000, slide=0, offset=0, tz_offset_ms=0,
+                    val_type="i64", count_star_index=-1, allowed_lateness=2000),
+        columns=["key", "sum", "out_ts"],
+        events=ev, expected=[dict(after_event=i, rows=r) for i, r in steps], expected_late_dropped=0))
     return out
 
 

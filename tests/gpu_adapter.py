@@ -23,7 +23,8 @@ class GpuOperator:
             window_of(cfg), aggs=cfg.get("aggs", ("count_star", "count", "sum", "avg", "sum0")), val_type=cfg["val_type"],
             mode=cfg["mode"], shift_tz_offset_ms=cfg.get("tz_offset_ms", 0), expected_keys=expected_keys,
             buffer_records=buffer_records, kernel_timing=kernel_timing, proctime=cfg.get("proctime", False),
-            zone=cfg.get("zone"), windowed=cfg.get("windowed", False))
+            zone=cfg.get("zone"), windowed=cfg.get("windowed", False),
+            allowed_lateness=cfg.get("allowed_lateness", 0), purging_trigger=cfg.get("purging", False))
         self._rows = []
 
     def process_batch(self, key, ts, val=None, isnull=None):
@@ -41,7 +42,8 @@ class GpuOperator:
             self.op.window, aggs=self.op.aggs, val_type=self.cfg["val_type"], mode=self.cfg["mode"],
             shift_tz_offset_ms=self.cfg.get("tz_offset_ms", 0), expected_keys=self.op.cfg.expected_keys,
             buffer_records=self.op.cfg.buffer_records, proctime=self.cfg.get("proctime", False),
-            zone=self.cfg.get("zone"), windowed=self.cfg.get("windowed", False)))
+            zone=self.cfg.get("zone"), windowed=self.cfg.get("windowed", False),
+            allowed_lateness=self.cfg.get("allowed_lateness", 0), purging_trigger=self.cfg.get("purging", False)))
         new.op.restore_state(img, wm)
         new._late_base = self.late_dropped
         return new

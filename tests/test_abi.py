@@ -31,14 +31,29 @@ def test_library_exports_every_declared_symbol():
     assert lib.fg_abi_version() == 8
 
 
-def test_struct_layouts_match_header_sizes():
-    # fg_config: 2*4 + 4*8 + 2*4 + 8*4 + 6*4 + 2*8 + zone rules (2 pointers + 2*4)
-    assert C.sizeof(L.FgConfig) == 8 + 32 + 8 + 32 + 24 + 16 + 16 + 8
-    assert C.sizeof(L.FgBatch) == 8 + 8 + 4 * 8
-    assert C.sizeof(L.FgRows) == 8 + 8 + 3 * 8 + 8 * 8 + 2 * 8
-    assert C.sizeof(L.FgPartials) == 8 + 8 + 7 * 8
-    assert C.sizeof(L.FgStateRows) == 8 + 7 * 8
-    assert C.sizeof(L.FgRowBatch) == 8 + 4 + 4 + 8 + 4 * 4
+def test_struct_layouts_match_header_sizes(tmp_path):
+    """Every ctypes mirror of a C-ABI struct has the header's layout: offsetof/sizeof from the
+    C compiler itself (gcc on include/flinkgpu.h) against the ctypes field offsets."""
+    import subprocess
+    structs = {"fg_config": L.FgConfig, "fg_batch": L.FgBatch, "fg_rows": L.FgRows, "fg_partials": L.FgPartials,
+               "fg_state_rows": L.FgStateRows, "fg_row_batch": L.FgRowBatch, "fg_kernel_stat": L.FgKernelStat,
+               "fg_stats": L.FgStats}
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "flinkgpu.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        src.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            src.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    src.append("return 0; }")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {(a, b): int(v) for a, b, v in (ln.split() for ln in out if ln)}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
 
 
 def test_binary_row_layout():

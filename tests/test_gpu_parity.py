@@ -24,7 +24,8 @@ def oracle_mk(O, cfg):
     return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"], slide=cfg["slide"],
                             offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"], val_type=VT[cfg["val_type"]],
                             count_star_index=cfg["count_star_index"], proctime=cfg.get("proctime", False),
-                            zone=cfg.get("zone"), windowed=cfg.get("windowed", False))
+                            zone=cfg.get("zone"), windowed=cfg.get("windowed", False),
+                            allowed_lateness=cfg.get("allowed_lateness", 0), purging=cfg.get("purging", False))
 
 
 @pytest.mark.parametrize("case", OP_CASES, ids=[c["name"] for c in OP_CASES])
@@ -37,7 +38,9 @@ def test_golden_cases_on_gpu(case):
 
 
 def sort_rows(r):
-    return r[np.lexsort((r["key"], r["window_end"]))]
+    # (window_end, key), then the accumulators: with allowed lateness one (key, window) may fire
+    # several times in a step (every late element re-fires it, EventTimeTrigger.onElement)
+    return r[np.lexsort((r["sum_d"], r["sum_i"], r["cnt_star"], r["key"], r["window_end"]))]
 
 
 F64_EPS = float(np.finfo(np.float64).eps)
@@ -888,3 +891,36 @@ def test_binary_rows_parity(oracle_mod, case):
         g.op.process_rows(bad, 32, 3)
     g.close()
     o.close()
+
+
+# DataStream allowed lateness (WindowOperator.java:608-681, EventTimeTrigger.java:37-51): the
+# jitter exceeds the watermark delay, so elements reach windows that fired already; those within
+# the lateness re-fire their window at once (with the whole state, or -- PurgingTrigger -- alone),
+# the rest are dropped; fired windows keep their state until maxTimestamp + lateness.
+LATENESS_CASES = [
+    ("tumble_i64_l500", dict(cfg_of("tumble", 1000, vt="i64", mode="datastream"), allowed_lateness=500),
+     dict(n=200_000, keys=3000, batch=10_000, delay=100, jitter=1500)),
+    ("tumble_f64_l800", dict(cfg_of("tumble", 1000, mode="datastream"), allowed_lateness=800),
+     dict(n=200_000, keys=3000, batch=10_000, delay=100, jitter=1500)),
+    ("tumble_i64_l500_purging", dict(cfg_of("tumble", 1000, vt="i64", mode="datastream"), allowed_lateness=500,
+                                     purging=True), dict(n=200_000, keys=3000, batch=10_000, delay=100, jitter=1500)),
+    ("sliding_i64_l700", dict(cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), allowed_lateness=700),
+     dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=2000)),
+    ("sliding_f64_l1500_purging", dict(cfg_of("hop", 3000, 1000, mode="datastream"), allowed_lateness=1500,
+                                       purging=True), dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=2500)),
+    # hot keys: many late elements of one key in one batch (several rounds of the late path)
+    ("tumble_i64_l600_zipf", dict(cfg_of("tumble", 1000, vt="i64", mode="datastream"), allowed_lateness=600),
+     dict(n=200_000, keys=5000, batch=20_000, delay=50, jitter=1200, zipf=1.3)),
+    # regions split while late elements append new keys (an operator sized for 100 keys)
+    ("tumble_i64_l500_split", dict(cfg_of("tumble", 1000, vt="i64", mode="datastream"), allowed_lateness=500),
+     dict(n=300_000, keys=60_000, batch=30_000, delay=100, jitter=1500, expected_keys=100)),
+]
+
+
+@pytest.mark.parametrize("name,cfg,kw", LATENESS_CASES, ids=[c[0] for c in LATENESS_CASES])
+def test_datastream_allowed_lateness_parity(oracle_mod, name, cfg, kw):
+    kw = dict(kw)
+    ek = kw.pop("expected_keys", None)
+    late = drive_both(oracle_mod, cfg, kw.pop("n"), kw.pop("keys"), kw.pop("batch"), kw.pop("delay"), kw.pop("jitter"),
+                      expected_keys=ek, **kw)
+    assert late > 0, "the stream should drop some elements beyond the lateness"

@@ -12,7 +12,8 @@ def make_oracle(O):
         return O.OracleOperator(mode=MODE[cfg["mode"]], kind=KIND[cfg["kind"]], size=cfg["size"],
                                 slide=cfg["slide"], offset=cfg["offset"], tz_offset_ms=cfg["tz_offset_ms"],
                                 val_type=VT[cfg["val_type"]], count_star_index=cfg["count_star_index"],
-                                proctime=cfg.get("proctime", False), zone=cfg.get("zone"))
+                                proctime=cfg.get("proctime", False), zone=cfg.get("zone"),
+                                allowed_lateness=cfg.get("allowed_lateness", 0), purging=cfg.get("purging", False))
     return mk
 
 
