@@ -111,6 +111,7 @@ struct Staged {
     int64_t lane_start[kMaxLanes] = {0, 0, 0, 0};
     int64_t lane_n[kMaxLanes] = {0, 0, 0, 0};
     bool has_null = false;
+    bool narrow = false;  // 12-B records {int32 key, value} (IngestParams.narrow)
     bool skew = false;    // some region may hold over kHeavyMin records of this pass (hot keys)
     int refs = 0;         // lanes still holding records of this pass
 };
@@ -133,7 +134,7 @@ struct DevCounters {     // device scratch words read back after the count pass
     long long qnext;       // smallest occupied slice index >= the pass's filter (JMAX: none)
     unsigned long long lane_total[kMaxLanes];
     unsigned int max_bucket;   // largest per-workgroup bucket count (skew hint)
-    unsigned int pad;
+    unsigned int wide;         // pass 1: an accepted key does not fit 32 bits (narrow staging off)
 };
 struct Counters {        // host view: per-lane slice index ranges (min > max: lane idle)
     unsigned long long drops;
@@ -244,6 +245,11 @@ struct fg_handle {
     // staged buffer (RecordsWindowBuffer analogue): one area of lane_cap records per lane
     int64_t lane_cap = 0;
     int st_stride = 2;          // int64 words per staged record: {key, val} or {key}
+    // narrow staging: passes write 12-B {int32 key, value} records while every key seen fits
+    // 32 bits; the first wider key flushes the lanes and turns it off for good (all live
+    // passes share one record format, so a lane's positions map to one byte layout)
+    bool narrow = false;
+    bool narrow_ok = false;   // the operator may stage narrow records (fg_reset restores `narrow`)
     DevBuf st_rec, st_null;
     Lane lane[kMaxLanes];
     // accumulator areas (global phase, fg_add_partials): SoA, acc_cap rows per lane
@@ -579,9 +585,11 @@ StagedBatch batch_of(const fg_handle* h, const JobBatch& jb) {
             b.val2 = h->acc_v2.as<int64_t>() + at;
         }
     } else {
-        b.rec = h->st_rec.as<int64_t>() + ((int64_t)l * h->lane_cap + s->lane_start[l]) * h->st_stride;
+        b.rec = s->narrow ? reinterpret_cast<const int64_t*>(h->st_rec.as<char>() +
+                                                             12 * ((int64_t)l * h->lane_cap + s->lane_start[l]))
+                          : h->st_rec.as<int64_t>() + ((int64_t)l * h->lane_cap + s->lane_start[l]) * h->st_stride;
         b.vnull = s->has_null ? h->st_null.as<uint8_t>() + (int64_t)l * h->lane_cap + s->lane_start[l] : nullptr;
-        b.stride = h->st_stride;
+        b.stride = s->narrow ? 3 : h->st_stride;
     }
     b.shift = h->region_bits - s->bits;
     return b;
@@ -1020,8 +1028,10 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         if (rc) return rc;
         // fast variants: plain staged {key, value} records bucketed at the current regions
         bool plain = h->st_stride == 2 && !ln.passes.empty() && ln.passes.size() <= (size_t)kMaxMergeBatches;
-        for (Staged* s : ln.passes) plain = plain && !s->has_null && !s->is_acc && s->bits == h->region_bits;
+        for (Staged* s : ln.passes)
+            plain = plain && !s->has_null && !s->is_acc && s->bits == h->region_bits && s->narrow == ln.passes[0]->narrow;
         p.fast_stream = plain ? 1 : 0;
+        p.narrow = plain && ln.passes[0]->narrow ? 1 : 0;
         // compact LDS table (two workgroups per CU) when no resident state is read and the
         // COUNT(*) of a key cannot reach 2^32
         p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) && !(p.emit && p.has_dst) ? 1 : 0;
@@ -1766,6 +1776,8 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     p.qnext = &dc->qnext;
     p.lane_total = dc->lane_total;
     p.max_bucket = &dc->max_bucket;
+    p.wide = &dc->wide;
+    p.narrow = two_pass && h->narrow ? 1 : 0;
     if (two_pass) {
         KTimer kt(h, K_PART1, n);
         HIPCHK(h, launch_part1(p, h->stream));
@@ -1868,6 +1880,14 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     // qmin/qmax span the batch's accepted records; the pass stages those inside the filter
     const int64_t fq0 = std::max<int64_t>(got.qmin, flo), fq1 = std::min<int64_t>(got.qmax, fhi - 1);
     if (fq0 > fq1) return FG_OK;                                            // none inside
+    if (p.narrow && got.wide) {
+        // a key wider than 32 bits under narrow staging (the device plan stopped pass 2): the
+        // lanes' narrow passes go into their tables and every later pass stages 16-B records
+        rc = flush(h);
+        if (rc) return rc;
+        h->narrow = false;
+        p.narrow = 0;
+    }
     if ((uint64_t)(fq1 - fq0) >= (uint64_t)h->lanes) return -1;              // more slices than lanes
     for (int64_t q = fq0; q <= fq1; q++) {
         const int l = (int)(q & (h->lanes - 1));
@@ -1950,6 +1970,7 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
         HIPCHK(h, launch_ingest_scatter(p, h->stream));
     }
     s->has_null = vnull != nullptr;
+    s->narrow = p.narrow != 0;
     s->bits = p.region_bits;   // (a flush above may have split the regions since the count)
     s->is_acc = false;
     s->skew = out->skew;
@@ -2712,6 +2733,10 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         return FG_EDEVICE;
     }
     if (const char* e = getenv("FG_SPECULATE")) hp->speculate = std::atoi(e) != 0;
+    // narrow 12-B staging for the two-pass partition of a one-value operator (FG_NARROW=0: off, A/B)
+    hp->narrow = hp->st_stride == 2 && !hp->mv && hp->region_bits >= kFineBits;
+    if (const char* e = getenv("FG_NARROW")) hp->narrow = hp->narrow && std::atoi(e) != 0;
+    hp->narrow_ok = hp->narrow;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";
         return FG_EDEVICE;
@@ -3392,6 +3417,7 @@ int fg_reset(fg_handle* h) {
     h->retire_at.clear();
     h->late_rows = 0;
     h->late_horizon = JMIN;
+    h->narrow = h->narrow_ok;
     return FG_OK;
 }
 

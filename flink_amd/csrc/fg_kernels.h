@@ -70,7 +70,8 @@ struct StagedBatch {
     const int64_t* cnt_null;   // is_acc only
     const uint32_t* bucket_off;
     int32_t is_acc;
-    int32_t stride;            // int64 words per record (1 or 2)
+    int32_t stride;            // int64 words per record (1 or 2); 3: narrow 12-B records {int32 key,
+                               // value bits}, 4-B aligned (rec then points at the first one's bytes)
     // regions split since the batch was staged (MergeParams.region_bits - the batch's bits):
     // region r's records are those of bucket r >> shift whose key mix lies in region r
     // (general merge path only)
@@ -79,6 +80,21 @@ struct StagedBatch {
     const int64_t* val1;       // is_acc of a multi-value operator: value slots 1 and 2
     const int64_t* val2;
 };
+
+// Narrow staged record: {int32 key, value bits} in 12 bytes (4-B aligned). The state keeps a
+// key as its fmix64 mix (fg_window.h), recomputed from the 32-bit key by its readers.
+struct __attribute__((packed, aligned(4))) Rec12 {
+    uint32_t k, lo, hi;
+};
+__host__ __device__ __forceinline__ Rec12 rec12_of(int64_t mix, int64_t val) {
+    Rec12 r;
+    r.k = (uint32_t)key_of(mix);
+    r.lo = (uint32_t)(uint64_t)val;
+    r.hi = (uint32_t)((uint64_t)val >> 32);
+    return r;
+}
+__host__ __device__ __forceinline__ int64_t rec12_mix(const Rec12& r) { return mix_of((int64_t)(int32_t)r.k); }
+__host__ __device__ __forceinline__ int64_t rec12_val(const Rec12& r) { return (int64_t)((uint64_t)r.hi << 32 | r.lo); }
 
 struct IngestParams {
     WindowSpec w;
@@ -112,12 +128,17 @@ struct IngestParams {
     unsigned long long* lane_mask;    // bit l: some record has slice index == l (mod lanes)
     unsigned long long* lane_total;   // [kMaxLanes] accepted records per lane
     unsigned int* max_bucket;  // max over workgroups and buckets of a workgroup's bucket count (skew hint)
+    unsigned int* wide;        // pass 1: set when an accepted record's key does not fit 32 bits (the word
+                               // after max_bucket in the counter block)
     // scatter inputs/outputs
     const uint32_t* bucket_base; // [F + 1] exclusive scan of bucket totals (lane-major)
     int64_t lane_shift[kMaxLanes];  // staged position = bucket_base[b] + prefix + lane_shift[lane]
     int64_t* st_rec;           // staged record area (all lanes), AoS {key, val} or {key}
     int32_t st_stride;
-    int32_t pad1;
+    // narrow staging (pass 2): 12-B records {int32 key, value bits} at byte 12 * position, for
+    // batches whose keys all fit 32 bits (pass 1 reports a wider one in *wide: the plan then
+    // stops the speculative pass 2 and the operator goes back to 16-B records)
+    int32_t narrow;
     uint8_t* st_null;          // NULL flags at the same positions (may be null)
     // two-pass partition
     longlong2* tmp;            // pass-1 output: tile (g, j) sorted by coarse bucket at its input offset
@@ -151,6 +172,7 @@ constexpr int kPartStride = kSlots + 1;      // heavy chunks: partial-table entr
 struct MergeParams {
     int32_t region_bits;       // log2(P): state regions
     int32_t fast_stream;       // every batch plain AoS {key, value}, n_batches <= kMaxMergeBatches
+    int32_t narrow;            // fast stream of narrow 12-B records (every batch stride 3)
     int32_t compact;           // compact LDS table (fast_stream, no src tables, < 2^32 records)
     int32_t n_src;
     const TableRef* src;       // device array [n_src]

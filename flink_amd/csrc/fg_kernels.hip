@@ -60,6 +60,18 @@ __device__ __forceinline__ const T __attribute__((address_space(1)))* gbl(const 
     return (const T __attribute__((address_space(1)))*)q;
 }
 
+// narrow record i of a staged batch (global loads of its three words; the load/store
+// vectorizer makes them one global_load_dwordx3)
+__device__ __forceinline__ Rec12 ld_rec12(const void* base, uint64_t i) {
+    const uint32_t __attribute__((address_space(1)))* w =
+        (const uint32_t __attribute__((address_space(1)))*)base + 3 * i;
+    Rec12 r;
+    r.k = w[0];
+    r.lo = w[1];
+    r.hi = w[2];
+    return r;
+}
+
 // A pointer every lane of the wave holds (loaded from LDS, so the compiler cannot tell):
 // moved to SGPRs, so loads off it take the scalar-base + 32-bit-offset form (no 64-bit
 // address arithmetic per lane).
@@ -513,6 +525,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
     const bool has_val = p.val != nullptr;
     const bool has_null = p.vnull != nullptr;
     uint32_t drops = 0, mask = 0;
+    bool wide = false;
     long long qmin = JMAX, qmax = JMIN, qnext = JMAX;
     const int lm = p.lanes - 1;
 
@@ -565,6 +578,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
             int64_t q;
             const int b = classify(p, k, ts, &q, &hk[u]);
             if (b >= 0) {
+                wide |= k != (int64_t)(int32_t)k;   // (narrow staging needs 32-bit keys)
                 atomicAdd(&s_hist[b], 1u);
                 qmin = q < qmin ? q : qmin;
                 qmax = q > qmax ? q : qmax;
@@ -630,6 +644,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
         if (qmax != JMIN) atomicMax(&s_qmax, qmax);
         if (qnext != JMAX) atomicMin(&s_qnext, qnext);
     }
+    if (p.wide && __ballot(wide) != 0 && (tid & 63) == 0) atomicOr(p.wide, 1u);
     __syncthreads();
     uint32_t lane_part = 0, bmax = 0;
     int lane_of = -1;
@@ -675,7 +690,7 @@ int32_t part2_group(int32_t max_tiles) {
     return k < 1 ? 1 : (k > 8 ? 8 : k);
 }
 
-template <bool AOS>
+template <bool AOS, bool NARROW = false>
 __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t group) {
     constexpr int NF = 1 << kFineBits;
     constexpr int R = kPart2Tile / kPart2Threads;   // 8
@@ -867,8 +882,15 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
                 if (wv[u].x == 0x5555 && wv[u].y == 0x7777) p.st_rec[0] = pos;   // keep the reads alive
                 continue;
             }
-            if constexpr (AOS) st2<8>(live ? p.st_rec + 2 * pos : p.sink, wv[u]);
-            else *(live ? p.st_rec + pos : p.sink) = wv[u].x;
+            if constexpr (NARROW) {   // 12-B record {int32 key, value}
+                Rec12* dst = live ? reinterpret_cast<Rec12*>(reinterpret_cast<char*>(p.st_rec) + 12 * pos)
+                                  : reinterpret_cast<Rec12*>(p.sink);
+                *dst = rec12_of(wv[u].x, wv[u].y);
+            } else if constexpr (AOS) {
+                st2<8>(live ? p.st_rec + 2 * pos : p.sink, wv[u]);
+            } else {
+                *(live ? p.st_rec + pos : p.sink) = wv[u].x;
+            }
         }
         if (has_null) {
 #pragma unroll
@@ -987,6 +1009,9 @@ __global__ __launch_bounds__(kScanPlanThreads) void k_scan_plan(IngestParams p, 
         for (int l = 0; l < kMaxLanes; l++) lt[l] = word(p.lane_total + l);
         IngestPlan pl;
         ingest_plan(p, pp, qmin, qmax, mask, lt, &pl);
+        // a key wider than 32 bits under narrow staging: the host switches to 16-B records
+        // (max_bucket and the wide flag share one counter word: max_bucket low, wide high)
+        if (p.narrow && (word(p.max_bucket) >> 32) != 0) pl.ok = 0;
         *a.plan = pl;
         IngestPlan* hp = reinterpret_cast<IngestPlan*>(a.host + a.n_words);
         *hp = pl;
@@ -1025,8 +1050,14 @@ hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
     const int32_t group = part2_group(p.max_tiles);
     const int64_t units = (int64_t)nslots * (1 << (p.region_bits - kFineBits)) * ((p.grid + group - 1) / group);
     if (units == 0) return hipSuccess;
-    if (p.st_stride == 2) hipLaunchKernelGGL(k_part2<true>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
-    else hipLaunchKernelGGL(k_part2<false>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+    if (p.narrow) {
+        if (p.st_stride != 2) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_part2<true, true>), dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+    } else if (p.st_stride == 2) {
+        hipLaunchKernelGGL(k_part2<true>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+    } else {
+        hipLaunchKernelGGL(k_part2<false>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+    }
     return hipGetLastError();
 }
 
@@ -1586,7 +1617,8 @@ struct MergeCursor {
 
 // VTC >= 0: the value op compiled in (kernel vt = val_type | op << 2: the LDS adds, identity and
 // row arithmetic of that op only -- a small straight-line stream loop); -1: read p.val_type
-template <bool C, int VTC, bool MV = false>
+// N12: the fast stream's records are narrow 12-B {int32 key, value} (every batch stride 3)
+template <bool C, int VTC, bool MV = false, bool N12 = false>
 // waves_per_eu(4): 128 VGPRs, so two compact workgroups (16 waves) fit a CU
 __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_waves_per_eu(4))) void k_merge(MergeParams p) {
     constexpr int S = MergeCfg<C, MV>::kSlotsT;
@@ -1666,6 +1698,17 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         // the base comes back from LDS: cast to the global address space so these are
         // global_load_dwordx4 (a flat load is waited for with vmcnt(0) AND lgkmcnt(0),
         // serializing every LDS probe behind the loads in flight)
+        if constexpr (N12) {   // 12-B records: the key's mix recomputed from its 32 bits
+            const void* rec = wave_uniform(s_brec[m.j]);
+            Rec12 v[kMergeU];
+#pragma unroll
+            for (int u = 0; u < kMergeU; u++) {
+                const uint32_t i = m.i0 + u * T + tid;
+                v[u] = ld_rec12(rec, i < m.end ? i : m.end - 1);
+            }
+#pragma unroll
+            for (int u = 0; u < kMergeU; u++) c[u] = make_longlong2(rec12_mix(v[u]), rec12_val(v[u]));
+        } else {
         const GlobalRec rec = (GlobalRec)wave_uniform(s_brec[m.j]);   // the cursor is workgroup-uniform
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
@@ -1674,6 +1717,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             if constexpr ((FG_NT & 16) != 0) v = __builtin_nontemporal_load(&rec[i < m.end ? i : m.end - 1]);
             else v = rec[i < m.end ? i : m.end - 1];
             c[u] = make_longlong2(v.x, v.y);
+        }
         }
     };
     // The home buckets of the chunk's records are read together. A record whose key is in
@@ -2015,6 +2059,16 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                         const bool isnull = vnull != nullptr && vnull[i] != 0;
                         lds_add1<C, MV>(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rc.y, isnull ? 0 : vt, p);
                     }
+                } else if (sb.stride == 3) {   // narrow 12-B records
+                    for (uint32_t i = beg + tid; i < end; i += T) {
+                        const Rec12 rc = ld_rec12(sb.rec, i);
+                        const int64_t k = rec12_mix(rc);
+                        if (!mine(k)) continue;
+                        const int slot = lds_find_or_insert<C, MV>(t, k, full);
+                        if (slot < 0) continue;
+                        const bool isnull = vnull != nullptr && vnull[i] != 0;
+                        lds_add1<C, MV>(t, slot, 1ull, isnull ? 1ull : 0ull, isnull ? 0 : rec12_val(rc), isnull ? 0 : vt, p);
+                    }
                 } else {
                     for (uint32_t i = beg + tid; i < end; i += T) {
                         if (!mine(srec[i])) continue;
@@ -2200,15 +2254,26 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
         }
         return hipGetLastError();
     }
+    const bool n12 = p.fast_stream && p.narrow;   // narrow 12-B staged records
     if (p.compact) {
         if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
         // the compact merge (the TUMBLE fire of plain staged records) per value op
+        if (n12) {
+            switch (p.val_type) {
+                case 1: hipLaunchKernelGGL((k_merge<true, 1, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+                case 2: hipLaunchKernelGGL((k_merge<true, 2, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+                default: hipLaunchKernelGGL((k_merge<true, -1, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            }
+            return hipGetLastError();
+        }
         switch (p.val_type) {
             case 0: hipLaunchKernelGGL((k_merge<true, 0>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
             case 1: hipLaunchKernelGGL((k_merge<true, 1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
             case 2: hipLaunchKernelGGL((k_merge<true, 2>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
             default: hipLaunchKernelGGL((k_merge<true, -1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
         }
+    } else if (n12) {
+        hipLaunchKernelGGL((k_merge<false, -1, false, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     } else {
         hipLaunchKernelGGL((k_merge<false, -1>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     }
@@ -2345,6 +2410,11 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
                         k = rc.x;
 #pragma unroll
                         for (int q = 0; q < NVS; q++) vals[q] = rc.y;
+                    } else if (sb.stride == 3) {   // narrow 12-B records
+                        const Rec12 rc = ld_rec12(sb.rec, (uint64_t)i);
+                        k = rec12_mix(rc);
+#pragma unroll
+                        for (int q = 0; q < NVS; q++) vals[q] = rec12_val(rc);
                     } else {
                         k = gbl(sb.rec)[i];
                     }
@@ -2355,7 +2425,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
                     }
                 }
                 // a record without a value column or a NULL record adds no value
-                const bool novalue = !sb.is_acc && (sb.stride != 2 || cn == 1);
+                const bool novalue = !sb.is_acc && (sb.stride < 2 || cn == 1);
                 // wave pre-reduction of the records equal to the first lane's key (no NULLs)
                 bool done = !valid;
                 const int64_t k0 = __builtin_amdgcn_readfirstlane(k);
@@ -2366,7 +2436,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
 #pragma unroll
                     for (int q = 0; q < NVS; q++) {
                         const int op = vops[q];
-                        part[q] = in && sb.stride == 2 ? vals[q] : vinit[q];
+                        part[q] = in && sb.stride >= 2 ? vals[q] : vinit[q];
                         if (op == 2) {
                             double d = __longlong_as_double(part[q]);
                             for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off);

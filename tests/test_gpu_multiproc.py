@@ -98,11 +98,12 @@ def _rank(rank, port, kind, strings, q):
             round_(mx - DELAY - 1)
         round_((1 << 63) - 1)
         rows = np.concatenate([x for x in out if len(x)]) if any(len(x) for x in out) else None
-        q.put((rank, None if rows is None else rows.tobytes(), None if rows is None else rows.dtype.descr, None))
         for o in (local, glob, kd, ko):
             if o is not None:
                 o.close()
+        torch.cuda.synchronize()
         dist.destroy_process_group()
+        q.put((rank, None if rows is None else rows.tobytes(), None if rows is None else rows.dtype.descr, None))
     except Exception as e:   # reported to the parent
         import traceback
         q.put((rank, None, None, traceback.format_exc() + repr(e)))
@@ -125,7 +126,7 @@ def test_two_processes_two_phase_hip_path_matches_oracle(oracle_mod, kind, strin
         p.join(timeout=60)
     errs = [e for *_, e in res if e]
     assert not errs, errs[0]
-    assert all(p.exitcode == 0 for p in procs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     dt = np.dtype([tuple(x) for x in res[0][2]])
     got = np.concatenate([np.frombuffer(b, dtype=dt) for _, b, _, _ in res if b is not None])
     # the single-phase oracle over both partitions, batch by batch at the min watermark

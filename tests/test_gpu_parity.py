@@ -924,3 +924,33 @@ def test_datastream_allowed_lateness_parity(oracle_mod, name, cfg, kw):
     late = drive_both(oracle_mod, cfg, kw.pop("n"), kw.pop("keys"), kw.pop("batch"), kw.pop("delay"), kw.pop("jitter"),
                       expected_keys=ek, **kw)
     assert late > 0, "the stream should drop some elements beyond the lateness"
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop"])
+def test_narrow_staging_switches_to_wide_keys(oracle_mod, kind):
+    """Narrow 12-B staging (keys within 32 bits, two-pass partition): batches of small keys are
+    staged narrow; the first batch holding a key beyond 32 bits flushes the narrow lanes into
+    their tables and the operator stages 16-B records from then on. Rows equal the oracle's
+    throughout (incl. Long.MIN_VALUE and negative 32-bit keys)."""
+    n, keys, batch = 1_200_000, 200_000, 100_000
+    cfg = cfg_of(kind, 1000 if kind == "tumble" else 3000, 0 if kind == "tumble" else 1000)
+    key, ts, val, _ = make_stream(n, keys, "f64", jitter_ms=800)
+    key = key - keys // 2                                    # negative 32-bit keys too
+    big = np.arange(n) >= n * 6 // 10                         # from 60 %: some keys beyond 32 bits
+    wide = big & (np.arange(n) % 7 == 0)
+    key[wide] = key[wide] * (1 << 33) + 12345
+    key[np.nonzero(wide)[0][:3]] = np.iinfo(np.int64).min
+    g = gpu_mk(cfg, expected_keys=keys, buffer_records=1 << 20)
+    o = oracle_mk(oracle_mod, cfg)
+    for step, (lo, hi, wm) in enumerate(batches_with_watermarks(n, batch, ts, 300)):
+        g.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), "f64", f"step {step}")
+        assert g.late_dropped == o.late_dropped
+    g.process_watermark(JMAX)
+    o.process_watermark(JMAX)
+    assert_rows_equal(g.take_rows(), o.take_rows(), "f64", "final")
+    g.close()
+    o.close()
