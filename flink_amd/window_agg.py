@@ -164,12 +164,9 @@ class WindowAggOperator:
     # -- lifecycle -------------------------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
-            # the in-flight device columns were recorded on the engine's stream: release them
-            # while that stream exists (the caching allocator records an event on it when a
-            # block is freed), then close the handle (fg_close drains and destroys the stream)
-            self._inflight = None
-            self._lib.fg_close(self._h)
+            self._lib.fg_close(self._h)   # drains the engine stream: no column is read any more
             self._h = None
+            self._inflight, self._held = None, []
 
     def __del__(self):
         try:
@@ -225,22 +222,29 @@ class WindowAggOperator:
                 b.val_null = val_null.ctypes.data
             keep = [key, rowtime, val, val_null]
         L.check(self._lib.fg_add_batch(self._h, C.byref(b)), self._h)
-        # device columns stay in use until the work the NEXT call queues on the engine stream
-        # has run (the engine finishes a batch's staging there): hold them until that call, and
-        # tell torch's caching allocator they are used on the engine stream, so that a block
-        # freed afterwards is reused only once the engine stream has passed that point
-        if kdev:
-            self._record_on_engine_stream((key, rowtime, val, val_null))
-        self._inflight = (key, rowtime, val, val_null) if kdev else None
+        self._hold((key, rowtime, val, val_null) if kdev else None)
         del keep
 
-    def _record_on_engine_stream(self, cols):
+    def _hold(self, cols):
+        """Device columns stay in use until the work the NEXT engine call queues has run (the
+        engine finishes a batch's staging there; include/flinkgpu.h, fg_batch). Keep a reference
+        to them until an event recorded on the engine stream after that call has completed, so
+        that torch's caching allocator cannot hand their blocks to other work earlier. (Not
+        record_stream: the allocator would record events on the engine stream when the block is
+        freed, which may be after fg_close destroyed that stream.)"""
+        held = self.__dict__.setdefault("_held", [])
+        prev = self.__dict__.get("_inflight")
         ext = self.__dict__.get("_ext_stream")
-        if ext is None:
-            return   # not torch tensors (CUDA-array-interface objects): the caller keeps them
-        for c in cols:
-            if c is not None and hasattr(c, "record_stream") and getattr(c, "is_cuda", False):
-                c.record_stream(ext)
+        if prev is not None:
+            if ext is None:
+                held.append((None, prev))   # not torch tensors: kept until close
+            else:
+                import torch
+                ev = torch.cuda.Event()
+                ev.record(ext)
+                held.append((ev, prev))
+        self._held = [(e, c) for e, c in held if e is None or not e.query()]
+        self._inflight = cols
 
     def process_rows(self, rows, stride: int, arity: int, key_field: int = 0, rowtime_field: int = 1,
                      val_field: int = 2):
@@ -266,7 +270,7 @@ class WindowAggOperator:
         b.arity, b.key_field, b.rowtime_field = int(arity), int(key_field), int(rowtime_field)
         b.val_field = int(val_field) if self.val_type != L.VAL_NONE else -1
         L.check(self._lib.fg_add_rows(self._h, C.byref(b)), self._h)
-        self._inflight = rows if rdev else None
+        self._hold((rows,) if rdev else None)
         del keep
 
     # -- global phase ----------------------------------------------------------------------------
@@ -304,6 +308,7 @@ class WindowAggOperator:
                 b.min, b.max = arrs[5].ctypes.data, arrs[6].ctypes.data
             keep = arrs
         L.check(self._lib.fg_add_partials(self._h, C.byref(b)), self._h)
+        self._hold(None)
         del keep
 
     # -- processWatermark ---------------------------------------------------------------------
@@ -317,9 +322,11 @@ class WindowAggOperator:
             rc = self._lib.fg_advance_progress(self._h, int(watermark), L.DEVICE, self._dev_rows_ref)
             if rc:
                 L.check(rc, self._h)
+            self._hold(None)
             return self._dev_rows
         r = L.FgRows()
         L.check(self._lib.fg_advance_progress(self._h, int(watermark), L.HOST, C.byref(r)), self._h)
+        self._hold(None)
         return self._host_rows(r)
 
     def _host_rows(self, r: L.FgRows) -> np.ndarray:
@@ -356,6 +363,7 @@ class WindowAggOperator:
     def prepare_snapshot_pre_barrier(self):
         """Flush the staged buffer into the GPU-resident state (RecordsWindowBuffer.flush)."""
         L.check(self._lib.fg_flush(self._h), self._h)
+        self._hold(None)
 
     def snapshot_state(self, copy: bool = True):
         """(state image dict of numpy arrays, timer watermark): the window-aggs ValueState.

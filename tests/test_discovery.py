@@ -24,7 +24,7 @@ def fake_smi(tmp_path, cards=8):
 
 
 def run(args, smi, env_extra=None):
-    env = dict(os.environ, ROCM_SMI=smi)
+    env = dict(os.environ, ROCM_SMI=smi, HIP_BUS_IDS="/nonexistent")   # (card indices as they are)
     env.update(env_extra or {})
     r = subprocess.run(["bash", SCRIPT] + args, capture_output=True, text=True, env=env)
     return r.returncode, r.stdout.strip()
@@ -56,6 +56,31 @@ def test_coordination_mode_gives_disjoint_sets(tmp_path):
     assert rc == 0 and d == "0,1,2,3"
 
 
+def fake_smi_with_bus(tmp_path, buses):
+    """rocm-smi answering --showid and --showbus (`card<i>,<PCI bus>` rows, as captured in
+    profiles/r02/discovery/rocm_smi_showbus.csv)."""
+    p = tmp_path / "rocm-smi"
+    ids = "\\n".join(f"card{i},N/A,0x75a3,0x00,0x75a3,{24656 + i}" for i in range(len(buses)))
+    bus = "\\n".join(f"card{i},{b}" for i, b in enumerate(buses))
+    p.write_text("#!/bin/sh\nif [ \"$1\" = --showbus ]; then printf 'device,PCI Bus\\n" + bus + "\\n'; "
+                 "else printf 'device,Device Name,Device ID,Device Rev,Subsystem ID,GUID\\n" + ids + "\\n'; fi\n")
+    p.chmod(0o755)
+    return str(p)
+
+
+def test_cards_map_to_hip_ordinals_by_pci_bus(tmp_path):
+    """rocm-smi numbers the host's cards, HIP only the visible devices in its own order: the
+    script maps each card to the HIP ordinal of the same PCI bus id (hip-pci-bus-ids) and
+    leaves out the cards HIP does not see."""
+    smi = fake_smi_with_bus(tmp_path, ["0000:0D:00.0", "0000:1A:00.0", "0000:8F:00.0", "0000:9C:00.0"])
+    tool = tmp_path / "busids"
+    tool.write_text("#!/bin/sh\nprintf '0 0000:8f:00.0\\n1 0000:0d:00.0\\n'\n")   # HIP sees cards 2 and 0
+    tool.chmod(0o755)
+    env = {"HIP_BUS_IDS": str(tool)}
+    assert run(["2"], smi, env) == (0, "1,0")        # card0 -> ordinal 1, card2 -> ordinal 0
+    assert run(["3"], smi, env)[0] == 1              # only two cards are visible to HIP
+
+
 @pytest.mark.gpu
 def test_real_rocm_smi_lists_the_visible_gpus():
     """On the GPU box: the script parses the real `rocm-smi --showid --csv` and lists as many
@@ -75,3 +100,23 @@ def test_real_rocm_smi_lists_the_visible_gpus():
     assert r.returncode == 0, r.stderr
     idx = [int(x) for x in r.stdout.strip().split(",")]
     assert len(idx) == n and all(0 <= i < n for i in idx)
+
+
+@pytest.mark.gpu
+def test_real_bus_id_map_matches_hip():
+    """On the GPU box: hip-pci-bus-ids lists every HIP ordinal with its bus id, and the card the
+    script maps to ordinal i has that bus id in `rocm-smi --showbus`."""
+    import shutil
+    tool = os.path.join(ROOT, "flink_amd", "discovery", "hip-pci-bus-ids")
+    if shutil.which("rocm-smi") is None or not os.path.exists(tool):
+        pytest.skip("no rocm-smi or bus-id tool")
+    hip = dict(ln.split() for ln in subprocess.run([tool], capture_output=True, text=True, check=True).stdout.split("\n")
+               if ln.strip())
+    bus = subprocess.run(["rocm-smi", "--showbus", "--csv"], capture_output=True, text=True).stdout
+    cards = {ln.split(",")[1].strip().lower() for ln in bus.splitlines() if ln.startswith("card")}
+    assert hip and all(b in cards for b in hip.values()), (hip, cards)
+    env = dict(os.environ)
+    env.pop("ROCM_SMI", None)
+    r = subprocess.run(["bash", SCRIPT, str(len(hip))], capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stderr
+    assert sorted(r.stdout.strip().split(",")) == sorted(hip)

@@ -71,8 +71,8 @@ def test_pinned_host_batches_overwritten_after_call(oracle_mod, kind):
 def test_device_columns_freed_after_call(oracle_mod):
     """Device columns dropped right after process_batch; the next allocations on torch's
     stream (same sizes, so the caching allocator offers the same blocks) are filled with
-    garbage at once. record_stream on the engine's stream keeps the blocks until the engine
-    has read them (fg_add_batch finishes a batch's staging in the next call)."""
+    garbage at once. The operator holds the columns until an event on the engine's stream after
+    the next call has completed (fg_add_batch finishes a batch's staging in the next call)."""
     import torch
 
     def feed(g, lo, hi, key, ts, val):
@@ -85,6 +85,29 @@ def test_device_columns_freed_after_call(oracle_mod):
         del junk
 
     _drive(oracle_mod, feed)
+
+
+def test_device_columns_outlive_the_operator():
+    """The caller's columns freed after the operator closed (and the cache emptied): nothing may
+    refer to the destroyed engine stream then (a record_stream on it did, and the allocator's
+    free path crashed)."""
+    import torch
+
+    from flink_amd import WindowAggOperator, tumbling
+    n = 200_000
+    k = torch.randint(0, 1000, (n,), dtype=torch.int64, device="cuda")
+    t = torch.arange(n, dtype=torch.int64, device="cuda")
+    v = torch.ones(n, dtype=torch.float64, device="cuda")
+    op = WindowAggOperator(tumbling(1000), aggs=("count", "sum"), expected_keys=1000, buffer_records=1 << 20)
+    op.process_batch(k, t, v)
+    op.process_batch(k[: n // 2], t[: n // 2] + n, v[: n // 2])
+    rows = op.process_watermark((1 << 63) - 1)
+    assert rows["count"].sum() == n + n // 2
+    op.close()
+    del k, t, v, op
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    torch.cuda.synchronize()
 
 
 def test_dictionary_reads_device_rows_after_their_producer():
