@@ -1881,12 +1881,22 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     const int64_t fq0 = std::max<int64_t>(got.qmin, flo), fq1 = std::min<int64_t>(got.qmax, fhi - 1);
     if (fq0 > fq1) return FG_OK;                                            // none inside
     if (p.narrow && got.wide) {
-        // a key wider than 32 bits under narrow staging (the device plan stopped pass 2): the
-        // lanes' narrow passes go into their tables and every later pass stages 16-B records
+        // a key wider than 32 bits under narrow staging (the device plan stopped pass 2; pass 1's
+        // 12-B tile records truncated it): the lanes' narrow passes go into their tables, pass 1
+        // runs again with 16-B tile records (same histogram and bucket bases; the counters it
+        // adds up again are reset before the next pass) and every later pass stays on 16 B
         rc = flush(h);
         if (rc) return rc;
         h->narrow = false;
         p.narrow = 0;
+        {
+            KTimer kt(h, K_PART1, n);
+            HIPCHK(h, launch_part1(p, h->stream));
+        }
+        // (pass 2 reads the histogram as per-workgroup prefixes: convert the rewritten one again)
+        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), p.lanes << p.region_bits,
+                                      p.grid, h->stream));
+        h->counters_clean = false;
     }
     if ((uint64_t)(fq1 - fq0) >= (uint64_t)h->lanes) return -1;              // more slices than lanes
     for (int64_t q = fq0; q <= fq1; q++) {

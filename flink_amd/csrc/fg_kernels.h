@@ -135,9 +135,10 @@ struct IngestParams {
     int64_t lane_shift[kMaxLanes];  // staged position = bucket_base[b] + prefix + lane_shift[lane]
     int64_t* st_rec;           // staged record area (all lanes), AoS {key, val} or {key}
     int32_t st_stride;
-    // narrow staging (pass 2): 12-B records {int32 key, value bits} at byte 12 * position, for
-    // batches whose keys all fit 32 bits (pass 1 reports a wider one in *wide: the plan then
-    // stops the speculative pass 2 and the operator goes back to 16-B records)
+    // narrow staging: pass 1's tile records and pass 2's staged records are 12 B {int32 key,
+    // value bits} at byte 12 * position, while every key seen fits 32 bits (pass 1 reports a
+    // wider one in *wide: the plan then stops the speculative pass 2, the host reruns pass 1
+    // with 16-B records and the operator stays on them)
     int32_t narrow;
     uint8_t* st_null;          // NULL flags at the same positions (may be null)
     // two-pass partition

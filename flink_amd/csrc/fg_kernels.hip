@@ -71,6 +71,13 @@ __device__ __forceinline__ Rec12 ld_rec12(const void* base, uint64_t i) {
     r.hi = w[2];
     return r;
 }
+// narrow record {int32 key, value} i of a 12-B record array (one global_store_dwordx3)
+__device__ __forceinline__ void st_rec12(void* base, uint64_t i, int64_t key, int64_t val) {
+    uint32_t __attribute__((address_space(1)))* w = (uint32_t __attribute__((address_space(1)))*)base + 3 * i;
+    w[0] = (uint32_t)key;
+    w[1] = (uint32_t)(uint64_t)val;
+    w[2] = (uint32_t)((uint64_t)val >> 32);
+}
 
 // A pointer every lane of the wave holds (loaded from LDS, so the compiler cannot tell):
 // moved to SGPRs, so loads off it take the scalar-base + 32-bit-offset form (no 64-bit
@@ -579,6 +586,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
             const int b = classify(p, k, ts, &q, &hk[u]);
             if (b >= 0) {
                 wide |= k != (int64_t)(int32_t)k;   // (narrow staging needs 32-bit keys)
+                if (p.narrow) hk[u] = k;            // narrow tiles carry the key, not its mix
                 atomicAdd(&s_hist[b], 1u);
                 qmin = q < qmin ? q : qmin;
                 qmax = q > qmax ? q : qmax;
@@ -620,9 +628,17 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
             if (has_null) s_nul[slot] = (uint8_t)((nb >> u) & 1u);
         }
         lds_barrier();
-        for (uint32_t i = tid; i < tile_total; i += T) {
-            st2<2>(&p.tmp[t0 + i], s_rec[i]);
-            if (has_null) p.tmp_null[t0 + i] = s_nul[i];
+        if (p.narrow) {   // 12-B tile records {int32 key, value} (a wider key: the host reruns the pass)
+            for (uint32_t i = tid; i < tile_total; i += T) {
+                const longlong2 r = s_rec[i];
+                st_rec12(p.tmp, (uint64_t)(t0 + i), r.x, r.y);
+                if (has_null) p.tmp_null[t0 + i] = s_nul[i];
+            }
+        } else {
+            for (uint32_t i = tid; i < tile_total; i += T) {
+                st2<2>(&p.tmp[t0 + i], s_rec[i]);
+                if (has_null) p.tmp_null[t0 + i] = s_nul[i];
+            }
         }
         lds_barrier();   // staging and the directory row have read the offsets
         for (int c = tid; c <= NC; c += T) s_cc[c] = 0;
@@ -824,7 +840,12 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
                 rr[u] = make_longlong2((long long)src * 0x9E3779B97F4A7C15ll, src);
                 continue;
             }
-            rr[u] = ld2<4>(&p.tmp[src]);
+            if constexpr (NARROW) {   // {int32 key, value}: the key sign-extended, its mix recomputed below
+                const Rec12 r = ld_rec12(p.tmp, src);
+                rr[u] = make_longlong2((long long)(int32_t)r.k, (long long)rec12_val(r));
+            } else {
+                rr[u] = ld2<4>(&p.tmp[src]);
+            }
             if (has_null && p.tmp_null[src] != 0) rn |= 1u << u;
         }
     };
@@ -838,7 +859,8 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
         for (int u = 0; u < R; u++) {
             rf[u] = 0xffffffffu;
             if (base + (uint32_t)(u * kPart2Threads + tid) >= total) continue;
-            const uint32_t f = (uint32_t)((uint64_t)cr[u].x >> (64 - p.region_bits)) & (NF - 1);   // staged mix
+            const int64_t mix = NARROW ? mix_of(cr[u].x) : cr[u].x;   // staged mix (narrow: of the key)
+            const uint32_t f = (uint32_t)((uint64_t)mix >> (64 - p.region_bits)) & (NF - 1);
             rf[u] = (atomicAdd(&s_cnt[f], 1u) << 6) | f;
         }
         lds_barrier();
@@ -883,9 +905,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
                 continue;
             }
             if constexpr (NARROW) {   // 12-B record {int32 key, value}
-                Rec12* dst = live ? reinterpret_cast<Rec12*>(reinterpret_cast<char*>(p.st_rec) + 12 * pos)
-                                  : reinterpret_cast<Rec12*>(p.sink);
-                *dst = rec12_of(wv[u].x, wv[u].y);
+                st_rec12(live ? (void*)p.st_rec : (void*)p.sink, live ? (uint64_t)pos : 0u, wv[u].x, wv[u].y);
             } else if constexpr (AOS) {
                 st2<8>(live ? p.st_rec + 2 * pos : p.sink, wv[u]);
             } else {
@@ -2451,7 +2471,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
                             const int slot = lds_find_or_insert<false, MV>(t, k0, full);
                             if (slot >= 0)
                                 lds_add<false, MV>(t, slot, (unsigned long long)__popcll(m), 0ull, part,
-                                                   sb.stride == 2 ? vt : 0, hp);
+                                                   sb.stride >= 2 ? vt : 0, hp);
                         }
                     }
                 }

@@ -12,17 +12,20 @@
 // aggregation by id is the aggregation by key row, and the id carries the row's key group
 // (FG_KEYHASH_DICT_ID routes by it).
 //
-// Layout in HBM: an open-addressing table of `cap` 16-B slots {tag u64 (a 64-bit hash of the
-// row, 0 = empty), loc u64 (where the row's entry lives in the arena, and its length)} plus the
-// claiming row of a new slot; the arena holds one entry per id, [id i64][row bytes padded to 8],
-// so a probe takes two random accesses (slot, entry). One intern call: k_dict_probe (per row
-// both hashes in one pass over its words, the slot of its tag or a CAS claiming an empty one,
-// and for a slot whose entry an earlier call wrote the byte comparison with that entry), then
-// over the rows whose slot is new in this call only: k_dict_assign (the first claimer allocates
-// the id and writes the entry) and k_dict_verify (the byte comparison). Reservations (pending
-// list, ids, arena bytes) take one atomic per wave. A 64-bit tag shared by distinct rows fails
-// the comparison and is
-// resolved on the host, so ids stay exact whatever the hash.
+// Layout in HBM: an open-addressing table of `cap` 64-B slots -- one memory line -- {tag u64
+// (a 64-bit hash of the row, 0 = empty), loc u64 (where the row's arena entry lives, and its
+// length), id i64, the row's first 40 bytes}; the arena holds one entry per id, [id i64][row
+// bytes padded to 8]. A steady-state lookup is one random access: the slot holds the tag, the
+// id and the bytes to compare (rows of up to 40 bytes -- BinaryRowData key rows of a short
+// string and a fixed field or two). One intern call: k_dict_lookup over every row (both hashes
+// in one pass over its words, the slot of its tag, the byte comparison, the id; rows whose tag
+// is not in the table go to a miss list -- none in a steady state), then over the misses only,
+// in chunks the table has room for: k_dict_probe (the slot of its tag or a CAS claiming an
+// empty one), k_dict_assign (the first claimer of a new slot allocates the id and writes the
+// slot and the entry) and k_dict_verify (the byte comparison of the rows whose slot is new).
+// Reservations (miss and pending lists, ids, arena bytes) take one atomic per wave. A 64-bit
+// tag shared by distinct rows fails the comparison and is resolved on the host, so ids stay
+// exact whatever the hash.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,7 +46,7 @@ namespace {
 
 constexpr int kDictThreads = 256;
 #ifndef FG_DICT_GROW
-#define FG_DICT_GROW 4   // table rebuilt at FG_DICT_GROW x (ids + chunk) slots (>= 2: at most half full)
+#define FG_DICT_GROW 4   // table rebuilt at FG_DICT_GROW x (ids + 1M) slots (>= 2: room for a chunk)
 #endif
 static_assert(FG_DICT_GROW >= 2, "FG_DICT_GROW: the table must stay at most half full after a rebuild");
 constexpr int kIdShift = 40;   // id = key group << kIdShift | ordinal
@@ -63,12 +66,17 @@ __host__ __device__ __forceinline__ int32_t binaryrow_hash_bytes(const uint8_t* 
 
 constexpr uint64_t kNoLoc = ~0ull;   // a slot whose entry is not written yet
 
-// Table slot: the row's 64-bit tag and where its entry lives in the arena (entry offset << 24 |
-// row length); one 16-B access finds both. An arena entry is [id i64][row bytes, padded to 8].
-struct alignas(16) Slot {
+// Table slot (one 64-B line): the row's 64-bit tag, where its entry lives in the arena (entry
+// offset << 24 | row length), its id and its first kSlotWords 4-byte words (zero padded). An
+// arena entry is [id i64][row bytes, padded to 8].
+constexpr int kSlotWords = 10;
+struct alignas(64) Slot {
     unsigned long long tag;   // 0: empty
-    unsigned long long loc;   // kNoLoc until the entry is written
+    unsigned long long loc;   // kNoLoc until the entry (and id, row words) are written
+    long long id;
+    uint32_t row[kSlotWords];
 };
+static_assert(sizeof(Slot) == 64, "one slot per 64-B line");
 __host__ __device__ __forceinline__ uint64_t loc_of(uint64_t entry, int32_t len) { return entry << 24 | (uint32_t)len; }
 
 struct DictDev {
@@ -78,7 +86,8 @@ struct DictDev {
     int32_t* ent_len;    // [ids]
     uint64_t* ent_tag;   // [ids] tag (0: resolved on the host, not in the table)
     uint8_t* arena;
-    unsigned long long* counters;   // [0] ids, [1] arena bytes, [2] collisions, [3] bad rows, [4] pending rows
+    unsigned long long* counters;   // [0] ids, [1] arena bytes, [2] collisions, [3] bad rows, [4] pending rows,
+                                    // [5] entry bytes (k_dict_check), [6] lookup misses
     uint64_t mask;       // cap - 1
 };
 
@@ -102,6 +111,7 @@ struct RowsIn {
     const uint8_t* bytes;   // 4-byte aligned; every row at a multiple of 4, of 4-byte words
     const int64_t* off;
     const int32_t* len;
+    const uint32_t* idx;    // rows idx[0..n) of off / len (the miss list), or null: rows 0..n
     int64_t n;
     int64_t nbytes;
     int32_t max_p;
@@ -165,6 +175,12 @@ __device__ __forceinline__ int64_t entry_id_if_equal(const DictDev& d, uint64_t 
 constexpr int kRegWords = 8;
 __device__ __forceinline__ void row_words(const uint8_t* p, int32_t len, uint32_t (&r)[kRegWords]) {
     const int32_t nw = len >> 2;
+    if (((uintptr_t)p & 15) == 0 && nw == kRegWords) {   // the common 32-B row, 16-B aligned
+        const uint4 a = *reinterpret_cast<const uint4*>(p), b = *reinterpret_cast<const uint4*>(p + 16);
+        r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+        r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+        return;
+    }
     const bool a8 = ((uintptr_t)p & 7) == 0;
 #pragma unroll
     for (int k = 0; k < kRegWords; k += 2) {
@@ -219,6 +235,91 @@ __device__ __forceinline__ int64_t entry_id_if_equal_reg(const DictDev& d, uint6
     return diff == 0 ? *reinterpret_cast<const int64_t*>(e) : -1;
 }
 
+// The id of a written slot if its row equals the row (register words r when `small`, else the
+// words at w): the slot's words first, an entry's bytes past them only for rows longer than the
+// slot holds; -1 for a distinct row with an equal tag.
+__device__ __forceinline__ int64_t slot_id_if_equal(const DictDev& d, const Slot& sl, const uint32_t (&r)[kRegWords],
+                                                    const uint32_t* w, bool small, int32_t len) {
+    if ((int32_t)(sl.loc & 0xFFFFFF) != len) return -1;
+    const int32_t nw = len >> 2;
+    uint32_t diff = 0;
+    if (small) {
+        static_assert(kRegWords <= kSlotWords, "register rows fit the slot");
+#pragma unroll
+        for (int k = 0; k < kRegWords; k++)
+            if (k < nw) diff |= r[k] ^ sl.row[k];
+    } else {
+        for (int k = 0; k < nw && k < kSlotWords; k++) diff |= w[k] ^ sl.row[k];
+        if (diff == 0 && nw > kSlotWords) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(d.arena + (sl.loc >> 24) + 8);
+            for (int k = kSlotWords; k < nw; k++) diff |= w[k] ^ q[k];
+        }
+    }
+    return diff == 0 ? (int64_t)sl.id : -1;
+}
+
+// a slot as four 16-B loads issued together (the line is fetched once)
+__device__ __forceinline__ Slot load_slot(const Slot* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 a = q[0], b = q[1], c = q[2], e = q[3];
+    Slot sl;
+    sl.tag = (unsigned long long)a.x | (unsigned long long)a.y << 32;
+    sl.loc = (unsigned long long)a.z | (unsigned long long)a.w << 32;
+    sl.id = (long long)((unsigned long long)b.x | (unsigned long long)b.y << 32);
+    sl.row[0] = b.z; sl.row[1] = b.w;
+    sl.row[2] = c.x; sl.row[3] = c.y; sl.row[4] = c.z; sl.row[5] = c.w;
+    sl.row[6] = e.x; sl.row[7] = e.y; sl.row[8] = e.z; sl.row[9] = e.w;
+    return sl;
+}
+
+// Lookup of every row of the call (no claims): both hashes, the slot of its tag (one 64-B line
+// holds tag, length, id and the row's first 40 bytes), the byte comparison, the id. A row whose
+// tag is not in the table joins the miss list (counters[6]); a distinct row with an equal tag
+// gets -1 (counters[2], resolved on the host). kg_out (optional) takes every row's key group.
+__global__ __launch_bounds__(kDictThreads) void k_dict_lookup(DictDev d, RowsIn in, int32_t* kg_out, int64_t* id_out,
+                                                              uint32_t* miss) {
+    const int64_t i0 = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
+    const bool valid = i0 < in.n;   // (every lane stays for the wave-wide reservation below)
+    const int64_t i = valid ? i0 : 0;
+    const int32_t len = in.len[i];
+    const uint8_t* rp = in.bytes + in.off[i];
+    const bool small = len <= 4 * kRegWords;
+    uint32_t r[kRegWords];
+    uint64_t t;
+    int32_t fh;
+    if (small) {
+        row_words(rp, len, r);
+        row_hashes_reg(r, len, in.tag_bits, &t, &fh);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kRegWords; k++) r[k] = 0;
+        row_hashes(reinterpret_cast<const uint32_t*>(rp), len, in.tag_bits, &t, &fh);
+    }
+    uint64_t s = fmix64(t) & d.mask;
+    bool found = false;
+    int64_t id = -1;
+    for (; valid;) {
+        const Slot sl = load_slot(&d.slots[s]);
+        if (sl.tag == t) {   // (every slot is written: no claims run beside the lookup)
+            found = true;
+            id = slot_id_if_equal(d, sl, r, reinterpret_cast<const uint32_t*>(rp), small, len);
+            break;
+        }
+        if (sl.tag == 0) break;
+        s = (s + 1) & d.mask;
+    }
+    if (valid) {
+        if (kg_out) kg_out[i] = murmur_hash(fh) % in.max_p;
+        if (found) {
+            if (id < 0) atomicAdd(&d.counters[2], 1ull);
+            id_out[i] = id;
+        }
+    }
+    const bool m = valid && !found;
+    const unsigned long long at = wave_reserve(&d.counters[6], m ? 1u : 0u);
+    if (m) miss[at] = (uint32_t)i;
+}
+
 // Pending rows (their slot is new in this call): row index, slot and key group, for
 // k_dict_assign / k_dict_verify.
 struct Pending {
@@ -233,11 +334,10 @@ struct Pending {
 // distinct row with an equal tag, left to the host). Rows whose slot is new in this call (claimed
 // by them or by an equal-tagged row) join the pending list (none in a steady state). kg_out
 // (optional) takes every row's key group.
-__global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn in, int32_t* kg_out, int64_t* id_out,
-                                                             Pending pend_out) {
-    const int64_t i0 = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    const bool valid = i0 < in.n;   // (every lane stays for the wave-wide reservation below)
-    const int64_t i = valid ? i0 : 0;
+__global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn in, int64_t* id_out, Pending pend_out) {
+    const int64_t j0 = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
+    const bool valid = j0 < in.n;   // (every lane stays for the wave-wide reservation below)
+    const int64_t i = in.idx ? (int64_t)in.idx[valid ? j0 : 0] : (valid ? j0 : 0);
     const int32_t len = in.len[i];
     const uint8_t* rp = in.bytes + in.off[i];
     const bool small = len <= 4 * kRegWords;
@@ -270,8 +370,7 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn i
     }
     const int32_t kg = murmur_hash(fh) % in.max_p;
     if (valid) {
-        if (kg_out) kg_out[i] = kg;
-        if (loc != kNoLoc) {
+        if (loc != kNoLoc) {   // written by an earlier chunk of this call
             const int64_t id = small ? entry_id_if_equal_reg(d, loc, r, len)
                                      : entry_id_if_equal(d, loc, reinterpret_cast<const uint32_t*>(rp), len);
             if (id < 0) atomicAdd(&d.counters[2], 1ull);
@@ -311,7 +410,11 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_assign(DictDev d, RowsIn 
         d.ent_off[ord] = (int64_t)at + 8;
         d.ent_len[ord] = len;
         d.ent_tag[ord] = d.slots[s].tag;
-        d.slots[s].loc = loc_of(at, len);
+        Slot& sl = d.slots[s];
+        sl.id = id;
+        for (int k = 0; k < kSlotWords; k++) sl.row[k] = k < (len >> 2) ? src[k] : 0u;
+        __threadfence();   // the slot's id and words before its loc (read by later chunks' probes)
+        sl.loc = loc_of(at, len);
     }
 }
 
@@ -339,7 +442,13 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_rehash(DictDev d, int64_t
         if (old == 0) break;
         s = (s + 1) & d.mask;
     }
-    d.slots[s].loc = loc_of((uint64_t)(d.ent_off[o] - 8), d.ent_len[o]);
+    const int32_t len = d.ent_len[o];
+    const uint8_t* e = d.arena + d.ent_off[o] - 8;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(e + 8);
+    Slot& sl = d.slots[s];
+    sl.id = *reinterpret_cast<const long long*>(e);
+    for (int k = 0; k < kSlotWords; k++) sl.row[k] = k < (len >> 2) ? w[k] : 0u;
+    sl.loc = loc_of((uint64_t)(d.ent_off[o] - 8), len);
 }
 
 __global__ __launch_bounds__(kDictThreads) void k_dict_gather(DictDev d, int64_t n, const int64_t* ids, int64_t nids,
@@ -354,7 +463,11 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_gather(DictDev d, int64_t
 
 __global__ __launch_bounds__(kDictThreads) void k_slots_clear(Slot* p, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    if (i < n) p[i] = Slot{0ull, kNoLoc};
+    if (i < n) {
+        uint4* q = reinterpret_cast<uint4*>(p + i);
+        q[0] = make_uint4(0u, 0u, 0xffffffffu, 0xffffffffu);   // tag 0, loc kNoLoc
+        q[1] = q[2] = q[3] = make_uint4(0u, 0u, 0u, 0u);
+    }
 }
 
 inline unsigned grid_of(int64_t n) { return (unsigned)((n + kDictThreads - 1) / kDictThreads); }
@@ -403,7 +516,7 @@ struct fg_key_dict {
     int64_t nids = 0;   // ids handed out (host mirror of counters[0])
     int64_t arena_used = 0;
     Buf slots, slot_row, ent_off, ent_len, ent_tag, arena, counters;
-    Buf in_bytes, in_off, in_len, row_tag, row_kg, row_slot, row_pkg, row_id;   // per-call scratch
+    Buf in_bytes, in_off, in_len, row_tag, row_kg, row_slot, row_pkg, row_id, miss;   // per-call scratch
     std::unordered_map<std::string, int64_t> side;   // rows whose tag another row holds
     std::string err;
     // kernel timing (fg_key_dict_set_timing): HIP events around each chunk's probe and its
@@ -616,11 +729,6 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     // k_dict_assign writes a new row's entry at a reserved arena offset without a bound check:
     // the arena holds every row of the call as a new entry
     DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)entry_need + 16, s, (size_t)d->arena_used));
-    // Chunks: the table stays at most half full against every row of a chunk being new, so a
-    // chunk takes at most the table's headroom; the table grows with the ids (at least
-    // kDictChunkMin rows, or as many rows as there are ids, per chunk), not with the call's size
-    // -- a 50M-row micro-batch over 10M keys probes a 64M-slot table (1 GiB), not a 256M one.
-    constexpr int64_t kDictChunkMin = 1 << 22;
     int32_t* kg_dev = nullptr;   // every row's key group, when asked for
     if (out_kg) {
         if (host) {
@@ -630,51 +738,69 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
             kg_dev = out_kg;
         }
     }
-    for (int64_t pos = 0; pos < n;) {
-        const int64_t want = std::min<int64_t>(n - pos, std::max<int64_t>(kDictChunkMin, d->nids));
-        if ((uint64_t)(d->nids + want) * 2 > d->cap)
-            if (int rc = rebuild(d, pow2_at_least(FG_DICT_GROW * (uint64_t)(d->nids + want)))) return rc;
-        const int64_t m = std::min<int64_t>(n - pos, (int64_t)(d->cap / 2) - d->nids);
+    // 1) lookup of every row: one random 64-B slot per row; the misses are listed
+    DCHK(d, d->miss.ensure(4 * (size_t)n, s));
+    unsigned long long* ctr = d->counters.as<unsigned long long>();
+    DCHK(d, hipMemsetAsync(ctr + 6, 0, 8, s));
+    if (d->timing) DCHK(d, hipEventRecord(d->ev[0], s));
+    hipLaunchKernelGGL(k_dict_lookup, dim3(g), dim3(kDictThreads), 0, s, d->dev(), in, kg_dev, ids,
+                       d->miss.as<uint32_t>());
+    if (d->timing) DCHK(d, hipEventRecord(d->ev[1], s));
+    DCHK(d, hipGetLastError());
+    unsigned long long cnt[7];
+    DCHK(d, hipMemcpyAsync(cnt, ctr, sizeof cnt, hipMemcpyDeviceToHost, s));
+    DCHK(d, hipStreamSynchronize(s));
+    if (d->timing) {
+        float ms = 0.f;
+        DCHK(d, hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
+        d->kstat[0].launches++;
+        d->kstat[0].total_ms += ms;
+        d->kstat[0].records += n;
+    }
+    uint64_t collisions = cnt[2];
+    const int64_t nmiss = (int64_t)cnt[6];
+    // 2) the misses, in chunks the table has room for: it stays at most half full even if every
+    // row of a chunk is new. It grows when that room falls under an eighth of the ids (and 1M
+    // rows): to 3 x (ids + 1M) slots rounded up -- sized by the distinct keys, not by the calls.
+    for (int64_t pos = 0; pos < nmiss;) {
+        const int64_t room = (int64_t)(d->cap / 2) - d->nids;
+        if (room < std::max<int64_t>(1 << 20, d->nids / 8))
+            if (int rc = rebuild(d, pow2_at_least(FG_DICT_GROW * (uint64_t)(d->nids + (1 << 20))))) return rc;
+        const int64_t m = std::min<int64_t>(nmiss - pos, (int64_t)(d->cap / 2) - d->nids);
         DCHK(d, d->row_tag.ensure(4 * (size_t)m, s));   // the pending list
         DCHK(d, d->row_slot.ensure(8 * (size_t)m, s));
         DCHK(d, d->row_pkg.ensure(4 * (size_t)m, s));
         RowsIn c = in;
-        c.off = in.off + pos;
-        c.len = in.len + pos;
+        c.idx = d->miss.as<uint32_t>() + pos;
         c.n = m;
-        int64_t* cids = ids + pos;
         const Pending pend{d->row_tag.as<uint32_t>(), d->row_slot.as<uint64_t>(), d->row_pkg.as<int32_t>()};
         const DictDev dv = d->dev();
         const unsigned gm = grid_of(m);
         DCHK(d, hipMemsetAsync(dv.counters + 4, 0, 8, s));
-        if (d->timing) DCHK(d, hipEventRecord(d->ev[0], s));
-        hipLaunchKernelGGL(k_dict_probe, dim3(gm), dim3(kDictThreads), 0, s, dv, c, kg_dev ? kg_dev + pos : nullptr,
-                           cids, pend);
         if (d->timing) DCHK(d, hipEventRecord(d->ev[1], s));
-        const unsigned gp = std::min(gm, 1024u);   // the pending list is short in a steady state
+        hipLaunchKernelGGL(k_dict_probe, dim3(gm), dim3(kDictThreads), 0, s, dv, c, ids, pend);
+        const unsigned gp = std::min(gm, 1024u);
         hipLaunchKernelGGL(k_dict_assign, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend);
-        hipLaunchKernelGGL(k_dict_verify, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend, cids);
+        hipLaunchKernelGGL(k_dict_verify, dim3(gp), dim3(kDictThreads), 0, s, dv, c, pend, ids);
         if (d->timing) DCHK(d, hipEventRecord(d->ev[2], s));
         DCHK(d, hipGetLastError());
-        unsigned long long cnt[5];
-        DCHK(d, hipMemcpyAsync(cnt, d->counters.p, sizeof cnt, hipMemcpyDeviceToHost, s));
+        DCHK(d, hipMemcpyAsync(cnt, ctr, sizeof cnt, hipMemcpyDeviceToHost, s));
         DCHK(d, hipStreamSynchronize(s));
         if (d->timing) {
-            float ms0 = 0.f, ms1 = 0.f;
-            DCHK(d, hipEventElapsedTime(&ms0, d->ev[0], d->ev[1]));
-            DCHK(d, hipEventElapsedTime(&ms1, d->ev[1], d->ev[2]));
-            d->kstat[0].launches++;
-            d->kstat[0].total_ms += ms0;
-            d->kstat[0].records += m;
+            float ms = 0.f;
+            DCHK(d, hipEventElapsedTime(&ms, d->ev[1], d->ev[2]));
             d->kstat[1].launches++;
-            d->kstat[1].total_ms += ms1;
-            d->kstat[1].records += (int64_t)cnt[4];   // pending rows
+            d->kstat[1].total_ms += ms;
+            d->kstat[1].records += m;
         }
         d->nids = (int64_t)cnt[0];
         d->arena_used = (int64_t)cnt[1];
-        if (cnt[2])
-            if (int rc = resolve_collisions(d, host, m, bytes, nbytes, offsets + pos, lengths + pos, cids)) return rc;
         pos += m;
+    }
+    collisions = cnt[2];
+    if (collisions) {   // rows whose tag another row holds: exact ids from the host-side map
+        DCHK(d, hipMemsetAsync(ctr + 2, 0, 8, s));
+        if (int rc = resolve_collisions(d, host, n, bytes, nbytes, offsets, lengths, ids)) return rc;
     }
     if (host) DCHK(d, hipMemcpy(out_id, ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
     if (out_kg && host) DCHK(d, hipMemcpy(out_kg, kg_dev, 4 * (size_t)n, hipMemcpyDeviceToHost));

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU call: the -m gpu suite (or a subset) then bench lines, each step under its own time
 # limit; the first failure ends the call.
-#   OUT=dir TESTS="files" K="-k expr" BENCH="args" BENCH_AB="ENV=val" scripts/gpu_round.sh
+#   OUT=dir TESTS="files" K="-k expr" BENCH="args" BENCH_AB="ENV=val" WL="strings hop" scripts/gpu_round.sh
+# WL: further workloads, one bench line each (--steps 5 --warmup 2, no CPU baseline, no h2d leg)
 set -o pipefail
 OUT=${OUT:-gpurun_out/r03}
 mkdir -p "$OUT"
@@ -18,3 +19,8 @@ if [ -n "$BENCH" ]; then
     tail -c 400 "$OUT/bench_ab.log"
   fi
 fi
+for w in $WL; do
+  timeout -k 10 300 python -u bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline --h2d-records 0 \
+      > "$OUT/wl_$w.log" 2>&1 || { tail -20 "$OUT/wl_$w.log"; exit 1; }
+  tail -c 300 "$OUT/wl_$w.log"
+done

@@ -919,9 +919,9 @@ LATENESS_CASES = [
     ("tumble_i64_l500_purging", dict(cfg_of("tumble", 1000, vt="i64", mode="datastream"), allowed_lateness=500,
                                      purging=True), dict(n=200_000, keys=3000, batch=10_000, delay=100, jitter=1500)),
     ("sliding_i64_l700", dict(cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), allowed_lateness=700),
-     dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=2000)),
+     dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=3500)),   # drops need > 2,000 + 700
     ("sliding_f64_l1500_purging", dict(cfg_of("hop", 3000, 1000, mode="datastream"), allowed_lateness=1500,
-                                       purging=True), dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=2500)),
+                                       purging=True), dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=4500)),
     # hot keys: many late elements of one key in one batch (several rounds of the late path)
     ("tumble_i64_l600_zipf", dict(cfg_of("tumble", 1000, vt="i64", mode="datastream"), allowed_lateness=600),
      dict(n=200_000, keys=5000, batch=20_000, delay=50, jitter=1200, zipf=1.3)),
