@@ -144,7 +144,11 @@ def test_two_processes_two_phase_hip_path_matches_oracle(oracle_mod, kind, strin
     o.process_watermark((1 << 63) - 1)
     exp.append(o.take_rows())
     e = np.concatenate(exp)
-    assert o.late_dropped > 0, "the stream should hold late records"
+    if k_ == "tumble":
+        # hop: a record is dropped only once its slice's LAST window fired (sliceEnd + size -
+        # slide - 1 <= wm), i.e. ~2 s behind the watermark -- beyond this stream's 1.5 s jitter;
+        # its late records are merged into fired-slice state instead (a2)
+        assert o.late_dropped > 0, "the stream should hold late records"
     g = got[np.lexsort((got["key"], got["window_end"]))]
     e = e[np.lexsort((e["key"], e["window_end"]))]
     assert len(g) == len(e), (len(g), len(e))
