@@ -2223,9 +2223,11 @@ int validate(const fg_config* c, std::string* msg) {
                 has_max |= c->aggs[a] == FG_AGG_MAX;
             }
             kinds = (int)sum_family + (int)has_min + (int)has_max;
-            (void)kinds;   // several kinds: a multi-value operator (value slots SUM, MIN, MAX)
-            if ((has_min || has_max) && c->mode != FG_MODE_SQL)
-                snprintf(buf, sizeof buf, "MIN/MAX are SQL aggregates (DataStream windows here reduce with SumAggregator)");
+            // several kinds: a multi-value operator (value slots SUM, MIN, MAX). DataStream
+            // windows reduce ONE aggregation per window (WindowedStream.sum / min / max / minBy /
+            // maxBy: SumAggregator or ComparableAggregator), so one value accumulator there
+            if (kinds > 1 && c->mode != FG_MODE_SQL)
+                snprintf(buf, sizeof buf, "DataStream windows reduce one aggregation (sum, min or max), not a mix");
         }
         if (c->val_type < FG_VAL_NONE || c->val_type > FG_VAL_F64) snprintf(buf, sizeof buf, "bad val_type");
         if (c->val_type == FG_VAL_NONE)
@@ -2360,7 +2362,7 @@ int late_fire(fg_handle* h, int64_t nl) {
         p.wm = wm;
         p.lateness = h->lateness;
         p.purging = h->purging ? 1 : 0;
-        p.vt = h->cfg.val_type;
+        p.vt = h->kvt;   // the value op (SumAggregator's sum, or a DataStream MIN / MAX)
         p.region_bits = h->region_bits;
         p.P = h->P;
         p.cap = table_cap(h->mv);
@@ -2629,9 +2631,12 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             for (int a = 0; a < c.num_aggs; a++)
                 h->agg_slot[a] = c.aggs[a] == FG_AGG_MIN ? 1 : c.aggs[a] == FG_AGG_MAX ? 2 : 0;
         } else {
+            // DataStream DOUBLE MIN / MAX compare by Double.compareTo (ComparableAggregator:
+            // ops 3 / 4, fg_kernels.hip kVtMinT); SQL's and BIGINT's by the primitive comparison
+            const int ds_f64 = c.mode == FG_MODE_DATASTREAM && c.val_type == FG_VAL_F64 ? 2 : 0;
             for (int a = 0; a < c.num_aggs; a++) {
-                if (c.aggs[a] == FG_AGG_MIN) h->kvt = c.val_type | (1 << 2);
-                if (c.aggs[a] == FG_AGG_MAX) h->kvt = c.val_type | (2 << 2);
+                if (c.aggs[a] == FG_AGG_MIN) h->kvt = c.val_type | ((1 + ds_f64) << 2);
+                if (c.aggs[a] == FG_AGG_MAX) h->kvt = c.val_type | ((2 + ds_f64) << 2);
             }
         }
     }

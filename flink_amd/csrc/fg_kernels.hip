@@ -1534,13 +1534,25 @@ constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / sli
 // the operand replaces the accumulator iff `operand < min` (`>` for MAX), Java primitive
 // comparison; a NULL accumulator is the identity (+inf / Long.MAX_VALUE for MIN), and an
 // entry without non-null values (COUNT(v) = 0) emits NULL, so the identity is never seen.
+// Ops 3 / 4 (DOUBLE only): the DataStream MIN / MAX of ComparableAggregator
+// (SJ/api/functions/aggregation/ComparableAggregator.java:83-104 with Comparator.java:48-137),
+// which compare by Double.compareTo: a total order in which -0.0 < +0.0 and NaN (every NaN
+// canonicalised, as doubleToLongBits does) is above +inf -- MAX picks a NaN, MIN avoids it.
+// Their identities are the order's top / bottom bit patterns (NaNs no record carries).
 constexpr int kOpShift = 2;
+constexpr int kVtMinT = 2 | (3 << kOpShift), kVtMaxT = 2 | (4 << kOpShift);
+__device__ __forceinline__ int64_t f64_ord(int64_t b) { return b >= 0 ? b : b ^ 0x7FFFFFFFFFFFFFFFll; }
+__device__ __forceinline__ int64_t f64_canon(int64_t b) {   // Double.doubleToLongBits
+    return (b & 0x7FFFFFFFFFFFFFFFll) > 0x7FF0000000000000ll ? 0x7FF8000000000000ll : b;
+}
 __device__ __forceinline__ int64_t val_identity(int vt) {
     switch (vt) {
         case 1 | (1 << kOpShift): return INT64_MAX;
         case 1 | (2 << kOpShift): return JMIN;
         case 2 | (1 << kOpShift): return 0x7FF0000000000000ll;    // +inf
         case 2 | (2 << kOpShift): return (int64_t)0xFFF0000000000000ull;   // -inf
+        case kVtMinT: return INT64_MAX;   // f64_ord: the top of the total order
+        case kVtMaxT: return -1;          // f64_ord: INT64_MIN, its bottom
         default: return 0;
     }
 }
@@ -1553,6 +1565,8 @@ __device__ __forceinline__ int64_t val_combine(int64_t a, int64_t b, int vt) {
         case 1 | (2 << kOpShift): return b > a ? b : a;
         case 2 | (1 << kOpShift): return __longlong_as_double(b) < __longlong_as_double(a) ? b : a;
         case 2 | (2 << kOpShift): return __longlong_as_double(b) > __longlong_as_double(a) ? b : a;
+        case kVtMinT: a = f64_canon(a); b = f64_canon(b); return f64_ord(b) < f64_ord(a) ? b : a;
+        case kVtMaxT: a = f64_canon(a); b = f64_canon(b); return f64_ord(b) > f64_ord(a) ? b : a;
         default: return 0;
     }
 }
@@ -1562,9 +1576,8 @@ __device__ __forceinline__ int64_t val_combine(int64_t a, int64_t b, int vt) {
 // compare-and-swap loop. The operand replaces the accumulator iff operand < min (> max) as
 // Java's primitive comparison, except that a NaN operand never wins (Java keeps a NaN that
 // arrived first) and -0.0 < +0.0 (Java keeps whichever zero came first): DESIGN.md section 3.
-__device__ __forceinline__ int64_t f64_ord(int64_t b) { return b >= 0 ? b : b ^ 0x7FFFFFFFFFFFFFFFll; }
 __device__ __forceinline__ bool is_f64_minmax(int op) {
-    return op == (2 | (1 << kOpShift)) || op == (2 | (2 << kOpShift));
+    return op == (2 | (1 << kOpShift)) || op == (2 | (2 << kOpShift)) || op == kVtMinT || op == kVtMaxT;
 }
 // the LDS form of a value slot's bits (and back: f64_ord is its own inverse)
 __device__ __forceinline__ int64_t lds_repr(int op, int64_t b) { return is_f64_minmax(op) ? f64_ord(b) : b; }
@@ -1588,6 +1601,8 @@ __device__ __forceinline__ void lds_val(unsigned long long* a, int64_t bits, int
             case 1 | (2 << kOpShift): atomicMax(reinterpret_cast<long long*>(a), (long long)bits); break;
             case 2 | (1 << kOpShift): lds_minmax_f64<true>(a, bits); break;
             case 2 | (2 << kOpShift): lds_minmax_f64<false>(a, bits); break;
+            case kVtMinT: atomicMin(reinterpret_cast<long long*>(a), (long long)f64_ord(f64_canon(bits))); break;
+            case kVtMaxT: atomicMax(reinterpret_cast<long long*>(a), (long long)f64_ord(f64_canon(bits))); break;
             default: break;
         }
     }

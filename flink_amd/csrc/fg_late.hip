@@ -74,7 +74,21 @@ __device__ __forceinline__ int wave_find(const TableRef& t, int64_t r, int cap, 
     return -1;
 }
 
+// acc (+) v under the kernel value op vt = val_type | op << 2: op 0 the sum (SumAggregator),
+// 1 / 2 BIGINT MIN / MAX, 3 / 4 DOUBLE MIN / MAX by Double.compareTo (ComparableAggregator,
+// fg_kernels.hip kVtMinT): the order of canonical bits mapped to ordered integers
+__device__ __forceinline__ int64_t canon_bits(int64_t b) {   // Double.doubleToLongBits
+    return (b & 0x7FFFFFFFFFFFFFFFll) > 0x7FF0000000000000ll ? 0x7FF8000000000000ll : b;
+}
+__device__ __forceinline__ int64_t ord_of(int64_t b) { return b >= 0 ? b : b ^ 0x7FFFFFFFFFFFFFFFll; }
 __device__ __forceinline__ int64_t add_value(int vt, int64_t acc, int64_t v) {
+    switch (vt >> 2) {
+        case 1: return v < acc ? v : acc;
+        case 2: return v > acc ? v : acc;
+        case 3: acc = canon_bits(acc); v = canon_bits(v); return ord_of(v) < ord_of(acc) ? v : acc;
+        case 4: acc = canon_bits(acc); v = canon_bits(v); return ord_of(v) > ord_of(acc) ? v : acc;
+        default: break;
+    }
     if ((vt & 3) == 2) return __double_as_longlong(__longlong_as_double(acc) + __longlong_as_double(v));
     return (int64_t)((uint64_t)acc + (uint64_t)v);   // Java long wrap
 }
@@ -178,7 +192,8 @@ __global__ __launch_bounds__(kLateThreads) void k_late_update(LateRound p) {
     const TableRef t = p.dir.t[d];
     const int64_t r = region_of(p.mix[j], p.region_bits);
     int64_t* base = t.base + r * p.cols * p.cap;
-    const int64_t v = p.vnull && p.vnull[j] ? 0 : p.val[j];
+    int64_t v = p.vnull && p.vnull[j] ? 0 : p.val[j];
+    if ((p.vt >> 2) >= 3) v = canon_bits(v);   // DOUBLE MIN / MAX by compareTo: canonical NaN
     const int64_t nul = p.vnull ? p.vnull[j] : 0;
     int f = p.found[j];
     if (f < 0) {
@@ -209,10 +224,11 @@ __global__ __launch_bounds__(kLateThreads) void k_late_emit(LateRound p) {
         const int64_t e = jadd(se, k * w.slide);   // windows holding the slice: ends se .. se + size - slide
         if (!ds_fired(e, p.wm) || ds_cleanup(e, p.lateness) <= p.wm) continue;
         int64_t cs = 0, cn = 0, sum = (p.vt & 3) == 2 ? __double_as_longlong(0.0) : 0;
+        bool have = false;   // the first slice's accumulator is taken as it is (no identity)
         if (p.purging) {
             cs = 1;
             cn = p.vnull ? p.vnull[j] : 0;
-            sum = cn ? sum : p.val[j];
+            sum = cn ? sum : (p.vt >> 2) >= 3 ? canon_bits(p.val[j]) : p.val[j];
         } else {
             const int64_t ns = w.kind == TUMBLE ? 1 : w.size / w.slice;
             for (int64_t q = 0; q < ns; q++) {   // slices of window e: e - size + slice .. e
@@ -224,7 +240,8 @@ __global__ __launch_bounds__(kLateThreads) void k_late_emit(LateRound p) {
                 const int64_t* base = p.dir.t[d].base + r * p.cols * p.cap;
                 cs += base[p.cap + f];
                 cn += base[2 * p.cap + f];
-                sum = add_value(p.vt, sum, base[3 * p.cap + f]);
+                sum = have ? add_value(p.vt, sum, base[3 * p.cap + f]) : base[3 * p.cap + f];
+                have = true;
             }
         }
         if (lane != 0 || cs == 0) continue;

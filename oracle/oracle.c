@@ -684,6 +684,25 @@ static int is_cleanup_timer(const or_op* op, int64_t ns, int64_t ts) {
     return op->cfg.mode == OR_MODE_DATASTREAM && op->cfg.allowed_lateness > 0 && ts == ds_cleanup_time(op, ns) &&
            ts != jsub(ns, 1);
 }
+/* WindowedStream.min / max (minBy / maxBy) on a DOUBLE field: ComparableAggregator.reduce
+ * SJ/api/functions/aggregation/ComparableAggregator.java:83-104 with Comparator.java:48-137:
+ * MIN keeps value1's field iff value1.compareTo(value2) < 0, else takes value2's (MAX: > 0),
+ * Double.compareTo's total order (-0.0 < +0.0, NaN above +inf, every NaN equal: the
+ * doubleToLongBits canonical form, which the result carries). BIGINT: Long.compareTo, the
+ * primitive order acc_accumulate applies. HeapReducingState.add keeps the first element as is. */
+static int64_t ds_canon(int64_t b) {
+    return (b & INT64_MAX) > 0x7FF0000000000000ll ? 0x7FF8000000000000ll : b;
+}
+static int64_t ds_ord(int64_t b) { return b >= 0 ? b : b ^ INT64_MAX; }
+static void ds_minmax_f64(or_acc* a, int64_t vbits, int first) {
+    int64_t v = ds_canon(vbits), mn, mx;
+    memcpy(&mn, &a->min_d, 8);
+    memcpy(&mx, &a->max_d, 8);
+    if (first || !(ds_ord(mn) < ds_ord(v))) mn = v;   /* c == 0: value1.field := value2.field */
+    if (first || !(ds_ord(mx) > ds_ord(v))) mx = v;
+    memcpy(&a->min_d, &mn, 8);
+    memcpy(&a->max_d, &mx, 8);
+}
 static int ds_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits, uint8_t isnull) {
     (void)isnull;
     int64_t size = op->cfg.size;
@@ -697,7 +716,9 @@ static int ds_process_element(or_op* op, int64_t key, int64_t ts, int64_t vbits,
         if (cleanup <= op->timer_wm) continue;       /* isWindowLate :608-611 */
         skipped = 0;
         or_acc* a = state_put(op, key, end);         /* windowState.add -> SumAggregator.reduce */
+        const int first = a->cnt_star == 0;
         acc_accumulate(a, op->cfg.val_type, vbits, 0);
+        if (op->cfg.val_type == OR_VAL_F64) ds_minmax_f64(a, vbits, first);   /* ComparableAggregator */
         /* EventTimeTrigger.onElement :37-46 (PurgingTrigger.onElement: FIRE -> FIRE_AND_PURGE) */
         if (max_ts <= op->timer_wm) {
             emit_row(op, key, start, end, a, max_ts);  /* emitWindowContents :574-579 */

@@ -25,14 +25,17 @@ def zipf_keys(u, keys, s):
 
 
 def make_stream(n, keys, val_type="f64", t0=1_600_000_000_000, rate_per_ms=100, jitter_ms=0, null_frac=0.0,
-                seed=SEED, key_spread=False, big_ints=False, zipf=0.0, signed=False, cancel=False):
+                seed=SEED, key_spread=False, big_ints=False, zipf=0.0, signed=False, cancel=False, specials=0.0):
     """Returns (key, rowtime, val, isnull) numpy arrays.
 
     rowtime = t0 + i / rate_per_ms (+ uniform jitter in [0, jitter_ms) when out of order);
     keys uniform over [0, keys), or Zipf(zipf) ranks (hot keys) when zipf > 0.
     signed: DOUBLE values uniform in [-1000, 1000) instead of [0, 1000).
     cancel: every odd record repeats the previous record's key and rowtime with the negated
-    value (plus a small perturbation), so (key, window) sums nearly cancel."""
+    value (plus a small perturbation), so (key, window) sums nearly cancel.
+    specials (DOUBLE): that fraction of the values replaced by NaNs (several payloads and
+    signs), -0.0, +0.0, +inf and -inf -- the cases where Double.compareTo and the primitive
+    comparison part ways."""
     i = np.arange(n, dtype=np.uint64)
     u = splitmix64(np.uint64(seed) ^ i)
     u2 = splitmix64(np.uint64(seed * 3 + 1) ^ i)
@@ -57,6 +60,11 @@ def make_stream(n, keys, val_type="f64", t0=1_600_000_000_000, rate_per_ms=100, 
         key[odd] = key[odd - 1]
         ts[odd] = ts[odd - 1]
         val[odd] = -val[odd - 1] + (val[odd] if val_type != "f64" else val[odd] * 1e-9)
+    if specials > 0 and val_type == "f64":
+        sp = np.array([0x7FF8000000000000, 0x7FF0000000000001, -0x0008000000000000, -0x0000000000000001,
+                       -0x8000000000000000, 0, 0x7FF0000000000000, -0x0010000000000000], dtype=np.int64).view(np.float64)
+        pick = (u2 >> np.uint64(20)) % np.uint64(1000) < np.uint64(int(specials * 1000))
+        val[pick] = sp[((u >> np.uint64(50)) % np.uint64(len(sp))).astype(np.int64)[pick]]
     isnull = None
     if null_frac > 0:
         isnull = ((u2 >> np.uint64(40)) % np.uint64(1000) < np.uint64(int(null_frac * 1000))).astype(np.uint8)

@@ -130,8 +130,8 @@ def test_min_max_accumulator_rules():
     then carry SUM, MIN and MAX); validated before any device call."""
     import torch
     import flink_amd as F
-    with pytest.raises(F.WindowSpecError):
-        F.WindowAggOperator(F.tumbling(1000), aggs=("max",), mode="datastream", val_type="i64")
+    with pytest.raises(F.WindowSpecError):   # DataStream reduces one aggregation per window
+        F.WindowAggOperator(F.tumbling(1000), aggs=("sum", "max"), mode="datastream", val_type="i64")
     with pytest.raises(F.WindowSpecError):
         F.WindowAggOperator(F.tumbling(1000), aggs=("count_star", "min"), val_type="none")
     if torch.cuda.is_available():
@@ -141,6 +141,11 @@ def test_min_max_accumulator_rules():
         with pytest.raises(F.FlinkGpuError) as ei:
             F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="i64")
         assert ei.value.code == L.FG_EDEVICE
+    for vt in ("i64", "f64"):   # WindowedStream.min / max (ComparableAggregator)
+        for aggs in (("max",), ("count_star", "min")):
+            with pytest.raises(F.FlinkGpuError) as ei:
+                F.WindowAggOperator(F.tumbling(1000), aggs=aggs, mode="datastream", val_type=vt)
+            assert ei.value.code == L.FG_EDEVICE
     for aggs in (("sum", "min"), ("min", "max"), ("avg", "max")):   # local phase, several accumulators
         with pytest.raises(F.FlinkGpuError) as ei:
             F.WindowAggOperator(F.tumbling(1000), aggs=aggs, val_type="f64", local_partials=True)

@@ -246,7 +246,7 @@ MAX_AGGS = ("count_star", "count", "max")
 # MIN / MAX (Min/MaxAggFunction): one operator per accumulator kind over the paths the SUM
 # family takes -- small-table and two-pass partitions, compact and wide merges, NULLs, late
 # records, hop/cumulate slice merges, Zipf heavy pass (wave pre-reduction by min/max),
-# processing time, daylight-saving zones, DataStream excluded (SumAggregator only)
+# processing time, daylight-saving zones (DataStream: test_datastream_min_max_parity)
 MINMAX_BASE = [c for c in STREAM_CASES if c[0] in (
     "tumble_f64_inorder", "tumble_i64_ooo", "tumble_i64_wrap", "tumble_f64_nulls_late", "tumble_spread_keys",
     "hop_f64", "hop_i64_late", "cumulate_f64", "cumulate_i64_late", "regions_f64_nulls_late",
@@ -259,6 +259,38 @@ MINMAX_CASES = [(f"{m}_{name}", dict(cfg, aggs=aggs), kw) for name, cfg, kw in M
 
 @pytest.mark.parametrize("name,cfg,kw", MINMAX_CASES, ids=[c[0] for c in MINMAX_CASES])
 def test_min_max_parity(oracle_mod, name, cfg, kw):
+    ks = {} if kw.get("zipf") else None
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    if ks is not None:
+        assert ks.get("merge_heavy", {}).get("launches", 0) > 0, ks
+
+
+# DataStream WindowedStream.min / max (minBy / maxBy: the same value for a (key, value) tuple):
+# ComparableAggregator (ComparableAggregator.java:83-104, Comparator.java:48-137); DOUBLE compares
+# by Double.compareTo, so NaN / -0.0 / +0.0 / infinities are exact here (`specials`)
+DS_MINMAX_BASE = [
+    ("ds_tumble_i64", cfg_of("tumble", 1000, vt="i64", mode="datastream"),
+     dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=700)),
+    ("ds_tumble_f64_specials", cfg_of("tumble", 1000, mode="datastream"),
+     dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=700, specials=0.05)),
+    ("ds_sliding_f64_specials", cfg_of("hop", 3000, 1000, mode="datastream"),
+     dict(n=150_000, keys=2000, batch=8_000, delay=100, jitter=1500, specials=0.05)),
+    ("ds_regions_sliding_f64_specials", cfg_of("hop", 3000, 1000, mode="datastream"),
+     dict(n=400_000, keys=100_000, batch=30_000, delay=100, jitter=1500, specials=0.02)),
+    ("ds_zipf_tumble_f64_specials", cfg_of("tumble", 2000, mode="datastream"),
+     dict(n=3_000_000, keys=100_000, batch=1_000_000, delay=0, jitter=0, rate_per_ms=1_000, zipf=1.1, specials=0.01)),
+    ("ds_lateness_tumble_f64_specials", dict(cfg_of("tumble", 1000, mode="datastream"), allowed_lateness=800),
+     dict(n=200_000, keys=3000, batch=10_000, delay=100, jitter=1500, specials=0.05)),
+    ("ds_lateness_sliding_i64_purging", dict(cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"),
+                                             allowed_lateness=1500, purging=True),
+     dict(n=200_000, keys=2000, batch=10_000, delay=100, jitter=4500)),
+]
+DS_MINMAX_CASES = [(f"{m}_{name}", dict(cfg, aggs=("count_star", m)), kw) for name, cfg, kw in DS_MINMAX_BASE
+                   for m in ("min", "max")]
+
+
+@pytest.mark.parametrize("name,cfg,kw", DS_MINMAX_CASES, ids=[c[0] for c in DS_MINMAX_CASES])
+def test_datastream_min_max_parity(oracle_mod, name, cfg, kw):
     ks = {} if kw.get("zipf") else None
     drive_both(oracle_mod, cfg, kstats=ks, **kw)
     if ks is not None:
