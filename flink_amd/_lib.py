@@ -100,7 +100,7 @@ EXPORTS = (
     "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
     "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_stream", "fg_key_dict_set_timing",
     "fg_key_dict_kernel_stats", "fg_key_dict_last_error", "fg_key_dict_close",
-    "fg_binaryrow_hash",
+    "fg_binaryrow_hash", "fg_host_register", "fg_host_unregister",
 )
 
 _lib = None
@@ -178,6 +178,9 @@ def load():
     L.fg_key_dict_close.restype = None
     L.fg_binaryrow_hash.argtypes = [P, C.c_int32]
     L.fg_binaryrow_hash.restype = C.c_int32
+    L.fg_host_register.argtypes = [C.c_int32, P, C.c_int64]
+    L.fg_host_unregister.argtypes = [C.c_int32, P]
+    L.fg_host_register.restype = L.fg_host_unregister.restype = C.c_int
     for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
                "fg_key_dict_copy_arena"):
         getattr(L, fn).restype = C.c_int
@@ -196,3 +199,35 @@ def check(rc: int, handle=None):
     if rc == FG_EINVAL:
         raise WindowSpecError(msg)
     raise FlinkGpuError(rc, msg)
+
+
+class HostRegistration:
+    """fg_host_register over host arrays (numpy arrays / CPU tensors): the pages they span are
+    locked while the context is open, so FG_HOST batches read from them are DMA'd directly --
+    what a JNI shim does once per off-heap MemorySegment of its managed memory."""
+
+    def __init__(self, *arrays, device: int = 0):
+        self.device = int(device)
+        self._ptrs = []
+        self._arrays = arrays   # kept alive while registered
+        L = load()
+        try:
+            for a in arrays:
+                ptr, nbytes = (a.ctypes.data, a.nbytes) if hasattr(a, "ctypes") else \
+                    (a.data_ptr(), a.numel() * a.element_size())
+                check(L.fg_host_register(self.device, ptr, nbytes))
+                self._ptrs.append(ptr)
+        except Exception:
+            self.close()
+            raise
+
+    def close(self):
+        L = load()
+        while self._ptrs:
+            check(L.fg_host_unregister(self.device, self._ptrs.pop()))
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -2513,6 +2513,43 @@ extern "C" {
 
 int fg_abi_version(void) { return FG_ABI_VERSION; }
 
+// Page-locking caller memory (the shim's off-heap MemorySegments): an FG_HOST batch read from
+// a registered range is DMA'd straight from it by hipMemcpyAsync; pageable memory is first
+// staged through the runtime's bounce buffers, chunk by chunk, at about half the link rate.
+int fg_host_register(int32_t device_id, void* p, int64_t bytes) {
+    if (!p || bytes <= 0) {
+        g_open_error = "fg_host_register: null range";
+        return FG_EINVAL;
+    }
+    if (hipSetDevice(device_id) != hipSuccess) {
+        g_open_error = "fg_host_register: bad device";
+        return FG_EDEVICE;
+    }
+    const hipError_t e = hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        g_open_error = std::string("hipHostRegister: ") + hipGetErrorString(e);
+        return e == hipErrorHostMemoryAlreadyRegistered || e == hipErrorInvalidValue ? FG_EINVAL : FG_EDEVICE;
+    }
+    return FG_OK;
+}
+
+int fg_host_unregister(int32_t device_id, void* p) {
+    if (!p) {
+        g_open_error = "fg_host_unregister: null pointer";
+        return FG_EINVAL;
+    }
+    if (hipSetDevice(device_id) != hipSuccess) {
+        g_open_error = "fg_host_unregister: bad device";
+        return FG_EDEVICE;
+    }
+    const hipError_t e = hipHostUnregister(p);
+    if (e != hipSuccess) {
+        g_open_error = std::string("hipHostUnregister: ") + hipGetErrorString(e);
+        return e == hipErrorHostMemoryNotRegistered || e == hipErrorInvalidValue ? FG_EINVAL : FG_EDEVICE;
+    }
+    return FG_OK;
+}
+
 int fg_open(const fg_config* cfg, fg_handle** out) {
     *out = nullptr;
     if (!cfg) {

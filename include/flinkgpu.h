@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 8
+#define FG_ABI_VERSION 9
 
 enum fg_status {
     FG_OK = 0,
@@ -361,6 +361,16 @@ const char* fg_key_dict_last_error(fg_key_dict* d);
 void fg_key_dict_close(fg_key_dict* d);
 /* BinarySection.hashCode of one row (MurmurHashUtils.hashBytesByWords, seed 42); len % 4 == 0. */
 int32_t fg_binaryrow_hash(const uint8_t* row, int32_t len);
+
+/* Page-lock a caller range for FG_HOST input (hipHostRegister): Flink's managed memory is
+ * off-heap MemorySegments (MemorySegmentFactory.allocateOffHeapUnsafeMemory,
+ * CO/core/memory/MemorySegmentFactory.java:130-167; address MemorySegment.getAddress :288)
+ * that live for the operator's life, so a shim registers each segment it hands batches from
+ * once, at open, and unregisters it at close. Batches read from a registered range are DMA'd
+ * directly; pageable ranges are staged by the runtime at a lower rate. Not per handle: the
+ * registration serves every handle on the device. Errors: fg_last_error(NULL). */
+int  fg_host_register(int32_t device_id, void* p, int64_t bytes);
+int  fg_host_unregister(int32_t device_id, void* p);
 
 int  fg_abi_version(void);
 

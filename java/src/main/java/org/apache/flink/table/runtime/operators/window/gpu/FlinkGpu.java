@@ -103,4 +103,13 @@ public final class FlinkGpu {
 
     /** fg_key_dict_close. */
     public static native void dictClose(long d);
+
+    /**
+     * fg_host_register: page-lock a whole direct buffer (an off-heap managed-memory segment,
+     * MemorySegment.wrap) once, so batches handed from it are DMA'd without staging.
+     */
+    public static native void hostRegister(int device, ByteBuffer segment);
+
+    /** fg_host_unregister (at close, before the segment is released to the MemoryManager). */
+    public static native void hostUnregister(int device, ByteBuffer segment);
 }

@@ -96,6 +96,11 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         rowtimes = direct(8L * spec.batchRecords);
         vals = direct(8L * spec.batchRecords);
         nulls = direct(spec.batchRecords);
+        // the staging columns live for the operator's life: page-lock them once, so every
+        // micro-batch is DMA'd straight from them (fg_host_register)
+        for (ByteBuffer b : new ByteBuffer[] {keys, rowtimes, vals, nulls}) {
+            FlinkGpu.hostRegister(spec.device, b);
+        }
         state =
                 backend.getPartitionedState(
                         LongSerializer.INSTANCE.createInstance(),
@@ -356,6 +361,9 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         if (handle != 0) {
             FlinkGpu.close(handle);
             handle = 0;
+            for (ByteBuffer b : new ByteBuffer[] {keys, rowtimes, vals, nulls}) {
+                FlinkGpu.hostUnregister(spec.device, b);
+            }
         }
         if (dict != 0) {
             FlinkGpu.dictClose(dict);

@@ -15,6 +15,8 @@
  *   lateDropped     fg_late_dropped      (numLateRecordsDropped)
  *   close           fg_close
  *   dict*           fg_key_dict_*        (BinaryRowDataKeySelector rows of any key type)
+ *   hostRegister    fg_host_register     (page-lock a managed-memory segment at open: direct DMA)
+ *   hostUnregister  fg_host_unregister   (at close)
  *
  * Buffers: every ByteBuffer argument is a DIRECT buffer (MemorySegment.wrap of an off-heap
  * segment, MemorySegment.java:288,307, or ByteBuffer.allocateDirect) in native byte order;
@@ -293,4 +295,24 @@ JNIEXPORT void JNICALL FN(dictClose)(JNIEnv* env, jclass cls, jlong dp) {
     (void)env;
     (void)cls;
     fg_key_dict_close((fg_key_dict*)(intptr_t)dp);
+}
+
+/* ---- page-locked managed memory --------------------------------------------------------------- */
+
+/* void hostRegister(int device, ByteBuffer segment): the whole direct buffer (an off-heap
+ * MemorySegment wrapped whole, MemorySegment.wrap :307) is page-locked for direct DMA */
+JNIEXPORT void JNICALL FN(hostRegister)(JNIEnv* env, jclass cls, jint device, jobject segment) {
+    (void)cls;
+    void* p = addr(env, segment);
+    if ((*env)->ExceptionCheck(env)) return;
+    const jlong bytes = (*env)->GetDirectBufferCapacity(env, segment);
+    check(env, NULL, fg_host_register(device, p, bytes));
+}
+
+/* void hostUnregister(int device, ByteBuffer segment) */
+JNIEXPORT void JNICALL FN(hostUnregister)(JNIEnv* env, jclass cls, jint device, jobject segment) {
+    (void)cls;
+    void* p = addr(env, segment);
+    if ((*env)->ExceptionCheck(env)) return;
+    check(env, NULL, fg_host_unregister(device, p));
 }

@@ -5,7 +5,8 @@ The reference's callers reuse their input objects as soon as addElement returns
 pinned staging ring the same way. These tests overwrite (or free and reallocate) every input
 buffer immediately after the call that consumed it and require the fired rows to still equal
 the oracle's on the original data:
-  * FG_HOST from PINNED host memory (the DMA reads the caller's buffer directly);
+  * FG_HOST from PINNED host memory (the DMA reads the caller's buffer directly), and from
+    plain host memory page-locked by fg_host_register (a shim's managed-memory segments);
   * FG_DEVICE torch columns dropped right after process_batch (torch's caching allocator
     hands the blocks to the next allocation on the current stream);
   * device key rows interned through the key dictionary straight after a producer kernel on
@@ -66,6 +67,36 @@ def test_pinned_host_batches_overwritten_after_call(oracle_mod, kind):
         nv[:m] = np.nan
 
     _drive(oracle_mod, feed, cfg=cfg)
+
+
+def test_registered_host_segments_overwritten_after_call(oracle_mod):
+    """The shim's managed-memory path (fg_host_register): plain host allocations -- numpy
+    arrays standing in for off-heap MemorySegments -- page-locked once, reused for every batch
+    and scribbled over as soon as process_batch returns; unregistered at the end (a second
+    unregister is an FG_EINVAL, a double register too)."""
+    import flink_amd as F
+    from flink_amd import _lib as L
+    cap = 100_000
+    nk, nt, nv = np.empty(cap, np.int64), np.empty(cap, np.int64), np.empty(cap, np.float64)
+    garbage = np.random.default_rng(11)
+    reg = F.HostRegistration(nk, nt, nv)
+
+    def feed(g, lo, hi, key, ts, val):
+        m = hi - lo
+        nk[:m], nt[:m], nv[:m] = key[lo:hi], ts[lo:hi], val[lo:hi]
+        g.process_batch(nk[:m], nt[:m], nv[:m])          # FG_HOST from registered memory
+        nk[:m] = garbage.integers(0, 1 << 40, m)
+        nt[:m] = garbage.integers(0, 1 << 42, m)
+        nv[:m] = np.nan
+
+    try:
+        with pytest.raises(F.WindowSpecError):   # already registered
+            L.check(L.load().fg_host_register(0, nk.ctypes.data, nk.nbytes))
+        _drive(oracle_mod, feed)
+    finally:
+        reg.close()
+    with pytest.raises(F.WindowSpecError):       # no longer registered
+        L.check(L.load().fg_host_unregister(0, nk.ctypes.data))
 
 
 def test_device_columns_freed_after_call(oracle_mod):
