@@ -19,6 +19,8 @@
 // (ds_cmpst_rtn_b64 / ds_add_u64 / ds_add_f64), never as global atomics.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fg_kernels.h"
 
 namespace fg {
@@ -1399,6 +1401,34 @@ struct LdsTableT<true, true> {
     unsigned long long v[kNV][kCompactSlotsMV + 1];
     uint32_t cs[kCompactSlotsMV + 1];
 };
+// Narrow compact table (staged 12-B records: keys within 32 bits): the slot holds the key
+// itself, so a 4-slot home bucket is ONE 16-B LDS read with an exact compare (the 64-bit mix
+// table reads 32 B). Empty = INT32_MIN; the key INT32_MIN takes the sentinel slot. The home
+// bucket is still picked by the key's mix (its low word; the region is its top bits).
+struct LdsTableN {
+    alignas(16) int32_t key[kCompactSlots + 1];
+    unsigned long long v[1][kCompactSlots + 1];
+    uint32_t cs[kCompactSlots + 1];
+};
+#ifndef FG_NARROW_TABLE
+#define FG_NARROW_TABLE 1
+#endif
+constexpr int32_t kEmpty32 = INT32_MIN;
+// linear probe of the narrow table from `slot` (as lds_find_or_insert_from)
+__device__ __forceinline__ int lds_find_or_insert_from32(LdsTableN& t, int32_t k, uint32_t slot, bool& full) {
+    constexpr int S = kCompactSlots;
+    for (int probe = 0; probe < S; probe++) {
+        const int32_t cur = t.key[slot];
+        if (cur == k) return (int)slot;
+        if (cur == kEmpty32) {
+            const int old = atomicCAS(&t.key[slot], kEmpty32, k);
+            if (old == kEmpty32 || old == k) return (int)slot;
+        }
+        slot = slot + 1 == (uint32_t)S ? 0u : slot + 1;
+    }
+    full = true;
+    return -1;
+}
 
 // Home bucket: the low 32 bits of the key's mix h (the region is its top bits; the low
 // word is independent of them) pick an aligned bucket of kBucket slots -- one 32-bit
@@ -1538,7 +1568,7 @@ constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / sli
 // (SJ/api/functions/aggregation/ComparableAggregator.java:83-104 with Comparator.java:48-137),
 // which compare by Double.compareTo: a total order in which -0.0 < +0.0 and NaN (every NaN
 // canonicalised, as doubleToLongBits does) is above +inf -- MAX picks a NaN, MIN avoids it.
-// Their identities are the order's top / bottom bit patterns (NaNs no record carries).
+// Their identities are the canonical order's top and bottom: NaN and -inf.
 constexpr int kOpShift = 2;
 constexpr int kVtMinT = 2 | (3 << kOpShift), kVtMaxT = 2 | (4 << kOpShift);
 __device__ __forceinline__ int64_t f64_ord(int64_t b) { return b >= 0 ? b : b ^ 0x7FFFFFFFFFFFFFFFll; }
@@ -1551,8 +1581,10 @@ __device__ __forceinline__ int64_t val_identity(int vt) {
         case 1 | (2 << kOpShift): return JMIN;
         case 2 | (1 << kOpShift): return 0x7FF0000000000000ll;    // +inf
         case 2 | (2 << kOpShift): return (int64_t)0xFFF0000000000000ull;   // -inf
-        case kVtMinT: return INT64_MAX;   // f64_ord: the top of the total order
-        case kVtMaxT: return -1;          // f64_ord: INT64_MIN, its bottom
+        // the top / bottom of the canonical total order (canonical themselves, so a combine
+        // that canonicalises its operands keeps them neutral): NaN, -inf
+        case kVtMinT: return 0x7FF8000000000000ll;
+        case kVtMaxT: return (int64_t)0xFFF0000000000000ull;
         default: return 0;
     }
 }
@@ -1611,8 +1643,8 @@ __device__ __forceinline__ void lds_val(unsigned long long* a, int64_t bits, int
 // Accumulate {COUNT(*), NULL count, values} into a slot. vt: the kernel value op for a
 // single-value table; for a multi-value table the value type (0: a NULL record, no value),
 // slot k taking op p.vop[k]. vals: one value per slot (a record's value repeated).
-template <bool C, bool MV, class PV>   // PV: MergeParams or HeavyPlan (vop)
-__device__ __forceinline__ void lds_add(LdsTableT<C, MV>& t, int slot, unsigned long long cs, unsigned long long cn,
+template <bool C, bool MV, class PV, class TT>   // PV: MergeParams or HeavyPlan (vop); TT: the LDS table
+__device__ __forceinline__ void lds_add(TT& t, int slot, unsigned long long cs, unsigned long long cn,
                                         const int64_t* vals, int vt, const PV& p) {
     if constexpr (C) {
         atomicAdd(&t.cs[slot], (uint32_t)cs);
@@ -1629,8 +1661,8 @@ __device__ __forceinline__ void lds_add(LdsTableT<C, MV>& t, int slot, unsigned 
     }
 }
 // the same with one value for every slot (a staged record)
-template <bool C, bool MV>
-__device__ __forceinline__ void lds_add1(LdsTableT<C, MV>& t, int slot, unsigned long long cs, unsigned long long cn,
+template <bool C, bool MV, class TT>
+__device__ __forceinline__ void lds_add1(TT& t, int slot, unsigned long long cs, unsigned long long cn,
                                          int64_t bits, int vt, const MergeParams& p) {
     const int64_t vals[kNV] = {bits, bits, bits};
     lds_add<C, MV>(t, slot, cs, cn, vals, vt, p);
@@ -1662,7 +1694,11 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     constexpr int kRounds = (S + T - 1) / T + 1;    // + 1: the sentinel slot (thread 0)
     constexpr int kMergeU = MergeCfg<C, MV>::kU;
     constexpr uint32_t kChunk = kMergeU * T;
-    __shared__ LdsTableT<C, MV> t;
+    // narrow table: the compact single-value merge over 12-B records keys its LDS table by the
+    // 32-bit key (records then travel as {key, value}; the mix is recomputed for the home bucket)
+    constexpr bool NT = N12 && C && !MV && FG_NARROW_TABLE;
+    using Tab = std::conditional_t<NT, LdsTableN, LdsTableT<C, MV>>;
+    __shared__ Tab t;
     __shared__ uint32_t s_grp[kRounds * kWaves];   // per (round, wave) row counts -> offsets
 #if FG_DENSE_EMIT
     __shared__ uint16_t s_map[S + 1];              // rank -> slot of the region's emitted entries
@@ -1742,7 +1778,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 v[u] = ld_rec12(rec, i < m.end ? i : m.end - 1);
             }
 #pragma unroll
-            for (int u = 0; u < kMergeU; u++) c[u] = make_longlong2(rec12_mix(v[u]), rec12_val(v[u]));
+            for (int u = 0; u < kMergeU; u++)
+                c[u] = make_longlong2(NT ? (int64_t)(int32_t)v[u].k : rec12_mix(v[u]), rec12_val(v[u]));
         } else {
         const GlobalRec rec = (GlobalRec)wave_uniform(s_brec[m.j]);   // the cursor is workgroup-uniform
 #pragma unroll
@@ -1761,8 +1798,13 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     auto insert = [&](const longlong2 (&c)[kMergeU], const MergeCursor& m, bool& full) {
         uint32_t home[kMergeU];
         RecV2 b01[kMergeU], b23[kMergeU];
+        int4 bq[kMergeU];   // narrow table: the home bucket's four keys (one 16-B read)
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
+            if constexpr (NT) {
+                home[u] = lds_home<C, MV>(mix_of(c[u].x));
+                bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
+            } else {
             home[u] = lds_home<C, MV>(c[u].x);
             const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
 #if FG_SWZ
@@ -1777,6 +1819,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             b01[u] = kb[0];
             b23[u] = kBucket == 4 ? kb[1] : b01[u];
 #endif
+            }
         }
         // Hot keys (Zipf regions below the heavy threshold: one key can fill most of a wave):
         // the wave's records equal to its first lane's key are combined with cross-lane
@@ -1814,6 +1857,35 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             if (pcnt[u] == 0) continue;
+            if constexpr (NT) {   // exact 32-bit keys, one bucket read
+                const int32_t k = (int32_t)c[u].x;
+                const int32_t q[4] = {bq[u].x, bq[u].y, bq[u].z, bq[u].w};
+                int hit = -1, empty = -1;
+#pragma unroll
+                for (int j = 3; j >= 0; j--) {
+                    if (q[j] == k) hit = j;
+                    if (q[j] == kEmpty32) empty = j;
+                }
+                constexpr uint32_t S_ = (uint32_t)kCompactSlots;
+                int slot;
+                if (k == kEmpty32) {
+                    slot = (int)S_;
+                } else if (hit >= 0 && (empty < 0 || hit < empty)) {
+                    slot = (int)home[u] + hit;
+                } else if (empty >= 0) {
+                    const uint32_t e = home[u] + (uint32_t)empty;
+                    const int old = atomicCAS(&t.key[e], kEmpty32, k);
+                    if (old == kEmpty32 || old == k) slot = (int)e;
+                    else slot = lds_find_or_insert_from32(t, k, e + 1 >= S_ ? 0u : e + 1, full);
+                } else {
+                    const uint32_t nx = home[u] + 4;
+                    slot = lds_find_or_insert_from32(t, k, nx >= S_ ? 0u : nx, full);
+                }
+                if (slot >= 0) {
+                    if constexpr (FG_WAVE_PRE) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
+                    else lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
+                }
+            } else {
             const int64_t k = c[u].x;
             const int64_t q[kBucket] = FG_BUCKET_KEYS(b01[u], b23[u]);
             int hit = -1, empty = -1;
@@ -1853,6 +1925,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 else lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
             }
             if ((FG_DIAG_MERGE & 1) && slot >= 0) t.cs[slot] = 1;
+            }
         }
     };
 #ifdef FG_STAMPS
@@ -1906,7 +1979,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         const int r = region_at(ri);
         const bool skip = skipped(r);
         for (int i = tid; i <= S; i += T) {
-            t.key[i] = JMIN;
+            if constexpr (NT) t.key[i] = kEmpty32;
+            else t.key[i] = JMIN;
             t.cs[i] = 0;
             if constexpr (!C) t.cn[i] = 0;
 #pragma unroll
@@ -2183,7 +2257,9 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         const unsigned long long obase = s_out_base;
         // one entry out: its table write-back and / or its fired row, at rank `at`
         auto emit_one = [&](int slot, uint32_t at) {
-            const int64_t key = slot == S ? JMIN : t.key[slot];
+            // (the state's form of the key: its mix; a narrow table holds the key itself)
+            const int64_t key = NT ? mix_of(slot == S ? (int64_t)kEmpty32 : (int64_t)t.key[slot])
+                                   : slot == S ? JMIN : (int64_t)t.key[slot];
             unsigned long long cs = t.cs[slot], cn = 0;
             if constexpr (!C) cn = t.cn[slot] & ~kMarkBit;
             int64_t vv[NVS];

@@ -51,7 +51,8 @@ def tolerance_record(ctx, col, rows, relaxed):
 def sort_rows(r):
     # (window_end, key), then the accumulators: with allowed lateness one (key, window) may fire
     # several times in a step (every late element re-fires it, EventTimeTrigger.onElement)
-    return r[np.lexsort((r["sum_d"], r["sum_i"], r["cnt_star"], r["key"], r["window_end"]))]
+    return r[np.lexsort((r["max_d"].view(np.int64), r["max_i"], r["min_d"].view(np.int64), r["min_i"], r["sum_d"],
+                         r["sum_i"], r["cnt_star"], r["key"], r["window_end"]))]
 
 
 F64_EPS = float(np.finfo(np.float64).eps)
