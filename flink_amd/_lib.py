@@ -39,8 +39,9 @@ class FgConfig(C.Structure):
 
 class FgBatch(C.Structure):
     _fields_ = [
-        ("n", C.c_int64), ("location", C.c_int32), ("reserved0", C.c_int32),
+        ("n", C.c_int64), ("location", C.c_int32), ("format", C.c_int32),
         ("key", C.c_void_p), ("rowtime", C.c_void_p), ("val", C.c_void_p), ("val_null", C.c_void_p),
+        ("rowtime_base", C.c_int64),
     ]
 
 
@@ -90,6 +91,7 @@ FLAG_LOCAL_PARTIALS = 2
 FLAG_PROCTIME = 4
 FLAG_WINDOWED = 8
 FLAG_PURGING_TRIGGER = 16
+BATCH_KEY32, BATCH_ROWTIME32, BATCH_VAL32 = 1, 2, 4   # fg_batch.format
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (

@@ -276,6 +276,7 @@ struct fg_handle {
     // event; a buffer is rewritten only after the kernels that read it)
     hipStream_t copy_stream = nullptr;
     DevBuf hb_key[2], hb_ts[2], hb_val[2], hb_null[2];
+    DevBuf hb_narrow[2];   // FG_HOST narrow columns (fg_batch.format) before widening
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     int hslot = 0;
     DevBuf part_tmp, part_tmp_null, part_dir;   // two-pass partition: pass-1 tiles + directory
@@ -2803,6 +2804,11 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 records");
     if (!b->key || !b->rowtime) return h->fail(FG_EINVAL, "batch key/rowtime columns are required");
     if (h->cfg.val_type != FG_VAL_NONE && !b->val) return h->fail(FG_EINVAL, "batch value column is required");
+    const int fmt = b->format;
+    if (fmt & ~(FG_BATCH_KEY32 | FG_BATCH_ROWTIME32 | FG_BATCH_VAL32)) return h->fail(FG_EINVAL, "bad fg_batch.format %d", fmt);
+    if (fmt && b->location != FG_HOST) return h->fail(FG_EINVAL, "narrow fg_batch columns are for FG_HOST batches");
+    if ((fmt & FG_BATCH_VAL32) && h->cfg.val_type != FG_VAL_I64)
+        return h->fail(FG_EINVAL, "FG_BATCH_VAL32 needs a BIGINT value column");
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc0 = settle_pending(h)) return rc0;
     maybe_reduce_lanes(h);
@@ -2830,16 +2836,31 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
         if (grow) HIPCHK(h, hipEventSynchronize(h->ev_free[slot]));   // the old buffers are freed
         HIPCHK(h, h->hb_key[slot].ensure(8 * n));
         HIPCHK(h, h->hb_ts[slot].ensure(8 * n));
+        if (val) HIPCHK(h, h->hb_val[slot].ensure(8 * n));
         HIPCHK(h, hipStreamWaitEvent(h->copy_stream, h->ev_free[slot], 0));
-        HIPCHK(h, hipMemcpyAsync(h->hb_key[slot].p, key, 8 * n, hipMemcpyHostToDevice, h->copy_stream));
-        HIPCHK(h, hipMemcpyAsync(h->hb_ts[slot].p, ts, 8 * n, hipMemcpyHostToDevice, h->copy_stream));
+        // a narrow column (fg_batch.format) crosses the link at 4 bytes a record into
+        // hb_narrow, and is widened into the 8-byte column on the copy stream
+        uint8_t* nw = nullptr;
+        if (fmt) {
+            HIPCHK(h, h->hb_narrow[slot].ensure(12 * n));
+            nw = h->hb_narrow[slot].as<uint8_t>();
+        }
+        auto h2d = [&](DevBuf& wide, const void* src, int bit, int k) -> hipError_t {
+            if (fmt & bit) return hipMemcpyAsync(nw + 4 * n * k, src, 4 * n, hipMemcpyHostToDevice, h->copy_stream);
+            return hipMemcpyAsync(wide.p, src, 8 * n, hipMemcpyHostToDevice, h->copy_stream);
+        };
+        HIPCHK(h, h2d(h->hb_key[slot], key, FG_BATCH_KEY32, 0));
+        HIPCHK(h, h2d(h->hb_ts[slot], ts, FG_BATCH_ROWTIME32, 1));
+        if (val) HIPCHK(h, h2d(h->hb_val[slot], val, FG_BATCH_VAL32, 2));
         key = h->hb_key[slot].as<int64_t>();
         ts = h->hb_ts[slot].as<int64_t>();
-        if (val) {
-            HIPCHK(h, h->hb_val[slot].ensure(8 * n));
-            HIPCHK(h, hipMemcpyAsync(h->hb_val[slot].p, val, 8 * n, hipMemcpyHostToDevice, h->copy_stream));
-            val = h->hb_val[slot].as<int64_t>();
-        }
+        if (val) val = h->hb_val[slot].as<int64_t>();
+        if (fmt)
+            HIPCHK(h, launch_widen_columns((fmt & FG_BATCH_KEY32) ? reinterpret_cast<const int32_t*>(nw) : nullptr,
+                                           (fmt & FG_BATCH_ROWTIME32) ? reinterpret_cast<const uint32_t*>(nw + 4 * n) : nullptr,
+                                           (fmt & FG_BATCH_VAL32) && val ? reinterpret_cast<const int32_t*>(nw + 8 * n) : nullptr,
+                                           n, b->rowtime_base, const_cast<int64_t*>(key), const_cast<int64_t*>(ts),
+                                           const_cast<int64_t*>(val), h->copy_stream));
         if (vnull) {
             HIPCHK(h, h->hb_null[slot].ensure(n));
             HIPCHK(h, hipMemcpyAsync(h->hb_null[slot].p, vnull, n, hipMemcpyHostToDevice, h->copy_stream));
@@ -2895,7 +2916,12 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     // ingest_pass: a lane without room is flushed into its slice table, then the pass stages
     h->records_in += n;
     {
-        int rc0 = b->location == FG_HOST && !h->windowed ? seed_anchor(h, nullptr, b->rowtime) : seed_anchor(h, ts, nullptr);
+        int64_t t_first = 0;   // the batch's first rowtime as the caller holds it
+        if (b->location == FG_HOST && !h->windowed)
+            t_first = (fmt & FG_BATCH_ROWTIME32)
+                          ? (int64_t)((uint64_t)b->rowtime_base + *reinterpret_cast<const uint32_t*>(b->rowtime))
+                          : b->rowtime[0];
+        int rc0 = b->location == FG_HOST && !h->windowed ? seed_anchor(h, nullptr, &t_first) : seed_anchor(h, ts, nullptr);
         if (rc0) return rc0;
     }
     // First pass: every slice -- or, while batches span more slices than the staged lanes

@@ -318,6 +318,8 @@ struct Words16 {
     int32_t n;
 };
 hipError_t launch_store_words(unsigned long long* dst, const Words16& w, hipStream_t s);
+hipError_t launch_widen_columns(const int32_t* k32, const uint32_t* t32, const int32_t* v32, int64_t n, int64_t tbase,
+                                int64_t* key, int64_t* ts, int64_t* val, hipStream_t s);
 hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,
                                      int64_t* out, unsigned long long* off_grid, hipStream_t s);
 hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStream_t s);

@@ -1148,6 +1148,24 @@ __global__ void k_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz,
     if (bad) atomicAdd(off_grid, bad);
 }
 
+// narrow FG_HOST columns (fg_batch.format), copied H2D into buffers of their own, widened
+// into the batch's 8-byte device columns
+__global__ void k_widen_columns(const int32_t* k32, const uint32_t* t32, const int32_t* v32, int64_t n, int64_t tbase,
+                                int64_t* key, int64_t* ts, int64_t* val) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (k32) key[i] = (int64_t)k32[i];
+    if (t32) ts[i] = (int64_t)((uint64_t)tbase + (uint64_t)t32[i]);   // Java long wrap
+    if (v32) val[i] = (int64_t)v32[i];
+}
+hipError_t launch_widen_columns(const int32_t* k32, const uint32_t* t32, const int32_t* v32, int64_t n, int64_t tbase,
+                                int64_t* key, int64_t* ts, int64_t* val, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_widen_columns, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k32, t32, v32, n, tbase,
+                       key, ts, val);
+    return hipGetLastError();
+}
+
 hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,
                                      int64_t* out, unsigned long long* off_grid, hipStream_t s) {
     int64_t blocks = (n + 255) / 256;

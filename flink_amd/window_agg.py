@@ -194,8 +194,11 @@ class WindowAggOperator:
                 ext.wait_stream(cur)
                 return
 
-    def process_batch(self, key, rowtime, val=None, val_null=None):
-        """processElement for every record of a micro-batch (arrival order = index order)."""
+    def process_batch(self, key, rowtime, val=None, val_null=None, rowtime_base=None):
+        """processElement for every record of a micro-batch (arrival order = index order).
+
+        Host columns may be narrow (fg_batch.format, fewer bytes over PCIe): an int32 key
+        column, rowtime as uint32 offsets from `rowtime_base`, an int32 BIGINT value column."""
         self._after_producers((key, rowtime, val, val_null))
         kp, kdev, key = _dev_ptr(key)
         tp, tdev, rowtime = _dev_ptr(rowtime)
@@ -208,15 +211,27 @@ class WindowAggOperator:
             b.location = L.DEVICE
             b.n = int(key.numel() if hasattr(key, "numel") else key.shape[0])
             b.key, b.rowtime, b.val, b.val_null = kp, tp, vp, np_
+            if rowtime_base is not None:   # (narrow columns are FG_HOST only: the engine says so)
+                b.format, b.rowtime_base = L.BATCH_ROWTIME32, int(rowtime_base)
         else:
-            key = np.ascontiguousarray(key, dtype=np.int64)
-            rowtime = np.ascontiguousarray(rowtime, dtype=np.int64)
+            fmt = 0
+            if getattr(key, "dtype", None) == np.int32:
+                fmt |= L.BATCH_KEY32
+            key = np.ascontiguousarray(key, dtype=np.int32 if fmt & L.BATCH_KEY32 else np.int64)
+            if rowtime_base is not None:
+                fmt |= L.BATCH_ROWTIME32
+                b.rowtime_base = int(rowtime_base)
+            rowtime = np.ascontiguousarray(rowtime, dtype=np.uint32 if rowtime_base is not None else np.int64)
             b.location = L.HOST
             b.n = len(key)
             b.key, b.rowtime = key.ctypes.data, rowtime.ctypes.data
             if val is not None and self.val_type != L.VAL_NONE:
-                val = np.ascontiguousarray(val, dtype=np.float64 if self.val_type == L.VAL_F64 else np.int64)
+                narrow = self.val_type == L.VAL_I64 and getattr(val, "dtype", None) == np.int32
+                fmt |= L.BATCH_VAL32 if narrow else 0
+                val = np.ascontiguousarray(val, dtype=np.float64 if self.val_type == L.VAL_F64 else
+                                           np.int32 if narrow else np.int64)
                 b.val = val.ctypes.data
+            b.format = fmt
             if val_null is not None:
                 val_null = np.ascontiguousarray(val_null, dtype=np.uint8)
                 b.val_null = val_null.ctypes.data

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 9
+#define FG_ABI_VERSION 10
 
 enum fg_status {
     FG_OK = 0,
@@ -174,14 +174,26 @@ typedef struct fg_config {
     int64_t allowed_lateness_ms;
 } fg_config;
 
+/* fg_batch.format bits -- narrow FG_HOST columns, so a batch moves fewer bytes over PCIe (the
+ * link, not the kernels, bounds a host-fed operator): a shim whose keys fit 32 bits (INT keys,
+ * dictionary ordinals, most BIGINT ids) and whose micro-batch spans < 2^32 ms hands 4-byte
+ * columns; the engine widens them on the device. 24 -> 16 B per record for a DOUBLE value, 12 B
+ * for a BIGINT value that fits 32 bits. */
+enum fg_batch_format {
+    FG_BATCH_KEY32 = 1,       /* key: int32_t[n], sign-extended */
+    FG_BATCH_ROWTIME32 = 2,   /* rowtime: uint32_t[n], each rowtime_base + the offset */
+    FG_BATCH_VAL32 = 4        /* BIGINT val: int32_t[n], sign-extended (FG_VAL_I64 only) */
+};
+
 typedef struct fg_batch {
     int64_t n;
     int32_t location;             /* fg_location of the column pointers */
-    int32_t reserved0;
-    const int64_t* key;           /* BIGINT grouping key */
-    const int64_t* rowtime;       /* event time, epoch ms (TIMESTAMP(3) compact form) */
+    int32_t format;               /* fg_batch_format bits; 0: 8-byte columns. Non-zero: FG_HOST only */
+    const int64_t* key;           /* BIGINT grouping key (FG_BATCH_KEY32: int32_t[]) */
+    const int64_t* rowtime;       /* event time, epoch ms (TIMESTAMP(3) compact form; FG_BATCH_ROWTIME32: uint32_t[]) */
     const void* val;              /* int64_t[] or double[] per fg_config.val_type; may be NULL for FG_VAL_NONE */
     const uint8_t* val_null;      /* optional: 1 = value is NULL */
+    int64_t rowtime_base;         /* FG_BATCH_ROWTIME32: rowtime[i] = rowtime_base + offset[i] */
 } fg_batch;
 
 typedef struct fg_rows {

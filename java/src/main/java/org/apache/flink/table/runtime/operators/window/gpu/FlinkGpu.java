@@ -23,6 +23,25 @@ public final class FlinkGpu {
     public static native void addBatch(
             long h, ByteBuffer key, ByteBuffer rowtime, ByteBuffer val, ByteBuffer valNull, int n);
 
+    /**
+     * fg_add_batch with fg_batch.format: FORMAT_KEY32 (int keys), FORMAT_ROWTIME32 (rowtime as
+     * unsigned int offsets from rowtimeBase), FORMAT_VAL32 (int BIGINT values) -- 16 instead of
+     * 24 bytes per record over PCIe for a DOUBLE value.
+     */
+    public static native void addBatchNarrow(
+            long h,
+            int format,
+            ByteBuffer key,
+            ByteBuffer rowtime,
+            long rowtimeBase,
+            ByteBuffer val,
+            ByteBuffer valNull,
+            int n);
+
+    public static final int FORMAT_KEY32 = 1;
+    public static final int FORMAT_ROWTIME32 = 2;
+    public static final int FORMAT_VAL32 = 4;
+
     /** fg_add_rows: n packed BinaryRowData fixed-length parts, stride bytes apart. */
     public static native void addRows(
             long h,

@@ -6,6 +6,7 @@
  * Every native of FlinkGpu.java maps one-for-one onto a C-ABI entry point:
  *   open            fg_open              (WindowBuffer.Factory.create / SlicingWindowAggOperatorBuilder.build)
  *   addBatch        fg_add_batch         (SlicingWindowOperator.processElement, batched)
+ *   addBatchNarrow  fg_add_batch         (the same with fg_batch.format: 4-byte key / rowtime / value columns)
  *   addRows         fg_add_rows          (packed BinaryRowData of a MemorySegment)
  *   addPartials     fg_add_partials      (GlobalAggCombiner.combine)
  *   advanceProgress fg_advance_progress  (processWatermark -> advanceProgress + fireWindow)
@@ -108,6 +109,27 @@ JNIEXPORT void JNICALL FN(addBatch)(JNIEnv* env, jclass cls, jlong hp, jobject k
     b.location = FG_HOST;
     b.key = (const int64_t*)addr(env, key);
     b.rowtime = (const int64_t*)addr(env, rowtime);
+    b.val = addr(env, val);
+    b.val_null = (const uint8_t*)addr(env, valNull);
+    if ((*env)->ExceptionCheck(env)) return;
+    check(env, h, fg_add_batch(h, &b));
+}
+
+/* void addBatchNarrow(long h, int format, ByteBuffer key, ByteBuffer rowtime, long rowtimeBase, ByteBuffer val,
+ *                     ByteBuffer valNull, int n) -- fg_batch.format columns (int key, rowtime offsets from
+ *                     rowtimeBase, int BIGINT values): fewer bytes per record over PCIe */
+JNIEXPORT void JNICALL FN(addBatchNarrow)(JNIEnv* env, jclass cls, jlong hp, jint format, jobject key, jobject rowtime,
+                                          jlong rowtimeBase, jobject val, jobject valNull, jint n) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_batch b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.location = FG_HOST;
+    b.format = format;
+    b.key = (const int64_t*)addr(env, key);
+    b.rowtime = (const int64_t*)addr(env, rowtime);
+    b.rowtime_base = rowtimeBase;
     b.val = addr(env, val);
     b.val_null = (const uint8_t*)addr(env, valNull);
     if ((*env)->ExceptionCheck(env)) return;

@@ -96,6 +96,67 @@ def test_registered_host_segments_overwritten_after_call(oracle_mod):
         L.check(L.load().fg_host_register(0, None, 8))
 
 
+@pytest.mark.parametrize("vt", ["f64", "i64"])
+def test_narrow_host_batches(oracle_mod, vt):
+    """fg_batch.format: int32 keys (negative ones too), rowtime as uint32 offsets from a per-batch
+    base, int32 BIGINT values -- widened on the device; rows equal the oracle's on the 8-byte
+    columns. Buffers are overwritten after each call as a shim's staging ring would be."""
+    cap = 100_000
+    nk, nt = np.empty(cap, np.int32), np.empty(cap, np.uint32)
+    nv = np.empty(cap, np.float64 if vt == "f64" else np.int32)
+
+    def feed(g, lo, hi, key, ts, val):
+        m = hi - lo
+        base = int(ts[lo:hi].min()) - 7
+        nk[:m] = key[lo:hi] - 10_000                       # (the oracle sees the same shift)
+        nt[:m] = (ts[lo:hi] - base).astype(np.uint32)
+        nv[:m] = val[lo:hi]
+        g.process_batch(nk[:m], nt[:m], nv[:m], rowtime_base=base)
+        nk[:m], nt[:m] = 12345, 0xFFFFFFFF
+        nv[:m] = -1
+
+    from tests.gpu_adapter import GpuOperator
+    cfg = dict(CFG, val_type=vt)
+    n, keys, batch = 1_200_000, 20_000, 100_000
+    key, ts, val, _ = make_stream(n, keys, vt, jitter_ms=1500)
+    g = GpuOperator(cfg, expected_keys=keys, buffer_records=batch * 4)
+    o = oracle_mk(oracle_mod, cfg)
+    for step, (lo, hi, wm) in enumerate(batches_with_watermarks(n, batch, ts, 500)):
+        feed(g, lo, hi, key, ts, val)
+        o.process_batch(key[lo:hi] - 10_000, ts[lo:hi], val[lo:hi])
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), vt, f"step {step}")
+        assert g.late_dropped == o.late_dropped
+    g.process_watermark((1 << 63) - 1)
+    o.process_watermark((1 << 63) - 1)
+    assert_rows_equal(g.take_rows(), o.take_rows(), vt, "final")
+    g.close()
+    o.close()
+
+
+def test_narrow_batch_format_rules():
+    """FG_BATCH_VAL32 needs a BIGINT value; narrow columns only from the host."""
+    import ctypes as C
+
+    import torch
+    import flink_amd as F
+    from flink_amd import _lib as L
+    op = F.WindowAggOperator(F.tumbling(1000), val_type="f64", expected_keys=1000)
+    z = np.zeros(4, np.int64)
+    b = L.FgBatch(n=4, location=L.HOST, format=L.BATCH_VAL32, key=z.ctypes.data, rowtime=z.ctypes.data,
+                  val=z.ctypes.data)
+    with pytest.raises(F.WindowSpecError):   # a DOUBLE operator's value cannot be narrow
+        L.check(L.load().fg_add_batch(op._h, C.byref(b)), op._h)
+    b.format = 8
+    with pytest.raises(F.WindowSpecError):   # unknown format bit
+        L.check(L.load().fg_add_batch(op._h, C.byref(b)), op._h)
+    with pytest.raises(F.WindowSpecError):   # device columns with a rowtime base
+        op.process_batch(torch.zeros(4, dtype=torch.int64, device="cuda"), torch.zeros(4, dtype=torch.int64, device="cuda"),
+                         torch.zeros(4, dtype=torch.float64, device="cuda"), rowtime_base=5)
+    op.close()
+
+
 def test_device_columns_freed_after_call(oracle_mod):
     """Device columns dropped right after process_batch; the next allocations on torch's
     stream (same sizes, so the caching allocator offers the same blocks) are filled with
