@@ -586,9 +586,11 @@ StagedBatch batch_of(const fg_handle* h, const JobBatch& jb) {
             b.val2 = h->acc_v2.as<int64_t>() + at;
         }
     } else {
-        b.rec = s->narrow ? reinterpret_cast<const int64_t*>(h->st_rec.as<char>() +
-                                                             12 * ((int64_t)l * h->lane_cap + s->lane_start[l]))
+        // narrow records: block-laid from the staged area's base (kRec12Block), the batch's
+        // first record by index
+        b.rec = s->narrow ? h->st_rec.as<int64_t>()
                           : h->st_rec.as<int64_t>() + ((int64_t)l * h->lane_cap + s->lane_start[l]) * h->st_stride;
+        b.rec_first = s->narrow ? (int32_t)((int64_t)l * h->lane_cap + s->lane_start[l]) : 0;
         b.vnull = s->has_null ? h->st_null.as<uint8_t>() + (int64_t)l * h->lane_cap + s->lane_start[l] : nullptr;
         b.stride = s->narrow ? 3 : h->st_stride;
     }
@@ -1699,7 +1701,7 @@ int grow_lanes(fg_handle* h, int64_t need) {
     if (need <= h->lane_cap) return FG_OK;
     if (staged_any(h)) return h->fail(FG_ESTATE, "internal: staged areas grown while holding records");
     const int64_t cap = std::max<int64_t>(need, h->lane_cap + h->lane_cap / 2);
-    HIPCHK(h, h->st_rec.ensure(8 * (size_t)h->st_stride * h->lanes * cap));
+    HIPCHK(h, h->st_rec.ensure(8 * (size_t)h->st_stride * h->lanes * cap + kRec12Block));
     HIPCHK(h, h->st_null.ensure((size_t)h->lanes * cap));
     h->lane_cap = cap;
     return FG_OK;
@@ -1754,7 +1756,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     if (two_pass) {
         p.max_tiles = part1_max_tiles(n, p.grid);
         p.n_coarse = h->F >> kFineBits;
-        HIPCHK(h, h->part_tmp.ensure(16 * (size_t)n));
+        HIPCHK(h, h->part_tmp.ensure(16 * (size_t)n + kRec12Block));   // (+ a narrow block's tail)
         HIPCHK(h, h->part_dir.ensure(2 * (size_t)p.grid * p.max_tiles * (p.n_coarse + 1)));
         p.tmp = h->part_tmp.as<longlong2>();
         p.dir = h->part_dir.as<uint16_t>();
@@ -2770,7 +2772,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     fg_handle* hp = h.get();
     auto chk = [&](hipError_t e) { return e == hipSuccess; };
     hp->st_stride = cfg->val_type == FG_VAL_NONE ? 1 : 2;
-    bool ok = chk(hp->st_rec.ensure(8 * (size_t)hp->st_stride * hp->lanes * hp->lane_cap)) &&
+    bool ok = chk(hp->st_rec.ensure(8 * (size_t)hp->st_stride * hp->lanes * hp->lane_cap + kRec12Block)) &&
               chk(hp->st_null.ensure((size_t)hp->lanes * hp->lane_cap)) &&
               chk(hp->hist.ensure(4 * (size_t)hp->F * hp->grid)) &&
               chk(hp->totals.ensure(4 * ((size_t)hp->F + 1))) &&

@@ -71,18 +71,20 @@ struct StagedBatch {
     const uint32_t* bucket_off;
     int32_t is_acc;
     int32_t stride;            // int64 words per record (1 or 2); 3: narrow 12-B records {int32 key,
-                               // value bits}, 4-B aligned (rec then points at the first one's bytes)
+                               // value bits} in 64-record blocks (rec: the staged area's base; the
+                               // batch's records are rec_first, rec_first + 1, ...)
     // regions split since the batch was staged (MergeParams.region_bits - the batch's bits):
     // region r's records are those of bucket r >> shift whose key mix lies in region r
     // (general merge path only)
     int32_t shift;
-    int32_t pad0;
+    int32_t rec_first;         // stride 3: block index of the batch's first record
     const int64_t* val1;       // is_acc of a multi-value operator: value slots 1 and 2
     const int64_t* val2;
 };
 
 // Narrow staged record: {int32 key, value bits} in 12 bytes (4-B aligned). The state keeps a
 // key as its fmix64 mix (fg_window.h), recomputed from the 32-bit key by its readers.
+constexpr int kRec12Block = 64 * 12;   // 64 narrow records: 64 int32 keys, then 64 values
 struct __attribute__((packed, aligned(4))) Rec12 {
     uint32_t k, lo, hi;
 };

@@ -62,23 +62,28 @@ __device__ __forceinline__ const T __attribute__((address_space(1)))* gbl(const 
     return (const T __attribute__((address_space(1)))*)q;
 }
 
-// narrow record i of a staged batch (global loads of its three words; the load/store
-// vectorizer makes them one global_load_dwordx3)
+// Narrow 12-B records {int32 key, value bits} in blocks of 64 (kRec12Block bytes): the block's
+// 64 keys (256 B), then its 64 values (512 B), record i in block i / 64 at lane i % 64. A
+// wave's consecutive records are then one 4-B and one 8-B coalesced, naturally aligned access
+// each (a packed 12-B record took unaligned dwordx3 accesses: pass 2's stores ran 1.7x slower
+// than its 16-B ones). Indices are absolute from the buffer's base (a staged batch's first
+// record is StagedBatch.rec_first), so batches appended to a lane share its blocks.
 __device__ __forceinline__ Rec12 ld_rec12(const void* base, uint64_t i) {
-    const uint32_t __attribute__((address_space(1)))* w =
-        (const uint32_t __attribute__((address_space(1)))*)base + 3 * i;
+    const char __attribute__((address_space(1)))* b =
+        (const char __attribute__((address_space(1)))*)base + (i >> 6) * kRec12Block;
+    const uint32_t k = *((const uint32_t __attribute__((address_space(1)))*)b + (i & 63));
+    const uint64_t v = *((const uint64_t __attribute__((address_space(1)))*)(b + 256) + (i & 63));
     Rec12 r;
-    r.k = w[0];
-    r.lo = w[1];
-    r.hi = w[2];
+    r.k = k;
+    r.lo = (uint32_t)v;
+    r.hi = (uint32_t)(v >> 32);
     return r;
 }
-// narrow record {int32 key, value} i of a 12-B record array (one global_store_dwordx3)
+// narrow record {int32 key, value} i of a block-laid record array
 __device__ __forceinline__ void st_rec12(void* base, uint64_t i, int64_t key, int64_t val) {
-    uint32_t __attribute__((address_space(1)))* w = (uint32_t __attribute__((address_space(1)))*)base + 3 * i;
-    w[0] = (uint32_t)key;
-    w[1] = (uint32_t)(uint64_t)val;
-    w[2] = (uint32_t)((uint64_t)val >> 32);
+    char __attribute__((address_space(1)))* b = (char __attribute__((address_space(1)))*)base + (i >> 6) * kRec12Block;
+    *((uint32_t __attribute__((address_space(1)))*)b + (i & 63)) = (uint32_t)key;
+    *((uint64_t __attribute__((address_space(1)))*)(b + 256) + (i & 63)) = (uint64_t)val;
 }
 
 // A pointer every lane of the wave holds (loaded from LDS, so the compiler cannot tell):
@@ -1725,6 +1730,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
     __shared__ const longlong2* s_brec[kMaxMergeBatches];     // fast path: batch record bases
+    __shared__ uint32_t s_bfirst[kMaxMergeBatches];            //   and (narrow) their first record
     __shared__ uint32_t s_rng[3][kMaxMergeBatches][2];         // fast path: [ri % 3][batch] = (beg, end)
     __shared__ uint32_t s_soff[kMaxSrcFlat + 1];               // source tables: entry prefix of the region
     __shared__ const int64_t* s_sbase[kMaxSrcFlat];            //   and each table's region base
@@ -1789,11 +1795,12 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         // serializing every LDS probe behind the loads in flight)
         if constexpr (N12) {   // 12-B records: the key's mix recomputed from its 32 bits
             const void* rec = wave_uniform(s_brec[m.j]);
+            const uint32_t first = __builtin_amdgcn_readfirstlane(s_bfirst[m.j]);
             Rec12 v[kMergeU];
 #pragma unroll
             for (int u = 0; u < kMergeU; u++) {
                 const uint32_t i = m.i0 + u * T + tid;
-                v[u] = ld_rec12(rec, i < m.end ? i : m.end - 1);
+                v[u] = ld_rec12(rec, (uint64_t)first + (i < m.end ? i : m.end - 1));
             }
 #pragma unroll
             for (int u = 0; u < kMergeU; u++)
@@ -1979,7 +1986,10 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         return cur.ri == ri && cur.ok;
     };
     if (fast) {
-        if (tid < nb) s_brec[tid] = reinterpret_cast<const longlong2*>(p.batches[tid].rec);
+        if (tid < nb) {
+            s_brec[tid] = reinterpret_cast<const longlong2*>(p.batches[tid].rec);
+            s_bfirst[tid] = (uint32_t)p.batches[tid].rec_first;
+        }
         for (int q = tid; q < 2 * nb; q += T) {   // ranges of regions 0 and 1
             const int ri = q / nb, j = q % nb;
             uint32_t beg = 0, end = 0;
@@ -2188,7 +2198,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     }
                 } else if (sb.stride == 3) {   // narrow 12-B records
                     for (uint32_t i = beg + tid; i < end; i += T) {
-                        const Rec12 rc = ld_rec12(sb.rec, i);
+                        const Rec12 rc = ld_rec12(sb.rec, (uint64_t)sb.rec_first + i);
                         const int64_t k = rec12_mix(rc);
                         if (!mine(k)) continue;
                         const int slot = lds_find_or_insert<C, MV>(t, k, full);
@@ -2540,7 +2550,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
 #pragma unroll
                         for (int q = 0; q < NVS; q++) vals[q] = rc.y;
                     } else if (sb.stride == 3) {   // narrow 12-B records
-                        const Rec12 rc = ld_rec12(sb.rec, (uint64_t)i);
+                        const Rec12 rc = ld_rec12(sb.rec, (uint64_t)sb.rec_first + (uint64_t)i);
                         k = rec12_mix(rc);
 #pragma unroll
                         for (int q = 0; q < NVS; q++) vals[q] = rec12_val(rc);

@@ -111,7 +111,7 @@ def test_narrow_host_batches(oracle_mod, vt):
         nk[:m] = key[lo:hi] - 10_000                       # (the oracle sees the same shift)
         nt[:m] = (ts[lo:hi] - base).astype(np.uint32)
         nv[:m] = val[lo:hi]
-        g.process_batch(nk[:m], nt[:m], nv[:m], rowtime_base=base)
+        g.op.process_batch(nk[:m], nt[:m], nv[:m], rowtime_base=base)
         nk[:m], nt[:m] = 12345, 0xFFFFFFFF
         nv[:m] = -1
 
