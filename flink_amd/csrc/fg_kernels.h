@@ -14,7 +14,10 @@ constexpr int kSlots = 1 << kSlotBits;        // 4096 slots x 32 B = 128 KiB of 
 constexpr int kRegionCap = 3584;              // max entries per region in HBM (87.5 % of kSlots)
 constexpr int kMergeThreads = 1024;           // persistent merge: one 1024-thread workgroup per CU
 constexpr int kCompactSlots = 3584;           // compact merge table: 3,584 x 20 B = 70 KiB of LDS
-constexpr int kCompactMergeThreads = 512;     // compact merge: two 512-thread workgroups per CU
+#ifndef FG_COMPACT_T
+#define FG_COMPACT_T 512
+#endif
+constexpr int kCompactMergeThreads = FG_COMPACT_T;   // compact merge: two 512-thread workgroups per CU
 // Several value accumulators over the one value column (SUM family + MIN + MAX in one
 // operator, the reference's generated accumulator row, AggsHandlerCodeGenerator.scala:578-700):
 // three value slots per entry, so the LDS tables hold fewer slots and regions fewer entries

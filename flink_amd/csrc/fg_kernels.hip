@@ -1375,24 +1375,28 @@ struct MergeCfg<false, false> {
     static constexpr int kSlotsT = kSlots;
     static constexpr int kThreads = kMergeThreads;
     static constexpr int kU = FG_WIDE_U;   // 1,024 threads: 128 VGPRs
+    static constexpr int kWavesPerEu = 4;
 };
 template <>
 struct MergeCfg<true, false> {
     static constexpr int kSlotsT = kCompactSlots;
     static constexpr int kThreads = kCompactMergeThreads;
     static constexpr int kU = FG_MERGE_U;
+    static constexpr int kWavesPerEu = kCompactMergeThreads / 128;   // two workgroups per CU
 };
 template <>
 struct MergeCfg<false, true> {   // multi-value: one 1,024-thread workgroup per CU
     static constexpr int kSlotsT = kSlotsMV;
     static constexpr int kThreads = kMergeThreads;
     static constexpr int kU = FG_WIDE_U;
+    static constexpr int kWavesPerEu = 4;
 };
 template <>
 struct MergeCfg<true, true> {    // multi-value compact: 108 KiB, one 1,024-thread workgroup per CU
     static constexpr int kSlotsT = kCompactSlotsMV;
     static constexpr int kThreads = kMergeThreads;
     static constexpr int kU = FG_MERGE_U;
+    static constexpr int kWavesPerEu = 4;
 };
 
 // v[k][slot]: value slot k (one slot; kNV for a multi-value operator)
@@ -1709,8 +1713,9 @@ struct MergeCursor {
 // row arithmetic of that op only -- a small straight-line stream loop); -1: read p.val_type
 // N12: the fast stream's records are narrow 12-B {int32 key, value} (every batch stride 3)
 template <bool C, int VTC, bool MV = false, bool N12 = false>
-// waves_per_eu(4): 128 VGPRs, so two compact workgroups (16 waves) fit a CU
-__global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_waves_per_eu(4))) void k_merge(MergeParams p) {
+// waves_per_eu(4): 128 VGPRs, so two 512-thread compact workgroups (16 waves) fit a CU (8 and 64
+// VGPRs for two 1,024-thread ones, FG_COMPACT_T)
+__global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_waves_per_eu(MergeCfg<C, MV>::kWavesPerEu))) void k_merge(MergeParams p) {
     constexpr int S = MergeCfg<C, MV>::kSlotsT;
     constexpr int T = MergeCfg<C, MV>::kThreads;
     constexpr int kWaves = T / 64;
