@@ -329,30 +329,57 @@ def h2d_leg(args, wl, window, aggs, expected_keys, dev):
     torch.cuda.empty_cache()
     op = F.WindowAggOperator(window, aggs=aggs, val_type="f64", expected_keys=expected_keys,
                              buffer_records=max(4 * args.batch, 1 << 26), device=dev.index)
-
-    def run():
-        op.reset()
-        rows = 0
+    # the narrow form a shim hands when its keys fit 32 bits (fg_batch.format): int32 keys and
+    # rowtime offsets from each micro-batch's first rowtime -- 16 B per record over the link
+    nk = nt = bases = None
+    if args.keys < (1 << 31):
+        nk = torch.empty(n, dtype=torch.int32).pin_memory()
+        nt = torch.empty(n, dtype=torch.int32).pin_memory()
+        bases = []
         for lo in range(0, n, args.batch):
             hi = min(n, lo + args.batch)
-            op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi])
+            base = int(ht[lo:hi].min())
+            bases.append(base)
+            nk[lo:hi].copy_(hk[lo:hi])
+            nt[lo:hi].copy_((ht[lo:hi] - base).to(torch.int32))   # (uint32 offsets: < 2^31 here)
+
+    def run(narrow):
+        op.reset()
+        rows = 0
+        for bi, lo in enumerate(range(0, n, args.batch)):
+            hi = min(n, lo + args.batch)
+            if narrow:
+                op.process_batch(nk[lo:hi], nt[lo:hi].numpy().view("uint32"), hv[lo:hi], rowtime_base=bases[bi])
+            else:
+                op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi])
             for wm in watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"]):
                 rows += op.process_watermark(wm, device_output=True).n
         rows += op.process_watermark(JMAX, device_output=True).n
         op.synchronize()
         return rows
-    run()   # warm-up
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rows = run()
-    el = time.perf_counter() - t0
+
+    def timed(narrow):
+        run(narrow)   # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rows = run(narrow)
+        return rows, time.perf_counter() - t0
+    rows, el = timed(False)
+    narrow = None
+    if nk is not None:
+        nrows, nel = timed(True)
+        assert nrows == rows, (nrows, rows)
+        narrow = {"value": n / nel, "seconds": nel, "pcie_gbs": 16 * n / nel / 1e9, "bytes_per_record": 16,
+                  "note": "the same job as narrow FG_HOST batches (fg_batch.format: int32 keys, rowtime as uint32 "
+                          "offsets from the batch's first rowtime, widened on the device)"}
     op.close()
-    del hk, ht, hv
+    del hk, ht, hv, nk, nt
     link = h2d_link_peak(dev)
     gbs = 24 * n / el / 1e9
     return {"value": n / el, "unit": "records/s", "records": n, "rows_fired": rows, "seconds": el,
             "pcie_gbs": gbs, "link_peak_gbs": link, "link_frac": gbs / link if link else None,
             "job_roofline_frac": (24 * n + 48 * rows) / el / (HBM_PEAK_GBS * 1e9),
+            "narrow": narrow,
             "note": "SURVEY 8(d) contract timing (kernels + H2D of columnar batches from pinned host memory): the "
                     "configs[1] job as FG_HOST batches (double-buffered H2D on the engine's copy stream, "
                     "overlapping the kernels; each call returns once its batch is copied). `value` is the "

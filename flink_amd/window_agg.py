@@ -247,8 +247,10 @@ class WindowAggOperator:
         that torch's caching allocator cannot hand their blocks to other work earlier. (Not
         record_stream: the allocator would record events on the engine stream when the block is
         freed, which may be after fg_close destroyed that stream.)"""
-        held = self.__dict__.setdefault("_held", [])
         prev = self.__dict__.get("_inflight")
+        if prev is None and cols is None:   # (the watermark path between batches: nothing to do)
+            return
+        held = self.__dict__.setdefault("_held", [])
         ext = self.__dict__.get("_ext_stream")
         if prev is not None:
             if ext is None:
@@ -258,7 +260,8 @@ class WindowAggOperator:
                 ev = torch.cuda.Event()
                 ev.record(ext)
                 held.append((ev, prev))
-        self._held = [(e, c) for e, c in held if e is None or not e.query()]
+        if cols is not None:   # a new batch: release the columns whose event completed
+            self._held = [(e, c) for e, c in held if e is None or not e.query()]
         self._inflight = cols
 
     def process_rows(self, rows, stride: int, arity: int, key_field: int = 0, rowtime_field: int = 1,
