@@ -358,6 +358,10 @@ struct fg_handle {
 
     // stats
     int64_t records_in = 0, rows_fired = 0, flushes = 0;
+    // bound on any (key, window)'s COUNT(*): records taken since the reset (JMAX once partial
+    // accumulators or a state image, whose counts are unbounded, entered) -- gates the compact
+    // merge's 32-bit LDS counts
+    int64_t cnt_bound = 0;
     bool timing = false;
     uint32_t timing_mask = ~0u;   // kernel classes bracketed with events (fg_set_kernel_timing)
     KStat kstat[K_NCLASS];
@@ -1165,6 +1169,9 @@ int ensure_out(fg_handle* h, int64_t need) {
     return FG_OK;
 }
 
+// the COUNT(*) of any key stays below 2^32 (the compact merge's u32 counts)
+bool ub_cnt_fits(const fg_handle* h) { return h->cnt_bound < ((int64_t)1 << 32); }
+
 // Emit one window from the union of `srcs`; optionally write the merged state to `dst`.
 // `defer`: no host synchronization -- the caller collects the row count (fire_collect)
 // after the advance's last fire (launches stay ordered on the handle's stream).
@@ -1207,9 +1214,18 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
             p.stamps = d_fst.as<unsigned long long>();
         }
 #endif
+        // the compact merge (two workgroups per CU, 20-B LDS slots) when the window is plain
+        // resident state: source tables without NULL counts or marks, nothing written back, one
+        // value accumulator, COUNT(*)s below 2^32 (FG_COMPACT_FIRE=0: the wide merge, A/B)
+        static const bool compact_fire = !getenv("FG_COMPACT_FIRE") || std::atoi(getenv("FG_COMPACT_FIRE")) != 0;
+        p.compact = compact_fire && !h->mv && !dst && p.n_batches == 0 && p.src_null_mask == 0 && !p.mark_mask &&
+                            !p.markonly_mask && !p.emit_marked && p.dst_mode == 0 && p.n_src <= 64 &&
+                            ub_cnt_fits(h)
+                        ? 1
+                        : 0;
         {
             KTimer kt(h, K_FIRE, 0);
-            HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
+            HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
         }
 #ifdef FG_STAMPS
         if (p.stamps) {
@@ -2806,6 +2822,7 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     if (b->n > (int64_t)0x7fffffff) return h->fail(FG_EINVAL, "batch larger than 2^31-1 records");
     if (!b->key || !b->rowtime) return h->fail(FG_EINVAL, "batch key/rowtime columns are required");
     if (h->cfg.val_type != FG_VAL_NONE && !b->val) return h->fail(FG_EINVAL, "batch value column is required");
+    h->cnt_bound = b->n > JMAX - h->cnt_bound ? JMAX : h->cnt_bound + b->n;
     const int fmt = b->format;
     if (fmt & ~(FG_BATCH_KEY32 | FG_BATCH_ROWTIME32 | FG_BATCH_VAL32)) return h->fail(FG_EINVAL, "bad fg_batch.format %d", fmt);
     if (fmt && b->location != FG_HOST) return h->fail(FG_EINVAL, "narrow fg_batch columns are for FG_HOST batches");
@@ -3025,6 +3042,7 @@ int fg_add_rows(fg_handle* h, const fg_row_batch* b) {
 }
 
 int fg_add_partials(fg_handle* h, const fg_partials* b) {
+    if (h) h->cnt_bound = JMAX;
     if (!h || !b) return FG_EINVAL;
     if (b->n <= 0) return FG_OK;
     if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
@@ -3293,6 +3311,7 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
 
 int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     if (!h || !in) return FG_EINVAL;
+    h->cnt_bound = JMAX;
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc0 = settle_pending(h)) return rc0;
     int rc = flush(h);
@@ -3480,6 +3499,7 @@ int fg_reset(fg_handle* h) {
     for (int l = 0; l < h->lanes; l++) release_lane(h, l);
     h->anchor_start = JMIN;
     h->q_guess = kEmptyLane;
+    h->cnt_bound = 0;
     h->current_progress = JMIN;
     h->arrival_progress = JMIN;
     h->next_trigger = JMIN;

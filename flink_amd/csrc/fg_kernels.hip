@@ -1764,7 +1764,9 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     };
     // heavy regions are left to the heavy pass (no state read, nothing emitted or written)
     auto skipped = [&](int r) -> bool { return p.heavy != nullptr && gbl(p.heavy)[r] != 0; };
-    const bool fast = C || p.fast_stream != 0;   // the compact merge always streams plain staged records
+    // the compact merge streams plain staged records, or (a fire of resident slice tables only:
+    // HOP windows) reads source tables alone
+    const bool fast = C ? p.n_batches > 0 : p.fast_stream != 0;
     const int nb = p.n_batches;
 
     // fast path state
@@ -2020,7 +2022,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             for (int k = 0; k < NVS; k++) t.v[k][i] = (unsigned long long)lds_repr(vops[k], vinit[k]);
         }
         if (tid == 0) s_flags = 0;
-        if constexpr (!C) if (tid < 64) {   // source tables: per-region entry counts -> flat prefix
+        if ((!C || p.n_src > 0) && tid < 64) {   // source tables: per-region entry counts -> flat prefix
             const int nsrc = p.n_src <= kMaxSrcFlat ? p.n_src : 0;
             const uint32_t v = tid < nsrc ? gbl(p.src[tid].counts)[r] : 0u;
             uint32_t x = v;
@@ -2044,8 +2046,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         // 1) resident slice regions (state) ------------------------------------------
         //    the entries of all source tables form one flat sequence (prefix of the
         //    tables' counts in s_soff), loaded kSrcU per thread at a time and inserted with
-        //    the bucketed probe
-        if constexpr (!C) {
+        //    the bucketed probe (compact: plain sources only -- no NULL counts, no marks)
+        if constexpr (!NT) if (!C || p.n_src > 0) {
             const uint32_t NT = skip ? 0u : s_soff[p.n_src <= kMaxSrcFlat ? p.n_src : 0];
             for (uint32_t i0 = 0; i0 < NT; i0 += kSrcU * T) {
                 int64_t k[kSrcU], cs[kSrcU], cn[kSrcU], sm[kSrcU][NVS];
@@ -2400,7 +2402,11 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
     }
     const bool n12 = p.fast_stream && p.narrow;   // narrow 12-B staged records
     if (p.compact) {
-        if (!p.fast_stream || p.n_src != 0) return hipErrorInvalidValue;
+        // staged records alone, or plain source tables alone (no NULL counts, marks, chains or
+        // destination: a HOP window's fire)
+        const bool plain_src = p.n_batches == 0 && !p.has_dst && !p.mark_mask && !p.markonly_mask &&
+                               !p.src_null_mask && !p.dst_mode && !p.emit_marked && p.n_src <= kMaxSrcFlat;
+        if (p.n_src == 0 ? !p.fast_stream : !plain_src) return hipErrorInvalidValue;
         // the compact merge (the TUMBLE fire of plain staged records) per value op
         if (n12) {
             switch (p.val_type) {
