@@ -362,6 +362,9 @@ struct fg_handle {
     // accumulators or a state image, whose counts are unbounded, entered) -- gates the compact
     // merge's 32-bit LDS counts
     int64_t cnt_bound = 0;
+    // every key staged since the reset fits 32 bits (narrow passes only, no partials or images):
+    // the compact merge may key its LDS table by the int32 key of a resident entry's mix
+    bool keys32 = true;
     bool timing = false;
     uint32_t timing_mask = ~0u;   // kernel classes bracketed with events (fg_set_kernel_timing)
     KStat kstat[K_NCLASS];
@@ -614,6 +617,9 @@ void set_values(const fg_handle* h, MergeParams* p) {
 
 // MergeParams of job `ji` at the current region bits (the general path; callers pick the
 // fast variants on a first launch)
+// the COUNT(*) of any key stays below 2^32 (the compact merge's u32 counts)
+bool ub_cnt_fits(const fg_handle* h) { return h->cnt_bound < ((int64_t)1 << 32); }
+
 int job_params(fg_handle* h, int ji, MergeParams* p) {
     const MergeJob& j = h->jobs[(size_t)ji];
     std::vector<StagedBatch> sb;
@@ -1041,7 +1047,15 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         p.narrow = plain && ln.passes[0]->narrow ? 1 : 0;
         // compact LDS table (two workgroups per CU) when no resident state is read and the
         // COUNT(*) of a key cannot reach 2^32
-        p.compact = plain && p.n_src == 0 && ln.fill < ((int64_t)1 << 32) && !(p.emit && p.has_dst) ? 1 : 0;
+        // (resident sources: plain ones -- no NULL counts, marks or chains -- at a COUNT(*) bound
+        // below 2^32, keyed by their int32 keys under narrow staging; a fired window that keeps
+        // its state (allowed lateness) takes the wide merge)
+        static const bool compact_src = !getenv("FG_COMPACT_FIRE") || std::atoi(getenv("FG_COMPACT_FIRE")) != 0;
+        const bool src_ok = p.n_src == 0 ||
+                            (compact_src && !h->mv && p.src_null_mask == 0 && !p.mark_mask && !p.markonly_mask &&
+                             !p.emit_marked && p.dst_mode == 0 && p.n_src <= 64 && ub_cnt_fits(h) &&
+                             (!p.narrow || h->keys32));
+        p.compact = plain && src_ok && ln.fill < ((int64_t)1 << 32) && !(p.emit && p.has_dst && h->retain) ? 1 : 0;
 #ifdef FG_STAMPS
         static DevBuf d_st;
         if (getenv("FG_STAMPS")) {
@@ -1169,9 +1183,6 @@ int ensure_out(fg_handle* h, int64_t need) {
     return FG_OK;
 }
 
-// the COUNT(*) of any key stays below 2^32 (the compact merge's u32 counts)
-bool ub_cnt_fits(const fg_handle* h) { return h->cnt_bound < ((int64_t)1 << 32); }
-
 // Emit one window from the union of `srcs`; optionally write the merged state to `dst`.
 // `defer`: no host synchronization -- the caller collects the row count (fire_collect)
 // after the advance's last fire (launches stay ordered on the handle's stream).
@@ -1223,6 +1234,7 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
                             ub_cnt_fits(h)
                         ? 1
                         : 0;
+        p.narrow = p.compact && h->keys32 ? 1 : 0;   // (narrow LDS table: keys from the entries' mixes)
         {
             KTimer kt(h, K_FIRE, 0);
             HIPCHK(h, launch_merge(p, p.compact ? std::min(h->P, 2 * h->merge_grid) : merge_grid(h), h->stream));
@@ -1797,6 +1809,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     p.max_bucket = &dc->max_bucket;
     p.wide = &dc->wide;
     p.narrow = two_pass && h->narrow ? 1 : 0;
+    if (!p.narrow) h->keys32 = false;
     if (two_pass) {
         KTimer kt(h, K_PART1, n);
         HIPCHK(h, launch_part1(p, h->stream));
@@ -1907,6 +1920,7 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
         rc = flush(h);
         if (rc) return rc;
         h->narrow = false;
+        h->keys32 = false;
         p.narrow = 0;
         {
             KTimer kt(h, K_PART1, n);
@@ -3042,7 +3056,10 @@ int fg_add_rows(fg_handle* h, const fg_row_batch* b) {
 }
 
 int fg_add_partials(fg_handle* h, const fg_partials* b) {
-    if (h) h->cnt_bound = JMAX;
+    if (h) {
+        h->cnt_bound = JMAX;
+        h->keys32 = false;
+    }
     if (!h || !b) return FG_EINVAL;
     if (b->n <= 0) return FG_OK;
     if (h->local) return h->fail(FG_ESTATE, "fg_add_partials on a FG_FLAG_LOCAL_PARTIALS (local phase) operator");
@@ -3312,6 +3329,7 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
 int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     if (!h || !in) return FG_EINVAL;
     h->cnt_bound = JMAX;
+    h->keys32 = false;
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc0 = settle_pending(h)) return rc0;
     int rc = flush(h);
@@ -3500,6 +3518,7 @@ int fg_reset(fg_handle* h) {
     h->anchor_start = JMIN;
     h->q_guess = kEmptyLane;
     h->cnt_bound = 0;
+    h->keys32 = true;
     h->current_progress = JMIN;
     h->arrival_progress = JMIN;
     h->next_trigger = JMIN;

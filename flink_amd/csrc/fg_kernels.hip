@@ -1456,6 +1456,28 @@ __device__ __forceinline__ int lds_find_or_insert_from32(LdsTableN& t, int32_t k
     full = true;
     return -1;
 }
+// slot of the 32-bit key k in the narrow table given its home bucket's four keys (read
+// beforehand): a match, else a CAS on the bucket's first empty slot, else the linear probe
+__device__ __forceinline__ int nt_bucket_slot(LdsTableN& t, int32_t k, uint32_t home, int4 b, bool& full) {
+    constexpr uint32_t S_ = (uint32_t)kCompactSlots;
+    if (k == kEmpty32) return (int)S_;
+    const int32_t q[4] = {b.x, b.y, b.z, b.w};
+    int hit = -1, empty = -1;
+#pragma unroll
+    for (int j = 3; j >= 0; j--) {
+        if (q[j] == k) hit = j;
+        if (q[j] == kEmpty32) empty = j;
+    }
+    if (hit >= 0 && (empty < 0 || hit < empty)) return (int)home + hit;
+    if (empty >= 0) {
+        const uint32_t e = home + (uint32_t)empty;
+        const int old = atomicCAS(&t.key[e], kEmpty32, k);
+        if (old == kEmpty32 || old == k) return (int)e;
+        return lds_find_or_insert_from32(t, k, e + 1 >= S_ ? 0u : e + 1, full);
+    }
+    const uint32_t nx = home + 4;
+    return lds_find_or_insert_from32(t, k, nx >= S_ ? 0u : nx, full);
+}
 
 // Home bucket: the low 32 bits of the key's mix h (the region is its top bits; the low
 // word is independent of them) pick an aligned bucket of kBucket slots -- one 32-bit
@@ -1890,29 +1912,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         for (int u = 0; u < kMergeU; u++) {
             if (pcnt[u] == 0) continue;
             if constexpr (NT) {   // exact 32-bit keys, one bucket read
-                const int32_t k = (int32_t)c[u].x;
-                const int32_t q[4] = {bq[u].x, bq[u].y, bq[u].z, bq[u].w};
-                int hit = -1, empty = -1;
-#pragma unroll
-                for (int j = 3; j >= 0; j--) {
-                    if (q[j] == k) hit = j;
-                    if (q[j] == kEmpty32) empty = j;
-                }
-                constexpr uint32_t S_ = (uint32_t)kCompactSlots;
-                int slot;
-                if (k == kEmpty32) {
-                    slot = (int)S_;
-                } else if (hit >= 0 && (empty < 0 || hit < empty)) {
-                    slot = (int)home[u] + hit;
-                } else if (empty >= 0) {
-                    const uint32_t e = home[u] + (uint32_t)empty;
-                    const int old = atomicCAS(&t.key[e], kEmpty32, k);
-                    if (old == kEmpty32 || old == k) slot = (int)e;
-                    else slot = lds_find_or_insert_from32(t, k, e + 1 >= S_ ? 0u : e + 1, full);
-                } else {
-                    const uint32_t nx = home[u] + 4;
-                    slot = lds_find_or_insert_from32(t, k, nx >= S_ ? 0u : nx, full);
-                }
+                const int slot = nt_bucket_slot(t, (int32_t)c[u].x, home[u], bq[u], full);
                 if (slot >= 0) {
                     if constexpr (FG_WAVE_PRE) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
                     else lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
@@ -2047,6 +2047,51 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         //    the entries of all source tables form one flat sequence (prefix of the
         //    tables' counts in s_soff), loaded kSrcU per thread at a time and inserted with
         //    the bucketed probe (compact: plain sources only -- no NULL counts, no marks)
+        if constexpr (NT) if (p.n_src > 0) {   // narrow table: a source entry's key from its mix
+            const uint32_t NE = skip ? 0u : s_soff[p.n_src];   // (compact: n_src <= kMaxSrcFlat)
+            for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
+                int64_t k[kSrcU], cs[kSrcU], sm[kSrcU][1];
+                int j = 0;
+                {
+                    const uint32_t f = i0 + tid;
+                    int lo = 0, hi = p.n_src;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_soff[mid] <= f) lo = mid;
+                        else hi = mid;
+                    }
+                    j = lo;
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    const uint32_t f = i0 + u * T + tid;
+                    k[u] = 0;
+                    cs[u] = 0;
+                    sm[u][0] = 0;
+                    if (f >= NE) continue;
+                    while (s_soff[j + 1] <= f) j++;
+                    const uint32_t i = f - s_soff[j];
+                    const auto base = gbl(s_sbase[j]);
+                    k[u] = base[i];
+                    cs[u] = base[cap + i];
+                    sm[u][0] = base[3 * cap + i];
+                }
+                uint32_t home[kSrcU];
+                int4 bq[kSrcU];
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    home[u] = lds_home<C, MV>(k[u]);
+                    bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    if (i0 + u * T + tid >= NE) continue;
+                    // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
+                    const int slot = nt_bucket_slot(t, (int32_t)key_of(k[u]), home[u], bq[u], full);
+                    if (slot >= 0 && cs[u]) lds_add<C, MV>(t, slot, (unsigned long long)cs[u], 0ull, sm[u], vt, p);
+                }
+            }
+        }
         if constexpr (!NT) if (!C || p.n_src > 0) {
             const uint32_t NT = skip ? 0u : s_soff[p.n_src <= kMaxSrcFlat ? p.n_src : 0];
             for (uint32_t i0 = 0; i0 < NT; i0 += kSrcU * T) {
@@ -2400,12 +2445,14 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
         }
         return hipGetLastError();
     }
-    const bool n12 = p.fast_stream && p.narrow;   // narrow 12-B staged records
+    // narrow 12-B staged records (a compact merge of resident sources alone: narrow keys, p.narrow)
+    const bool n12 = p.narrow && (p.fast_stream || (p.compact && p.n_batches == 0));
     if (p.compact) {
         // staged records alone, or plain source tables alone (no NULL counts, marks, chains or
         // destination: a HOP window's fire)
-        const bool plain_src = p.n_batches == 0 && !p.has_dst && !p.mark_mask && !p.markonly_mask &&
-                               !p.src_null_mask && !p.dst_mode && !p.emit_marked && p.n_src <= kMaxSrcFlat;
+        // staged records and / or plain source tables (no NULL counts, marks or chains)
+        const bool plain_src = !p.mark_mask && !p.markonly_mask && !p.src_null_mask && !p.dst_mode && !p.emit_marked &&
+                               p.n_src <= kMaxSrcFlat && (p.n_batches == 0 || p.fast_stream);
         if (p.n_src == 0 ? !p.fast_stream : !plain_src) return hipErrorInvalidValue;
         // the compact merge (the TUMBLE fire of plain staged records) per value op
         if (n12) {
