@@ -545,25 +545,38 @@ def main():
         ckpt["n"] += 1
         ckpt["s"] += time.perf_counter() - c0
 
+    def intern(lo):
+        """BinaryRowDataKeySelector.getKey rows -> dictionary ids (on the GPU, the dictionary's
+        own stream); the call returns with the ids complete"""
+        hi = min(n, lo + args.batch)
+        k, _ = kdict.intern(packed=(rows_u8[32 * lo:32 * hi], row_off[:hi - lo], row_len[:hi - lo]),
+                            key_groups=False)
+        return k
+
     def one_step():
         op.reset()
         if op_local:
             op_local.reset()
         rows = 0
         xgmi = 0
+        # STRING keys: the next micro-batch's key rows are interned while the engine aggregates
+        # the current one (the key selector runs as records arrive, ahead of the operator; the
+        # dictionary assigns ids in the same first-seen order)
+        k_next = intern(0) if strings else None
         for bi, lo in enumerate(range(0, n, args.batch)):
             if args.checkpoint_every and bi > 0 and bi % args.checkpoint_every == 0:
                 checkpoint()
             hi = min(n, lo + args.batch)
-            if strings:   # BinaryRowDataKeySelector.getKey rows -> dictionary ids (on the GPU)
-                k, _ = kdict.intern(packed=(rows_u8[32 * lo:32 * hi], row_off[:hi - lo], row_len[:hi - lo]),
-                                    key_groups=False)
+            if strings:
+                k = k_next
             else:
                 k = key[lo:hi]
             t, v = ts[lo:hi], val[lo:hi]
             wms = watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"])
             if two_phase:
                 op_local.process_batch(k, t, v)
+                if strings and hi < n:
+                    k_next = intern(hi)
                 if wms:   # the micro-batch's last watermark (in-order input: same output)
                     nr, sent = partials_round(wms[-1])
                     rows += nr
@@ -575,6 +588,8 @@ def main():
                 xgmi += sent
                 torch.cuda.current_stream().synchronize()
             op.process_batch(k, t, v)
+            if strings and hi < n:   # overlaps this batch's partition passes
+                k_next = intern(hi)
             if world > 1 and wms:
                 wms[-1] = global_watermark(wms[-1], device=dev)
             for wm in wms:
