@@ -2783,6 +2783,12 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (cfg->expected_keys > 0) {
         const int slots = h->mv ? kSlotsMV : kSlots;
         while (bits < kMaxRegionBits && ((int64_t)1 << bits) * (int64_t)(slots * 0.35) < cfg->expected_keys) bits++;
+        // a merge runs one region per workgroup: an operator of a few thousand keys would fire
+        // each window on a handful of CUs, so from 4,096 expected keys it takes at least
+        // 2^FG_MIN_REGION_BITS regions (more, emptier LDS tables; every CU busy at a fire)
+        int min_bits = 8;
+        if (const char* e = getenv("FG_MIN_REGION_BITS")) min_bits = std::max(0, std::min(kMaxRegionBits, std::atoi(e)));
+        if (cfg->expected_keys >= 4096 && bits < min_bits) bits = min_bits;
     } else {
         bits = kDefaultRegionBits;
     }
