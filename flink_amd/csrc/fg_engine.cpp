@@ -365,6 +365,9 @@ struct fg_handle {
     // every key staged since the reset fits 32 bits (narrow passes only, no partials or images):
     // the compact merge may key its LDS table by the int32 key of a resident entry's mix
     bool keys32 = true;
+    bool skew_seen = false;     // some ingest pass saw hot-key skew (pass-2 units of one workgroup)
+    int32_t p2_skew_group = 0;  // FG_P2_SKEW_GROUP=k: pass-2 units of k pass-1 workgroups for skewed
+                                // streams (A/B on Zipf: k = 1 19.3, 2 12.6, default 10.9 ms per step)
     bool timing = false;
     uint32_t timing_mask = ~0u;   // kernel classes bracketed with events (fg_set_kernel_timing)
     KStat kstat[K_NCLASS];
@@ -1810,6 +1813,9 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     p.wide = &dc->wide;
     p.narrow = two_pass && h->narrow ? 1 : 0;
     if (!p.narrow) h->keys32 = false;
+    // a stream seen skewed (hot keys) partitions in pass-2 units of one pass-1 workgroup: the
+    // hot key's coarse bucket is then spread over as many units as there are workgroups
+    p.p2_group = h->skew_seen ? h->p2_skew_group : 0;
     if (two_pass) {
         KTimer kt(h, K_PART1, n);
         HIPCHK(h, launch_part1(p, h->stream));
@@ -2017,6 +2023,7 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     s->bits = p.region_bits;   // (a flush above may have split the regions since the count)
     s->is_acc = false;
     s->skew = out->skew;
+    h->skew_seen = h->skew_seen || out->skew;
     s->refs = 0;
     for (int l = 0; l < h->lanes; l++) {
         if (out->lane_total[l] == 0) continue;
@@ -2827,6 +2834,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     // narrow 12-B staging for the two-pass partition of a one-value operator (FG_NARROW=0: off, A/B)
     hp->narrow = hp->st_stride == 2 && !hp->mv && hp->region_bits >= kFineBits;
     if (const char* e = getenv("FG_NARROW")) hp->narrow = hp->narrow && std::atoi(e) != 0;
+    if (const char* e = getenv("FG_P2_SKEW_GROUP")) hp->p2_skew_group = std::max(0, std::atoi(e));
     hp->narrow_ok = hp->narrow;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";
@@ -3525,6 +3533,7 @@ int fg_reset(fg_handle* h) {
     h->q_guess = kEmptyLane;
     h->cnt_bound = 0;
     h->keys32 = true;
+    h->skew_seen = false;
     h->current_progress = JMIN;
     h->arrival_progress = JMIN;
     h->next_trigger = JMIN;

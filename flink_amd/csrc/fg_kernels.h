@@ -151,6 +151,8 @@ struct IngestParams {
     uint8_t* tmp_null;         // NULL flags of tmp (when vnull)
     uint16_t* dir;             // [grid * max_tiles][n_coarse + 1] coarse offsets within each tile
     int32_t max_tiles;         // tiles per workgroup segment (ceil(segment / kPart1Tile))
+    int32_t p2_group;          // pass-1 workgroups per pass-2 unit (0: part2_group's default); 1 for
+                               // skewed input, whose hot coarse bucket would load a few units
     int32_t n_coarse;          // lanes << (region_bits - kFineBits)
     int64_t* sink;             // >= 32 B of scratch: idle lanes store here (static store counts)
     // speculative pass 2 (launched right after pass 1, no host round trip): the staged
