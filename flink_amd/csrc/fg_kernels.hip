@@ -1074,7 +1074,7 @@ hipError_t launch_part1(const IngestParams& p, hipStream_t s) {
 hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
     int nslots = 0;
     for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
-    const int32_t group = part2_group(p.max_tiles);
+    const int32_t group = p.p2_group > 0 ? std::min(p.p2_group, part2_group(p.max_tiles)) : part2_group(p.max_tiles);
     const int64_t units = (int64_t)nslots * (1 << (p.region_bits - kFineBits)) * ((p.grid + group - 1) / group);
     if (units == 0) return hipSuccess;
     if (p.narrow) {
