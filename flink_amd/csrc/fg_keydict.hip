@@ -8,7 +8,7 @@
 // BinarySegmentUtils.hash -> MurmurHashUtils.java:92-96,131-170), which KeyGroupStreamPartitioner
 // turns into a key group (KeyGroupRangeAssignment.java:63-77). The window engine aggregates
 // 64-bit keys; this dictionary interns each distinct key row once and hands out an id
-// (key group << 40 | ordinal): equal rows get equal ids, distinct rows distinct ids, so the
+// (ordinal << kg_bits | key group): equal rows get equal ids, distinct rows distinct ids, so the
 // aggregation by id is the aggregation by key row, and the id carries the row's key group
 // (FG_KEYHASH_DICT_ID routes by it).
 //
@@ -49,8 +49,9 @@ constexpr int kDictThreads = 256;
 #define FG_DICT_GROW 4   // table rebuilt at FG_DICT_GROW x (ids + 1M) slots (>= 2: room for a chunk)
 #endif
 static_assert(FG_DICT_GROW >= 2, "FG_DICT_GROW: the table must stay at most half full after a rebuild");
-constexpr int kIdShift = 40;   // id = key group << kIdShift | ordinal
-constexpr uint64_t kOrdMask = (1ull << kIdShift) - 1;
+// id = ordinal << kg_bits | key group, kg_bits = dict_kg_bits(max parallelism) (7 at Flink's
+// default 128): ids stay below 2^31 for 16.7M keys, so the window engine stages them as narrow
+// 32-bit keys (fg_window.h key_group_of reads the key group back from the low bits)
 
 __host__ __device__ __forceinline__ uint32_t load_u32(const uint8_t* p) {
     return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
@@ -89,6 +90,7 @@ struct DictDev {
     unsigned long long* counters;   // [0] ids, [1] arena bytes, [2] collisions, [3] bad rows, [4] pending rows,
                                     // [5] entry bytes (k_dict_check), [6] lookup misses
     uint64_t mask;       // cap - 1
+    int32_t kg_bits;     // id = ordinal << kg_bits | key group
 };
 
 // one atomic per wave: lane-exclusive offsets of `amount` (0 for a lane that takes nothing)
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_assign(DictDev d, RowsIn 
         const unsigned long long ord = wave_reserve(&d.counters[0], own ? 1u : 0u);
         const unsigned long long at = wave_reserve(&d.counters[1], own ? (uint32_t)(8 + ((len + 7) & ~7)) : 0u);
         if (!own) continue;
-        const int64_t id = (int64_t)((uint64_t)pend.kg[j] << kIdShift | ord);
+        const int64_t id = (int64_t)(ord << d.kg_bits | (uint64_t)pend.kg[j]);
         *reinterpret_cast<int64_t*>(d.arena + at) = id;
         const uint32_t* src = reinterpret_cast<const uint32_t*>(in.bytes + in.off[i]);
         uint32_t* dst = reinterpret_cast<uint32_t*>(d.arena + at + 8);
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_gather(DictDev d, int64_t
                                                               int64_t* off_out, int32_t* len_out) {
     const int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
     if (i >= n) return;
-    const uint64_t ord = (uint64_t)ids[i] & kOrdMask;
+    const uint64_t ord = (uint64_t)ids[i] >> d.kg_bits;
     const bool ok = ids[i] >= 0 && (int64_t)ord < nids;
     off_out[i] = ok ? d.ent_off[ord] : -1;
     len_out[i] = ok ? d.ent_len[ord] : -1;
@@ -564,6 +566,7 @@ struct fg_key_dict {
         d.arena = arena.as<uint8_t>();
         d.counters = counters.as<unsigned long long>();
         d.mask = cap - 1;
+        d.kg_bits = dict_kg_bits(max_p);
         return d;
     }
 };
@@ -639,7 +642,7 @@ int resolve_collisions(fg_key_dict* d, bool host, int64_t n, const uint8_t* byte
             DCHK(d, d->ent_tag.ensure(8 * (size_t)d->nids, s, 8 * (size_t)ord));
             DCHK(d, d->arena.ensure((size_t)d->arena_used, s, (size_t)at));
             const int32_t kg = murmur_hash(binaryrow_hash_bytes(row, l)) % d->max_p;
-            id = (int64_t)((uint64_t)kg << kIdShift | (uint64_t)ord);
+            id = (int64_t)((uint64_t)ord << dict_kg_bits(d->max_p) | (uint64_t)kg);
             std::vector<uint8_t> entry(8 + ((l + 7) & ~7), 0);
             std::memcpy(entry.data(), &id, 8);
             std::memcpy(entry.data() + 8, row, (size_t)l);

@@ -280,8 +280,15 @@ __host__ __device__ __forceinline__ int32_t murmur_hash(int32_t code) {
     if (r != INT32_MIN) return -r;
     return 0;
 }
+// bits of the key group in an fg_key_dict id: ceil(log2(max parallelism))
+__host__ __device__ __forceinline__ int32_t dict_kg_bits(int32_t max_p) {
+    int32_t b = 0;
+    while (b < 31 && (1 << b) < max_p) b++;
+    return b;
+}
 __host__ __device__ __forceinline__ int32_t key_group_of(int64_t key, int32_t key_hash, int32_t max_p) {
-    if (key_hash == 2) return (int32_t)((uint64_t)key >> 40) % max_p;   // an fg_key_dict id carries it
+    // an fg_key_dict id carries its key group in its low bits (ordinal << kg_bits | key group)
+    if (key_hash == 2) return (int32_t)((uint64_t)key & ((1ull << dict_kg_bits(max_p)) - 1)) % max_p;
     int32_t h = key_hash == 0 ? binaryrow_hash_i64(key) : java_long_hash(key);
     return murmur_hash(h) % max_p;
 }

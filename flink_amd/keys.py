@@ -22,7 +22,12 @@ import numpy as np
 from . import _lib as L
 from .rows import HEADER_SIZE_IN_BITS, bit_set_width
 
-DICT_ID_SHIFT = 40
+def dict_kg_bits(max_parallelism: int) -> int:
+    """Bits of the key group in a dictionary id: ceil(log2(max parallelism)) (fg_window.h)."""
+    b = 0
+    while b < 31 and (1 << b) < max_parallelism:
+        b += 1
+    return b
 
 
 def key_row(fields, types, row_kind: int = 0) -> bytes:
@@ -106,7 +111,8 @@ def pack_key_rows(rows):
 
 def key_group_of_id(ids, max_parallelism: int = 128):
     """Key group carried by a dictionary id (FG_KEYHASH_DICT_ID)."""
-    return (np.asarray(ids, dtype=np.int64).view(np.uint64) >> np.uint64(DICT_ID_SHIFT)).astype(np.int32) % max_parallelism
+    mask = np.uint64((1 << dict_kg_bits(max_parallelism)) - 1)   # id = ordinal << kg_bits | key group
+    return (np.asarray(ids, dtype=np.int64).view(np.uint64) & mask).astype(np.int32) % max_parallelism
 
 
 def binaryrow_hash(row: bytes) -> int:

@@ -101,7 +101,8 @@ enum fg_agg { FG_AGG_COUNT_STAR = 0, FG_AGG_COUNT = 1, FG_AGG_SUM = 2, FG_AGG_AV
  * be running on the handle's stream). */
 enum fg_location { FG_HOST = 0, FG_DEVICE = 1 };
 /* FG_KEYHASH_DICT_ID: the key is an id of an fg_key_dict (any key type); its key group, computed
- * from the key row's bytes when it was interned, is carried in the id (id >> 40). */
+ * from the key row's bytes when it was interned, is carried in the id's low ceil(log2(max_parallelism))
+ * bits. */
 enum fg_key_hash { FG_KEYHASH_BINARYROW_BIGINT = 0, FG_KEYHASH_JAVA_LONG = 1, FG_KEYHASH_DICT_ID = 2 };
 enum fg_flags {
     FG_FLAG_KERNEL_TIMING = 1,    /* HIP-event timing of every launch (fg_kernel_stats) */
@@ -342,7 +343,8 @@ int  fg_partition_columns_by_owner(int32_t device_id, void* stream, int64_t n, i
  * MurmurHashUtils.hashBytesByWords over those bytes, seed 42 (BinarySection.hashCode :76-78,
  * MurmurHashUtils.java:92-96,131-170) -> KeyGroupRangeAssignment. fg_key_dict_intern maps each row
  * to a 64-bit id: equal rows -> equal ids, distinct rows -> distinct ids (exact: a hash collision
- * is resolved by comparing the bytes), id = key group << 40 | ordinal. The ids are the BIGINT key
+ * is resolved by comparing the bytes), id = ordinal << ceil(log2(max_parallelism)) | key group (below
+ * 2^31 for 16.7M keys at max parallelism 128, so the window engine stages them as 32-bit keys). The ids are the BIGINT key
  * column of fg_add_batch / the key field of fg_add_rows; FG_KEYHASH_DICT_ID routes them by the
  * carried key group; fired rows' ids map back to their rows with fg_key_dict_lookup. A handle is
  * single-threaded like fg_handle; ids are stable for the dictionary's life (a restored operator

@@ -9,6 +9,8 @@ import socket
 import numpy as np
 import pytest
 
+from flink_amd.keys import dict_kg_bits, key_group_of_id
+
 WORLD = 2
 MAXP = 128
 
@@ -214,7 +216,7 @@ def test_two_phase_exchange_matches_single_operator(oracle_mod, kind, columns):
 # ---- STRING keys over the two-phase exchange -------------------------------------------------
 class HostKeyDict:
     """A dictionary of key rows with the KeyDictionary interface exchange_partials uses
-    (locate / intern_rows), on the host: ids = key group << 40 | ordinal in THIS dictionary's
+    (locate / intern_rows), on the host: ids = ordinal << kg_bits | key group in THIS dictionary's
     first-seen order, so two ranks' ids for one key differ, as the GPU dictionaries' do."""
 
     def __init__(self, max_parallelism=MAXP):
@@ -225,19 +227,19 @@ class HostKeyDict:
         from oracle import oracle as O
         i = self.ids.get(row)
         if i is None:
-            i = O.key_group_of_row(row, self.maxp) << 40 | len(self.rows)
+            i = len(self.rows) << dict_kg_bits(self.maxp) | O.key_group_of_row(row, self.maxp)
             self.ids[row] = i
             self.rows.append(row)
         return i
 
     def row_of(self, i: int) -> bytes:
-        return self.rows[i & ((1 << 40) - 1)]
+        return self.rows[i >> dict_kg_bits(self.maxp)]
 
     def locate(self, ids):
         import torch
         blob = b"".join(self.rows)
         starts = np.cumsum([0] + [len(r) for r in self.rows])
-        ords = ids.numpy() & ((1 << 40) - 1)
+        ords = ids.numpy() >> dict_kg_bits(self.maxp)
         woff = torch.from_numpy((starts[ords] // 4).astype(np.int64))
         nw = torch.from_numpy(np.array([len(self.rows[o]) // 4 for o in ords], dtype=np.int64))
         return woff, nw, torch.from_numpy(np.frombuffer(blob or b"\0" * 4, dtype=np.int32).copy())
@@ -281,7 +283,7 @@ def _two_phase_strings_rank(rank, world, port, out_q):
     def round_(local_wm):
         local.process_watermark(local_wm)
         part = local.take_rows()
-        kg = (part["key"].view(np.uint64) >> np.uint64(40)).astype(np.int64) % MAXP   # FG_KEYHASH_DICT_ID
+        kg = key_group_of_id(part["key"], MAXP).astype(np.int64)   # FG_KEYHASH_DICT_ID
         owner = kg * world // MAXP
         part = part[np.argsort(owner, kind="stable")]
         counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
