@@ -409,6 +409,9 @@ def main():
                     "e.g. count_star,min")
     ap.add_argument("--expected-keys", type=int, default=None,
                     help="operator sizing hint: distinct keys per slice (default: the key space x 1.05)")
+    ap.add_argument("--wm-sync", action="store_true",
+                    help="deliver watermarks with the synchronous fg_advance_progress (A/B; default: "
+                         "fg_advance_progress_async, the host does not wait for a window's fire)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
@@ -555,6 +558,7 @@ def main():
 
     def one_step():
         op.reset()
+        rows0 = op.stats()["rows_fired"]
         if op_local:
             op_local.reset()
         rows = 0
@@ -593,13 +597,17 @@ def main():
             if world > 1 and wms:
                 wms[-1] = global_watermark(wms[-1], device=dev)
             for wm in wms:
-                r = op.process_watermark(wm, device_output=True)
-                rows += r.n
+                if args.wm_sync:
+                    rows += op.process_watermark(wm, device_output=True).n
+                else:   # fg_advance_progress_async: fired rows stay in HBM, counted below
+                    op.process_watermark(wm, device_output=True, wait=False)
         if two_phase:
             nr, sent = partials_round(JMAX)
             return rows + nr, xgmi + sent
         r = op.process_watermark(JMAX, device_output=True)
         rows += r.n
+        if not args.wm_sync:   # (the stats call completes every fire)
+            rows = op.stats()["rows_fired"] - rows0
         return rows, xgmi
 
     def kstats():

@@ -95,7 +95,8 @@ BATCH_KEY32, BATCH_ROWTIME32, BATCH_VAL32 = 1, 2, 4   # fg_batch.format
 
 # every symbol include/flinkgpu.h declares
 EXPORTS = (
-    "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_advance_progress_async",
+    "fg_collect_fired", "fg_flush", "fg_snapshot_state", "fg_restore",
     "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
@@ -139,6 +140,8 @@ def load():
     L.fg_add_rows.argtypes = [P, C.POINTER(FgRowBatch)]
     L.fg_add_partials.argtypes = [P, C.POINTER(FgPartials)]
     L.fg_advance_progress.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(FgRows)]
+    L.fg_advance_progress_async.argtypes = [P, C.c_int64]
+    L.fg_collect_fired.argtypes = [P, C.POINTER(FgRows)]
     L.fg_flush.argtypes = [P]
     L.fg_snapshot_state.argtypes = [P, C.POINTER(FgStateRows), C.POINTER(C.c_int64)]
     L.fg_restore.argtypes = [P, C.POINTER(FgStateRows), C.c_int64]
@@ -186,7 +189,8 @@ def load():
     for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
                "fg_key_dict_copy_arena"):
         getattr(L, fn).restype = C.c_int
-    for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_flush", "fg_snapshot_state", "fg_restore",
+    for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress",
+               "fg_advance_progress_async", "fg_collect_fired", "fg_flush", "fg_snapshot_state", "fg_restore",
                "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int

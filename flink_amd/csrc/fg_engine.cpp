@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <csignal>
+#include <execinfo.h>
 #include <map>
 #include <memory>
 #include <string>
@@ -288,6 +290,19 @@ struct fg_handle {
     DevBuf plan_dev;          // k_scan_plan's lane plan (speculative pass 2)
     HostBuf h_pass;           // coherent host memory k_scan_plan writes the pass's counters + plan to
     unsigned long long pass_seq = 0;   // k_scan_plan's sequence word in h_pass
+    // asynchronous advance (fg_advance_progress_async): its fires publish the scalars to h_fire
+    // (k_publish_words) instead of synchronizing; the completion -- row count, region retries,
+    // overflow check -- is taken by complete_fire at the next call that needs it
+    HostBuf h_fire;
+    unsigned long long fire_seq = 0;
+    bool async_advance = false;   // the advance in progress publishes its fires
+    bool fire_pending = false;    // published, not yet completed
+    bool fire_rows_open = false;  // the pending fire's rows are not yet in rows_fired
+    int fire_kclass = 0;          // kernel class credited with the pending fire's rows
+    int64_t fire_before = 0;      // out_n when the pending fire was published
+    bool async_open = false;      // rows of async advances not yet collected: the next one appends
+    int64_t adv_base = 0;         // rows ahead of the current advance's in the output buffers
+    int64_t fire_rows_base = 0;   // adv_base of the advance whose rows complete_fire counts
     bool counters_clean = false;   // the device counters hold their initial values
     bool speculate = true;    // FG_SPECULATE=0 turns the speculative pass 2 off (A/B)
     PendingBatch pending;     // deferred first pass of the last batch
@@ -430,22 +445,30 @@ hipEvent_t ev_get(fg_handle* h) {
     (void)hipEventCreate(&e);
     return e;
 }
-// bracket one launch with HIP events on the handle's stream (FG_FLAG_KERNEL_TIMING)
+// bracket one launch call with HIP events on the handle's stream (FG_FLAG_KERNEL_TIMING): the
+// events ride in the kernels' dispatch packets (fg_launch), so timing adds no queue markers
 struct KTimer {
     fg_handle* h;
     int cls;
     int64_t records;
-    hipEvent_t a = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
     KTimer(fg_handle* hh, int c, int64_t r) : h(hh), cls(c), records(r) {
         if (h->timing && ((h->timing_mask >> cls) & 1u)) {
             a = ev_get(h);
-            (void)hipEventRecord(a, h->stream);
+            b = ev_get(h);
+            g_launch_ev.start = a;
+            g_launch_ev.stop = b;
         }
     }
     ~KTimer() {
         if (!a) return;
-        hipEvent_t b = ev_get(h);
-        (void)hipEventRecord(b, h->stream);
+        const bool launched = g_launch_ev.start == nullptr;
+        g_launch_ev = LaunchEvents{};
+        if (!launched) {   // the call launched nothing: no span
+            h->ev_pool.push_back(a);
+            h->ev_pool.push_back(b);
+            return;
+        }
         h->pend.push_back(PendingEv{cls, a, b, records});
     }
 };
@@ -518,7 +541,7 @@ void table_free(fg_handle* h, int64_t slice_end) {
     auto it = h->tables.find(slice_end);
     if (it == h->tables.end()) return;
     // a merge launched since the last synchronization may still need it (region retry)
-    if (h->defer_free) h->deferred.push_back(std::move(it->second));
+    if (h->defer_free || h->fire_pending) h->deferred.push_back(std::move(it->second));
     else h->table_pool.push_back(std::move(it->second));
     h->tables.erase(it);
 }
@@ -779,6 +802,48 @@ int settle_jobs(fg_handle* h) {
 
 // Reduce the slice lanes to lanes_for(region bits) once the lanes above it hold nothing
 // (after a split to 2^13 regions, two lanes keep the two-pass partition).
+// ---- asynchronous advance: publish a fire's results, complete it later -----------------
+// The fires of fg_advance_progress_async end with k_publish_words (the scalars -- overflow
+// flags, fired-row count, fail count -- into coherent host memory, then a sequence word)
+// instead of a D2H copy and a stream synchronization; the host's bookkeeping (tables freed,
+// lanes released) is done at once, tables freed meanwhile are held (table_free) and the staged
+// passes stay intact until the next ingest, which completes the fire first -- so a region retry
+// still finds its inputs.
+int publish_fire(fg_handle* h, int kclass) {
+    h->fire_seq++;
+    HIPCHK(h, launch_publish_words(h->scalars.as<unsigned long long>(), (int32_t)(kScalarBytes / 8),
+                                   h->h_fire.as<unsigned long long>(), h->fire_seq, h->stream));
+    h->fire_pending = true;
+    h->fire_kclass = kclass;
+    h->fire_before = h->out_n;
+    return FG_OK;
+}
+int complete_fire(fg_handle* h) {
+    if (!h->fire_pending) return FG_OK;
+    h->fire_pending = false;
+    const volatile unsigned long long* sq = h->h_fire.as<unsigned long long>() + kScalarBytes / 8;
+    for (int64_t spin = 0; *sq != h->fire_seq; spin++) {
+        if (spin > (1 << 12) && hipStreamQuery(h->stream) != hipErrorNotReady) {
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            if (*sq != h->fire_seq) return h->fail(FG_EDEVICE, "internal: fire scalars never arrived");
+            break;
+        }
+    }
+    std::memcpy(h->h_scalars.p, h->h_fire.p, kScalarBytes);
+    int rc = settle_jobs(h);   // regions that overflowed: split and redone (their rows counted)
+    if (rc) return rc;
+    rc = check_overflow(h);
+    if (rc) return rc;
+    h->out_n = (int64_t)h->h_scalars.as<unsigned long long>()[1];
+    h->kstat[h->fire_kclass].rows += h->out_n - h->fire_before;
+    h->pending_out = 0;
+    if (h->fire_rows_open) {   // the advance returned before its rows were known
+        h->rows_fired += h->out_n - h->fire_rows_base;
+        h->fire_rows_open = false;
+    }
+    return FG_OK;
+}
+
 void maybe_reduce_lanes(fg_handle* h) {
     if (h->lanes_target <= 0 || h->lanes_target >= h->lanes) return;
     for (int l = h->lanes_target; l < h->lanes; l++)
@@ -795,9 +860,10 @@ int fire_collect(fg_handle* h);
 int reset_out_count(fg_handle* h) {
     if (!h->out_count_reset) {
         HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
-        if (h->late_rows > 0) {   // rows fired by late elements lead the advance's rows
+        // rows fired by late elements, or by async advances not yet collected, lead the advance's rows
+        if (h->adv_base + h->late_rows > 0) {
             Words16 w{};
-            w.v[0] = (unsigned long long)h->late_rows;
+            w.v[0] = (unsigned long long)(h->adv_base + h->late_rows);
             w.n = 1;
             HIPCHK(h, launch_store_words(reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8), w, h->stream));
         }
@@ -940,6 +1006,7 @@ int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, Heav
 // AbstractWindowAggProcessor.java:200-206).
 int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* fire) {
     if (sel_in.empty()) return FG_OK;
+    if (int rc0 = complete_fire(h)) return rc0;   // (one fire's rows and scalars at a time)
     std::vector<int> sel = sel_in;   // slice order: windows fired by the flush fire in order
     std::sort(sel.begin(), sel.end(), [&](int a, int b) { return h->lane[a].q < h->lane[b].q; });
     if (h->out_count_reset) HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
@@ -1141,6 +1208,17 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             t->upper = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, kStateCapMax);
         }
     }
+    if (h->async_advance && any_emit) {
+        // fg_advance_progress_async: the host's bookkeeping now, the device's results later
+        // (complete_fire); tables freed here are held until then
+        rc = publish_fire(h, K_FLUSH_FIRE);   // (first: the tables freed below are held)
+        if (rc) return rc;
+        for (int64_t se : fired_tables) table_free(h, se);
+        for (int64_t se : retained) retire(h, se, se);
+        for (int l : sel) release_lane(h, l);
+        h->flushes++;
+        return FG_OK;
+    }
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, kScalarBytes, hipMemcpyDeviceToHost, h->stream));
     rc = sync(h);
     if (rc) return rc;
@@ -1190,6 +1268,7 @@ int ensure_out(fg_handle* h, int64_t need) {
 // `defer`: no host synchronization -- the caller collects the row count (fire_collect)
 // after the advance's last fire (launches stay ordered on the handle's stream).
 int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, SliceTable* dst, bool defer = false) {
+    if (int rc0 = complete_fire(h)) return rc0;
     int64_t ub = 0;
     for (auto* s : srcs) ub += s->upper;
     ub = std::min<int64_t>(ub, kStateCapMax);
@@ -1264,6 +1343,9 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
 
 // after fires: region retries, overflow check and the fired-row count (one synchronization)
 int fire_collect(fg_handle* h) {
+    if (h->async_advance) {   // fg_advance_progress_async: completed by the next call that needs it
+        return publish_fire(h, K_FIRE);   // (tables freed by the fires stay held until then)
+    }
     HIPCHK(h, hipMemcpyAsync(h->h_scalars.p, h->scalars.p, kScalarBytes, hipMemcpyDeviceToHost, h->stream));
     int rc = sync(h);
     if (rc) return rc;
@@ -1290,6 +1372,7 @@ int fire_windows(fg_handle* h, int64_t prev, int64_t wm) {
     h->defer_free = false;
     if (rc) return rc;
     if (fired) return fire_collect(h);
+    if (h->fire_pending) return FG_OK;   // (freed tables held until the pending fire completes)
     for (auto& t : h->deferred) h->table_pool.push_back(std::move(t));
     h->deferred.clear();
     return FG_OK;
@@ -1535,6 +1618,7 @@ int refire_datastream(fg_handle* h, int64_t wm) {
 }
 
 int refire(fg_handle* h, int64_t wm) {
+    if (int rc0 = complete_fire(h)) return rc0;
     if (h->cfg.mode == FG_MODE_DATASTREAM) return refire_datastream(h, wm);
     const WindowSpec& w = h->w;
     const int64_t S = w.slice;
@@ -2338,6 +2422,7 @@ int64_t late_wm(const fg_handle* h) { return std::max(h->current_progress, h->la
 // cleaned windows at once (EventTimeTrigger.onElement :37-46) -- rows appended to the output
 // buffers, returned by the next fg_advance_progress ahead of its own rows.
 int late_fire(fg_handle* h, int64_t nl) {
+    if (int rc0 = complete_fire(h)) return rc0;
     const WindowSpec& w = h->w;
     const int64_t wm = late_wm(h);
     const int64_t nwin = w.kind == TUMBLE ? 1 : w.size / w.slide;
@@ -2530,6 +2615,7 @@ int late_split(fg_handle* h, int64_t n, const int64_t** key, const int64_t** ts,
 // Every entry point first completes a deferred batch (its counters were copied behind
 // pass 1's plan, so the wait is usually over before pass 2 ends).
 int settle_pending(fg_handle* h) {
+    if (int rc0 = complete_fire(h)) return rc0;   // every entry point but a quiet async advance
     if (!h->pending.active) return FG_OK;
     h->pending.active = false;
     // k_scan_plan writes its sequence word into coherent host memory after the counters and
@@ -2590,7 +2676,27 @@ int fg_host_unregister(int32_t device_id, void* p) {
     return FG_OK;
 }
 
+// FG_BACKTRACE=1 (diagnostics): a host fault prints the native frames to stderr
+static void fg_fault_trace(int sig) {
+    void* b[64];
+    const int n = backtrace(b, 64);
+    backtrace_symbols_fd(b, n, 2);
+    std::signal(sig, SIG_DFL);
+    std::raise(sig);
+}
+
 int fg_open(const fg_config* cfg, fg_handle** out) {
+    if (getenv("FG_BACKTRACE")) {   // (on its own stack: a stack overflow is traced too)
+        static char alt[1 << 16];
+        stack_t ss{};
+        ss.ss_sp = alt;
+        ss.ss_size = sizeof alt;
+        sigaltstack(&ss, nullptr);
+        struct sigaction sa{};
+        sa.sa_handler = fg_fault_trace;
+        sa.sa_flags = SA_ONSTACK;
+        sigaction(SIGSEGV, &sa, nullptr);
+    }
     *out = nullptr;
     if (!cfg) {
         g_open_error = "null config";
@@ -2824,6 +2930,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
               chk(hp->h_counters.ensure(sizeof(Counters) + sizeof(IngestPlan))) &&
               chk(hp->plan_dev.ensure(sizeof(IngestPlan))) && chk(hp->row_bad.ensure(16)) &&
               chk(hp->h_pass.ensure(sizeof(DevCounters) + sizeof(IngestPlan) + 8, hipHostMallocCoherent)) &&
+              chk(hp->h_fire.ensure(kScalarBytes + 8, hipHostMallocCoherent)) &&
               chk(hp->arena.ensure(1 << 20)) && chk(hp->h_arena.ensure(1 << 20)) && chk(hp->scalars.ensure(64)) && chk(hp->sink.ensure(256)) &&
               chk(hp->h_scalars.ensure(64)) && chk(hp->fail_list.ensure(4 * (size_t)kFailCap));
     if (!ok) {
@@ -3144,11 +3251,12 @@ int fg_flush(fg_handle* h) {
     return flush(h);
 }
 
-int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows* fired) {
-    if (!h) return FG_EINVAL;
-    HIPCHK(h, hipSetDevice(h->device));
+// (static: inside the extern "C" block an exported `advance` is interposed by libc's)
+// processWatermark without the output: flushes, re-fires, fires, cleanup timers
+static int advance_progress(fg_handle* h, int64_t wm) {
     if (int rc0 = settle_pending(h)) return rc0;
-    h->out_n = h->late_rows;   // rows fired by late elements since the last advance come first
+    h->adv_base = h->async_advance && h->async_open ? h->out_n : 0;
+    h->out_n = h->adv_base + h->late_rows;   // rows fired by late elements since the last advance come first
     h->pending_out = 0;
     h->out_count_reset = false;
     h->fused_fired.clear();
@@ -3222,6 +3330,89 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     }
     if (h->late_horizon != JMIN && h->current_progress >= h->late_horizon) h->late_horizon = JMIN;
     h->late_rows = 0;
+    return FG_OK;
+}
+
+// A watermark that can neither flush, fire, re-fire nor free anything (TUMBLE / DataStream
+// tumbling between window ends: no resident tables, the staged slices not yet fired): with a
+// fire pending, fg_advance_progress_async takes only its progress bookkeeping -- the fire's
+// completion is left to the call that needs it, so the host does not wait for the fire here.
+static bool quiet_advance(const fg_handle* h, int64_t wm) {
+    if (!h->fire_pending || h->pending.active || h->late_rows > 0 || h->local || h->refire_hi != JMIN ||
+        !h->retire_at.empty() || !h->tables.empty() || h->lateness > 0)
+        return false;
+    if (!staged_any(h)) return true;
+    const bool fired = is_window_fired(h->w, min_staged_slice_end(h), wm);
+    if (h->cfg.mode == FG_MODE_SQL)   // (advance: flush iff progress moves past the next trigger onto a fired slice)
+        return !(wm > h->current_progress && wm >= h->next_trigger && fired);
+    return !fired;
+}
+static void quiet_progress(fg_handle* h, int64_t wm) {   // advance()'s bookkeeping on the quiet path
+    if (h->cfg.mode == FG_MODE_SQL) {
+        if (wm > h->current_progress) {
+            h->current_progress = wm;
+            if (h->current_progress >= h->next_trigger) h->next_trigger = next_trigger_watermark(h->w, wm, h->w.slice);
+        }
+    } else if (wm > h->current_progress) {
+        h->current_progress = wm;
+    }
+    h->arrival_progress = h->current_progress;
+    if (wm > h->timer_wm) h->timer_wm = wm;
+    if (h->late_horizon != JMIN && h->current_progress >= h->late_horizon) h->late_horizon = JMIN;
+}
+
+int fg_advance_progress_async(fg_handle* h, int64_t wm) {
+    if (!h) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (quiet_advance(h, wm)) {
+        quiet_progress(h, wm);
+        return FG_OK;
+    }
+    if (h->lateness > 0)   // (late elements fire rows at fg_add_batch, ahead of any advance's)
+        return h->fail(FG_EINVAL, "fg_advance_progress_async: allowed lateness needs fg_advance_progress");
+    h->async_advance = true;
+    const int rc = advance_progress(h, wm);
+    h->async_advance = false;
+    if (rc) return rc;
+    h->async_open = true;
+    if (h->fire_pending) {   // rows_fired at completion
+        h->fire_rows_open = true;
+        h->fire_rows_base = h->adv_base;
+    } else {
+        h->rows_fired += h->out_n - h->adv_base;
+    }
+    return FG_OK;
+}
+
+static void device_rows(fg_handle* h, int32_t out_location, fg_rows* fired) {
+    std::memset(fired, 0, sizeof *fired);
+    fired->n = h->out_n;
+    fired->num_aggs = h->cfg.num_aggs;
+    fired->location = out_location;
+    fired->key = h->o_key.as<int64_t>();
+    fired->window_start = h->o_ws.as<int64_t>();
+    fired->window_end = h->o_we.as<int64_t>();
+    fired->null_mask = h->o_null.as<uint8_t>();
+    fired->rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->o_rt.as<int64_t>() : nullptr;
+    for (int a = 0; a < h->cfg.num_aggs; a++) fired->agg[a] = h->o_agg[a].as<int64_t>();
+}
+
+int fg_collect_fired(fg_handle* h, fg_rows* fired) {
+    if (!h || !fired) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (int rc = complete_fire(h)) return rc;
+    device_rows(h, FG_DEVICE, fired);
+    if (!h->async_open) fired->n = 0;   // (every async advance since the last collect fired nothing)
+    h->async_open = false;
+    return FG_OK;
+}
+
+int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows* fired) {
+    if (!h) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    h->async_open = false;   // (rows of async advances not collected by now are dropped)
+    int rc = advance_progress(h, wm);
+    if (rc) return rc;
     h->rows_fired += h->out_n;
     if (fired) {
         std::memset(fired, 0, sizeof *fired);
@@ -3232,12 +3423,7 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
             rc = copy_out_to_host(h, fired);
             if (rc) return rc;
         } else {
-            fired->key = h->o_key.as<int64_t>();
-            fired->window_start = h->o_ws.as<int64_t>();
-            fired->window_end = h->o_we.as<int64_t>();
-            fired->null_mask = h->o_null.as<uint8_t>();
-            fired->rowtime = h->cfg.mode == FG_MODE_DATASTREAM ? h->o_rt.as<int64_t>() : nullptr;
-            for (int a = 0; a < h->cfg.num_aggs; a++) fired->agg[a] = h->o_agg[a].as<int64_t>();
+            device_rows(h, out_location, fired);
         }
     }
     return FG_OK;
@@ -3541,6 +3727,7 @@ int fg_reset(fg_handle* h) {
     h->late_dropped = 0;
     h->out_n = 0;
     h->pending_out = 0;
+    h->async_open = false;
     h->re_new.clear();
     h->re_delta.clear();
     h->re_tmp.clear();

@@ -3,9 +3,30 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <hip/hip_ext.h>
+
 #include "fg_window.h"
 
 namespace fg {
+
+// Kernel timing (FG_FLAG_KERNEL_TIMING): the engine's KTimer arms these events and the next
+// launches on this thread carry them in their own dispatch packets (hipExtLaunchKernel) --
+// the first launch of the bracketed call records `start`, every launch `stop` (the last one
+// wins). Separate hipEventRecord markers each cost a queue round of 6-20 us between kernels.
+struct LaunchEvents {
+    hipEvent_t start = nullptr;
+    hipEvent_t stop = nullptr;
+};
+extern thread_local LaunchEvents g_launch_ev;
+template <class K, class... A>
+inline void fg_launch(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, A... a) {
+    if (g_launch_ev.stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, g_launch_ev.start, g_launch_ev.stop, 0u, a...);
+        g_launch_ev.start = nullptr;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, a...);
+    }
+}
 
 // LDS hash table of one state region: kSlots open-addressing slots + 1 slot reserved
 // for the key that equals the EMPTY sentinel (Long.MIN_VALUE).
@@ -325,6 +346,8 @@ struct Words16 {
     int32_t n;
 };
 hipError_t launch_store_words(unsigned long long* dst, const Words16& w, hipStream_t s);
+hipError_t launch_publish_words(const unsigned long long* src, int32_t n, unsigned long long* host,
+                                unsigned long long seq, hipStream_t s);
 hipError_t launch_widen_columns(const int32_t* k32, const uint32_t* t32, const int32_t* v32, int64_t n, int64_t tbase,
                                 int64_t* key, int64_t* ts, int64_t* val, hipStream_t s);
 hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz, int64_t S, int64_t phase,

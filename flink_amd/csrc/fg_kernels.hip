@@ -25,6 +25,8 @@
 
 namespace fg {
 
+thread_local LaunchEvents g_launch_ev;
+
 #ifndef FG_DIAG_PART2
 #define FG_DIAG_PART2 0    // diagnostic builds only (wrong results): bit0 no writes, bit1 no loads, bit2 no map
 #endif
@@ -1053,7 +1055,7 @@ __global__ __launch_bounds__(kScanPlanThreads) void k_scan_plan(IngestParams p, 
 
 hipError_t launch_scan_plan(const IngestParams& p, const PlanParams& pp, const ScanPlanArgs& a, hipStream_t s) {
     if (a.n_words < 1 || a.n_words > 16 || a.reset.n > a.n_words) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_scan_plan, dim3(1), dim3(kScanPlanThreads), 0, s, p, pp, a);
+    fg_launch(k_scan_plan, dim3(1), dim3(kScanPlanThreads), 0, s, p, pp, a);
     return hipGetLastError();
 }
 
@@ -1067,7 +1069,7 @@ hipError_t launch_part1(const IngestParams& p, hipStream_t s) {
     if (p.n_coarse < 1 || p.n_coarse > kMaxCoarse || (p.lanes << p.region_bits) > kMaxPart1Fine ||
         p.region_bits < kFineBits || p.max_tiles > kPart2MaxFrags)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_part1, dim3(p.grid), dim3(kPart1Threads), 0, s, p);
+    fg_launch(k_part1, dim3(p.grid), dim3(kPart1Threads), 0, s, p);
     return hipGetLastError();
 }
 
@@ -1079,11 +1081,11 @@ hipError_t launch_part2(const IngestParams& p, hipStream_t s) {
     if (units == 0) return hipSuccess;
     if (p.narrow) {
         if (p.st_stride != 2) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_part2<true, true>), dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+        fg_launch((k_part2<true, true>), dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
     } else if (p.st_stride == 2) {
-        hipLaunchKernelGGL(k_part2<true>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+        fg_launch(k_part2<true>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
     } else {
-        hipLaunchKernelGGL(k_part2<false>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
+        fg_launch(k_part2<false>, dim3((unsigned)units), dim3(kPart2Threads), 0, s, p, group);
     }
     return hipGetLastError();
 }
@@ -1132,7 +1134,7 @@ __global__ void k_rows_to_columns(const uint8_t* rows, int64_t n, RowLayout L, i
 hipError_t launch_rows_to_columns(const uint8_t* rows, int64_t n, const RowLayout& L, int64_t* key, int64_t* ts,
                                   int64_t* val, uint8_t* vnull, unsigned long long* bad, hipStream_t s) {
     const int64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_rows_to_columns, dim3((unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096)), dim3(256),
+    fg_launch(k_rows_to_columns, dim3((unsigned)(blocks < 4096 ? (blocks > 0 ? blocks : 1) : 4096)), dim3(256),
                        0, s, rows, n, L, key, ts, val, vnull, bad);
     return hipGetLastError();
 }
@@ -1166,7 +1168,7 @@ __global__ void k_widen_columns(const int32_t* k32, const uint32_t* t32, const i
 hipError_t launch_widen_columns(const int32_t* k32, const uint32_t* t32, const int32_t* v32, int64_t n, int64_t tbase,
                                 int64_t* key, int64_t* ts, int64_t* val, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_widen_columns, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k32, t32, v32, n, tbase,
+    fg_launch(k_widen_columns, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k32, t32, v32, n, tbase,
                        key, ts, val);
     return hipGetLastError();
 }
@@ -1175,7 +1177,7 @@ hipError_t launch_window_end_rowtime(const int64_t* wend, int64_t n, int64_t tz,
                                      int64_t* out, unsigned long long* off_grid, hipStream_t s) {
     int64_t blocks = (n + 255) / 256;
     blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
-    hipLaunchKernelGGL(k_window_end_rowtime, dim3((unsigned)blocks), dim3(256), 0, s, wend, n, tz, S, phase, out, off_grid);
+    fg_launch(k_window_end_rowtime, dim3((unsigned)blocks), dim3(256), 0, s, wend, n, tz, S, phase, out, off_grid);
     return hipGetLastError();
 }
 
@@ -1185,14 +1187,34 @@ __global__ void k_store_words(unsigned long long* dst, Words16 w) {
 
 hipError_t launch_store_words(unsigned long long* dst, const Words16& w, hipStream_t s) {
     if (w.n < 0 || w.n > 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_store_words, dim3(1), dim3(64), 0, s, dst, w);
+    fg_launch(k_store_words, dim3(1), dim3(64), 0, s, dst, w);
+    return hipGetLastError();
+}
+
+// n device words to coherent host memory, then the sequence word after them: the host polls
+// for `seq` instead of synchronizing the stream (no interrupt wake-up, no D2H blit)
+__global__ void k_publish_words(const unsigned long long* src, int32_t n, unsigned long long* host,
+                                unsigned long long seq) {
+    if ((int)threadIdx.x < n) host[threadIdx.x] = src[threadIdx.x];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *reinterpret_cast<volatile unsigned long long*>(host + n) = seq;
+        __threadfence_system();
+    }
+}
+
+hipError_t launch_publish_words(const unsigned long long* src, int32_t n, unsigned long long* host,
+                                unsigned long long seq, hipStream_t s) {
+    if (n < 0 || n > 64) return hipErrorInvalidValue;
+    fg_launch(k_publish_words, dim3(1), dim3(64), 0, s, src, n, host, seq);
     return hipGetLastError();
 }
 
 hipError_t launch_pseudo_rowtime(const int64_t* slice_end, int64_t n, int64_t tz, int64_t* out, hipStream_t s) {
     int64_t blocks = (n + 255) / 256;
     blocks = blocks > 8192 ? 8192 : (blocks < 1 ? 1 : blocks);
-    hipLaunchKernelGGL(k_pseudo_rowtime, dim3((unsigned)blocks), dim3(256), 0, s, slice_end, n, tz, out);
+    fg_launch(k_pseudo_rowtime, dim3((unsigned)blocks), dim3(256), 0, s, slice_end, n, tz, out);
     return hipGetLastError();
 }
 
@@ -1227,7 +1249,7 @@ __global__ __launch_bounds__(kIngestThreads) void k_acc_scatter(IngestParams p, 
 }
 
 hipError_t launch_acc_scatter(const IngestParams& p, const AccColumns& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_acc_scatter, dim3(p.grid), dim3(kIngestThreads), 0, s, p, a);
+    fg_launch(k_acc_scatter, dim3(p.grid), dim3(kIngestThreads), 0, s, p, a);
     return hipGetLastError();
 }
 
@@ -1267,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_hist_columns(uint32_t* hist, uint32_t* 
 
 hipError_t launch_hist_columns(uint32_t* hist, uint32_t* totals, int32_t F, int32_t grid, hipStream_t s) {
     if (grid > 4 * kHcRows) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_hist_columns, dim3((F + 63) / 64), dim3(256), 0, s, hist, totals, F, grid);
+    fg_launch(k_hist_columns, dim3((F + 63) / 64), dim3(256), 0, s, hist, totals, F, grid);
     return hipGetLastError();
 }
 
@@ -1326,14 +1348,14 @@ size_t scan_tmp_words(int64_t n) { return (size_t)((n + kScanChunk - 1) / kScanC
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, int64_t n, uint32_t* tmp, hipStream_t s) {
     const int64_t nb = (n + kScanChunk - 1) / kScanChunk;
     if (nb == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, n, tmp);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, tmp, nb);
-    hipLaunchKernelGGL(k_scan_final, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, n, tmp, out);
+    fg_launch(k_scan_reduce, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, n, tmp);
+    fg_launch(k_scan_blocks, dim3(1), dim3(kScanThreads), 0, s, tmp, nb);
+    fg_launch(k_scan_final, dim3((unsigned)nb), dim3(kScanThreads), 0, s, in, n, tmp, out);
     return hipGetLastError();
 }
 
 hipError_t launch_ingest_count(const IngestParams& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_ingest_count, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    fg_launch(k_ingest_count, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     return hipGetLastError();
 }
 hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
@@ -1341,11 +1363,11 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
     for (int l = 0; l < kMaxLanes; l++) nslots += p.lane_slot[l] >= 0 ? 1 : 0;
     const int FS = nslots << p.region_bits;
     if (p.sorted && FS <= 4 * kIngestThreads)
-        hipLaunchKernelGGL(k_ingest_scatter_sorted<4>, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+        fg_launch(k_ingest_scatter_sorted<4>, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     else if (p.sorted)
-        hipLaunchKernelGGL(k_ingest_scatter_sorted<kMaxSortedBuckets / kIngestThreads>, dim3(p.grid),
+        fg_launch(k_ingest_scatter_sorted<kMaxSortedBuckets / kIngestThreads>, dim3(p.grid),
                            dim3(kIngestThreads), 0, s, p);
-    else hipLaunchKernelGGL(k_ingest_scatter_direct, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
+    else fg_launch(k_ingest_scatter_direct, dim3(p.grid), dim3(kIngestThreads), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2426,7 +2448,7 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit_table(MergeParams p, Tabl
 }
 
 hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_t s) {
-    hipLaunchKernelGGL(k_emit_table, dim3(1u << p.region_bits), dim3(kEmitThreads), 0, s, p, t);
+    fg_launch(k_emit_table, dim3(1u << p.region_bits), dim3(kEmitThreads), 0, s, p, t);
     return hipGetLastError();
 }
 
@@ -2437,11 +2459,11 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
             // the common list (SUM family, MIN and MAX) over BIGINT / DOUBLE: ops compiled in
             const bool all3 = p.vop[0] == 0 && p.vop[1] == 1 && p.vop[2] == 2;
             constexpr int MT = MergeCfg<true, true>::kThreads;
-            if (all3 && p.val_type == 2) hipLaunchKernelGGL((k_merge<true, 2, true>), dim3(workgroups), dim3(MT), 0, s, p);
-            else if (all3 && p.val_type == 1) hipLaunchKernelGGL((k_merge<true, 1, true>), dim3(workgroups), dim3(MT), 0, s, p);
-            else hipLaunchKernelGGL((k_merge<true, -1, true>), dim3(workgroups), dim3(MT), 0, s, p);
+            if (all3 && p.val_type == 2) fg_launch((k_merge<true, 2, true>), dim3(workgroups), dim3(MT), 0, s, p);
+            else if (all3 && p.val_type == 1) fg_launch((k_merge<true, 1, true>), dim3(workgroups), dim3(MT), 0, s, p);
+            else fg_launch((k_merge<true, -1, true>), dim3(workgroups), dim3(MT), 0, s, p);
         } else {
-            hipLaunchKernelGGL((k_merge<false, -1, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+            fg_launch((k_merge<false, -1, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
         }
         return hipGetLastError();
     }
@@ -2457,22 +2479,22 @@ hipError_t launch_merge(const MergeParams& p, int32_t workgroups, hipStream_t s)
         // the compact merge (the TUMBLE fire of plain staged records) per value op
         if (n12) {
             switch (p.val_type) {
-                case 1: hipLaunchKernelGGL((k_merge<true, 1, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
-                case 2: hipLaunchKernelGGL((k_merge<true, 2, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
-                default: hipLaunchKernelGGL((k_merge<true, -1, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+                case 1: fg_launch((k_merge<true, 1, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+                case 2: fg_launch((k_merge<true, 2, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+                default: fg_launch((k_merge<true, -1, false, true>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
             }
             return hipGetLastError();
         }
         switch (p.val_type) {
-            case 0: hipLaunchKernelGGL((k_merge<true, 0>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
-            case 1: hipLaunchKernelGGL((k_merge<true, 1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
-            case 2: hipLaunchKernelGGL((k_merge<true, 2>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
-            default: hipLaunchKernelGGL((k_merge<true, -1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            case 0: fg_launch((k_merge<true, 0>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            case 1: fg_launch((k_merge<true, 1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            case 2: fg_launch((k_merge<true, 2>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
+            default: fg_launch((k_merge<true, -1>), dim3(workgroups), dim3(kCompactMergeThreads), 0, s, p); break;
         }
     } else if (n12) {
-        hipLaunchKernelGGL((k_merge<false, -1, false, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+        fg_launch((k_merge<false, -1, false, true>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     } else {
-        hipLaunchKernelGGL((k_merge<false, -1>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
+        fg_launch((k_merge<false, -1>), dim3(workgroups), dim3(kMergeThreads), 0, s, p);
     }
     return hipGetLastError();
 }
@@ -2686,13 +2708,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_heavy_chunks(HeavyPlan hp) {
 
 hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s) {
     if (hp.region_bits > 13 || hp.n_batches < 1 || hp.chunk < 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_heavy_plan, dim3(1), dim3(kPlanThreads), 0, s, hp);
+    fg_launch(k_heavy_plan, dim3(1), dim3(kPlanThreads), 0, s, hp);
     return hipGetLastError();
 }
 
 hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s) {
-    if (hp.mv) hipLaunchKernelGGL(k_heavy_chunks<true>, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
-    else hipLaunchKernelGGL(k_heavy_chunks<false>, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
+    if (hp.mv) fg_launch(k_heavy_chunks<true>, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
+    else fg_launch(k_heavy_chunks<false>, dim3(workgroups), dim3(kMergeThreads), 0, s, hp);
     return hipGetLastError();
 }
 
@@ -2720,7 +2742,7 @@ __global__ __launch_bounds__(256) void k_export(ExportParams p) {
 }
 
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s) {
-    hipLaunchKernelGGL(k_export, dim3(regions), dim3(256), 0, s, p);
+    fg_launch(k_export, dim3(regions), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 
@@ -2756,7 +2778,7 @@ __global__ __launch_bounds__(kSplitThreads) void k_split_table(TableRef src, Tab
 hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift, int32_t mv,
                               hipStream_t s) {
     if (shift < 1 || old_bits < 0 || old_bits + shift > 13) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_split_table, dim3(1u << old_bits), dim3(kSplitThreads), 0, s, src, dst, old_bits, shift, mv);
+    fg_launch(k_split_table, dim3(1u << old_bits), dim3(kSplitThreads), 0, s, src, dst, old_bits, shift, mv);
     return hipGetLastError();
 }
 
@@ -2773,7 +2795,7 @@ hipError_t launch_key_groups(const int64_t* key, int64_t n, int32_t key_hash, in
     int64_t blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_key_groups, dim3((unsigned)blocks), dim3(256), 0, s, key, n, key_hash, max_p, out);
+    fg_launch(k_key_groups, dim3((unsigned)blocks), dim3(256), 0, s, key, n, key_hash, max_p, out);
     return hipGetLastError();
 }
 
@@ -2847,13 +2869,13 @@ hipError_t launch_partition_cols_by_owner(const OwnerCols& c, int64_t n, int32_t
     uint32_t* hist = scratch;
     uint32_t* offs = scratch + m;
     uint32_t* tmp = scratch + 2 * m + 1;
-    hipLaunchKernelGGL(k_owner_count, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, c.in[0], n, key_hash, max_p, par,
+    fg_launch(k_owner_count, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, c.in[0], n, key_hash, max_p, par,
                        hist);
     hipError_t e = launch_scan_u32(hist, offs, m, tmp, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_owner_scatter_cols, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, c, n, key_hash, max_p, par,
+    fg_launch(k_owner_scatter_cols, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, c, n, key_hash, max_p, par,
                        offs);
-    hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
+    fg_launch(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
     return hipGetLastError();
 }
 
@@ -2871,12 +2893,12 @@ hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, cons
     uint32_t* hist = scratch;
     uint32_t* offs = scratch + m;
     uint32_t* tmp = scratch + 2 * m + 1;
-    hipLaunchKernelGGL(k_owner_count, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, n, key_hash, max_p, par, hist);
+    fg_launch(k_owner_count, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, n, key_hash, max_p, par, hist);
     hipError_t e = launch_scan_u32(hist, offs, m, tmp, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_owner_scatter, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, ts, val, n, key_hash, max_p,
+    fg_launch(k_owner_scatter, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, ts, val, n, key_hash, max_p,
                        par, offs, out_key, out_ts, out_val);
-    hipLaunchKernelGGL(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
+    fg_launch(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
     return hipGetLastError();
 }
 

@@ -286,32 +286,32 @@ inline unsigned grid_of(int64_t n, int per_block) { return (unsigned)((n + per_b
 
 hipError_t launch_late_split(const LateSplit& p, hipStream_t s) {
     if (p.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_late_split, dim3(grid_of(p.n, kLateThreads)), dim3(kLateThreads), 0, s, p);
+    fg_launch(k_late_split, dim3(grid_of(p.n, kLateThreads)), dim3(kLateThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_late_reset(const LateRound& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_late_reset, dim3(grid_of((int64_t)p.claim_mask + 2, kLateThreads)), dim3(kLateThreads), 0, s, p);
+    fg_launch(k_late_reset, dim3(grid_of((int64_t)p.claim_mask + 2, kLateThreads)), dim3(kLateThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_late_claim(const LateRound& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_late_claim, dim3(grid_of(p.n, kLateThreads)), dim3(kLateThreads), 0, s, p);
+    fg_launch(k_late_claim, dim3(grid_of(p.n, kLateThreads)), dim3(kLateThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_late_lookup(const LateRound& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_late_lookup, dim3(grid_of(p.n, kLateThreads / 64)), dim3(kLateThreads), 0, s, p);
+    fg_launch(k_late_lookup, dim3(grid_of(p.n, kLateThreads / 64)), dim3(kLateThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_late_update(const LateRound& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_late_update, dim3(grid_of(p.n, kLateThreads)), dim3(kLateThreads), 0, s, p);
+    fg_launch(k_late_update, dim3(grid_of(p.n, kLateThreads)), dim3(kLateThreads), 0, s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_late_emit(const LateRound& p, hipStream_t s) {
-    hipLaunchKernelGGL(k_late_emit, dim3(grid_of(p.n, kLateThreads / 64)), dim3(kLateThreads), 0, s, p);
+    fg_launch(k_late_emit, dim3(grid_of(p.n, kLateThreads / 64)), dim3(kLateThreads), 0, s, p);
     return hipGetLastError();
 }
 

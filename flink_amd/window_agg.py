@@ -330,10 +330,18 @@ class WindowAggOperator:
         del keep
 
     # -- processWatermark ---------------------------------------------------------------------
-    def process_watermark(self, watermark: int, device_output: bool = False):
+    def process_watermark(self, watermark: int, device_output: bool = False, wait: bool = True):
         """Advance event time; returns the rows fired by this watermark: a structured numpy
         array, or with device_output=True the operator's FgRows (device pointers, reused and
-        valid until the next call on this operator)."""
+        valid until the next call on this operator). device_output=True, wait=False is
+        fg_advance_progress_async: the fires are queued and the call returns None at once;
+        collect_fired() waits for them and returns their rows."""
+        if device_output and not wait:
+            rc = self._lib.fg_advance_progress_async(self._h, int(watermark))
+            if rc:
+                L.check(rc, self._h)
+            self._hold(None)
+            return None
         if device_output:
             # one FgRows per operator: device rows are library-owned and valid until the next
             # call on this handle anyway; no per-call allocation on the watermark path
@@ -347,7 +355,30 @@ class WindowAggOperator:
         self._hold(None)
         return self._host_rows(r)
 
-    def _host_rows(self, r: L.FgRows) -> np.ndarray:
+    def collect_fired(self):
+        """The rows of the last process_watermark(..., wait=False) (fg_collect_fired: waits for
+        its fires): the operator's FgRows, device pointers valid until the next call that fires."""
+        L.check(self._lib.fg_collect_fired(self._h, self._dev_rows_ref), self._h)
+        return self._dev_rows
+
+    def rows_to_host(self, r: L.FgRows) -> np.ndarray:
+        """Host copy of device FgRows (process_watermark(device_output=True) / collect_fired) in the
+        layout of the host rows."""
+        import torch
+
+        class _Col:
+            def __init__(self, ptr, typestr, n):
+                self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (int(ptr or 0), False),
+                                                 "version": 2}
+
+        def col(ptr, dtype, count):
+            ts = "|u1" if dtype is C.c_uint8 else "<i8"
+            return torch.as_tensor(_Col(ptr, ts, count), device=torch.device("cuda", self.cfg.device_id)).cpu().numpy()
+
+        torch.cuda.synchronize(self.cfg.device_id)   # (the rows are complete once collected; torch's copy runs on its stream)
+        return self._host_rows(r, col)
+
+    def _host_rows(self, r: L.FgRows, col=None) -> np.ndarray:
         n = r.n
         fields = [("key", "<i8"), ("window_start", "<i8"), ("window_end", "<i8")]
         for a in self.aggs:
@@ -361,8 +392,9 @@ class WindowAggOperator:
         if n == 0:
             return out
 
-        def col(ptr, dtype, count):
-            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(dtype)), shape=(count,)).copy()
+        if col is None:
+            def col(ptr, dtype, count):
+                return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(dtype)), shape=(count,)).copy()
 
         out["key"] = col(r.key, C.c_int64, n)
         out["window_start"] = col(r.window_start, C.c_int64, n)

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 10
+#define FG_ABI_VERSION 11
 
 enum fg_status {
     FG_OK = 0,
@@ -295,6 +295,19 @@ int  fg_add_rows(fg_handle* h, const fg_row_batch* rows);
  * the partial's slice). */
 int  fg_add_partials(fg_handle* h, const fg_partials* partials);
 int  fg_advance_progress(fg_handle* h, int64_t watermark, int32_t out_location, fg_rows* fired);
+/* Asynchronous fg_advance_progress (ABI 11; the same processWatermark, device output): the
+ * windows the watermark fires are queued on the handle's stream and the call returns without
+ * waiting for them. A shim that forwards the watermark only after the fired rows (Flink emits a
+ * window's rows before the watermark, SlicingWindowOperator.java:207-237 / WindowOperator
+ * onEventTime) takes them with fg_collect_fired, which waits; until then the host is free to
+ * deliver the next watermarks and batches. The fires' completion -- row count, region retries,
+ * overflow check -- is taken by the next call that needs it: a watermark that fires again, any
+ * batch, flush, snapshot or restore. Errors of a fire are reported by that call. The rows of an
+ * async advance stay valid until the next call that fires windows. */
+int  fg_advance_progress_async(fg_handle* h, int64_t watermark);
+/* Waits for the fires of the last fg_advance_progress_async call and returns their rows (device
+ * pointers, as fg_advance_progress with FG_DEVICE); n = 0 when it fired nothing. */
+int  fg_collect_fired(fg_handle* h, fg_rows* fired);
 int  fg_flush(fg_handle* h);
 int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
