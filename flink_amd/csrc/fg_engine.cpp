@@ -303,6 +303,7 @@ struct fg_handle {
     bool async_open = false;      // rows of async advances not yet collected: the next one appends
     int64_t adv_base = 0;         // rows ahead of the current advance's in the output buffers
     int64_t fire_rows_base = 0;   // adv_base of the advance whose rows complete_fire counts
+    bool fail_zeroed = false;     // the fail count was zeroed by flush_lanes' fill (job_add skips its own)
     bool counters_clean = false;   // the device counters hold their initial values
     bool speculate = true;    // FG_SPECULATE=0 turns the speculative pass 2 off (A/B)
     PendingBatch pending;     // deferred first pass of the last batch
@@ -589,7 +590,8 @@ int lanes_for(int bits) {
 
 // A new job set starts after every synchronization: zero its fail count.
 int job_add(fg_handle* h, MergeJob&& j, int* id) {
-    if (h->jobs.empty()) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 16, 0, 8, h->stream));
+    if (h->jobs.empty() && !h->fail_zeroed) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 16, 0, 8, h->stream));
+    h->fail_zeroed = false;
     j.bits = h->region_bits;
     h->jobs.push_back(std::move(j));
     *id = (int)h->jobs.size() - 1;
@@ -1009,8 +1011,16 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     if (int rc0 = complete_fire(h)) return rc0;   // (one fire's rows and scalars at a time)
     std::vector<int> sel = sel_in;   // slice order: windows fired by the flush fire in order
     std::sort(sel.begin(), sel.end(), [&](int a, int b) { return h->lane[a].q < h->lane[b].q; });
-    if (h->out_count_reset) HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
-    else HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+    // flags (and out_count unless this advance already counts rows; and the fail count when no
+    // job is pending) zeroed by one fill: reset_out_count and job_add then need none of their own
+    bool zeroed_out = false;
+    if (h->out_count_reset) {
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
+    } else {
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, h->jobs.empty() ? 24 : 16, h->stream));
+        zeroed_out = true;
+        h->fail_zeroed = h->jobs.empty();
+    }
     std::vector<int64_t> fired_tables, retained;
     bool any_emit = false;
     int rc;
@@ -1051,13 +1061,15 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             }
             continue;
         }
-        SliceTable* t = nullptr;
-        rc = table_get(h, se, true, &t);
-        if (rc) return rc;
         const int64_t trig = trigger_time(h->w, se);
         const bool due = fire && se != JMAX && trig > fire->prev && trig <= fire->wm;
         // local phase: every fired slice lane emits its partial accumulators
         const bool fire_now = fire && (h->local || (h->w.kind == TUMBLE && due));
+        // a slice fired here whose state is not kept needs no table unless one exists (no fill
+        // of an empty table's counts per fire)
+        SliceTable* t = nullptr;
+        rc = table_get(h, se, !(fire_now && !(h->retain && !h->local)), &t);
+        if (rc) return rc;
         // CUMULATE: the step window W = se fires now -- combine the staged slice with the
         // first slice's state, write the state back (unless W is the last window) and emit
         // W in one pass, instead of a flush into the slice table and a fire re-reading it
@@ -1074,7 +1086,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         SliceTable* dstt = t;          // table written by this merge (null: none)
         MergeJob job;
         for (Staged* s : ln.passes) job.batches.push_back(JobBatch{s, l, StagedBatch{}, 0});
-        if (t->upper > 0) job.srcs.push_back(t);
+        if (t && t->upper > 0) job.srcs.push_back(t);
         int64_t cum_first = 0, cum_last = 0;
         if (cum_fire) {
             const int64_t ws = window_start(h->w, se);
@@ -1093,6 +1105,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         for (SliceTable* r : job.srcs) ub_in += r->upper;
         const int64_t ub = std::min<int64_t>(ub_in, kStateCapMax);
         if (fire_now || cum_fire) {
+            if (zeroed_out && !h->out_count_reset && h->adv_base + h->late_rows == 0) h->out_count_reset = true;
             rc = reset_out_count(h);
             if (rc) return rc;
             rc = ensure_out(h, h->out_n + h->pending_out + ub);
@@ -1190,7 +1203,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             if (h->retain && !h->local) {
                 t->upper = ub;
                 retained.push_back(se);
-            } else {
+            } else if (t) {
                 fired_tables.push_back(se);
             }
             any_emit = true;
@@ -3333,14 +3346,33 @@ static int advance_progress(fg_handle* h, int64_t wm) {
     return FG_OK;
 }
 
-// A watermark that can neither flush, fire, re-fire nor free anything (TUMBLE / DataStream
-// tumbling between window ends: no resident tables, the staged slices not yet fired): with a
+// A watermark that can neither flush, fire, re-fire nor free anything (between window ends:
+// no window timer in (timer watermark, wm], the staged slices not yet fired): with a
 // fire pending, fg_advance_progress_async takes only its progress bookkeeping -- the fire's
 // completion is left to the call that needs it, so the host does not wait for the fire here.
+// true when a window end on the slice grid may have its timer in (prev, wm]: exact for zones
+// without rules (trigger_time(e) = e - 1 - tz, increasing in e), assumed otherwise
+static bool trigger_between(const fg_handle* h, int64_t prev, int64_t wm) {
+    const WindowSpec& w = h->w;
+    if (wm <= prev) return false;
+    const int64_t lim = (int64_t)1 << 61;
+    if (w.tz_n > 0 || prev < -lim || prev > lim || wm > lim) return true;
+    const int64_t q = floor_div(prev + 1 + w.tz - h->slice_phase, w.slice);
+    for (int64_t k = q - 1; k <= q + 2; k++) {
+        const int64_t t = trigger_time(w, k * w.slice + h->slice_phase);
+        if (t > prev) return t <= wm;
+    }
+    return true;
+}
+
 static bool quiet_advance(const fg_handle* h, int64_t wm) {
     if (!h->fire_pending || h->pending.active || h->late_rows > 0 || h->local || h->refire_hi != JMIN ||
-        !h->retire_at.empty() || !h->tables.empty() || h->lateness > 0)
+        !h->retire_at.empty() || h->lateness > 0)
         return false;
+    if (!h->tables.empty()) {   // resident slices: no window may come due, and (TUMBLE) none is overdue
+        if (trigger_between(h, h->timer_wm, wm)) return false;
+        if (h->w.kind == TUMBLE && trigger_time(h->w, h->tables.begin()->first) <= h->timer_wm) return false;
+    }
     if (!staged_any(h)) return true;
     const bool fired = is_window_fired(h->w, min_staged_slice_end(h), wm);
     if (h->cfg.mode == FG_MODE_SQL)   // (advance: flush iff progress moves past the next trigger onto a fired slice)
