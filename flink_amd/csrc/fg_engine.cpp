@@ -1920,6 +1920,8 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         KTimer kt(h, K_COUNT, n);
         HIPCHK(h, launch_ingest_count(p, h->stream));
     }
+    // (fg_add_batch: a pending async fire -- before a staged pass is reused below)
+    if (int rc0 = complete_fire(h)) return rc0;
     // per-bucket prefix over workgroups and bucket bases: they depend on the histogram only,
     // so they are queued before the host waits for the counters (no idle GPU across the
     // round trip); a pass that stages nothing goes back to the pool
@@ -2977,8 +2979,12 @@ int fg_add_batch(fg_handle* h, const fg_batch* b) {
     if ((fmt & FG_BATCH_VAL32) && h->cfg.val_type != FG_VAL_I64)
         return h->fail(FG_EINVAL, "FG_BATCH_VAL32 needs a BIGINT value column");
     HIPCHK(h, hipSetDevice(h->device));
-    if (int rc0 = settle_pending(h)) return rc0;
-    maybe_reduce_lanes(h);
+    // A fire queued by fg_advance_progress_async completes once this batch's pass 1 is queued
+    // behind it (ingest_launch): pass 1 touches nothing a region retry of the fire reads.
+    if (!(h->fire_pending && !h->pending.active && !h->windowed && h->lateness == 0)) {
+        if (int rc0 = settle_pending(h)) return rc0;
+        maybe_reduce_lanes(h);
+    }
     int64_t n = b->n;
     const int64_t *key = b->key, *ts = b->rowtime;
     const int64_t* val = h->cfg.val_type != FG_VAL_NONE ? static_cast<const int64_t*>(b->val) : nullptr;
