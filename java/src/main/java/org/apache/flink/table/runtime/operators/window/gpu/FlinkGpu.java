@@ -71,6 +71,18 @@ public final class FlinkGpu {
      */
     public static native long advanceProgress(long h, long watermark, ByteBuffer[] cols);
 
+    /**
+     * fg_advance_progress_async: the watermark's fires are queued and the call returns at once; the
+     * caller holds the watermark until {@link #collectFired} has returned the fired rows.
+     */
+    public static native void advanceProgressAsync(long h, long watermark);
+
+    /**
+     * fg_collect_fired: waits for the fires of every async advance since the last collect; fills
+     * cols as {@link #advanceProgress} (device columns); returns the row count.
+     */
+    public static native long collectFired(long h, ByteBuffer[] cols);
+
     /** fg_flush (prepareSnapshotPreBarrier). */
     public static native void flush(long h);
 

@@ -10,6 +10,8 @@
  *   addRows         fg_add_rows          (packed BinaryRowData of a MemorySegment)
  *   addPartials     fg_add_partials      (GlobalAggCombiner.combine)
  *   advanceProgress fg_advance_progress  (processWatermark -> advanceProgress + fireWindow)
+ *   advanceProgressAsync fg_advance_progress_async (the same, the fires queued: the watermark held)
+ *   collectFired    fg_collect_fired     (the held watermark's rows, then the watermark is forwarded)
  *   flush           fg_flush             (prepareSnapshotPreBarrier)
  *   snapshotState   fg_snapshot_state    (snapshotState: the window-aggs image)
  *   restore         fg_restore           (initializeState)
@@ -188,6 +190,37 @@ JNIEXPORT jlong JNICALL FN(advanceProgress)(JNIEnv* env, jclass cls, jlong hp, j
     const jlong n = r.n, bytes = 8 * n;
     if ((*env)->GetArrayLength(env, cols) < 5 + r.num_aggs) {
         throw_code(env, FG_EINVAL, "advanceProgress: column array too short");
+        return 0;
+    }
+    int i = 0;
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.key, bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_start, bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_end, bytes));
+    for (int a = 0; a < r.num_aggs; a++) (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.agg[a], bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.null_mask, n));
+    (*env)->SetObjectArrayElement(env, cols, i++, r.rowtime ? wrap(env, r.rowtime, bytes) : NULL);
+    return n;
+}
+
+/* void advanceProgressAsync(long h, long watermark): the watermark's fires are queued; the shim
+ * holds the watermark until collectFired has returned the rows of every async advance since the
+ * last collect (rows before the watermark, as processWatermark emits them). */
+JNIEXPORT void JNICALL FN(advanceProgressAsync)(JNIEnv* env, jclass cls, jlong hp, jlong wm) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    check(env, h, fg_advance_progress_async(h, wm));
+}
+
+/* long collectFired(long h, ByteBuffer[] cols): as advanceProgress (device columns: the shim
+ * hands them to a GPU-side consumer, or copies them out) */
+JNIEXPORT jlong JNICALL FN(collectFired)(JNIEnv* env, jclass cls, jlong hp, jobjectArray cols) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_rows r;
+    if (check(env, h, fg_collect_fired(h, &r))) return 0;
+    const jlong n = r.n, bytes = 8 * n;
+    if ((*env)->GetArrayLength(env, cols) < 5 + r.num_aggs) {
+        throw_code(env, FG_EINVAL, "collectFired: column array too short");
         return 0;
     }
     int i = 0;
