@@ -353,8 +353,12 @@ def h2d_leg(args, wl, window, aggs, expected_keys, dev):
                 op.process_batch(nk[lo:hi], nt[lo:hi].numpy().view("uint32"), hv[lo:hi], rowtime_base=bases[bi])
             else:
                 op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi])
+            if bi > 0 and not args.wm_sync:   # the previous batch's held watermarks (as in one_step)
+                op.collect_fired()
             for wm in watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"]):
                 op.process_watermark(wm, device_output=True, wait=args.wm_sync)
+        if not args.wm_sync:
+            op.collect_fired()
         op.process_watermark(JMAX, device_output=True)
         op.synchronize()
         return op.stats()["rows_fired"] - rows0
@@ -564,6 +568,10 @@ def main():
             op_local.reset()
         rows = 0
         xgmi = 0
+        # async watermarks (the default): a batch's watermarks are held until the next batch has
+        # been handed over, then their fired rows are collected (fg_collect_fired) -- the fires
+        # complete while the next batch's pass 1 is queued, so the host never waits on a merge
+        held = False
         # STRING keys: the next micro-batch's key rows are interned while the engine aggregates
         # the current one (the key selector runs as records arrive, ahead of the operator; the
         # dictionary assigns ids in the same first-seen order)
@@ -593,6 +601,9 @@ def main():
                 xgmi += sent
                 torch.cuda.current_stream().synchronize()
             op.process_batch(k, t, v)
+            if held:   # the previous batch's watermarks: their rows, then (a shim) the watermarks go on
+                rows += op.collect_fired().n
+                held = False
             if strings and hi < n:   # overlaps this batch's partition passes
                 k_next = intern(hi)
             if world > 1 and wms:
@@ -600,15 +611,17 @@ def main():
             for wm in wms:
                 if args.wm_sync:
                     rows += op.process_watermark(wm, device_output=True).n
-                else:   # fg_advance_progress_async: fired rows stay in HBM, counted below
+                else:   # fg_advance_progress_async: the fires are queued, the watermarks held
                     op.process_watermark(wm, device_output=True, wait=False)
+                    held = True
         if two_phase:
             nr, sent = partials_round(JMAX)
             return rows + nr, xgmi + sent
+        if held:
+            rows += op.collect_fired().n
         r = op.process_watermark(JMAX, device_output=True)
         rows += r.n
-        if not args.wm_sync:   # (the stats call completes every fire)
-            rows = op.stats()["rows_fired"] - rows0
+        assert args.wm_sync or rows == op.stats()["rows_fired"] - rows0
         return rows, xgmi
 
     def kstats():
