@@ -1,5 +1,5 @@
 """Per-step kernel time and inter-kernel gaps of a rocprofv3 kernel trace of the default bench.
-usage: python scripts/gaps.py run_kernel_trace.csv [step index]"""
+usage: python scripts/gaps.py run_kernel_trace.csv [step index] [pass-1 launches per step (10: 100M batches)]"""
 import collections
 import csv
 import sys
@@ -9,7 +9,8 @@ ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"
             for r in rows)
 p1 = [i for i, k in enumerate(ks) if k[2].endswith("k_part1")]
 step = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-a, b = p1[20 * step], p1[20 * (step + 1)] if len(p1) > 20 * (step + 1) else len(ks)
+per = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+a, b = p1[per * step], p1[per * (step + 1)] if len(p1) > per * (step + 1) else len(ks)
 sel = ks[a:b]
 span = (sel[-1][0] - sel[0][0]) / 1e6
 busy = sum(k[1] - k[0] for k in sel) / 1e6
