@@ -417,6 +417,8 @@ def main():
     ap.add_argument("--wm-sync", action="store_true",
                     help="deliver watermarks with the synchronous fg_advance_progress (A/B; default: "
                          "fg_advance_progress_async, the host does not wait for a window's fire)")
+    ap.add_argument("--intern-serial", action="store_true",
+                    help="strings: intern the next micro-batch after the engine's passes instead of beside them (A/B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-max-records", type=int, default=200_000_000)
@@ -605,6 +607,9 @@ def main():
                 rows += op.collect_fired().n
                 held = False
             if strings and hi < n:   # overlaps this batch's partition passes
+                if args.intern_serial:   # A/B: the lookup after them (the dictionary's stream waits
+                    # on torch's, which here waits on the engine's)
+                    torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(op.stream, device=dev))
                 k_next = intern(hi)
             if world > 1 and wms:
                 wms[-1] = global_watermark(wms[-1], device=dev)
