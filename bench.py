@@ -70,7 +70,7 @@ WORKLOADS = {
                         "10M uniform keys (BASELINE configs[1])"),
     # configs[2]: SQL HOP 5min/1min, rowtime over 30 event-minutes
     "hop": dict(window=("hopping", 300_000, 60_000), keys=10_000_000, rate=1_000_000_000 // 1800, jitter=0, delay=0,
-                zipf=0.0, batch=25_000_000, desc="SQL HOP 5min/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 30 event-minutes, "
+                zipf=0.0, batch=33_333_334, desc="SQL HOP 5min/1min COUNT(*)/SUM/AVG(double), 1B records per GPU over 30 event-minutes, "
                                "10M uniform keys (BASELINE configs[2])"),
     # configs[3]: CUMULATE 1h/1min over 60 event-minutes; 100M keys sharded over 8 GPUs ->
     # the key space is 12.5M per GPU: the per-GPU share at N = 1, the whole 100M space at N = 8
@@ -90,7 +90,7 @@ WORKLOADS = {
     # configs[1] with a STRING grouping key: every record's key is a 32-B BinaryRowData key row
     # ("user" + 8 hex digits) interned by the GPU key dictionary inside the timed region
     "strings": dict(window=("tumbling", 1000), keys=10_000_000, rate=100_000_000, jitter=0, delay=0, zipf=0.0,
-                    desc="SQL TUMBLE 1s COUNT(*)/SUM/AVG(double) GROUP BY a STRING key ('user' + 8 hex digits, "
+                    batch=100_000_000, desc="SQL TUMBLE 1s COUNT(*)/SUM/AVG(double) GROUP BY a STRING key ('user' + 8 hex digits, "
                          "32-B BinaryRowData key rows interned by the GPU key dictionary each micro-batch), "
                          "1B records per GPU, 10M distinct keys (BASELINE configs[1] with a STRING key)"),
     # configs[4]: TUMBLE 1s AVG(double), Zipf s = 1.1 keys, 2 s jitter, bounded out-of-orderness 2 s
