@@ -1076,7 +1076,10 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         // (CumulativeSliceAssigner.mergeSlices :359-370 + SliceSharedWindowAggProcessor.fireWindow)
         // (only when every earlier step window of this cumulative window fired in an earlier
         // advance, so that no earlier window still has to fire from the unextended state)
-        bool cum_fire = !h->local && h->w.kind == CUMULATE && due;
+        // (not while a restore re-fire is pending: the re-fire folds the new state of this
+        // cumulative window's earlier slices into its first slice first -- advance_progress runs
+        // it after this flush -- and fire_windows then fires W from the complete state)
+        bool cum_fire = !h->local && h->w.kind == CUMULATE && due && h->refire_hi == JMIN;
         if (cum_fire) {
             const int64_t ws0 = window_start(h->w, se);
             const int64_t prev_w = jsub(se, h->w.slice);

@@ -25,14 +25,15 @@ def _cfg(kind, mode="sql", vt="f64"):
 
 
 def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0, delay=0, collect_every=1,
-         regions_small=False):
+         regions_small=False, ckpt_every=0, zipf=0.0, sync=False):
     from tests.gpu_adapter import GpuOperator
-    key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter)
+    key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, zipf=zipf)
     g = GpuOperator(cfg, expected_keys=1000 if regions_small else keys, buffer_records=4 * batch)
     o = oracle_mk(O, cfg)
     op = g.op
     exp = []
     fired_total = 0
+    o_base = 0
     mx = np.iinfo(np.int64).min
     nb = 0
     for lo in range(0, n, batch):
@@ -43,24 +44,42 @@ def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0
         for c in np.linspace(lo, hi, wms_per_batch + 1)[1:].astype(np.int64):
             mx = max(mx, int(ts[lo:c].max()))
             wm = mx - delay - 1
-            assert op.process_watermark(wm, device_output=True, wait=False) is None
+            if sync:   # (the synchronous advance, host rows: the A/B reference of these tests)
+                g.process_watermark(wm)
+            else:
+                assert op.process_watermark(wm, device_output=True, wait=False) is None
             o.process_watermark(wm)
             exp.append(o.take_rows())
         nb += 1
-        if nb % collect_every == 0:
-            r = op.collect_fired()
-            got = op.rows_to_host(r)
-            g._rows = [got]
-            assert_rows_equal(g.take_rows(), np.concatenate(exp), cfg["val_type"], f"batch {nb}")
+        ckpt = ckpt_every and nb % ckpt_every == 0
+        if ckpt:   # checkpoint while the watermarks' fires are pending and their rows uncollected
+            g.prepare_snapshot()
+            o.prepare_snapshot()
+        if nb % collect_every == 0 or ckpt:
+            if not sync:
+                g._rows = [op.rows_to_host(op.collect_fired())]
+            got = g.take_rows()
+            assert_rows_equal(got, np.concatenate(exp), cfg["val_type"], f"batch {nb}")
             fired_total += len(got)
             exp = []
-            assert op.num_late_records_dropped == o.late_dropped
-    op.process_watermark(JMAX, device_output=True, wait=False)
+            assert g.late_dropped == o_base + o.late_dropped
+        if ckpt:   # restore both from their images and go on
+            assert op.stats()["rows_fired"] == fired_total
+            g2, o2 = g.restore_copy(), o.restore_copy()
+            o_base += o.late_dropped
+            g.close()
+            o.close()
+            g, o, op = g2, o2, g2.op
+            fired_total = 0
+    if sync:
+        g.process_watermark(JMAX)
+    else:
+        op.process_watermark(JMAX, device_output=True, wait=False)
+        g._rows.append(op.rows_to_host(op.collect_fired()))
     o.process_watermark(JMAX)
     exp.append(o.take_rows())
-    got = op.rows_to_host(op.collect_fired())
-    g._rows = [got]
-    assert_rows_equal(g.take_rows(), np.concatenate(exp), cfg["val_type"], "final")
+    got = g.take_rows()
+    assert_rows_equal(got, np.concatenate(exp), cfg["val_type"], "final")
     fired_total += len(got)
     assert op.stats()["rows_fired"] == fired_total
     # a collect with nothing fired since the last one
@@ -73,6 +92,24 @@ def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0
 @pytest.mark.parametrize("collect_every", [1, 2])
 def test_async_watermarks_match_oracle(oracle_mod, kind, collect_every):
     _run(oracle_mod, _cfg(kind), collect_every=collect_every)
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+@pytest.mark.parametrize("sync", [False, True], ids=["async", "sync"])
+def test_async_watermarks_checkpoint_restore(oracle_mod, kind, sync):
+    """prepareSnapshotPreBarrier + snapshotState with fires pending and rows uncollected, then
+    initializeState of a new operator from the image; out of order, late data. (Also with the
+    synchronous advance: CUMULATE once lost the rows of a key whose post-restore record landed in
+    a slice fired before the checkpoint, when the first watermark after the restore passed the
+    re-fire horizon and fired the next step window -- the fused flush+fire ran before the re-fire
+    had folded that record into the cumulative window's first slice.)"""
+    _run(oracle_mod, _cfg(kind), jitter=1500, delay=300, ckpt_every=4, collect_every=2, sync=sync)
+
+
+def test_async_watermarks_zipf(oracle_mod):
+    """Hot keys (Zipf 1.1): the heavy-region pass behind deferred fires."""
+    _run(oracle_mod, _cfg("tumble"), n=2_000_000, keys=200_000, batch=400_000, zipf=1.1, jitter=800, delay=500,
+         collect_every=2)
 
 
 @pytest.mark.parametrize("kind", ["tumble", "hop"])
