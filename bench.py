@@ -218,7 +218,11 @@ def cpu_baseline(args, rate):
     group, on a bounded prefix of the same stream."""
     from oracle import oracle as O
     O.build()
-    cores = min(85, host_cores()) if args.cpu_threads is None else args.cpu_threads
+    quota = cpu_quota()
+    # P = the CPUs this process may use: its affinity mask, capped by the cgroup's CPU quota (a
+    # box grants a 16-CPU share of a larger machine), and by 85 (maxParallelism 128)
+    avail = host_cores() if quota is None else max(1, min(host_cores(), int(quota)))
+    cores = min(85, avail) if args.cpu_threads is None else args.cpu_threads
 
     def gen(n):
         i = np.arange(n, dtype=np.uint64)
@@ -251,32 +255,26 @@ def cpu_baseline(args, rate):
     n = int(min(args.cpu_max_records, max(4_000_000, rate_est * args.cpu_seconds)))
     n -= n % args.wm_every
     el, rows = run(n)
-    quota = cpu_quota()
     return dict(value=n / el, unit="records/s", cores=cores, kind="port", cpu_quota=quota,
+                cores_note="P = min(affinity CPUs, cgroup CPU quota, 85) threads, one operator instance each",
                 sample=f"first {n:,} records of the configs[1] stream (10M-key space), watermark every "
                        f"{args.wm_every:,} records + final Long.MAX_VALUE; C restatement of "
                        f"SlicingWindowOperator/RecordsWindowBuffer/AggCombiner, {cores} instances routed by "
                        f"key group (maxParallelism 128); {el:.1f} s, {rows:,} rows fired" +
-                       (f"; the cgroup grants {quota:g} CPUs of time to the {cores} threads" if quota else ""))
-
-
-def lib_sha256():
-    import hashlib
-    h = hashlib.sha256()
-    with open(os.path.join(ROOT, "flink_amd", "libflinkgpu.so"), "rb") as f:
-        for chunk in iter(lambda: f.read(1 << 20), b""):
-            h.update(chunk)
-    return h.hexdigest()
+                       (f"; the cgroup grants {quota:g} CPUs of time" if quota else ""))
 
 
 def pmc_traffic(kernel_class):
     """HBM bytes per launch of `kernel_class` from the newest committed rocprofv3 PMC summary
     (profiles/**/pmc_traffic.json, profiles/pmc_summary.py) -- only if it was counted on THIS
-    library build (same sha256 of libflinkgpu.so); otherwise None. Returns (bytes, source)."""
+    build's kernels (same sha256 of libflinkgpu.so's device code objects, flink_amd.buildinfo: a
+    host-only change keeps the kernels' traffic); otherwise None. Returns (bytes, source)."""
     import glob
+
+    from flink_amd import buildinfo
     try:
-        sha = lib_sha256()
-    except OSError:
+        ksha = buildinfo.kernels_sha256()
+    except (OSError, ValueError, KeyError):
         return None, None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_traffic.json"), recursive=True),
                        reverse=True):
@@ -284,12 +282,12 @@ def pmc_traffic(kernel_class):
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("_provenance", {}).get("lib_sha256") != sha:
+        if d.get("_provenance", {}).get("kernels_sha256") != ksha:
             continue
         v = d.get(kernel_class.replace("local_", ""), {}).get("hbm_bytes_per_launch")
         if v is not None:
-            return v, os.path.relpath(path, ROOT) + f" (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, lib {sha[:12]})"
-    return None, f"no PMC summary of this build (lib {sha[:12]}) under profiles/"
+            return v, os.path.relpath(path, ROOT) + f" (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, kernels {ksha[:12]})"
+    return None, f"no PMC summary of this build's kernels ({ksha[:12]}) under profiles/"
 
 
 def h2d_link_peak(dev, nbytes=1 << 30, reps=4):
@@ -722,8 +720,10 @@ def main():
                 (" + RCCL all-to-all of partial accumulators (two-phase)" if two_phase else
                  " + RCCL all-to-all of records") if world > 1 else ""),
         },
+        # the dominant kernel (task contract): algorithmic bytes per launch / its HIP-event duration
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "frac": achieved / HBM_PEAK_GBS, "kernel_frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": dom_name,
                      "avg_launch_ms": avg_s * 1e3,
                      "alg_bytes_per_launch": alg_bytes,
@@ -731,6 +731,10 @@ def main():
                      "copy_peak_gbs": copy_gbs,
                      "frac_of_copy_peak": achieved / copy_gbs if copy_gbs else None,
                      "actual_gbs": traffic / avg_s / 1e9 if traffic else None},
+        # the whole job: B_alg = 24 B per record + 48 B per
+        # fired row over the wall time of the timed steps, against N x 8 TB/s -- the north-star figure
+        "job_roofline": {"achieved": b_alg / el / 1e9, "peak": world * HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": b_alg / el / (world * HBM_PEAK_GBS * 1e9), "b_alg_bytes": b_alg},
         "job_roofline_frac": b_alg / el / (world * HBM_PEAK_GBS * 1e9),
         "rows_fired": tot_rows,
         "late_dropped": late,

@@ -1,6 +1,6 @@
 """ctypes binding of libflinkgpu.so (the C-ABI declared in include/flinkgpu.h).
 
-The library is built in-tree (``flink_amd/libflinkgpu.so``, see flink_amd/build.py).
+The library is built in-tree (``flink_amd/libflinkgpu.so``, flink_amd/Makefile via __graft_entry__.build()).
 There is no fallback: if the library is missing or cannot be loaded, importing the
 engine raises -- the product path never runs on a CPU substitute.
 """
@@ -96,7 +96,7 @@ BATCH_KEY32, BATCH_ROWTIME32, BATCH_VAL32 = 1, 2, 4   # fg_batch.format
 # every symbol include/flinkgpu.h declares
 EXPORTS = (
     "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_advance_progress_async",
-    "fg_collect_fired", "fg_flush", "fg_snapshot_state", "fg_restore",
+    "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_snapshot_state", "fg_restore",
     "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
@@ -142,6 +142,7 @@ def load():
     L.fg_advance_progress.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(FgRows)]
     L.fg_advance_progress_async.argtypes = [P, C.c_int64]
     L.fg_collect_fired.argtypes = [P, C.POINTER(FgRows)]
+    L.fg_collect_fired_to.argtypes = [P, C.c_int32, C.POINTER(FgRows)]
     L.fg_flush.argtypes = [P]
     L.fg_snapshot_state.argtypes = [P, C.POINTER(FgStateRows), C.POINTER(C.c_int64)]
     L.fg_restore.argtypes = [P, C.POINTER(FgStateRows), C.c_int64]
@@ -190,8 +191,8 @@ def load():
                "fg_key_dict_copy_arena"):
         getattr(L, fn).restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress",
-               "fg_advance_progress_async", "fg_collect_fired", "fg_flush", "fg_snapshot_state", "fg_restore",
-               "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
+               "fg_advance_progress_async", "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_snapshot_state",
+               "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int
     _lib = L

@@ -2617,6 +2617,9 @@ int late_split(fg_handle* h, int64_t n, const int64_t** key, const int64_t** ts,
     const int64_t nr = (int64_t)h->lt_h.as<unsigned long long>()[1];
     *n_regular = n;
     if (nl == 0) return FG_OK;   // nothing late: the batch as it is
+    // late elements go into the resident slice tables without pass 1's 32-bit key check: the
+    // narrow LDS table (keyed by the int32 of an entry's mix) is off from here on
+    h->keys32 = false;
     if (!*vnull) {   // (the late list's NULL flags are all 0)
         HIPCHK(h, hipMemsetAsync(h->lt_null.p, 0, (size_t)nl, h->stream));
     }
@@ -2694,7 +2697,10 @@ int fg_host_unregister(int32_t device_id, void* p) {
     return FG_OK;
 }
 
-// FG_BACKTRACE=1 (diagnostics): a host fault prints the native frames to stderr
+// FG_BACKTRACE=1 (diagnostics, standalone or Python hosts only): a host fault prints the native
+// frames to stderr. Installed only while SIGSEGV has its default disposition -- a JVM (the JNI
+// shim) handles SIGSEGV itself for implicit null checks and safepoint polls, and its handler is
+// never replaced.
 static void fg_fault_trace(int sig) {
     void* b[64];
     const int n = backtrace(b, 64);
@@ -2705,15 +2711,19 @@ static void fg_fault_trace(int sig) {
 
 int fg_open(const fg_config* cfg, fg_handle** out) {
     if (getenv("FG_BACKTRACE")) {   // (on its own stack: a stack overflow is traced too)
-        static char alt[1 << 16];
-        stack_t ss{};
-        ss.ss_sp = alt;
-        ss.ss_size = sizeof alt;
-        sigaltstack(&ss, nullptr);
-        struct sigaction sa{};
-        sa.sa_handler = fg_fault_trace;
-        sa.sa_flags = SA_ONSTACK;
-        sigaction(SIGSEGV, &sa, nullptr);
+        struct sigaction old{};
+        sigaction(SIGSEGV, nullptr, &old);
+        if (!(old.sa_flags & SA_SIGINFO) && old.sa_handler == SIG_DFL) {
+            static char alt[1 << 16];
+            stack_t ss{};
+            ss.ss_sp = alt;
+            ss.ss_size = sizeof alt;
+            sigaltstack(&ss, nullptr);
+            struct sigaction sa{};
+            sa.sa_handler = fg_fault_trace;
+            sa.sa_flags = SA_ONSTACK;
+            sigaction(SIGSEGV, &sa, nullptr);
+        }
     }
     *out = nullptr;
     if (!cfg) {
@@ -3277,7 +3287,9 @@ int fg_flush(fg_handle* h) {
 // processWatermark without the output: flushes, re-fires, fires, cleanup timers
 static int advance_progress(fg_handle* h, int64_t wm) {
     if (int rc0 = settle_pending(h)) return rc0;
-    h->adv_base = h->async_advance && h->async_open ? h->out_n : 0;
+    // rows of async advances not collected yet lead this advance's rows (an async advance appends
+    // to them; a synchronous one returns them ahead of its own)
+    h->adv_base = h->async_open ? h->out_n : 0;
     h->out_n = h->adv_base + h->late_rows;   // rows fired by late elements since the last advance come first
     h->pending_out = 0;
     h->out_count_reset = false;
@@ -3438,23 +3450,32 @@ static void device_rows(fg_handle* h, int32_t out_location, fg_rows* fired) {
     for (int a = 0; a < h->cfg.num_aggs; a++) fired->agg[a] = h->o_agg[a].as<int64_t>();
 }
 
-int fg_collect_fired(fg_handle* h, fg_rows* fired) {
-    if (!h || !fired) return FG_EINVAL;
+int fg_collect_fired_to(fg_handle* h, int32_t out_location, fg_rows* fired) {
+    if (!h || !fired || (out_location != FG_HOST && out_location != FG_DEVICE)) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
     if (int rc = complete_fire(h)) return rc;
-    device_rows(h, FG_DEVICE, fired);
-    if (!h->async_open) fired->n = 0;   // (every async advance since the last collect fired nothing)
+    if (!h->async_open) h->out_n = 0;   // (every async advance since the last collect fired nothing)
     h->async_open = false;
+    if (out_location == FG_HOST) {
+        std::memset(fired, 0, sizeof *fired);
+        fired->n = h->out_n;
+        fired->num_aggs = h->cfg.num_aggs;
+        fired->location = FG_HOST;
+        return copy_out_to_host(h, fired);
+    }
+    device_rows(h, FG_DEVICE, fired);
     return FG_OK;
 }
+
+int fg_collect_fired(fg_handle* h, fg_rows* fired) { return fg_collect_fired_to(h, FG_DEVICE, fired); }
 
 int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows* fired) {
     if (!h) return FG_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
-    h->async_open = false;   // (rows of async advances not collected by now are dropped)
-    int rc = advance_progress(h, wm);
+    int rc = advance_progress(h, wm);   // (uncollected async rows lead its rows: adv_base)
     if (rc) return rc;
-    h->rows_fired += h->out_n;
+    h->rows_fired += h->out_n - h->adv_base;   // (the async rows were counted by their advances)
+    h->async_open = false;
     if (fired) {
         std::memset(fired, 0, sizeof *fired);
         fired->n = h->out_n;

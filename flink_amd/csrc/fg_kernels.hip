@@ -27,35 +27,19 @@ namespace fg {
 
 thread_local LaunchEvents g_launch_ev;
 
-#ifndef FG_DIAG_PART2
-#define FG_DIAG_PART2 0    // diagnostic builds only (wrong results): bit0 no writes, bit1 no loads, bit2 no map
-#endif
-
 typedef long long RecV2 __attribute__((ext_vector_type(2)));
 typedef const RecV2 __attribute__((address_space(1)))* GlobalRec;
 
-// Non-temporal (streaming) forms of the record streams, by FG_NT bit (experiment knob):
-// 1 pass-1 input loads, 2 pass-1 tile stores, 4 pass-2 tile loads, 8 pass-2 staged stores,
-// 16 merge staged loads
-#ifndef FG_NT
-#define FG_NT 0
-#endif
-template <int BIT>
+// 16-B record loads / stores (non-temporal forms measured within +-2 % or slower)
 __device__ __forceinline__ longlong2 ld2(const void* q) {
-    const RecV2* r = static_cast<const RecV2*>(q);
-    RecV2 v;
-    if constexpr ((FG_NT & BIT) != 0) v = __builtin_nontemporal_load(r);
-    else v = *r;
+    const RecV2 v = *static_cast<const RecV2*>(q);
     return make_longlong2(v.x, v.y);
 }
-template <int BIT>
 __device__ __forceinline__ void st2(void* q, longlong2 a) {
     RecV2 v;
     v.x = a.x;
     v.y = a.y;
-    RecV2* r = static_cast<RecV2*>(q);
-    if constexpr ((FG_NT & BIT) != 0) __builtin_nontemporal_store(v, r);
-    else *r = v;
+    *static_cast<RecV2*>(q) = v;
 }
 // a pointer that was itself loaded from memory is generic (flat) to the compiler: view it in
 // the global address space so its loads are global_load (see `load` below)
@@ -554,9 +538,9 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
 #pragma unroll
             for (int u = 0; u < R / 2; u++) {
                 const int64_t i = t0 + li_of(2 * u);
-                k2[u] = ld2<1>(p.key + i);
-                t2[u] = ld2<1>(p.ts + i);
-                v2[u] = has_val ? ld2<1>(p.val + i) : make_longlong2(0, 0);
+                k2[u] = ld2(p.key + i);
+                t2[u] = ld2(p.ts + i);
+                v2[u] = has_val ? ld2(p.val + i) : make_longlong2(0, 0);
             }
         } else {
 #pragma unroll
@@ -645,7 +629,7 @@ __global__ __launch_bounds__(kPart1Threads) void k_part1(IngestParams p) {
             }
         } else {
             for (uint32_t i = tid; i < tile_total; i += T) {
-                st2<2>(&p.tmp[t0 + i], s_rec[i]);
+                st2(&p.tmp[t0 + i], s_rec[i]);
                 if (has_null) p.tmp_null[t0 + i] = s_nul[i];
             }
         }
@@ -845,15 +829,11 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             const bool ok = idx < total;
             const int q = ok ? (int)s_map[idx - base] : 0;
             const uint32_t src = ok ? s_fsrc[q] + (idx - s_fstart[q]) : 0u;
-            if (FG_DIAG_PART2 & 2) {
-                rr[u] = make_longlong2((long long)src * 0x9E3779B97F4A7C15ll, src);
-                continue;
-            }
             if constexpr (NARROW) {   // {int32 key, value}: the key sign-extended, its mix recomputed below
                 const Rec12 r = ld_rec12(p.tmp, src);
                 rr[u] = make_longlong2((long long)(int32_t)r.k, (long long)rec12_val(r));
             } else {
-                rr[u] = ld2<4>(&p.tmp[src]);
+                rr[u] = ld2(&p.tmp[src]);
             }
             if (has_null && p.tmp_null[src] != 0) rn |= 1u << u;
         }
@@ -861,7 +841,7 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
     // sub-tile at `base` (records in cr, NULL bits cn); loads the next one into nr/nn
     // first; cr is reused for the write-out once its records are staged in LDS
     auto step = [&](longlong2 (&cr)[R], const uint32_t cn, longlong2 (&nr)[R], uint32_t& nn, uint32_t base) {
-        if (base + kPart2Tile < total && !(FG_DIAG_PART2 & 4)) build_map(base + kPart2Tile);
+        if (base + kPart2Tile < total) build_map(base + kPart2Tile);
         load(nr, nn, base + kPart2Tile);
         uint32_t rf[R];   // (rank << 6) | fine, 0xffffffff = none
 #pragma unroll
@@ -909,14 +889,10 @@ __global__ __launch_bounds__(kPart2Threads) void k_part2(IngestParams p, int32_t
             const uint32_t i = (uint32_t)(u * kPart2Threads + tid);
             const int f = (int)(wfb[u] & (NF - 1));
             const int64_t pos = live ? (int64_t)(s_cur[f] + (i - s_off[f])) : 0;
-            if (FG_DIAG_PART2 & 1) {
-                if (wv[u].x == 0x5555 && wv[u].y == 0x7777) p.st_rec[0] = pos;   // keep the reads alive
-                continue;
-            }
             if constexpr (NARROW) {   // 12-B record {int32 key, value}
                 st_rec12(live ? (void*)p.st_rec : (void*)p.sink, live ? (uint64_t)pos : 0u, wv[u].x, wv[u].y);
             } else if constexpr (AOS) {
-                st2<8>(live ? p.st_rec + 2 * pos : p.sink, wv[u]);
+                st2(live ? p.st_rec + 2 * pos : p.sink, wv[u]);
             } else {
                 *(live ? p.st_rec + pos : p.sink) = wv[u].x;
             }
@@ -1380,15 +1356,9 @@ hipError_t launch_ingest_scatter(const IngestParams& p, hipStream_t s) {
 // plain staged records (no NULLs, no resident state, < 2^32 records).
 //
 // staged-stream chunk of the compact merge: 16-B loads per thread (overridable for experiments)
-#ifndef FG_MERGE_U
-#define FG_MERGE_U 2
-#endif
-#ifndef FG_WIDE_U
-#define FG_WIDE_U 2        // the wide merge's staged records per thread per chunk
-#endif
-#ifndef FG_DIAG_MERGE
-#define FG_DIAG_MERGE 0    // diagnostic builds only (wrong results): bit0 no adds, bit1 no probe loop, bit2 no emit
-#endif
+// staged records per thread per chunk (compact and wide merges; 1, 3 and 4 measured slower,
+// DESIGN.md section 9 v10)
+constexpr int kMergeRecsPerThread = 2;
 
 template <bool C, bool MV = false>
 struct MergeCfg;
@@ -1396,28 +1366,28 @@ template <>
 struct MergeCfg<false, false> {
     static constexpr int kSlotsT = kSlots;
     static constexpr int kThreads = kMergeThreads;
-    static constexpr int kU = FG_WIDE_U;   // 1,024 threads: 128 VGPRs
+    static constexpr int kU = kMergeRecsPerThread;   // 1,024 threads: 128 VGPRs
     static constexpr int kWavesPerEu = 4;
 };
 template <>
 struct MergeCfg<true, false> {
     static constexpr int kSlotsT = kCompactSlots;
     static constexpr int kThreads = kCompactMergeThreads;
-    static constexpr int kU = FG_MERGE_U;
+    static constexpr int kU = kMergeRecsPerThread;
     static constexpr int kWavesPerEu = kCompactMergeThreads / 128;   // two workgroups per CU
 };
 template <>
 struct MergeCfg<false, true> {   // multi-value: one 1,024-thread workgroup per CU
     static constexpr int kSlotsT = kSlotsMV;
     static constexpr int kThreads = kMergeThreads;
-    static constexpr int kU = FG_WIDE_U;
+    static constexpr int kU = kMergeRecsPerThread;
     static constexpr int kWavesPerEu = 4;
 };
 template <>
 struct MergeCfg<true, true> {    // multi-value compact: 108 KiB, one 1,024-thread workgroup per CU
     static constexpr int kSlotsT = kCompactSlotsMV;
     static constexpr int kThreads = kMergeThreads;
-    static constexpr int kU = FG_MERGE_U;
+    static constexpr int kU = kMergeRecsPerThread;
     static constexpr int kWavesPerEu = 4;
 };
 
@@ -1459,9 +1429,6 @@ struct LdsTableN {
     unsigned long long v[1][kCompactSlots + 1];
     uint32_t cs[kCompactSlots + 1];
 };
-#ifndef FG_NARROW_TABLE
-#define FG_NARROW_TABLE 1
-#endif
 constexpr int32_t kEmpty32 = INT32_MIN;
 // linear probe of the narrow table from `slot` (as lds_find_or_insert_from)
 __device__ __forceinline__ int lds_find_or_insert_from32(LdsTableN& t, int32_t k, uint32_t slot, bool& full) {
@@ -1507,21 +1474,9 @@ __device__ __forceinline__ int nt_bucket_slot(LdsTableN& t, int32_t k, uint32_t 
 // linear, slot by slot, from the bucket's first slot. At the regions' load factor (<= ~0.35)
 // a key sits in its home bucket ~99 % of the time, against ~84 % for a single home slot, so
 // a wave's lanes rarely leave the fast path.
-#ifndef FG_WAVE_PRE
-#define FG_WAVE_PRE 1
-#endif
-#ifndef FG_SWZ
-#define FG_SWZ 0
-#endif
-#ifndef FG_BUCKET
-#define FG_BUCKET 4
-#endif
-constexpr int kBucket = FG_BUCKET;   // 4 (two 16-B reads) or 2 (one): slots per home bucket
-#if FG_BUCKET == 4
-#define FG_BUCKET_KEYS(b01, b23) {(b01).x, (b01).y, (b23).x, (b23).y}
-#else
-#define FG_BUCKET_KEYS(b01, b23) {(b01).x, (b01).y}
-#endif
+// (2-slot buckets, one 16-B read, measured slower: more probes leave the home bucket; odd buckets
+// read half-swapped to spread banks measured slower too -- DESIGN.md section 9)
+constexpr int kBucket = 4;   // slots per home bucket (two 16-B reads of 64-bit keys)
 template <bool C, bool MV>
 __device__ __forceinline__ uint32_t lds_home(int64_t h) {
     constexpr uint32_t NB = (uint32_t)(MergeCfg<C, MV>::kSlotsT / kBucket);
@@ -1560,7 +1515,7 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C, MV>& t, int64_t k, u
                                                bool& full) {
     constexpr uint32_t S_ = (uint32_t)MergeCfg<C, MV>::kSlotsT;
     if (k == JMIN) return (int)S_;
-    const int64_t q[kBucket] = FG_BUCKET_KEYS(b01, b23);
+    const int64_t q[kBucket] = {b01.x, b01.y, b23.x, b23.y};
     int hit = -1, empty = -1;
 #pragma unroll
     for (int j = kBucket - 1; j >= 0; j--) {
@@ -1619,13 +1574,7 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
     p.out_null[o] = nm;
 }
 
-#ifndef FG_DENSE_EMIT
-#define FG_DENSE_EMIT 1
-#endif
-#ifndef FG_SRC_U
-#define FG_SRC_U 2
-#endif
-constexpr int kSrcU = FG_SRC_U;   // source-table entries per thread per round (wide merge)
+constexpr int kSrcU = 2;   // source-table entries per thread per round (1, 3, 4 measured +-2 % or slower)
 constexpr unsigned long long kMarkBit = 1ull << 63;   // wide table: entry touched by a marking source (NULL-count word)
 constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
 
@@ -1768,13 +1717,11 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     constexpr uint32_t kChunk = kMergeU * T;
     // narrow table: the compact single-value merge over 12-B records keys its LDS table by the
     // 32-bit key (records then travel as {key, value}; the mix is recomputed for the home bucket)
-    constexpr bool NT = N12 && C && !MV && FG_NARROW_TABLE;
+    constexpr bool NT = N12 && C && !MV;
     using Tab = std::conditional_t<NT, LdsTableN, LdsTableT<C, MV>>;
     __shared__ Tab t;
     __shared__ uint32_t s_grp[kRounds * kWaves];   // per (round, wave) row counts -> offsets
-#if FG_DENSE_EMIT
     __shared__ uint16_t s_map[S + 1];              // rank -> slot of the region's emitted entries
-#endif
     __shared__ unsigned int s_flags;
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
@@ -1861,9 +1808,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             const uint32_t i = m.i0 + u * T + tid;
-            RecV2 v;
-            if constexpr ((FG_NT & 16) != 0) v = __builtin_nontemporal_load(&rec[i < m.end ? i : m.end - 1]);
-            else v = rec[i < m.end ? i : m.end - 1];
+            const RecV2 v = rec[i < m.end ? i : m.end - 1];
             c[u] = make_longlong2(v.x, v.y);
         }
         }
@@ -1883,18 +1828,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             } else {
             home[u] = lds_home<C, MV>(c[u].x);
             const RecV2* kb = reinterpret_cast<const RecV2*>(&t.key[home[u]]);
-#if FG_SWZ
-            // odd buckets read their second half first: the first read of every lane then
-            // spans all 16 four-bank groups instead of the even ones only (32-B buckets)
-            const uint32_t sw = kBucket == 4 ? (home[u] >> 2) & 1u : 0u;
-            const RecV2 x0 = kb[sw];
-            const RecV2 x1 = kBucket == 4 ? kb[sw ^ 1u] : x0;
-            b01[u] = sw ? x1 : x0;
-            b23[u] = sw ? x0 : x1;
-#else
             b01[u] = kb[0];
-            b23[u] = kBucket == 4 ? kb[1] : b01[u];
-#endif
+            b23[u] = kb[1];
             }
         }
         // Hot keys (Zipf regions below the heavy threshold: one key can fill most of a wave):
@@ -1909,7 +1844,6 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             pcnt[u] = valid ? 1u : 0u;
 #pragma unroll
             for (int q = 0; q < NVS; q++) pval[u][q] = C ? c[u].y : 0;
-#if FG_WAVE_PRE
             if (C && p.hot_keys) {   // (compact merges only, and only over skewed staging: a
                                      // uniform stream has no equal keys in a wave to combine)
             const int64_t k0 = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)c[u].x) |
@@ -1928,20 +1862,16 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 if (in) pcnt[u] = lane == __ffsll((long long)msk) - 1 ? (uint32_t)__popcll(msk) : 0u;
             }
             }
-#endif
         }
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             if (pcnt[u] == 0) continue;
             if constexpr (NT) {   // exact 32-bit keys, one bucket read
                 const int slot = nt_bucket_slot(t, (int32_t)c[u].x, home[u], bq[u], full);
-                if (slot >= 0) {
-                    if constexpr (FG_WAVE_PRE) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
-                    else lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
-                }
+                if (slot >= 0) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
             } else {
             const int64_t k = c[u].x;
-            const int64_t q[kBucket] = FG_BUCKET_KEYS(b01[u], b23[u]);
+            const int64_t q[kBucket] = {b01[u].x, b01[u].y, b23[u].x, b23[u].y};
             int hit = -1, empty = -1;
 #pragma unroll
             for (int j = kBucket - 1; j >= 0; j--) {   // the first match / first empty slot
@@ -1950,10 +1880,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             }
             constexpr uint32_t S_ = (uint32_t)MergeCfg<C, MV>::kSlotsT;
             int slot;
-            if (FG_DIAG_MERGE & 2) {
-                slot = (int)home[u] + (hit >= 0 ? hit : 0);
-                if (q[0] == JMIN) t.key[slot] = k;
-            } else if (k == JMIN) {
+            if (k == JMIN) {
                 slot = (int)S_;
             } else if (hit >= 0 && (empty < 0 || hit < empty)) {
                 slot = (int)home[u] + hit;
@@ -1974,11 +1901,10 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
 #pragma unroll
                     for (int k = 0; k < NVS; k++) lds_val(&t.v[k][slot], C ? pval[u][k] : c[u].y, vops[k], true);
                 }
-            } else if (!(FG_DIAG_MERGE & 1) && slot >= 0) {
-                if constexpr (C && FG_WAVE_PRE) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
+            } else if (slot >= 0) {
+                if constexpr (C) lds_add<C, MV>(t, slot, (unsigned long long)pcnt[u], 0ull, pval[u], vt, p);
                 else lds_add1<C, MV>(t, slot, 1ull, 0ull, c[u].y, vt, p);
             }
-            if ((FG_DIAG_MERGE & 1) && slot >= 0) t.cs[slot] = 1;
             }
         }
     };
@@ -2354,7 +2280,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         MSTAMP(2);   // compaction + scan + barriers
         const unsigned int fl = s_flags;
         const bool write_dst = !skip && p.has_dst && !(fl & 5u);
-        const bool write_out = !(FG_DIAG_MERGE & 4) && p.emit && !(fl & 7u);
+        const bool write_out = p.emit && !(fl & 7u);
         int64_t* dbase = p.has_dst ? p.dst.base + (int64_t)r * cols * cap : nullptr;
         const unsigned long long obase = s_out_base;
         // one entry out: its table write-back and / or its fired row, at rank `at`
@@ -2378,7 +2304,6 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             if (write_out) write_row(p, obase + at, key, cs, cn, vv, vt);
         };
         // per round: the wave's occupied lanes below this lane give the rank within the group
-#if FG_DENSE_EMIT
         // the ranks are gathered into a rank -> slot map first, then every lane writes one
         // entry at consecutive ranks (full-width stores instead of the ~1/3 of a wave that a
         // round's occupied lanes fill)
@@ -2395,16 +2320,6 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             const uint32_t total = s_total;
             for (uint32_t i = tid; i < total; i += T) emit_one(s_map[i], i);
         }
-#else
-#pragma unroll
-        for (int k = 0; k < kRounds; k++) {
-            const bool occ = (occ_mask >> k) & 1;
-            const uint64_t bal = __ballot(occ);
-            if (!occ) continue;
-            const int slot = k < kRounds - 1 ? k * T + tid : S;
-            emit_one(slot, s_grp[k * kWaves + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1)));
-        }
-#endif
         if (tid == 0 && write_dst) {
             const uint32_t total = s_total;
             const uint32_t old = p.dst.counts[r];

@@ -358,9 +358,15 @@ class WindowAggOperator:
         self._hold(None)
         return self._host_rows(r)
 
-    def collect_fired(self):
-        """The rows of the last process_watermark(..., wait=False) (fg_collect_fired: waits for
-        its fires): the operator's FgRows, device pointers valid until the next call that fires."""
+    def collect_fired(self, host: bool = False):
+        """The rows of the process_watermark(..., wait=False) calls since the last collect
+        (fg_collect_fired: waits for their fires): the operator's FgRows, device pointers valid
+        until the next call that fires; host=True: a structured numpy array copied out by the
+        library (fg_collect_fired_to FG_HOST, what a JVM shim takes)."""
+        if host:
+            r = L.FgRows()
+            L.check(self._lib.fg_collect_fired_to(self._h, L.HOST, C.byref(r)), self._h)
+            return self._host_rows(r)
         L.check(self._lib.fg_collect_fired(self._h, self._dev_rows_ref), self._h)
         return self._dev_rows
 

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 11
+#define FG_ABI_VERSION 12
 
 enum fg_status {
     FG_OK = 0,
@@ -306,8 +306,14 @@ int  fg_advance_progress(fg_handle* h, int64_t watermark, int32_t out_location, 
  * async advance stay valid until the next call that fires windows. */
 int  fg_advance_progress_async(fg_handle* h, int64_t watermark);
 /* Waits for the fires of the last fg_advance_progress_async call and returns their rows (device
- * pointers, as fg_advance_progress with FG_DEVICE); n = 0 when it fired nothing. */
+ * pointers, as fg_advance_progress with FG_DEVICE); n = 0 when it fired nothing. A synchronous
+ * fg_advance_progress called while async rows are uncollected returns them ahead of its own rows
+ * (none is dropped). */
 int  fg_collect_fired(fg_handle* h, fg_rows* fired);
+/* fg_collect_fired with the rows at out_location (ABI 12): FG_HOST copies them into library-owned
+ * host memory (as fg_advance_progress with FG_HOST) -- what a JVM shim wraps in direct buffers;
+ * FG_DEVICE is fg_collect_fired. */
+int  fg_collect_fired_to(fg_handle* h, int32_t out_location, fg_rows* fired);
 int  fg_flush(fg_handle* h);
 int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);

@@ -11,7 +11,7 @@
  *   addPartials     fg_add_partials      (GlobalAggCombiner.combine)
  *   advanceProgress fg_advance_progress  (processWatermark -> advanceProgress + fireWindow)
  *   advanceProgressAsync fg_advance_progress_async (the same, the fires queued: the watermark held)
- *   collectFired    fg_collect_fired     (the held watermark's rows, then the watermark is forwarded)
+ *   collectFired    fg_collect_fired_to  (the held watermark's rows, in host memory; then the watermark is forwarded)
  *   flush           fg_flush             (prepareSnapshotPreBarrier)
  *   snapshotState   fg_snapshot_state    (snapshotState: the window-aggs image)
  *   restore         fg_restore           (initializeState)
@@ -211,13 +211,14 @@ JNIEXPORT void JNICALL FN(advanceProgressAsync)(JNIEnv* env, jclass cls, jlong h
     check(env, h, fg_advance_progress_async(h, wm));
 }
 
-/* long collectFired(long h, ByteBuffer[] cols): as advanceProgress (device columns: the shim
- * hands them to a GPU-side consumer, or copies them out) */
+/* long collectFired(long h, ByteBuffer[] cols): as advanceProgress -- the rows are copied to
+ * library-owned host memory (fg_collect_fired_to FG_HOST), so the direct buffers the shim reads
+ * with getLong are host memory, valid until the next call on the handle */
 JNIEXPORT jlong JNICALL FN(collectFired)(JNIEnv* env, jclass cls, jlong hp, jobjectArray cols) {
     (void)cls;
     fg_handle* h = (fg_handle*)(intptr_t)hp;
     fg_rows r;
-    if (check(env, h, fg_collect_fired(h, &r))) return 0;
+    if (check(env, h, fg_collect_fired_to(h, FG_HOST, &r))) return 0;
     const jlong n = r.n, bytes = 8 * n;
     if ((*env)->GetArrayLength(env, cols) < 5 + r.num_aggs) {
         throw_code(env, FG_EINVAL, "collectFired: column array too short");

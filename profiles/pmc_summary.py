@@ -59,16 +59,10 @@ def traffic(res):
     return t
 
 
-def lib_sha256(path):
-    import hashlib
-    h = hashlib.sha256()
-    with open(path, "rb") as f:
-        for chunk in iter(lambda: f.read(1 << 20), b""):
-            h.update(chunk)
-    return h.hexdigest()
-
-
 if __name__ == "__main__":
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from flink_amd import buildinfo
     res = summarize(glob.glob(sys.argv[1]))
     for k, cs in sorted(res.items()):
         print(k)
@@ -76,9 +70,11 @@ if __name__ == "__main__":
             print(f"   {c:28s} {v:16.1f}")
     if len(sys.argv) > 2:
         t = traffic(res)
-        # provenance: bench.py reports these bytes only for the library build they were
-        # counted on (sha256 of libflinkgpu.so), never for another build
+        # provenance: bench.py reports these bytes only for the kernels they were counted on
+        # (sha256 of libflinkgpu.so's device code objects), never for other kernels
         lib = sys.argv[3] if len(sys.argv) > 3 else None
-        t["_provenance"] = {"lib_sha256": lib_sha256(lib) if lib else None, "source": sys.argv[1]}
+        t["_provenance"] = {"lib_sha256": buildinfo.file_sha256(lib) if lib else None,
+                            "kernels_sha256": buildinfo.kernels_sha256(lib) if lib else None,
+                            "source": sys.argv[1]}
         json.dump(t, open(sys.argv[2], "w"), indent=1)
         print("wrote", sys.argv[2])

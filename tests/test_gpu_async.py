@@ -1,4 +1,4 @@
-"""fg_advance_progress_async / fg_collect_fired (ABI 11) on the GPU.
+"""fg_advance_progress_async / fg_collect_fired (ABI 11) / fg_collect_fired_to (ABI 12) on the GPU.
 
 The asynchronous advance queues a watermark's fires and returns at once; the fires' completion
 (row count, region retries, overflow check) is taken by the next call that needs it, and the
@@ -25,7 +25,10 @@ def _cfg(kind, mode="sql", vt="f64"):
 
 
 def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0, delay=0, collect_every=1,
-         regions_small=False, ckpt_every=0, zipf=0.0, sync=False):
+         regions_small=False, ckpt_every=0, zipf=0.0, sync=False, collect="device"):
+    """collect: "device" (fg_collect_fired, rows copied out by torch), "host" (fg_collect_fired_to
+    FG_HOST), or "sync_wm" (no collect: a synchronous watermark instead, whose rows must lead with
+    every async row not collected yet)."""
     from tests.gpu_adapter import GpuOperator
     key, ts, val, _ = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, zipf=zipf)
     g = GpuOperator(cfg, expected_keys=1000 if regions_small else keys, buffer_records=4 * batch)
@@ -56,7 +59,13 @@ def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0
             g.prepare_snapshot()
             o.prepare_snapshot()
         if nb % collect_every == 0 or ckpt:
-            if not sync:
+            if sync:
+                pass
+            elif collect == "host":
+                g._rows = [op.collect_fired(host=True)]
+            elif collect == "sync_wm":   # the last watermark again, synchronously: fires nothing new
+                g._rows = [op.process_watermark(wm)]
+            else:
                 g._rows = [op.rows_to_host(op.collect_fired())]
             got = g.take_rows()
             assert_rows_equal(got, np.concatenate(exp), cfg["val_type"], f"batch {nb}")
@@ -104,6 +113,14 @@ def test_async_watermarks_checkpoint_restore(oracle_mod, kind, sync):
     re-fire horizon and fired the next step window -- the fused flush+fire ran before the re-fire
     had folded that record into the cumulative window's first slice.)"""
     _run(oracle_mod, _cfg(kind), jitter=1500, delay=300, ckpt_every=4, collect_every=2, sync=sync)
+
+
+@pytest.mark.parametrize("collect", ["host", "sync_wm"])
+def test_async_rows_to_host_and_sync_watermark(oracle_mod, collect):
+    """fg_collect_fired_to(FG_HOST) returns the async rows in library-owned host memory (what the
+    JNI collectFired wraps in direct buffers); a synchronous watermark while async rows are
+    uncollected returns them ahead of its own (none is dropped)."""
+    _run(oracle_mod, _cfg("hop"), collect_every=2, collect=collect)
 
 
 def test_async_watermarks_zipf(oracle_mod):

@@ -11,6 +11,10 @@ Tolerance (north_star): keys, windows, COUNT(*), COUNT bit-exact, late drops equ
 SUM / AVG within 1e-9 relative (the GPU sums a (key, window) in another order than
 AggCombiner's arrival order).
 
+Each of configs[1..4] runs twice: with synchronous watermarks (host rows) and with the path the
+bench times -- asynchronous watermarks held until the next micro-batch has been handed over, their
+rows collected then (bench.one_step); rows returned equal the engine's rows_fired either way.
+
 Sizes: configs[1] 200M records = 2 windows x 10M uniform keys; configs[2] 200M records = 6
 event-minutes of HOP 5min/1min over 10M keys; configs[3] 70M records = 4+ steps of a
 CUMULATE 1h/1min window over the 12.5M-key per-GPU share of 100M; configs[4] 300M records
@@ -40,22 +44,45 @@ def log(msg):
 
 
 def gpu_rows_run(op, key, ts, val, n, batch, rate, wm_every, delay, jitter, snapshot_after_batch=None,
-                 reopen=None, final_wm=JMAX):
+                 reopen=None, final_wm=JMAX, async_wm=False):
     """Drive the engine like bench.one_step; returns (rows, late drops, oracle watermark schedule,
-    index of the snapshot watermark or -1)."""
+    index of the snapshot watermark or -1).
+
+    async_wm: the bench's (and a shim's) watermark path -- process_watermark(wm, device_output=True,
+    wait=False) for every watermark of a batch, held until the NEXT batch has been handed over, then
+    collect_fired() (bench.one_step); else the synchronous advance with host rows."""
     B = _bench()
     parts = []
     wm_at, wm_val = [], []
     snap_idx = -1
     late_base = 0
+    held = False
+    fired = 0   # rows returned, against the engine's own rows_fired
+
+    def collect():
+        r = op.collect_fired()
+        parts.append(op.rows_to_host(r))
+        return r.n
     for bi, lo in enumerate(range(0, n, batch)):
         hi = min(n, lo + batch)
         op.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        if held:   # the previous batch's watermarks: their rows now (fires completed behind this pass 1)
+            fired += collect()
+            held = False
         for wm in B.watermarks_for(lo, hi, rate, wm_every, delay, jitter):
-            parts.append(op.process_watermark(wm))
+            if async_wm:
+                assert op.process_watermark(wm, device_output=True, wait=False) is None
+                held = True
+            else:
+                parts.append(op.process_watermark(wm))
+                fired += len(parts[-1])
             wm_at.append(hi)
             wm_val.append(wm)
         if snapshot_after_batch is not None and bi == snapshot_after_batch:
+            if held:   # the rows go out before the checkpoint barrier
+                fired += collect()
+                held = False
+            assert op.stats()["rows_fired"] == fired
             # prepareSnapshotPreBarrier + snapshotState, then a failover: a new operator
             # restored from the image (initializeState)
             op.prepare_snapshot_pre_barrier()
@@ -65,10 +92,15 @@ def gpu_rows_run(op, key, ts, val, n, batch, rate, wm_every, delay, jitter, snap
             op = reopen()
             op.restore_state(img, twm)
             snap_idx = len(wm_at) - 1
+            fired = 0
+    if held:
+        fired += collect()
     parts.append(op.process_watermark(final_wm))
+    fired += len(parts[-1])
     wm_at.append(n)
     wm_val.append(final_wm)
     late = late_base + op.num_late_records_dropped
+    assert op.stats()["rows_fired"] == fired, "rows returned vs the engine's rows_fired"
     op.close()
     parts = [p for p in parts if len(p)]
     rows = np.concatenate(parts) if parts else None
@@ -102,7 +134,7 @@ def compare_rows(g, e, S, ctx, aggs):
 
 
 def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch=None, keys=None,
-               final_wm_after=None):
+               final_wm_after=None, async_wm=False):
     """final_wm_after: end with the watermark `final_wm_after` ms past the last regular one
     instead of Long.MAX_VALUE (CUMULATE: MAX_VALUE would fire every remaining step window of
     the hour for every key -- 60 x 12.5M rows)."""
@@ -135,9 +167,10 @@ def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch
     final_wm = JMAX
     if final_wm_after is not None:
         final_wm = B.watermarks_for(0, n, rate, wm_every, wl["delay"], wl["jitter"])[-1] + final_wm_after
-    log(f"{workload}: {n:,} records generated; GPU run")
+    log(f"{workload}: {n:,} records generated; GPU run ({'async' if async_wm else 'sync'} watermarks)")
     rows, late, wm_at, wm_val, snap = gpu_rows_run(mk(), key, ts, val, n, batch, rate, wm_every, wl["delay"],
-                                                   wl["jitter"], snapshot_after_batch, reopen=mk, final_wm=final_wm)
+                                                   wl["jitter"], snapshot_after_batch, reopen=mk, final_wm=final_wm,
+                                                   async_wm=async_wm)
     log(f"{workload}: GPU fired {0 if rows is None else len(rows):,} rows; oracle run")
     kh, th, vh = key.cpu().numpy(), ts.cpu().numpy(), val.cpu().numpy()
     del key, ts, val
@@ -168,37 +201,44 @@ def test_config0_datastream_tumble_10M_records():
     assert nrows == 10 * 10_000
 
 
-def test_config1_tumble_10M_keys():
+@pytest.mark.parametrize("wm", ["sync", "async"])
+def test_config1_tumble_10M_keys(wm):
     """configs[1]: SQL TUMBLE 1s COUNT(*)/COUNT/SUM/AVG(double), 10M uniform keys, 200M records =
     2 windows of 100M records (~10 records per (key, window))."""
     from oracle import oracle as O
-    nrows, late = run_config("tumble", 200_000_000, ("count_star", "count", "sum", "avg"), O.TUMBLE, 1000, 0)
+    nrows, late = run_config("tumble", 200_000_000, ("count_star", "count", "sum", "avg"), O.TUMBLE, 1000, 0,
+                             async_wm=wm == "async")
     assert nrows > 19_000_000 and late == 0
 
 
-def test_config2_hop_5min_1min_10M_keys():
+@pytest.mark.parametrize("wm", ["sync", "async"])
+def test_config2_hop_5min_1min_10M_keys(wm):
     """configs[2]: SQL HOP 5min/1min, 10M keys, 200M records = 6 event-minutes: every window
     merges up to 5 one-minute slice tables on fire."""
     from oracle import oracle as O
-    nrows, _ = run_config("hop", 200_000_000, ("count_star", "sum", "avg"), O.HOP, 300_000, 60_000)
+    nrows, _ = run_config("hop", 200_000_000, ("count_star", "sum", "avg"), O.HOP, 300_000, 60_000,
+                          async_wm=wm == "async")
     assert nrows > 50_000_000
 
 
-def test_config3_cumulate_1h_1min_per_gpu_share():
+@pytest.mark.parametrize("wm", ["sync", "async"])
+def test_config3_cumulate_1h_1min_per_gpu_share(wm):
     """configs[3]: SQL CUMULATE 1h/1min over the 12.5M-key per-GPU share of 100M keys, 70M
     records = 4+ one-minute steps of the hour window (each step window folds its slice into
     the first slice's state and emits every key seen so far)."""
     from oracle import oracle as O
     nrows, _ = run_config("cumulate", 70_000_000, ("count_star", "sum", "avg"), O.CUMULATE, 3_600_000, 60_000,
-                          final_wm_after=60_000)
+                          final_wm_after=60_000, async_wm=wm == "async")
     assert nrows > 30_000_000
 
 
-def test_config4_zipf_jitter_checkpoint_restore():
+@pytest.mark.parametrize("wm", ["sync", "async"])
+def test_config4_zipf_jitter_checkpoint_restore(wm):
     """configs[4]: TUMBLE 1s AVG(double) over Zipf(1.1) keys (10M ranks), rowtime jitter
     U[0, 2 s), watermark = max rowtime - 2 s - 1 (bounded out-of-orderness), and a checkpoint
     after the third micro-batch followed by a failover: the operator is closed and a new one
     restored from the snapshot image continues the stream."""
     from oracle import oracle as O
-    nrows, _ = run_config("zipf", 300_000_000, ("count_star", "avg"), O.TUMBLE, 1000, 0, snapshot_after_batch=2)
+    nrows, _ = run_config("zipf", 300_000_000, ("count_star", "avg"), O.TUMBLE, 1000, 0, snapshot_after_batch=2,
+                          async_wm=wm == "async")
     assert nrows > 5_000_000

@@ -973,6 +973,37 @@ def test_datastream_allowed_lateness_parity(oracle_mod, name, cfg, kw):
     assert late > 0, "the stream should drop some elements beyond the lateness"
 
 
+def test_datastream_lateness_wide_late_keys(oracle_mod):
+    """Late-allowed elements enter the resident slice tables without pass 1's 32-bit key check
+    (late_split): a late element whose key is k + 2^33 -- the same int32 as the staged key k --
+    must not meet k in a sliding window's fire over those tables (the narrow LDS table keys
+    entries by the int32 of their mix). Only late elements carry such keys."""
+    cfg = dict(cfg_of("hop", 3000, 1000, vt="i64", mode="datastream"), allowed_lateness=1500)
+    n, keys, batch, delay = 200_000, 2000, 10_000, 100
+    key, ts, val, _ = make_stream(n, keys, "i64", jitter_ms=2500)
+    prev = np.iinfo(np.int64).min
+    for lo, hi, wm in batches_with_watermarks(n, batch, ts, delay):
+        first_end = (ts[lo:hi] // 1000) * 1000 + 1000   # earliest window of the element
+        late = np.nonzero(first_end - 1 <= prev)[0] + lo
+        key[late[::2]] += 1 << 33
+        prev = wm
+    g = gpu_mk(cfg, expected_keys=keys, buffer_records=1 << 18)
+    o = oracle_mk(oracle_mod, cfg)
+    for step, (lo, hi, wm) in enumerate(batches_with_watermarks(n, batch, ts, delay)):
+        g.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), "i64", f"step {step}")
+        assert g.late_dropped == o.late_dropped
+    g.process_watermark(JMAX)
+    o.process_watermark(JMAX)
+    assert_rows_equal(g.take_rows(), o.take_rows(), "i64", "final")
+    assert (key > (1 << 32)).any()
+    g.close()
+    o.close()
+
+
 @pytest.mark.parametrize("kind", ["tumble", "hop"])
 def test_narrow_staging_switches_to_wide_keys(oracle_mod, kind):
     """Narrow 12-B staging (keys within 32 bits, two-pass partition): batches of small keys are
