@@ -116,6 +116,16 @@ struct Staged {
     bool narrow = false;  // 12-B records {int32 key, value} (IngestParams.narrow)
     bool skew = false;    // some region may hold over kHeavyMin records of this pass (hot keys)
     int refs = 0;         // lanes still holding records of this pass
+    // tile staging (fg_kernels.h): the records stay in pass-1 tiles sorted by consumer bucket
+    // until a TUMBLE / local-phase fire reads them (k_tile_fire) or they are materialized
+    bool tiles = false;
+    DevBuf t_rec, t_dt;   // block-laid 12-B records at their batch index; per-bucket (offset, length) columns
+    int64_t t_seg_per = 0;
+    int t_nt = 0, t_mt = 0, t_nc = 0;
+    bool busy = false;    // read by a merge job not yet settled: not reused from the pool
+    // a materialized tile pass: its own narrow record area (block-laid from index 0)
+    bool own = false;
+    DevBuf own_rec;
 };
 
 // A slice lane of the staged buffer (RecordsWindowBuffer analogue, one per live slice):
@@ -155,10 +165,11 @@ constexpr int64_t kHeavyMin = 1 << 16;
 constexpr int64_t kHeavyChunk = 1 << 16;
 
 enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_PART1, K_PART2, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE,
-              K_HEAVY, K_NCLASS };
+              K_HEAVY, K_TILE1, K_TILE_FIRE, K_TILE_MAT, K_NCLASS };
 const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan",      "ingest_scatter", "ingest_part1",
                                            "ingest_part2", "merge_flush",      "merge_flush_fire", "merge_fire",
-                                           "export",       "restore",          "merge_heavy"};
+                                           "export",       "restore",          "merge_heavy",      "tile_part1",
+                                           "tile_fire",    "tile_materialize"};
 struct KStat {
     int64_t launches = 0;
     double ms = 0;
@@ -192,6 +203,7 @@ struct PassState {
     IngestParams p{};
     std::unique_ptr<Staged> s;
     bool two_pass = false, spec = false;
+    bool tiles = false;    // tile staging (k_tile_part1): no pass 2
     int64_t n = 0;
     const uint8_t* vnull = nullptr;
     int64_t flo = 0, fhi = 0;
@@ -208,6 +220,8 @@ struct MergeJob {
     // restore re-fire (MergeParams): marking / mark-only sources, marked emission, chain dst
     uint64_t mark_mask = 0, markonly_mask = 0;
     int emit_marked = 0, dst_mode = 0;
+    bool tile = false;     // a fire straight from tile passes (k_tile_fire; batches: the passes, tbits)
+    int tbits = 0;
 };
 
 }  // namespace
@@ -282,6 +296,13 @@ struct fg_handle {
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     int hslot = 0;
     DevBuf part_tmp, part_tmp_null, part_dir;   // two-pass partition: pass-1 tiles + directory
+    // tile staging (FG_TILE=0 turns it off, A/B): in-order TUMBLE and local-phase batches of 32-bit
+    // keys stay in their pass-1 tiles until the fire; off for good once a wider key is seen
+    bool tile_ok = true;
+    bool tile_env = true;     // FG_TILE (fg_reset restores tile_ok from it)
+    bool tile_skew = false;   // a tile pass saw hot-key skew: later batches take the two-pass partition
+                              // (a performance hint kept across fg_reset)
+    DevBuf tile_dir, tile_hist;
     // skewed-region plan and chunk partial tables
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
     DevBuf hv_mv1, hv_mv2;   // multi-value operator: value slots 1 and 2 of the chunks' partial rows
@@ -620,6 +641,11 @@ StagedBatch batch_of(const fg_handle* h, const JobBatch& jb) {
             b.val1 = h->acc_v1.as<int64_t>() + at;
             b.val2 = h->acc_v2.as<int64_t>() + at;
         }
+    } else if (s->own) {   // a materialized tile pass: narrow records of its own area, from index 0
+        b.rec = s->own_rec.as<int64_t>();
+        b.rec_first = 0;
+        b.vnull = nullptr;
+        b.stride = 3;
     } else {
         // narrow records: block-laid from the staged area's base (kRec12Block), the batch's
         // first record by index
@@ -696,6 +722,42 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     p->dst_mode = j.dst_mode;
     p->src_null_mask = null_mask;
     return FG_OK;
+}
+
+// ---- tile staging (fg_kernels.h) ------------------------------------------------------------
+TilePass tile_pass_of(const Staged* s, int lane) {
+    TilePass tp{};
+    tp.rec = s->t_rec.p;
+    tp.dt = s->t_dt.as<uint32_t>();
+    tp.seg_per = s->t_seg_per;
+    tp.nt = s->t_nt;
+    tp.mt = s->t_mt;
+    tp.nc = s->t_nc;
+    tp.bits = s->bits;
+    tp.lane = lane;
+    return tp;
+}
+
+// TileFire of tile job `ji` at the current region bits (retry: regions in retry_list)
+int tile_job_params(fg_handle* h, int ji, TileFire* f) {
+    const MergeJob& j = h->jobs[(size_t)ji];
+    std::vector<TilePass> tps;
+    for (const JobBatch& jb : j.batches) tps.push_back(tile_pass_of(jb.s, jb.lane));
+    *f = TileFire{};
+    MergeParams& p = f->m;
+    p.region_bits = h->region_bits;
+    set_values(h, &p);
+    fill_emit(h, p, j.wend);
+    p.emit = 1;
+    p.overflow = h->scalars.as<unsigned int>();
+    p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
+    p.fail_list = h->fail_list.as<uint32_t>();
+    p.fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 16);
+    p.fail_cap = kFailCap;
+    p.job = ji;
+    f->n_passes = (int32_t)tps.size();
+    f->tbits = j.tbits;
+    return arena_put(h, tps.data(), tps.size(), &f->passes);
 }
 
 // Split every slice table's regions 2^b -> 2^nb (k_split_table). Staged passes keep their
@@ -777,6 +839,17 @@ int retry_failed(fg_handle* h) {
             for (int32_t r : kv.second)
                 for (int c = 0; c < (1 << sh); c++) regs.push_back((r << sh) | c);
             j.bits = h->region_bits;
+            if (j.tile) {   // one region per item, the bucket's records filtered by region
+                TileFire f{};
+                rc = tile_job_params(h, kv.first, &f);
+                if (rc) return rc;
+                rc = arena_put(h, regs.data(), regs.size(), &f.m.retry_list);
+                if (rc) return rc;
+                f.m.n_retry = (int)regs.size();
+                KTimer kt(h, j.kclass, 0);
+                HIPCHK(h, launch_tile_fire(f, std::min<int>((int)regs.size(), merge_grid(h)), h->stream));
+                continue;
+            }
             MergeParams p{};
             rc = job_params(h, kv.first, &p);
             if (rc) return rc;
@@ -794,6 +867,9 @@ int retry_failed(fg_handle* h) {
 }
 int settle_jobs(fg_handle* h) {
     const int rc = retry_failed(h);
+    for (MergeJob& j : h->jobs)   // (tile passes the jobs read may be reused from the pool now)
+        for (JobBatch& jb : j.batches)
+            if (jb.s) jb.s->busy = false;
     h->jobs.clear();
     // tables freed while the jobs ran go back to the pool (or away, after a split)
     for (auto& t : h->deferred)
@@ -943,6 +1019,80 @@ void release_lane(fg_handle* h, int l) {
 
 int merge_grid(const fg_handle* h) { return std::min(h->P, h->merge_grid); }
 
+// A Staged from the pool that no unsettled job reads (or a new one)
+std::unique_ptr<Staged> pass_from_pool(fg_handle* h) {
+    std::unique_ptr<Staged> s;
+    for (size_t i = h->pass_pool.size(); i-- > 0;) {
+        if (h->pass_pool[i]->busy) continue;
+        s = std::move(h->pass_pool[i]);
+        h->pass_pool.erase(h->pass_pool.begin() + (long)i);
+        break;
+    }
+    if (!s) s.reset(new Staged());
+    return s;
+}
+
+// Lane l's tile passes become regular narrow staged passes (their own record areas) at the
+// current regions: per-region counts (k_tile_count), their scan, the records written by region
+// (k_tile_scatter). Every consumer other than the fire straight from the tiles -- a flush into
+// the slice table, a checkpoint, a restore re-fire, the heavy pass -- then reads the lane as it
+// reads any staged pass.
+int materialize_lane(fg_handle* h, int l) {
+    Lane& ln = h->lane[l];
+    for (size_t i = 0; i < ln.passes.size(); i++) {
+        Staged* s = ln.passes[i];
+        if (!s->tiles) continue;
+        const int bits = h->region_bits;
+        if (bits - s->bits + kTileBits > 6)
+            return h->fail(FG_ECAPACITY, "internal: regions split %d times since a tile pass", bits - s->bits);
+        std::unique_ptr<Staged> m = pass_from_pool(h);
+        const TilePass tp = tile_pass_of(s, l);
+        const int64_t P = (int64_t)1 << bits;
+        HIPCHK(h, h->tile_hist.ensure(4 * (size_t)(P + 1)));
+        HIPCHK(h, h->scan_tmp.ensure(4 * scan_tmp_words(P)));
+        HIPCHK(h, m->bucket_off.ensure(sizeof(uint32_t) * (((size_t)kMaxLanes << bits) + 1)));
+        HIPCHK(h, m->own_rec.ensure((size_t)(s->lane_n[l] / 64 + 2) * kRec12Block));
+        uint32_t* bo = m->bucket_off.as<uint32_t>() + ((int64_t)l << bits);
+        {
+            KTimer kt(h, K_TILE_MAT, s->lane_n[l]);
+            HIPCHK(h, launch_tile_count(tp, bits, h->tile_hist.as<uint32_t>(), h->stream));
+            HIPCHK(h, launch_scan_u32(h->tile_hist.as<uint32_t>(), bo, P, h->scan_tmp.as<uint32_t>(), h->stream));
+            HIPCHK(h, launch_tile_scatter(tp, bits, bo, m->own_rec.p, h->stream));
+        }
+        m->bits = bits;
+        m->is_acc = false;
+        m->has_null = false;
+        m->narrow = true;
+        m->tiles = false;
+        m->own = true;
+        m->busy = false;
+        m->skew = s->skew;
+        for (int q = 0; q < kMaxLanes; q++) m->lane_start[q] = m->lane_n[q] = 0;
+        m->lane_n[l] = s->lane_n[l];
+        m->refs = 1;
+        ln.passes[i] = m.get();
+        h->passes.push_back(std::move(m));
+        if (--s->refs == 0) {
+            for (size_t k = 0; k < h->passes.size(); k++) {
+                if (h->passes[k].get() != s) continue;
+                h->pass_pool.push_back(std::move(h->passes[k]));
+                h->passes.erase(h->passes.begin() + (long)k);
+                break;
+            }
+        }
+    }
+    return FG_OK;
+}
+
+// Lane l fires straight from its tile passes: every pass a tile pass of the same bits, no skew,
+// COUNT(*) below 2^32
+bool tile_fire_ok(const fg_handle* h, const Lane& ln) {
+    if (ln.passes.empty() || ln.acc_fill != 0 || ln.fill >= ((int64_t)1 << 32) || h->mv) return false;
+    for (const Staged* s : ln.passes)
+        if (!s->tiles || s->skew || s->bits != ln.passes[0]->bits) return false;
+    return true;
+}
+
 // Plan the skewed regions of one lane's merge (k_heavy_plan): regions over
 // max(kHeavyMin, 8 x mean) staged records, cut into kHeavyChunk-record chunks.
 int plan_heavy(fg_handle* h, const StagedBatch* d_sb, int nb, int64_t fill, HeavyPlan* hp) {
@@ -1023,10 +1173,59 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     }
     std::vector<int64_t> fired_tables, retained;
     bool any_emit = false;
+    int fire_class = K_FLUSH_FIRE;   // kernel class credited with the fired rows
     int rc;
     for (int l : sel) {
         const Lane& ln = h->lane[l];
         const int64_t se = slice_end_of(h, ln.q);
+        bool lane_tiles = false;
+        for (const Staged* st : ln.passes) lane_tiles = lane_tiles || st->tiles;
+        if (lane_tiles) {
+            // tile passes: a TUMBLE window (or a local slice) due now fires straight from the
+            // tiles; anything else reads the lane's records once they are materialized
+            const int64_t trig0 = trigger_time(h->w, se);
+            const bool due0 = fire && se != JMAX && trig0 > fire->prev && trig0 <= fire->wm;
+            const bool fire0 = fire && (h->local || (h->w.kind == TUMBLE && due0));
+            SliceTable* t0 = nullptr;
+            rc = table_get(h, se, false, &t0);
+            if (rc) return rc;
+            if (fire0 && !refire_slice(h, se) && !(h->retain && !h->local) && (!t0 || t0->upper == 0) &&
+                tile_fire_ok(h, ln)) {
+                const int64_t ub = std::min<int64_t>(ln.fill, kStateCapMax);
+                if (zeroed_out && !h->out_count_reset && h->adv_base + h->late_rows == 0) h->out_count_reset = true;
+                rc = reset_out_count(h);
+                if (rc) return rc;
+                rc = ensure_out(h, h->out_n + h->pending_out + ub);
+                if (rc) return rc;
+                h->pending_out += ub;
+                MergeJob job;
+                for (Staged* st : ln.passes) {
+                    job.batches.push_back(JobBatch{st, l, StagedBatch{}, 0});
+                    st->busy = true;
+                }
+                job.emit = true;
+                job.wend = se;
+                job.kclass = K_TILE_FIRE;
+                job.tile = true;
+                job.tbits = ln.passes[0]->bits;
+                int ji = 0;
+                rc = job_add(h, std::move(job), &ji);
+                if (rc) return rc;
+                TileFire f{};
+                rc = tile_job_params(h, ji, &f);
+                if (rc) return rc;
+                {
+                    KTimer kt(h, K_TILE_FIRE, ln.fill);
+                    HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                }
+                if (t0) fired_tables.push_back(se);
+                any_emit = true;
+                fire_class = K_TILE_FIRE;
+                continue;
+            }
+            rc = materialize_lane(h, l);
+            if (rc) return rc;
+        }
         if (refire_slice(h, se)) {
             // after a restore, records of a slice whose windows fired before the checkpoint:
             // their state (re_new) and their keys (re_delta, at the window their timer chain
@@ -1227,7 +1426,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     if (h->async_advance && any_emit) {
         // fg_advance_progress_async: the host's bookkeeping now, the device's results later
         // (complete_fire); tables freed here are held until then
-        rc = publish_fire(h, K_FLUSH_FIRE);   // (first: the tables freed below are held)
+        rc = publish_fire(h, fire_class);   // (first: the tables freed below are held)
         if (rc) return rc;
         for (int64_t se : fired_tables) table_free(h, se);
         for (int64_t se : retained) retire(h, se, se);
@@ -1245,7 +1444,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     if (any_emit) {
         const int64_t before = h->out_n;
         h->out_n = (int64_t)h->h_scalars.as<unsigned long long>()[1];
-        h->kstat[K_FLUSH_FIRE].rows += h->out_n - before;
+        h->kstat[fire_class].rows += h->out_n - before;
         h->pending_out = 0;
     }
     for (int64_t se : fired_tables) table_free(h, se);
@@ -1884,7 +2083,30 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     // two-pass partition when the regions split into 64-bucket coarse groups
     const bool two_pass = h->region_bits >= kFineBits && h->F <= kMaxPart1Fine;
     ps.two_pass = two_pass;
-    if (two_pass) {
+    // tile staging: TUMBLE windows and the local phase's slices fire straight from pass 1's tiles
+    // (32-bit keys, one value accumulator, no NULL values, no allowed lateness, no hot-key skew)
+    const bool tiles = two_pass && h->tile_ok && !h->tile_skew && h->narrow && !vnull && !h->mv && h->lateness == 0 &&
+                       (h->w.kind == TUMBLE || h->local) && (h->F >> kTileBits) <= kMaxTileBuckets;
+    ps.tiles = tiles;
+    if (tiles) {
+        // the pass's own Staged (its tiles live until the fire): a pooled one no unsettled job reads
+        ps.s = pass_from_pool(h);
+        Staged* st = ps.s.get();
+        int64_t per = (n + p.grid - 1) / p.grid;
+        per = (per + 1) & ~int64_t(1);   // (seg_bounds)
+        p.max_tiles = (int32_t)((per + kTileRecs - 1) / kTileRecs);
+        p.n_coarse = h->F >> kTileBits;
+        const int64_t NT = (int64_t)p.grid * p.max_tiles;
+        HIPCHK(h, st->t_rec.ensure((size_t)(n / 64 + 2) * kRec12Block));
+        HIPCHK(h, st->t_dt.ensure(4 * (size_t)p.n_coarse * NT));
+        HIPCHK(h, h->tile_dir.ensure(2 * (size_t)NT * (p.n_coarse + 1)));
+        p.tmp = st->t_rec.as<longlong2>();
+        p.dir = h->tile_dir.as<uint16_t>();
+        st->t_seg_per = per;
+        st->t_mt = p.max_tiles;
+        st->t_nt = (int)NT;
+        st->t_nc = p.n_coarse;
+    } else if (two_pass) {
         p.max_tiles = part1_max_tiles(n, p.grid);
         p.n_coarse = h->F >> kFineBits;
         HIPCHK(h, h->part_tmp.ensure(16 * (size_t)n + kRec12Block));   // (+ a narrow block's tail)
@@ -1916,7 +2138,15 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     // a stream seen skewed (hot keys) partitions in pass-2 units of one pass-1 workgroup: the
     // hot key's coarse bucket is then spread over as many units as there are workgroups
     p.p2_group = h->skew_seen ? h->p2_skew_group : 0;
-    if (two_pass) {
+    if (tiles) {
+        {
+            KTimer kt(h, K_TILE1, n);
+            HIPCHK(h, launch_tile_part1(p, h->stream));
+        }
+        // each bucket's (offset, length) column (before k_scan_plan resets the lane mask it reads)
+        HIPCHK(h, launch_tile_dirt(p.dir, ps.s->t_nt, p.n_coarse, h->region_bits - kTileBits, p.lane_mask,
+                                   ps.s->t_dt.as<uint32_t>(), h->stream));
+    } else if (two_pass) {
         KTimer kt(h, K_PART1, n);
         HIPCHK(h, launch_part1(p, h->stream));
     } else {
@@ -1929,26 +2159,22 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     // so they are queued before the host waits for the counters (no idle GPU across the
     // round trip); a pass that stages nothing goes back to the pool
     std::unique_ptr<Staged>& s = ps.s;
-    if (!h->pass_pool.empty()) {
-        s = std::move(h->pass_pool.back());
-        h->pass_pool.pop_back();
-    } else {
-        s.reset(new Staged());
-    }
-    const int Fp = p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
+    if (!s) s = pass_from_pool(h);   // (a tile pass took its Staged before pass 1)
+    const int Fp = tiles ? 0 : p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
     HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (Fp + 1)));
     // Speculative pass 2 (two-pass partition): the lane decision the host takes below is
     // taken on the device from pass 1's counters (k_scan_plan), and pass 2 is queued at
     // once, so the GPU does not idle across the counters' round trip. When the batch needs a
     // flush first (another slice in a lane, no room) the plan says so and pass 2 does
     // nothing; the host then takes the regular path below.
-    const bool spec = two_pass && h->speculate;
+    // (a tile pass is finished at the next call too: nothing of it depends on the host's decisions)
+    const bool spec = two_pass && (h->speculate || tiles);
     ps.spec = spec;
     {
         // per-bucket prefix over workgroups, then one workgroup: bucket bases, the counters
         // to the host (reset for the next pass), the lane plan
         KTimer kt(h, K_SCAN, 0);
-        HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), Fp, p.grid, h->stream));
+        if (Fp > 0) HIPCHK(h, launch_hist_columns(h->hist.as<uint32_t>(), h->totals.as<uint32_t>(), Fp, p.grid, h->stream));
         PlanParams pp{};
         pp.lane_cap = h->lane_cap;
         for (int l = 0; l < kMaxLanes; l++) {
@@ -1964,13 +2190,13 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         sa.host = h->h_pass.as<unsigned long long>();
         sa.reset.n = sa.n_words;
         std::memcpy(sa.reset.v, &init, sizeof init);
-        sa.do_plan = spec ? 1 : 0;
+        sa.do_plan = spec && !tiles ? 1 : 0;
         sa.plan = h->plan_dev.as<IngestPlan>();
         sa.seq = ++h->pass_seq;   // settle_pending polls for it (no event between the kernels)
         HIPCHK(h, launch_scan_plan(p, pp, sa, h->stream));
         h->counters_clean = true;
     }
-    if (spec) {
+    if (spec && !tiles) {
         IngestParams q = p;
         q.bucket_base = s->bucket_off.as<uint32_t>();
         // one lane's units: each workgroup takes its unit of every lane the plan finds active
@@ -2002,14 +2228,17 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     int rc = FG_OK;
     DevCounters got;   // written by k_scan_plan into host-visible memory
     std::memcpy(&got, h->h_pass.p, sizeof got);
+    const bool tiles = ps.tiles;
     IngestPlan plan{};
-    if (spec) std::memcpy(&plan, h->h_pass.as<char>() + sizeof(DevCounters), sizeof plan);
-    const bool staged_by_plan = spec && plan.ok;
+    if (spec && !tiles) std::memcpy(&plan, h->h_pass.as<char>() + sizeof(DevCounters), sizeof plan);
+    const bool staged_by_plan = spec && !tiles && plan.ok;
     out->drops = got.drops;
     out->qmin = got.qmin;
     out->qmax = got.qmax;
     out->qnext = got.qnext;
-    out->skew = (int64_t)got.max_bucket * p.grid > kHeavyMin;
+    // (a tile pass reports its largest bucket count of one tile: > 16x the uniform mean is skew)
+    out->skew = tiles ? (int64_t)got.max_bucket > kTileRecs / 64
+                      : (int64_t)got.max_bucket * p.grid > kHeavyMin;
     for (int l = 0; l < kMaxLanes; l++) {
         out->lane_min[l] = JMAX;
         out->lane_max[l] = JMIN;
@@ -2020,6 +2249,27 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     // qmin/qmax span the batch's accepted records; the pass stages those inside the filter
     const int64_t fq0 = std::max<int64_t>(got.qmin, flo), fq1 = std::min<int64_t>(got.qmax, fhi - 1);
     if (fq0 > fq1) return FG_OK;                                            // none inside
+    if (tiles && got.wide) {
+        // a key wider than 32 bits: the tile pass truncated it -- void. The lanes' narrow passes go
+        // into their tables, tile staging and narrow staging end for good, and the batch is staged
+        // again by the two-pass partition with 16-B records (its drops were counted by this pass)
+        rc = flush(h);
+        if (rc) return rc;
+        h->narrow = false;
+        h->keys32 = false;
+        h->tile_ok = false;
+        PassState ps2;
+        rc = ingest_launch(h, n, p.key, p.ts, p.val, vnull, flo, fhi, false, ps2);
+        if (rc) return rc;
+        rc = sync(h);
+        if (rc) return rc;
+        Counters c2{};
+        rc = ingest_finish(h, ps2, &c2);
+        const unsigned long long drops = out->drops;
+        *out = c2;
+        out->drops = drops;
+        return rc;
+    }
     if (p.narrow && got.wide) {
         // a key wider than 32 bits under narrow staging (the device plan stopped pass 2; pass 1's
         // 12-B tile records truncated it): the lanes' narrow passes go into their tables, pass 1
@@ -2111,8 +2361,8 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     p.st_rec = h->st_rec.as<int64_t>();
     p.st_null = vnull ? h->st_null.as<uint8_t>() : nullptr;
     if (h->cfg.val_type == FG_VAL_NONE) p.val = nullptr;
-    if (staged_by_plan) {
-        // (already staged by the speculative pass 2 at these positions)
+    if (staged_by_plan || tiles) {
+        // (already staged: by the speculative pass 2 at these positions, or in the pass's tiles)
     } else if (two_pass) {
         KTimer kt(h, K_PART2, n);
         HIPCHK(h, launch_part2(p, h->stream));
@@ -2124,8 +2374,12 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     s->narrow = p.narrow != 0;
     s->bits = p.region_bits;   // (a flush above may have split the regions since the count)
     s->is_acc = false;
+    s->tiles = tiles;
+    s->own = false;
+    s->busy = false;
     s->skew = out->skew;
     h->skew_seen = h->skew_seen || out->skew;
+    if (tiles && out->skew) h->tile_skew = true;
     s->refs = 0;
     for (int l = 0; l < h->lanes; l++) {
         if (out->lane_total[l] == 0) continue;
@@ -2250,13 +2504,7 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
         rc = flush_lane(h, l);
         if (rc) return rc;
     }
-    std::unique_ptr<Staged> s;
-    if (!h->pass_pool.empty()) {
-        s = std::move(h->pass_pool.back());
-        h->pass_pool.pop_back();
-    } else {
-        s.reset(new Staged());
-    }
+    std::unique_ptr<Staged> s = pass_from_pool(h);
     const int Fp = p.lanes << p.region_bits;   // the pass's buckets (the regions may split meanwhile)
     HIPCHK(h, s->bucket_off.ensure(sizeof(uint32_t) * (Fp + 1)));
     {
@@ -2296,6 +2544,8 @@ int acc_pass(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, con
     s->has_null = false;
     s->bits = p.region_bits;
     s->is_acc = true;
+    s->tiles = false;
+    s->own = false;
     s->skew = false;
     s->refs = 0;
     for (int l = 0; l < h->lanes; l++) {
@@ -2971,6 +3221,8 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_NARROW")) hp->narrow = hp->narrow && std::atoi(e) != 0;
     if (const char* e = getenv("FG_P2_SKEW_GROUP")) hp->p2_skew_group = std::max(0, std::atoi(e));
     hp->narrow_ok = hp->narrow;
+    if (const char* e = getenv("FG_TILE")) hp->tile_env = std::atoi(e) != 0;
+    hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";
         return FG_EDEVICE;
@@ -3801,6 +4053,7 @@ int fg_reset(fg_handle* h) {
     h->late_rows = 0;
     h->late_horizon = JMIN;
     h->narrow = h->narrow_ok;
+    h->tile_ok = h->tile_env;
     return FG_OK;
 }
 

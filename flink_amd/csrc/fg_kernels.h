@@ -405,6 +405,63 @@ hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t 
                               hipStream_t s);
 hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s);
 hipError_t launch_heavy_chunks(const HeavyPlan& hp, int32_t workgroups, hipStream_t s);
+// ---- tile staging: a TUMBLE window (or a local-phase slice) fired straight from pass-1 tiles ----
+// Pass 1 (k_tile_part1) sorts each tile of kTileRecs records by CONSUMER BUCKET -- (lane, region
+// >> kTileBits): 4 state regions, ~4.9k keys at 10M keys / 2^13 regions -- and writes it back in
+// place (block-laid 12-B records {int32 key, value}, absolute record index) with a directory row
+// of bucket offsets; k_tile_dirt transposes the directory into one (offset, length) column per
+// bucket. At the fire, k_tile_fire gives each bucket one workgroup: it gathers the bucket's
+// fragment of every tile, aggregates its keys in an LDS table and emits the fired rows -- the
+// staged area of pass 2 is never written nor read back (RecordsWindowBuffer.flush + AggCombiner
+// + fireWindow in one kernel). Anything else that needs the lane's records (a flush into a slice
+// table, a checkpoint, a re-fire after restore) first converts the pass into a regular staged
+// pass (k_tile_count + scan + k_tile_scatter).
+constexpr int kTileBits = 2;                  // state regions per consumer bucket = 4
+#ifndef FG_TILE_T
+#define FG_TILE_T 768
+#endif
+#ifndef FG_TILE_R
+#define FG_TILE_R 12
+#endif
+constexpr int kTileThreads = FG_TILE_T;       // tile pass 1 (170 VGPRs at 768 threads: no spills)
+constexpr int kTileR = FG_TILE_R;             // records per thread per tile (even: paired loads)
+constexpr int kTileRecs = kTileR * kTileThreads;   // records per pass-1 tile (9,216)
+constexpr int kMaxTileBuckets = 4096;         // lanes << (region_bits - kTileBits)
+constexpr int kTileSlots = 8192;              // consumer LDS table (~4.9k keys: 60 % load)
+constexpr int kTileFireThreads = 1024;
+constexpr int kTileMaxSub = 64;               // regions of one bucket at the current bits (materialize)
+
+// One tile-staged pass as the fire / materialize kernels read it (lane `lane`'s buckets)
+struct TilePass {
+    const void* rec;          // block-laid 12-B records at their absolute batch index
+    const uint32_t* dt;       // [nc][nt]: offset | length << 16 of bucket c's fragment of tile t
+    int64_t seg_per;          // records per pass-1 segment (seg_bounds); tile t = (t / mt, t % mt)
+    int32_t nt, mt;           // tiles, tiles per segment
+    int32_t nc;               // buckets of the pass (all lanes)
+    int32_t bits;             // region bits of the pass
+    int32_t lane;
+    int32_t pad;
+};
+struct TileFire {
+    MergeParams m;            // emit fields, value op, overflow / out_count / fail list, job, region_bits
+    const TilePass* passes;   // device array [n_passes], all at bits `tbits`
+    int32_t n_passes;
+    int32_t tbits;
+    // items: the lane's buckets 0 .. (1 << (tbits - kTileBits)) - 1, or (retry) regions at
+    // m.region_bits: m.retry_list[0 .. m.n_retry)
+};
+hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s);
+// directory transpose of a tile pass: dir [tiles][nc + 1] -> dt [nc][tiles] (lanes absent from
+// *lane_mask skipped)
+hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
+                            const unsigned long long* lane_mask, uint32_t* dt, hipStream_t s);
+hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s);
+// materialize: per-region counts of one tile pass's lane (hist[P] at `bits`), then -- after the
+// exclusive scan into bucket_off -- the records into a regular narrow staged area
+hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s);
+hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, const uint32_t* bucket_off, void* out_rec,
+                               hipStream_t s);
+
 constexpr int kMaxOwnerCols = 8;
 struct OwnerCols {
     int32_t ncols;

@@ -1537,9 +1537,9 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C, MV>& t, int64_t k, u
 // the accumulator {COUNT(*), NULL count, sum} (a6: Count1/Count/Sum/AvgAggFunction)
 // v: the entry's value slots (one; kNV for a multi-value operator, aggregate a reading slot
 // p.agg_slot[a]); vt: the kernel value op (its low bits the value type)
-__device__ __forceinline__ void write_row(const MergeParams& p, unsigned long long o, int64_t h,
-                                          unsigned long long cs, unsigned long long cn, const int64_t* vals, int vt) {
-    p.out_key[o] = key_of(h);   // state holds the key's mix
+__device__ __forceinline__ void write_row_k(const MergeParams& p, unsigned long long o, int64_t key,
+                                            unsigned long long cs, unsigned long long cn, const int64_t* vals, int vt) {
+    p.out_key[o] = key;
     p.out_ws[o] = p.wstart;
     p.out_we[o] = p.wend;
     if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
@@ -1572,6 +1572,10 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
         p.out_agg[a][o] = v;
     }
     p.out_null[o] = nm;
+}
+__device__ __forceinline__ void write_row(const MergeParams& p, unsigned long long o, int64_t h,
+                                          unsigned long long cs, unsigned long long cn, const int64_t* vals, int vt) {
+    write_row_k(p, o, key_of(h), cs, cn, vals, vt);   // state holds the key's mix
 }
 
 constexpr int kSrcU = 2;   // source-table entries per thread per round (1, 3, 4 measured +-2 % or slower)
@@ -2814,6 +2818,589 @@ hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, cons
     fg_launch(k_owner_scatter, dim3(kOwnerGrid), dim3(kOwnerThreads), 0, s, key, ts, val, n, key_hash, max_p,
                        par, offs, out_key, out_ts, out_val);
     fg_launch(k_owner_counts, dim3(1), dim3(kMaxOwners), 0, s, offs, par, counts);
+    return hipGetLastError();
+}
+
+
+// ----------------------------------------------------------------------------------------
+// tile staging (fg_kernels.h): pass 1 by consumer bucket, directory transpose, fire straight
+// from the tiles, and the conversion of a tile pass into a regular staged pass
+// ----------------------------------------------------------------------------------------
+// Pass 1 of a tile-staged batch: k_part1's bookkeeping (slice assignment with the late rules,
+// drops, slice range, lane totals, the 32-bit key check) and a sort of each tile by consumer
+// bucket (lane << (region_bits - kTileBits) | region >> kTileBits), written back in place as
+// block-laid 12-B records at their absolute batch index, with the tile's bucket offsets in
+// p.dir. Software-pipelined like k_part1 (the next tile's loads in flight across this tile's
+// scan, staging and write-out). *p.max_bucket: the largest bucket count of one tile (skew).
+__global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
+    constexpr int T = kTileThreads;
+    constexpr int R = kTileR;
+    constexpr int TILE = kTileRecs;
+    static_assert(R % 2 == 0, "pairs of records per thread");
+    static_assert(TILE < (1 << 20) && kMaxTileBuckets <= (1 << 12) && TILE < (1 << 16), "rank << 12 | bucket; u16 offsets");
+    __shared__ uint32_t s_k[TILE];                   // the tile, bucket sorted: keys
+    __shared__ unsigned long long s_v[TILE];         //   and value bits
+    __shared__ uint32_t s_cc[kMaxTileBuckets + 1];   // bucket counts, then offsets
+    __shared__ uint32_t s_wave[T / 64];
+    __shared__ unsigned long long s_drop;
+    __shared__ long long s_qmin, s_qmax, s_qnext;
+    __shared__ uint32_t s_mask, s_bmax;
+    __shared__ uint32_t s_lane[kMaxLanes];
+    const int NC = p.n_coarse;
+    const int tid = threadIdx.x;
+    for (int i = tid; i <= NC; i += T) s_cc[i] = 0;
+    if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; s_bmax = 0; }
+    if (tid < kMaxLanes) s_lane[tid] = 0;
+    __syncthreads();
+    int64_t beg, end;
+    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    const bool has_val = p.val != nullptr;
+    uint32_t drops = 0, mask = 0, bmax = 0;
+    uint32_t lc[kMaxLanes] = {0u, 0u, 0u, 0u};
+    bool wide = false;
+    long long qmin = JMAX, qmax = JMIN, qnext = JMAX;
+    const int lm = p.lanes - 1;
+    const int per = (NC + T - 1) / T;   // buckets per thread in the scan
+    auto li_of = [&](int u) -> int64_t { return 2 * ((int64_t)tid + (int64_t)(u >> 1) * T) + (u & 1); };
+    auto load = [&](int64_t t0, longlong2 (&k2)[R / 2], longlong2 (&t2)[R / 2], longlong2 (&v2)[R / 2]) {
+        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
+        if (tn == TILE && p.vec) {
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                const int64_t i = t0 + li_of(2 * u);
+                k2[u] = ld2(p.key + i);
+                t2[u] = ld2(p.ts + i);
+                v2[u] = has_val ? ld2(p.val + i) : make_longlong2(0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                const int64_t l0 = li_of(2 * u);
+                k2[u] = t2[u] = v2[u] = make_longlong2(0, 0);
+                if (l0 < tn) {
+                    k2[u].x = p.key[t0 + l0]; t2[u].x = p.ts[t0 + l0];
+                    if (has_val) v2[u].x = p.val[t0 + l0];
+                }
+                if (l0 + 1 < tn) {
+                    k2[u].y = p.key[t0 + l0 + 1]; t2[u].y = p.ts[t0 + l0 + 1];
+                    if (has_val) v2[u].y = p.val[t0 + l0 + 1];
+                }
+            }
+        }
+    };
+    longlong2 ka[R / 2], ta[R / 2], va[R / 2];
+    if (beg < end) load(beg, ka, ta, va);
+    int j = 0;
+    for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
+        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
+        // 1) classify + rank the tile's records by bucket (LDS atomics)
+        uint32_t rcb[R];   // (rank << 12) | bucket, 0xffffffff = not staged
+        uint32_t k32[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const int64_t li = li_of(u);
+            rcb[u] = 0xffffffffu;
+            const int64_t k = (u & 1) ? ka[u >> 1].y : ka[u >> 1].x;
+            k32[u] = (uint32_t)k;
+            if (li >= tn) continue;
+            const int64_t ts = (u & 1) ? ta[u >> 1].y : ta[u >> 1].x;
+            int64_t q, h;
+            const int b = classify(p, k, ts, &q, &h);
+            if (b >= 0) {
+                wide |= k != (int64_t)(int32_t)k;
+                qmin = q < qmin ? q : qmin;
+                qmax = q > qmax ? q : qmax;
+                mask |= 1u << ((int)q & lm);
+                const int ln = b >> p.region_bits;   // (selects: a dynamic register index would go to scratch)
+#pragma unroll
+                for (int l = 0; l < kMaxLanes; l++) lc[l] += ln == l ? 1u : 0u;
+                const uint32_t cb = (uint32_t)b >> kTileBits;
+                rcb[u] = (atomicAdd(&s_cc[cb], 1u) << 12) | cb;
+            } else if (b == -1) {
+                drops++;
+            } else {   // outside the slice filter: in the batch's slice range only
+                qmin = q < qmin ? q : qmin;
+                qmax = q > qmax ? q : qmax;
+                if (q >= p.filter_hi) qnext = q < qnext ? q : qnext;
+            }
+        }
+        int64_t rv[R];
+#pragma unroll
+        for (int u = 0; u < R; u++) rv[u] = (u & 1) ? va[u >> 1].y : va[u >> 1].x;
+        // 2) prefetch the next tile: in flight across this tile's scan, staging and write-out
+        if (t0 + TILE < end) load(t0 + TILE, ka, ta, va);
+        lds_barrier();
+        {   // exclusive scan of the tile's bucket counts (per consecutive buckets per thread)
+            constexpr int kPer = (kMaxTileBuckets + T - 1) / T;
+            uint32_t c[kPer], run = 0;
+#pragma unroll
+            for (int q = 0; q < kPer; q++) {
+                const int b = tid * per + q;
+                c[q] = (q < per && b < NC) ? s_cc[b] : 0u;
+                run += c[q];
+                bmax = c[q] > bmax ? c[q] : bmax;
+            }
+            uint32_t total;
+            uint32_t ex = block_exclusive_scan_t<true>(run, s_wave, &total);
+#pragma unroll
+            for (int q = 0; q < kPer; q++) {
+                const int b = tid * per + q;
+                if (q < per && b < NC) s_cc[b] = ex;
+                ex += c[q];
+            }
+            if (tid == 0) s_cc[NC] = total;
+        }
+        lds_barrier();
+        uint16_t* drow = p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * (NC + 1);
+        for (int c = tid; c <= NC; c += T) drow[c] = (uint16_t)s_cc[c];
+        const uint32_t tile_total = s_cc[NC];
+        // 3) stage the tile bucket sorted, then write it back in place
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if (rcb[u] == 0xffffffffu) continue;
+            const uint32_t slot = s_cc[rcb[u] & 4095u] + (rcb[u] >> 12);
+            s_k[slot] = k32[u];
+            s_v[slot] = (unsigned long long)rv[u];
+        }
+        lds_barrier();
+        for (uint32_t i = tid; i < tile_total; i += T) st_rec12(p.tmp, (uint64_t)(t0 + i), (int64_t)s_k[i], (int64_t)s_v[i]);
+        lds_barrier();   // staging and the directory row have read the offsets
+        for (int c = tid; c <= NC; c += T) s_cc[c] = 0;
+        lds_barrier();
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        drops += __shfl_down(drops, off);
+        mask |= __shfl_down(mask, off);
+        const uint32_t bm = __shfl_down(bmax, off);
+        bmax = bm > bmax ? bm : bmax;
+#pragma unroll
+        for (int l = 0; l < kMaxLanes; l++) lc[l] += __shfl_down(lc[l], off);
+        const long long oa = __shfl_down(qmin, off), oz = __shfl_down(qmax, off), on = __shfl_down(qnext, off);
+        qmin = oa < qmin ? oa : qmin;
+        qmax = oz > qmax ? oz : qmax;
+        qnext = on < qnext ? on : qnext;
+    }
+    if ((tid & 63) == 0) {
+        if (drops) atomicAdd(&s_drop, (unsigned long long)drops);
+        if (mask) atomicOr(&s_mask, mask);
+        if (bmax) atomicMax(&s_bmax, bmax);
+#pragma unroll
+        for (int l = 0; l < kMaxLanes; l++)
+            if (lc[l]) atomicAdd(&s_lane[l], lc[l]);
+        if (qmin != JMAX) atomicMin(&s_qmin, qmin);
+        if (qmax != JMIN) atomicMax(&s_qmax, qmax);
+        if (qnext != JMAX) atomicMin(&s_qnext, qnext);
+    }
+    if (p.wide && __ballot(wide) != 0 && (tid & 63) == 0) atomicOr(p.wide, 1u);
+    __syncthreads();
+    if (tid < p.lanes && s_lane[tid]) atomicAdd(&p.lane_total[tid], (unsigned long long)s_lane[tid]);
+    if (tid == 0) {
+        if (p.count_drops && s_drop) atomicAdd(p.drops, s_drop);
+        if (s_mask) atomicOr(p.lane_mask, (unsigned long long)s_mask);
+        if (s_bmax && p.max_bucket) atomicMax(p.max_bucket, s_bmax);
+        if (s_qmin != JMAX) atomicMin(p.qmin, s_qmin);
+        if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
+        if (s_qnext != JMAX) atomicMin(p.qnext, s_qnext);
+    }
+}
+
+hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
+    if (p.n_coarse < 1 || p.n_coarse > kMaxTileBuckets || p.region_bits < kTileBits || !p.tmp || !p.dir ||
+        p.vnull != nullptr)
+        return hipErrorInvalidValue;
+    fg_launch(k_tile_part1, dim3(p.grid), dim3(kTileThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+// dir [tiles][nc + 1] (u16 offsets) -> dt [nc][tiles] = offset | length << 16, 64 x 64 blocks
+// through LDS; buckets of lanes without records (lane_mask) are skipped
+__global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t NT, int32_t NC, int32_t lshift,
+                                                   const unsigned long long* lane_mask, uint32_t* dt) {
+    __shared__ uint16_t s[64][66];
+    const int tb = blockIdx.x * 64, cb = blockIdx.y * 64;
+    const unsigned long long lm = *gbl(lane_mask);
+    const int l0 = cb >> lshift, l1 = (cb + 63 < NC ? cb + 63 : NC - 1) >> lshift;
+    bool any = false;
+    for (int l = l0; l <= l1; l++) any = any || ((lm >> l) & 1);
+    if (!any) return;
+    for (int i = threadIdx.x; i < 64 * 65; i += 256) {
+        const int tt = i / 65, cc = i % 65;
+        const int t = tb + tt, c = cb + cc;
+        s[tt][cc] = (t < NT && c <= NC) ? gbl(dir)[(int64_t)t * (NC + 1) + c] : (uint16_t)0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        const int cc = i / 64, tt = i % 64;
+        const int t = tb + tt, c = cb + cc;
+        if (t < NT && c < NC && ((lm >> (c >> lshift)) & 1)) {
+            const uint32_t a = s[tt][cc], b = s[tt][cc + 1];
+            dt[(int64_t)c * NT + t] = a | ((b - a) << 16);
+        }
+    }
+}
+
+hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
+                            const unsigned long long* lane_mask, uint32_t* dt, hipStream_t s) {
+    if (tiles <= 0 || nc <= 0) return hipSuccess;
+    fg_launch(k_tile_dirt, dim3((unsigned)((tiles + 63) / 64), (unsigned)((nc + 63) / 64)), dim3(256), 0, s, dir,
+              tiles, nc, lane_shift, lane_mask, dt);
+    return hipGetLastError();
+}
+
+// Order a wave's LDS writes before its other lanes' reads (wave-private scratch, no barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// A wave's walk over the fragments of one bucket (column `col` of a tile pass): groups of 64
+// tiles (one per lane, this wave's every W-th group), each cut into windows of up to kTileWin
+// records; next() fills the window's records (up to kTileWin / 64 per lane, loads in flight on
+// return) -- a wave-private map from a window position to its fragment (the fragments mark
+// their first position, an inclusive max-scan fills the map) gives each record its source.
+constexpr int kTileWin = 256;
+constexpr int kTileRpl = kTileWin / 64;
+struct TileWalk {
+    const uint32_t* col;
+    const void* rec;
+    int64_t seg_per;
+    int32_t nt, mt;
+    int32_t t0, stride;         // current group's first tile, groups' stride
+    uint32_t xn;                // the next group's directory entry (prefetched)
+    uint32_t g_len, g_st, g_tot, b;
+};
+__device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp, int32_t cb, int wave, int W,
+                                                int lane) {
+    w.col = tp.dt + (int64_t)cb * tp.nt;
+    w.rec = tp.rec;
+    w.seg_per = tp.seg_per;
+    w.nt = tp.nt;
+    w.mt = tp.mt;
+    w.stride = W * 64;
+    w.t0 = wave * 64 - w.stride;
+    const int t = wave * 64 + lane;
+    w.xn = t < w.nt ? gbl(w.col)[t] : 0u;
+    w.g_len = w.g_st = w.g_tot = w.b = 0;
+}
+// the next window of the walk: records in kr / vr (lanes past nrec hold key 0), false when done
+__device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_t* dl, int lane,
+                                               int32_t (&kr)[kTileRpl], int64_t (&vr)[kTileRpl], uint32_t& nrec) {
+    while (w.b >= w.g_tot) {   // the next group with records
+        w.t0 += w.stride;
+        if (w.t0 >= w.nt) return false;
+        const int t = w.t0 + lane;
+        const uint32_t x = w.xn;
+        w.xn = t + w.stride < w.nt ? gbl(w.col)[t + w.stride] : 0u;
+        w.g_len = x >> 16;
+        const uint32_t base = (uint32_t)(w.seg_per * (t / w.mt) + (int64_t)(t % w.mt) * kTileRecs) + (x & 0xffffu);
+        uint32_t inc = w.g_len;
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint32_t y = __shfl_up(inc, s);
+            if (lane >= s) inc += y;
+        }
+        w.g_st = inc - w.g_len;
+        w.g_tot = __shfl(inc, 63);
+        w.b = 0;
+        wave_lds_sync();   // (the last window's reads of dl are done: its loads were issued)
+        dl[lane] = base - w.g_st;
+    }
+#pragma unroll
+    for (int q = 0; q < kTileRpl; q++) fm[lane * kTileRpl + q] = 0;
+    wave_lds_sync();
+    if (w.g_len > 0 && w.g_st < w.b + kTileWin && w.g_st + w.g_len > w.b) fm[w.g_st > w.b ? w.g_st - w.b : 0] = (uint8_t)lane;
+    wave_lds_sync();
+    uint32_t e[kTileRpl];
+#pragma unroll
+    for (int q = 0; q < kTileRpl; q++) e[q] = fm[lane * kTileRpl + q];
+#pragma unroll
+    for (int q = 1; q < kTileRpl; q++) e[q] = e[q] > e[q - 1] ? e[q] : e[q - 1];
+    uint32_t m = e[kTileRpl - 1];
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t y = __shfl_up(m, s);
+        if (lane >= s) m = m > y ? m : y;
+    }
+    uint32_t pre = __shfl_up(m, 1);
+    if (lane == 0) pre = 0;
+#pragma unroll
+    for (int q = 0; q < kTileRpl; q++) fm[lane * kTileRpl + q] = (uint8_t)(e[q] > pre ? e[q] : pre);
+    wave_lds_sync();
+    nrec = w.g_tot - w.b < (uint32_t)kTileWin ? w.g_tot - w.b : (uint32_t)kTileWin;
+#pragma unroll
+    for (int u = 0; u < kTileRpl; u++) {
+        const uint32_t jr = lane + 64 * u;
+        kr[u] = 0;
+        vr[u] = 0;
+        if (jr < nrec) {
+            const uint32_t src = dl[fm[jr]] + w.b + jr;
+            const Rec12 r = ld_rec12(w.rec, (uint64_t)src);
+            kr[u] = (int32_t)r.k;
+            vr[u] = rec12_val(r);
+        }
+    }
+    w.b += kTileWin;
+    return true;
+}
+
+// Fire from tile passes: one workgroup per item -- a bucket of the lane (4 << (bits - tbits)
+// regions at the current bits), or on a retry one region (its bucket's records filtered by the
+// key's region) -- gathers the item's records from every pass, aggregates them in an LDS table
+// of kTileSlots 32-bit keys (COUNT(*) u32, one value slot; the home bucket of 4 slots from a
+// 32-bit multiplicative hash) and emits one row per key (a6 arithmetic: write_row_k). Two
+// windows in flight per wave: the next window's loads are issued before this one's inserts. A
+// full table emits nothing and lists the item's regions in the fail list (the host splits the
+// regions and redoes them one region per item, MergeParams fail protocol).
+template <int VTC>
+__global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
+    constexpr int T = kTileFireThreads, W = T / 64, S = kTileSlots;
+    constexpr int kRounds = S / T + 1;   // + 1: the sentinel slot (thread 0)
+    static_assert(S % T == 0 && (S & (S - 1)) == 0, "table rounds");
+    __shared__ int32_t t_key[S + 1];            // slot S: the key INT32_MIN (the empty sentinel)
+    __shared__ uint32_t t_cs[S + 1];
+    __shared__ unsigned long long t_v[S + 1];
+    __shared__ uint8_t s_fm[W][kTileWin];
+    __shared__ uint32_t s_dl[W][64];
+    __shared__ uint32_t s_grp[kRounds * W];
+    __shared__ uint16_t s_map[S + 1];
+    __shared__ unsigned int s_flags;
+    __shared__ uint32_t s_total;
+    __shared__ unsigned long long s_out_base;
+    const MergeParams& p = f.m;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int vt = VTC >= 0 ? VTC : p.val_type;
+    const int64_t vinit = lds_repr(vt, val_identity(vt));
+    const int sub = p.region_bits - f.tbits;          // current region bits above the passes'
+    const bool retry = p.retry_list != nullptr;
+    const int NI = retry ? p.n_retry : 1 << (f.tbits - kTileBits);
+    const int G = gridDim.x;
+    const bool xcd = !retry && G % 8 == 0;            // consecutive buckets on one XCD (shared L2 lines)
+    for (int k = 0;; k++) {
+        const int b = (int)blockIdx.x;
+        const int x = xcd ? k * G + (b % 8) * (G / 8) + b / 8 : b + k * G;
+        if (k * G >= NI) break;
+        const bool live = x < NI;
+        int r_lo = 0, r_hi = 0, item = 0;
+        if (live) {
+            if (retry) {
+                r_lo = gbl(p.retry_list)[x];
+                r_hi = r_lo + 1;
+                item = r_lo >> (sub + kTileBits);
+            } else {
+                item = x;
+                r_lo = x << (sub + kTileBits);
+                r_hi = (x + 1) << (sub + kTileBits);
+            }
+        }
+        for (int i = tid; i <= S; i += T) {
+            t_key[i] = kEmpty32;
+            t_cs[i] = 0;
+            t_v[i] = (unsigned long long)vinit;
+        }
+        if (tid == 0) s_flags = 0;
+        __syncthreads();
+        bool full = false;
+        if (live) {
+            auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+                uint32_t hm[kTileRpl];
+                int4 bq[kTileRpl];
+#pragma unroll
+                for (int u = 0; u < kTileRpl; u++) {   // every home bucket read first, then resolved
+                    hm[u] = __umulhi((uint32_t)kr[u] * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
+                    bq[u] = *reinterpret_cast<const int4*>(&t_key[hm[u]]);
+                }
+#pragma unroll
+                for (int u = 0; u < kTileRpl; u++) {
+                    if (lane + 64 * u >= nrec) continue;
+                    const int32_t key = kr[u];
+                    if (retry && (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) != r_lo) continue;
+                    int sl = -1;
+                    if (key == kEmpty32) {
+                        sl = S;
+                    } else {
+                        uint32_t home = hm[u];
+                        int4 q4 = bq[u];
+                        for (int probe = 0; probe < S / 4; probe++) {
+                            const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
+                            int hit = -1, emp = -1;
+#pragma unroll
+                            for (int z = 3; z >= 0; z--) {
+                                if (qq[z] == key) hit = z;
+                                if (qq[z] == kEmpty32) emp = z;
+                            }
+                            if (hit >= 0 && (emp < 0 || hit < emp)) {
+                                sl = (int)home + hit;
+                                break;
+                            }
+                            if (emp >= 0) {
+                                const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
+                                if (old == kEmpty32 || old == key) {
+                                    sl = (int)home + emp;
+                                    break;
+                                }
+                            } else {
+                                home = (home + 4) & (S - 1);
+                            }
+                            q4 = *reinterpret_cast<const int4*>(&t_key[home]);
+                        }
+                    }
+                    if (sl < 0) {
+                        full = true;
+                        continue;
+                    }
+                    atomicAdd(&t_cs[sl], 1u);
+                    lds_val(&t_v[sl], vr[u], vt, true);
+                }
+            };
+            for (int pi = 0; pi < f.n_passes; pi++) {
+                const TilePass tp = f.passes[pi];
+                TileWalk w;
+                tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane);
+                int32_t ka[kTileRpl], kb[kTileRpl];
+                int64_t va[kTileRpl], vb[kTileRpl];
+                uint32_t na = 0, nb = 0;
+                bool more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
+                while (more) {   // (buffer roles static: the loop is unrolled by two)
+                    const bool hb = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kb, vb, nb);
+                    insert(ka, va, na);
+                    if (!hb) break;
+                    more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
+                    insert(kb, vb, nb);
+                }
+            }
+        }
+        if (full) atomicOr(&s_flags, 4u);
+        __syncthreads();
+        // compaction: the occupied slots' ranks (round k covers slots [k*T, (k+1)*T); the last
+        // round the sentinel slot), a dense rank -> slot map, then one row per lane
+        uint32_t occ_mask = 0;
+#pragma unroll
+        for (int r = 0; r < kRounds; r++) {
+            const int slot = r < kRounds - 1 ? r * T + tid : S;
+            const bool occ = (r < kRounds - 1 || tid == 0) && t_cs[slot] != 0;
+            const uint64_t bal = __ballot(occ);
+            if (occ) occ_mask |= 1u << r;
+            if (lane == 0) s_grp[r * W + wave] = (uint32_t)__popcll(bal);
+        }
+        __syncthreads();
+        if (wave == 0) {
+            constexpr int NG = kRounds * W;
+            constexpr int GPL = (NG + 63) / 64;   // groups per lane
+            uint32_t gv[GPL], xs = 0;
+#pragma unroll
+            for (int q = 0; q < GPL; q++) {
+                gv[q] = GPL * lane + q < NG ? s_grp[GPL * lane + q] : 0u;
+                xs += gv[q];
+            }
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(xs, off);
+                if (lane >= off) xs += y;
+            }
+            uint32_t ex = xs;
+#pragma unroll
+            for (int q = 0; q < GPL; q++) ex -= gv[q];
+#pragma unroll
+            for (int q = 0; q < GPL; q++) {
+                if (GPL * lane + q < NG) s_grp[GPL * lane + q] = ex;
+                ex += gv[q];
+            }
+            const uint32_t total = __shfl(xs, 63);
+            if (lane == 0) {
+                unsigned int fl = s_flags;
+                if (live && !(fl & 4u)) {
+                    const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
+                    s_out_base = ob;
+                    if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
+                }
+                s_flags = fl;
+                s_total = total;
+                if (fl) atomicOr(p.overflow, fl);
+                if (live && (fl & 4u) && p.fail_list) {   // the item does nothing; the host redoes its regions
+                    const uint32_t nr = (uint32_t)(r_hi - r_lo);
+                    const uint32_t at = atomicAdd(p.fail_n, nr);
+                    for (uint32_t q = 0; q < nr; q++)
+                        if (at + q < (uint32_t)p.fail_cap)
+                            p.fail_list[at + q] = ((uint32_t)p.job << kFailJobShift) | (uint32_t)(r_lo + (int)q);
+                }
+            }
+        }
+        __syncthreads();
+        const unsigned int fl = s_flags;
+#pragma unroll
+        for (int r = 0; r < kRounds; r++) {
+            const bool occ = (occ_mask >> r) & 1;
+            const uint64_t bal = __ballot(occ);
+            if (occ) s_map[s_grp[r * W + wave] + (uint32_t)__popcll(bal & ((1ull << lane) - 1))] =
+                (uint16_t)(r < kRounds - 1 ? r * T + tid : S);
+        }
+        __syncthreads();
+        if (live && !(fl & 6u)) {
+            const uint32_t total = s_total;
+            const unsigned long long ob = s_out_base;
+            for (uint32_t i = tid; i < total; i += T) {
+                const int sl = s_map[i];
+                const int64_t v = lds_repr(vt, (int64_t)t_v[sl]);
+                write_row_k(p, ob + i, sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl], t_cs[sl], 0ull, &v, vt);
+            }
+        }
+        __syncthreads();   // the table is cleared for the next item
+    }
+}
+
+hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s) {
+    if (f.n_passes < 1 || f.tbits < kTileBits || f.m.region_bits < f.tbits || f.m.mv) return hipErrorInvalidValue;
+    const dim3 g((unsigned)workgroups), b(kTileFireThreads);
+    switch (f.m.val_type) {   // the value op compiled in: SUM / AVG over DOUBLE, BIGINT, or COUNT only
+        case 2: fg_launch(k_tile_fire<2>, g, b, 0, s, f); break;
+        case 1: fg_launch(k_tile_fire<1>, g, b, 0, s, f); break;
+        case 0: fg_launch(k_tile_fire<0>, g, b, 0, s, f); break;
+        default: fg_launch(k_tile_fire<-1>, g, b, 0, s, f); break;
+    }
+    return hipGetLastError();
+}
+
+// Materialize a tile pass's lane into a regular narrow staged pass: per bucket (workgroup) the
+// records' regions at `bits` are counted (hist[region]), and after the exclusive scan into
+// bucket_off written at bucket_off[region] + their rank (order inside a region is immaterial)
+constexpr int kTileMatThreads = 256;
+template <bool SCATTER>
+__global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32_t bits, uint32_t* hist,
+                                                              const uint32_t* bucket_off, void* out) {
+    __shared__ uint32_t s_c[kTileMaxSub];
+    const int item = blockIdx.x;
+    const int sub = bits - tp.bits;
+    const int nsub = kTileBits + sub <= 6 ? 1 << (kTileBits + sub) : kTileMaxSub;
+    const int r_lo = item << (kTileBits + sub);
+    const int tid = threadIdx.x;
+    if (tid < nsub) s_c[tid] = SCATTER ? gbl(bucket_off)[r_lo + tid] : 0u;
+    __syncthreads();
+    const uint32_t* col = tp.dt + (int64_t)((tp.lane << (tp.bits - kTileBits)) | item) * tp.nt;
+    for (int t = tid; t < tp.nt; t += kTileMatThreads) {
+        const uint32_t x = gbl(col)[t];
+        const uint32_t len = x >> 16;
+        if (!len) continue;
+        const uint64_t base = (uint64_t)(tp.seg_per * (t / tp.mt) + (int64_t)(t % tp.mt) * kTileRecs) + (x & 0xffffu);
+        for (uint32_t i = 0; i < len; i++) {
+            const Rec12 r = ld_rec12(tp.rec, base + i);
+            const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
+            const uint32_t pos = atomicAdd(&s_c[region - r_lo], 1u);
+            if (SCATTER) st_rec12(out, pos, (int64_t)(int32_t)r.k, rec12_val(r));
+        }
+    }
+    __syncthreads();
+    if (!SCATTER && tid < nsub) hist[r_lo + tid] = s_c[tid];
+}
+
+hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s) {
+    if (bits - tp.bits + kTileBits > 6) return hipErrorInvalidValue;   // (kTileMaxSub regions per bucket)
+    fg_launch(k_tile_mat<false>, dim3(1u << (tp.bits - kTileBits)), dim3(kTileMatThreads), 0, s, tp, bits, hist,
+              (const uint32_t*)nullptr, (void*)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, const uint32_t* bucket_off, void* out_rec,
+                               hipStream_t s) {
+    if (bits - tp.bits + kTileBits > 6) return hipErrorInvalidValue;
+    fg_launch(k_tile_mat<true>, dim3(1u << (tp.bits - kTileBits)), dim3(kTileMatThreads), 0, s, tp, bits,
+              (uint32_t*)nullptr, bucket_off, out_rec);
     return hipGetLastError();
 }
 

@@ -40,7 +40,13 @@ constexpr int TC = 1024;               // consumer threads
 #define SLOTS 8192
 #endif
 constexpr int S = SLOTS;               // LDS table slots
+#ifndef WIN
+#define WIN 256                        // consumer: records per wave window (WIN / 64 per lane)
+#endif
 constexpr int kBlk = 768;              // 64 narrow records: 64 int32 keys, then 64 values
+#ifndef PACKED
+#define PACKED 1                       // 1: packed 12-B records {key, value lo, value hi}; 0: block-laid
+#endif
 
 __host__ __device__ inline uint64_t fmix64(uint64_t h) {
     h ^= h >> 33;
@@ -82,8 +88,13 @@ __device__ inline void st12(char* base, uint64_t i, uint32_t k, uint64_t v) {
 // ---- pass 1: tile sort by consumer bucket ------------------------------------------------
 __global__ __launch_bounds__(T1) void k_p1(int64_t n, const int64_t* key, const int64_t* ts, const double* val,
                                           char* tmp, uint16_t* dir, int MT) {
+#if PACKED
+    __shared__ uint4 s_w4[(TILE * 3 + 3) / 4];       // the sorted tile as packed 12-B records
+    uint32_t* s_w = reinterpret_cast<uint32_t*>(s_w4);
+#else
     __shared__ uint32_t s_k[TILE];
     __shared__ uint64_t s_v[TILE];
+#endif
     __shared__ uint32_t s_cc[NC + 1];
     __shared__ uint32_t s_wave[T1 / 64];
     const int tid = threadIdx.x;
@@ -146,11 +157,25 @@ __global__ __launch_bounds__(T1) void k_p1(int64_t n, const int64_t* key, const 
         for (int u = 0; u < R1; u++) {
             if (rc[u] == 0xffffffffu) continue;
             const uint32_t slot = s_cc[rc[u] & 2047u] + (rc[u] >> 11);
+#if PACKED
+            s_w[3 * slot] = k32[u];
+            s_w[3 * slot + 1] = (uint32_t)v64[u];
+            s_w[3 * slot + 2] = (uint32_t)(v64[u] >> 32);
+#else
             s_k[slot] = k32[u];
             s_v[slot] = v64[u];
+#endif
         }
         __syncthreads();
+#if PACKED
+        {   // the tile's bytes as aligned 16-B stores (12 * t0 is 16-B aligned: TILE % 4 == 0)
+            uint4* dst = reinterpret_cast<uint4*>(tmp + 12 * (uint64_t)t0);
+            const uint32_t nch = (total * 12 + 15) / 16;
+            for (uint32_t i = tid; i < nch; i += T1) dst[i] = s_w4[i];
+        }
+#else
         for (uint32_t i = tid; i < total; i += T1) st12(tmp, (uint64_t)(t0 + i), s_k[i], s_v[i]);
+#endif
         __syncthreads();
         for (int c = tid; c <= NC; c += T1) s_cc[c] = 0;
         __syncthreads();
@@ -191,11 +216,11 @@ __device__ inline void wave_sync() {
 }
 
 __global__ __launch_bounds__(TC) void k_tm(int64_t n, const char* tmp, const uint32_t* dt, int NT, int MT, Out o,
-                                          int64_t ws, int64_t we) {
+                                          int64_t ws, int64_t we, int mode) {
     __shared__ int32_t t_key[S];
     __shared__ uint32_t t_cs[S];
     __shared__ double t_v[S];
-    __shared__ uint8_t s_fm[TC / 64][512];           // per-wave fragment map (u8 lane ids)
+    __shared__ uint8_t s_fm[TC / 64][WIN];           // per-wave fragment map (u8 lane ids)
     __shared__ uint32_t s_dl[TC / 64][64];           // per-wave fragment delta (src - idx)
     __shared__ uint32_t s_grp[(S / TC + 1) * (TC / 64)];
     __shared__ uint16_t s_map[S];
@@ -219,77 +244,140 @@ __global__ __launch_bounds__(TC) void k_tm(int64_t n, const char* tmp, const uin
         }
         __syncthreads();
         const uint32_t* col = dt + (int64_t)c * NT;
-        for (int t0 = wave * 64; t0 < NT; t0 += W * 64) {
-            const int t = t0 + lane;
-            const uint32_t x = t < NT ? col[t] : 0u;
-            const uint32_t off = x & 0xffffu, len = x >> 16;
-            const int g = t / MT, jj = t % MT;
-            const uint32_t base = (uint32_t)(per1 * g + (int64_t)jj * TILE) + off;
-            uint32_t inc = len;
-            for (int s = 1; s < 64; s <<= 1) {
-                const uint32_t y = __shfl_up(inc, s);
-                if (lane >= s) inc += y;
+        constexpr int RPL = WIN / 64;   // records per lane per window
+        // home bucket: a multiplicative 32-bit hash of the key (keys of one consumer share the
+        // top bits of their fmix64 mix, not of the key itself)
+        auto home_of = [&](int32_t k) -> uint32_t {
+            return __umulhi((uint32_t)k * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
+        };
+        auto resolve = [&](int32_t k, uint32_t home, int4 q4) -> int {
+            for (int probe = 0; probe < S / 4; probe++) {
+                const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
+                int hit = -1, emp = -1;
+#pragma unroll
+                for (int z = 3; z >= 0; z--) {
+                    if (qq[z] == k) hit = z;
+                    if (qq[z] == kEmpty) emp = z;
+                }
+                if (hit >= 0 && (emp < 0 || hit < emp)) return home + hit;
+                if (emp >= 0) {
+                    const int old = atomicCAS(&t_key[home + emp], kEmpty, k);
+                    if (old == kEmpty || old == k) return home + emp;
+                } else {
+                    home = (home + 4) & (S - 1);
+                }
+                q4 = *reinterpret_cast<const int4*>(&t_key[home]);
             }
-            const uint32_t st = inc - len, tot = __shfl(inc, 63);
-            wave_sync();   // (the previous group's reads of s_dl are done)
-            s_dl[wave][lane] = base - st;
-            for (uint32_t b = 0; b < tot; b += 512) {
-#pragma unroll
-                for (int q = 0; q < 8; q++) s_fm[wave][lane * 8 + q] = 0;
-                wave_sync();
-                if (len > 0 && st < b + 512 && st + len > b) s_fm[wave][st > b ? st - b : 0] = (uint8_t)lane;
-                wave_sync();
-                uint32_t e[8];
-#pragma unroll
-                for (int q = 0; q < 8; q++) e[q] = s_fm[wave][lane * 8 + q];
-#pragma unroll
-                for (int q = 1; q < 8; q++) e[q] = e[q] > e[q - 1] ? e[q] : e[q - 1];
-                uint32_t m = e[7];
+            return -1;
+        };
+        // window iterator over this wave's groups of 64 tiles (group gi: tiles t0 .. t0 + 63,
+        // t0 = (wave + gi * W) * 64); a window = up to WIN consecutive records of a group
+        int t0 = wave * 64 - W * 64;   // (advanced to the first group below)
+        uint32_t xn = wave * 64 + lane < NT ? col[wave * 64 + lane] : 0u;   // next group's entry, prefetched
+        uint32_t g_len = 0, g_st = 0, g_tot = 0, b = 0;
+        auto next_window = [&](int32_t (&kr)[RPL], double (&vr)[RPL], uint32_t& nrec) -> bool {
+            while (b >= g_tot) {   // the next non-empty group
+                t0 += W * 64;
+                if (t0 >= NT) return false;
+                const int t = t0 + lane;
+                const uint32_t x = xn;
+                xn = t + W * 64 < NT ? col[t + W * 64] : 0u;
+                const uint32_t off = x & 0xffffu;
+                g_len = x >> 16;
+                const int g = t / MT, jj = t % MT;
+                const uint32_t base = (uint32_t)(per1 * g + (int64_t)jj * TILE) + off;
+                uint32_t inc = g_len;
                 for (int s = 1; s < 64; s <<= 1) {
-                    const uint32_t y = __shfl_up(m, s);
-                    if (lane >= s) m = m > y ? m : y;
+                    const uint32_t y = __shfl_up(inc, s);
+                    if (lane >= s) inc += y;
                 }
-                uint32_t pre = __shfl_up(m, 1);
-                if (lane == 0) pre = 0;
+                g_st = inc - g_len;
+                g_tot = __shfl(inc, 63);
+                b = 0;
+                wave_sync();   // (the previous group's reads of s_dl are done: its loads are issued)
+                s_dl[wave][lane] = base - g_st;
+            }
 #pragma unroll
-                for (int q = 0; q < 8; q++) s_fm[wave][lane * 8 + q] = (uint8_t)(e[q] > pre ? e[q] : pre);
-                wave_sync();
-                const uint32_t nrec = tot - b < 512 ? tot - b : 512;
-#pragma unroll 2
-                for (uint32_t jr = lane; jr < nrec; jr += 64) {
-                    const uint32_t idx = b + jr;
-                    const uint32_t f = s_fm[wave][jr];
-                    const uint32_t src = s_dl[wave][f] + idx;
-                    const char* blk = tmp + (uint64_t)(src >> 6) * kBlk;
-                    const int32_t k = reinterpret_cast<const int32_t*>(blk)[src & 63];
-                    const double v = reinterpret_cast<const double*>(blk + 256)[src & 63];
-                    // narrow table: home bucket of 4 slots from the key's mix
-                    const uint64_t h = fmix64((uint64_t)(int64_t)k);
-                    uint32_t home = __umulhi((uint32_t)h, (uint32_t)(S / 4)) * 4;
-                    int sl = -1;
-                    for (int probe = 0; probe < S / 4 && sl < 0; probe++) {
-                        const int4 q4 = *reinterpret_cast<const int4*>(&t_key[home]);
-                        const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
-                        int hit = -1, emp = -1;
+            for (int q = 0; q < RPL; q++) s_fm[wave][lane * RPL + q] = 0;
+            wave_sync();
+            if (g_len > 0 && g_st < b + WIN && g_st + g_len > b) s_fm[wave][g_st > b ? g_st - b : 0] = (uint8_t)lane;
+            wave_sync();
+            uint32_t e[RPL];
 #pragma unroll
-                        for (int z = 3; z >= 0; z--) {
-                            if (qq[z] == k) hit = z;
-                            if (qq[z] == kEmpty) emp = z;
-                        }
-                        if (hit >= 0 && (emp < 0 || hit < emp)) {
-                            sl = home + hit;
-                        } else if (emp >= 0) {
-                            const int old = atomicCAS(&t_key[home + emp], kEmpty, k);
-                            if (old == kEmpty || old == k) sl = home + emp;
-                            // (lost CAS: re-read the bucket)
-                        } else {
-                            home = (home + 4) & (S - 1);
-                        }
+            for (int q = 0; q < RPL; q++) e[q] = s_fm[wave][lane * RPL + q];
+#pragma unroll
+            for (int q = 1; q < RPL; q++) e[q] = e[q] > e[q - 1] ? e[q] : e[q - 1];
+            uint32_t m = e[RPL - 1];
+            for (int s = 1; s < 64; s <<= 1) {
+                const uint32_t y = __shfl_up(m, s);
+                if (lane >= s) m = m > y ? m : y;
+            }
+            uint32_t pre = __shfl_up(m, 1);
+            if (lane == 0) pre = 0;
+#pragma unroll
+            for (int q = 0; q < RPL; q++) s_fm[wave][lane * RPL + q] = (uint8_t)(e[q] > pre ? e[q] : pre);
+            wave_sync();
+            nrec = g_tot - b < WIN ? g_tot - b : WIN;
+#pragma unroll
+            for (int u = 0; u < RPL; u++) {
+                const uint32_t jr = lane + 64 * u;
+                kr[u] = 0;
+                vr[u] = 0;
+                if (jr < nrec) {
+                    const uint32_t src = s_dl[wave][s_fm[wave][jr]] + b + jr;
+                    if (mode & 2) {   // (diagnostic: no gather; <= 4,096 keys per consumer)
+                        kr[u] = (int32_t)(c * 4096 + (src & 4095));
+                        vr[u] = 1.0;
+                    } else {
+#if PACKED
+                        const uint3 w = *reinterpret_cast<const uint3*>(tmp + 12 * (uint64_t)src);
+                        kr[u] = (int32_t)w.x;
+                        vr[u] = __longlong_as_double((long long)(((uint64_t)w.z << 32) | w.y));
+#else
+                        const char* blk = tmp + (uint64_t)(src >> 6) * kBlk;
+                        kr[u] = reinterpret_cast<const int32_t*>(blk)[src & 63];
+                        vr[u] = reinterpret_cast<const double*>(blk + 256)[src & 63];
+#endif
                     }
-                    atomicAdd(&t_cs[sl], 1u);
-                    atomicAdd(&t_v[sl], v);
                 }
-                wave_sync();
+            }
+            b += WIN;
+            return true;
+        };
+        auto insert_window = [&](const int32_t (&kr)[RPL], const double (&vr)[RPL], uint32_t nrec) {
+            if (mode & 1) {
+#pragma unroll
+                for (int u = 0; u < RPL; u++)
+                    if (lane + 64 * u < nrec && vr[u] == -1.0 && kr[u] == 7) o.count[1] = 1;
+                return;
+            }
+            // every home bucket read first (RPL 16-B LDS reads in flight), then resolved
+            uint32_t hm[RPL];
+            int4 bq[RPL];
+#pragma unroll
+            for (int u = 0; u < RPL; u++) {
+                hm[u] = home_of(kr[u]);
+                bq[u] = *reinterpret_cast<const int4*>(&t_key[hm[u]]);
+            }
+#pragma unroll
+            for (int u = 0; u < RPL; u++) {
+                if (lane + 64 * u >= nrec) continue;
+                const int sl = resolve(kr[u], hm[u], bq[u]);
+                atomicAdd(&t_cs[sl], 1u);
+                atomicAdd(&t_v[sl], vr[u]);
+            }
+        };
+        {   // two windows in flight: the next window's loads are issued before this one's inserts
+            int32_t ka[RPL], kb[RPL];
+            double va[RPL], vb[RPL];
+            uint32_t na = 0, nb = 0;
+            bool more = next_window(ka, va, na);
+            while (more) {
+                const bool hb = next_window(kb, vb, nb);
+                insert_window(ka, va, na);
+                if (!hb) break;
+                more = next_window(ka, va, na);
+                insert_window(kb, vb, nb);
             }
         }
         __syncthreads();
@@ -368,6 +456,7 @@ int main(int argc, char** argv) {
     const int64_t n = argc > 1 ? atoll(argv[1]) : 100000000;
     const int64_t K = argc > 2 ? atoll(argv[2]) : 10000000;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const int mode = argc > 4 ? atoi(argv[4]) : 0;
     int64_t *key, *ts;
     double* val;
     CK(hipMalloc(&key, 8 * n));
@@ -381,7 +470,7 @@ int main(int argc, char** argv) {
     char* tmp;
     uint16_t* dir;
     uint32_t* dt;
-    CK(hipMalloc(&tmp, (size_t)(n / 64 + 2) * kBlk));
+    CK(hipMalloc(&tmp, (size_t)(n / 64 + 2) * kBlk + 64));
     CK(hipMalloc(&dir, (size_t)NT * (NC + 1) * 2));
     CK(hipMalloc(&dt, (size_t)NT * NC * 4));
     CK(hipMemset(dir, 0, (size_t)NT * (NC + 1) * 2));
@@ -406,7 +495,7 @@ int main(int argc, char** argv) {
         CK(hipEventRecord(e[1]));
         k_dirt<<<dim3((NT + 63) / 64, (NC + 63) / 64 + 1), 256>>>(dir, NT, dt);
         CK(hipEventRecord(e[2]));
-        k_tm<<<256, TC>>>(n, tmp, dt, NT, MT, o, 1600000000000ll, 1600000001000ll);
+        k_tm<<<256, TC>>>(n, tmp, dt, NT, MT, o, 1600000000000ll, 1600000001000ll, mode);
         CK(hipEventRecord(e[3]));
         CK(hipEventSynchronize(e[3]));
         float a, b, c;

@@ -1032,3 +1032,54 @@ def test_narrow_staging_switches_to_wide_keys(oracle_mod, kind):
     assert_rows_equal(g.take_rows(), o.take_rows(), "f64", "final")
     g.close()
     o.close()
+
+
+# Tile staging (fg_kernels.h): TUMBLE batches of 32-bit keys stay in their pass-1 tiles, sorted by
+# consumer bucket (4 state regions), and the window fires straight from them (k_tile_fire). The
+# cases below take its other paths: the LDS table of a bucket overflowing (regions split, one
+# region per retried item), and lanes whose tile passes must be materialized into regular staged
+# passes (a batch with NULL values in the same slice; a checkpoint while tile passes are staged).
+def test_tile_fire_bucket_overflow_splits(oracle_mod):
+    """~1.3M distinct keys in one 30-s window of an operator sized for 60k keys (2^8 regions, 64
+    buckets of ~20k keys against the 8,192-slot table): every bucket overflows, the regions split
+    and each region is fired again on its own from the same six tile passes."""
+    cfg = cfg_of("tumble", 30_000)
+    st = {}
+    drive_both(oracle_mod, cfg, n=3_000_000, keys=1_500_000, batch=500_000, delay=0, jitter=0, expected_keys=60_000,
+               stats=st)
+    assert st["state_regions"] >= 512, st
+
+
+@pytest.mark.parametrize("vt", ["f64", "i64"])
+def test_tile_passes_materialized(oracle_mod, vt):
+    """A slice lane holding tile passes and a batch with NULL values (staged by pass 2): the tile
+    passes are materialized and the lane merged as any staged lane; then a checkpoint while tile
+    passes are staged (flushed into the slice table through the same conversion), a restore, and
+    more batches. Rows and late drops equal the oracle's throughout."""
+    cfg = cfg_of("tumble", 10_000, vt=vt)
+    n, keys, batch = 1_200_000, 50_000, 100_000
+    key, ts, val, isnull = make_stream(n, keys, vt, null_frac=0.05)
+    g = gpu_mk(cfg, expected_keys=keys, buffer_records=1 << 21)
+    o = oracle_mk(oracle_mod, cfg)
+    o_base = 0
+    for step, (lo, hi, wm) in enumerate(batches_with_watermarks(n, batch, ts, 200)):
+        nl = isnull[lo:hi] if step in (2, 7) else None   # two batches with NULL values, the rest tile-staged
+        g.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], nl)
+        o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi], nl)
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        assert_rows_equal(g.take_rows(), o.take_rows(), vt, f"step {step}")
+        assert g.late_dropped == o_base + o.late_dropped
+        if step == 4:   # checkpoint with tile passes staged, failover, restore
+            g.prepare_snapshot()
+            o.prepare_snapshot()
+            g2, o2 = g.restore_copy(), o.restore_copy()
+            o_base += o.late_dropped
+            g.close()
+            o.close()
+            g, o = g2, o2
+    g.process_watermark(JMAX)
+    o.process_watermark(JMAX)
+    assert_rows_equal(g.take_rows(), o.take_rows(), vt, "final")
+    g.close()
+    o.close()
