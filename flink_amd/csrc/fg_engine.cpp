@@ -2975,6 +2975,10 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
             sigaction(SIGSEGV, &sa, nullptr);
         }
     }
+    if (!out) {
+        g_open_error = "null handle pointer";
+        return FG_EINVAL;
+    }
     *out = nullptr;
     if (!cfg) {
         g_open_error = "null config";
