@@ -274,6 +274,7 @@ struct fg_handle {
     DevBuf acc_v1, acc_v2;   // multi-value operator: the partial rows' MIN / MAX
     DevBuf in_cs, in_cv, in_sum, in_slice, in_v1, in_v2;
     bool local = false;     // FG_FLAG_LOCAL_PARTIALS: fired slices emit partial accumulators
+    bool local_emit_all = false;   // fg_flush_partials: every staged slice emits now
     bool proctime = false;  // FG_FLAG_PROCTIME: processing-time windows, nothing is late
     std::vector<int64_t> tz_trans, tz_offs;   // zone rules (host copy); tz_dev: the HBM copy
     DevBuf tz_dev;
@@ -3563,15 +3564,18 @@ static int advance_progress(fg_handle* h, int64_t wm) {
         // the smallest buffered slice, the combiner emits partial accumulators; here every
         // fired slice lane emits its partials, and slices flushed earlier to make room are
         // emitted from their tables
+        // (fg_flush_partials: prepareSnapshotPreBarrier -> RecordsWindowBuffer.flush, every
+        // buffered slice emits its partials now, the local operator keeps no state)
+        const bool every = h->local_emit_all;
         if (wm > h->current_progress) h->current_progress = wm;
-        if (staged_any(h) && is_window_fired(h->w, min_staged_slice_end(h), wm)) {
-            const FireRange all{JMIN, wm};
-            rc = flush(h, &all, true);
+        if (staged_any(h) && (every || is_window_fired(h->w, min_staged_slice_end(h), wm))) {
+            const FireRange all{JMIN, every ? JMAX : wm};
+            rc = flush(h, &all, !every);
             if (rc) return rc;
         }
         std::vector<int64_t> ends;
         for (auto& kv : h->tables)
-            if (is_window_fired(h->w, kv.first, wm)) ends.push_back(kv.first);
+            if (every || is_window_fired(h->w, kv.first, wm)) ends.push_back(kv.first);
         for (int64_t e : ends) {
             rc = fire_one(h, e, {h->tables[e].get()}, nullptr);
             if (rc) return rc;
@@ -3724,6 +3728,25 @@ int fg_collect_fired_to(fg_handle* h, int32_t out_location, fg_rows* fired) {
 }
 
 int fg_collect_fired(fg_handle* h, fg_rows* fired) { return fg_collect_fired_to(h, FG_DEVICE, fired); }
+
+int fg_flush_partials(fg_handle* h, int32_t out_location, fg_rows* fired) {
+    if (!h || !fired || (out_location != FG_HOST && out_location != FG_DEVICE)) return FG_EINVAL;
+    if (!h->local) return h->fail(FG_ESTATE, "fg_flush_partials on an operator without FG_FLAG_LOCAL_PARTIALS");
+    HIPCHK(h, hipSetDevice(h->device));
+    h->local_emit_all = true;
+    const int rc = advance_progress(h, h->current_progress);   // (the progress does not move)
+    h->local_emit_all = false;
+    if (rc) return rc;
+    h->rows_fired += h->out_n - h->adv_base;
+    h->async_open = false;
+    std::memset(fired, 0, sizeof *fired);
+    fired->n = h->out_n;
+    fired->num_aggs = h->cfg.num_aggs;
+    fired->location = out_location;
+    if (out_location == FG_HOST) return copy_out_to_host(h, fired);
+    device_rows(h, out_location, fired);
+    return FG_OK;
+}
 
 int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows* fired) {
     if (!h) return FG_EINVAL;

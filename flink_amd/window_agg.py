@@ -420,9 +420,22 @@ class WindowAggOperator:
 
     # -- checkpointing ----------------------------------------------------------------------------
     def prepare_snapshot_pre_barrier(self):
-        """Flush the staged buffer into the GPU-resident state (RecordsWindowBuffer.flush)."""
+        """Flush the staged buffer into the GPU-resident state (RecordsWindowBuffer.flush). A local
+        operator (local_partials) keeps no state: its buffer flushes to the output instead -- the
+        partial rows of every buffered slice are returned (flush_partials)."""
+        if self.local_partials:
+            return self.flush_partials()
         L.check(self._lib.fg_flush(self._h), self._h)
         self._hold(None)
+
+    def flush_partials(self):
+        """Local phase: every buffered slice emits its partial accumulator rows now
+        (LocalSlicingWindowAggOperator.prepareSnapshotPreBarrier -> WindowBuffer.flush ->
+        LocalAggCombiner, fg_flush_partials); host rows as process_watermark returns them."""
+        r = L.FgRows()
+        L.check(self._lib.fg_flush_partials(self._h, L.HOST, C.byref(r)), self._h)
+        self._hold(None)
+        return self._host_rows(r)
 
     def snapshot_state(self, copy: bool = True):
         """(state image dict of numpy arrays, timer watermark): the window-aggs ValueState.

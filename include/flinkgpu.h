@@ -315,6 +315,13 @@ int  fg_collect_fired(fg_handle* h, fg_rows* fired);
  * FG_DEVICE is fg_collect_fired. */
 int  fg_collect_fired_to(fg_handle* h, int32_t out_location, fg_rows* fired);
 int  fg_flush(fg_handle* h);
+/* Local phase only (FG_FLAG_LOCAL_PARTIALS; ABI 12): every buffered slice emits its partial
+ * accumulator rows now, as fg_advance_progress does for the slices a watermark fires --
+ * LocalSlicingWindowAggOperator.prepareSnapshotPreBarrier -> WindowBuffer.flush
+ * (LocalSlicingWindowAggOperator.java:142-144, RecordsWindowBuffer.java:108-119 with
+ * LocalAggCombiner.java:69-106): the local operator holds no state across a checkpoint. The
+ * progress does not move. Rows as fg_advance_progress at out_location. */
+int  fg_flush_partials(fg_handle* h, int32_t out_location, fg_rows* fired);
 int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
 int  fg_late_dropped(fg_handle* h, int64_t* out);

@@ -619,8 +619,20 @@ TWO_PHASE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("name", ["tumble_f64_regions", "tumble_i64_ooo_late", "hop_f64_late", "cumulate_i64_late"])
+def test_two_phase_local_checkpoints(oracle_mod, name):
+    """Checkpoint barriers at the local operators every other batch: each one's buffer flushes
+    its partials to the output (LocalSlicingWindowAggOperator.prepareSnapshotPreBarrier ->
+    WindowBuffer.flush; fg_flush_partials), so a slice's partials reach the global operators in
+    several rows; the global result still equals the single-phase oracle."""
+    case = {c[0]: c for c in TWO_PHASE_CASES}.get(name)
+    if case is None:
+        pytest.skip(f"no two-phase case {name}")
+    test_two_phase_parity(oracle_mod, *case, local_ckpt=2)
+
+
 @pytest.mark.parametrize("name,cfg,kw", TWO_PHASE_CASES, ids=[c[0] for c in TWO_PHASE_CASES])
-def test_two_phase_parity(oracle_mod, name, cfg, kw):
+def test_two_phase_parity(oracle_mod, name, cfg, kw, local_ckpt=0):
     """LocalAggCombiner -> key-group exchange -> GlobalAggCombiner: 3 source partitions with a
     local operator each, partial rows routed to 2 owners by KeyGroupRangeAssignment, global
     operators fire; the union of their rows equals the single-phase oracle over the whole
@@ -660,11 +672,14 @@ def test_two_phase_parity(oracle_mod, name, cfg, kw):
                                      rows["count"][m], sums[m], *extra)
 
     got, exp = [], []
-    for lo, hi, wm in batches_with_watermarks(n, batch, ts, delay):
+    for bi, (lo, hi, wm) in enumerate(batches_with_watermarks(n, batch, ts, delay)):
         for s in range(S):
             m = src[lo:hi] == s
             local[s].process_batch(key[lo:hi][m], ts[lo:hi][m], val[lo:hi][m])
         o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
+        if local_ckpt and bi % local_ckpt == local_ckpt - 1:
+            # a checkpoint barrier: each local operator's buffer flushes to the output (fg_flush_partials)
+            route([local[s].prepare_snapshot_pre_barrier() for s in range(S)])
         route([local[s].process_watermark(wm) for s in range(S)])
         got += [g.process_watermark(wm) for g in glob]
         o.process_watermark(wm)
