@@ -421,11 +421,11 @@ constexpr int kTileBits = 2;                  // state regions per consumer buck
 #define FG_TILE_T 768
 #endif
 #ifndef FG_TILE_R
-#define FG_TILE_R 12
+#define FG_TILE_R 8
 #endif
-constexpr int kTileThreads = FG_TILE_T;       // tile pass 1 (170 VGPRs at 768 threads: no spills)
-constexpr int kTileR = FG_TILE_R;             // records per thread per tile (even: paired loads)
-constexpr int kTileRecs = kTileR * kTileThreads;   // records per pass-1 tile (9,216)
+constexpr int kTileThreads = FG_TILE_T;       // tile pass 1 (768 x 8: no spills at 170 VGPRs; larger
+constexpr int kTileR = FG_TILE_R;             // tiles spill -- profiles/r04 variants)
+constexpr int kTileRecs = kTileR * kTileThreads;   // records per pass-1 tile (6,144; even R: paired loads)
 constexpr int kMaxTileBuckets = 4096;         // lanes << (region_bits - kTileBits)
 constexpr int kTileSlots = 8192;              // consumer LDS table (~4.9k keys: 60 % load)
 constexpr int kTileFireThreads = 1024;

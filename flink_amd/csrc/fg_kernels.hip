@@ -2862,7 +2862,9 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     const int lm = p.lanes - 1;
     const int per = (NC + T - 1) / T;   // buckets per thread in the scan
     auto li_of = [&](int u) -> int64_t { return 2 * ((int64_t)tid + (int64_t)(u >> 1) * T) + (u & 1); };
-    auto load = [&](int64_t t0, longlong2 (&k2)[R / 2], longlong2 (&t2)[R / 2], longlong2 (&v2)[R / 2]) {
+    // keys and rowtimes (classification); the values are read once the tile's ranks are known
+    // (only into the sorted tile: never held in registers beside the next tile's prefetch)
+    auto load = [&](int64_t t0, longlong2 (&k2)[R / 2], longlong2 (&t2)[R / 2]) {
         const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
         if (tn == TILE && p.vec) {
 #pragma unroll
@@ -2870,26 +2872,40 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
                 const int64_t i = t0 + li_of(2 * u);
                 k2[u] = ld2(p.key + i);
                 t2[u] = ld2(p.ts + i);
-                v2[u] = has_val ? ld2(p.val + i) : make_longlong2(0, 0);
             }
         } else {
 #pragma unroll
             for (int u = 0; u < R / 2; u++) {
                 const int64_t l0 = li_of(2 * u);
-                k2[u] = t2[u] = v2[u] = make_longlong2(0, 0);
+                k2[u] = t2[u] = make_longlong2(0, 0);
                 if (l0 < tn) {
-                    k2[u].x = p.key[t0 + l0]; t2[u].x = p.ts[t0 + l0];
-                    if (has_val) v2[u].x = p.val[t0 + l0];
+                    k2[u].x = p.key[t0 + l0];
+                    t2[u].x = p.ts[t0 + l0];
                 }
                 if (l0 + 1 < tn) {
-                    k2[u].y = p.key[t0 + l0 + 1]; t2[u].y = p.ts[t0 + l0 + 1];
-                    if (has_val) v2[u].y = p.val[t0 + l0 + 1];
+                    k2[u].y = p.key[t0 + l0 + 1];
+                    t2[u].y = p.ts[t0 + l0 + 1];
                 }
             }
         }
     };
-    longlong2 ka[R / 2], ta[R / 2], va[R / 2];
-    if (beg < end) load(beg, ka, ta, va);
+    auto load_vals = [&](int64_t t0, longlong2 (&v2)[R / 2]) {
+        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
+        if (tn == TILE && p.vec && has_val) {
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) v2[u] = ld2(p.val + t0 + li_of(2 * u));
+        } else {
+#pragma unroll
+            for (int u = 0; u < R / 2; u++) {
+                const int64_t l0 = li_of(2 * u);
+                v2[u] = make_longlong2(0, 0);
+                if (has_val && l0 < tn) v2[u].x = p.val[t0 + l0];
+                if (has_val && l0 + 1 < tn) v2[u].y = p.val[t0 + l0 + 1];
+            }
+        }
+    };
+    longlong2 ka[R / 2], ta[R / 2];
+    if (beg < end) load(beg, ka, ta);
     int j = 0;
     for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
         const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
@@ -2924,11 +2940,15 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
                 if (q >= p.filter_hi) qnext = q < qnext ? q : qnext;
             }
         }
-        int64_t rv[R];
-#pragma unroll
-        for (int u = 0; u < R; u++) rv[u] = (u & 1) ? va[u >> 1].y : va[u >> 1].x;
+        longlong2 va[R / 2];
+        load_vals(t0, va);   // (in flight across the scan)
+#ifndef FG_TILE_LATE_PREFETCH
+#define FG_TILE_LATE_PREFETCH 1
+#endif
         // 2) prefetch the next tile: in flight across this tile's scan, staging and write-out
-        if (t0 + TILE < end) load(t0 + TILE, ka, ta, va);
+        // (late: only across the write-out -- the raw loads are then not live beside this tile's
+        // ranks, keys and values, which lets a tile hold more records per thread)
+        if (!FG_TILE_LATE_PREFETCH && t0 + TILE < end) load(t0 + TILE, ka, ta);
         lds_barrier();
         {   // exclusive scan of the tile's bucket counts (per consecutive buckets per thread)
             constexpr int kPer = (kMaxTileBuckets + T - 1) / T;
@@ -2960,8 +2980,9 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
             if (rcb[u] == 0xffffffffu) continue;
             const uint32_t slot = s_cc[rcb[u] & 4095u] + (rcb[u] >> 12);
             s_k[slot] = k32[u];
-            s_v[slot] = (unsigned long long)rv[u];
+            s_v[slot] = (unsigned long long)((u & 1) ? va[u >> 1].y : va[u >> 1].x);
         }
+        if (FG_TILE_LATE_PREFETCH && t0 + TILE < end) load(t0 + TILE, ka, ta);
         lds_barrier();
         for (uint32_t i = tid; i < tile_total; i += T) st_rec12(p.tmp, (uint64_t)(t0 + i), (int64_t)s_k[i], (int64_t)s_v[i]);
         lds_barrier();   // staging and the directory row have read the offsets
@@ -3053,21 +3074,31 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// A wave's walk over the fragments of one bucket (column `col` of a tile pass): groups of 64
-// tiles (one per lane, this wave's every W-th group), each cut into windows of up to kTileWin
-// records; next() fills the window's records (up to kTileWin / 64 per lane, loads in flight on
-// return) -- a wave-private map from a window position to its fragment (the fragments mark
-// their first position, an inclusive max-scan fills the map) gives each record its source.
-constexpr int kTileWin = 256;
+// A wave's walk over the fragments of one bucket (column `col` of a tile pass): groups of
+// 64 * kTileTPL tiles (kTileTPL consecutive tiles per lane, this wave's every W-th group), each
+// cut into windows of up to kTileWin records; next() fills the window's records (kTileWin / 64
+// per lane, loads in flight on return) -- a wave-private map from a window position to its
+// fragment (the fragments mark their first position, an inclusive max-scan fills the map)
+// gives each record its source.
+#ifndef FG_TILE_WIN
+#define FG_TILE_WIN 256
+#endif
+#ifndef FG_TILE_TPL
+#define FG_TILE_TPL 1
+#endif
+constexpr int kTileWin = FG_TILE_WIN;
 constexpr int kTileRpl = kTileWin / 64;
+constexpr int kTileTPL = FG_TILE_TPL;
+constexpr int kTileGroup = 64 * kTileTPL;   // tiles per group (<= 256: u8 fragment ids)
+static_assert(kTileGroup <= 256 && kTileWin % 64 == 0, "tile walk shape");
 struct TileWalk {
     const uint32_t* col;
     const void* rec;
     int64_t seg_per;
     int32_t nt, mt;
     int32_t t0, stride;         // current group's first tile, groups' stride
-    uint32_t xn;                // the next group's directory entry (prefetched)
-    uint32_t g_len, g_st, g_tot, b;
+    uint32_t xn[kTileTPL];      // the next group's directory entries (prefetched)
+    uint32_t g_len[kTileTPL], g_st[kTileTPL], g_tot, b;
 };
 __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp, int32_t cb, int wave, int W,
                                                 int lane) {
@@ -3076,11 +3107,15 @@ __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp,
     w.seg_per = tp.seg_per;
     w.nt = tp.nt;
     w.mt = tp.mt;
-    w.stride = W * 64;
-    w.t0 = wave * 64 - w.stride;
-    const int t = wave * 64 + lane;
-    w.xn = t < w.nt ? gbl(w.col)[t] : 0u;
-    w.g_len = w.g_st = w.g_tot = w.b = 0;
+    w.stride = W * kTileGroup;
+    w.t0 = wave * kTileGroup - w.stride;
+#pragma unroll
+    for (int q = 0; q < kTileTPL; q++) {
+        const int t = wave * kTileGroup + lane * kTileTPL + q;
+        w.xn[q] = t < w.nt ? gbl(w.col)[t] : 0u;
+        w.g_len[q] = w.g_st[q] = 0;
+    }
+    w.g_tot = w.b = 0;
 }
 // the next window of the walk: records in kr / vr (lanes past nrec hold key 0), false when done
 __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_t* dl, int lane,
@@ -3088,26 +3123,40 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
     while (w.b >= w.g_tot) {   // the next group with records
         w.t0 += w.stride;
         if (w.t0 >= w.nt) return false;
-        const int t = w.t0 + lane;
-        const uint32_t x = w.xn;
-        w.xn = t + w.stride < w.nt ? gbl(w.col)[t + w.stride] : 0u;
-        w.g_len = x >> 16;
-        const uint32_t base = (uint32_t)(w.seg_per * (t / w.mt) + (int64_t)(t % w.mt) * kTileRecs) + (x & 0xffffu);
-        uint32_t inc = w.g_len;
+        uint32_t base[kTileTPL], sum = 0;
+#pragma unroll
+        for (int q = 0; q < kTileTPL; q++) {
+            const int t = w.t0 + lane * kTileTPL + q;
+            const uint32_t x = w.xn[q];
+            w.xn[q] = t + w.stride < w.nt ? gbl(w.col)[t + w.stride] : 0u;
+            w.g_len[q] = x >> 16;
+            base[q] = (uint32_t)(w.seg_per * (t / w.mt) + (int64_t)(t % w.mt) * kTileRecs) + (x & 0xffffu);
+            w.g_st[q] = sum;   // (local prefix; the wave's exclusive prefix added below)
+            sum += w.g_len[q];
+        }
+        uint32_t inc = sum;
         for (int s = 1; s < 64; s <<= 1) {
             const uint32_t y = __shfl_up(inc, s);
             if (lane >= s) inc += y;
         }
-        w.g_st = inc - w.g_len;
+        const uint32_t ex = inc - sum;
         w.g_tot = __shfl(inc, 63);
         w.b = 0;
         wave_lds_sync();   // (the last window's reads of dl are done: its loads were issued)
-        dl[lane] = base - w.g_st;
+#pragma unroll
+        for (int q = 0; q < kTileTPL; q++) {
+            w.g_st[q] += ex;
+            dl[lane * kTileTPL + q] = base[q] - w.g_st[q];
+        }
     }
 #pragma unroll
     for (int q = 0; q < kTileRpl; q++) fm[lane * kTileRpl + q] = 0;
     wave_lds_sync();
-    if (w.g_len > 0 && w.g_st < w.b + kTileWin && w.g_st + w.g_len > w.b) fm[w.g_st > w.b ? w.g_st - w.b : 0] = (uint8_t)lane;
+#pragma unroll
+    for (int q = 0; q < kTileTPL; q++) {
+        const uint32_t st = w.g_st[q], len = w.g_len[q];
+        if (len > 0 && st < w.b + kTileWin && st + len > w.b) fm[st > w.b ? st - w.b : 0] = (uint8_t)(lane * kTileTPL + q);
+    }
     wave_lds_sync();
     uint32_t e[kTileRpl];
 #pragma unroll
@@ -3158,7 +3207,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     __shared__ uint32_t t_cs[S + 1];
     __shared__ unsigned long long t_v[S + 1];
     __shared__ uint8_t s_fm[W][kTileWin];
-    __shared__ uint32_t s_dl[W][64];
+    __shared__ uint32_t s_dl[W][kTileGroup];
     __shared__ uint32_t s_grp[kRounds * W];
     __shared__ uint16_t s_map[S + 1];
     __shared__ unsigned int s_flags;
