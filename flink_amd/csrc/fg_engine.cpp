@@ -2100,7 +2100,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         const int64_t NT = (int64_t)p.grid * p.max_tiles;
         HIPCHK(h, st->t_rec.ensure((size_t)(n / 64 + 2) * kRec12Block));
         HIPCHK(h, st->t_dt.ensure(4 * (size_t)p.n_coarse * NT));
-        HIPCHK(h, h->tile_dir.ensure(2 * (size_t)NT * (p.n_coarse + 1)));
+        HIPCHK(h, h->tile_dir.ensure(2 * (size_t)NT * kTileDirStride(p.n_coarse)));
         p.tmp = st->t_rec.as<longlong2>();
         p.dir = h->tile_dir.as<uint16_t>();
         st->t_seg_per = per;

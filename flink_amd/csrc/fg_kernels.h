@@ -423,9 +423,15 @@ constexpr int kTileBits = 2;                  // state regions per consumer buck
 #ifndef FG_TILE_R
 #define FG_TILE_R 8
 #endif
-constexpr int kTileThreads = FG_TILE_T;       // tile pass 1 (768 x 8: no spills at 170 VGPRs; larger
-constexpr int kTileR = FG_TILE_R;             // tiles spill -- profiles/r04 variants)
-constexpr int kTileRecs = kTileR * kTileThreads;   // records per pass-1 tile (6,144; even R: paired loads)
+#ifndef FG_TILE_H
+#define FG_TILE_H 1
+#endif
+constexpr int kTileThreads = FG_TILE_T;       // tile pass 1: one classification round of R records per
+constexpr int kTileR = FG_TILE_R;             // thread (768 x 8: no spills at 170 VGPRs; more spill)
+constexpr int kTileH = FG_TILE_H;             // rounds (halves) per tile
+constexpr int kTileRecs = kTileH * kTileR * kTileThreads;   // records per pass-1 tile (6,144; even R: paired loads)
+// directory row of one tile: nc u16 bucket offsets, the tile's total, padded to 4-B alignment
+__host__ __device__ constexpr int64_t kTileDirStride(int nc) { return nc + 2; }
 constexpr int kMaxTileBuckets = 4096;         // lanes << (region_bits - kTileBits)
 constexpr int kTileSlots = 8192;              // consumer LDS table (~4.9k keys: 60 % load)
 constexpr int kTileFireThreads = 1024;

@@ -2830,25 +2830,33 @@ hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, cons
 // drops, slice range, lane totals, the 32-bit key check) and a sort of each tile by consumer
 // bucket (lane << (region_bits - kTileBits) | region >> kTileBits), written back in place as
 // block-laid 12-B records at their absolute batch index, with the tile's bucket offsets in
-// p.dir. Software-pipelined like k_part1 (the next tile's loads in flight across this tile's
-// scan, staging and write-out). *p.max_bucket: the largest bucket count of one tile (skew).
+// p.dir (rows of kTileDirStride u16). A tile is kTileH halves of R records per thread: the
+// second half's keys and rowtimes are loaded while the first is classified, the values are read
+// once the tile's ranks are known (straight into the sorted tile), and the next tile's first
+// half is prefetched across the write-out -- so a tile holds twice the records the registers of
+// one classification round allow, and the fire reads half as many fragments. Bucket counts are
+// u16 pairs in one LDS word (ds_add_u32 of 1 << 16 * (b & 1): a tile has < 2^16 records).
+// *p.max_bucket: the largest bucket count of one tile (skew).
 __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     constexpr int T = kTileThreads;
     constexpr int R = kTileR;
+    constexpr int H = kTileH;
+    constexpr int HALF = T * R;
     constexpr int TILE = kTileRecs;
-    static_assert(R % 2 == 0, "pairs of records per thread");
-    static_assert(TILE < (1 << 20) && kMaxTileBuckets <= (1 << 12) && TILE < (1 << 16), "rank << 12 | bucket; u16 offsets");
-    __shared__ uint32_t s_k[TILE];                   // the tile, bucket sorted: keys
-    __shared__ unsigned long long s_v[TILE];         //   and value bits
-    __shared__ uint32_t s_cc[kMaxTileBuckets + 1];   // bucket counts, then offsets
+    static_assert(R % 2 == 0 && H >= 1 && H <= 2 && TILE == H * HALF, "tile shape");
+    static_assert(TILE < (1 << 16) && kMaxTileBuckets <= (1 << 12), "u16 counts and offsets; rank << 12 | bucket");
+    __shared__ uint32_t s_k[TILE];                       // the tile, bucket sorted: keys
+    __shared__ unsigned long long s_v[TILE];             //   and value bits
+    __shared__ uint32_t s_cw[kMaxTileBuckets / 2 + 1];   // bucket counts, then offsets (u16 pairs); [NC/2] total
     __shared__ uint32_t s_wave[T / 64];
     __shared__ unsigned long long s_drop;
     __shared__ long long s_qmin, s_qmax, s_qnext;
     __shared__ uint32_t s_mask, s_bmax;
     __shared__ uint32_t s_lane[kMaxLanes];
-    const int NC = p.n_coarse;
+    const int NC = p.n_coarse;   // (even: >= 16 buckets)
+    const int NW = NC / 2;
     const int tid = threadIdx.x;
-    for (int i = tid; i <= NC; i += T) s_cc[i] = 0;
+    for (int i = tid; i <= NW; i += T) s_cw[i] = 0;
     if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; s_bmax = 0; }
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
@@ -2860,16 +2868,15 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     bool wide = false;
     long long qmin = JMAX, qmax = JMIN, qnext = JMAX;
     const int lm = p.lanes - 1;
-    const int per = (NC + T - 1) / T;   // buckets per thread in the scan
+    const int pw = (NW + T - 1) / T;   // count words per thread in the scan
     auto li_of = [&](int u) -> int64_t { return 2 * ((int64_t)tid + (int64_t)(u >> 1) * T) + (u & 1); };
-    // keys and rowtimes (classification); the values are read once the tile's ranks are known
-    // (only into the sorted tile: never held in registers beside the next tile's prefetch)
-    auto load = [&](int64_t t0, longlong2 (&k2)[R / 2], longlong2 (&t2)[R / 2]) {
-        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
-        if (tn == TILE && p.vec) {
+    // keys and rowtimes of the half at h0 (classification)
+    auto load = [&](int64_t h0, longlong2 (&k2)[R / 2], longlong2 (&t2)[R / 2]) {
+        const int64_t hn = end - h0 < HALF ? end - h0 : HALF;
+        if (hn == HALF && p.vec) {
 #pragma unroll
             for (int u = 0; u < R / 2; u++) {
-                const int64_t i = t0 + li_of(2 * u);
+                const int64_t i = h0 + li_of(2 * u);
                 k2[u] = ld2(p.key + i);
                 t2[u] = ld2(p.ts + i);
             }
@@ -2878,48 +2885,44 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
             for (int u = 0; u < R / 2; u++) {
                 const int64_t l0 = li_of(2 * u);
                 k2[u] = t2[u] = make_longlong2(0, 0);
-                if (l0 < tn) {
-                    k2[u].x = p.key[t0 + l0];
-                    t2[u].x = p.ts[t0 + l0];
+                if (l0 < hn) {
+                    k2[u].x = p.key[h0 + l0];
+                    t2[u].x = p.ts[h0 + l0];
                 }
-                if (l0 + 1 < tn) {
-                    k2[u].y = p.key[t0 + l0 + 1];
-                    t2[u].y = p.ts[t0 + l0 + 1];
+                if (l0 + 1 < hn) {
+                    k2[u].y = p.key[h0 + l0 + 1];
+                    t2[u].y = p.ts[h0 + l0 + 1];
                 }
             }
         }
     };
-    auto load_vals = [&](int64_t t0, longlong2 (&v2)[R / 2]) {
-        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
-        if (tn == TILE && p.vec && has_val) {
+    auto load_vals = [&](int64_t h0, longlong2 (&v2)[R / 2]) {
+        const int64_t hn = end - h0 < HALF ? end - h0 : HALF;
+        if (hn == HALF && p.vec && has_val) {
 #pragma unroll
-            for (int u = 0; u < R / 2; u++) v2[u] = ld2(p.val + t0 + li_of(2 * u));
+            for (int u = 0; u < R / 2; u++) v2[u] = ld2(p.val + h0 + li_of(2 * u));
         } else {
 #pragma unroll
             for (int u = 0; u < R / 2; u++) {
                 const int64_t l0 = li_of(2 * u);
                 v2[u] = make_longlong2(0, 0);
-                if (has_val && l0 < tn) v2[u].x = p.val[t0 + l0];
-                if (has_val && l0 + 1 < tn) v2[u].y = p.val[t0 + l0 + 1];
+                if (has_val && l0 < hn) v2[u].x = p.val[h0 + l0];
+                if (has_val && l0 + 1 < hn) v2[u].y = p.val[h0 + l0 + 1];
             }
         }
     };
-    longlong2 ka[R / 2], ta[R / 2];
-    if (beg < end) load(beg, ka, ta);
-    int j = 0;
-    for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
-        const int64_t tn = end - t0 < TILE ? end - t0 : TILE;
-        // 1) classify + rank the tile's records by bucket (LDS atomics)
-        uint32_t rcb[R];   // (rank << 12) | bucket, 0xffffffff = not staged
-        uint32_t k32[R];
+    // classify + rank the half's records by bucket (LDS atomics on the u16 pairs)
+    auto classify_half = [&](int64_t h0, const longlong2 (&k2)[R / 2], const longlong2 (&t2)[R / 2],
+                             uint32_t (&rcb)[R], uint32_t (&k32)[R]) {
+        const int64_t hn = end - h0 < HALF ? end - h0 : HALF;
 #pragma unroll
         for (int u = 0; u < R; u++) {
             const int64_t li = li_of(u);
             rcb[u] = 0xffffffffu;
-            const int64_t k = (u & 1) ? ka[u >> 1].y : ka[u >> 1].x;
+            const int64_t k = (u & 1) ? k2[u >> 1].y : k2[u >> 1].x;
             k32[u] = (uint32_t)k;
-            if (li >= tn) continue;
-            const int64_t ts = (u & 1) ? ta[u >> 1].y : ta[u >> 1].x;
+            if (li >= hn) continue;
+            const int64_t ts = (u & 1) ? t2[u >> 1].y : t2[u >> 1].x;
             int64_t q, h;
             const int b = classify(p, k, ts, &q, &h);
             if (b >= 0) {
@@ -2931,7 +2934,9 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
 #pragma unroll
                 for (int l = 0; l < kMaxLanes; l++) lc[l] += ln == l ? 1u : 0u;
                 const uint32_t cb = (uint32_t)b >> kTileBits;
-                rcb[u] = (atomicAdd(&s_cc[cb], 1u) << 12) | cb;
+                const uint32_t sh = (cb & 1u) * 16u;
+                const uint32_t old = atomicAdd(&s_cw[cb >> 1], 1u << sh);
+                rcb[u] = (((old >> sh) & 0xffffu) << 12) | cb;
             } else if (b == -1) {
                 drops++;
             } else {   // outside the slice filter: in the batch's slice range only
@@ -2940,53 +2945,76 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
                 if (q >= p.filter_hi) qnext = q < qnext ? q : qnext;
             }
         }
-        longlong2 va[R / 2];
-        load_vals(t0, va);   // (in flight across the scan)
-#ifndef FG_TILE_LATE_PREFETCH
-#define FG_TILE_LATE_PREFETCH 1
-#endif
-        // 2) prefetch the next tile: in flight across this tile's scan, staging and write-out
-        // (late: only across the write-out -- the raw loads are then not live beside this tile's
-        // ranks, keys and values, which lets a tile hold more records per thread)
-        if (!FG_TILE_LATE_PREFETCH && t0 + TILE < end) load(t0 + TILE, ka, ta);
-        lds_barrier();
-        {   // exclusive scan of the tile's bucket counts (per consecutive buckets per thread)
-            constexpr int kPer = (kMaxTileBuckets + T - 1) / T;
-            uint32_t c[kPer], run = 0;
+    };
+    longlong2 ka[R / 2], ta[R / 2];
+    if (beg < end) load(beg, ka, ta);
+    int j = 0;
+    for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
+        uint32_t rcb[H][R], k32[H][R];
+        {
+            longlong2 kb[R / 2], tb[R / 2];
+            if (H > 1 && t0 + HALF < end) load(t0 + HALF, kb, tb);   // (in flight across the first half's ranking)
+            classify_half(t0, ka, ta, rcb[0], k32[0]);
+            if (H > 1) {
+                if (t0 + HALF < end) {
+                    classify_half(t0 + HALF, kb, tb, rcb[H - 1], k32[H - 1]);
+                } else {
 #pragma unroll
-            for (int q = 0; q < kPer; q++) {
-                const int b = tid * per + q;
-                c[q] = (q < per && b < NC) ? s_cc[b] : 0u;
-                run += c[q];
-                bmax = c[q] > bmax ? c[q] : bmax;
+                    for (int u = 0; u < R; u++) rcb[H - 1][u] = 0xffffffffu;
+                }
+            }
+        }
+        longlong2 va[H][R / 2];
+#pragma unroll
+        for (int hh = 0; hh < H; hh++) load_vals(t0 + (int64_t)hh * HALF, va[hh]);   // (in flight across the scan)
+        lds_barrier();
+        {   // exclusive scan of the tile's bucket counts, u16 pairs per word, consecutive words per thread
+            constexpr int kPw = (kMaxTileBuckets / 2 + T - 1) / T;
+            uint32_t c[kPw], run = 0;
+#pragma unroll
+            for (int q = 0; q < kPw; q++) {
+                const int w = tid * pw + q;
+                c[q] = (q < pw && w < NW) ? s_cw[w] : 0u;
+                const uint32_t lo = c[q] & 0xffffu, hi = c[q] >> 16;
+                run += lo + hi;
+                bmax = lo > bmax ? lo : bmax;
+                bmax = hi > bmax ? hi : bmax;
             }
             uint32_t total;
             uint32_t ex = block_exclusive_scan_t<true>(run, s_wave, &total);
 #pragma unroll
-            for (int q = 0; q < kPer; q++) {
-                const int b = tid * per + q;
-                if (q < per && b < NC) s_cc[b] = ex;
-                ex += c[q];
+            for (int q = 0; q < kPw; q++) {
+                const int w = tid * pw + q;
+                const uint32_t lo = c[q] & 0xffffu, hi = c[q] >> 16;
+                if (q < pw && w < NW) s_cw[w] = ex | ((ex + lo) << 16);
+                ex += lo + hi;
             }
-            if (tid == 0) s_cc[NC] = total;
+            if (tid == 0) s_cw[NW] = total;
         }
         lds_barrier();
-        uint16_t* drow = p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * (NC + 1);
-        for (int c = tid; c <= NC; c += T) drow[c] = (uint16_t)s_cc[c];
-        const uint32_t tile_total = s_cc[NC];
-        // 3) stage the tile bucket sorted, then write it back in place
-#pragma unroll
-        for (int u = 0; u < R; u++) {
-            if (rcb[u] == 0xffffffffu) continue;
-            const uint32_t slot = s_cc[rcb[u] & 4095u] + (rcb[u] >> 12);
-            s_k[slot] = k32[u];
-            s_v[slot] = (unsigned long long)((u & 1) ? va[u >> 1].y : va[u >> 1].x);
+        {   // the directory row: the offsets (u16 pairs) and the tile's total
+            uint32_t* drow = reinterpret_cast<uint32_t*>(p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * kTileDirStride(NC));
+            for (int w = tid; w <= NW; w += T) drow[w] = s_cw[w];
         }
-        if (FG_TILE_LATE_PREFETCH && t0 + TILE < end) load(t0 + TILE, ka, ta);
+        const uint32_t tile_total = s_cw[NW];
+        // stage the tile bucket sorted (the values arrive here), then write it back in place
+#pragma unroll
+        for (int hh = 0; hh < H; hh++) {
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                const uint32_t rc = rcb[hh][u];
+                if (rc == 0xffffffffu) continue;
+                const uint32_t cb = rc & 4095u;
+                const uint32_t slot = ((s_cw[cb >> 1] >> ((cb & 1u) * 16u)) & 0xffffu) + (rc >> 12);
+                s_k[slot] = k32[hh][u];
+                s_v[slot] = (unsigned long long)((u & 1) ? va[hh][u >> 1].y : va[hh][u >> 1].x);
+            }
+        }
+        if (t0 + TILE < end) load(t0 + TILE, ka, ta);   // the next tile's first half, across the write-out
         lds_barrier();
         for (uint32_t i = tid; i < tile_total; i += T) st_rec12(p.tmp, (uint64_t)(t0 + i), (int64_t)s_k[i], (int64_t)s_v[i]);
         lds_barrier();   // staging and the directory row have read the offsets
-        for (int c = tid; c <= NC; c += T) s_cc[c] = 0;
+        for (int w = tid; w <= NW; w += T) s_cw[w] = 0;
         lds_barrier();
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -3026,14 +3054,14 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
 }
 
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
-    if (p.n_coarse < 1 || p.n_coarse > kMaxTileBuckets || p.region_bits < kTileBits || !p.tmp || !p.dir ||
-        p.vnull != nullptr)
+    if (p.n_coarse < 2 || p.n_coarse % 2 != 0 || p.n_coarse > kMaxTileBuckets || p.region_bits < kTileBits || !p.tmp ||
+        !p.dir || p.vnull != nullptr)
         return hipErrorInvalidValue;
     fg_launch(k_tile_part1, dim3(p.grid), dim3(kTileThreads), 0, s, p);
     return hipGetLastError();
 }
 
-// dir [tiles][nc + 1] (u16 offsets) -> dt [nc][tiles] = offset | length << 16, 64 x 64 blocks
+// dir [tiles][kTileDirStride(nc)] (u16 offsets, [nc] the total) -> dt [nc][tiles] = offset | length << 16, 64 x 64 blocks
 // through LDS; buckets of lanes without records (lane_mask) are skipped
 __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t NT, int32_t NC, int32_t lshift,
                                                    const unsigned long long* lane_mask, uint32_t* dt) {
@@ -3047,7 +3075,7 @@ __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t 
     for (int i = threadIdx.x; i < 64 * 65; i += 256) {
         const int tt = i / 65, cc = i % 65;
         const int t = tb + tt, c = cb + cc;
-        s[tt][cc] = (t < NT && c <= NC) ? gbl(dir)[(int64_t)t * (NC + 1) + c] : (uint16_t)0;
+        s[tt][cc] = (t < NT && c <= NC) ? gbl(dir)[(int64_t)t * kTileDirStride(NC) + c] : (uint16_t)0;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * 64; i += 256) {
