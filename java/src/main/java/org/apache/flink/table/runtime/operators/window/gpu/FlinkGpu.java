@@ -78,13 +78,19 @@ public final class FlinkGpu {
     public static native void advanceProgressAsync(long h, long watermark);
 
     /**
-     * fg_collect_fired: waits for the fires of every async advance since the last collect; fills
-     * cols as {@link #advanceProgress} (device columns); returns the row count.
+     * fg_collect_fired_to(FG_HOST): waits for the fires of every async advance since the last
+     * collect; fills cols as {@link #advanceProgress} (host memory); returns the row count.
      */
     public static native long collectFired(long h, ByteBuffer[] cols);
 
     /** fg_flush (prepareSnapshotPreBarrier). */
     public static native void flush(long h);
+
+    /**
+     * fg_flush_partials (FG_FLAG_LOCAL_PARTIALS handles): every buffered slice's partial rows, in
+     * host memory; cols (length >= 10) as {@link #advanceProgress}; returns the row count.
+     */
+    public static native long flushPartials(long h, ByteBuffer[] cols);
 
     /**
      * fg_snapshot_state: cols (length 7) receives key, slice_end, cnt_star, cnt_val, sum, min, max;

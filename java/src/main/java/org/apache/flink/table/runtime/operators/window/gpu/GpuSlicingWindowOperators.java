@@ -1,23 +1,37 @@
 /*
- * The plug point: SlicingWindowAggOperatorBuilder.build (SlicingWindowAggOperatorBuilder
- * .java:127-170) builds `new SlicingWindowOperator<>(windowProcessor)` around the processor it
- * picks at :146-170; with the GPU engine enabled it returns create(spec) instead (see
- * INTEGRATION.md for the two-line builder change). The local phase of the two-phase plan
- * (StreamExecLocalWindowAggregate.java:149-155) passes a spec with FLAG_LOCAL_PARTIALS.
+ * The plug points of the GPU engine in the planner's window-aggregate translation
+ * (INTEGRATION.md section 5 has the builder lines):
+ *
+ *   create(spec, zone)        SlicingWindowAggOperatorBuilder.build (SlicingWindowAggOperatorBuilder
+ *                             .java:127-170) returns this operator -- the engine holds the window
+ *                             state and fires windows (single-phase, and the global phase of the
+ *                             two-phase plan with spec.partialInput)
+ *   recordsBuffer(spec)       the WindowBuffer.Factory the builder passes to the reference's own
+ *                             processors instead of RecordsWindowBuffer.Factory: GPU
+ *                             pre-aggregation, the reference's state and timers
+ *   localBuffer(spec)         StreamExecLocalWindowAggregate.java:149-155: the LocalFactory of the
+ *                             unchanged LocalSlicingWindowAggOperator (local phase)
  */
 package org.apache.flink.table.runtime.operators.window.gpu;
 
-import org.apache.flink.table.data.RowData;
-import org.apache.flink.table.runtime.operators.window.slicing.SlicingWindowOperator;
+import org.apache.flink.table.runtime.operators.aggregate.window.buffers.WindowBuffer;
 
-/** Factory of GPU-backed slicing window operators. */
+import java.time.ZoneId;
+
+/** Factories of the GPU engine's window-aggregate operators and buffers. */
 public final class GpuSlicingWindowOperators {
     private GpuSlicingWindowOperators() {}
 
-    public static SlicingWindowOperator<RowData, Long> create(GpuWindowAggSpec spec) {
-        GpuSlicingWindowProcessor processor = new GpuSlicingWindowProcessor(spec);
-        SlicingWindowOperator<RowData, Long> operator = new SlicingWindowOperator<>(processor);
-        processor.attach(operator);
-        return operator;
+    public static GpuSlicingWindowAggOperator create(GpuWindowAggSpec spec, ZoneId shiftTimeZone) {
+        return new GpuSlicingWindowAggOperator(
+                new GpuSlicingWindowProcessor(spec, shiftTimeZone), spec.asyncWatermarks);
+    }
+
+    public static WindowBuffer.Factory recordsBuffer(GpuWindowAggSpec spec) {
+        return new GpuRecordsWindowBuffer.Factory(spec);
+    }
+
+    public static WindowBuffer.LocalFactory localBuffer(GpuWindowAggSpec spec) {
+        return new GpuLocalWindowBuffer.LocalFactory(spec);
     }
 }

@@ -1,25 +1,33 @@
 /*
- * SlicingWindowProcessor<Long> backed by the MI355X engine (libflinkgpu.so through
- * FlinkGpu/JNI). Replaces SliceUnsharedWindowAggProcessor / SliceSharedWindowAggProcessor +
- * RecordsWindowBuffer + AggCombiner (SlicingWindowAggOperatorBuilder.java:146-170):
+ * SlicingWindowProcessor<Long> backed by the MI355X engine (libflinkgpu.so through FlinkGpu/JNI):
+ * replaces SliceUnsharedWindowAggProcessor / SliceSharedWindowAggProcessor + RecordsWindowBuffer
+ * + AggCombiner (SlicingWindowAggOperatorBuilder.java:146-170), and, for the global phase of the
+ * two-phase plan, GlobalAggCombiner (spec.partialInput). The engine keeps the (key, slice)
+ * accumulators in HBM and fires windows itself.
  *
- *   processElement      -> the record is appended to direct column buffers; a full micro-batch
- *                          goes to fg_add_batch (AbstractWindowAggProcessor.java:135-165)
- *   advanceProgress     -> the pending micro-batch, then fg_advance_progress: the engine applies
- *                          the progress gate, flushes, fires the windows whose timers the
- *                          watermark passes and returns their rows, emitted here before
- *                          SlicingWindowOperator forwards the watermark (SlicingWindowOperator
- *                          .java:207-210)
- *   prepareCheckpoint   -> fg_flush, then the resident (key, slice) accumulators are written to
- *                          the keyed state "gpu-window-aggs" (namespace = slice end), as
- *                          AggCombiner.combine writes "window-aggs" (AggCombiner.java:76-115)
- *   fireWindow/clearWindow -> no-ops: the engine fires windows itself, no per-key timer is
- *                          registered (DESIGN.md section 3)
+ *   processElement      the record (or, global phase, the local phase's partial accumulator row)
+ *                       joins columnar micro-batch buffers; a full micro-batch goes to
+ *                       fg_add_batch / fg_add_partials with its key rows interned by ONE
+ *                       dictionary call (AbstractWindowAggProcessor.java:135-165). Processing
+ *                       time: the record carries the operator clock's time, and a processing-time
+ *                       timer is registered once per new slice end (the reference registers one per
+ *                       record, :137-140) -- its firing calls advanceProgress
+ *   advanceProgress     fg_advance_progress: the engine applies the progress gate, fires the windows
+ *                       the progress passes and returns their rows (one dictionary lookup + one
+ *                       arena copy for every fired key row), emitted before the operator forwards
+ *                       the watermark (SlicingWindowOperator.java:207-210)
+ *   advanceAsync / collectHeld   fg_advance_progress_async + fg_collect_fired for an operator that
+ *                       holds the watermark while the fires complete (GpuSlicingWindowAggOperator)
+ *   prepareCheckpoint   fg_flush + fg_snapshot_state: the resident accumulators are written to the
+ *                       reference's own keyed state "window-aggs" (namespace = slice end, the
+ *                       accumulator row in the accSerializer layout, GpuAccRows) and the window
+ *                       timers AggCombiner would hold are registered -- a savepoint the reference
+ *                       processors restore, and restore from (INTEGRATION.md section 6)
+ *   fireWindow / clearWindow  no-ops: the engine fires windows; the timers registered at a
+ *                       checkpoint fire into these no-ops
  *
  * Late drops: the engine counts them; advanceProgress adds the new ones to the operator's
- * numLateRecordsDropped counter, which also drives lateRecordsDroppedRate (a MeterView over
- * that counter, SlicingWindowOperator.java:159-163); watermarkLatency is the operator's own
- * gauge over its timer service's watermark and is unchanged.
+ * numLateRecordsDropped counter (lateRecordsDroppedRate is a MeterView over it).
  */
 package org.apache.flink.table.runtime.operators.window.gpu;
 
@@ -28,52 +36,77 @@ import org.apache.flink.api.common.state.ValueStateDescriptor;
 import org.apache.flink.api.common.typeutils.TypeSerializer;
 import org.apache.flink.api.common.typeutils.base.LongSerializer;
 import org.apache.flink.api.java.tuple.Tuple2;
-import org.apache.flink.core.memory.MemorySegmentFactory;
+import org.apache.flink.metrics.Counter;
 import org.apache.flink.runtime.state.CheckpointableKeyedStateBackend;
 import org.apache.flink.runtime.state.KeyGroupRange;
 import org.apache.flink.runtime.state.KeyedStateBackend;
+import org.apache.flink.runtime.state.internal.InternalValueState;
+import org.apache.flink.streaming.api.operators.InternalTimerService;
 import org.apache.flink.table.data.GenericRowData;
 import org.apache.flink.table.data.RowData;
 import org.apache.flink.table.data.TimestampData;
 import org.apache.flink.table.data.binary.BinaryRowData;
 import org.apache.flink.table.data.utils.JoinedRowData;
-import org.apache.flink.table.runtime.operators.window.slicing.SlicingWindowOperator;
+import org.apache.flink.table.runtime.operators.window.TimeWindow;
 import org.apache.flink.table.runtime.operators.window.slicing.SlicingWindowProcessor;
+import org.apache.flink.table.runtime.operators.window.slicing.WindowTimerService;
+import org.apache.flink.table.runtime.operators.window.slicing.WindowTimerServiceImpl;
+import org.apache.flink.table.runtime.operators.window.state.WindowValueState;
 
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.time.ZoneId;
 import java.util.ArrayList;
+import java.util.HashMap;
+import java.util.HashSet;
 import java.util.List;
+import java.util.Map;
+import java.util.Set;
 import java.util.stream.Collectors;
+
+import static org.apache.flink.table.runtime.util.TimeWindowUtil.isWindowFired;
+import static org.apache.flink.table.runtime.util.TimeWindowUtil.toUtcTimestampMills;
 
 /** The slicing window processor of the GPU engine. */
 public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<Long> {
     private static final long serialVersionUID = 1L;
-    static final String STATE_NAME = "gpu-window-aggs";
+    /** the reference's state name (AbstractWindowAggProcessor.java:103-107) */
+    static final String STATE_NAME = "window-aggs";
 
     private final GpuWindowAggSpec spec;
+    private final ZoneId shiftTimeZone;
 
     private transient Context<Long> ctx;
-    private transient SlicingWindowOperator<?, ?> owner;
+    private transient Counter lateDropped;
     private transient long handle;
-    private transient long dict;
-    private transient ByteBuffer keys, rowtimes, vals, nulls;
-    private transient ByteBuffer keyRows, keyOffsets, keyLengths;
+    private transient GpuKeyRows keys;
+    private transient GpuAccRows accRows;
+    private transient ByteBuffer keyCol, timeCol, valCol, nullCol;
+    private transient ByteBuffer csCol, cvCol, sumCol, minCol, maxCol;   // partial input
     private transient int count;
-    private transient int keyBytes;
     private transient long droppedSeen;
-    private transient ValueState<GenericRowData> state;
+    private transient WindowValueState<Long> windowState;
+    private transient WindowTimerService<Long> timerService;
+    private transient long lastProcTimer;
+    private transient boolean asyncPending;
+    private transient boolean batchHanded;
 
-    public GpuSlicingWindowProcessor(GpuWindowAggSpec spec) {
+    public GpuSlicingWindowProcessor(GpuWindowAggSpec spec, ZoneId shiftTimeZone) {
         this.spec = spec;
+        this.shiftTimeZone = shiftTimeZone;
     }
 
-    /** the operator whose numLateRecordsDropped the engine's drop count feeds */
-    public void attach(SlicingWindowOperator<?, ?> operator) {
-        this.owner = operator;
+    /** the operator's numLateRecordsDropped, fed from the engine's drop count */
+    void attach(Counter numLateRecordsDropped) {
+        this.lateDropped = numLateRecordsDropped;
+    }
+
+    private boolean proctime() {
+        return (spec.flags & FgConfig.FLAG_PROCTIME) != 0;
     }
 
     @Override
+    @SuppressWarnings("unchecked")
     public void open(Context<Long> context) throws Exception {
         this.ctx = context;
         KeyedStateBackend<RowData> backend = ctx.getKeyedStateBackend();
@@ -82,64 +115,73 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         int nTz = spec.tzTransitionsMs == null ? 0 : spec.tzTransitionsMs.length;
         handle =
                 FlinkGpu.open(
-                        FgConfig.of(
-                                spec, maxP, range.getStartKeyGroup(), range.getEndKeyGroup(), nTz),
+                        FgConfig.of(spec, maxP, range.getStartKeyGroup(), range.getEndKeyGroup(), nTz),
                         spec.tzTransitionsMs,
                         spec.tzOffsetsMs);
-        if (!spec.bigintKey) {
-            dict = FlinkGpu.dictOpen(spec.device, maxP, spec.expectedKeys);
-            keyRows = direct(64L * spec.batchRecords);
-            keyOffsets = direct(8L * spec.batchRecords);
-            keyLengths = direct(4L * spec.batchRecords);
-        }
-        keys = direct(8L * spec.batchRecords);
-        rowtimes = direct(8L * spec.batchRecords);
-        vals = direct(8L * spec.batchRecords);
-        nulls = direct(spec.batchRecords);
+        keys = new GpuKeyRows(spec, maxP);
+        accRows = new GpuAccRows(spec.aggs, spec.valType);
+        int b = spec.batchRecords;
+        keyCol = GpuKeyRows.direct(8L * b);
+        timeCol = GpuKeyRows.direct(8L * b);
+        valCol = GpuKeyRows.direct(8L * b);
+        nullCol = GpuKeyRows.direct(b);
         // the staging columns live for the operator's life: page-lock them once, so every
         // micro-batch is DMA'd straight from them (fg_host_register)
-        for (ByteBuffer b : new ByteBuffer[] {keys, rowtimes, vals, nulls}) {
-            FlinkGpu.hostRegister(spec.device, b);
+        for (ByteBuffer c : new ByteBuffer[] {keyCol, timeCol, valCol, nullCol}) {
+            FlinkGpu.hostRegister(spec.device, c);
         }
-        state =
-                backend.getPartitionedState(
-                        LongSerializer.INSTANCE.createInstance(),
-                        LongSerializer.INSTANCE,
-                        new ValueStateDescriptor<>(STATE_NAME, GenericRowData.class));
+        if (spec.partialInput) {
+            csCol = GpuKeyRows.direct(8L * b);
+            cvCol = GpuKeyRows.direct(8L * b);
+            sumCol = GpuKeyRows.direct(8L * b);
+            minCol = GpuKeyRows.direct(8L * b);
+            maxCol = GpuKeyRows.direct(8L * b);
+        }
+        ValueState<RowData> state =
+                backend.getOrCreateKeyedState(
+                        LongSerializer.INSTANCE, new ValueStateDescriptor<>(STATE_NAME, accRows.serializer()));
+        windowState = new WindowValueState<>((InternalValueState<RowData, Long, RowData>) state);
+        timerService = new WindowTimerServiceImpl(ctx.getTimerService(), shiftTimeZone);
+        lastProcTimer = Long.MIN_VALUE;
         restoreFromKeyedState(backend);
     }
 
-    private static ByteBuffer direct(long bytes) {
-        return ByteBuffer.allocateDirect((int) Math.max(bytes, 8)).order(ByteOrder.nativeOrder());
-    }
+    // ---- input ------------------------------------------------------------------------------
 
     @Override
     public boolean processElement(RowData key, RowData element) throws Exception {
-        if (spec.bigintKey) {
-            keys.putLong(8 * count, key.getLong(0));
-        } else {
-            BinaryRowData row = (BinaryRowData) key;   // BinaryRowDataKeySelector output
-            int len = row.getSizeInBytes();
-            if (keyBytes + len > keyRows.capacity()) {
-                flushBatch();
-            }
-            keyRows.position(keyBytes);   // (the selector's copy: one segment)
-            row.getSegments()[0].get(row.getOffset(), keyRows, len);
-            keyOffsets.putLong(8 * count, keyBytes);
-            keyLengths.putInt(4 * count, len);
-            keyBytes += (len + 7) & ~7;
+        if (!keys.fits(key)) {
+            flushBatch();
         }
-        rowtimes.putLong(8 * count, element.getTimestamp(spec.rowtimeIndex, 3).getMillisecond());
-        if (spec.valueIndex >= 0) {
-            boolean isNull = element.isNullAt(spec.valueIndex);
-            nulls.put(count, (byte) (isNull ? 1 : 0));
-            long bits =
-                    isNull
-                            ? 0L
-                            : spec.valType == FgConfig.VAL_F64
-                                    ? Double.doubleToRawLongBits(element.getDouble(spec.valueIndex))
-                                    : element.getLong(spec.valueIndex);
-            vals.putLong(8 * count, bits);
+        keys.add(key, count, keyCol);
+        if (spec.partialInput) {
+            // LocalAggCombiner's row (key, acc..., slice_end): the accumulators from valueIndex
+            long[] p = accRows.toPartial(element, spec.valueIndex);
+            timeCol.putLong(8 * count, element.getLong(spec.rowtimeIndex));
+            csCol.putLong(8 * count, p[0]);
+            cvCol.putLong(8 * count, p[1]);
+            sumCol.putLong(8 * count, p[2]);
+            minCol.putLong(8 * count, p[3]);
+            maxCol.putLong(8 * count, p[4]);
+        } else {
+            long t;
+            if (proctime()) {
+                t = ctx.getTimerService().currentProcessingTime();
+                registerProcTimer(t);
+            } else {
+                t = element.getTimestamp(spec.rowtimeIndex, 3).getMillisecond();
+            }
+            timeCol.putLong(8 * count, t);
+            if (spec.valueIndex >= 0) {
+                boolean isNull = element.isNullAt(spec.valueIndex);
+                nullCol.put(count, (byte) (isNull ? 1 : 0));
+                valCol.putLong(
+                        8 * count,
+                        isNull ? 0L
+                                : spec.valType == FgConfig.VAL_F64
+                                        ? Double.doubleToRawLongBits(element.getDouble(spec.valueIndex))
+                                        : element.getLong(spec.valueIndex));
+            }
         }
         if (++count == spec.batchRecords) {
             flushBatch();
@@ -147,139 +189,230 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         return false;   // late drops are counted by the engine (see advanceProgress)
     }
 
+    /** the slice grid: TUMBLE size, HOP gcd(size, slide), CUMULATE step (SliceAssigners.java:59-96) */
+    private long sliceSize() {
+        if (spec.windowKind == FgConfig.TUMBLE) {
+            return spec.sizeMs;
+        }
+        if (spec.windowKind == FgConfig.HOP) {
+            long a = spec.sizeMs, c = spec.slideMs;
+            while (c != 0) {
+                long t = a % c;
+                a = c;
+                c = t;
+            }
+            return a;
+        }
+        return spec.slideMs;
+    }
+
+    /** window ends: TUMBLE every size, HOP every slide, CUMULATE every step (getSliceEndInterval) */
+    private long windowInterval() {
+        return spec.windowKind == FgConfig.TUMBLE ? spec.sizeMs : spec.slideMs;
+    }
+
+    /**
+     * one processing-time timer per new slice end (under the current key: SlicingWindowOperator
+     * .onProcessingTime advances the progress for any key's timer, and the engine fires every key)
+     */
+    private void registerProcTimer(long now) {
+        long s = sliceSize();
+        long end = TimeWindow.getWindowStartWithOffset(toUtcTimestampMills(now, shiftTimeZone), spec.offsetMs, s) + s;
+        if (end > lastProcTimer) {
+            timerService.registerProcessingTimeWindowTimer(end);
+            lastProcTimer = end;
+        }
+    }
+
     /** hands the gathered micro-batch to the engine (which has read it when this returns) */
     private void flushBatch() {
         if (count == 0) {
             return;
         }
-        if (!spec.bigintKey) {   // key rows -> dictionary ids (BinarySection.equals identity)
-            FlinkGpu.dictIntern(dict, keyRows, keyBytes, keyOffsets, keyLengths, count, keys, null);
-            keyBytes = 0;
+        keys.intern(count, keyCol);
+        if (spec.partialInput) {
+            boolean mv = accRows.multiValue();
+            FlinkGpu.addPartials(
+                    handle, count, keyCol, timeCol, csCol, cvCol, sumCol, mv ? minCol : null, mv ? maxCol : null);
+        } else {
+            FlinkGpu.addBatch(
+                    handle,
+                    keyCol,
+                    timeCol,
+                    spec.valueIndex >= 0 ? valCol : null,
+                    spec.valueIndex >= 0 ? nullCol : null,
+                    count);
         }
-        FlinkGpu.addBatch(
-                handle,
-                keys,
-                rowtimes,
-                spec.valueIndex >= 0 ? vals : null,
-                spec.valueIndex >= 0 ? nulls : null,
-                count);
         count = 0;
+        batchHanded = true;
     }
+
+    /** a micro-batch went to the engine since the last call (the operator releases a held watermark) */
+    boolean takeBatchHanded() {
+        boolean b = batchHanded;
+        batchHanded = false;
+        return b;
+    }
+
+    // ---- progress ---------------------------------------------------------------------------
 
     @Override
     public void advanceProgress(long progress) throws Exception {
         flushBatch();
+        collectHeld();   // (an operator's async progress: its rows first, in order)
         ByteBuffer[] cols = new ByteBuffer[5 + spec.aggs.length];
-        long n = FlinkGpu.advanceProgress(handle, progress, cols);
+        emit(cols, FlinkGpu.advanceProgress(handle, progress, cols));
+    }
+
+    /** fg_advance_progress_async: the fires are queued; collectHeld() returns their rows */
+    void advanceAsync(long progress) {
+        flushBatch();
+        FlinkGpu.advanceProgressAsync(handle, progress);
+        asyncPending = true;
+    }
+
+    /** the rows of every async advance since the last collect (fg_collect_fired, host memory) */
+    void collectHeld() {
+        if (!asyncPending) {
+            return;
+        }
+        asyncPending = false;
+        ByteBuffer[] cols = new ByteBuffer[5 + spec.aggs.length];
+        emit(cols, FlinkGpu.collectFired(handle, cols));
+    }
+
+    /** fired rows -> JoinedRowData(key, [aggs..., window_start, window_end]) (collect :223-226) */
+    private void emit(ByteBuffer[] cols, long n) {
         for (ByteBuffer c : cols) {
             if (c != null) {
                 c.order(ByteOrder.nativeOrder());
             }
         }
+        int nAggs = spec.aggs.length;
+        RowData[] keyRows = keys.rows(cols[0], (int) n);
         for (int i = 0; i < n; i++) {
-            ctx.output(outputRow(cols, i));
+            byte nullMask = cols[3 + nAggs].get(i);
+            GenericRowData aggs = new GenericRowData(nAggs + 2);
+            for (int a = 0; a < nAggs; a++) {
+                if ((nullMask >> a & 1) != 0) {
+                    continue;   // NULL
+                }
+                long bits = cols[3 + a].getLong(8 * i);
+                int agg = spec.aggs[a];
+                boolean valueTyped = agg != FgConfig.AGG_COUNT_STAR && agg != FgConfig.AGG_COUNT;
+                aggs.setField(
+                        a,
+                        valueTyped && spec.valType == FgConfig.VAL_F64
+                                ? (Object) Double.longBitsToDouble(bits)
+                                : (Object) bits);
+            }
+            aggs.setField(nAggs, TimestampData.fromEpochMillis(cols[1].getLong(8 * i)));
+            aggs.setField(nAggs + 1, TimestampData.fromEpochMillis(cols[2].getLong(8 * i)));
+            ctx.output(new JoinedRowData(keyRows[i], aggs));
         }
         long dropped = FlinkGpu.lateDropped(handle);
-        if (owner != null && dropped > droppedSeen) {
-            owner.getNumLateRecordsDropped().inc(dropped - droppedSeen);
+        if (lateDropped != null && dropped > droppedSeen) {
+            lateDropped.inc(dropped - droppedSeen);
         }
         droppedSeen = dropped;
     }
 
-    /** JoinedRowData(key, [aggs..., window_start, window_end]) (AbstractWindowAggProcessor.collect) */
-    private RowData outputRow(ByteBuffer[] cols, int i) {
-        long key = cols[0].getLong(8 * i);
-        int nAggs = spec.aggs.length;
-        byte nullMask = cols[3 + nAggs].get(i);
-        GenericRowData aggs = new GenericRowData(nAggs + 2);
-        for (int a = 0; a < nAggs; a++) {
-            if ((nullMask >> a & 1) != 0) {
-                continue;   // NULL
-            }
-            long bits = cols[3 + a].getLong(8 * i);
-            int agg = spec.aggs[a];
-            boolean valueTyped = agg != FgConfig.AGG_COUNT_STAR && agg != FgConfig.AGG_COUNT;
-            aggs.setField(
-                    a,
-                    valueTyped && spec.valType == FgConfig.VAL_F64
-                            ? (Object) Double.longBitsToDouble(bits)
-                            : (Object) bits);
-        }
-        aggs.setField(nAggs, TimestampData.fromEpochMillis(cols[1].getLong(8 * i)));
-        aggs.setField(nAggs + 1, TimestampData.fromEpochMillis(cols[2].getLong(8 * i)));
-        return new JoinedRowData(keyRow(key), aggs);
-    }
-
-    private RowData keyRow(long key) {
-        if (spec.bigintKey) {
-            return GenericRowData.of(key);
-        }
-        ByteBuffer id = direct(8);
-        id.putLong(0, key);
-        ByteBuffer off = direct(8);
-        ByteBuffer len = direct(4);
-        FlinkGpu.dictLookup(dict, id, 1, off, len);
-        int n = len.getInt(0);
-        ByteBuffer bytes = direct(n);
-        FlinkGpu.dictCopyArena(dict, off.getLong(0), n, bytes);
-        byte[] b = new byte[n];
-        bytes.get(b);
-        BinaryRowData row = new BinaryRowData(spec.keyArity);
-        row.pointTo(MemorySegmentFactory.wrap(b), 0, n);
-        return row;
-    }
+    // ---- checkpoints ------------------------------------------------------------------------
 
     @Override
     public void prepareCheckpoint() throws Exception {
         flushBatch();
+        collectHeld();
         FlinkGpu.flush(handle);
         writeKeyedState();
     }
 
     /**
-     * The window-aggs image into keyed state: per (key, slice end) one row (cnt_star, cnt_val,
-     * sum, min, max), as AggCombiner.combine leaves one accumulator per (key, slice). Entries of
-     * slices fired since the last checkpoint are removed first.
+     * The engine's (key, slice) accumulators into "window-aggs" as the reference keeps them, and
+     * the window timers AggCombiner / SliceSharedWindowAggProcessor would hold:
+     *  - one accumulator row per (key, slice end) in the accSerializer layout; CUMULATE slices of
+     *    windows that have fired are merged into the window's first slice, as
+     *    CumulativeSliceAssigner.mergeSlices leaves them (SliceAssigners.java:359-370);
+     *  - an event-time window timer at every unfired slice end holding state (AggCombiner.java:
+     *    104-112) and, for a key holding state of fired slices only (HOP / CUMULATE), at the next
+     *    window end after the progress (fireWindow's nextTriggerWindow registration).
+     * The image of the previous checkpoint (entries, timers) is replaced.
      */
     private void writeKeyedState() throws Exception {
         KeyedStateBackend<RowData> backend = ctx.getKeyedStateBackend();
-        List<Tuple2<RowData, Long>> old =
-                backend.<Long>getKeysAndNamespaces(STATE_NAME).collect(Collectors.toList());
+        InternalTimerService<Long> timers = ctx.getTimerService();
+        List<Tuple2<RowData, Long>> old = backend.<Long>getKeysAndNamespaces(STATE_NAME).collect(Collectors.toList());
         for (Tuple2<RowData, Long> kn : old) {
             backend.setCurrentKey(kn.f0);
-            backend.getPartitionedState(
-                            kn.f1,
-                            LongSerializer.INSTANCE,
-                            new ValueStateDescriptor<>(STATE_NAME, GenericRowData.class))
-                    .clear();
+            windowState.clear(kn.f1);
         }
+        // (forEachEventTimeTimer sets each timer's key as the current key before the action)
+        List<Tuple2<RowData, Tuple2<Long, Long>>> oldTimers = new ArrayList<>();
+        timers.forEachEventTimeTimer(
+                (w, ts) -> oldTimers.add(Tuple2.of(backend.getCurrentKey(), Tuple2.of(w, ts))));
+        for (Tuple2<RowData, Tuple2<Long, Long>> kt : oldTimers) {
+            backend.setCurrentKey(kt.f0);
+            timers.deleteEventTimeTimer(kt.f1.f0, kt.f1.f1);
+        }
+
         ByteBuffer[] cols = new ByteBuffer[7];
         long[] wm = new long[1];
-        long n = FlinkGpu.snapshotState(handle, cols, wm);
+        int n = (int) FlinkGpu.snapshotState(handle, cols, wm);
         for (ByteBuffer c : cols) {
             if (c != null) {
                 c.order(ByteOrder.nativeOrder());
             }
         }
+        final long progress = wm[0];
+        RowData[] keyRows = keys.rows(cols[0], n);
+        Map<BinaryRowData, Map<Long, RowData>> image = new HashMap<>();
+        Set<BinaryRowData> needNextTimer = new HashSet<>();
         for (int i = 0; i < n; i++) {
-            backend.setCurrentKey(keyRow(cols[0].getLong(8 * i)));
-            ValueState<GenericRowData> s =
-                    backend.getPartitionedState(
-                            cols[1].getLong(8 * i),
-                            LongSerializer.INSTANCE,
-                            new ValueStateDescriptor<>(STATE_NAME, GenericRowData.class));
-            s.update(
-                    GenericRowData.of(
+            long slice = cols[1].getLong(8 * i);
+            GenericRowData acc =
+                    accRows.fromPartial(
                             cols[2].getLong(8 * i),
                             cols[3].getLong(8 * i),
                             cols[4].getLong(8 * i),
-                            cols[5] == null ? null : cols[5].getLong(8 * i),
-                            cols[6] == null ? null : cols[6].getLong(8 * i),
-                            wm[0]));
+                            cols[5] == null ? cols[4].getLong(8 * i) : cols[5].getLong(8 * i),
+                            cols[6] == null ? cols[4].getLong(8 * i) : cols[6].getLong(8 * i));
+            BinaryRowData key = (BinaryRowData) keyRows[i];
+            boolean fired = isWindowFired(slice, progress, shiftTimeZone);
+            long target = slice;
+            if (fired && spec.windowKind == FgConfig.CUMULATE) {
+                target = TimeWindow.getWindowStartWithOffset(slice - 1, spec.offsetMs, spec.sizeMs) + spec.slideMs;
+            }
+            Map<Long, RowData> m = image.computeIfAbsent(key, k -> new HashMap<>());
+            RowData prev = m.get(target);
+            m.put(target, prev == null ? acc : accRows.merge(prev, acc));
+            if (fired) {
+                needNextTimer.add(key);
+            }
+        }
+        long interval = windowInterval();
+        long nextEnd =
+                TimeWindow.getWindowStartWithOffset(toUtcTimestampMills(progress, shiftTimeZone), spec.offsetMs, interval)
+                        + interval;
+        for (Map.Entry<BinaryRowData, Map<Long, RowData>> e : image.entrySet()) {
+            backend.setCurrentKey(e.getKey());
+            for (Map.Entry<Long, RowData> s : e.getValue().entrySet()) {
+                windowState.update(s.getKey(), s.getValue());
+                if (!proctime() && !isWindowFired(s.getKey(), progress, shiftTimeZone)) {
+                    timerService.registerEventTimeWindowTimer(s.getKey());
+                }
+            }
+            if (!proctime() && needNextTimer.contains(e.getKey())) {
+                timerService.registerEventTimeWindowTimer(nextEnd);
+            }
         }
     }
 
-    /** initializeState: the keyed image of the subtask's key groups back into the engine */
+    /**
+     * initializeState: "window-aggs" of the subtask's key groups back into the engine (one
+     * dictionary intern of every key row); the timer watermark is the smallest registered window
+     * timer's time - 1: every window ending before it has fired (a key with state holds a timer
+     * at its first unfired window), none after it has.
+     */
     private void restoreFromKeyedState(KeyedStateBackend<RowData> backend) throws Exception {
         List<Tuple2<RowData, Long>> entries =
                 backend.<Long>getKeysAndNamespaces(STATE_NAME).collect(Collectors.toList());
@@ -287,67 +420,34 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
             return;
         }
         int n = entries.size();
-        List<ByteBuffer> c = new ArrayList<>();
+        ByteBuffer[] c = new ByteBuffer[7];
         for (int j = 0; j < 7; j++) {
-            c.add(direct(8L * n));
+            c[j] = GpuKeyRows.direct(8L * n);
         }
-        boolean mv = false;
-        long timerWm = Long.MIN_VALUE;
-        List<byte[]> rows = new ArrayList<>();
+        byte[][] rows = new byte[n][];
         for (int i = 0; i < n; i++) {
             Tuple2<RowData, Long> kn = entries.get(i);
             backend.setCurrentKey(kn.f0);
-            GenericRowData acc =
-                    backend.getPartitionedState(
-                                    kn.f1,
-                                    LongSerializer.INSTANCE,
-                                    new ValueStateDescriptor<>(STATE_NAME, GenericRowData.class))
-                            .value();
+            long[] p = accRows.toPartial(windowState.value(kn.f1), 0);
             if (spec.bigintKey) {
-                c.get(0).putLong(8 * i, kn.f0.getLong(0));
+                c[0].putLong(8 * i, kn.f0.getLong(0));
             } else {
                 BinaryRowData r = (BinaryRowData) kn.f0;
-                byte[] b = new byte[r.getSizeInBytes()];
-                r.getSegments()[0].get(r.getOffset(), b);
-                rows.add(b);
+                rows[i] = new byte[r.getSizeInBytes()];
+                r.getSegments()[0].get(r.getOffset(), rows[i]);
             }
-            c.get(1).putLong(8 * i, kn.f1);
-            for (int j = 0; j < 3; j++) {
-                c.get(2 + j).putLong(8 * i, acc.getLong(j));
+            c[1].putLong(8 * i, kn.f1);
+            for (int j = 0; j < 5; j++) {
+                c[2 + j].putLong(8 * i, p[j]);
             }
-            if (!acc.isNullAt(3)) {
-                mv = true;
-                c.get(5).putLong(8 * i, acc.getLong(3));
-                c.get(6).putLong(8 * i, acc.getLong(4));
-            }
-            timerWm = acc.getLong(5);
         }
-        if (!spec.bigintKey) {   // the image carries key rows: re-intern them first
-            ByteBuffer all = direct(rows.stream().mapToLong(b -> (b.length + 7) & ~7).sum());
-            ByteBuffer off = direct(8L * n);
-            ByteBuffer len = direct(4L * n);
-            int at = 0;
-            for (int i = 0; i < n; i++) {
-                byte[] b = rows.get(i);
-                all.position(at);
-                all.put(b);
-                off.putLong(8 * i, at);
-                len.putInt(4 * i, b.length);
-                at += (b.length + 7) & ~7;
-            }
-            FlinkGpu.dictIntern(dict, all, at, off, len, n, c.get(0), null);
-        }
-        FlinkGpu.restore(
-                handle,
-                n,
-                c.get(0),
-                c.get(1),
-                c.get(2),
-                c.get(3),
-                c.get(4),
-                mv ? c.get(5) : null,
-                mv ? c.get(6) : null,
-                timerWm);
+        keys.internRows(rows, c[0]);
+        long[] minTimer = {Long.MAX_VALUE};
+        ctx.getTimerService()
+                .forEachEventTimeTimer((w, ts) -> minTimer[0] = Math.min(minTimer[0], ts));
+        long timerWm = minTimer[0] == Long.MAX_VALUE ? Long.MIN_VALUE : minTimer[0] - 1;
+        boolean mv = accRows.multiValue();
+        FlinkGpu.restore(handle, n, c[0], c[1], c[2], c[3], c[4], mv ? c[5] : null, mv ? c[6] : null, timerWm);
     }
 
     @Override
@@ -361,13 +461,12 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         if (handle != 0) {
             FlinkGpu.close(handle);
             handle = 0;
-            for (ByteBuffer b : new ByteBuffer[] {keys, rowtimes, vals, nulls}) {
+            for (ByteBuffer b : new ByteBuffer[] {keyCol, timeCol, valCol, nullCol}) {
                 FlinkGpu.hostUnregister(spec.device, b);
             }
         }
-        if (dict != 0) {
-            FlinkGpu.dictClose(dict);
-            dict = 0;
+        if (keys != null) {
+            keys.close();
         }
     }
 

@@ -42,4 +42,46 @@ public final class GpuWindowAggSpec implements Serializable {
 
     /** records gathered before one engine call (one micro-batch) */
     public int batchRecords = 1 << 20;
+
+    /**
+     * global phase of the two-phase plan: input rows are LocalAggCombiner's (key, acc...,
+     * slice_end) -- the accumulators from valueIndex, the slice end (BIGINT) at rowtimeIndex
+     */
+    public boolean partialInput;
+
+    /**
+     * hold each watermark while its fires complete on the GPU (fg_advance_progress_async): the
+     * fired rows, then the watermark, are forwarded once the next micro-batch has been handed over
+     * (or at the next watermark, checkpoint or end of input) -- GpuSlicingWindowAggOperator
+     */
+    public boolean asyncWatermarks = true;
+
+    /** a field-by-field copy (the arrays cloned) */
+    public GpuWindowAggSpec copy() {
+        GpuWindowAggSpec c = new GpuWindowAggSpec();
+        c.mode = mode;
+        c.windowKind = windowKind;
+        c.sizeMs = sizeMs;
+        c.slideMs = slideMs;
+        c.offsetMs = offsetMs;
+        c.shiftTzOffsetMs = shiftTzOffsetMs;
+        c.tzTransitionsMs = tzTransitionsMs == null ? null : tzTransitionsMs.clone();
+        c.tzOffsetsMs = tzOffsetsMs == null ? null : tzOffsetsMs.clone();
+        c.tzUseDaylight = tzUseDaylight;
+        c.valType = valType;
+        c.aggs = aggs.clone();
+        c.flags = flags;
+        c.expectedKeys = expectedKeys;
+        c.bufferRecords = bufferRecords;
+        c.device = device;
+        c.allowedLatenessMs = allowedLatenessMs;
+        c.rowtimeIndex = rowtimeIndex;
+        c.valueIndex = valueIndex;
+        c.bigintKey = bigintKey;
+        c.keyArity = keyArity;
+        c.batchRecords = batchRecords;
+        c.partialInput = partialInput;
+        c.asyncWatermarks = asyncWatermarks;
+        return c;
+    }
 }

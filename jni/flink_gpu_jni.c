@@ -13,6 +13,7 @@
  *   advanceProgressAsync fg_advance_progress_async (the same, the fires queued: the watermark held)
  *   collectFired    fg_collect_fired_to  (the held watermark's rows, in host memory; then the watermark is forwarded)
  *   flush           fg_flush             (prepareSnapshotPreBarrier)
+ *   flushPartials   fg_flush_partials    (local phase: WindowBuffer.flush of LocalSlicingWindowAggOperator)
  *   snapshotState   fg_snapshot_state    (snapshotState: the window-aggs image)
  *   restore         fg_restore           (initializeState)
  *   lateDropped     fg_late_dropped      (numLateRecordsDropped)
@@ -34,6 +35,7 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -179,27 +181,33 @@ JNIEXPORT void JNICALL FN(addPartials)(JNIEnv* env, jclass cls, jlong hp, jint n
     check(env, h, fg_add_partials(h, &p));
 }
 
-/* long advanceProgress(long h, long watermark, ByteBuffer[] cols)
- * cols (length >= 5 + numAggs) receives: key, window_start, window_end, agg[0..numAggs), null_mask,
- * rowtime (DataStream; else null). Returns the number of fired rows. */
+/* the columns of fg_rows into cols (length >= 5 + num_aggs): key, window_start, window_end,
+ * agg[0..num_aggs), null_mask, rowtime (DataStream; else null); returns the row count */
+static jlong put_rows(JNIEnv* env, const fg_rows* r, jobjectArray cols, const char* who) {
+    const jlong n = r->n, bytes = 8 * n;
+    if ((*env)->GetArrayLength(env, cols) < 5 + r->num_aggs) {
+        char msg[96];
+        snprintf(msg, sizeof msg, "%s: column array too short", who);
+        throw_code(env, FG_EINVAL, msg);
+        return 0;
+    }
+    int i = 0;
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r->key, bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r->window_start, bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r->window_end, bytes));
+    for (int a = 0; a < r->num_aggs; a++) (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r->agg[a], bytes));
+    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r->null_mask, n));
+    (*env)->SetObjectArrayElement(env, cols, i++, r->rowtime ? wrap(env, r->rowtime, bytes) : NULL);
+    return n;
+}
+
+/* long advanceProgress(long h, long watermark, ByteBuffer[] cols): the fired rows (put_rows) */
 JNIEXPORT jlong JNICALL FN(advanceProgress)(JNIEnv* env, jclass cls, jlong hp, jlong wm, jobjectArray cols) {
     (void)cls;
     fg_handle* h = (fg_handle*)(intptr_t)hp;
     fg_rows r;
     if (check(env, h, fg_advance_progress(h, wm, FG_HOST, &r))) return 0;
-    const jlong n = r.n, bytes = 8 * n;
-    if ((*env)->GetArrayLength(env, cols) < 5 + r.num_aggs) {
-        throw_code(env, FG_EINVAL, "advanceProgress: column array too short");
-        return 0;
-    }
-    int i = 0;
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.key, bytes));
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_start, bytes));
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_end, bytes));
-    for (int a = 0; a < r.num_aggs; a++) (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.agg[a], bytes));
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.null_mask, n));
-    (*env)->SetObjectArrayElement(env, cols, i++, r.rowtime ? wrap(env, r.rowtime, bytes) : NULL);
-    return n;
+    return put_rows(env, &r, cols, "advanceProgress");
 }
 
 /* void advanceProgressAsync(long h, long watermark): the watermark's fires are queued; the shim
@@ -219,19 +227,7 @@ JNIEXPORT jlong JNICALL FN(collectFired)(JNIEnv* env, jclass cls, jlong hp, jobj
     fg_handle* h = (fg_handle*)(intptr_t)hp;
     fg_rows r;
     if (check(env, h, fg_collect_fired_to(h, FG_HOST, &r))) return 0;
-    const jlong n = r.n, bytes = 8 * n;
-    if ((*env)->GetArrayLength(env, cols) < 5 + r.num_aggs) {
-        throw_code(env, FG_EINVAL, "collectFired: column array too short");
-        return 0;
-    }
-    int i = 0;
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.key, bytes));
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_start, bytes));
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.window_end, bytes));
-    for (int a = 0; a < r.num_aggs; a++) (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.agg[a], bytes));
-    (*env)->SetObjectArrayElement(env, cols, i++, wrap(env, r.null_mask, n));
-    (*env)->SetObjectArrayElement(env, cols, i++, r.rowtime ? wrap(env, r.rowtime, bytes) : NULL);
-    return n;
+    return put_rows(env, &r, cols, "collectFired");
 }
 
 /* void flush(long h) */
@@ -239,6 +235,16 @@ JNIEXPORT void JNICALL FN(flush)(JNIEnv* env, jclass cls, jlong hp) {
     (void)cls;
     fg_handle* h = (fg_handle*)(intptr_t)hp;
     check(env, h, fg_flush(h));
+}
+
+/* long flushPartials(long h, ByteBuffer[] cols): a local-phase handle's partial rows of every
+ * buffered slice, in host memory (LocalSlicingWindowAggOperator's WindowBuffer.flush) */
+JNIEXPORT jlong JNICALL FN(flushPartials)(JNIEnv* env, jclass cls, jlong hp, jobjectArray cols) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_rows r;
+    if (check(env, h, fg_flush_partials(h, FG_HOST, &r))) return 0;
+    return put_rows(env, &r, cols, "flushPartials");
 }
 
 /* long snapshotState(long h, ByteBuffer[] cols, long[] timerWatermark)
