@@ -526,17 +526,22 @@ def main():
     kdict_owner = F.KeyDictionary(max_parallelism=128, expected_keys=int(args.keys / world * 1.05) + 1,
                                   device=local) if strings and two_phase else None
 
-    def partials_round(wm):
-        """local fire -> exchange of partial accumulators -> global merge + fire"""
+    def partials_round(wm, held):
+        """local fire -> exchange of partial accumulators (the watermarks min-combined in-band
+        with the counts) -> [the previous round's global fires collected] -> global merge ->
+        async global fire (held until the next round). Returns (rows collected, bytes sent)."""
         r = op_local.process_watermark(wm, device_output=True)
         # key, slice end, COUNT(*), COUNT(v), SUM (+ MIN, MAX for several value accumulators)
         cols = device_columns(r, aggs=tuple(range(len(op_local.aggs))), device=dev)
-        recv, sent = exchange_partials(cols, max_parallelism=maxp, key_hash=key_hash, via_cpu=via_cpu,
-                                       key_rows=(kdict, kdict_owner) if kdict_owner else None)
+        recv, sent, gwm = exchange_partials(cols, max_parallelism=maxp, key_hash=key_hash, via_cpu=via_cpu,
+                                            key_rows=(kdict, kdict_owner) if kdict_owner else None, watermark=wm)
+        # the previous round's global fires ran behind this round's local batch, local fire and
+        # exchange; their rows go out before this round's partials are merged
+        rows = op.collect_fired().n if held else 0
         # (process_partials orders the engine's stream after torch's: no host synchronization)
         op.process_partials(*recv)
-        g = op.process_watermark(global_watermark(wm, device=dev), device_output=True)
-        return g.n, sent
+        op.process_watermark(gwm, device_output=True, wait=False)
+        return rows, sent
 
     ckpt = dict(n=0, s=0.0, state_rows=0)
 
@@ -591,7 +596,8 @@ def main():
                 if strings and hi < n:
                     k_next = intern(hi)
                 if wms:   # the micro-batch's last watermark (in-order input: same output)
-                    nr, sent = partials_round(wms[-1])
+                    nr, sent = partials_round(wms[-1], held)
+                    held = True
                     rows += nr
                     xgmi += sent
                 continue
@@ -618,8 +624,8 @@ def main():
                     op.process_watermark(wm, device_output=True, wait=False)
                     held = True
         if two_phase:
-            nr, sent = partials_round(JMAX)
-            return rows + nr, xgmi + sent
+            nr, sent = partials_round(JMAX, held)
+            return rows + nr + op.collect_fired().n, xgmi + sent
         if held:
             rows += op.collect_fired().n
         r = op.process_watermark(JMAX, device_output=True)

@@ -116,13 +116,18 @@ def partition_columns_by_owner(cols, parallelism: int, max_parallelism: int = 12
 
 
 def exchange_partials(cols, group=None, max_parallelism: int = 128, key_hash: int = L.KEYHASH_BINARYROW_BIGINT,
-                      via_cpu: bool = False, key_rows=None):
+                      via_cpu: bool = False, key_rows=None, watermark=None):
     """Key-group exchange of partial accumulator rows (int64 device columns, key first).
-    Returns the received columns and the bytes this rank sent to peers.
+    Returns the received columns and the bytes this rank sent to peers -- and, given this
+    rank's `watermark`, the minimum over all ranks (StatusWatermarkValve) as a third value.
 
     Per call: the owner partition (a device counting sort), ONE all-to-all of the per-peer
-    counts, one host read of them (the split sizes of the next collective), ONE all-to-all of
-    the rows packed [n, c] (and, with key_rows, one of the key rows' words).
+    counts with the watermark in-band, ONE host read of them (the split sizes of the next
+    collective, and the combined watermark: no separate all-reduce and no second host read),
+    ONE all-to-all of the rows packed [n, c] (and, with key_rows, one of the key rows' words).
+    The host read stays because the receiving fg_add_partials takes its row count on the host
+    (and RCCL's all-to-all its split sizes); a fixed per-peer capacity would need a bound every
+    rank agrees on beforehand -- world x the rows on the wire, or one more collective per round.
 
     key_rows = (local, owner) dictionaries (flink_amd.keys.KeyDictionary, or any objects with
     the same `locate` / `intern_rows` methods): the key column holds ids of this rank's `local`
@@ -140,17 +145,20 @@ def exchange_partials(cols, group=None, max_parallelism: int = 128, key_hash: in
         key_hash = L.KEYHASH_DICT_ID
     outs, counts = partition_columns_by_owner(cols, world, max_parallelism, key_hash)
     if world == 1 and key_rows is None:
-        return outs, 0
-    return exchange_grouped_columns(outs, counts, group, via_cpu=via_cpu, key_rows=key_rows)
+        return (outs, 0) if watermark is None else (outs, 0, int(watermark))
+    return exchange_grouped_columns(outs, counts, group, via_cpu=via_cpu, key_rows=key_rows, watermark=watermark)
 
 
-def exchange_grouped_columns(outs, counts, group=None, via_cpu: bool = False, key_rows=None):
+def exchange_grouped_columns(outs, counts, group=None, via_cpu: bool = False, key_rows=None, watermark=None):
     """The collective step of exchange_partials: int64 columns already grouped by destination
-    rank (counts[d] rows for rank d; device tensors, or host tensors with gloo)."""
+    rank (counts[d] rows for rank d; device tensors, or host tensors with gloo). With
+    `watermark`, it travels in-band with the counts and the minimum over the ranks is returned
+    as a third value."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     cols = outs
     words = None
+    meta = [counts]
     if key_rows is not None:
         local, owner = key_rows
         woff, nw, arena = local.locate(outs[0])          # the key rows of the local ids
@@ -159,9 +167,10 @@ def exchange_grouped_columns(outs, counts, group=None, via_cpu: bool = False, ke
         at = torch.cat([torch.zeros(1, dtype=cw.dtype, device=cw.device), cw])
         wcounts = at[ends] - at[torch.cat([torch.zeros(1, dtype=ends.dtype, device=ends.device), ends[:-1]])]
         outs = outs + [nw]                                # row lengths (words) travel as a column
-        counts_all = torch.stack([counts, wcounts], dim=1)
-    else:
-        counts_all = counts.view(world, 1)
+        meta.append(wcounts)
+    if watermark is not None:                             # the same value to every peer
+        meta.append(torch.full_like(counts, int(watermark)))
+    counts_all = torch.stack(meta, dim=1)                 # [world, 1 + key_rows + watermark]
     packed = torch.stack(outs, dim=1)                     # [n, c]: one collective for every column
     if via_cpu:
         packed, counts_all = packed.cpu(), counts_all.cpu()
@@ -169,6 +178,7 @@ def exchange_grouped_columns(outs, counts, group=None, via_cpu: bool = False, ke
     dist.all_to_all_single(recv_counts, counts_all, group=group)
     sc, rc = counts_all.cpu(), recv_counts.cpu()          # the one host read per exchange
     send, recv = sc[:, 0].tolist(), rc[:, 0].tolist()
+    wm_min = int(rc[:, -1].min()) if watermark is not None else None
     out = torch.empty((sum(recv), packed.shape[1]), dtype=packed.dtype, device=packed.device)
     dist.all_to_all_single(out, packed, output_split_sizes=recv, input_split_sizes=send, group=group)
     rank = dist.get_rank(group)
@@ -197,7 +207,7 @@ def exchange_grouped_columns(outs, counts, group=None, via_cpu: bool = False, ke
         rlen = cols_out.pop() * 4                          # bytes per received row
         roff = torch.cumsum(rlen, 0) - rlen
         cols_out[0] = owner.intern_rows(rwords.view(torch.uint8), roff, rlen.to(torch.int32))
-    return cols_out, sent_bytes
+    return (cols_out, sent_bytes) if watermark is None else (cols_out, sent_bytes, wm_min)
 
 
 def exchange_columns(cols, counts, group=None):

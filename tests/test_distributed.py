@@ -113,7 +113,7 @@ def _two_phase_rank(rank, world, port, kind, out_q, columns=False):
     import torch
     import torch.distributed as dist
 
-    from flink_amd.exchange import exchange_columns, exchange_grouped, global_watermark
+    from flink_amd.exchange import exchange_columns, exchange_grouped, exchange_grouped_columns, global_watermark
     from oracle import oracle as O
     from tests.streams import make_stream
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -137,7 +137,12 @@ def _two_phase_rank(rank, world, port, kind, out_q, columns=False):
         part = part[np.argsort(owner, kind="stable")]
         counts = torch.from_numpy(np.bincount(owner, minlength=world).astype(np.int64))
         packed = torch.from_numpy(part.view(np.int64).reshape(len(part), O.ROW_DTYPE.itemsize // 8).copy())
-        if columns:   # exchange_partials' form: one all-to-all per column
+        gwm = None
+        if columns == "inband":   # bench.py's form: the watermark travels with the counts
+            rc, sent, gwm = exchange_grouped_columns([packed[:, j].contiguous() for j in range(packed.shape[1])],
+                                                     counts, watermark=local_wm)
+            recv = torch.stack(rc, dim=1) if rc else packed[:0]
+        elif columns:   # one all-to-all per column
             rc, sent = exchange_columns([packed[:, j].contiguous() for j in range(packed.shape[1])], counts)
             recv = torch.stack(rc, dim=1) if rc else packed[:0]
         else:
@@ -146,7 +151,7 @@ def _two_phase_rank(rank, world, port, kind, out_q, columns=False):
         got = np.ascontiguousarray(recv.numpy()).view(O.ROW_DTYPE).reshape(-1)
         glob.process_partials(got)
         # StatusWatermarkValve: the global operator's watermark is the min over its inputs
-        glob.process_watermark(global_watermark(local_wm))
+        glob.process_watermark(global_watermark(local_wm) if gwm is None else gwm)
         rows.append(glob.take_rows())
 
     for lo in range(0, TP_N, TP_BATCH):
@@ -160,7 +165,8 @@ def _two_phase_rank(rank, world, port, kind, out_q, columns=False):
 
 
 @pytest.mark.parametrize("kind,columns", [("tumble", False), ("hop", False), ("cumulate", False),
-                                          ("tumble", True), ("hop", True)])
+                                          ("tumble", True), ("hop", True), ("tumble", "inband"),
+                                          ("cumulate", "inband")])
 def test_two_phase_exchange_matches_single_operator(oracle_mod, kind, columns):
     """Two ranks run the local phase on their source partitions, exchange the partial
     accumulator rows by key-group owner (flink_amd.exchange.exchange_grouped, or exchange_columns:
