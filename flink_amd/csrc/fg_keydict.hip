@@ -49,6 +49,9 @@ constexpr int kDictThreads = 256;
 #define FG_DICT_GROW 4   // table rebuilt at FG_DICT_GROW x (ids + 1M) slots (>= 2: room for a chunk)
 #endif
 static_assert(FG_DICT_GROW >= 2, "FG_DICT_GROW: the table must stay at most half full after a rebuild");
+#ifndef FG_DICT_INIT
+#define FG_DICT_INIT 2   // slots at open: FG_DICT_INIT x expected keys, rounded up to a power of two
+#endif
 // id = ordinal << kg_bits | key group, kg_bits = dict_kg_bits(max parallelism) (7 at Flink's
 // default 128): ids stay below 2^31 for 16.7M keys, so the window engine stages them as narrow
 // 32-bit keys (fg_window.h key_group_of reads the key group back from the low bits)
@@ -303,48 +306,73 @@ __device__ __forceinline__ Slot load_slot(const Slot* p) {
 // holds tag, length, id and the row's first 40 bytes), the byte comparison, the id. A row whose
 // tag is not in the table joins the miss list (counters[6]); a distinct row with an equal tag
 // gets -1 (counters[2], resolved on the host). kg_out (optional) takes every row's key group.
+// Each thread takes kLookupRows rows (a block's rows in kLookupRows coalesced strides) and issues
+// all their slot loads before resolving any.
+#ifndef FG_DICT_ROWS
+#define FG_DICT_ROWS 1   // rows per thread (A/B in DESIGN.md)
+#endif
+constexpr int kLookupRows = FG_DICT_ROWS;
 __global__ __launch_bounds__(kDictThreads) void k_dict_lookup(DictDev d, RowsIn in, int32_t* kg_out, int64_t* id_out,
                                                               uint32_t* miss) {
-    const int64_t i0 = (int64_t)blockIdx.x * kDictThreads + threadIdx.x;
-    const bool valid = i0 < in.n;   // (every lane stays for the wave-wide reservation below)
-    const int64_t i = valid ? i0 : 0;
-    const int32_t len = in.len[i];
-    const uint8_t* rp = in.bytes + in.off[i];
-    const bool small = len <= 4 * kRegWords;
-    uint32_t r[kRegWords];
-    uint64_t t;
-    int32_t fh;
-    if (small) {
-        row_words(rp, len, r);
-        row_hashes_reg(r, len, in.tag_bits, &t, &fh);
-    } else {
+    constexpr int R = kLookupRows;
+    const int64_t b0 = (int64_t)blockIdx.x * kDictThreads * R + threadIdx.x;
+    int64_t ii[R];
+    bool valid[R], small[R];
+    int32_t len[R], fh[R];
+    const uint8_t* rp[R];
+    uint32_t r[R][kRegWords];
+    uint64_t t[R], s[R];
 #pragma unroll
-        for (int k = 0; k < kRegWords; k++) r[k] = 0;
-        row_hashes(reinterpret_cast<const uint32_t*>(rp), len, in.tag_bits, &t, &fh);
+    for (int u = 0; u < R; u++) {   // (every lane stays for the wave-wide reservations below)
+        const int64_t i0 = b0 + (int64_t)u * kDictThreads;
+        valid[u] = i0 < in.n;
+        ii[u] = valid[u] ? i0 : 0;
+        len[u] = in.len[ii[u]];
+        rp[u] = in.bytes + in.off[ii[u]];
     }
-    uint64_t s = fmix64(t) & d.mask;
-    bool found = false;
-    int64_t id = -1;
-    for (; valid;) {
-        const Slot sl = load_slot(&d.slots[s]);
-        if (sl.tag == t) {   // (every slot is written: no claims run beside the lookup)
-            found = true;
-            id = slot_id_if_equal(d, sl, r, reinterpret_cast<const uint32_t*>(rp), small, len);
-            break;
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+        small[u] = len[u] <= 4 * kRegWords;
+        if (small[u]) {
+            row_words(rp[u], len[u], r[u]);
+            row_hashes_reg(r[u], len[u], in.tag_bits, &t[u], &fh[u]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < kRegWords; k++) r[u][k] = 0;
+            row_hashes(reinterpret_cast<const uint32_t*>(rp[u]), len[u], in.tag_bits, &t[u], &fh[u]);
         }
-        if (sl.tag == 0) break;
-        s = (s + 1) & d.mask;
+        s[u] = fmix64(t[u]) & d.mask;
     }
-    if (valid) {
-        if (kg_out) kg_out[i] = murmur_hash(fh) % in.max_p;
-        if (found) {
-            if (id < 0) atomicAdd(&d.counters[2], 1ull);
-            id_out[i] = id;
+    Slot sl[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) sl[u] = load_slot(&d.slots[s[u]]);   // every row's line in flight
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+        bool found = false;
+        int64_t id = -1;
+        if (valid[u]) {
+            Slot cur = sl[u];
+            uint64_t at = s[u];
+            for (;;) {   // (the home slot resolves almost every row; probing past it is rare)
+                if (cur.tag == t[u]) {   // (every slot is written: no claims run beside the lookup)
+                    found = true;
+                    id = slot_id_if_equal(d, cur, r[u], reinterpret_cast<const uint32_t*>(rp[u]), small[u], len[u]);
+                    break;
+                }
+                if (cur.tag == 0) break;
+                at = (at + 1) & d.mask;
+                cur = load_slot(&d.slots[at]);
+            }
+            if (kg_out) kg_out[ii[u]] = murmur_hash(fh[u]) % in.max_p;
+            if (found) {
+                if (id < 0) atomicAdd(&d.counters[2], 1ull);
+                id_out[ii[u]] = id;
+            }
         }
+        const bool m = valid[u] && !found;
+        const unsigned long long w = wave_reserve(&d.counters[6], m ? 1u : 0u);
+        if (m) miss[w] = (uint32_t)ii[u];
     }
-    const bool m = valid && !found;
-    const unsigned long long at = wave_reserve(&d.counters[6], m ? 1u : 0u);
-    if (m) miss[at] = (uint32_t)i;
 }
 
 // Pending rows (their slot is new in this call): row index, slot and key group, for
@@ -375,14 +403,21 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn i
         row_words(rp, len, r);
         row_hashes_reg(r, len, in.tag_bits, &t, &fh);
     } else {
+#pragma unroll
+        for (int k = 0; k < kRegWords; k++) r[k] = 0;
         row_hashes(reinterpret_cast<const uint32_t*>(rp), len, in.tag_bits, &t, &fh);
     }
     uint64_t s = fmix64(t) & d.mask;
     uint64_t loc = kNoLoc;
+    int64_t sid = -1;
     for (; valid;) {
-        const Slot cur = d.slots[s];
+        // the whole line in four 16-B loads: a written slot holds the row's first kSlotWords
+        // words and its id, so a row of up to 40 bytes is compared and resolved from the slot
+        // alone -- no second random access into the arena (the 32-B key rows of a STRING key)
+        const Slot cur = load_slot(&d.slots[s]);
         if (cur.tag == t) {   // (a slot claimed earlier in this call still has no entry: kNoLoc)
             loc = cur.loc;
+            if (loc != kNoLoc) sid = slot_id_if_equal(d, cur, r, reinterpret_cast<const uint32_t*>(rp), small, len);
             break;
         }
         if (cur.tag == 0) {
@@ -397,11 +432,9 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_probe(DictDev d, RowsIn i
     }
     const int32_t kg = murmur_hash(fh) % in.max_p;
     if (valid) {
-        if (loc != kNoLoc) {   // written by an earlier chunk of this call
-            const int64_t id = small ? entry_id_if_equal_reg(d, loc, r, len)
-                                     : entry_id_if_equal(d, loc, reinterpret_cast<const uint32_t*>(rp), len);
-            if (id < 0) atomicAdd(&d.counters[2], 1ull);
-            id_out[i] = id;
+        if (loc != kNoLoc) {   // written by an earlier call, or an earlier chunk of this one
+            if (sid < 0) atomicAdd(&d.counters[2], 1ull);
+            id_out[i] = sid;
         }
     }
     const bool pend = valid && loc == kNoLoc;
@@ -685,7 +718,7 @@ int fg_key_dict_open(int32_t device_id, int32_t max_parallelism, int64_t expecte
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) return FG_EDEVICE;
     if (d->counters.ensure(64, d->stream) != hipSuccess) return FG_EDEVICE;
     if (hipMemsetAsync(d->counters.p, 0, 64, d->stream) != hipSuccess) return FG_EDEVICE;
-    if (rebuild(d.get(), pow2_at_least(2 * (uint64_t)std::max<int64_t>(expected_keys, 1)))) return FG_EDEVICE;
+    if (rebuild(d.get(), pow2_at_least(FG_DICT_INIT * (uint64_t)std::max<int64_t>(expected_keys, 1)))) return FG_EDEVICE;
     *out = d.release();
     return FG_OK;
 }
@@ -772,8 +805,9 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     unsigned long long* ctr = d->counters.as<unsigned long long>();
     DCHK(d, hipMemsetAsync(ctr + 6, 0, 8, s));
     if (d->timing) DCHK(d, hipEventRecord(d->ev[0], s));
-    hipLaunchKernelGGL(k_dict_lookup, dim3(g), dim3(kDictThreads), 0, s, d->dev(), in, kg_dev, ids,
-                       d->miss.as<uint32_t>());
+    hipLaunchKernelGGL(k_dict_lookup, dim3((unsigned)((n + (int64_t)kDictThreads * kLookupRows - 1) /
+                                                ((int64_t)kDictThreads * kLookupRows))),
+                       dim3(kDictThreads), 0, s, d->dev(), in, kg_dev, ids, d->miss.as<uint32_t>());
     if (d->timing) DCHK(d, hipEventRecord(d->ev[1], s));
     DCHK(d, hipGetLastError());
     unsigned long long cnt[7];
