@@ -165,11 +165,11 @@ constexpr int64_t kHeavyMin = 1 << 16;
 constexpr int64_t kHeavyChunk = 1 << 16;
 
 enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_PART1, K_PART2, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE,
-              K_HEAVY, K_TILE1, K_TILE_FIRE, K_TILE_MAT, K_NCLASS };
+              K_HEAVY, K_TILE1, K_TILE_FIRE, K_TILE_MAT, K_TILE_FLUSH, K_NCLASS };
 const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan",      "ingest_scatter", "ingest_part1",
                                            "ingest_part2", "merge_flush",      "merge_flush_fire", "merge_fire",
                                            "export",       "restore",          "merge_heavy",      "tile_part1",
-                                           "tile_fire",    "tile_materialize"};
+                                           "tile_fire",    "tile_materialize", "tile_flush"};
 struct KStat {
     int64_t launches = 0;
     double ms = 0;
@@ -301,6 +301,10 @@ struct fg_handle {
     // keys stay in their pass-1 tiles until the fire; off for good once a wider key is seen
     bool tile_ok = true;
     bool tile_env = true;     // FG_TILE (fg_reset restores tile_ok from it)
+    // FG_TILE_STATE: tile passes of HOP / CUMULATE (and TUMBLE lanes with resident state) flush
+    // into their slice tables straight from the tiles (k_tile_fire with tables); 0: TUMBLE and
+    // local fires only, anything else materialized (the round-4 first tile build)
+    bool tile_state = true;
     bool tile_skew = false;   // a tile pass saw hot-key skew: later batches take the two-pass partition
                               // (a performance hint kept across fg_reset)
     DevBuf tile_dir, tile_hist;
@@ -748,8 +752,19 @@ int tile_job_params(fg_handle* h, int ji, TileFire* f) {
     MergeParams& p = f->m;
     p.region_bits = h->region_bits;
     set_values(h, &p);
-    fill_emit(h, p, j.wend);
-    p.emit = 1;
+    if (j.emit) {
+        fill_emit(h, p, j.wend);
+        p.emit = 1;
+    }
+    std::vector<TableRef> srcs;
+    for (SliceTable* x : j.srcs) srcs.push_back(ref_of(x));
+    p.n_src = (int)srcs.size();
+    if (!srcs.empty()) {
+        int rc = arena_put(h, srcs.data(), srcs.size(), &p.src);
+        if (rc) return rc;
+    }
+    p.has_dst = j.dst ? 1 : 0;
+    if (j.dst) p.dst = ref_of(j.dst);
     p.overflow = h->scalars.as<unsigned int>();
     p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
     p.fail_list = h->fail_list.as<uint32_t>();
@@ -1224,8 +1239,11 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 fire_class = K_TILE_FIRE;
                 continue;
             }
-            rc = materialize_lane(h, l);
-            if (rc) return rc;
+            if (refire_slice(h, se) || !h->tile_state) {
+                rc = materialize_lane(h, l);
+                if (rc) return rc;
+                lane_tiles = false;
+            }
         }
         if (refire_slice(h, se)) {
             // after a restore, records of a slice whose windows fired before the checkpoint:
@@ -1288,7 +1306,6 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         SliceTable* F = nullptr;       // first slice's table of W's cumulative window
         SliceTable* dstt = t;          // table written by this merge (null: none)
         MergeJob job;
-        for (Staged* s : ln.passes) job.batches.push_back(JobBatch{s, l, StagedBatch{}, 0});
         if (t && t->upper > 0) job.srcs.push_back(t);
         int64_t cum_first = 0, cum_last = 0;
         if (cum_fire) {
@@ -1319,6 +1336,41 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         job.emit = fire_now || cum_fire;
         job.wend = se;
         job.kclass = fire_now || cum_fire ? K_FLUSH_FIRE : K_FLUSH;
+        if (lane_tiles) {
+            // the lane's tile passes straight into the slice state (and the fired window's rows):
+            // the resident tables the merge would read inserted first, the destination's regions
+            // written back by the same workgroups -- no materialized pass, no staged pass 2
+            bool ok = tile_fire_ok(h, ln) && h->keys32 && ub_cnt_fits(h) && job.srcs.size() <= 8 &&
+                      kTileBits + h->region_bits - ln.passes[0]->bits <= kTileMaxRegionBits &&
+                      !(job.emit && h->retain && !h->local);
+            for (SliceTable* x : job.srcs) ok = ok && !x->has_null;
+            if (ok) {
+                for (Staged* st : ln.passes) {
+                    job.batches.push_back(JobBatch{st, l, StagedBatch{}, 0});
+                    st->busy = true;
+                }
+                job.tile = true;
+                job.tbits = ln.passes[0]->bits;
+                job.kclass = job.emit ? K_TILE_FIRE : K_TILE_FLUSH;
+                const int kc = job.kclass;
+                int ji = 0;
+                rc = job_add(h, std::move(job), &ji);
+                if (rc) return rc;
+                TileFire f{};
+                rc = tile_job_params(h, ji, &f);
+                if (rc) return rc;
+                {
+                    KTimer kt(h, kc, ln.fill);
+                    HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                }
+                if (kc == K_TILE_FIRE) fire_class = K_TILE_FIRE;
+                goto merged;
+            }
+            rc = materialize_lane(h, l);
+            if (rc) return rc;
+        }
+        for (Staged* s : ln.passes) job.batches.push_back(JobBatch{s, l, StagedBatch{}, 0});
+        {
         int ji = 0;
         rc = job_add(h, std::move(job), &ji);
         if (rc) return rc;
@@ -1402,6 +1454,8 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                     (double)st[1] / waves, (double)st[2] / waves, (double)st[3] / waves);
         }
 #endif
+        }
+    merged:
         if (fire_now) {
             if (h->retain && !h->local) {
                 t->upper = ub;
@@ -2087,7 +2141,8 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     // tile staging: TUMBLE windows and the local phase's slices fire straight from pass 1's tiles
     // (32-bit keys, one value accumulator, no NULL values, no allowed lateness, no hot-key skew)
     const bool tiles = two_pass && h->tile_ok && !h->tile_skew && h->narrow && !vnull && !h->mv && h->lateness == 0 &&
-                       (h->w.kind == TUMBLE || h->local) && (h->F >> kTileBits) <= kMaxTileBuckets;
+                       (h->w.kind == TUMBLE || h->local || (h->tile_state && h->cfg.mode == FG_MODE_SQL)) &&
+                       (h->F >> kTileBits) <= kMaxTileBuckets;
     ps.tiles = tiles;
     if (tiles) {
         // the pass's own Staged (its tiles live until the fire): a pooled one no unsettled job reads
@@ -3227,6 +3282,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_P2_SKEW_GROUP")) hp->p2_skew_group = std::max(0, std::atoi(e));
     hp->narrow_ok = hp->narrow;
     if (const char* e = getenv("FG_TILE")) hp->tile_env = std::atoi(e) != 0;
+    if (const char* e = getenv("FG_TILE_STATE")) hp->tile_state = std::atoi(e) != 0;
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";

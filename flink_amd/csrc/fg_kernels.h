@@ -436,6 +436,8 @@ constexpr int kMaxTileBuckets = 4096;         // lanes << (region_bits - kTileBi
 constexpr int kTileSlots = 8192;              // consumer LDS table (~4.9k keys: 60 % load)
 constexpr int kTileFireThreads = 1024;
 constexpr int kTileMaxSub = 64;               // regions of one bucket at the current bits (materialize)
+constexpr int kTileMaxRegionBits = 8;         // tile jobs with tables: at most 2^8 regions per item
+constexpr int kTileMaxRegions = 1 << kTileMaxRegionBits;
 
 // One tile-staged pass as the fire / materialize kernels read it (lane `lane`'s buckets)
 struct TilePass {

@@ -3226,7 +3226,15 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
 // windows in flight per wave: the next window's loads are issued before this one's inserts. A
 // full table emits nothing and lists the item's regions in the fail list (the host splits the
 // regions and redoes them one region per item, MergeParams fail protocol).
-template <int VTC>
+// With resident state (m.n_src > 0: slice tables -- a HOP slice's own table, a CUMULATE window's
+// first slice, AggCombiner's accState) the item's regions of every source table are inserted
+// first (their COUNT(*) and value accumulator, the keys from their mixes); with m.has_dst the
+// item's aggregate is written back as the destination table's regions -- each key into its
+// region's block, the regions' counts replaced (RecordsWindowBuffer.flush + AggCombiner.combine
+// straight from the tiles, no staged pass 2). A region holding more than kRegionCap keys fails
+// the item like a full table: nothing is written or emitted and its regions are redone.
+// m.emit = 0: a flush (the table written, no rows).
+template <int VTC, bool TAB>   // TAB: source / destination tables (compiled out of the plain fire)
 __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     constexpr int T = kTileFireThreads, W = T / 64, S = kTileSlots;
     constexpr int kRounds = S / T + 1;   // + 1: the sentinel slot (thread 0)
@@ -3241,7 +3249,10 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     __shared__ unsigned int s_flags;
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_out_base;
+    __shared__ uint32_t s_rc[kTileMaxRegions];   // destination: keys per region of the item
+    __shared__ uint32_t s_rb[kTileMaxRegions];   // destination: each region's first rank
     const MergeParams& p = f.m;
+    const bool dst = TAB && p.has_dst != 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int vt = VTC >= 0 ? VTC : p.val_type;
     const int64_t vinit = lds_repr(vt, val_identity(vt));
@@ -3272,9 +3283,98 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             t_cs[i] = 0;
             t_v[i] = (unsigned long long)vinit;
         }
+        if (TAB)
+            for (int i = tid; i < kTileMaxRegions; i += T) s_rc[i] = 0;
         if (tid == 0) s_flags = 0;
         __syncthreads();
         bool full = false;
+        // the slot of `key` in the table (claimed if new), -1 when the table is full
+        auto slot_of = [&](int32_t key) -> int {
+            if (key == kEmpty32) return S;
+            uint32_t home = __umulhi((uint32_t)key * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
+            for (int probe = 0; probe < S / 4; probe++) {
+                const int4 q4 = *reinterpret_cast<const int4*>(&t_key[home]);
+                const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
+                int hit = -1, emp = -1;
+#pragma unroll
+                for (int z = 3; z >= 0; z--) {
+                    if (qq[z] == key) hit = z;
+                    if (qq[z] == kEmpty32) emp = z;
+                }
+                if (hit >= 0 && (emp < 0 || hit < emp)) return (int)home + hit;
+                if (emp >= 0) {
+                    const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
+                    if (old == kEmpty32 || old == key) return (int)home + emp;
+                    continue;   // (lost the slot to another key: the same bucket again)
+                }
+                home = (home + 4) & (S - 1);
+            }
+            return -1;
+        };
+        if (TAB && p.n_src > 0) {
+            // resident state first: the item's regions of every source table (keys as mixes; the
+            // operator's keys fit 32 bits, so a mix's key is its int32) -- one flat sequence over
+            // the (source, region) ranges (their counts' exclusive prefix in s_rb, wave 0), every
+            // thread kSrcU entries per round, their loads issued before any insert
+            constexpr int cap = kRegionCap;
+            const int nreg = r_hi - r_lo, nrange = live ? p.n_src * nreg : 0;   // (host: <= kTileMaxRegions)
+            if (wave == 0) {
+                constexpr int RPL = kTileMaxRegions / 64;
+                uint32_t c[RPL], x = 0;
+#pragma unroll
+                for (int q = 0; q < RPL; q++) {
+                    const int g = RPL * lane + q;
+                    c[q] = g < nrange ? gbl(p.src[g / nreg].counts)[r_lo + g % nreg] : 0u;
+                    x += c[q];
+                }
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t y = __shfl_up(x, off);
+                    if (lane >= off) x += y;
+                }
+                uint32_t ex = x;
+#pragma unroll
+                for (int q = 0; q < RPL; q++) ex -= c[q];
+#pragma unroll
+                for (int q = 0; q < RPL; q++) {
+                    if (RPL * lane + q < nrange) s_rb[RPL * lane + q] = ex;
+                    ex += c[q];
+                }
+                if (lane == 63) s_total = x;
+            }
+            __syncthreads();
+            const uint32_t NE = nrange ? s_total : 0u;
+            for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
+                int64_t mk[kSrcU], cs[kSrcU], v[kSrcU];
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    const uint32_t i = i0 + u * T + tid;
+                    mk[u] = cs[u] = v[u] = 0;
+                    if (i >= NE) continue;
+                    int lo = 0, hi = nrange;   // the range of entry i: the last base <= i
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_rb[mid] <= i) lo = mid;
+                        else hi = mid;
+                    }
+                    const int64_t* base = p.src[lo / nreg].base + (int64_t)(r_lo + lo % nreg) * 4 * cap;
+                    const uint32_t e = i - s_rb[lo];
+                    mk[u] = gbl(base)[e];
+                    cs[u] = gbl(base)[cap + e];
+                    v[u] = gbl(base)[3 * cap + e];
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    if (i0 + u * T + tid >= NE) continue;
+                    const int sl = slot_of((int32_t)key_of(mk[u]));
+                    if (sl < 0) {
+                        full = true;
+                        continue;
+                    }
+                    atomicAdd(&t_cs[sl], (uint32_t)cs[u]);
+                    lds_val(&t_v[sl], v[u], vt, true);
+                }
+            }
+        }
         if (live) {
             auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
                 uint32_t hm[kTileRpl];
@@ -3349,6 +3449,11 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
         // compaction: the occupied slots' ranks (round k covers slots [k*T, (k+1)*T); the last
         // round the sentinel slot), a dense rank -> slot map, then one row per lane
         uint32_t occ_mask = 0;
+        // a key's region at the current bits, relative to the item's first
+        auto region_of = [&](int slot) -> int {
+            const int64_t key = slot == S ? (int64_t)kEmpty32 : (int64_t)t_key[slot];
+            return (int)((uint64_t)mix_of(key) >> (64 - p.region_bits)) - r_lo;
+        };
 #pragma unroll
         for (int r = 0; r < kRounds; r++) {
             const int slot = r < kRounds - 1 ? r * T + tid : S;
@@ -3356,6 +3461,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             const uint64_t bal = __ballot(occ);
             if (occ) occ_mask |= 1u << r;
             if (lane == 0) s_grp[r * W + wave] = (uint32_t)__popcll(bal);
+            if (dst && occ && live) atomicAdd(&s_rc[region_of(slot)], 1u);
         }
         __syncthreads();
         if (wave == 0) {
@@ -3380,9 +3486,13 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 ex += gv[q];
             }
             const uint32_t total = __shfl(xs, 63);
+            bool over = false;   // a destination region above its capacity: the item fails
+            if (dst)
+                for (int q = lane; q < r_hi - r_lo; q += 64) over = over || s_rc[q] > (uint32_t)kRegionCap;
+            over = __ballot(over) != 0;
             if (lane == 0) {
-                unsigned int fl = s_flags;
-                if (live && !(fl & 4u)) {
+                unsigned int fl = s_flags | (over ? 4u : 0u);
+                if (live && !(fl & 4u) && (!TAB || p.emit)) {
                     const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
                     s_out_base = ob;
                     if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
@@ -3409,7 +3519,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 (uint16_t)(r < kRounds - 1 ? r * T + tid : S);
         }
         __syncthreads();
-        if (live && !(fl & 6u)) {
+        if (live && (!TAB || p.emit) && !(fl & 6u)) {
             const uint32_t total = s_total;
             const unsigned long long ob = s_out_base;
             for (uint32_t i = tid; i < total; i += T) {
@@ -3418,19 +3528,89 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 write_row_k(p, ob + i, sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl], t_cs[sl], 0ull, &v, vt);
             }
         }
+        if (TAB && dst && live && !(fl & 5u)) {
+            // the regions' counts and bases (exclusive prefix, wave 0), the rank -> slot map
+            // rebuilt region-major (s_map is free once the rows are out), then every region's
+            // entries written at consecutive ranks: full-width stores into each SoA column
+            constexpr int cap = kRegionCap;
+            const int nreg = r_hi - r_lo;
+            __syncthreads();   // (the emit's reads of s_map are done)
+            if (wave == 0) {
+                constexpr int RPL = kTileMaxRegions / 64;
+                uint32_t c[RPL], x = 0;
+#pragma unroll
+                for (int q = 0; q < RPL; q++) {
+                    c[q] = RPL * lane + q < nreg ? s_rc[RPL * lane + q] : 0u;
+                    x += c[q];
+                }
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t y = __shfl_up(x, off);
+                    if (lane >= off) x += y;
+                }
+                uint32_t ex = x;
+#pragma unroll
+                for (int q = 0; q < RPL; q++) ex -= c[q];
+#pragma unroll
+                for (int q = 0; q < RPL; q++) {
+                    const int rr = RPL * lane + q;
+                    if (rr < nreg) {
+                        const uint32_t old = p.dst.counts[r_lo + rr];
+                        p.dst.counts[r_lo + rr] = c[q];
+                        if (p.dst_total) atomicAdd(p.dst_total, (unsigned long long)((int64_t)c[q] - (int64_t)old));
+                        s_rb[rr] = ex;   // region rr's first rank
+                        s_rc[rr] = ex;   // (its cursor)
+                    }
+                    ex += c[q];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < kRounds; r++) {
+                if (!((occ_mask >> r) & 1)) continue;
+                const int slot = r < kRounds - 1 ? r * T + tid : S;
+                s_map[atomicAdd(&s_rc[region_of(slot)], 1u)] = (uint16_t)slot;
+            }
+            __syncthreads();
+            const uint32_t total = s_total;
+            for (uint32_t i = tid; i < total; i += T) {
+                int lo = 0, hi = nreg;   // the region of rank i: the last base <= i
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_rb[mid] <= i) lo = mid;
+                    else hi = mid;
+                }
+                const int sl = s_map[i];
+                const uint32_t at = i - s_rb[lo];
+                int64_t* db = p.dst.base + (int64_t)(r_lo + lo) * 4 * cap;
+                db[at] = mix_of(sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl]);
+                db[cap + at] = (int64_t)t_cs[sl];
+                db[2 * cap + at] = 0;
+                db[3 * cap + at] = lds_repr(vt, (int64_t)t_v[sl]);
+            }
+        }
         __syncthreads();   // the table is cleared for the next item
     }
 }
 
 hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s) {
     if (f.n_passes < 1 || f.tbits < kTileBits || f.m.region_bits < f.tbits || f.m.mv) return hipErrorInvalidValue;
+    if ((f.m.has_dst || f.m.n_src > 0) && (kTileBits + f.m.region_bits - f.tbits > kTileMaxRegionBits || f.m.src_null_mask))
+        return hipErrorInvalidValue;   // (s_rc holds an item's regions; sources without NULL counts)
     const dim3 g((unsigned)workgroups), b(kTileFireThreads);
-    switch (f.m.val_type) {   // the value op compiled in: SUM / AVG over DOUBLE, BIGINT, or COUNT only
-        case 2: fg_launch(k_tile_fire<2>, g, b, 0, s, f); break;
-        case 1: fg_launch(k_tile_fire<1>, g, b, 0, s, f); break;
-        case 0: fg_launch(k_tile_fire<0>, g, b, 0, s, f); break;
-        default: fg_launch(k_tile_fire<-1>, g, b, 0, s, f); break;
+    const bool tab = f.m.has_dst || f.m.n_src > 0;
+    // the value op compiled in: SUM / AVG over DOUBLE, BIGINT, or COUNT only
+#define FG_TILE_FIRE(V)                                                     \
+    do {                                                                    \
+        if (tab) fg_launch((k_tile_fire<V, true>), g, b, 0, s, f);         \
+        else fg_launch((k_tile_fire<V, false>), g, b, 0, s, f);            \
+    } while (0)
+    switch (f.m.val_type) {
+        case 2: FG_TILE_FIRE(2); break;
+        case 1: FG_TILE_FIRE(1); break;
+        case 0: FG_TILE_FIRE(0); break;
+        default: FG_TILE_FIRE(-1); break;
     }
+#undef FG_TILE_FIRE
     return hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ CLASSES = {
     "fg::k_ingest_scatter_direct": ["ingest_scatter"],
     "fg::k_merge": ["merge_flush_fire", "merge_flush", "merge_fire", "restore"],
     "fg::k_tile_part1": ["tile_part1"],
-    "fg::k_tile_fire": ["tile_fire"],
+    "fg::k_tile_fire": ["tile_fire", "tile_flush"],
 }
 
 
