@@ -2326,6 +2326,26 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
         out->drops = drops;
         return rc;
     }
+    if (tiles && out->skew) {
+        // hot keys (a bucket of one tile above 16x the uniform mean): a tile pass would be fired by
+        // one overloaded workgroup per hot bucket, or materialized by one (9.6 ms per 100M-record
+        // Zipf(1.1) batch, round 4). Tile staging ends for good and the batch is staged again by
+        // the two-pass partition, whose heavy-region path spreads hot keys (its drops were
+        // counted by this pass); the pass's tiles go back to the pool unused
+        h->tile_skew = true;
+        h->pass_pool.push_back(std::move(ps.s));
+        PassState ps2;
+        rc = ingest_launch(h, n, p.key, p.ts, p.val, vnull, flo, fhi, false, ps2);
+        if (rc) return rc;
+        rc = sync(h);
+        if (rc) return rc;
+        Counters c2{};
+        rc = ingest_finish(h, ps2, &c2);
+        const unsigned long long drops = out->drops;
+        *out = c2;
+        out->drops = drops;
+        return rc;
+    }
     if (p.narrow && got.wide) {
         // a key wider than 32 bits under narrow staging (the device plan stopped pass 2; pass 1's
         // 12-B tile records truncated it): the lanes' narrow passes go into their tables, pass 1
