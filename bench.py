@@ -617,12 +617,12 @@ def main():
                 k_next = intern(hi)
             if world > 1 and wms:
                 wms[-1] = global_watermark(wms[-1], device=dev)
-            for wm in wms:
-                if args.wm_sync:
+            if args.wm_sync:
+                for wm in wms:
                     rows += op.process_watermark(wm, device_output=True).n
-                else:   # fg_advance_progress_async: the fires are queued, the watermarks held
-                    op.process_watermark(wm, device_output=True, wait=False)
-                    held = True
+            elif wms:   # fg_advance_progress_async_n: every watermark's fires queued, the watermarks held
+                op.process_watermarks(wms)
+                held = True
         if two_phase:
             nr, sent = partials_round(JMAX, held)
             return rows + nr + op.collect_fired().n, xgmi + sent

@@ -96,6 +96,7 @@ BATCH_KEY32, BATCH_ROWTIME32, BATCH_VAL32 = 1, 2, 4   # fg_batch.format
 # every symbol include/flinkgpu.h declares
 EXPORTS = (
     "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_advance_progress_async",
+    "fg_advance_progress_async_n",
     "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials", "fg_snapshot_state",
     "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
@@ -141,6 +142,7 @@ def load():
     L.fg_add_partials.argtypes = [P, C.POINTER(FgPartials)]
     L.fg_advance_progress.argtypes = [P, C.c_int64, C.c_int32, C.POINTER(FgRows)]
     L.fg_advance_progress_async.argtypes = [P, C.c_int64]
+    L.fg_advance_progress_async_n.argtypes = [P, P, C.c_int64]
     L.fg_collect_fired.argtypes = [P, C.POINTER(FgRows)]
     L.fg_collect_fired_to.argtypes = [P, C.c_int32, C.POINTER(FgRows)]
     L.fg_flush_partials.argtypes = [P, C.c_int32, C.POINTER(FgRows)]
@@ -192,7 +194,7 @@ def load():
                "fg_key_dict_copy_arena"):
         getattr(L, fn).restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress",
-               "fg_advance_progress_async", "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials",
+               "fg_advance_progress_async", "fg_advance_progress_async_n", "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials",
                "fg_snapshot_state", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int

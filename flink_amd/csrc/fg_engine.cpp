@@ -2292,8 +2292,11 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     out->qmin = got.qmin;
     out->qmax = got.qmax;
     out->qnext = got.qnext;
-    // (a tile pass reports its largest bucket count of one tile: > 16x the uniform mean is skew)
-    out->skew = tiles ? (int64_t)got.max_bucket > kTileRecs / 64
+    // (a tile pass reports its largest bucket count of one tile: skew is > 4x the uniform mean of
+    // a lane's 2^(bits - 2) buckets, and > 96 records -- 16x the mean at 1,024 buckets per lane;
+    // a uniform stream over few buckets stays on the tiles, a hot key's bucket does not)
+    const int64_t tile_mean = kTileRecs >> std::max(0, p.region_bits - kTileBits);
+    out->skew = tiles ? (int64_t)got.max_bucket > std::max<int64_t>(kTileRecs / 64, 4 * tile_mean)
                       : (int64_t)got.max_bucket * p.grid > kHeavyMin;
     for (int l = 0; l < kMaxLanes; l++) {
         out->lane_min[l] = JMAX;
@@ -3257,7 +3260,10 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         // a merge runs one region per workgroup: an operator of a few thousand keys would fire
         // each window on a handful of CUs, so from 4,096 expected keys it takes at least
         // 2^FG_MIN_REGION_BITS regions (more, emptier LDS tables; every CU busy at a fire)
-        int min_bits = 8;
+        // (TUMBLE and the local phase: 2^10 -- their windows fire straight from the tile passes,
+        // one workgroup per bucket of 4 regions, so 256 buckets per slice keep every CU busy and
+        // a tile's fragment of a bucket at ~24 records; their slice tables are rarely written)
+        int min_bits = (w.kind == TUMBLE || local) && h->lateness == 0 ? 10 : 8;
         if (const char* e = getenv("FG_MIN_REGION_BITS")) min_bits = std::max(0, std::min(kMaxRegionBits, std::atoi(e)));
         if (cfg->expected_keys >= 4096 && bits < min_bits) bits = min_bits;
     } else {
@@ -3770,6 +3776,13 @@ int fg_advance_progress_async(fg_handle* h, int64_t wm) {
     } else {
         h->rows_fired += h->out_n - h->adv_base;
     }
+    return FG_OK;
+}
+
+int fg_advance_progress_async_n(fg_handle* h, const int64_t* wms, int64_t n) {
+    if (!h || n < 0 || (n > 0 && !wms)) return FG_EINVAL;
+    for (int64_t i = 0; i < n; i++)
+        if (int rc = fg_advance_progress_async(h, wms[i])) return rc;
     return FG_OK;
 }
 

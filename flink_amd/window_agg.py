@@ -358,6 +358,18 @@ class WindowAggOperator:
         self._hold(None)
         return self._host_rows(r)
 
+    def process_watermarks(self, watermarks):
+        """process_watermark(wm, device_output=True, wait=False) of each watermark in order, in
+        one library call (fg_advance_progress_async_n): the watermarks a shim holds between two
+        batches; collect_fired() returns their rows."""
+        if len(watermarks) == 0:
+            return
+        wm = np.ascontiguousarray(watermarks, dtype=np.int64)
+        rc = self._lib.fg_advance_progress_async_n(self._h, wm.ctypes.data, len(wm))
+        if rc:
+            L.check(rc, self._h)
+        self._hold(None)
+
     def collect_fired(self, host: bool = False):
         """The rows of the process_watermark(..., wait=False) calls since the last collect
         (fg_collect_fired: waits for their fires): the operator's FgRows, device pointers valid

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 12
+#define FG_ABI_VERSION 13
 
 enum fg_status {
     FG_OK = 0,
@@ -305,6 +305,11 @@ int  fg_advance_progress(fg_handle* h, int64_t watermark, int32_t out_location, 
  * batch, flush, snapshot or restore. Errors of a fire are reported by that call. The rows of an
  * async advance stay valid until the next call that fires windows. */
 int  fg_advance_progress_async(fg_handle* h, int64_t watermark);
+/* fg_advance_progress_async of n watermarks in order, as n calls would (ABI 13): the
+ * watermarks a shim received since its last batch -- with no element between them -- in one
+ * call instead of one JNI / C call each (configs[0]: 100 watermarks per 1M-record batch; each
+ * one that fires nothing only moves the progress). Stops at the first error. */
+int  fg_advance_progress_async_n(fg_handle* h, const int64_t* watermarks, int64_t n);
 /* Waits for the fires of the last fg_advance_progress_async call and returns their rows (device
  * pointers, as fg_advance_progress with FG_DEVICE); n = 0 when it fired nothing. A synchronous
  * fg_advance_progress called while async rows are uncollected returns them ahead of its own rows

@@ -25,7 +25,7 @@ def _cfg(kind, mode="sql", vt="f64"):
 
 
 def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0, delay=0, collect_every=1,
-         regions_small=False, ckpt_every=0, zipf=0.0, sync=False, collect="device"):
+         regions_small=False, ckpt_every=0, zipf=0.0, sync=False, collect="device", batched=False):
     """collect: "device" (fg_collect_fired, rows copied out by torch), "host" (fg_collect_fired_to
     FG_HOST), or "sync_wm" (no collect: a synchronous watermark instead, whose rows must lead with
     every async row not collected yet)."""
@@ -44,15 +44,20 @@ def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0
         op.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
         o.process_batch(key[lo:hi], ts[lo:hi], val[lo:hi])
         # watermarks at sub-batch boundaries (max rowtime so far - delay - 1)
+        held = []
         for c in np.linspace(lo, hi, wms_per_batch + 1)[1:].astype(np.int64):
             mx = max(mx, int(ts[lo:c].max()))
             wm = mx - delay - 1
             if sync:   # (the synchronous advance, host rows: the A/B reference of these tests)
                 g.process_watermark(wm)
+            elif batched:   # (the batch's watermarks in one call: fg_advance_progress_async_n)
+                held.append(wm)
             else:
                 assert op.process_watermark(wm, device_output=True, wait=False) is None
             o.process_watermark(wm)
             exp.append(o.take_rows())
+        if held:
+            op.process_watermarks(held)
         nb += 1
         ckpt = ckpt_every and nb % ckpt_every == 0
         if ckpt:   # checkpoint while the watermarks' fires are pending and their rows uncollected
@@ -101,6 +106,17 @@ def _run(O, cfg, n=900_000, keys=30_000, batch=60_000, wms_per_batch=6, jitter=0
 @pytest.mark.parametrize("collect_every", [1, 2])
 def test_async_watermarks_match_oracle(oracle_mod, kind, collect_every):
     _run(oracle_mod, _cfg(kind), collect_every=collect_every)
+
+
+@pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
+def test_batched_watermarks_match_oracle(oracle_mod, kind):
+    """fg_advance_progress_async_n (ABI 13): each batch's six watermarks in one call, rows as the
+    oracle's after every watermark"""
+    _run(oracle_mod, _cfg(kind), batched=True, collect_every=2)
+
+
+def test_batched_watermarks_datastream_out_of_order(oracle_mod):
+    _run(oracle_mod, _cfg("tumble", mode="datastream", vt="i64"), batched=True, jitter=1500, delay=200)
 
 
 @pytest.mark.parametrize("kind", ["tumble", "hop", "cumulate"])
