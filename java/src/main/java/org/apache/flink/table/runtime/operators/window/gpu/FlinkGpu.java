@@ -77,6 +77,9 @@ public final class FlinkGpu {
      */
     public static native void advanceProgressAsync(long h, long watermark);
 
+    /** fg_advance_progress_async_n: watermarks[0..n) in order, as n advanceProgressAsync calls. */
+    public static native void advanceProgressAsyncN(long h, long[] watermarks, int n);
+
     /**
      * fg_collect_fired_to(FG_HOST): waits for the fires of every async advance since the last
      * collect; fills cols as {@link #advanceProgress} (host memory); returns the row count.

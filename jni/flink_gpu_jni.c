@@ -11,6 +11,7 @@
  *   addPartials     fg_add_partials      (GlobalAggCombiner.combine)
  *   advanceProgress fg_advance_progress  (processWatermark -> advanceProgress + fireWindow)
  *   advanceProgressAsync fg_advance_progress_async (the same, the fires queued: the watermark held)
+ *   advanceProgressAsyncN fg_advance_progress_async_n (a batch's held watermarks in one call)
  *   collectFired    fg_collect_fired_to  (the held watermark's rows, in host memory; then the watermark is forwarded)
  *   flush           fg_flush             (prepareSnapshotPreBarrier)
  *   flushPartials   fg_flush_partials    (local phase: WindowBuffer.flush of LocalSlicingWindowAggOperator)
@@ -217,6 +218,21 @@ JNIEXPORT void JNICALL FN(advanceProgressAsync)(JNIEnv* env, jclass cls, jlong h
     (void)cls;
     fg_handle* h = (fg_handle*)(intptr_t)hp;
     check(env, h, fg_advance_progress_async(h, wm));
+}
+
+/* void advanceProgressAsyncN(long h, long[] watermarks, int n): the watermarks a shim received
+ * between two batches, in one call (fg_advance_progress_async_n) */
+JNIEXPORT void JNICALL FN(advanceProgressAsyncN)(JNIEnv* env, jclass cls, jlong hp, jlongArray wms, jint n) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    if (n < 0 || !wms || (*env)->GetArrayLength(env, wms) < n) {
+        throw_code(env, FG_EINVAL, "advanceProgressAsyncN: watermark array shorter than n");
+        return;
+    }
+    jlong* w = (*env)->GetLongArrayElements(env, wms, NULL);
+    const int rc = fg_advance_progress_async_n(h, (const int64_t*)w, n);
+    (*env)->ReleaseLongArrayElements(env, wms, w, JNI_ABORT);
+    check(env, h, rc);
 }
 
 /* long collectFired(long h, ByteBuffer[] cols): as advanceProgress -- the rows are copied to
