@@ -3263,9 +3263,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         // (TUMBLE and the local phase: 2^10 -- their windows fire straight from the tile passes,
         // one workgroup per bucket of 4 regions, so 256 buckets per slice keep every CU busy and
         // a tile's fragment of a bucket at ~24 records; their slice tables are rarely written)
-        // (not for the wide merge's operators -- allowed lateness, several value accumulators:
-        // DESIGN.md §8 'Known issue', rows lost at >= 4 regions per workgroup)
-        int min_bits = (w.kind == TUMBLE || local) && h->lateness == 0 && !h->mv ? 10 : 8;
+        int min_bits = (w.kind == TUMBLE || local) && h->lateness == 0 ? 10 : 8;
         if (const char* e = getenv("FG_MIN_REGION_BITS")) min_bits = std::max(0, std::min(kMaxRegionBits, std::atoi(e)));
         if (cfg->expected_keys >= 4096 && bits < min_bits) bits = min_bits;
     } else {

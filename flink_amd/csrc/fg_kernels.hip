@@ -2123,7 +2123,12 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 cur.i0 = s_rng[ri % 3][0][0];
                 settle(cur, ri + 1);
                 nbuf = 0;
-                if (cur.ok && cur.ri == ri) load(ca, cur);
+                // (the chunk is loaded even when it lies in region ri + 1 -- this region empty:
+                // region ri + 1 then streams from buffer ca without another settle. Loading it
+                // only for region ri left ca holding an earlier region's records, which region
+                // ri + 1 inserted in place of its first chunk: rows lost, rows with foreign keys
+                // -- found in round 4 with sparse regions, FG_MIN_REGION_BITS=10/12)
+                if (cur.ok) load(ca, cur);
             }
             bool go = cur.ri == ri && cur.ok;
             if (go && nbuf == 1) {
