@@ -415,6 +415,9 @@ def main():
     ap.add_argument("--wm-sync", action="store_true",
                     help="deliver watermarks with the synchronous fg_advance_progress (A/B; default: "
                          "fg_advance_progress_async, the host does not wait for a window's fire)")
+    ap.add_argument("--intern-at", choices=["batch", "fires"], default="batch",
+                    help="STRING keys: launch the next batch's lookup before this batch is handed over "
+                         "(beside pass 1) or after its watermarks (beside the fires)")
     ap.add_argument("--intern-serial", action="store_true",
                     help="strings: intern the next micro-batch after the engine's passes instead of beside them (A/B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -566,6 +569,12 @@ def main():
                             key_groups=False)
         return k
 
+    def intern_async(lo):
+        """the same, launched (fg_key_dict_intern_async): the ids are complete after intern_wait"""
+        hi = min(n, lo + args.batch)
+        k, _ = kdict.intern_async((rows_u8[32 * lo:32 * hi], row_off[:hi - lo], row_len[:hi - lo]))
+        return k
+
     def one_step():
         op.reset()
         rows0 = op.stats()["rows_fired"]
@@ -591,6 +600,9 @@ def main():
                 k = key[lo:hi]
             t, v = ts[lo:hi], val[lo:hi]
             wms = watermarks_for(lo, hi, args.rate, args.wm_every, wl["delay"], wl["jitter"])
+            if strings and hi < n and not two_phase and not args.intern_serial and args.intern_at == "batch":
+                # the next micro-batch's lookup runs beside this batch's passes and fires
+                k_next = intern_async(hi)
             if two_phase:
                 op_local.process_batch(k, t, v)
                 if strings and hi < n:
@@ -610,11 +622,6 @@ def main():
             if held:   # the previous batch's watermarks: their rows, then (a shim) the watermarks go on
                 rows += op.collect_fired().n
                 held = False
-            if strings and hi < n:   # overlaps this batch's partition passes
-                if args.intern_serial:   # A/B: the lookup after them (the dictionary's stream waits
-                    # on torch's, which here waits on the engine's)
-                    torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(op.stream, device=dev))
-                k_next = intern(hi)
             if world > 1 and wms:
                 wms[-1] = global_watermark(wms[-1], device=dev)
             if args.wm_sync:
@@ -623,6 +630,19 @@ def main():
             elif wms:   # fg_advance_progress_async_n: every watermark's fires queued, the watermarks held
                 op.process_watermarks(wms)
                 held = True
+            # STRING keys: the next micro-batch's lookup (launched above on the dictionary's own
+            # stream) ran beside this batch's passes and the fires its watermarks queued; its ids
+            # are complete before the next batch is handed over (the key selector runs as the
+            # records arrive)
+            if strings and hi < n:
+                if args.intern_serial:   # A/B: the lookup after them (the dictionary's stream waits
+                    # on torch's, which here waits on the engine's)
+                    torch.cuda.current_stream().wait_stream(torch.cuda.ExternalStream(op.stream, device=dev))
+                    k_next = intern(hi)
+                else:
+                    if args.intern_at == "fires":
+                        k_next = intern_async(hi)
+                    kdict.intern_wait()
         if two_phase:
             nr, sent = partials_round(JMAX, held)
             return rows + nr + op.collect_fired().n, xgmi + sent

@@ -101,7 +101,8 @@ EXPORTS = (
     "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
-    "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
+    "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async",
+    "fg_key_dict_intern_wait", "fg_key_dict_lookup", "fg_key_dict_arena",
     "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_stream", "fg_key_dict_set_timing",
     "fg_key_dict_kernel_stats", "fg_key_dict_last_error", "fg_key_dict_close",
     "fg_binaryrow_hash", "fg_host_register", "fg_host_unregister",
@@ -170,6 +171,8 @@ def load():
     L.fg_abi_version.restype = C.c_int
     L.fg_key_dict_open.argtypes = [C.c_int32, C.c_int32, C.c_int64, C.POINTER(P)]
     L.fg_key_dict_intern.argtypes = [P, C.c_int32, C.c_int64, P, C.c_int64, P, P, P, P]
+    L.fg_key_dict_intern_async.argtypes = [P, C.c_int64, P, C.c_int64, P, P, P, P]
+    L.fg_key_dict_intern_wait.argtypes = [P]
     L.fg_key_dict_lookup.argtypes = [P, C.c_int32, C.c_int64, P, P, P]
     L.fg_key_dict_arena.argtypes = [P, C.POINTER(P), C.POINTER(C.c_int64)]
     L.fg_key_dict_copy_arena.argtypes = [P, C.c_int64, C.c_int64, P]
@@ -190,7 +193,8 @@ def load():
     L.fg_host_register.argtypes = [C.c_int32, P, C.c_int64]
     L.fg_host_unregister.argtypes = [C.c_int32, P]
     L.fg_host_register.restype = L.fg_host_unregister.restype = C.c_int
-    for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_lookup", "fg_key_dict_arena",
+    for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async", "fg_key_dict_intern_wait",
+               "fg_key_dict_lookup", "fg_key_dict_arena",
                "fg_key_dict_copy_arena"):
         getattr(L, fn).restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress",

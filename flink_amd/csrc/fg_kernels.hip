@@ -3070,17 +3070,23 @@ hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
 // through LDS; buckets of lanes without records (lane_mask) are skipped
 __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t NT, int32_t NC, int32_t lshift,
                                                    const unsigned long long* lane_mask, uint32_t* dt) {
-    __shared__ uint16_t s[64][66];
+    __shared__ uint16_t s[64][67];
     const int tb = blockIdx.x * 64, cb = blockIdx.y * 64;
     const unsigned long long lm = *gbl(lane_mask);
     const int l0 = cb >> lshift, l1 = (cb + 63 < NC ? cb + 63 : NC - 1) >> lshift;
     bool any = false;
     for (int l = l0; l <= l1; l++) any = any || ((lm >> l) & 1);
     if (!any) return;
-    for (int i = threadIdx.x; i < 64 * 65; i += 256) {
-        const int tt = i / 65, cc = i % 65;
-        const int t = tb + tt, c = cb + cc;
-        s[tt][cc] = (t < NT && c <= NC) ? gbl(dir)[(int64_t)t * kTileDirStride(NC) + c] : (uint16_t)0;
+    // the block's 64 rows of 65 offsets as 33 4-B words each (rows start 4-B aligned: the row
+    // stride and the block's first bucket are even; a word past the row's NC + 2 entries is not
+    // read), instead of 2-B loads
+    for (int i = threadIdx.x; i < 64 * 33; i += 256) {
+        const int tt = i / 33, k = i % 33;
+        const int t = tb + tt, c = cb + 2 * k;
+        uint32_t w = 0;
+        if (t < NT && c <= NC) w = *gbl(reinterpret_cast<const uint32_t*>(dir + (int64_t)t * kTileDirStride(NC) + c));
+        s[tt][2 * k] = (uint16_t)w;
+        s[tt][2 * k + 1] = (uint16_t)(w >> 16);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * 64; i += 256) {

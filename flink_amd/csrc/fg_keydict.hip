@@ -91,7 +91,7 @@ struct DictDev {
     uint64_t* ent_tag;   // [ids] tag (0: resolved on the host, not in the table)
     uint8_t* arena;
     unsigned long long* counters;   // [0] ids, [1] arena bytes, [2] collisions, [3] bad rows, [4] pending rows,
-                                    // [5] entry bytes (k_dict_check), [6] lookup misses
+                                    // [5] entry bytes of the lookup's misses, [6] lookup misses
     uint64_t mask;       // cap - 1
     int32_t kg_bits;     // id = ordinal << kg_bits | key group
 };
@@ -121,49 +121,11 @@ struct RowsIn {
     int64_t nbytes;
     int32_t max_p;
     int32_t tag_bits;
+    int32_t check;          // device rows: k_dict_lookup checks them (bad rows -> counters[3])
 };
 
 // arena bytes an entry of a row of `len` bytes takes: [id i64][row bytes, padded to 8]
 __host__ __device__ __forceinline__ uint64_t entry_bytes(int32_t len) { return 8 + (((uint64_t)len + 7) & ~7ull); }
-
-// device rows: offsets / lengths checked before anything is inserted (counters[3]), and the
-// arena bytes the call may take if every row is new (counters[5]: rows may overlap in the
-// caller's buffer, so this is not bounded by its size)
-// Grid-stride with a fixed grid (kCheckBlocks): each thread sums its rows' entry bytes, the
-// block reduces them, one atomic per block -- the totals land on one counter word, and one
-// atomic per wave (781k for 50M rows) serialized there for ~9 ms.
-constexpr unsigned kCheckBlocks = 1024;
-__global__ __launch_bounds__(kDictThreads) void k_dict_check(RowsIn in, unsigned long long* counters) {
-    __shared__ unsigned long long s_sum[kDictThreads / 64], s_bad[kDictThreads / 64];
-    unsigned long long sum = 0, nbad = 0;
-    for (int64_t i = (int64_t)blockIdx.x * kDictThreads + threadIdx.x; i < in.n;
-         i += (int64_t)gridDim.x * kDictThreads) {
-        const int32_t len = in.len[i];
-        const int64_t off = in.off[i];
-        const bool bad = len < 0 || len >= (1 << 24) || (len & 3) != 0 || off < 0 || (off & 3) != 0 ||
-                         off + len > in.nbytes;   // (BinaryRowData rows are 8-byte multiples)
-        nbad += bad ? 1u : 0u;
-        sum += bad ? 0u : entry_bytes(len);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        sum += __shfl_xor(sum, o);
-        nbad += __shfl_xor(nbad, o);
-    }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) {
-        s_sum[wave] = sum;
-        s_bad[wave] = nbad;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kDictThreads / 64; w++) {
-            sum += s_sum[w];
-            nbad += s_bad[w];
-        }
-        if (nbad) atomicAdd(&counters[3], nbad);
-        if (sum) atomicAdd(&counters[5], sum);
-    }
-}
 
 // Both hashes of a row in one pass over its 4-byte words: the Flink hash (hashBytesByWords,
 // seed 42) and the table's own 64-bit tag (independent of it: equal Flink hashes are common at
@@ -322,13 +284,29 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_lookup(DictDev d, RowsIn 
     const uint8_t* rp[R];
     uint32_t r[R][kRegWords];
     uint64_t t[R], s[R];
+    uint32_t nbad = 0;
 #pragma unroll
     for (int u = 0; u < R; u++) {   // (every lane stays for the wave-wide reservations below)
         const int64_t i0 = b0 + (int64_t)u * kDictThreads;
         valid[u] = i0 < in.n;
         ii[u] = valid[u] ? i0 : 0;
         len[u] = in.len[ii[u]];
-        rp[u] = in.bytes + in.off[ii[u]];
+        const int64_t off = in.off[ii[u]];
+        if (in.check && valid[u]) {   // device rows: inside the buffer, 4-byte words (BinaryRowData)
+            const bool bad = len[u] < 0 || len[u] >= (1 << 24) || (len[u] & 3) != 0 || off < 0 || (off & 3) != 0 ||
+                             off + len[u] > in.nbytes;
+            if (bad) {
+                nbad++;
+                valid[u] = false;   // (not looked up; the call fails before anything is inserted)
+                len[u] = 0;
+            }
+        }
+        rp[u] = in.bytes + (valid[u] ? off : 0);
+    }
+    if (in.check) {
+        uint32_t b = nbad;
+        for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o);
+        if ((threadIdx.x & 63) == 0 && b) atomicAdd(&d.counters[3], (unsigned long long)b);
     }
 #pragma unroll
     for (int u = 0; u < R; u++) {
@@ -372,6 +350,10 @@ __global__ __launch_bounds__(kDictThreads) void k_dict_lookup(DictDev d, RowsIn 
         const bool m = valid[u] && !found;
         const unsigned long long w = wave_reserve(&d.counters[6], m ? 1u : 0u);
         if (m) miss[w] = (uint32_t)ii[u];
+        // the arena bytes the misses may take as new entries (counters[5], one atomic per wave)
+        uint64_t eb = m ? entry_bytes(len[u]) : 0;
+        for (int o = 32; o > 0; o >>= 1) eb += __shfl_xor(eb, o);
+        if ((threadIdx.x & 63) == 0 && eb) atomicAdd(&d.counters[5], (unsigned long long)eb);
     }
 }
 
@@ -584,6 +566,20 @@ struct fg_key_dict {
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     fg_kernel_stat kstat[2] = {};
+    // fg_key_dict_intern_async: the lookup launched, the rest of the call taken by _wait
+    struct Pending {
+        bool active = false, host = false;
+        int64_t n = 0, nbytes = 0;
+        RowsIn in{};
+        int64_t* ids = nullptr;
+        int32_t* kg_dev = nullptr;
+        const uint8_t* bytes = nullptr;
+        const int64_t* offsets = nullptr;
+        const int32_t* lengths = nullptr;
+        int64_t* out_id = nullptr;
+        int32_t* out_kg = nullptr;
+        uint64_t entry_need = 0;   // host rows: every row as a new entry
+    } pend;
 
     int fail(int rc, const std::string& m) {
         err = m;
@@ -723,10 +719,13 @@ int fg_key_dict_open(int32_t device_id, int32_t max_parallelism, int64_t expecte
     return FG_OK;
 }
 
-int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_t* bytes, int64_t nbytes,
-                       const int64_t* offsets, const int32_t* lengths, int64_t* out_id, int32_t* out_kg) {
+// The first half of an intern call: arguments checked, scratch sized, the lookup of every row
+// launched (device rows are checked by the lookup itself: a bad row is counted, not looked up,
+// and the call fails in intern_finish before anything is inserted). No host synchronization.
+static int intern_begin(fg_key_dict* d, int32_t location, int64_t n, const uint8_t* bytes, int64_t nbytes,
+                        const int64_t* offsets, const int32_t* lengths, int64_t* out_id, int32_t* out_kg) {
     if (!d) return FG_EINVAL;
-    if (n == 0) return FG_OK;
+    if (d->pend.active) return d->fail(FG_ESTATE, "fg_key_dict_intern: an async intern is pending (fg_key_dict_intern_wait)");
     if (n < 0 || n > 0x7fffffff || !bytes || nbytes < 0 || !offsets || !lengths || !out_id)
         return d->fail(FG_EINVAL, "fg_key_dict_intern: invalid arguments");
     if (hipSetDevice(d->device) != hipSuccess) return d->fail(FG_EDEVICE, "hipSetDevice failed");
@@ -734,7 +733,7 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     const bool host = location == FG_HOST;
     if (!host && (uintptr_t)bytes % 4 != 0)
         return d->fail(FG_EINVAL, "fg_key_dict_intern: the row buffer must be 4-byte aligned");
-    uint64_t entry_need = 0;   // arena bytes if every row is new (rows may overlap in the buffer)
+    uint64_t entry_need = 0;   // host rows: arena bytes if every row is new
     if (host) {   // validate on the host: every row inside the buffer, 4-byte words
         for (int64_t i = 0; i < n; i++) {
             if (lengths[i] < 0 || lengths[i] >= (1 << 24) || (lengths[i] & 3) || (offsets[i] & 3) || offsets[i] < 0 ||
@@ -753,6 +752,7 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     in.nbytes = nbytes;
     in.max_p = d->max_p;
     in.tag_bits = d->tag_bits;
+    in.check = host ? 0 : 1;
     if (host) {
         DCHK(d, d->in_bytes.ensure((size_t)nbytes + 8, s));
         DCHK(d, d->in_off.ensure(8 * (size_t)n, s));
@@ -773,24 +773,6 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
         DCHK(d, d->row_id.ensure(8 * (size_t)n, s));
         ids = d->row_id.as<int64_t>();
     }
-    const unsigned g = grid_of(n);
-    if (!host) {   // device rows are checked on the device before anything is inserted
-        hipLaunchKernelGGL(k_dict_check, dim3(std::min(g, kCheckBlocks)), dim3(kDictThreads), 0, s, in,
-                           d->counters.as<unsigned long long>());
-        DCHK(d, hipGetLastError());
-        unsigned long long chk[3] = {0, 0, 0};   // counters[3..5]: bad rows, (pending), entry bytes
-        DCHK(d, hipMemcpyAsync(chk, d->counters.as<unsigned long long>() + 3, sizeof chk, hipMemcpyDeviceToHost, s));
-        DCHK(d, hipMemsetAsync(d->counters.as<unsigned long long>() + 5, 0, 8, s));
-        if (chk[0]) DCHK(d, hipMemsetAsync(d->counters.as<unsigned long long>() + 3, 0, 8, s));
-        DCHK(d, hipStreamSynchronize(s));
-        if (chk[0])
-            return d->fail(FG_EINVAL, "fg_key_dict_intern: " + std::to_string(chk[0]) +
-                                          " key rows outside the buffer or not a multiple of 4 bytes");
-        entry_need = chk[2];
-    }
-    // k_dict_assign writes a new row's entry at a reserved arena offset without a bound check:
-    // the arena holds every row of the call as a new entry
-    DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)entry_need + 16, s, (size_t)d->arena_used));
     int32_t* kg_dev = nullptr;   // every row's key group, when asked for
     if (out_kg) {
         if (host) {
@@ -800,19 +782,58 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
             kg_dev = out_kg;
         }
     }
-    // 1) lookup of every row: one random 64-B slot per row; the misses are listed
-    DCHK(d, d->miss.ensure(4 * (size_t)n, s));
+    // 1) lookup of every row: one random 64-B slot per row; the misses are listed, their arena
+    // bytes summed (counters[5]), bad device rows counted (counters[3])
+    DCHK(d, d->miss.ensure(4 * (size_t)std::max<int64_t>(n, 1), s));
     unsigned long long* ctr = d->counters.as<unsigned long long>();
-    DCHK(d, hipMemsetAsync(ctr + 6, 0, 8, s));
-    if (d->timing) DCHK(d, hipEventRecord(d->ev[0], s));
-    hipLaunchKernelGGL(k_dict_lookup, dim3((unsigned)((n + (int64_t)kDictThreads * kLookupRows - 1) /
-                                                ((int64_t)kDictThreads * kLookupRows))),
-                       dim3(kDictThreads), 0, s, d->dev(), in, kg_dev, ids, d->miss.as<uint32_t>());
-    if (d->timing) DCHK(d, hipEventRecord(d->ev[1], s));
-    DCHK(d, hipGetLastError());
+    DCHK(d, hipMemsetAsync(ctr + 5, 0, 16, s));   // [5] miss entry bytes, [6] misses
+    if (n > 0) {
+        if (d->timing) DCHK(d, hipEventRecord(d->ev[0], s));
+        hipLaunchKernelGGL(k_dict_lookup, dim3((unsigned)((n + (int64_t)kDictThreads * kLookupRows - 1) /
+                                                    ((int64_t)kDictThreads * kLookupRows))),
+                           dim3(kDictThreads), 0, s, d->dev(), in, kg_dev, ids, d->miss.as<uint32_t>());
+        if (d->timing) DCHK(d, hipEventRecord(d->ev[1], s));
+        DCHK(d, hipGetLastError());
+    }
+    auto& pc = d->pend;
+    pc.active = true;
+    pc.host = host;
+    pc.n = n;
+    pc.nbytes = nbytes;
+    pc.in = in;
+    pc.ids = ids;
+    pc.kg_dev = kg_dev;
+    pc.bytes = bytes;
+    pc.offsets = offsets;
+    pc.lengths = lengths;
+    pc.out_id = out_id;
+    pc.out_kg = out_kg;
+    pc.entry_need = entry_need;
+    return FG_OK;
+}
+
+// The second half: the lookup's counters (one synchronization), then the misses -- none in a
+// steady state -- in chunks, and the collisions.
+static int intern_finish(fg_key_dict* d) {
+    if (!d) return FG_EINVAL;
+    if (!d->pend.active) return FG_OK;
+    auto pc = d->pend;
+    d->pend.active = false;
+    hipStream_t s = d->stream;
+    const int64_t n = pc.n;
+    RowsIn in = pc.in;
+    int64_t* ids = pc.ids;
+    unsigned long long* ctr = d->counters.as<unsigned long long>();
     unsigned long long cnt[7];
     DCHK(d, hipMemcpyAsync(cnt, ctr, sizeof cnt, hipMemcpyDeviceToHost, s));
     DCHK(d, hipStreamSynchronize(s));
+    if (n == 0) return FG_OK;
+    if (cnt[3]) {   // bad device rows: nothing was inserted
+        DCHK(d, hipMemsetAsync(ctr + 3, 0, 8, s));
+        DCHK(d, hipStreamSynchronize(s));
+        return d->fail(FG_EINVAL, "fg_key_dict_intern: " + std::to_string(cnt[3]) +
+                                      " key rows outside the buffer or not a multiple of 4 bytes");
+    }
     if (d->timing) {
         float ms = 0.f;
         DCHK(d, hipEventElapsedTime(&ms, d->ev[0], d->ev[1]));
@@ -822,9 +843,15 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     }
     uint64_t collisions = cnt[2];
     const int64_t nmiss = (int64_t)cnt[6];
+    if (nmiss > 0) {
+        // k_dict_assign writes a new row's entry at a reserved arena offset without a bound check:
+        // the arena holds every missed row of the call as a new entry
+        const uint64_t need = pc.host ? pc.entry_need : cnt[5];
+        DCHK(d, d->arena.ensure((size_t)d->arena_used + (size_t)need + 16, s, (size_t)d->arena_used));
+    }
     // 2) the misses, in chunks the table has room for: it stays at most half full even if every
     // row of a chunk is new. It grows when that room falls under an eighth of the ids (and 1M
-    // rows): to 3 x (ids + 1M) slots rounded up -- sized by the distinct keys, not by the calls.
+    // rows): to FG_DICT_GROW x (ids + 1M) slots rounded up -- sized by the distinct keys.
     for (int64_t pos = 0; pos < nmiss;) {
         const int64_t room = (int64_t)(d->cap / 2) - d->nids;
         if (room < std::max<int64_t>(1 << 20, d->nids / 8))
@@ -863,17 +890,38 @@ int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_
     collisions = cnt[2];
     if (collisions) {   // rows whose tag another row holds: exact ids from the host-side map
         DCHK(d, hipMemsetAsync(ctr + 2, 0, 8, s));
-        if (int rc = resolve_collisions(d, host, n, bytes, nbytes, offsets, lengths, ids)) return rc;
+        if (int rc = resolve_collisions(d, pc.host, n, pc.bytes, pc.nbytes, pc.offsets, pc.lengths, ids)) return rc;
     }
-    if (host) DCHK(d, hipMemcpy(out_id, ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
-    if (out_kg && host) DCHK(d, hipMemcpy(out_kg, kg_dev, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    if (pc.host) DCHK(d, hipMemcpy(pc.out_id, ids, 8 * (size_t)n, hipMemcpyDeviceToHost));
+    if (pc.out_kg && pc.host) DCHK(d, hipMemcpy(pc.out_kg, pc.kg_dev, 4 * (size_t)n, hipMemcpyDeviceToHost));
     return FG_OK;
+}
+
+int fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_t* bytes, int64_t nbytes,
+                       const int64_t* offsets, const int32_t* lengths, int64_t* out_id, int32_t* out_kg) {
+    if (!d) return FG_EINVAL;
+    if (n == 0 && !d->pend.active) return FG_OK;
+    if (int rc = intern_begin(d, location, n, bytes, nbytes, offsets, lengths, out_id, out_kg)) return rc;
+    return intern_finish(d);
+}
+
+int fg_key_dict_intern_async(fg_key_dict* d, int64_t n, const uint8_t* bytes, int64_t nbytes, const int64_t* offsets,
+                             const int32_t* lengths, int64_t* out_id, int32_t* out_kg) {
+    if (!d) return FG_EINVAL;
+    return intern_begin(d, FG_DEVICE, n, bytes, nbytes, offsets, lengths, out_id, out_kg);
+}
+
+int fg_key_dict_intern_wait(fg_key_dict* d) {
+    if (!d) return FG_EINVAL;
+    if (hipSetDevice(d->device) != hipSuccess) return d->fail(FG_EDEVICE, "hipSetDevice failed");
+    return intern_finish(d);
 }
 
 int fg_key_dict_lookup(fg_key_dict* d, int32_t location, int64_t n, const int64_t* ids, int64_t* out_offsets,
                        int32_t* out_lengths) {
     if (!d) return FG_EINVAL;
     if (n == 0) return FG_OK;
+    if (d->pend.active) return d->fail(FG_ESTATE, "fg_key_dict_lookup: an async intern is pending (fg_key_dict_intern_wait)");
     if (n < 0 || !ids || !out_offsets || !out_lengths) return d->fail(FG_EINVAL, "fg_key_dict_lookup: invalid arguments");
     if (hipSetDevice(d->device) != hipSuccess) return d->fail(FG_EDEVICE, "hipSetDevice failed");
     hipStream_t s = d->stream;
@@ -909,6 +957,8 @@ int fg_key_dict_arena(fg_key_dict* d, const uint8_t** dev_bytes, int64_t* size) 
 }
 
 int fg_key_dict_copy_arena(fg_key_dict* d, int64_t begin, int64_t nbytes, uint8_t* host) {
+    if (d && d->pend.active)
+        return d->fail(FG_ESTATE, "fg_key_dict_copy_arena: an async intern is pending (fg_key_dict_intern_wait)");
     if (!d || begin < 0 || nbytes < 0 || begin + nbytes > d->arena_used || (nbytes && !host))
         return d ? d->fail(FG_EINVAL, "fg_key_dict_copy_arena: range outside the arena") : FG_EINVAL;
     if (!nbytes) return FG_OK;

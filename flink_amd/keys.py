@@ -143,6 +143,33 @@ class KeyDictionary:
             raise L.WindowSpecError(msg)
         raise L.FlinkGpuError(rc, msg)
 
+    def intern_async(self, packed, key_groups=False):
+        """fg_key_dict_intern_async of device rows packed=(bytes u8, offsets i64, lengths i32
+        tensors): the lookup is launched on the dictionary's stream and (ids, key_groups) tensors
+        are returned at once -- complete after intern_wait(). The packed tensors must stay alive
+        until then."""
+        import torch
+        buf, off, ln = packed
+        n = len(off)
+        ext = self.__dict__.get("_ext_stream")
+        if ext is None or ext.device != buf.device:
+            ext = self._ext_stream = torch.cuda.ExternalStream(self._lib.fg_key_dict_stream(self._h), device=buf.device)
+        ext.wait_stream(torch.cuda.current_stream(buf.device))
+        ids = torch.empty(n, dtype=torch.int64, device=buf.device)
+        kg = torch.empty(n, dtype=torch.int32, device=buf.device) if key_groups else None
+        self._pending = (buf, off, ln, ids, kg)
+        self._check(self._lib.fg_key_dict_intern_async(self._h, n, C.c_void_p(buf.data_ptr()), buf.numel(),
+                                                       C.c_void_p(off.data_ptr()), C.c_void_p(ln.data_ptr()),
+                                                       C.c_void_p(ids.data_ptr()),
+                                                       C.c_void_p(kg.data_ptr() if key_groups else None)))
+        return ids, kg
+
+    def intern_wait(self):
+        """fg_key_dict_intern_wait: the pending intern_async's ids (and key groups) complete"""
+        rc = self._lib.fg_key_dict_intern_wait(self._h)
+        self._pending = None
+        self._check(rc)
+
     def intern(self, rows=None, packed=None, key_groups=True):
         """rows: list of key-row bytes, or packed=(bytes u8[], offsets i64[], lengths i32[]) on the
         host (numpy) or the device (torch tensors). Returns (ids, key_groups) of the same kind

@@ -390,6 +390,15 @@ int  fg_key_dict_open(int32_t device_id, int32_t max_parallelism, int64_t expect
  * producer before it; the outputs are complete when the call returns. */
 int  fg_key_dict_intern(fg_key_dict* d, int32_t location, int64_t n, const uint8_t* bytes, int64_t nbytes,
                         const int64_t* offsets, const int32_t* lengths, int64_t* out_id, int32_t* out_kg);
+/* fg_key_dict_intern of device rows in two halves (ABI 13): _async launches the lookup of every
+ * row on the dictionary's stream (fg_key_dict_stream) and returns at once; _wait synchronizes,
+ * interns the rows the table did not hold yet and resolves tag collisions -- out_id / out_kg are
+ * complete when it returns. A key selector interns the next micro-batch's rows while the engine
+ * aggregates the current one. One call pending per dictionary (FG_ESTATE otherwise); bad rows are
+ * reported by _wait, before anything is inserted. */
+int  fg_key_dict_intern_async(fg_key_dict* d, int64_t n, const uint8_t* bytes, int64_t nbytes, const int64_t* offsets,
+                              const int32_t* lengths, int64_t* out_id, int32_t* out_kg);
+int  fg_key_dict_intern_wait(fg_key_dict* d);
 /* For each id: its row's offset and length in the dictionary's arena (-1 / -1 for an unknown id). */
 int  fg_key_dict_lookup(fg_key_dict* d, int32_t location, int64_t n, const int64_t* ids, int64_t* out_offsets,
                         int32_t* out_lengths);

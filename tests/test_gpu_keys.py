@@ -281,3 +281,82 @@ def test_intern_chunked_call_unaligned_rows_and_no_key_groups():
     assert np.array_equal(ids4.cpu().numpy(), ids)
     assert len(d) == len(distinct)
     d.close()
+
+
+def test_intern_async_matches_sync_and_overlaps_the_engine():
+    """fg_key_dict_intern_async + _wait: the same id partition as the one-call intern for new and known rows
+    (misses interned in _wait), key groups when asked for, one call pending at a time (a second
+    async call, a lookup or a copy of the arena in between fail with FG_ESTATE), bad device rows
+    reported by _wait with nothing inserted -- and the window engine fed the awaited ids gives the
+    oracle's rows while the next batch's lookup runs beside it."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(21)
+    keys = random_keys(rng, 20_000)
+    rows_all = [K.key_row(list(k), TYPES) for k in keys]
+    d = F.KeyDictionary(max_parallelism=MAXP, expected_keys=1000)
+    ref = F.KeyDictionary(max_parallelism=MAXP, expected_keys=1000)
+    seen = {}
+
+    def packed_dev(rows):
+        buf, off, ln = K.pack_key_rows(rows)
+        return torch.from_numpy(buf.copy()).to(dev), torch.from_numpy(off).to(dev), torch.from_numpy(ln).to(dev)
+
+    for b in range(4):   # the first batches hold mostly new rows, the later ones mostly known
+        rows = [rows_all[i] for i in rng.integers(0, len(rows_all) * (b + 1) // 4, 30_000)]
+        p = packed_dev(rows)
+        ids_t, kg_t = d.intern_async(p, key_groups=True)
+        with pytest.raises(F.FlinkGpuError):
+            d.intern_async(p)
+        with pytest.raises(F.FlinkGpuError):
+            d.lookup(np.zeros(1, dtype=np.int64))
+        d.intern_wait()
+        ids_r, kg_r = ref.intern(rows)   # ordinals are assigned in parallel: the same partition
+        pairs = np.unique(np.stack([ids_t.cpu().numpy(), ids_r]), axis=1)
+        assert len(np.unique(pairs[0])) == len(np.unique(pairs[1])) == pairs.shape[1]
+        assert np.array_equal(kg_t.cpu().numpy(), kg_r)
+        for r, i in check_interned(d, rows, ids_t.cpu().numpy(), kg_t.cpu().numpy()).items():
+            assert seen.setdefault(r, i) == i, "an id changed across calls"
+    n0 = len(d)
+    bad = (torch.zeros(64, dtype=torch.uint8, device=dev), torch.tensor([4, 60], device=dev),
+           torch.tensor([16, 8], dtype=torch.int32, device=dev))
+    d.intern_async(bad)
+    with pytest.raises(F.WindowSpecError):
+        d.intern_wait()
+    assert len(d) == n0
+    d.intern_wait()   # nothing pending: a no-op
+    # the pipeline of bench.py --keys string: batch k+1's lookup beside batch k's aggregation
+    from tests.test_gpu_parity import assert_rows_equal, cfg_of, gpu_mk, oracle_mk
+    index = {}
+    n, batch = 240_000, 40_000
+    pick = rng.integers(0, len(rows_all), n)
+    ts = (1_000_000 + np.arange(n) // 100 + rng.integers(0, 300, n)).astype(np.int64)
+    val = rng.random(n) * 1000.0
+    cfg = cfg_of("tumble", 1000)
+    g = gpu_mk(cfg, expected_keys=len(rows_all))
+    o = oracle_mk(O, cfg)
+    packs = [packed_dev([rows_all[i] for i in pick[lo:lo + batch]]) for lo in range(0, n, batch)]
+    k_next, _ = d.intern_async(packs[0])
+    d.intern_wait()
+    for bi, lo in enumerate(range(0, n, batch)):
+        hi = lo + batch
+        k = k_next
+        if bi + 1 < len(packs):
+            k_next, _ = d.intern_async(packs[bi + 1])
+        g.process_batch(k, torch.from_numpy(ts[lo:hi]).to(dev), torch.from_numpy(val[lo:hi]).to(dev))
+        o.process_batch(pick[lo:hi].astype(np.int64), ts[lo:hi], val[lo:hi])
+        wm = int(ts[hi - 1]) - 400
+        g.process_watermark(wm)
+        o.process_watermark(wm)
+        if bi + 1 < len(packs):
+            d.intern_wait()
+    g.process_watermark((1 << 63) - 1)
+    o.process_watermark((1 << 63) - 1)
+    r = g.take_rows()
+    index = {rows_all[i]: i for i in range(len(rows_all))}
+    r["key"] = [index[x] for x in d.lookup(r["key"])]
+    assert_rows_equal(r, o.take_rows(), "f64", "async intern pipeline")
+    g.close()
+    o.close()
+    d.close()
+    ref.close()
