@@ -264,7 +264,7 @@ def cpu_baseline(args, rate):
                        (f"; the cgroup grants {quota:g} CPUs of time" if quota else ""))
 
 
-def pmc_traffic(kernel_class):
+def pmc_traffic(kernel_class, workload="tumble"):
     """HBM bytes per launch of `kernel_class` from the newest committed rocprofv3 PMC summary
     (profiles/**/pmc_traffic.json, profiles/pmc_summary.py) -- only if it was counted on THIS
     build's kernels (same sha256 of libflinkgpu.so's device code objects, flink_amd.buildinfo: a
@@ -283,6 +283,8 @@ def pmc_traffic(kernel_class):
         except Exception:
             continue
         if d.get("_provenance", {}).get("kernels_sha256") != ksha:
+            continue
+        if d["_provenance"].get("workload", "tumble") != workload:   # counted on another workload's launches
             continue
         v = d.get(kernel_class.replace("local_", ""), {}).get("hbm_bytes_per_launch")
         if v is not None:
@@ -730,7 +732,7 @@ def main():
     # dictionary's probe: the 32-B key row read + the 8-B id written per row
     alg_bytes = ((40 if dom_name.startswith("dict_") else 24) * dom["records"] + 48 * dom["rows"]) / dom["launches"]
     achieved = alg_bytes / avg_s / 1e9
-    traffic, traffic_src = pmc_traffic(dom_name)
+    traffic, traffic_src = pmc_traffic(dom_name, args.workload)
 
     copy_gbs = measure_copy_peak(dev)
     total_records = world * n * args.steps

@@ -208,25 +208,6 @@ __device__ __forceinline__ void row_hashes_reg(const uint32_t (&r)[kRegWords], i
     *tag = h ? h : 1;
     *fh = (int32_t)fmix32(h1 ^ (uint32_t)len);
 }
-// entry_id_if_equal against register words (entries are 8-byte aligned: 8-byte loads)
-__device__ __forceinline__ int64_t entry_id_if_equal_reg(const DictDev& d, uint64_t loc, const uint32_t (&r)[kRegWords],
-                                                         int32_t len) {
-    if ((int32_t)(loc & 0xFFFFFF) != len) return -1;
-    const uint8_t* e = d.arena + (loc >> 24);
-    const int32_t nw = len >> 2;
-    uint32_t diff = 0;
-#pragma unroll
-    for (int k = 0; k < kRegWords; k += 2) {
-        if (k + 2 <= nw) {
-            const uint2 v = *reinterpret_cast<const uint2*>(e + 8 + 4 * k);
-            diff |= (v.x ^ r[k]) | (v.y ^ r[k + 1]);
-        } else if (k < nw) {
-            diff |= *reinterpret_cast<const uint32_t*>(e + 8 + 4 * k) ^ r[k];
-        }
-    }
-    return diff == 0 ? *reinterpret_cast<const int64_t*>(e) : -1;
-}
-
 // The id of a written slot if its row equals the row (register words r when `small`, else the
 // words at w): the slot's words first, an entry's bytes past them only for rows longer than the
 // slot holds; -1 for a distinct row with an equal tag.

@@ -77,6 +77,9 @@ if __name__ == "__main__":
         lib = sys.argv[3] if len(sys.argv) > 3 else None
         t["_provenance"] = {"lib_sha256": buildinfo.file_sha256(lib) if lib else None,
                             "kernels_sha256": buildinfo.kernels_sha256(lib) if lib else None,
-                            "source": sys.argv[1]}
+                            "source": sys.argv[1],
+                            # the bench workload counted (a kernel class's bytes differ by workload:
+                            # the CUMULATE tile_fire reads and writes tables, the TUMBLE one does not)
+                            "workload": sys.argv[4] if len(sys.argv) > 4 else os.environ.get("WL") or "tumble"}
         json.dump(t, open(sys.argv[2], "w"), indent=1)
         print("wrote", sys.argv[2])
