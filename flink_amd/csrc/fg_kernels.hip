@@ -3022,6 +3022,12 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
         for (int w = tid; w <= NW; w += T) s_cw[w] = 0;
         lds_barrier();
     }
+    // tiles past the segment's end (a short last segment, or none): empty directory rows -- the
+    // fire reads every workgroup's max_tiles rows, and the buffer holds the last batch's
+    for (; j < p.max_tiles; j++) {
+        uint32_t* drow = reinterpret_cast<uint32_t*>(p.dir + ((int64_t)blockIdx.x * p.max_tiles + j) * kTileDirStride(NC));
+        for (int w = tid; w <= NW; w += T) drow[w] = 0u;
+    }
     for (int off = 32; off > 0; off >>= 1) {
         drops += __shfl_down(drops, off);
         mask |= __shfl_down(mask, off);

@@ -1133,3 +1133,28 @@ def test_sparse_regions_parity(oracle_mod, monkeypatch, bits, name, kind, case):
         test_datastream_allowed_lateness_parity(oracle_mod, *case)
     else:
         test_snapshot_restore_many_regions(oracle_mod, case)
+
+
+def test_tile_batches_with_a_short_last_segment(oracle_mod):
+    """Tile staging with a pass-1 workgroup holding fewer tiles than the others: a batch of
+    256 x 18,434 records (every workgroup 4 tiles, the last tile of each 2 records), then one of
+    100 records fewer (the last workgroup 3 tiles). The missing tile's directory row must read as
+    empty, not as the previous batch's row -- whose fragment would re-count the previous batch's
+    last records (still in the reused tile buffer) into this batch's window. The batches fill
+    windows 0 and 4: the same slice lane of 4, so the stale row's columns are the lane's own."""
+    cfg = cfg_of("tumble", 1000)
+    rng = np.random.default_rng(77)
+    g = gpu_mk(cfg, expected_keys=100_000, buffer_records=1 << 23)
+    o = oracle_mk(oracle_mod, cfg)
+    for b, n in enumerate((256 * 18_434, 256 * 18_434 - 100)):
+        key = rng.integers(0, 100_000, n).astype(np.int64)
+        w0 = 4000 * b
+        ts = (w0 + np.sort(rng.integers(0, 1000, n))).astype(np.int64)
+        val = rng.random(n) * 100.0
+        g.process_batch(key, ts, val)
+        o.process_batch(key, ts, val)
+        g.process_watermark(w0 + 999)
+        o.process_watermark(w0 + 999)
+        assert_rows_equal(g.take_rows(), o.take_rows(), "f64", f"batch {b} ({n} records)")
+    g.close()
+    o.close()
