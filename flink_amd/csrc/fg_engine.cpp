@@ -594,9 +594,23 @@ int side_create(fg_handle* h, std::map<int64_t, std::unique_ptr<SliceTable>>& m,
 
 TableRef ref_of(SliceTable* t) { return TableRef{t->data.as<int64_t>(), t->counts.as<uint32_t>()}; }
 
-// device scalars: [0] overflow flags (u32), [8] fired-row counter (u64), [16] fail count (u32)
+// device scalars: [0] overflow flags (u32), [4] fail count (u32), [8] fired-row counter (u64)
+// (flags and fail count adjacent: one 8-B fill zeroes both and keeps the counter)
 constexpr size_t kScalarBytes = 24;
-uint32_t fail_count(const fg_handle* h) { return h->h_scalars.as<uint32_t>()[4]; }
+uint32_t fail_count(const fg_handle* h) { return h->h_scalars.as<uint32_t>()[1]; }
+// zero the flags, the fired-row counter (with_out) and -- no job pending -- the fail count, in as
+// few fills as the layout allows
+int zero_scalars(fg_handle* h, bool with_out) {
+    const bool fail = h->jobs.empty();
+    if (fail) {
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, with_out ? 16 : 8, h->stream));
+        h->fail_zeroed = true;
+    } else {
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 4, h->stream));
+        if (with_out) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 8, 0, 8, h->stream));
+    }
+    return FG_OK;
+}
 
 int check_overflow(fg_handle* h) {
     // region overflows (bits 0 and 2) are handled by the fail list (settle_jobs)
@@ -616,7 +630,7 @@ int lanes_for(int bits) {
 
 // A new job set starts after every synchronization: zero its fail count.
 int job_add(fg_handle* h, MergeJob&& j, int* id) {
-    if (h->jobs.empty() && !h->fail_zeroed) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 16, 0, 8, h->stream));
+    if (h->jobs.empty() && !h->fail_zeroed) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 4, 0, 4, h->stream));
     h->fail_zeroed = false;
     j.bits = h->region_bits;
     h->jobs.push_back(std::move(j));
@@ -718,7 +732,7 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     p->overflow = h->scalars.as<unsigned int>();
     p->out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
     p->fail_list = h->fail_list.as<uint32_t>();
-    p->fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 16);
+    p->fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 4);
     p->fail_cap = kFailCap;
     p->job = ji;
     p->mark_mask = j.mark_mask;
@@ -768,11 +782,15 @@ int tile_job_params(fg_handle* h, int ji, TileFire* f) {
     p.overflow = h->scalars.as<unsigned int>();
     p.out_count = reinterpret_cast<unsigned long long*>(h->scalars.as<char>() + 8);
     p.fail_list = h->fail_list.as<uint32_t>();
-    p.fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 16);
+    p.fail_n = reinterpret_cast<uint32_t*>(h->scalars.as<char>() + 4);
     p.fail_cap = kFailCap;
     p.job = ji;
     f->n_passes = (int32_t)tps.size();
     f->tbits = j.tbits;
+    if (tps.size() == 1) {   // (the common case: one pass per lane, in the kernel's arguments)
+        f->one = tps[0];
+        return FG_OK;
+    }
     return arena_put(h, tps.data(), tps.size(), &f->passes);
 }
 
@@ -846,8 +864,7 @@ int retry_failed(fg_handle* h) {
         int rc = grow(h, h->region_bits + 1);
         if (rc) return rc;
         h->arena_used = 0;
-        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 4, h->stream));                    // flags
-        HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 16, 0, 8, h->stream));     // fail count
+        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // flags and fail count
         for (auto& kv : per_job) {
             MergeJob& j = h->jobs[(size_t)kv.first];
             const int sh = h->region_bits - j.bits;
@@ -953,7 +970,7 @@ int fire_collect(fg_handle* h);
 // zero the overflow word and the fired-row counter once per advance
 int reset_out_count(fg_handle* h) {
     if (!h->out_count_reset) {
-        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+        if (int rc = zero_scalars(h, true)) return rc;
         // rows fired by late elements, or by async advances not yet collected, lead the advance's rows
         if (h->adv_base + h->late_rows > 0) {
             Words16 w{};
@@ -1181,11 +1198,10 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
     // job is pending) zeroed by one fill: reset_out_count and job_add then need none of their own
     bool zeroed_out = false;
     if (h->out_count_reset) {
-        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 8, h->stream));   // keep out_count
+        if (int rc0 = zero_scalars(h, false)) return rc0;   // keep out_count
     } else {
-        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, h->jobs.empty() ? 24 : 16, h->stream));
+        if (int rc0 = zero_scalars(h, true)) return rc0;
         zeroed_out = true;
-        h->fail_zeroed = h->jobs.empty();
     }
     std::vector<int64_t> fired_tables, retained;
     bool any_emit = false;
@@ -4053,7 +4069,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         j.srcs.push_back(t);
         j.dst = t;
         j.kclass = K_RESTORE;
-        HIPCHK(h, hipMemsetAsync(h->scalars.p, 0, 16, h->stream));
+        if (int rc0 = zero_scalars(h, true)) return rc0;
         int ji = 0;
         rc = job_add(h, std::move(j), &ji);
         if (rc) return rc;

@@ -3445,7 +3445,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 }
             };
             for (int pi = 0; pi < f.n_passes; pi++) {
-                const TilePass tp = f.passes[pi];
+                const TilePass tp = f.n_passes == 1 ? f.one : f.passes[pi];
                 TileWalk w;
                 tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane);
                 int32_t ka[kTileRpl], kb[kTileRpl];
