@@ -1540,9 +1540,11 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C, MV>& t, int64_t k, u
 __device__ __forceinline__ void write_row_k(const MergeParams& p, unsigned long long o, int64_t key,
                                             unsigned long long cs, unsigned long long cn, const int64_t* vals, int vt) {
     p.out_key[o] = key;
+#ifndef FG_EXP_NO_CONST_COLS   // (experiment only: the per-window constant columns not written)
     p.out_ws[o] = p.wstart;
     p.out_we[o] = p.wend;
     if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
+#endif
     const int64_t cv = (int64_t)(cs - cn);
     uint8_t nm = 0;
 #pragma unroll
