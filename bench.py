@@ -175,6 +175,84 @@ def watermarks_for(lo, hi, rate_s, every, delay=0, jitter=0):
     return out
 
 
+class TwoPhase:
+    """The N > 1 schedule of one rank (TwoStageOptimizedWindowAggregateRule.java:81-104): the
+    local operator (LocalSlicingWindowAggOperator + LocalAggCombiner) -> key-group exchange of its
+    partial rows -> the owner's global operator (GlobalAggCombiner). bench.py's timed loop and
+    tests/test_gpu_multiproc.py drive this same object, so the tested schedule is the timed one.
+
+    Per micro-batch (`round`): the local operator takes EVERY watermark of the batch
+    (LocalSlicingWindowAggOperator.processWatermark, :113-134 -- fg_advance_progress_async_n, its
+    flushed partial rows collected once), then one exchange ships the rows with the batch's last
+    watermark in-band (StatusWatermarkValve: the min over the ranks), the previous round's global
+    fires are collected, the partials merged (late rules per partial row at the global's
+    progress) and the global fire at the combined watermark queued asynchronously. Firing only at
+    the batch's last combined watermark fires the same windows in the same order as firing at
+    each: no partial row reaches the global operator between two watermarks of one batch (the
+    batch's records all precede its watermarks), and a window's trigger set is cumulative in the
+    watermark.
+
+    `checkpoint()` is prepareSnapshotPreBarrier on both: the local buffer is flushed and its
+    partial rows go through the exchange before the barrier (the reference forwards them
+    downstream ahead of it, LocalSlicingWindowAggOperator.java:142-144), then the global
+    operator's staged state is flushed and imaged (window-aggs)."""
+
+    def __init__(self, op_local, op_global, device, max_parallelism=128, key_hash=None, via_cpu=False,
+                 key_rows=None, host_rows=False):
+        from flink_amd import _lib as FL
+        self.local, self.glob = op_local, op_global
+        self.device, self.maxp = device, max_parallelism
+        self.key_hash = FL.KEYHASH_BINARYROW_BIGINT if key_hash is None else key_hash
+        self.via_cpu, self.key_rows, self.host_rows = via_cpu, key_rows, host_rows
+        self.held = False      # the global fire of the last round, not collected yet
+        self.wm = -(1 << 63)   # this rank's last watermark
+
+    def _collect(self):
+        """the held global fire's rows (numpy with host_rows, else the row count)"""
+        if not self.held:
+            return None if self.host_rows else 0
+        self.held = False
+        r = self.glob.collect_fired(host=self.host_rows)
+        return r if self.host_rows else r.n
+
+    def _ship(self, r, wm):
+        """exchange the local rows `r` (device FgRows) by key-group owner, collect the held global
+        fire, merge the received partials; returns (collected, bytes sent, combined watermark)"""
+        from flink_amd.exchange import device_columns, exchange_partials
+        cols = device_columns(r, aggs=tuple(range(int(r.num_aggs))), device=self.device)
+        recv, sent, gwm = exchange_partials(cols, max_parallelism=self.maxp, key_hash=self.key_hash,
+                                            via_cpu=self.via_cpu, key_rows=self.key_rows, watermark=wm)
+        got = self._collect()   # (rows of the previous fire go out before these partials merge)
+        self.glob.process_partials(*recv)
+        return got, sent, gwm
+
+    def round(self, wms):
+        """one micro-batch's watermarks (in order); returns (collected rows, bytes sent)"""
+        self.local.process_watermarks(wms)
+        r = self.local.collect_fired()
+        self.wm = int(wms[-1])
+        got, sent, gwm = self._ship(r, self.wm)
+        self.glob.process_watermark(gwm, device_output=True, wait=False)
+        self.held = True
+        return got, sent
+
+    def checkpoint(self):
+        """prepareSnapshotPreBarrier + snapshotState; returns (collected rows, bytes sent,
+        (global image, timer watermark))"""
+        r = self.local.flush_partials(device_output=True)
+        got, sent, _ = self._ship(r, self.wm)
+        self.glob.prepare_snapshot_pre_barrier()
+        return got, sent, self.glob.snapshot_state(copy=not self.host_rows)
+
+    def finish(self):
+        """end of input (Long.MAX_VALUE); returns (rows of both last fires, bytes sent)"""
+        a, sent = self.round([JMAX])
+        b = self._collect()
+        if self.host_rows:
+            return [x for x in (a, b) if x is not None and len(x)], sent
+        return a + b, sent
+
+
 def measure_copy_peak(dev, nbytes=2 << 30, reps=5):
     """Device-to-device copy bandwidth (read + write bytes / time) on this GPU."""
     try:
@@ -477,7 +555,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
 
     import flink_amd as F
-    from flink_amd.exchange import device_columns, exchange, exchange_partials, global_watermark
+    from flink_amd.exchange import exchange, global_watermark
 
     n = args.records
     key, ts, val = gen_columns(n, args.keys, args.rate, rank * n, dev, jitter=wl["jitter"], zipf=wl["zipf"])
@@ -531,37 +609,29 @@ def main():
     kdict_owner = F.KeyDictionary(max_parallelism=128, expected_keys=int(args.keys / world * 1.05) + 1,
                                   device=local) if strings and two_phase else None
 
-    def partials_round(wm, held):
-        """local fire -> exchange of partial accumulators (the watermarks min-combined in-band
-        with the counts) -> [the previous round's global fires collected] -> global merge ->
-        async global fire (held until the next round). Returns (rows collected, bytes sent)."""
-        r = op_local.process_watermark(wm, device_output=True)
-        # key, slice end, COUNT(*), COUNT(v), SUM (+ MIN, MAX for several value accumulators)
-        cols = device_columns(r, aggs=tuple(range(len(op_local.aggs))), device=dev)
-        recv, sent, gwm = exchange_partials(cols, max_parallelism=maxp, key_hash=key_hash, via_cpu=via_cpu,
-                                            key_rows=(kdict, kdict_owner) if kdict_owner else None, watermark=wm)
-        # the previous round's global fires ran behind this round's local batch, local fire and
-        # exchange; their rows go out before this round's partials are merged
-        rows = op.collect_fired().n if held else 0
-        # (process_partials orders the engine's stream after torch's: no host synchronization)
-        op.process_partials(*recv)
-        op.process_watermark(gwm, device_output=True, wait=False)
-        return rows, sent
+    tp = TwoPhase(op_local, op, dev, maxp, key_hash, via_cpu,
+                  key_rows=(kdict, kdict_owner) if kdict_owner else None) if two_phase else None
 
     ckpt = dict(n=0, s=0.0, state_rows=0)
 
     def checkpoint():
         """CheckpointedFunction path of the window operator: prepareSnapshotPreBarrier flushes
         the staged records into the GPU-resident state, snapshotState copies the window-aggs
-        image (key, slice_end, accumulators) to host memory for the keyed state backend."""
+        image (key, slice_end, accumulators) to host memory for the keyed state backend.
+        Two-phase: the local buffer's partial rows go through the exchange first (TwoPhase.checkpoint).
+        Returns (rows collected, bytes sent)."""
         torch.cuda.synchronize()
         c0 = time.perf_counter()
-        for o in (op_local, op) if op_local else (op,):
-            o.prepare_snapshot_pre_barrier()
-            img, _ = o.snapshot_state(copy=False)   # the pinned image a JNI shim hands to the backend
-            ckpt["state_rows"] += len(img["key"])
+        if tp is not None:
+            got, sent, (img, _) = tp.checkpoint()
+        else:
+            got, sent = 0, 0
+            op.prepare_snapshot_pre_barrier()
+            img, _ = op.snapshot_state(copy=False)   # the pinned image a JNI shim hands to the backend
+        ckpt["state_rows"] += len(img["key"])
         ckpt["n"] += 1
         ckpt["s"] += time.perf_counter() - c0
+        return got, sent
 
     def intern(lo):
         """BinaryRowDataKeySelector.getKey rows -> dictionary ids (on the GPU, the dictionary's
@@ -594,7 +664,12 @@ def main():
         k_next = intern(0) if strings else None
         for bi, lo in enumerate(range(0, n, args.batch)):
             if args.checkpoint_every and bi > 0 and bi % args.checkpoint_every == 0:
-                checkpoint()
+                if held and tp is None:   # the rows go out before the checkpoint barrier
+                    rows += op.collect_fired().n
+                    held = False
+                nr, sent = checkpoint()
+                rows += nr
+                xgmi += sent
             hi = min(n, lo + args.batch)
             if strings:
                 k = k_next
@@ -609,9 +684,8 @@ def main():
                 op_local.process_batch(k, t, v)
                 if strings and hi < n:
                     k_next = intern(hi)
-                if wms:   # the micro-batch's last watermark (in-order input: same output)
-                    nr, sent = partials_round(wms[-1], held)
-                    held = True
+                if wms:   # every watermark of the micro-batch to the local operator, one exchange
+                    nr, sent = tp.round(wms)
                     rows += nr
                     xgmi += sent
                 continue
@@ -646,8 +720,8 @@ def main():
                         k_next = intern_async(hi)
                     kdict.intern_wait()
         if two_phase:
-            nr, sent = partials_round(JMAX, held)
-            return rows + nr + op.collect_fired().n, xgmi + sent
+            nr, sent = tp.finish()
+            return rows + nr, xgmi + sent
         if held:
             rows += op.collect_fired().n
         r = op.process_watermark(JMAX, device_output=True)

@@ -305,6 +305,7 @@ struct fg_handle {
     // into their slice tables straight from the tiles (k_tile_fire with tables); 0: TUMBLE and
     // local fires only, anything else materialized (the round-4 first tile build)
     bool tile_state = true;
+    int tile_grid_force = 0;  // FG_TILE_GRID (test knob, tile_grid)
     bool tile_skew = false;   // a tile pass saw hot-key skew: later batches take the two-pass partition
                               // (a performance hint kept across fg_reset)
     DevBuf tile_dir, tile_hist;
@@ -797,10 +798,20 @@ int tile_job_params(fg_handle* h, int ji, TileFire* f) {
 // Split every slice table's regions 2^b -> 2^nb (k_split_table). Staged passes keep their
 // bucketing (the merge reads a region's records through its parent bucket); new passes
 // bucket at nb. The slice lanes stay until the lanes above lanes_for(nb) drain.
+int materialize_lane(fg_handle* h, int l);
 int grow(fg_handle* h, int nb) {
     const int sh = nb - h->region_bits;
     if (sh <= 0) return FG_OK;
     if (nb > kMaxRegionBits) return h->fail(FG_ECAPACITY, "internal: region bits above %d", kMaxRegionBits);
+    // a staged tile pass is read at most kTileMaxSub regions per bucket by the materialize
+    // kernels: a lane whose tile passes would pass that bound at nb is materialized first, at
+    // the current bits (its regular staged pass is then read through its parent buckets)
+    for (int l = 0; l < h->lanes; l++) {
+        bool deep = false;
+        for (const Staged* s : h->lane[l].passes) deep = deep || (s->tiles && nb - s->bits + kTileBits > 6);
+        if (!deep) continue;
+        if (int rc = materialize_lane(h, l)) return rc;
+    }
     const int64_t P2 = (int64_t)1 << nb;
     std::vector<std::unique_ptr<DevBuf>> old;   // freed once the split kernels are done
     auto split = [&](SliceTable* t) -> int {
@@ -1356,8 +1367,11 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             // the lane's tile passes straight into the slice state (and the fired window's rows):
             // the resident tables the merge would read inserted first, the destination's regions
             // written back by the same workgroups -- no materialized pass, no staged pass 2
+            // (an item's (source, region) ranges fit the kernel's kTileMaxRegions prefix slots)
+            const int tsub = kTileBits + h->region_bits - ln.passes[0]->bits;
             bool ok = tile_fire_ok(h, ln) && h->keys32 && ub_cnt_fits(h) && job.srcs.size() <= 8 &&
-                      kTileBits + h->region_bits - ln.passes[0]->bits <= kTileMaxRegionBits &&
+                      tsub <= kTileMaxRegionBits &&
+                      ((int64_t)job.srcs.size() << tsub) <= (int64_t)kTileMaxRegions &&
                       !(job.emit && h->retain && !h->local);
             for (SliceTable* x : job.srcs) ok = ok && !x->has_null;
             if (ok) {
@@ -2125,6 +2139,18 @@ int ensure_scratch(fg_handle* h) {
 // the host; ingest_finish takes the host's decisions once the counters are there (flushes,
 // the regular pass 2 when the plan said no, the lanes' bookkeeping).
 
+// Pass 1's grid for a tile pass of n records: one workgroup per 6,144-record tile, at most one
+// per CU. FG_TILE_GRID (test knob, read at fg_open) forces a grid: N > 0 exactly N workgroups (more than the
+// tiles leaves empty segments), -1 the two-pass partition's rule (one per 16,384 records).
+int tile_grid(const fg_handle* h, int64_t n) {
+    const int force = h->tile_grid_force;
+    int64_t g;
+    if (force > 0) g = force;
+    else if (force < 0) g = std::min<int64_t>(h->grid, (n + 16383) / 16384);
+    else g = std::min<int64_t>(h->grid, (n + kTileRecs - 1) / kTileRecs);
+    return (int)std::max<int64_t>(1, g);
+}
+
 int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
                   const uint8_t* vnull, int64_t flo, int64_t fhi, bool count_drops, PassState& ps) {
     if (int rc0 = ensure_scratch(h)) return rc0;
@@ -2164,6 +2190,11 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         // the pass's own Staged (its tiles live until the fire): a pooled one no unsettled job reads
         ps.s = pass_from_pool(h);
         Staged* st = ps.s.get();
+        // pass 1's grid for tiles: one workgroup per tile up to one per CU (a small batch's pass
+        // is then one tile's latency); the segment split (seg_per, max_tiles, tiles) is carried
+        // with the pass -- every consumer (k_tile_dirt, the fire's walk, materialize) reads it
+        // from there, never from a grid of its own
+        p.grid = tile_grid(h, n);
         int64_t per = (n + p.grid - 1) / p.grid;
         per = (per + 1) & ~int64_t(1);   // (seg_bounds)
         p.max_tiles = (int32_t)((per + kTileRecs - 1) / kTileRecs);
@@ -3325,6 +3356,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     hp->narrow_ok = hp->narrow;
     if (const char* e = getenv("FG_TILE")) hp->tile_env = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_STATE")) hp->tile_state = std::atoi(e) != 0;
+    if (const char* e = getenv("FG_TILE_GRID")) hp->tile_grid_force = std::atoi(e);
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";

@@ -1540,11 +1540,9 @@ __device__ __forceinline__ int lds_bucket_slot(LdsTableT<C, MV>& t, int64_t k, u
 __device__ __forceinline__ void write_row_k(const MergeParams& p, unsigned long long o, int64_t key,
                                             unsigned long long cs, unsigned long long cn, const int64_t* vals, int vt) {
     p.out_key[o] = key;
-#ifndef FG_EXP_NO_CONST_COLS   // (experiment only: the per-window constant columns not written)
     p.out_ws[o] = p.wstart;
     p.out_we[o] = p.wend;
     if (p.out_rowtime) p.out_rowtime[o] = p.out_ts;
-#endif
     const int64_t cv = (int64_t)(cs - cn);
     uint8_t nm = 0;
 #pragma unroll
@@ -3613,8 +3611,15 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
 
 hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s) {
     if (f.n_passes < 1 || f.tbits < kTileBits || f.m.region_bits < f.tbits || f.m.mv) return hipErrorInvalidValue;
-    if ((f.m.has_dst || f.m.n_src > 0) && (kTileBits + f.m.region_bits - f.tbits > kTileMaxRegionBits || f.m.src_null_mask))
-        return hipErrorInvalidValue;   // (s_rc holds an item's regions; sources without NULL counts)
+    if (f.m.has_dst || f.m.n_src > 0) {
+        // s_rc holds an item's regions and s_rb its (source, region) ranges: an item is one
+        // region on a retry, else the 2^(kTileBits + sub) regions of its bucket
+        if (f.m.src_null_mask) return hipErrorInvalidValue;   // (sources without NULL counts)
+        const int sub = kTileBits + f.m.region_bits - f.tbits;
+        if (!f.m.retry_list && sub > kTileMaxRegionBits) return hipErrorInvalidValue;
+        const int64_t nreg = f.m.retry_list ? 1 : (int64_t)1 << sub;
+        if ((int64_t)f.m.n_src * nreg > kTileMaxRegions) return hipErrorInvalidValue;
+    }
     const dim3 g((unsigned)workgroups), b(kTileFireThreads);
     const bool tab = f.m.has_dst || f.m.n_src > 0;
     // the value op compiled in: SUM / AVG over DOUBLE, BIGINT, or COUNT only

@@ -440,10 +440,15 @@ class WindowAggOperator:
         L.check(self._lib.fg_flush(self._h), self._h)
         self._hold(None)
 
-    def flush_partials(self):
+    def flush_partials(self, device_output: bool = False):
         """Local phase: every buffered slice emits its partial accumulator rows now
         (LocalSlicingWindowAggOperator.prepareSnapshotPreBarrier -> WindowBuffer.flush ->
-        LocalAggCombiner, fg_flush_partials); host rows as process_watermark returns them."""
+        LocalAggCombiner, fg_flush_partials); host rows as process_watermark returns them, or
+        with device_output=True the operator's FgRows (device pointers, valid until the next call)."""
+        if device_output:
+            L.check(self._lib.fg_flush_partials(self._h, L.DEVICE, self._dev_rows_ref), self._h)
+            self._hold(None)
+            return self._dev_rows
         r = L.FgRows()
         L.check(self._lib.fg_flush_partials(self._h, L.HOST, C.byref(r)), self._h)
         self._hold(None)

@@ -325,10 +325,11 @@ __global__ __launch_bounds__(TC) void k_tm(int64_t n, const char* tmp, const uin
                 vr[u] = 0;
                 if (jr < nrec) {
                     const uint32_t src = s_dl[wave][s_fm[wave][jr]] + b + jr;
-                    if (mode & 2) {   // (diagnostic: no gather; <= 4,096 keys per consumer)
-                        kr[u] = (int32_t)(c * 4096 + (src & 4095));
-                        vr[u] = 1.0;
-                    } else {
+                    // (round 4 had a "mode 2" no-gather diagnostic here that synthesised
+                    // c * 4096 + (src & 4095) keys: more distinct keys than the consumer's
+                    // table holds, so its probe ran past the table -- the illegal access in
+                    // gpurun_out/proto3.log. Removed in round 5.)
+                    {
 #if PACKED
                         const uint3 w = *reinterpret_cast<const uint3*>(tmp + 12 * (uint64_t)src);
                         kr[u] = (int32_t)w.x;

@@ -201,6 +201,18 @@ def test_config0_datastream_tumble_10M_records():
     assert nrows == 10 * 10_000
 
 
+@pytest.mark.parametrize("grid", ["-1", "3", "400"])
+def test_config0_datastream_forced_tile_grid(monkeypatch, grid):
+    """configs[0] with pass 1's grid of tile passes forced (FG_TILE_GRID, read at fg_open): the
+    round-4 rule (one workgroup per 16,384 records), several tiles per workgroup, and more
+    workgroups than a 1M-record batch's 163 tiles (empty segments). The default is one
+    workgroup per tile; every consumer reads the segment split from the pass."""
+    from oracle import oracle as O
+    monkeypatch.setenv("FG_TILE_GRID", grid)
+    nrows, _ = run_config("datastream", 4_000_000, ("sum",), O.TUMBLE, 1000, 0)
+    assert nrows == 4 * 10_000
+
+
 @pytest.mark.parametrize("wm", ["sync", "async"])
 def test_config1_tumble_10M_keys(wm):
     """configs[1]: SQL TUMBLE 1s COUNT(*)/COUNT/SUM/AVG(double), 10M uniform keys, 200M records =
