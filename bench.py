@@ -198,8 +198,13 @@ class TwoPhase:
     operator's staged state is flushed and imaged (window-aggs)."""
 
     def __init__(self, op_local, op_global, device, max_parallelism=128, key_hash=None, via_cpu=False,
-                 key_rows=None, host_rows=False):
+                 key_rows=None, host_rows=False, comm=None):
+        """comm: a flink_amd.comm.Communicator -- the exchange through the C-ABI's RCCL edge
+        (fg_comm_exchange_fired / _flushed) instead of torch.distributed (exchange_partials)."""
         from flink_amd import _lib as FL
+        if comm is not None and (key_rows is not None or via_cpu):
+            raise ValueError("the C-ABI exchange moves BIGINT keys over RCCL (no key rows, no gloo)")
+        self.comm = comm
         self.local, self.glob = op_local, op_global
         self.device, self.maxp = device, max_parallelism
         self.key_hash = FL.KEYHASH_BINARYROW_BIGINT if key_hash is None else key_hash
@@ -226,12 +231,23 @@ class TwoPhase:
         self.glob.process_partials(*recv)
         return got, sent, gwm
 
+    def _ship_capi(self, flushed):
+        """the same through the C-ABI (fg_comm_exchange_fired / _flushed: collect or flush the
+        local rows, exchange, fg_add_partials of the global operator)"""
+        got = self._collect()
+        b0 = self.comm.bytes_sent
+        f = self.comm.exchange_flushed if flushed else self.comm.exchange_fired
+        gwm = f(self.local, self.glob, self.wm, key_hash=self.key_hash, max_parallelism=self.maxp)
+        return got, self.comm.bytes_sent - b0, gwm
+
     def round(self, wms):
         """one micro-batch's watermarks (in order); returns (collected rows, bytes sent)"""
         self.local.process_watermarks(wms)
-        r = self.local.collect_fired()
         self.wm = int(wms[-1])
-        got, sent, gwm = self._ship(r, self.wm)
+        if self.comm is not None:
+            got, sent, gwm = self._ship_capi(False)
+        else:
+            got, sent, gwm = self._ship(self.local.collect_fired(), self.wm)
         self.glob.process_watermark(gwm, device_output=True, wait=False)
         self.held = True
         return got, sent
@@ -239,8 +255,10 @@ class TwoPhase:
     def checkpoint(self):
         """prepareSnapshotPreBarrier + snapshotState; returns (collected rows, bytes sent,
         (global image, timer watermark))"""
-        r = self.local.flush_partials(device_output=True)
-        got, sent, _ = self._ship(r, self.wm)
+        if self.comm is not None:
+            got, sent, _ = self._ship_capi(True)
+        else:
+            got, sent, _ = self._ship(self.local.flush_partials(device_output=True), self.wm)
         self.glob.prepare_snapshot_pre_barrier()
         return got, sent, self.glob.snapshot_state(copy=not self.host_rows)
 

@@ -75,6 +75,14 @@ class FgPartials(C.Structure):
     ]
 
 
+class FgExchanged(C.Structure):
+    _fields_ = [("n", C.c_int64), ("ncols", C.c_int32), ("reserved0", C.c_int32), ("cols", C.c_void_p * 8),
+                ("min_watermark", C.c_int64), ("bytes_sent", C.c_int64)]
+
+
+COMM_ID_BYTES = 128
+
+
 class FgStats(C.Structure):
     _fields_ = [(n, C.c_int64) for n in (
         "records_in", "records_staged", "late_dropped", "rows_fired", "flushes", "live_slices",
@@ -106,6 +114,8 @@ EXPORTS = (
     "fg_key_dict_copy_arena", "fg_key_dict_size", "fg_key_dict_stream", "fg_key_dict_set_timing",
     "fg_key_dict_kernel_stats", "fg_key_dict_last_error", "fg_key_dict_close",
     "fg_binaryrow_hash", "fg_host_register", "fg_host_unregister",
+    "fg_comm_unique_id", "fg_comm_open", "fg_comm_exchange_columns", "fg_comm_exchange_partials",
+    "fg_comm_exchange_fired", "fg_comm_exchange_flushed", "fg_comm_stream", "fg_comm_bytes_sent", "fg_comm_last_error", "fg_comm_close",
 )
 
 _lib = None
@@ -193,6 +203,25 @@ def load():
     L.fg_host_register.argtypes = [C.c_int32, P, C.c_int64]
     L.fg_host_unregister.argtypes = [C.c_int32, P]
     L.fg_host_register.restype = L.fg_host_unregister.restype = C.c_int
+    L.fg_comm_unique_id.argtypes = [P]
+    L.fg_comm_open.argtypes = [C.c_int32, C.c_int32, C.c_int32, P, C.POINTER(P)]
+    L.fg_comm_exchange_columns.argtypes = [P, P, C.c_int64, C.c_int32, P, C.c_int32, C.c_int32, C.c_int64,
+                                           C.POINTER(FgExchanged)]
+    L.fg_comm_exchange_partials.argtypes = [P, P, C.POINTER(FgRows), C.c_int32, C.c_int32, C.c_int64, P,
+                                            C.POINTER(C.c_int64)]
+    L.fg_comm_exchange_fired.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int64, P, C.POINTER(C.c_int64)]
+    L.fg_comm_exchange_flushed.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int64, P, C.POINTER(C.c_int64)]
+    L.fg_comm_bytes_sent.argtypes = [P]
+    L.fg_comm_bytes_sent.restype = C.c_int64
+    L.fg_comm_stream.argtypes = [P]
+    L.fg_comm_stream.restype = P
+    L.fg_comm_last_error.argtypes = [P]
+    L.fg_comm_last_error.restype = C.c_char_p
+    L.fg_comm_close.argtypes = [P]
+    L.fg_comm_close.restype = None
+    for fn in ("fg_comm_unique_id", "fg_comm_open", "fg_comm_exchange_columns", "fg_comm_exchange_partials",
+               "fg_comm_exchange_fired", "fg_comm_exchange_flushed"):
+        getattr(L, fn).restype = C.c_int
     for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async", "fg_key_dict_intern_wait",
                "fg_key_dict_lookup", "fg_key_dict_arena",
                "fg_key_dict_copy_arena"):

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 13
+#define FG_ABI_VERSION 14
 
 enum fg_status {
     FG_OK = 0,
@@ -366,6 +366,57 @@ int  fg_partition_by_owner(int32_t device_id, void* stream, int64_t n, const int
 int  fg_partition_columns_by_owner(int32_t device_id, void* stream, int64_t n, int32_t ncols,
                                    const int64_t* const* cols, int32_t key_hash, int32_t max_parallelism,
                                    int32_t parallelism, int64_t* const* out_cols, int64_t* counts);
+
+/* The keyBy edge of the two-phase plan over RCCL (ABI 14; libflinkgpu.so links librccl): replaces,
+ * between co-located subtasks, KeyGroupStreamPartitioner.selectChannel
+ * (SJ/runtime/partitioner/KeyGroupStreamPartitioner.java:55-65) + RecordWriter.emit
+ * (RT/io/network/api/writer/RecordWriter.java:101-128) on the edge LocalSlicingWindowAggOperator ->
+ * GlobalSlicingWindowAggOperator, and StatusWatermarkValve's min over the input channels
+ * (SJ/runtime/watermarkstatus/StatusWatermarkValve.java). One communicator per subtask (one process
+ * per GPU): a coordinator (the JobManager) makes the id once with fg_comm_unique_id and ships its
+ * bytes with the deployment; every subtask calls fg_comm_open(device, parallelism, its index, id),
+ * which blocks until all have joined. Owner of a row = computeOperatorIndexForKeyGroup(key group)
+ * (KeyGroupRangeAssignment.java:124-127) with fg_key_hash routing. Per exchange: the rows grouped by
+ * owner on the device, ONE all-to-all of (row count, this rank's watermark) per peer, ONE host read
+ * of them, grouped send / receive of each column's runs. Collective: every rank calls the same
+ * exchanges in the same order (a rank with no rows still calls). Not for per-rank dictionary ids
+ * (FG_KEYHASH_DICT_ID of different dictionaries): those ship key rows. */
+#define FG_COMM_ID_BYTES 128
+typedef struct fg_comm fg_comm;
+typedef struct fg_exchanged {
+    int64_t n;                        /* rows received (this rank's key groups) */
+    int32_t ncols;
+    int32_t reserved0;
+    const int64_t* cols[8];           /* device columns, communicator-owned, valid until the next exchange;
+                                       * complete in stream order on fg_comm_stream */
+    int64_t min_watermark;            /* min over the ranks of the watermarks passed in (StatusWatermarkValve) */
+    int64_t bytes_sent;               /* to other ranks */
+} fg_exchanged;
+int  fg_comm_unique_id(uint8_t* id /* FG_COMM_ID_BYTES */);
+int  fg_comm_open(int32_t device_id, int32_t world, int32_t rank, const uint8_t* id, fg_comm** out);
+/* ncols <= 8 int64 device columns (cols[0] = key) produced on `stream` (hipStream_t; the
+ * communicator's stream waits for it), grouped by owner and exchanged. */
+int  fg_comm_exchange_columns(fg_comm* c, void* stream, int64_t n, int32_t ncols, const int64_t* const* cols,
+                              int32_t key_hash, int32_t max_parallelism, int64_t watermark, fg_exchanged* out);
+/* The local operator's partial rows (FG_DEVICE rows of a FG_FLAG_LOCAL_PARTIALS handle: key,
+ * window_end = slice end, agg[0..2] or [0..4]) exchanged and merged into this rank's global operator
+ * (fg_add_partials on `global`, ordered after the collective on its stream). *min_watermark receives
+ * the combined watermark the caller then advances `global` to. */
+int  fg_comm_exchange_partials(fg_comm* c, fg_handle* local, const fg_rows* rows, int32_t key_hash,
+                               int32_t max_parallelism, int64_t watermark, fg_handle* global, int64_t* min_watermark);
+/* fg_comm_exchange_partials of the rows fg_collect_fired(local) returns (the local fires of the
+ * async advances since the last collect) -- a shim's per-batch call: LocalSlicingWindowAggOperator
+ * .processWatermark's output edge. */
+int  fg_comm_exchange_fired(fg_comm* c, fg_handle* local, int32_t key_hash, int32_t max_parallelism,
+                            int64_t watermark, fg_handle* global, int64_t* min_watermark);
+/* ... of fg_flush_partials(local) (LocalSlicingWindowAggOperator.prepareSnapshotPreBarrier :142-144:
+ * the local buffer crosses the edge before the barrier). */
+int  fg_comm_exchange_flushed(fg_comm* c, fg_handle* local, int32_t key_hash, int32_t max_parallelism,
+                              int64_t watermark, fg_handle* global, int64_t* min_watermark);
+void* fg_comm_stream(fg_comm* c);
+int64_t fg_comm_bytes_sent(fg_comm* c);      /* bytes sent to other ranks by every exchange so far */
+const char* fg_comm_last_error(fg_comm* c);   /* c may be NULL: last error of fg_comm_open / _unique_id */
+void fg_comm_close(fg_comm* c);
 
 /* Grouping keys of any type (STRING, several key columns ...): a GPU-resident dictionary of the
  * serialized key rows. The reference groups by the BinaryRowData key row the key selector

@@ -123,3 +123,107 @@ def test_rccl_world1_exchange_between_hip_operators(oracle_mod):
     ok = e["sum_null"] == 0
     a, bb = g["sum"][ok], e["sum_d"][ok]
     assert (np.abs(a - bb) <= 1e-9 * np.maximum(np.abs(a), np.abs(bb))).all()
+
+
+def _capi_child(q):
+    """world size 1 through the C-ABI: fg_comm_unique_id -> fg_comm_open -> bench.TwoPhase with
+    the communicator (fg_comm_exchange_fired / _flushed into the global operator)"""
+    try:
+        import torch
+
+        import bench as B
+        import flink_amd as F
+        from flink_amd.comm import Communicator, unique_id
+        from tests.streams import make_stream
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        comm = Communicator(0, 1, 0, unique_id())
+        # the column exchange alone: at world size 1 every row comes back unchanged, watermark as given
+        cols = [torch.arange(1000, dtype=torch.int64, device=dev) * 7 + j for j in range(5)]
+        got, wm = comm.exchange_columns(cols, watermark=123)
+        assert wm == 123 and all(torch.equal(a, b) for a, b in zip(got, cols)) and comm.bytes_sent == 0
+        empty, wm = comm.exchange_columns([c[:0] for c in cols], watermark=5)
+        assert wm == 5 and all(e.numel() == 0 for e in empty)
+        key, ts, val, _ = make_stream(N, KEYS, "f64", seed=78, jitter_ms=1200)
+        aggs = ("count_star", "count", "sum", "avg")
+        w = F.tumbling(1000)
+        local = F.WindowAggOperator(w, aggs=aggs, expected_keys=KEYS, local_partials=True)
+        glob = F.WindowAggOperator(w, aggs=aggs, expected_keys=KEYS)
+        tp = B.TwoPhase(local, glob, dev, comm=comm, host_rows=True)
+        out, mx = [], -(1 << 63)
+        for bi, lo in enumerate(range(0, N, BATCH)):
+            hi = lo + BATCH
+            local.process_batch(torch.from_numpy(key[lo:hi]).to(dev), torch.from_numpy(ts[lo:hi]).to(dev),
+                                torch.from_numpy(val[lo:hi]).to(dev))
+            m0 = mx
+            mx = max(mx, int(ts[lo:hi].max()))
+            got, _ = tp.round([m0 - 101 if m0 > -(1 << 62) else mx - 900, mx - 501, mx - 101])
+            out.append(got)
+            if bi == 1:
+                got, _, (img, twm) = tp.checkpoint()
+                out.append(got)
+                assert len(img["key"]) > 0
+        rest, _ = tp.finish()
+        out += rest
+        rows = np.concatenate([x for x in out if x is not None and len(x)])
+        late = tp.glob.num_late_records_dropped
+        local.close()
+        glob.close()
+        comm.close()
+        q.put((rows.tobytes(), rows.dtype.descr, late, None))
+    except Exception as e:
+        import traceback
+        q.put((None, None, 0, traceback.format_exc() + repr(e)))
+
+
+def test_capi_comm_world1_two_phase(oracle_mod):
+    """fg_comm_* (the C-ABI's RCCL edge) at world size 1: bench.TwoPhase through the
+    communicator -- three watermarks per batch to the local operator, a checkpoint whose local
+    flush crosses the edge -- against the two-phase oracle on the same schedule."""
+    import torch.multiprocessing as mp
+
+    from tests.streams import make_stream
+    O = oracle_mod
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_capi_child, args=(q,))
+    p.start()
+    b, descr, late, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    assert p.exitcode == 0
+    got = np.frombuffer(b, dtype=np.dtype([tuple(x) for x in descr]))
+    key, ts, val, _ = make_stream(N, KEYS, "f64", seed=78, jitter_ms=1200)
+    loc = O.OracleOperator(kind=O.TUMBLE, size=1000, val_type=O.VAL_F64, phase=O.PHASE_LOCAL)
+    glo = O.OracleOperator(kind=O.TUMBLE, size=1000, val_type=O.VAL_F64, phase=O.PHASE_GLOBAL)
+    exp, mx = [], -(1 << 63)
+    for bi, lo in enumerate(range(0, N, BATCH)):
+        loc.process_batch(key[lo:lo + BATCH], ts[lo:lo + BATCH], val[lo:lo + BATCH])
+        m0 = mx
+        mx = max(mx, int(ts[lo:lo + BATCH].max()))
+        for wm in (m0 - 101 if m0 > -(1 << 62) else mx - 900, mx - 501, mx - 101):
+            loc.process_watermark(wm)
+            glo.process_partials(loc.take_rows())
+            glo.process_watermark(wm)
+            exp.append(glo.take_rows())
+        if bi == 1:
+            loc.prepare_snapshot()
+            glo.process_partials(loc.take_rows())
+            glo.prepare_snapshot()
+            exp.append(glo.take_rows())
+    loc.process_watermark((1 << 63) - 1)
+    glo.process_partials(loc.take_rows())
+    glo.process_watermark((1 << 63) - 1)
+    exp.append(glo.take_rows())
+    e = np.concatenate(exp)
+    assert late == glo.late_dropped and late > 0
+    loc.close()
+    glo.close()
+    g = got[np.lexsort((got["key"], got["window_end"]))]
+    e = e[np.lexsort((e["key"], e["window_end"]))]
+    assert len(g) == len(e), (len(g), len(e))
+    for f, fe in (("key", "key"), ("window_end", "window_end"), ("count_star", "cnt_star"), ("count", "cnt_val")):
+        assert np.array_equal(g[f], e[fe]), f
+    ok = e["sum_null"] == 0
+    a, bb = g["sum"][ok], e["sum_d"][ok]
+    assert (np.abs(a - bb) <= 1e-9 * np.maximum(np.abs(a), np.abs(bb))).all()
