@@ -3,17 +3,21 @@
  * (SlicingWindowOperator.java:96-242, a final class) around GpuSlicingWindowProcessor, with one
  * difference in how a watermark moves on -- it is HELD while the engine fires its windows:
  *
- *   processWatermark(mark)  fg_advance_progress_async(mark): the fires are queued behind the
- *                           pending micro-batch and the call returns; the watermark is held
- *                           (a later one replaces it: watermarks only grow)
+ *   processWatermark(mark)  the previously held watermark is released first (see below); then
+ *                           fg_advance_progress_async(mark): the pending records are handed over,
+ *                           the fires queued behind them and the call returns; the watermark is
+ *                           held
  *   the held watermark is released -- fg_collect_fired, its rows emitted, then the watermark
- *   forwarded (timers advanced, downstream notified) -- as soon as the next micro-batch has been
- *   handed to the engine (its partition passes overlap the fires), at a checkpoint barrier
- *   (prepareSnapshotPreBarrier), at a processing-time timer, at end of input and at close.
+ *   forwarded (timers advanced, downstream notified) -- at the first of: the next micro-batch
+ *   handed to the engine (its partition passes overlap the fires), the NEXT watermark, a
+ *   processing-time callback spec.maxWatermarkHoldMs after the hold began, a checkpoint barrier
+ *   (prepareSnapshotPreBarrier), a processing-time timer, end of input and close.
  *
  * No row is emitted after a watermark that passes its window (rows always precede the watermark
- * that fired them), so downstream operators see the reference's output; watermarks may reach
- * them up to one micro-batch later. spec.asyncWatermarks = false forwards every watermark at
+ * that fired them), so downstream operators see the reference's output; a watermark reaches
+ * them at most one watermark interval (or maxWatermarkHoldMs of processing time) later -- also on
+ * a slow or idle stream, where a micro-batch fills rarely (the reference forwards at once,
+ * SlicingWindowOperator.java:207-210). spec.asyncWatermarks = false forwards every watermark at
  * once, as SlicingWindowOperator does. Metrics: numLateRecordsDropped (fed by the engine's
  * count), lateRecordsDroppedRate, watermarkLatency, as SlicingWindowOperator.java:158-174.
  */
@@ -49,12 +53,21 @@ public final class GpuSlicingWindowAggOperator extends TableStreamOperator<RowDa
     private transient InternalTimerService<Long> timers;
     private transient Counter numLateRecordsDropped;
     private transient long lastTriggeredProcessingTime;
+    private final long maxHoldMs;
+
     private transient Watermark held;
+    private transient long holdSeq;   // which hold a processing-time release callback belongs to
     private transient boolean closed;
 
     public GpuSlicingWindowAggOperator(GpuSlicingWindowProcessor processor, boolean asyncWatermarks) {
+        this(processor, asyncWatermarks, GpuWindowAggSpec.DEFAULT_MAX_WATERMARK_HOLD_MS);
+    }
+
+    public GpuSlicingWindowAggOperator(
+            GpuSlicingWindowProcessor processor, boolean asyncWatermarks, long maxWatermarkHoldMs) {
         this.processor = processor;
         this.async = asyncWatermarks;
+        this.maxHoldMs = maxWatermarkHoldMs;
         setChainingStrategy(ChainingStrategy.ALWAYS);
     }
 
@@ -63,6 +76,7 @@ public final class GpuSlicingWindowAggOperator extends TableStreamOperator<RowDa
         super.open();
         closed = false;
         held = null;
+        holdSeq = 0;
         lastTriggeredProcessingTime = Long.MIN_VALUE;
         collector = new TimestampedCollector<>(output);
         collector.eraseTimestamp();
@@ -135,9 +149,25 @@ public final class GpuSlicingWindowAggOperator extends TableStreamOperator<RowDa
             super.processWatermark(mark);
             return;
         }
+        if (held != null) {
+            release();   // a watermark waits at most one watermark interval
+        }
         processor.advanceAsync(mark.getTimestamp());
         processor.takeBatchHanded();   // (the pending records went with this advance)
         held = mark;
+        final long seq = ++holdSeq;
+        if (maxHoldMs >= 0) {
+            // and at most maxHoldMs of processing time on an idle stream (the callback runs in the
+            // task's mailbox thread, like every operator call)
+            getProcessingTimeService()
+                    .registerTimer(
+                            getProcessingTimeService().getCurrentProcessingTime() + maxHoldMs,
+                            t -> {
+                                if (held != null && holdSeq == seq) {
+                                    release();
+                                }
+                            });
+        }
     }
 
     /** the held watermark's rows, then the watermark itself */

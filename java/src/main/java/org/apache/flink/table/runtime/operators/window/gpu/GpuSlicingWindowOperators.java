@@ -24,7 +24,7 @@ public final class GpuSlicingWindowOperators {
 
     public static GpuSlicingWindowAggOperator create(GpuWindowAggSpec spec, ZoneId shiftTimeZone) {
         return new GpuSlicingWindowAggOperator(
-                new GpuSlicingWindowProcessor(spec, shiftTimeZone), spec.asyncWatermarks);
+                new GpuSlicingWindowProcessor(spec, shiftTimeZone), spec.asyncWatermarks, spec.maxWatermarkHoldMs);
     }
 
     public static WindowBuffer.Factory recordsBuffer(GpuWindowAggSpec spec) {

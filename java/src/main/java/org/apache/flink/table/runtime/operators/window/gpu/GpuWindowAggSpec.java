@@ -56,6 +56,12 @@ public final class GpuWindowAggSpec implements Serializable {
      */
     public boolean asyncWatermarks = true;
 
+    /** a held watermark is released at the latest this long (processing time) after its hold began */
+    public static final long DEFAULT_MAX_WATERMARK_HOLD_MS = 200L;
+
+    /** bound on a watermark's hold in processing time (< 0: none; the next watermark still releases it) */
+    public long maxWatermarkHoldMs = DEFAULT_MAX_WATERMARK_HOLD_MS;
+
     /** a field-by-field copy (the arrays cloned) */
     public GpuWindowAggSpec copy() {
         GpuWindowAggSpec c = new GpuWindowAggSpec();
@@ -82,6 +88,7 @@ public final class GpuWindowAggSpec implements Serializable {
         c.batchRecords = batchRecords;
         c.partialInput = partialInput;
         c.asyncWatermarks = asyncWatermarks;
+        c.maxWatermarkHoldMs = maxWatermarkHoldMs;
         return c;
     }
 }
