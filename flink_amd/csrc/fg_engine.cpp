@@ -120,7 +120,7 @@ struct Staged {
     // until a TUMBLE / local-phase fire reads them (k_tile_fire) or they are materialized
     bool tiles = false;
     DevBuf t_rec, t_dt;   // block-laid 12-B records at their batch index; per-bucket (offset, length) columns
-    int64_t t_seg_per = 0;
+    int64_t t_n = 0;
     int t_nt = 0, t_mt = 0, t_nc = 0;
     bool busy = false;    // read by a merge job not yet settled: not reused from the pool
     // a materialized tile pass: its own narrow record area (block-laid from index 0)
@@ -749,7 +749,7 @@ TilePass tile_pass_of(const Staged* s, int lane) {
     TilePass tp{};
     tp.rec = s->t_rec.p;
     tp.dt = s->t_dt.as<uint32_t>();
-    tp.seg_per = s->t_seg_per;
+    tp.n = s->t_n;
     tp.nt = s->t_nt;
     tp.mt = s->t_mt;
     tp.nc = s->t_nc;
@@ -2191,13 +2191,16 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         ps.s = pass_from_pool(h);
         Staged* st = ps.s.get();
         // pass 1's grid for tiles: one workgroup per tile up to one per CU (a small batch's pass
-        // is then one tile's latency); the segment split (seg_per, max_tiles, tiles) is carried
-        // with the pass -- every consumer (k_tile_dirt, the fire's walk, materialize) reads it
-        // from there, never from a grid of its own
+        // is then one tile's latency); the segment split (max_tiles, tiles) is carried with the
+        // pass -- every consumer (k_tile_dirt, the fire's walk, materialize) reads it from there,
+        // never from a grid of its own
         p.grid = tile_grid(h, n);
-        int64_t per = (n + p.grid - 1) / p.grid;
-        per = (per + 1) & ~int64_t(1);   // (seg_bounds)
-        p.max_tiles = (int32_t)((per + kTileRecs - 1) / kTileRecs);
+        // whole-tile segments: max_tiles tiles per workgroup, the grid trimmed to the workgroups
+        // that get records; tile t of the pass then starts at record t * kTileRecs
+        const int64_t per = (n + p.grid - 1) / p.grid;
+        p.max_tiles = (int32_t)std::max<int64_t>(1, (per + kTileRecs - 1) / kTileRecs);
+        const int64_t seg = (int64_t)p.max_tiles * kTileRecs;
+        p.grid = (int)std::max<int64_t>(1, (n + seg - 1) / seg);
         p.n_coarse = h->F >> kTileBits;
         const int64_t NT = (int64_t)p.grid * p.max_tiles;
         HIPCHK(h, st->t_rec.ensure((size_t)(n / 64 + 2) * kRec12Block));
@@ -2205,7 +2208,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         HIPCHK(h, h->tile_dir.ensure(2 * (size_t)NT * kTileDirStride(p.n_coarse)));
         p.tmp = st->t_rec.as<longlong2>();
         p.dir = h->tile_dir.as<uint16_t>();
-        st->t_seg_per = per;
+        st->t_n = n;
         st->t_mt = p.max_tiles;
         st->t_nt = (int)NT;
         st->t_nc = p.n_coarse;

@@ -443,8 +443,9 @@ constexpr int kTileMaxRegions = 1 << kTileMaxRegionBits;
 struct TilePass {
     const void* rec;          // block-laid 12-B records at their absolute batch index
     const uint32_t* dt;       // [nc][nt]: offset | length << 16 of bucket c's fragment of tile t
-    int64_t seg_per;          // records per pass-1 segment (seg_bounds); tile t = (t / mt, t % mt)
-    int32_t nt, mt;           // tiles, tiles per segment
+    int64_t n;                // records of the pass (tile t holds records [t * kTileRecs, ...): pass 1's
+                              // segments are whole tiles, so a tile's first record needs no division)
+    int32_t nt, mt;           // tiles, tiles per pass-1 segment
     int32_t nc;               // buckets of the pass (all lanes)
     int32_t bits;             // region bits of the pass
     int32_t lane;

@@ -2865,8 +2865,11 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; s_bmax = 0; }
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
-    int64_t beg, end;
-    seg_bounds(p.n, p.grid, blockIdx.x, &beg, &end);
+    // whole-tile segments (the host trims the grid): tile j of this workgroup is tile
+    // blockIdx.x * max_tiles + j of the pass and starts at record (that tile) * TILE
+    const int64_t seg = (int64_t)p.max_tiles * TILE;
+    const int64_t beg = (int64_t)blockIdx.x * seg < p.n ? (int64_t)blockIdx.x * seg : p.n;
+    const int64_t end = beg + seg < p.n ? beg + seg : p.n;
     const bool has_val = p.val != nullptr;
     uint32_t drops = 0, mask = 0, bmax = 0;
     uint32_t lc[kMaxLanes] = {0u, 0u, 0u, 0u};
@@ -3066,7 +3069,8 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
 
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
     if (p.n_coarse < 2 || p.n_coarse % 2 != 0 || p.n_coarse > kMaxTileBuckets || p.region_bits < kTileBits || !p.tmp ||
-        !p.dir || p.vnull != nullptr)
+        !p.dir || p.vnull != nullptr || p.max_tiles < 1 || p.grid < 1 ||
+        (int64_t)p.grid * p.max_tiles * kTileRecs < p.n)   // (whole-tile segments cover the batch)
         return hipErrorInvalidValue;
     fg_launch(k_tile_part1, dim3(p.grid), dim3(kTileThreads), 0, s, p);
     return hipGetLastError();
@@ -3139,53 +3143,83 @@ static_assert(kTileGroup <= 256 && kTileWin % 64 == 0, "tile walk shape");
 struct TileWalk {
     const uint32_t* col;
     const void* rec;
-    int64_t seg_per;
-    int32_t nt, mt;
+    int32_t nt;
     int32_t t0, stride;         // current group's first tile, groups' stride
     uint32_t xn[kTileTPL];      // the next group's directory entries (prefetched)
     uint32_t g_len[kTileTPL], g_st[kTileTPL], g_tot, b;
 };
+// Wave-wide inclusive scans on the DPP network (row_shr 1/2/4/8 inside each row of 16 lanes, then
+// row_bcast 15 / 31 across rows): one fused VALU op per step, no LDS round trip (a __shfl_up
+// step is a ds_bpermute plus a select).
+template <bool MAX>
+__device__ __forceinline__ uint32_t dpp_op(uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : a + b; }
+template <bool MAX>
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    // lanes without a DPP source (or masked) read 0: the identity of max (values >= 0) and of +
+    v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = dpp_op<MAX>(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return v;
+}
+// the value of the lane below (0 for lane 0): DPP wave_shr:1
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp, int32_t cb, int wave, int W,
                                                 int lane) {
     w.col = tp.dt + (int64_t)cb * tp.nt;
     w.rec = tp.rec;
-    w.seg_per = tp.seg_per;
     w.nt = tp.nt;
-    w.mt = tp.mt;
     w.stride = W * kTileGroup;
     w.t0 = wave * kTileGroup - w.stride;
 #pragma unroll
     for (int q = 0; q < kTileTPL; q++) {
+        // (every load issued, the index clamped and the entry masked: a load under a branch would
+        // keep the compiler from counting the wave's loads in flight -- s_waitcnt vmcnt(0))
         const int t = wave * kTileGroup + lane * kTileTPL + q;
-        w.xn[q] = t < w.nt ? gbl(w.col)[t] : 0u;
+        const uint32_t x = gbl(w.col)[t < w.nt ? t : 0];
+        w.xn[q] = t < w.nt ? x : 0u;
         w.g_len[q] = w.g_st[q] = 0;
     }
     w.g_tot = w.b = 0;
 }
-// the next window of the walk: records in kr / vr (lanes past nrec hold key 0), false when done
+// the next window of the walk: records in kr / vr (lanes at or past nrec: garbage, masked by the
+// caller), false when done. Every record load is issued unconditionally (lanes past nrec read
+// record 0), so the loads in flight are counted and the previous window's inserts wait only for
+// their own loads.
 __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_t* dl, int lane,
                                                int32_t (&kr)[kTileRpl], int64_t (&vr)[kTileRpl], uint32_t& nrec) {
+    static_assert(kTileRpl == 4, "one fragment-map word per lane");
+    // (every path issues the window's loads, also the one that ends the walk: the caller's
+    // inserts then wait for exactly their own loads -- a path without them would make the
+    // compiler count the loads of the window just issued as possibly absent)
+    bool done = false;
     while (w.b >= w.g_tot) {   // the next group with records
         w.t0 += w.stride;
-        if (w.t0 >= w.nt) return false;
+        if (w.t0 >= w.nt) {
+            done = true;
+            break;
+        }
         uint32_t base[kTileTPL], sum = 0;
 #pragma unroll
         for (int q = 0; q < kTileTPL; q++) {
             const int t = w.t0 + lane * kTileTPL + q;
             const uint32_t x = w.xn[q];
-            w.xn[q] = t + w.stride < w.nt ? gbl(w.col)[t + w.stride] : 0u;
+            const int tn = t + w.stride;
+            const uint32_t xn = gbl(w.col)[tn < w.nt ? tn : 0];
+            w.xn[q] = tn < w.nt ? xn : 0u;
             w.g_len[q] = x >> 16;
-            base[q] = (uint32_t)(w.seg_per * (t / w.mt) + (int64_t)(t % w.mt) * kTileRecs) + (x & 0xffffu);
+            base[q] = (uint32_t)t * (uint32_t)kTileRecs + (x & 0xffffu);   // (whole-tile segments)
             w.g_st[q] = sum;   // (local prefix; the wave's exclusive prefix added below)
             sum += w.g_len[q];
         }
-        uint32_t inc = sum;
-        for (int s = 1; s < 64; s <<= 1) {
-            const uint32_t y = __shfl_up(inc, s);
-            if (lane >= s) inc += y;
-        }
+        const uint32_t inc = wave_incl_scan<false>(sum);
         const uint32_t ex = inc - sum;
-        w.g_tot = __shfl(inc, 63);
+        w.g_tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         w.b = 0;
         wave_lds_sync();   // (the last window's reads of dl are done: its loads were issued)
 #pragma unroll
@@ -3194,8 +3228,13 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             dl[lane * kTileTPL + q] = base[q] - w.g_st[q];
         }
     }
-#pragma unroll
-    for (int q = 0; q < kTileRpl; q++) fm[lane * kTileRpl + q] = 0;
+    // the fragment map of the window: each position's fragment (the fragments mark their first
+    // position, then an inclusive max-scan), one 4-byte word of 4 positions per lane
+    if (done) {
+        w.b = w.g_tot = 0;   // (nrec = 0 below: the loads read record 0)
+    }
+    uint32_t* fm32 = reinterpret_cast<uint32_t*>(fm);
+    fm32[lane] = 0;
     wave_lds_sync();
 #pragma unroll
     for (int q = 0; q < kTileTPL; q++) {
@@ -3203,36 +3242,29 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
         if (len > 0 && st < w.b + kTileWin && st + len > w.b) fm[st > w.b ? st - w.b : 0] = (uint8_t)(lane * kTileTPL + q);
     }
     wave_lds_sync();
-    uint32_t e[kTileRpl];
-#pragma unroll
-    for (int q = 0; q < kTileRpl; q++) e[q] = fm[lane * kTileRpl + q];
-#pragma unroll
-    for (int q = 1; q < kTileRpl; q++) e[q] = e[q] > e[q - 1] ? e[q] : e[q - 1];
-    uint32_t m = e[kTileRpl - 1];
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t y = __shfl_up(m, s);
-        if (lane >= s) m = m > y ? m : y;
-    }
-    uint32_t pre = __shfl_up(m, 1);
-    if (lane == 0) pre = 0;
-#pragma unroll
-    for (int q = 0; q < kTileRpl; q++) fm[lane * kTileRpl + q] = (uint8_t)(e[q] > pre ? e[q] : pre);
+    const uint32_t e4 = fm32[lane];
+    uint32_t e0 = e4 & 255u, e1 = (e4 >> 8) & 255u, e2 = (e4 >> 16) & 255u, e3 = e4 >> 24;
+    e1 = e1 > e0 ? e1 : e0;
+    e2 = e2 > e1 ? e2 : e1;
+    e3 = e3 > e2 ? e3 : e2;
+    const uint32_t pre = wave_shr1(wave_incl_scan<true>(e3));
+    e0 = e0 > pre ? e0 : pre;
+    e1 = e1 > pre ? e1 : pre;
+    e2 = e2 > pre ? e2 : pre;
+    e3 = e3 > pre ? e3 : pre;
+    fm32[lane] = e0 | e1 << 8 | e2 << 16 | e3 << 24;
     wave_lds_sync();
     nrec = w.g_tot - w.b < (uint32_t)kTileWin ? w.g_tot - w.b : (uint32_t)kTileWin;
 #pragma unroll
     for (int u = 0; u < kTileRpl; u++) {
         const uint32_t jr = lane + 64 * u;
-        kr[u] = 0;
-        vr[u] = 0;
-        if (jr < nrec) {
-            const uint32_t src = dl[fm[jr]] + w.b + jr;
-            const Rec12 r = ld_rec12(w.rec, (uint64_t)src);
-            kr[u] = (int32_t)r.k;
-            vr[u] = rec12_val(r);
-        }
+        const uint32_t src = jr < nrec ? dl[fm[jr]] + w.b + jr : 0u;
+        const Rec12 r = ld_rec12(w.rec, (uint64_t)src);
+        kr[u] = (int32_t)r.k;
+        vr[u] = rec12_val(r);
     }
     w.b += kTileWin;
-    return true;
+    return !done;
 }
 
 // Fire from tile passes: one workgroup per item -- a bucket of the lane (4 << (bits - tbits)
@@ -3256,10 +3288,13 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     constexpr int T = kTileFireThreads, W = T / 64, S = kTileSlots;
     constexpr int kRounds = S / T + 1;   // + 1: the sentinel slot (thread 0)
     static_assert(S % T == 0 && (S & (S - 1)) == 0, "table rounds");
-    __shared__ int32_t t_key[S + 1];            // slot S: the key INT32_MIN (the empty sentinel)
-    __shared__ uint32_t t_cs[S + 1];
-    __shared__ unsigned long long t_v[S + 1];
-    __shared__ uint8_t s_fm[W][kTileWin];
+    // slot S: the key INT32_MIN (the empty sentinel); slot S + 1: a dummy that window lanes without
+    // a record (or whose key found no slot) add into, so the inserts need no branch (never emitted)
+    constexpr int kDummy = S + 1;
+    __shared__ __attribute__((aligned(16))) int32_t t_key[S + 2];
+    __shared__ uint32_t t_cs[S + 2];
+    __shared__ unsigned long long t_v[S + 2];
+    __shared__ __attribute__((aligned(16))) uint8_t s_fm[W][kTileWin];
     __shared__ uint32_t s_dl[W][kTileGroup];
     __shared__ uint32_t s_grp[kRounds * W];
     __shared__ uint16_t s_map[S + 1];
@@ -3295,7 +3330,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 r_hi = (x + 1) << (sub + kTileBits);
             }
         }
-        for (int i = tid; i <= S; i += T) {
+        for (int i = tid; i <= S + 1; i += T) {
             t_key[i] = kEmpty32;
             t_cs[i] = 0;
             t_v[i] = (unsigned long long)vinit;
@@ -3393,55 +3428,71 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
         }
         if (live) {
+            // one window's records into the table. A bucket fills in slot order and keys are never
+            // removed, so a key present in a bucket sits before its first empty slot: the common
+            // case -- the key in its home bucket -- is four compares and a select, no branch; the
+            // lanes whose key is not there (its first record in this fire, or a full home bucket)
+            // claim a slot by CAS or probe on, in a loop entered only when some lane needs it; the
+            // adds are unconditional (lanes without a record add into the dummy slot)
             auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
                 uint32_t hm[kTileRpl];
                 int4 bq[kTileRpl];
+                int sl[kTileRpl];
 #pragma unroll
                 for (int u = 0; u < kTileRpl; u++) {   // every home bucket read first, then resolved
                     hm[u] = __umulhi((uint32_t)kr[u] * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
                     bq[u] = *reinterpret_cast<const int4*>(&t_key[hm[u]]);
                 }
+                bool pend[kTileRpl];
 #pragma unroll
                 for (int u = 0; u < kTileRpl; u++) {
-                    if (lane + 64 * u >= nrec) continue;
                     const int32_t key = kr[u];
-                    if (retry && (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) != r_lo) continue;
-                    int sl = -1;
-                    if (key == kEmpty32) {
-                        sl = S;
-                    } else {
-                        uint32_t home = hm[u];
-                        int4 q4 = bq[u];
-                        for (int probe = 0; probe < S / 4; probe++) {
-                            const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
-                            int hit = -1, emp = -1;
+                    bool valid = lane + 64 * u < (int)nrec;
+                    if (retry) valid = valid && (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) == r_lo;
+                    const int4 q4 = bq[u];
+                    int z = q4.w == key ? 3 : -1;
+                    z = q4.z == key ? 2 : z;
+                    z = q4.y == key ? 1 : z;
+                    z = q4.x == key ? 0 : z;
+                    int s0 = z >= 0 ? (int)hm[u] + z : -1;
+                    s0 = key == kEmpty32 ? S : s0;
+                    pend[u] = valid && s0 < 0;
+                    sl[u] = valid ? s0 : kDummy;
+                }
 #pragma unroll
-                            for (int z = 3; z >= 0; z--) {
-                                if (qq[z] == key) hit = z;
-                                if (qq[z] == kEmpty32) emp = z;
-                            }
-                            if (hit >= 0 && (emp < 0 || hit < emp)) {
-                                sl = (int)home + hit;
-                                break;
-                            }
-                            if (emp >= 0) {
-                                const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
-                                if (old == kEmpty32 || old == key) {
-                                    sl = (int)home + emp;
-                                    break;
-                                }
-                            } else {
-                                home = (home + 4) & (S - 1);
-                            }
+                for (int u = 0; u < kTileRpl; u++) {
+                    if (__ballot(pend[u]) == 0) continue;   // (uniform)
+                    if (!pend[u]) continue;
+                    const int32_t key = kr[u];
+                    uint32_t home = hm[u];
+                    int4 q4 = bq[u];
+                    int found = -1;
+                    for (int probe = 0; probe < S / 4 && found < 0; probe++) {
+                        const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
+                        int hit = -1, emp = -1;
+#pragma unroll
+                        for (int z = 3; z >= 0; z--) {
+                            if (qq[z] == key) hit = z;
+                            if (qq[z] == kEmpty32) emp = z;
+                        }
+                        if (hit >= 0 && (emp < 0 || hit < emp)) {
+                            found = (int)home + hit;
+                        } else if (emp >= 0) {
+                            const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
+                            if (old == kEmpty32 || old == key) found = (int)home + emp;
+                            else q4 = *reinterpret_cast<const int4*>(&t_key[home]);   // (lost the slot: again)
+                        } else {
+                            home = (home + 4) & (S - 1);
                             q4 = *reinterpret_cast<const int4*>(&t_key[home]);
                         }
                     }
-                    if (sl < 0) {
-                        full = true;
-                        continue;
-                    }
-                    atomicAdd(&t_cs[sl], 1u);
-                    lds_val(&t_v[sl], vr[u], vt, true);
+                    if (found < 0) full = true;
+                    sl[u] = found >= 0 ? found : kDummy;
+                }
+#pragma unroll
+                for (int u = 0; u < kTileRpl; u++) {
+                    atomicAdd(&t_cs[sl[u]], 1u);
+                    lds_val(&t_v[sl[u]], vr[u], vt, true);
                 }
             };
             for (int pi = 0; pi < f.n_passes; pi++) {
@@ -3658,7 +3709,7 @@ __global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32
         const uint32_t x = gbl(col)[t];
         const uint32_t len = x >> 16;
         if (!len) continue;
-        const uint64_t base = (uint64_t)(tp.seg_per * (t / tp.mt) + (int64_t)(t % tp.mt) * kTileRecs) + (x & 0xffffu);
+        const uint64_t base = (uint64_t)t * kTileRecs + (x & 0xffffu);
         for (uint32_t i = 0; i < len; i++) {
             const Rec12 r = ld_rec12(tp.rec, base + i);
             const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
