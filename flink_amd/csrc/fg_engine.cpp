@@ -617,6 +617,7 @@ int check_overflow(fg_handle* h) {
     // region overflows (bits 0 and 2) are handled by the fail list (settle_jobs)
     unsigned int fl = h->h_scalars.as<unsigned int>()[0];
     if (fl & 2u) return h->fail(FG_EDEVICE, "internal: fired-row buffer overflow");
+    if (fl & 8u) return h->fail(FG_EDEVICE, "internal: a tile walk addressed a record past its pass");
     return FG_OK;
 }
 

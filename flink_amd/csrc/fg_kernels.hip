@@ -3143,6 +3143,8 @@ static_assert(kTileGroup <= 256 && kTileWin % 64 == 0, "tile walk shape");
 struct TileWalk {
     const uint32_t* col;
     const void* rec;
+    uint32_t n;                 // records of the pass: a source at or past it is a walk error
+    bool bad;                   // (reported as overflow flag 8, the record not read)
     int32_t nt;
     int32_t t0, stride;         // current group's first tile, groups' stride
     uint32_t xn[kTileTPL];      // the next group's directory entries (prefetched)
@@ -3173,6 +3175,8 @@ __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp,
                                                 int lane) {
     w.col = tp.dt + (int64_t)cb * tp.nt;
     w.rec = tp.rec;
+    w.n = (uint32_t)tp.n;
+    w.bad = false;
     w.nt = tp.nt;
     w.stride = W * kTileGroup;
     w.t0 = wave * kTileGroup - w.stride;
@@ -3258,7 +3262,11 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
 #pragma unroll
     for (int u = 0; u < kTileRpl; u++) {
         const uint32_t jr = lane + 64 * u;
-        const uint32_t src = jr < nrec ? dl[fm[jr]] + w.b + jr : 0u;
+        uint32_t src = jr < nrec ? dl[fm[jr]] + w.b + jr : 0u;
+        if (src >= w.n) {   // (never, if the directory and the walk agree: reported, not read)
+            w.bad = true;
+            src = 0;
+        }
         const Rec12 r = ld_rec12(w.rec, (uint64_t)src);
         kr[u] = (int32_t)r.k;
         vr[u] = rec12_val(r);
@@ -3510,6 +3518,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
                     insert(kb, vb, nb);
                 }
+                if (__ballot(w.bad) != 0 && lane == 0) atomicOr(p.overflow, 8u);
             }
         }
         if (full) atomicOr(&s_flags, 4u);
