@@ -3221,7 +3221,10 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             w.g_st[q] = sum;   // (local prefix; the wave's exclusive prefix added below)
             sum += w.g_len[q];
         }
-        const uint32_t inc = wave_incl_scan<false>(sum);
+        uint32_t inc = wave_incl_scan<false>(sum);
+        // (the scan materialized: the compiler otherwise folds `base - (prefix + inc - sum)` into a
+        // chain of DPP subtracts, which produced wrong fragment bases -- DESIGN section 8)
+        asm volatile("" : "+v"(inc));
         const uint32_t ex = inc - sum;
         w.g_tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         w.b = 0;
@@ -3264,6 +3267,12 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
         const uint32_t jr = lane + 64 * u;
         uint32_t src = jr < nrec ? dl[fm[jr]] + w.b + jr : 0u;
         if (src >= w.n) {   // (never, if the directory and the walk agree: reported, not read)
+#ifdef FG_DEBUG_WALK
+            if (!w.bad)
+                printf("walk: lane %d u %d jr %u nrec %u b %u g_tot %u t0 %d nt %d n %u src %u fm %u dl %u "
+                       "g_st %u %u g_len %u %u xn %u %u\n", lane, u, jr, nrec, w.b, w.g_tot, w.t0, w.nt, w.n, src,
+                       (uint32_t)fm[jr], dl[fm[jr]], w.g_st[0], w.g_st[1], w.g_len[0], w.g_len[1], w.xn[0], w.xn[1]);
+#endif
             w.bad = true;
             src = 0;
         }
