@@ -3221,7 +3221,15 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             w.g_st[q] = sum;   // (local prefix; the wave's exclusive prefix added below)
             sum += w.g_len[q];
         }
+#ifdef FG_EXP_SHFL_SCAN   // (A/B: __shfl_up scans)
+        uint32_t inc = sum;
+        for (int sft = 1; sft < 64; sft <<= 1) {
+            const uint32_t y = __shfl_up(inc, sft);
+            if (lane >= sft) inc += y;
+        }
+#else
         uint32_t inc = wave_incl_scan<false>(sum);
+#endif
         // (the scan materialized: the compiler otherwise folds `base - (prefix + inc - sum)` into a
         // chain of DPP subtracts, which produced wrong fragment bases -- DESIGN section 8)
         asm volatile("" : "+v"(inc));
@@ -3254,7 +3262,17 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
     e1 = e1 > e0 ? e1 : e0;
     e2 = e2 > e1 ? e2 : e1;
     e3 = e3 > e2 ? e3 : e2;
+#ifdef FG_EXP_SHFL_SCAN
+    uint32_t mm = e3;
+    for (int sft = 1; sft < 64; sft <<= 1) {
+        const uint32_t y = __shfl_up(mm, sft);
+        if (lane >= sft) mm = mm > y ? mm : y;
+    }
+    uint32_t pre = __shfl_up(mm, 1);
+    if (lane == 0) pre = 0;
+#else
     const uint32_t pre = wave_shr1(wave_incl_scan<true>(e3));
+#endif
     e0 = e0 > pre ? e0 : pre;
     e1 = e1 > pre ? e1 : pre;
     e2 = e2 > pre ? e2 : pre;
@@ -3265,6 +3283,13 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
 #pragma unroll
     for (int u = 0; u < kTileRpl; u++) {
         const uint32_t jr = lane + 64 * u;
+#ifdef FG_EXP_COND_LOADS   // (A/B: loads only for records in the window)
+        if (jr >= nrec) {
+            kr[u] = 0;
+            vr[u] = 0;
+            continue;
+        }
+#endif
         uint32_t src = jr < nrec ? dl[fm[jr]] + w.b + jr : 0u;
         if (src >= w.n) {   // (never, if the directory and the walk agree: reported, not read)
 #ifdef FG_DEBUG_WALK
@@ -3445,6 +3470,59 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
         }
         if (live) {
+#ifdef FG_EXP_OLD_INSERT   // (A/B: the round-4 insert, one probe loop per record)
+            auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+                uint32_t hm[kTileRpl];
+                int4 bq[kTileRpl];
+#pragma unroll
+                for (int u = 0; u < kTileRpl; u++) {   // every home bucket read first, then resolved
+                    hm[u] = __umulhi((uint32_t)kr[u] * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
+                    bq[u] = *reinterpret_cast<const int4*>(&t_key[hm[u]]);
+                }
+#pragma unroll
+                for (int u = 0; u < kTileRpl; u++) {
+                    if (lane + 64 * u >= nrec) continue;
+                    const int32_t key = kr[u];
+                    if (retry && (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) != r_lo) continue;
+                    int sl = -1;
+                    if (key == kEmpty32) {
+                        sl = S;
+                    } else {
+                        uint32_t home = hm[u];
+                        int4 q4 = bq[u];
+                        for (int probe = 0; probe < S / 4; probe++) {
+                            const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
+                            int hit = -1, emp = -1;
+#pragma unroll
+                            for (int z = 3; z >= 0; z--) {
+                                if (qq[z] == key) hit = z;
+                                if (qq[z] == kEmpty32) emp = z;
+                            }
+                            if (hit >= 0 && (emp < 0 || hit < emp)) {
+                                sl = (int)home + hit;
+                                break;
+                            }
+                            if (emp >= 0) {
+                                const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
+                                if (old == kEmpty32 || old == key) {
+                                    sl = (int)home + emp;
+                                    break;
+                                }
+                            } else {
+                                home = (home + 4) & (S - 1);
+                            }
+                            q4 = *reinterpret_cast<const int4*>(&t_key[home]);
+                        }
+                    }
+                    if (sl < 0) {
+                        full = true;
+                        continue;
+                    }
+                    atomicAdd(&t_cs[sl], 1u);
+                    lds_val(&t_v[sl], vr[u], vt, true);
+                }
+            };
+#else
             // one window's records into the table. A bucket fills in slot order and keys are never
             // removed, so a key present in a bucket sits before its first empty slot: the common
             // case -- the key in its home bucket -- is four compares and a select, no branch; the
@@ -3512,6 +3590,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     lds_val(&t_v[sl[u]], vr[u], vt, true);
                 }
             };
+#endif
             for (int pi = 0; pi < f.n_passes; pi++) {
                 const TilePass tp = f.n_passes == 1 ? f.one : f.passes[pi];
                 TileWalk w;
