@@ -120,6 +120,7 @@ struct Staged {
     // until a TUMBLE / local-phase fire reads them (k_tile_fire) or they are materialized
     bool tiles = false;
     DevBuf t_rec, t_dt;   // block-laid 12-B records at their batch index; per-bucket (offset, length) columns
+    DevBuf t_btot;        // records per bucket of the pass (a skewed pass's fire plans its chunks from them)
     int64_t t_n = 0;
     int t_nt = 0, t_mt = 0, t_nc = 0;
     bool busy = false;    // read by a merge job not yet settled: not reused from the pool
@@ -165,11 +166,11 @@ constexpr int64_t kHeavyMin = 1 << 16;
 constexpr int64_t kHeavyChunk = 1 << 16;
 
 enum KClass { K_COUNT = 0, K_SCAN, K_SCATTER, K_PART1, K_PART2, K_FLUSH, K_FLUSH_FIRE, K_FIRE, K_EXPORT, K_RESTORE,
-              K_HEAVY, K_TILE1, K_TILE_FIRE, K_TILE_MAT, K_TILE_FLUSH, K_NCLASS };
+              K_HEAVY, K_TILE1, K_TILE_FIRE, K_TILE_MAT, K_TILE_FLUSH, K_TILE_SPLIT, K_NCLASS };
 const char* const kClassName[K_NCLASS] = {"ingest_count", "ingest_scan",      "ingest_scatter", "ingest_part1",
                                            "ingest_part2", "merge_flush",      "merge_flush_fire", "merge_fire",
                                            "export",       "restore",          "merge_heavy",      "tile_part1",
-                                           "tile_fire",    "tile_materialize", "tile_flush"};
+                                           "tile_fire",    "tile_materialize", "tile_flush",       "tile_split_fire"};
 struct KStat {
     int64_t launches = 0;
     double ms = 0;
@@ -308,7 +309,11 @@ struct fg_handle {
     int tile_grid_force = 0;  // FG_TILE_GRID (test knob, tile_grid)
     bool tile_skew = false;   // a tile pass saw hot-key skew: later batches take the two-pass partition
                               // (a performance hint kept across fg_reset)
+    // FG_TILE_SPLIT (default on): a skewed tile pass of a TUMBLE / local-phase operator stays on the
+    // tiles; its fire splits the hot buckets into chunk items (k_tile_plan / k_tile_merge_parts)
+    bool tile_split = true;
     DevBuf tile_dir, tile_hist;
+    DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail;   // split fire plan + partials
     // skewed-region plan and chunk partial tables
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
     DevBuf hv_mv1, hv_mv2;   // multi-value operator: value slots 1 and 2 of the chunks' partial rows
@@ -756,6 +761,7 @@ TilePass tile_pass_of(const Staged* s, int lane) {
     tp.nc = s->t_nc;
     tp.bits = s->bits;
     tp.lane = lane;
+    tp.btot = s->t_btot.p ? s->t_btot.as<uint32_t>() : nullptr;
     return tp;
 }
 
@@ -1100,9 +1106,13 @@ int materialize_lane(fg_handle* h, int l) {
         uint32_t* bo = m->bucket_off.as<uint32_t>() + ((int64_t)l << bits);
         {
             KTimer kt(h, K_TILE_MAT, s->lane_n[l]);
-            HIPCHK(h, launch_tile_count(tp, bits, h->tile_hist.as<uint32_t>(), h->stream));
-            HIPCHK(h, launch_scan_u32(h->tile_hist.as<uint32_t>(), bo, P, h->scan_tmp.as<uint32_t>(), h->stream));
-            HIPCHK(h, launch_tile_scatter(tp, bits, bo, m->own_rec.p, h->stream));
+            uint32_t* hist = h->tile_hist.as<uint32_t>();
+            HIPCHK(h, hipMemsetAsync(hist, 0, 4 * (size_t)P, h->stream));
+            HIPCHK(h, launch_tile_count(tp, bits, hist, h->stream));
+            HIPCHK(h, launch_scan_u32(hist, bo, P, h->scan_tmp.as<uint32_t>(), h->stream));
+            // (the scan's bases copied: the scatter's workgroups reserve their blocks from them)
+            HIPCHK(h, hipMemcpyAsync(hist, bo, 4 * (size_t)P, hipMemcpyDeviceToDevice, h->stream));
+            HIPCHK(h, launch_tile_scatter(tp, bits, hist, m->own_rec.p, h->stream));
         }
         m->bits = bits;
         m->is_acc = false;
@@ -1131,11 +1141,67 @@ int materialize_lane(fg_handle* h, int l) {
 
 // Lane l fires straight from its tile passes: every pass a tile pass of the same bits, no skew,
 // COUNT(*) below 2^32
-bool tile_fire_ok(const fg_handle* h, const Lane& ln) {
+bool tile_fire_ok(const fg_handle* h, const Lane& ln, bool allow_skew = false) {
     if (ln.passes.empty() || ln.acc_fill != 0 || ln.fill >= ((int64_t)1 << 32) || h->mv) return false;
+    if (allow_skew && ln.passes.size() > (size_t)kMaxTilePasses) return false;
     for (const Staged* s : ln.passes)
-        if (!s->tiles || s->skew || s->bits != ln.passes[0]->bits) return false;
+        if (!s->tiles || (s->skew && !allow_skew) || s->bits != ln.passes[0]->bits) return false;
     return true;
+}
+
+// A skewed tile pass stays on the tiles (FG_TILE_SPLIT): TUMBLE windows and local-phase slices,
+// whose lanes fire straight from the tiles by the split fire (anything else materializes them)
+bool tile_split_ok(const fg_handle* h) { return h->tile_split && (h->w.kind == TUMBLE || h->local); }
+
+// The split fire of a lane holding a skewed tile pass (fg_kernels.h TileSplit): k_tile_plan cuts
+// the buckets above max(kTileChunk, 4x the lane's mean) into chunk items, k_tile_fire aggregates
+// every item (chunks into partial entries), k_tile_merge_parts merges each split bucket's chunks
+// into its rows. f is the job's TileFire (tile_job_params).
+int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f) {
+    const int nb = 1 << (f.tbits - kTileBits);
+    const int64_t fill = ln.fill;
+    const int64_t max_chunks = fill / kTileChunk + nb + 1;   // (chunks >= kTileChunk records, + 1 per bucket)
+    const int64_t max_items = max_chunks + nb;
+    const int64_t part_cap = std::min<int64_t>(fill, max_chunks * (kTileSlots + 1)) + 1;
+    if (part_cap >= ((int64_t)1 << 32)) return h->fail(FG_ECAPACITY, "internal: split fire partials above 2^32");
+    HIPCHK(h, h->sp_items.ensure(sizeof(TileItem) * (size_t)max_items));
+    HIPCHK(h, h->sp_n.ensure(16));
+    HIPCHK(h, h->sp_split.ensure(4 * 3 * (size_t)nb));
+    HIPCHK(h, h->sp_parts.ensure(4 * 2 * (size_t)max_chunks));
+    HIPCHK(h, h->sp_pkey.ensure(4 * (size_t)part_cap));
+    HIPCHK(h, h->sp_pcs.ensure(4 * (size_t)part_cap));
+    HIPCHK(h, h->sp_pv.ensure(8 * (size_t)part_cap));
+    HIPCHK(h, h->sp_bfail.ensure(4 * (size_t)nb));
+    HIPCHK(h, hipMemsetAsync(h->sp_n.p, 0, 16, h->stream));   // n_items, n_split, part_fill
+    TileSplit& sp = f.sp;
+    sp.items = h->sp_items.as<TileItem>();
+    sp.n_items = h->sp_n.as<uint32_t>();
+    sp.n_split = h->sp_n.as<uint32_t>() + 1;
+    sp.part_fill = h->sp_n.as<uint32_t>() + 2;
+    sp.max_items = (int32_t)max_items;
+    sp.max_split = nb;
+    sp.split_b = h->sp_split.as<int32_t>();
+    sp.split_c0 = sp.split_b + nb;
+    sp.split_k = sp.split_b + 2 * nb;
+    sp.part_off = h->sp_parts.as<uint32_t>();
+    sp.part_n = sp.part_off + max_chunks;
+    sp.part_cap = (uint32_t)part_cap;
+    sp.p_key = h->sp_pkey.as<int32_t>();
+    sp.p_cs = h->sp_pcs.as<uint32_t>();
+    sp.p_v = h->sp_pv.as<unsigned long long>();
+    sp.bfail = h->sp_bfail.as<uint32_t>();
+    int32_t g = 0;
+    for (size_t i = 0; i < ln.passes.size(); i++) {
+        sp.gpre[i] = g;
+        g += ln.passes[i]->t_nt;
+    }
+    sp.gpre[ln.passes.size()] = g;
+    f.split = 1;
+    f.hot = 1;
+    HIPCHK(h, launch_tile_plan(f, h->stream));
+    HIPCHK(h, launch_tile_fire(f, (int)std::min<int64_t>(max_items, h->merge_grid), h->stream));
+    HIPCHK(h, launch_tile_merge_parts(f, std::min(nb, h->merge_grid), h->stream));
+    return FG_OK;
 }
 
 // Plan the skewed regions of one lane's merge (k_heavy_plan): regions over
@@ -1234,7 +1300,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             rc = table_get(h, se, false, &t0);
             if (rc) return rc;
             if (fire0 && !refire_slice(h, se) && !(h->retain && !h->local) && (!t0 || t0->upper == 0) &&
-                tile_fire_ok(h, ln)) {
+                tile_fire_ok(h, ln, tile_split_ok(h))) {
                 const int64_t ub = std::min<int64_t>(ln.fill, kStateCapMax);
                 if (zeroed_out && !h->out_count_reset && h->adv_base + h->late_rows == 0) h->out_count_reset = true;
                 rc = reset_out_count(h);
@@ -1258,9 +1324,16 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 TileFire f{};
                 rc = tile_job_params(h, ji, &f);
                 if (rc) return rc;
+                bool skewed = false;
+                for (const Staged* st : ln.passes) skewed = skewed || st->skew;
                 {
-                    KTimer kt(h, K_TILE_FIRE, ln.fill);
-                    HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                    KTimer kt(h, skewed ? K_TILE_SPLIT : K_TILE_FIRE, ln.fill);
+                    if (skewed) {
+                        rc = tile_split_fire(h, ln, f);
+                        if (rc) return rc;
+                    } else {
+                        HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                    }
                 }
                 if (t0) fired_tables.push_back(se);
                 any_emit = true;
@@ -2206,6 +2279,8 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         const int64_t NT = (int64_t)p.grid * p.max_tiles;
         HIPCHK(h, st->t_rec.ensure((size_t)(n / 64 + 2) * kRec12Block));
         HIPCHK(h, st->t_dt.ensure(4 * (size_t)p.n_coarse * NT));
+        HIPCHK(h, st->t_btot.ensure(4 * (size_t)p.n_coarse));
+        p.tile_btot = st->t_btot.as<uint32_t>();
         HIPCHK(h, h->tile_dir.ensure(2 * (size_t)NT * kTileDirStride(p.n_coarse)));
         p.tmp = st->t_rec.as<longlong2>();
         p.dir = h->tile_dir.as<uint16_t>();
@@ -2252,7 +2327,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         }
         // each bucket's (offset, length) column (before k_scan_plan resets the lane mask it reads)
         HIPCHK(h, launch_tile_dirt(p.dir, ps.s->t_nt, p.n_coarse, h->region_bits - kTileBits, p.lane_mask,
-                                   ps.s->t_dt.as<uint32_t>(), h->stream));
+                                   ps.s->t_dt.as<uint32_t>(), p.tile_btot, h->stream));
     } else if (two_pass) {
         KTimer kt(h, K_PART1, n);
         HIPCHK(h, launch_part1(p, h->stream));
@@ -2380,7 +2455,7 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
         out->drops = drops;
         return rc;
     }
-    if (tiles && out->skew) {
+    if (tiles && out->skew && !tile_split_ok(h)) {
         // hot keys (a bucket of one tile above 16x the uniform mean): a tile pass would be fired by
         // one overloaded workgroup per hot bucket, or materialized by one (9.6 ms per 100M-record
         // Zipf(1.1) batch, round 4). Tile staging ends for good and the batch is staged again by
@@ -2509,7 +2584,7 @@ int ingest_finish(fg_handle* h, PassState& ps, Counters* out) {
     s->busy = false;
     s->skew = out->skew;
     h->skew_seen = h->skew_seen || out->skew;
-    if (tiles && out->skew) h->tile_skew = true;
+    if (tiles && out->skew && !tile_split_ok(h)) h->tile_skew = true;
     s->refs = 0;
     for (int l = 0; l < h->lanes; l++) {
         if (out->lane_total[l] == 0) continue;
@@ -3361,6 +3436,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_TILE")) hp->tile_env = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_STATE")) hp->tile_state = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_GRID")) hp->tile_grid_force = std::atoi(e);
+    if (const char* e = getenv("FG_TILE_SPLIT")) hp->tile_split = std::atoi(e) != 0;
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";

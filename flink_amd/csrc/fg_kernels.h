@@ -172,6 +172,8 @@ struct IngestParams {
     uint8_t* tmp_null;         // NULL flags of tmp (when vnull)
     uint16_t* dir;             // [grid * max_tiles][n_coarse + 1] coarse offsets within each tile
     int32_t max_tiles;         // tiles per workgroup segment (ceil(segment / kPart1Tile))
+    uint32_t* tile_btot;       // tile pass: [n_coarse] per-bucket totals, zeroed by k_tile_part1's
+                               // workgroup 0 (k_tile_dirt adds into them after it); may be null
     int32_t p2_group;          // pass-1 workgroups per pass-2 unit (0: part2_group's default); 1 for
                                // skewed input, whose hot coarse bucket would load a few units
     int32_t n_coarse;          // lanes << (region_bits - kFineBits)
@@ -450,6 +452,39 @@ struct TilePass {
     int32_t bits;             // region bits of the pass
     int32_t lane;
     int32_t pad;
+    const uint32_t* btot;     // [nc] records per bucket of the pass (k_tile_dirt); may be null
+};
+// Skewed tile passes (hot keys, Zipf): a bucket whose records exceed kTileChunk is fired by
+// several workgroups -- chunk items over equal ranges of its tiles, each aggregating its range in
+// an LDS table (hot keys pre-combined across the wave) and writing the table as partial entries
+// -- and the chunks' partials are then merged per bucket (k_tile_merge_parts) into the rows; the
+// other buckets fire as usual. k_tile_plan lists the items on the device.
+constexpr int kTileChunk = 1 << 16;           // records per chunk item of a split bucket
+constexpr int kMaxTilePasses = 8;             // passes one split fire walks
+struct TileItem {
+    int32_t bucket;           // the lane's bucket (item of the plain fire)
+    int32_t g_lo, g_hi;       // tiles [g_lo, g_hi) of the passes' concatenated tile sequence
+    int32_t part;             // chunk ordinal of a split bucket (its partials); -1: rows directly
+};
+struct TileSplit {
+    TileItem* items;          // [max_items], *n_items listed by k_tile_plan
+    uint32_t* n_items;
+    int32_t max_items;
+    int32_t max_split;
+    int32_t* split_b;         // split entry i: its bucket, first chunk ordinal, chunks
+    int32_t* split_c0;
+    int32_t* split_k;
+    uint32_t* n_split;
+    uint32_t* part_off;       // per chunk ordinal: first partial entry, entries (kChunkFailed: failed)
+    uint32_t* part_n;
+    uint32_t* part_fill;      // partial entries written (reservation counter)
+    uint32_t part_cap;
+    int32_t* p_key;           // partial entries: int32 key, COUNT(*), value bits (the LDS repr)
+    uint32_t* p_cs;
+    unsigned long long* p_v;
+    uint32_t* bfail;          // [buckets] a chunk of the bucket failed: the merge skips it (the
+                              // regions are redone by the split-and-retry protocol, listed once)
+    int32_t gpre[kMaxTilePasses + 1];   // tiles before pass pi in the concatenated sequence
 };
 struct TileFire {
     MergeParams m;            // emit fields, value op, overflow / out_count / fail list, job, region_bits
@@ -458,19 +493,25 @@ struct TileFire {
     int32_t n_passes;
     int32_t tbits;
     // items: the lane's buckets 0 .. (1 << (tbits - kTileBits)) - 1, or (retry) regions at
-    // m.region_bits: m.retry_list[0 .. m.n_retry)
+    // m.region_bits: m.retry_list[0 .. m.n_retry), or (split) sp.items[0 .. *sp.n_items)
+    int32_t split;            // sp holds a plan (k_tile_plan): a skewed pass's fire
+    int32_t hot;              // pre-combine a wave's records of its first lane's key (skewed passes)
+    TileSplit sp;
 };
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s);
 // directory transpose of a tile pass: dir [tiles][nc + 1] -> dt [nc][tiles] (lanes absent from
 // *lane_mask skipped)
 hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
-                            const unsigned long long* lane_mask, uint32_t* dt, hipStream_t s);
+                            const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot, hipStream_t s);
 hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s);
-// materialize: per-region counts of one tile pass's lane (hist[P] at `bits`), then -- after the
-// exclusive scan into bucket_off -- the records into a regular narrow staged area
+// a split fire: the plan (one workgroup), the fire over its items, the merge of split buckets
+hipError_t launch_tile_plan(const TileFire& f, hipStream_t s);
+hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStream_t s);
+// materialize: per-region counts of one tile pass's lane added into hist[P] at `bits` (zeroed
+// first), then -- after the exclusive scan into bucket_off, copied into `cursor` -- the records
+// into a regular narrow staged area (each workgroup reserves its regions' blocks from cursor)
 hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s);
-hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, const uint32_t* bucket_off, void* out_rec,
-                               hipStream_t s);
+hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, uint32_t* cursor, void* out_rec, hipStream_t s);
 
 constexpr int kMaxOwnerCols = 8;
 struct OwnerCols {

@@ -2863,6 +2863,8 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     const int tid = threadIdx.x;
     for (int i = tid; i <= NW; i += T) s_cw[i] = 0;
     if (tid == 0) { s_drop = 0; s_qmin = JMAX; s_qmax = JMIN; s_qnext = JMAX; s_mask = 0; s_bmax = 0; }
+    if (p.tile_btot && blockIdx.x == 0)
+        for (int i = tid; i < NC; i += T) p.tile_btot[i] = 0u;
     if (tid < kMaxLanes) s_lane[tid] = 0;
     __syncthreads();
     // whole-tile segments (the host trims the grid): tile j of this workgroup is tile
@@ -3079,8 +3081,9 @@ hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
 // dir [tiles][kTileDirStride(nc)] (u16 offsets, [nc] the total) -> dt [nc][tiles] = offset | length << 16, 64 x 64 blocks
 // through LDS; buckets of lanes without records (lane_mask) are skipped
 __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t NT, int32_t NC, int32_t lshift,
-                                                   const unsigned long long* lane_mask, uint32_t* dt) {
+                                                   const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot) {
     __shared__ uint16_t s[64][67];
+    __shared__ uint32_t s_tot[64];   // the block's records per bucket (btot: per-bucket totals of the pass)
     const int tb = blockIdx.x * 64, cb = blockIdx.y * 64;
     const unsigned long long lm = *gbl(lane_mask);
     const int l0 = cb >> lshift, l1 = (cb + 63 < NC ? cb + 63 : NC - 1) >> lshift;
@@ -3098,6 +3101,7 @@ __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t 
         s[tt][2 * k] = (uint16_t)w;
         s[tt][2 * k + 1] = (uint16_t)(w >> 16);
     }
+    if (threadIdx.x < 64) s_tot[threadIdx.x] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * 64; i += 256) {
         const int cc = i / 64, tt = i % 64;
@@ -3105,15 +3109,21 @@ __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t 
         if (t < NT && c < NC && ((lm >> (c >> lshift)) & 1)) {
             const uint32_t a = s[tt][cc], b = s[tt][cc + 1];
             dt[(int64_t)c * NT + t] = a | ((b - a) << 16);
+            if (btot) atomicAdd(&s_tot[cc], b - a);
         }
+    }
+    if (btot) {
+        __syncthreads();
+        if (threadIdx.x < 64 && cb + (int)threadIdx.x < NC && s_tot[threadIdx.x])
+            atomicAdd(&btot[cb + threadIdx.x], s_tot[threadIdx.x]);
     }
 }
 
 hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
-                            const unsigned long long* lane_mask, uint32_t* dt, hipStream_t s) {
+                            const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot, hipStream_t s) {
     if (tiles <= 0 || nc <= 0) return hipSuccess;
     fg_launch(k_tile_dirt, dim3((unsigned)((tiles + 63) / 64), (unsigned)((nc + 63) / 64)), dim3(256), 0, s, dir,
-              tiles, nc, lane_shift, lane_mask, dt);
+              tiles, nc, lane_shift, lane_mask, dt, btot);
     return hipGetLastError();
 }
 
@@ -3145,7 +3155,7 @@ struct TileWalk {
     const void* rec;
     uint32_t n;                 // records of the pass: a source at or past it is a walk error
     bool bad;                   // (reported as overflow flag 8, the record not read)
-    int32_t nt;
+    int32_t nt;                 // the walk's end tile (exclusive)
     int32_t t0, stride;         // current group's first tile, groups' stride
     uint32_t xn[kTileTPL];      // the next group's directory entries (prefetched)
     uint32_t g_len[kTileTPL], g_st[kTileTPL], g_tot, b;
@@ -3171,20 +3181,21 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// (the walk covers the pass's tiles [t_lo, t_hi): all of them, or a split bucket's chunk)
 __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp, int32_t cb, int wave, int W,
-                                                int lane) {
+                                                int lane, int32_t t_lo, int32_t t_hi) {
     w.col = tp.dt + (int64_t)cb * tp.nt;
     w.rec = tp.rec;
     w.n = (uint32_t)tp.n;
     w.bad = false;
-    w.nt = tp.nt;
+    w.nt = t_hi;
     w.stride = W * kTileGroup;
-    w.t0 = wave * kTileGroup - w.stride;
+    w.t0 = t_lo + wave * kTileGroup - w.stride;
 #pragma unroll
     for (int q = 0; q < kTileTPL; q++) {
         // (every load issued, the index clamped and the entry masked: a load under a branch would
         // keep the compiler from counting the wave's loads in flight -- s_waitcnt vmcnt(0))
-        const int t = wave * kTileGroup + lane * kTileTPL + q;
+        const int t = t_lo + wave * kTileGroup + lane * kTileTPL + q;
         const uint32_t x = gbl(w.col)[t < w.nt ? t : 0];
         w.xn[q] = t < w.nt ? x : 0u;
         w.g_len[q] = w.g_st[q] = 0;
@@ -3352,20 +3363,31 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     const int64_t vinit = lds_repr(vt, val_identity(vt));
     const int sub = p.region_bits - f.tbits;          // current region bits above the passes'
     const bool retry = p.retry_list != nullptr;
-    const int NI = retry ? p.n_retry : 1 << (f.tbits - kTileBits);
+    const bool split = !TAB && f.split != 0;          // items planned by k_tile_plan (a skewed pass)
+    const bool hot = f.hot != 0 && vt >= 0 && vt <= 2;   // (SUM-family value ops: pre-combine hot keys)
+    const int NI = retry ? p.n_retry : split ? (int)*gbl(f.sp.n_items) : 1 << (f.tbits - kTileBits);
     const int G = gridDim.x;
-    const bool xcd = !retry && G % 8 == 0;            // consecutive buckets on one XCD (shared L2 lines)
+    const bool xcd = !retry && !split && G % 8 == 0;  // consecutive buckets on one XCD (shared L2 lines)
     for (int k = 0;; k++) {
         const int b = (int)blockIdx.x;
         const int x = xcd ? k * G + (b % 8) * (G / 8) + b / 8 : b + k * G;
         if (k * G >= NI) break;
         const bool live = x < NI;
         int r_lo = 0, r_hi = 0, item = 0;
+        int32_t g_lo = 0, g_hi = 0x7fffffff, part = -1;   // (split: the item's tile range, chunk ordinal)
         if (live) {
             if (retry) {
                 r_lo = gbl(p.retry_list)[x];
                 r_hi = r_lo + 1;
                 item = r_lo >> (sub + kTileBits);
+            } else if (split) {
+                const TileItem it = f.sp.items[x];
+                item = it.bucket;
+                g_lo = it.g_lo;
+                g_hi = it.g_hi;
+                part = it.part;
+                r_lo = item << (sub + kTileBits);
+                r_hi = (item + 1) << (sub + kTileBits);
             } else {
                 item = x;
                 r_lo = x << (sub + kTileBits);
@@ -3533,10 +3555,14 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 uint32_t hm[kTileRpl];
                 int4 bq[kTileRpl];
                 int sl[kTileRpl];
+                uint32_t cn[kTileRpl];   // records a lane adds (> 1: a hot key's wave pre-combined)
+                int64_t va[kTileRpl];
 #pragma unroll
                 for (int u = 0; u < kTileRpl; u++) {   // every home bucket read first, then resolved
                     hm[u] = __umulhi((uint32_t)kr[u] * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
                     bq[u] = *reinterpret_cast<const int4*>(&t_key[hm[u]]);
+                    cn[u] = 1u;
+                    va[u] = vr[u];
                 }
                 bool pend[kTileRpl];
 #pragma unroll
@@ -3544,6 +3570,32 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     const int32_t key = kr[u];
                     bool valid = lane + 64 * u < (int)nrec;
                     if (retry) valid = valid && (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) == r_lo;
+                    if (hot) {
+                        // skewed pass: the records of the wave's first key (a hot key, when it is
+                        // the key of 16+ lanes) are added once, by one lane, with their count and
+                        // value sum (SUM-family value ops only); the other lanes of it add nothing
+                        const int32_t k0 = __builtin_amdgcn_readfirstlane(key);
+                        const bool mine = valid && key == k0;
+                        const uint64_t m = __ballot(mine);
+                        if (__popcll(m) >= 16) {   // (uniform)
+                            int64_t sv = mine ? vr[u] : 0;   // (0 bits: +0.0 and 0, the sum identity)
+#pragma unroll
+                            for (int off = 32; off > 0; off >>= 1) {
+                                const int64_t o = __shfl_xor(sv, off);
+                                if (vt == 2) sv = __double_as_longlong(__longlong_as_double(sv) + __longlong_as_double(o));
+                                else sv += o;
+                            }
+                            const int leader = __ffsll((long long)m) - 1;
+                            if (mine) {
+                                if (lane == leader) {
+                                    cn[u] = (uint32_t)__popcll(m);
+                                    va[u] = sv;
+                                } else {
+                                    valid = false;
+                                }
+                            }
+                        }
+                    }
                     const int4 q4 = bq[u];
                     int z = q4.w == key ? 3 : -1;
                     z = q4.z == key ? 2 : z;
@@ -3586,15 +3638,21 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 }
 #pragma unroll
                 for (int u = 0; u < kTileRpl; u++) {
-                    atomicAdd(&t_cs[sl[u]], 1u);
-                    lds_val(&t_v[sl[u]], vr[u], vt, true);
+                    atomicAdd(&t_cs[sl[u]], cn[u]);
+                    lds_val(&t_v[sl[u]], va[u], vt, true);
                 }
             };
 #endif
             for (int pi = 0; pi < f.n_passes; pi++) {
                 const TilePass tp = f.n_passes == 1 ? f.one : f.passes[pi];
+                int32_t t_lo = 0, t_hi = tp.nt;
+                if (split) {   // the item's range of the concatenated tile sequence, in this pass
+                    t_lo = g_lo - f.sp.gpre[pi] > 0 ? g_lo - f.sp.gpre[pi] : 0;
+                    t_hi = g_hi - f.sp.gpre[pi] < tp.nt ? g_hi - f.sp.gpre[pi] : tp.nt;
+                    if (t_lo >= t_hi) continue;
+                }
                 TileWalk w;
-                tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane);
+                tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane, t_lo, t_hi);
                 int32_t ka[kTileRpl], kb[kTileRpl];
                 int64_t va[kTileRpl], vb[kTileRpl];
                 uint32_t na = 0, nb = 0;
@@ -3657,15 +3715,26 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             over = __ballot(over) != 0;
             if (lane == 0) {
                 unsigned int fl = s_flags | (over ? 4u : 0u);
-                if (live && !(fl & 4u) && (!TAB || p.emit)) {
+                const bool to_part = split && part >= 0;
+                if (live && !(fl & 4u) && !to_part && (!TAB || p.emit)) {
                     const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
                     s_out_base = ob;
                     if ((int64_t)(ob + total) > p.out_cap) fl |= 2u;
                 }
+                if (live && !(fl & 4u) && to_part) {   // a chunk of a split bucket: its partial entries
+                    const uint32_t ob = atomicAdd(f.sp.part_fill, total);
+                    s_out_base = ob;
+                    if ((uint64_t)ob + total > (uint64_t)f.sp.part_cap) fl |= 2u;
+                    f.sp.part_off[part] = ob;
+                    f.sp.part_n[part] = total;
+                }
+                if (live && to_part && (fl & 4u)) f.sp.part_n[part] = kChunkFailed;
                 s_flags = fl;
                 s_total = total;
                 if (fl) atomicOr(p.overflow, fl);
-                if (live && (fl & 4u) && p.fail_list) {   // the item does nothing; the host redoes its regions
+                // the item does nothing; the host redoes its regions (a split bucket's regions are
+                // listed by its first failing chunk only, and its merge skips it)
+                if (live && (fl & 4u) && p.fail_list && (!to_part || atomicExch(&f.sp.bfail[item], 1u) == 0u)) {
                     const uint32_t nr = (uint32_t)(r_hi - r_lo);
                     const uint32_t at = atomicAdd(p.fail_n, nr);
                     for (uint32_t q = 0; q < nr; q++)
@@ -3684,7 +3753,16 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 (uint16_t)(r < kRounds - 1 ? r * T + tid : S);
         }
         __syncthreads();
-        if (live && (!TAB || p.emit) && !(fl & 6u)) {
+        if (live && split && part >= 0 && !(fl & 6u)) {   // partial entries (LDS repr), merged later
+            const uint32_t total = s_total;
+            const uint32_t ob = (uint32_t)s_out_base;
+            for (uint32_t i = tid; i < total; i += T) {
+                const int sl = s_map[i];
+                f.sp.p_key[ob + i] = sl == S ? kEmpty32 : t_key[sl];
+                f.sp.p_cs[ob + i] = t_cs[sl];
+                f.sp.p_v[ob + i] = t_v[sl];
+            }
+        } else if (live && (!TAB || p.emit) && !(fl & 6u)) {
             const uint32_t total = s_total;
             const unsigned long long ob = s_out_base;
             for (uint32_t i = tid; i < total; i += T) {
@@ -3786,50 +3864,291 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
     return hipGetLastError();
 }
 
-// Materialize a tile pass's lane into a regular narrow staged pass: per bucket (workgroup) the
-// records' regions at `bits` are counted (hist[region]), and after the exclusive scan into
-// bucket_off written at bucket_off[region] + their rank (order inside a region is immaterial)
-constexpr int kTileMatThreads = 256;
-template <bool SCATTER>
-__global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32_t bits, uint32_t* hist,
-                                                              const uint32_t* bucket_off, void* out) {
-    __shared__ uint32_t s_c[kTileMaxSub];
-    const int item = blockIdx.x;
-    const int sub = bits - tp.bits;
-    const int nsub = kTileBits + sub <= 6 ? 1 << (kTileBits + sub) : kTileMaxSub;
-    const int r_lo = item << (kTileBits + sub);
+// ---- split (skewed) tile fires ---------------------------------------------------------------
+// k_tile_plan (one workgroup): per bucket of the lane, its records over the fire's passes (the
+// passes' btot); a bucket above kTileChunk records becomes K = ceil(records / kTileChunk) chunk
+// items over equal ranges of the passes' concatenated tiles (records of a Zipf hot key spread
+// evenly over the tiles, as the stream does), the others one item each; the items, the split
+// entries and the counts are written for k_tile_fire / k_tile_merge_parts.
+constexpr int kTilePlanThreads = 1024;
+__global__ __launch_bounds__(kTilePlanThreads) void k_tile_plan(TileFire f) {
+    __shared__ uint32_t s_wave[kTilePlanThreads / 64];
+    const TileSplit& sp = f.sp;
+    const int nb = 1 << (f.tbits - kTileBits);
     const int tid = threadIdx.x;
-    if (tid < nsub) s_c[tid] = SCATTER ? gbl(bucket_off)[r_lo + tid] : 0u;
-    __syncthreads();
-    const uint32_t* col = tp.dt + (int64_t)((tp.lane << (tp.bits - kTileBits)) | item) * tp.nt;
-    for (int t = tid; t < tp.nt; t += kTileMatThreads) {
-        const uint32_t x = gbl(col)[t];
-        const uint32_t len = x >> 16;
-        if (!len) continue;
-        const uint64_t base = (uint64_t)t * kTileRecs + (x & 0xffffu);
-        for (uint32_t i = 0; i < len; i++) {
-            const Rec12 r = ld_rec12(tp.rec, base + i);
-            const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
-            const uint32_t pos = atomicAdd(&s_c[region - r_lo], 1u);
-            if (SCATTER) st_rec12(out, pos, (int64_t)(int32_t)r.k, rec12_val(r));
+    const int32_t G = sp.gpre[f.n_passes];
+    constexpr int BPT = kMaxTileBuckets / kTilePlanThreads;   // buckets per thread (consecutive)
+    uint32_t kk[BPT], tb[BPT], mine = 0, nitem = 0, nsplit = 0, nchunk = 0;
+#pragma unroll
+    for (int q = 0; q < BPT; q++) {
+        const int bk = tid * BPT + q;
+        tb[q] = 0;
+        if (bk >= nb) continue;
+        for (int pi = 0; pi < f.n_passes; pi++) {
+            const TilePass& tp = f.n_passes == 1 ? f.one : f.passes[pi];
+            if (tp.btot) tb[q] += gbl(tp.btot)[(tp.lane << (f.tbits - kTileBits)) | bk];
+        }
+        mine += tb[q];
+    }
+    // chunk size: kTileChunk records, at least 4x the lane's mean bucket (only hot buckets split)
+    uint32_t lane_total;
+    (void)block_exclusive_scan(mine, s_wave, &lane_total);
+    const uint64_t chunk = max((uint64_t)kTileChunk, 4 * ((uint64_t)lane_total / (uint64_t)nb));
+#pragma unroll
+    for (int q = 0; q < BPT; q++) {
+        const int bk = tid * BPT + q;
+        kk[q] = 0;
+        if (bk >= nb) continue;
+        uint64_t k = tb[q] > chunk ? (tb[q] + chunk - 1) / chunk : 1;
+        if (k > (uint64_t)G) k = G > 0 ? (uint64_t)G : 1;
+        kk[q] = (uint32_t)k;
+        nitem += (uint32_t)k;
+        if (k > 1) {
+            nsplit++;
+            nchunk += (uint32_t)k;
         }
     }
-    __syncthreads();
-    if (!SCATTER && tid < nsub) hist[r_lo + tid] = s_c[tid];
+    uint32_t t_item, t_split, t_chunk;
+    const uint32_t b_item = block_exclusive_scan(nitem, s_wave, &t_item);
+    const uint32_t b_split = block_exclusive_scan(nsplit, s_wave, &t_split);
+    const uint32_t b_chunk = block_exclusive_scan(nchunk, s_wave, &t_chunk);
+    const bool fits = t_item <= (uint32_t)sp.max_items && t_split <= (uint32_t)sp.max_split;
+    if (tid == 0) {
+        *sp.n_items = fits ? t_item : 0u;
+        *sp.n_split = fits ? t_split : 0u;
+        if (!fits) atomicOr(f.m.overflow, 2u);   // (the host sized the lists from the lane's records)
+    }
+    if (!fits) return;
+    uint32_t it = b_item, si = b_split, ci = b_chunk;
+#pragma unroll
+    for (int q = 0; q < BPT; q++) {
+        const int bk = tid * BPT + q;
+        const uint32_t k = kk[q];
+        if (k == 0) continue;
+        if (k > 1) {
+            sp.split_b[si] = bk;
+            sp.split_c0[si] = (int32_t)ci;
+            sp.split_k[si] = (int32_t)k;
+            sp.bfail[bk] = 0u;
+            si++;
+        }
+        for (uint32_t c = 0; c < k; c++) {
+            TileItem x;
+            x.bucket = bk;
+            x.g_lo = k > 1 ? (int32_t)((int64_t)G * c / k) : 0;
+            x.g_hi = k > 1 ? (int32_t)((int64_t)G * (c + 1) / k) : G;
+            x.part = k > 1 ? (int32_t)(ci + c) : -1;
+            sp.items[it + c] = x;
+        }
+        it += k;
+        if (k > 1) ci += k;
+    }
 }
 
-hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s) {
-    if (bits - tp.bits + kTileBits > 6) return hipErrorInvalidValue;   // (kTileMaxSub regions per bucket)
-    fg_launch(k_tile_mat<false>, dim3(1u << (tp.bits - kTileBits)), dim3(kTileMatThreads), 0, s, tp, bits, hist,
-              (const uint32_t*)nullptr, (void*)nullptr);
+hipError_t launch_tile_plan(const TileFire& f, hipStream_t s) {
+    if (!f.split || f.n_passes < 1 || f.n_passes > kMaxTilePasses || (1 << (f.tbits - kTileBits)) > kMaxTileBuckets ||
+        !f.sp.items || !f.sp.n_items || !f.sp.split_b || !f.sp.n_split || !f.sp.bfail)
+        return hipErrorInvalidValue;
+    fg_launch(k_tile_plan, dim3(1), dim3(kTilePlanThreads), 0, s, f);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, const uint32_t* bucket_off, void* out_rec,
-                               hipStream_t s) {
-    if (bits - tp.bits + kTileBits > 6) return hipErrorInvalidValue;
-    fg_launch(k_tile_mat<true>, dim3(1u << (tp.bits - kTileBits)), dim3(kTileMatThreads), 0, s, tp, bits,
-              (uint32_t*)nullptr, bucket_off, out_rec);
+// k_tile_merge_parts: one split bucket per workgroup (persistent): its chunks' partial entries
+// into one LDS table (COUNT(*) and the value accumulator added; the value's LDS repr as the chunks
+// left it), then one row per key (a6: write_row_k). A bucket whose chunk failed is skipped -- the
+// region split-and-retry redoes its regions from the tiles. A full table fails the bucket the same
+// way (its regions listed, nothing emitted).
+template <int VTC>
+__global__ __launch_bounds__(kTileFireThreads) void k_tile_merge_parts(TileFire f) {
+    constexpr int T = kTileFireThreads, S = kTileSlots;
+    __shared__ __attribute__((aligned(16))) int32_t t_key[S + 1];
+    __shared__ uint32_t t_cs[S + 1];
+    __shared__ unsigned long long t_v[S + 1];
+    __shared__ unsigned int s_full;
+    const MergeParams& p = f.m;
+    const TileSplit& sp = f.sp;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int vt = VTC >= 0 ? VTC : p.val_type;
+    const int64_t vinit = lds_repr(vt, val_identity(vt));
+    const int sub = p.region_bits - f.tbits;
+    const uint32_t NS = *gbl(sp.n_split);
+    for (uint32_t si = blockIdx.x; si < NS; si += gridDim.x) {
+        const int bk = sp.split_b[si];
+        if (*gbl(&sp.bfail[bk])) continue;   // (uniform: the retry redoes it)
+        for (int i = tid; i <= S; i += T) {
+            t_key[i] = kEmpty32;
+            t_cs[i] = 0;
+            t_v[i] = (unsigned long long)vinit;
+        }
+        if (tid == 0) s_full = 0;
+        __syncthreads();
+        bool full = false;
+        const int c0 = sp.split_c0[si], K = sp.split_k[si];
+        for (int c = c0; c < c0 + K; c++) {
+            const uint32_t off = sp.part_off[c], n = sp.part_n[c];
+            if ((uint64_t)off + n > (uint64_t)sp.part_cap) {   // (a failed chunk -- its bucket is listed -- or
+                if (tid == 0) atomicOr(p.overflow, 2u);        // partials past the capacity: none read)
+                continue;
+            }
+            for (uint32_t i = tid; i < n; i += T) {
+                const int32_t key = sp.p_key[off + i];
+                int sl = -1;
+                if (key == kEmpty32) {
+                    sl = S;
+                } else {
+                    uint32_t home = __umulhi((uint32_t)key * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
+                    for (int probe = 0; probe < S / 4 && sl < 0; probe++) {
+                        const int4 q4 = *reinterpret_cast<const int4*>(&t_key[home]);
+                        const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
+                        int hit = -1, emp = -1;
+#pragma unroll
+                        for (int z = 3; z >= 0; z--) {
+                            if (qq[z] == key) hit = z;
+                            if (qq[z] == kEmpty32) emp = z;
+                        }
+                        if (hit >= 0 && (emp < 0 || hit < emp)) {
+                            sl = (int)home + hit;
+                        } else if (emp >= 0) {
+                            const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
+                            if (old == kEmpty32 || old == key) sl = (int)home + emp;
+                        } else {
+                            home = (home + 4) & (S - 1);
+                        }
+                    }
+                }
+                if (sl < 0) {
+                    full = true;
+                    continue;
+                }
+                atomicAdd(&t_cs[sl], sp.p_cs[off + i]);
+                // (the partial holds the LDS repr: combine it as the fire combined the records --
+                // the SUM family adds, an ordered-int MIN / MAX image takes the integer min / max)
+                lds_val(&t_v[sl], (int64_t)lds_repr(vt, (int64_t)sp.p_v[off + i]), vt, true);
+            }
+        }
+        if (full) atomicOr(&s_full, 1u);
+        __syncthreads();
+        if (s_full) {
+            if (tid == 0) {
+                atomicOr(p.overflow, 4u);
+                if (p.fail_list && atomicExch(&sp.bfail[bk], 1u) == 0u) {
+                    const int r_lo = bk << (sub + kTileBits);
+                    const uint32_t nr = 1u << (sub + kTileBits);
+                    const uint32_t at = atomicAdd(p.fail_n, nr);
+                    for (uint32_t q = 0; q < nr; q++)
+                        if (at + q < (uint32_t)p.fail_cap)
+                            p.fail_list[at + q] = ((uint32_t)p.job << kFailJobShift) | (uint32_t)(r_lo + (int)q);
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        // one row per occupied slot (rows reserved per wave: a ballot, one atomic)
+        for (int i0 = 0; i0 <= S; i0 += T) {
+            const int sl = i0 + tid;
+            const bool occ = sl <= S && t_cs[sl] != 0;
+            const uint64_t bal = __ballot(occ);
+            unsigned long long base = 0;
+            if (lane == 0 && bal) base = atomicAdd(p.out_count, (unsigned long long)__popcll(bal));
+            base = __shfl(base, 0);
+            if (occ) {
+                const unsigned long long o = base + (unsigned long long)__popcll(bal & ((1ull << lane) - 1));
+                if ((int64_t)o < p.out_cap) {
+                    const int64_t v = lds_repr(vt, (int64_t)t_v[sl]);
+                    write_row_k(p, o, sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl], t_cs[sl], 0ull, &v, vt);
+                } else {
+                    atomicOr(p.overflow, 2u);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStream_t s) {
+    if (!f.split || workgroups < 1) return hipErrorInvalidValue;
+    const dim3 g((unsigned)workgroups), b(kTileFireThreads);
+    switch (f.m.val_type) {
+        case 2: fg_launch(k_tile_merge_parts<2>, g, b, 0, s, f); break;
+        case 1: fg_launch(k_tile_merge_parts<1>, g, b, 0, s, f); break;
+        case 0: fg_launch(k_tile_merge_parts<0>, g, b, 0, s, f); break;
+        default: fg_launch(k_tile_merge_parts<-1>, g, b, 0, s, f); break;
+    }
+    return hipGetLastError();
+}
+
+// Materialize a tile pass's lane into a regular narrow staged pass. Workgroup (bucket, y) takes
+// kTileMatThreads tiles of the bucket's column (a hot key's bucket is spread over the whole
+// column's workgroups, not one): its fragments' lengths scanned into a flat record sequence, the
+// records' regions at `bits` counted in LDS. COUNT: the counts added into hist[region] (zeroed by
+// the host). SCATTER: each region's block reserved at once from cursor[region] (the exclusive
+// scan of the counts, copied), the records read again and written at their rank (order inside a
+// region is immaterial).
+constexpr int kTileMatThreads = 256;
+template <bool SCATTER>
+__global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32_t bits, uint32_t* hist,
+                                                              uint32_t* cursor, void* out) {
+    constexpr int T = kTileMatThreads;
+    __shared__ uint32_t s_c[kTileMaxSub];
+    __shared__ uint32_t s_pre[T + 1];
+    __shared__ uint32_t s_wave[T / 64];
+    const int item = blockIdx.x;
+    const int sub = bits - tp.bits;
+    const int nsub = 1 << (kTileBits + sub);   // (host: kTileBits + sub <= 6)
+    const int r_lo = item << (kTileBits + sub);
+    const int tid = threadIdx.x;
+    if (tid < nsub) s_c[tid] = 0u;
+    const uint32_t* col = tp.dt + (int64_t)((tp.lane << (tp.bits - kTileBits)) | item) * tp.nt;
+    const int t = (int)blockIdx.y * T + tid;
+    const uint32_t x = t < tp.nt ? gbl(col)[t] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_exclusive_scan(x >> 16, s_wave, &total);   // (synchronizes: s_c is zeroed)
+    s_pre[tid] = ex;
+    if (tid == 0) s_pre[T] = total;
+    __syncthreads();
+    if (total == 0) return;   // (uniform)
+    // record i of the flat sequence: its tile (the last prefix <= i) and batch index
+    auto rec_at = [&](uint32_t i) -> uint64_t {
+        int lo = 0, hi = T;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_pre[mid] <= i) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t xt = gbl(col)[(int)blockIdx.y * T + lo];
+        return ((uint64_t)blockIdx.y * T + lo) * kTileRecs + (xt & 0xffffu) + (i - s_pre[lo]);
+    };
+    for (uint32_t i = tid; i < total; i += T) {
+        const Rec12 r = ld_rec12(tp.rec, rec_at(i));
+        const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
+        atomicAdd(&s_c[region - r_lo], 1u);
+    }
+    __syncthreads();
+    if (!SCATTER) {
+        if (tid < nsub && s_c[tid]) atomicAdd(&hist[r_lo + tid], s_c[tid]);
+        return;
+    }
+    if (tid < nsub && s_c[tid]) s_c[tid] = atomicAdd(&cursor[r_lo + tid], s_c[tid]);
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += T) {
+        const Rec12 r = ld_rec12(tp.rec, rec_at(i));
+        const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
+        const uint32_t pos = atomicAdd(&s_c[region - r_lo], 1u);
+        st_rec12(out, pos, (int64_t)(int32_t)r.k, rec12_val(r));
+    }
+}
+
+hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s) {
+    if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0) return hipErrorInvalidValue;   // (kTileMaxSub regions per bucket)
+    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatThreads - 1) / kTileMatThreads));
+    fg_launch(k_tile_mat<false>, g, dim3(kTileMatThreads), 0, s, tp, bits, hist, (uint32_t*)nullptr, (void*)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, uint32_t* cursor, void* out_rec, hipStream_t s) {
+    if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0) return hipErrorInvalidValue;
+    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatThreads - 1) / kTileMatThreads));
+    fg_launch(k_tile_mat<true>, g, dim3(kTileMatThreads), 0, s, tp, bits, (uint32_t*)nullptr, cursor, out_rec);
     return hipGetLastError();
 }
 

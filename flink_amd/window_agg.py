@@ -502,11 +502,11 @@ class WindowAggOperator:
 
     def kernel_stats(self) -> dict:
         """{kernel: dict(launches, total_ms, records, rows)} (needs kernel_timing=True)."""
-        arr = (L.FgKernelStat * 16)()
+        arr = (L.FgKernelStat * 32)()
         n = C.c_int32()
-        L.check(self._lib.fg_kernel_stats(self._h, arr, 16, C.byref(n)), self._h)
+        L.check(self._lib.fg_kernel_stats(self._h, arr, 32, C.byref(n)), self._h)
         return {arr[i].name.decode(): dict(launches=arr[i].launches, total_ms=arr[i].total_ms,
-                                           records=arr[i].records, rows=arr[i].rows) for i in range(n.value)}
+                                           records=arr[i].records, rows=arr[i].rows) for i in range(min(n.value, 32))}
 
     def set_kernel_timing(self, classes=None):
         """Time only the named kernel classes (names of kernel_stats); None: all."""

@@ -1,0 +1,45 @@
+"""Skewed tile passes (Zipf hot keys) on the tile path: the split fire (k_tile_plan ->
+k_tile_fire over chunk items with hot-key wave pre-combine -> k_tile_merge_parts) against the
+oracle, and the parallel materialize of a skewed lane (checkpoint). A hot key's bucket above
+max(kTileChunk, 4x the lane's mean) records is cut into chunk items over its tiles
+(fg_kernels.h TileSplit); results must equal the oracle's exactly as any other fire's
+(bit-exact keys, counts, i64 sums, MIN / MAX; f64 sums within the north_star tolerance)."""
+import pytest
+
+from tests.test_gpu_parity import cfg_of, drive_both
+
+pytestmark = pytest.mark.gpu
+
+# slices of 4M records (rate 4000 / ms, 1 s windows): the top Zipf(1.1) key holds ~11 % of them,
+# several kTileChunk chunks; jitter + delay leave a slice's records in 2-3 tile passes
+BIG = dict(n=12_000_000, keys=1_000_000, batch=2_000_000, rate_per_ms=4_000, zipf=1.1)
+
+CASES = [
+    ("tumble_f64_inorder", cfg_of("tumble", 1000), dict(BIG, delay=0, jitter=0)),
+    ("tumble_f64_ooo_passes", cfg_of("tumble", 1000), dict(BIG, delay=400, jitter=700)),
+    ("tumble_i64_hot13", cfg_of("tumble", 1000, vt="i64"), dict(BIG, zipf=1.3, delay=200, jitter=300)),
+    ("tumble_i64_min", dict(cfg_of("tumble", 1000, vt="i64"), aggs=("count_star", "count", "min")),
+     dict(BIG, delay=200, jitter=300)),
+    ("tumble_f64_max", dict(cfg_of("tumble", 1000), aggs=("count_star", "count", "max")),
+     dict(BIG, delay=0, jitter=0)),
+    ("ds_tumble_f64", cfg_of("tumble", 1000, mode="datastream"), dict(BIG, delay=100, jitter=200)),
+    ("tumble_f64_snapshot", cfg_of("tumble", 1000), dict(BIG, delay=400, jitter=700, snapshot_at=3)),
+]
+
+
+@pytest.mark.parametrize("name,cfg,kw", CASES, ids=[c[0] for c in CASES])
+def test_zipf_split_fire_parity(oracle_mod, name, cfg, kw):
+    ks = {}
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    assert ks.get("tile_split_fire", {}).get("launches", 0) > 0, ks
+    if "snapshot_at" not in kw:   # (the skewed passes stayed on the tiles; a snapshot materializes them)
+        assert ks.get("merge_heavy", {}).get("launches", 0) == 0, ks
+
+
+def test_zipf_split_off_takes_heavy_path(oracle_mod, monkeypatch):
+    """FG_TILE_SPLIT=0: a skewed tile pass is staged again by the two-pass partition (heavy path)."""
+    monkeypatch.setenv("FG_TILE_SPLIT", "0")
+    ks = {}
+    drive_both(oracle_mod, cfg_of("tumble", 1000), kstats=ks, **dict(BIG, n=6_000_000, delay=0, jitter=0))
+    assert ks.get("tile_split_fire", {}).get("launches", 0) == 0, ks
+    assert ks.get("merge_heavy", {}).get("launches", 0) > 0, ks
