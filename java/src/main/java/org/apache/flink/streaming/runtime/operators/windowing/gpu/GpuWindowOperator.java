@@ -1,35 +1,58 @@
 /*
- * DataStream keyBy(f0).window(Tumbling|SlidingEventTimeWindows).sum(1) on Tuple2<Long, Long>
- * (WindowedStream.sum -> SumAggregator, WindowedStream.java:671-674,891-893) as one operator
+ * DataStream keyBy(f0).window(Tumbling|SlidingEventTimeWindows).sum / min / max(1) (and minBy /
+ * maxBy, which give the same Tuple2) on Tuple2<Long, Long> or Tuple2<Long, Double> as one operator
  * backed by the GPU engine in FG_MODE_DATASTREAM. Replaces WindowOperator + EventTimeTrigger +
- * HeapReducingState (WindowOperator.java:300-503, built by WindowOperatorBuilder.java:150-172):
+ * HeapReducingState (WindowOperator.java:300-503, built by WindowOperatorBuilder.java:150-172 from
+ * WindowedStream.sum / min / max, WindowedStream.java:671-850), with the reference's keyed-state
+ * layout on both sides of a checkpoint:
  *
  *   processElement     -> (key, timestamp, value) appended to direct buffers; a full micro-batch
  *                         goes to fg_add_batch
  *   processWatermark   -> the pending batch, fg_advance_progress: every window whose
- *                         maxTimestamp the watermark passes fires with its SumAggregator result,
- *                         emitted with timestamp window.maxTimestamp() (emitWindowContents
- *                         :574-579) before the watermark is forwarded
- *   prepareSnapshotPreBarrier -> pending batch + fg_flush; snapshotState writes the resident
- *                         (key, window) sums into keyed state "gpu-window-contents"
- *   allowedLateness    -> GpuWindowAggSpec.allowedLatenessMs (fg_config.allowed_lateness_ms)
+ *                         maxTimestamp the watermark passes fires with the aggregator's result,
+ *                         emitted at window.maxTimestamp() (emitWindowContents :574-579), before
+ *                         the watermark is forwarded
+ *   prepareSnapshotPreBarrier -> "window-contents": the ReducingState of the input type in the TimeWindow
+ *                         namespace (WindowOperatorBuilder.java:71,165-167) -- one reduced Tuple2 per
+ *                         (key, window), a sliding window's value the reduce of its slices -- and
+ *                         "window-timers" (WindowOperator.java:225): the trigger timer of every
+ *                         window not fired yet, the cleanup timer at maxTimestamp + allowedLateness
+ *                         (:630-642,669-673). A CPU WindowOperator restores this image.
+ *   initializeState    -> an image of the same layout (the CPU operator's or this one's) is held as
+ *                         restored window contents; the engine restarts at Long.MIN_VALUE (as the
+ *                         restored timer service does). A fired GPU row of a restored (key, window)
+ *                         is reduced with the restored value; a restored window whose trigger timer
+ *                         is pending and that fired no GPU row emits its restored value alone.
  *
+ * The timers this operator registers are for the image only: the engine fires the windows, so
+ * onEventTime / onProcessingTime do nothing. flink_amd/datastream.py is the Python mirror of this
+ * class, tested against the oracle in tests/test_gpu_datastream_state.py.
  * The late-drop count feeds numLateRecordsDropped (WindowOperator.java:222).
  */
 package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
-import org.apache.flink.api.common.state.ValueState;
-import org.apache.flink.api.common.state.ValueStateDescriptor;
-import org.apache.flink.api.common.typeutils.base.LongSerializer;
+import org.apache.flink.api.common.functions.ReduceFunction;
+import org.apache.flink.api.common.state.ReducingStateDescriptor;
+import org.apache.flink.api.common.typeinfo.BasicTypeInfo;
+import org.apache.flink.api.common.typeinfo.TypeInformation;
 import org.apache.flink.api.java.tuple.Tuple2;
+import org.apache.flink.api.java.typeutils.TupleTypeInfo;
 import org.apache.flink.metrics.Counter;
 import org.apache.flink.runtime.state.CheckpointableKeyedStateBackend;
 import org.apache.flink.runtime.state.KeyGroupRange;
-import org.apache.flink.runtime.state.StateSnapshotContext;
+import org.apache.flink.runtime.state.StateInitializationContext;
+import org.apache.flink.runtime.state.internal.InternalReducingState;
+import org.apache.flink.streaming.api.functions.aggregation.AggregationFunction;
+import org.apache.flink.streaming.api.functions.aggregation.ComparableAggregator;
+import org.apache.flink.streaming.api.functions.aggregation.SumAggregator;
 import org.apache.flink.streaming.api.operators.AbstractStreamOperator;
+import org.apache.flink.streaming.api.operators.InternalTimer;
+import org.apache.flink.streaming.api.operators.InternalTimerService;
 import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
 import org.apache.flink.streaming.api.operators.TimestampedCollector;
+import org.apache.flink.streaming.api.operators.Triggerable;
 import org.apache.flink.streaming.api.watermark.Watermark;
+import org.apache.flink.streaming.api.windowing.windows.TimeWindow;
 import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
 import org.apache.flink.table.runtime.operators.window.gpu.FgConfig;
 import org.apache.flink.table.runtime.operators.window.gpu.FlinkGpu;
@@ -37,30 +60,115 @@ import org.apache.flink.table.runtime.operators.window.gpu.GpuWindowAggSpec;
 
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.util.ArrayList;
+import java.util.Arrays;
+import java.util.HashMap;
+import java.util.HashSet;
+import java.util.Iterator;
 import java.util.List;
+import java.util.Map;
+import java.util.Set;
+import java.util.TreeMap;
 import java.util.stream.Collectors;
 
-/** keyBy(f0).window(...).sum(1) over Tuple2<Long, Long> on the GPU engine. */
-public final class GpuWindowOperator extends AbstractStreamOperator<Tuple2<Long, Long>>
-        implements OneInputStreamOperator<Tuple2<Long, Long>, Tuple2<Long, Long>> {
-    private static final long serialVersionUID = 1L;
-    private static final String STATE_NAME = "gpu-window-contents";
+/** keyBy(f0).window(...).sum / min / max(1) over Tuple2<Long, V> (V = Long or Double) on the GPU. */
+public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Long, V>>
+        implements OneInputStreamOperator<Tuple2<Long, V>, Tuple2<Long, V>>, Triggerable<Long, TimeWindow> {
+    private static final long serialVersionUID = 2L;
+    private static final String WINDOW_STATE_NAME = "window-contents";   // WindowOperatorBuilder.java:71
+    private static final String WINDOW_TIMERS_NAME = "window-timers";    // WindowOperator.java:225
+
+    /** The WindowedStream aggregation: sum(1), min(1) / minBy(1), max(1) / maxBy(1). */
+    public enum Aggregation {
+        SUM,
+        MIN,
+        MAX
+    }
 
     private final GpuWindowAggSpec spec;
+    private final TypeInformation<Tuple2<Long, V>> inputType;
+    private final Aggregation aggregation;
+    private final boolean isDouble;
+    private final boolean purging;
 
     private transient long handle;
     private transient ByteBuffer keys, timestamps, vals;
     private transient int count;
     private transient long droppedSeen;
+    private transient long currentWatermark;
     private transient Counter numLateRecordsDropped;
-    private transient TimestampedCollector<Tuple2<Long, Long>> collector;
+    private transient TimestampedCollector<Tuple2<Long, V>> collector;
+    private transient ReduceFunction<Tuple2<Long, V>> reducer;
+    private transient InternalReducingState<Long, TimeWindow, Tuple2<Long, V>> windowState;
+    private transient InternalTimerService<TimeWindow> timers;
+    /** Restored window contents by window end (initializeState), until their cleanup time. */
+    private transient TreeMap<Long, Restored> restored;
 
-    /** spec: mode DATASTREAM, TUMBLE or HOP (sliding), valType I64, aggs {SUM} */
-    public GpuWindowOperator(GpuWindowAggSpec spec) {
+    /** A restored window: its keys (sorted), value bits, trigger pending, still holding state. */
+    private static final class Restored {
+        final TimeWindow window;
+        final long[] keys;
+        final long[] values;
+        final boolean[] pending;
+        final boolean[] alive;
+
+        Restored(TimeWindow window, long[] keys, long[] values, boolean[] pending) {
+            this.window = window;
+            this.keys = keys;
+            this.values = values;
+            this.pending = pending;
+            this.alive = new boolean[keys.length];
+            Arrays.fill(alive, true);
+        }
+    }
+
+    /**
+     * spec: windowKind TUMBLE or HOP (sliding), sizeMs / slideMs / offsetMs, allowedLatenessMs,
+     * flags FgConfig.FLAG_PURGING_TRIGGER for PurgingTrigger.of(EventTimeTrigger).
+     */
+    public GpuWindowOperator(
+            GpuWindowAggSpec spec, TypeInformation<Tuple2<Long, V>> inputType, Aggregation aggregation) {
+        TypeInformation<?> f1 = ((TupleTypeInfo<?>) inputType).getTypeAt(1);
+        if (!f1.equals(BasicTypeInfo.LONG_TYPE_INFO) && !f1.equals(BasicTypeInfo.DOUBLE_TYPE_INFO)) {
+            throw new IllegalArgumentException("GPU window aggregation of a Long or Double field, got " + f1);
+        }
+        this.isDouble = f1.equals(BasicTypeInfo.DOUBLE_TYPE_INFO);
         spec.mode = FgConfig.MODE_DATASTREAM;
-        spec.valType = FgConfig.VAL_I64;
-        spec.aggs = new int[] {FgConfig.AGG_SUM};
+        spec.valType = isDouble ? FgConfig.VAL_F64 : FgConfig.VAL_I64;
+        int agg =
+                aggregation == Aggregation.SUM
+                        ? FgConfig.AGG_SUM
+                        : aggregation == Aggregation.MIN ? FgConfig.AGG_MIN : FgConfig.AGG_MAX;
+        spec.aggs = new int[] {FgConfig.AGG_COUNT_STAR, agg};
         this.spec = spec;
+        this.inputType = inputType;
+        this.aggregation = aggregation;
+        this.purging = (spec.flags & FgConfig.FLAG_PURGING_TRIGGER) != 0;
+    }
+
+    @Override
+    public void initializeState(StateInitializationContext context) throws Exception {
+        super.initializeState(context);
+        // the reference's reduce function and state: WindowedStream.sum / min / max build
+        // exactly these aggregators (WindowedStream.java:671-850)
+        reducer =
+                aggregation == Aggregation.SUM
+                        ? new SumAggregator<>(1, inputType, getExecutionConfig())
+                        : new ComparableAggregator<>(
+                                1,
+                                inputType,
+                                aggregation == Aggregation.MIN
+                                        ? AggregationFunction.AggregationType.MIN
+                                        : AggregationFunction.AggregationType.MAX,
+                                getExecutionConfig());
+        ReducingStateDescriptor<Tuple2<Long, V>> desc =
+                new ReducingStateDescriptor<>(
+                        WINDOW_STATE_NAME, reducer, inputType.createSerializer(getExecutionConfig()));
+        @SuppressWarnings("unchecked")
+        InternalReducingState<Long, TimeWindow, Tuple2<Long, V>> st =
+                (InternalReducingState<Long, TimeWindow, Tuple2<Long, V>>)
+                        getOrCreateKeyedState(new TimeWindow.Serializer(), desc);
+        windowState = st;
     }
 
     @Override
@@ -68,6 +176,7 @@ public final class GpuWindowOperator extends AbstractStreamOperator<Tuple2<Long,
         super.open();
         collector = new TimestampedCollector<>(output);
         numLateRecordsDropped = metrics.counter("numLateRecordsDropped");
+        timers = getInternalTimerService(WINDOW_TIMERS_NAME, new TimeWindow.Serializer(), this);
         KeyGroupRange range =
                 ((CheckpointableKeyedStateBackend<?>) getKeyedStateBackend()).getKeyGroupRange();
         handle =
@@ -83,18 +192,40 @@ public final class GpuWindowOperator extends AbstractStreamOperator<Tuple2<Long,
         keys = direct(8L * spec.batchRecords);
         timestamps = direct(8L * spec.batchRecords);
         vals = direct(8L * spec.batchRecords);
-        restore();
+        currentWatermark = Long.MIN_VALUE;
+        restored = new TreeMap<>();
+        restoreImage();
     }
 
     private static ByteBuffer direct(long bytes) {
         return ByteBuffer.allocateDirect((int) Math.max(bytes, 8)).order(ByteOrder.nativeOrder());
     }
 
+    private long bitsOf(V v) {
+        return isDouble ? Double.doubleToRawLongBits((Double) v) : (Long) v;
+    }
+
+    @SuppressWarnings("unchecked")
+    private V valueOf(long bits) {
+        return (V) (isDouble ? (Object) Double.longBitsToDouble(bits) : (Object) bits);
+    }
+
+    private long reduceBits(long a, long b) throws Exception {   // value1 = a (the earlier value)
+        return bitsOf(reducer.reduce(Tuple2.of(0L, valueOf(a)), Tuple2.of(0L, valueOf(b))).f1);
+    }
+
+    /** WindowOperator.cleanupTime (:669-673). */
+    private long cleanupTime(long end) {
+        long maxTs = end - 1;
+        long c = maxTs + spec.allowedLatenessMs;
+        return c >= maxTs ? c : Long.MAX_VALUE;
+    }
+
     @Override
-    public void processElement(StreamRecord<Tuple2<Long, Long>> element) throws Exception {
+    public void processElement(StreamRecord<Tuple2<Long, V>> element) throws Exception {
         keys.putLong(8 * count, element.getValue().f0);
         timestamps.putLong(8 * count, element.getTimestamp());
-        vals.putLong(8 * count, element.getValue().f1);
+        vals.putLong(8 * count, bitsOf(element.getValue().f1));
         if (++count == spec.batchRecords) {
             flushBatch();
         }
@@ -107,20 +238,64 @@ public final class GpuWindowOperator extends AbstractStreamOperator<Tuple2<Long,
         }
     }
 
+    private void emit(long key, long end, long bits) {
+        collector.setAbsoluteTimestamp(end - 1);   // window.maxTimestamp()
+        collector.collect(Tuple2.of(key, valueOf(bits)));
+    }
+
     @Override
     public void processWatermark(Watermark mark) throws Exception {
         flushBatch();
-        ByteBuffer[] cols = new ByteBuffer[6];
-        long n = FlinkGpu.advanceProgress(handle, mark.getTimestamp(), cols);
+        long wm = mark.getTimestamp();
+        ByteBuffer[] cols = new ByteBuffer[7];
+        long n = FlinkGpu.advanceProgress(handle, wm, cols);
         for (ByteBuffer c : cols) {
             if (c != null) {
                 c.order(ByteOrder.nativeOrder());
             }
         }
-        for (int i = 0; i < n; i++) {   // Tuple2(key, sum) at window.maxTimestamp()
-            collector.setAbsoluteTimestamp(cols[5].getLong(8 * i));
-            collector.collect(Tuple2.of(cols[0].getLong(8 * i), cols[3].getLong(8 * i)));
+        // columns: key, window_start, window_end, COUNT(*), the aggregate, null mask, rowtime
+        for (int i = 0; i < n; i++) {
+            long key = cols[0].getLong(8 * i);
+            long end = cols[2].getLong(8 * i);
+            long bits = cols[4].getLong(8 * i);
+            Restored r = restored.get(end);
+            if (r != null) {
+                int at = Arrays.binarySearch(r.keys, key);
+                if (at >= 0 && r.alive[at]) {
+                    bits = reduceBits(r.values[at], bits);
+                    r.pending[at] = false;
+                    if (purging) {
+                        r.alive[at] = false;
+                    }
+                }
+            }
+            emit(key, end, bits);
         }
+        for (Iterator<Map.Entry<Long, Restored>> it = restored.entrySet().iterator(); it.hasNext(); ) {
+            Map.Entry<Long, Restored> e = it.next();
+            long end = e.getKey();
+            Restored r = e.getValue();
+            if (end - 1 <= wm) {   // the trigger: pending restored contents without a GPU row
+                for (int j = 0; j < r.keys.length; j++) {
+                    if (r.pending[j] && r.alive[j]) {
+                        emit(r.keys[j], end, r.values[j]);
+                        if (purging) {
+                            r.alive[j] = false;
+                        }
+                    }
+                    r.pending[j] = false;
+                }
+            }
+            boolean any = false;
+            for (boolean a : r.alive) {
+                any |= a;
+            }
+            if (cleanupTime(end) <= wm || !any) {
+                it.remove();
+            }
+        }
+        currentWatermark = Math.max(currentWatermark, wm);
         long dropped = FlinkGpu.lateDropped(handle);
         numLateRecordsDropped.inc(dropped - droppedSeen);
         droppedSeen = dropped;
@@ -128,76 +303,133 @@ public final class GpuWindowOperator extends AbstractStreamOperator<Tuple2<Long,
     }
 
     @Override
-    public void prepareSnapshotPreBarrier(long checkpointId) throws Exception {
-        flushBatch();
-        FlinkGpu.flush(handle);
-    }
-
-    private ValueState<long[]> stateFor(long window) throws Exception {
-        return getKeyedStateBackend()
-                .getPartitionedState(
-                        window,
-                        LongSerializer.INSTANCE,
-                        new ValueStateDescriptor<>(STATE_NAME, long[].class));
+    public void onEventTime(InternalTimer<Long, TimeWindow> timer) {
+        // the engine fires and cleans the windows; the timers describe them for the image only
     }
 
     @Override
-    public void snapshotState(StateSnapshotContext context) throws Exception {
-        List<Tuple2<Object, Long>> old =
-                getKeyedStateBackend().<Long>getKeysAndNamespaces(STATE_NAME)
-                        .map(t -> Tuple2.<Object, Long>of(t.f0, t.f1))
+    public void onProcessingTime(InternalTimer<Long, TimeWindow> timer) {}
+
+    /**
+     * The pending batch and the engine's buffer flushed, then the image written into keyed state
+     * and the timer service here, before the barrier: StreamOperatorStateHandler.snapshotState
+     * writes the timers to raw keyed state before it calls the operator's snapshotState
+     * (StreamOperatorStateHandler.java:198-218).
+     */
+    @Override
+    public void prepareSnapshotPreBarrier(long checkpointId) throws Exception {
+        flushBatch();
+        FlinkGpu.flush(handle);
+        writeImage();
+    }
+
+    private void writeImage() throws Exception {
+        // the previous image goes: every (key, window) of the state is written again below
+        List<Tuple2<Long, TimeWindow>> old =
+                getKeyedStateBackend().<TimeWindow>getKeysAndNamespaces(WINDOW_STATE_NAME)
+                        .map(t -> Tuple2.of((Long) t.f0, t.f1))
                         .collect(Collectors.toList());
-        for (Tuple2<Object, Long> kn : old) {
+        for (Tuple2<Long, TimeWindow> kn : old) {
             setCurrentKey(kn.f0);
-            stateFor(kn.f1).clear();
+            windowState.setCurrentNamespace(kn.f1);
+            windowState.clear();
         }
         ByteBuffer[] cols = new ByteBuffer[7];
-        long[] wm = new long[1];
-        long n = FlinkGpu.snapshotState(handle, cols, wm);
+        long[] wmOut = new long[1];
+        long n = FlinkGpu.snapshotState(handle, cols, wmOut);
         for (ByteBuffer c : cols) {
             if (c != null) {
                 c.order(ByteOrder.nativeOrder());
             }
         }
-        for (int i = 0; i < n; i++) {   // namespace: the slice end; value: the accumulators
-            setCurrentKey(cols[0].getLong(8 * i));
-            stateFor(cols[1].getLong(8 * i))
-                    .update(
-                            new long[] {
-                                cols[2].getLong(8 * i),
-                                cols[3].getLong(8 * i),
-                                cols[4].getLong(8 * i),
-                                wm[0]
-                            });
+        long wm = currentWatermark;
+        long slide = spec.windowKind == FgConfig.TUMBLE ? spec.sizeMs : spec.slideMs;
+        long perSlice = spec.sizeMs / slide;
+        // per (key, window): the restored value first (value1 of the reduce), then every slice
+        Map<Long, Map<Long, Long>> contents = new HashMap<>();   // window end -> key -> value bits
+        for (Map.Entry<Long, Restored> e : restored.entrySet()) {
+            Restored r = e.getValue();
+            Map<Long, Long> w = contents.computeIfAbsent(e.getKey(), x -> new HashMap<>());
+            for (int j = 0; j < r.keys.length; j++) {
+                if (r.alive[j]) {
+                    w.put(r.keys[j], r.values[j]);
+                }
+            }
         }
-        super.snapshotState(context);
+        // state columns: key, slice_end, cnt_star, cnt_val, the value accumulator
+        for (int i = 0; i < n; i++) {
+            long key = cols[0].getLong(8 * i);
+            long sliceEnd = cols[1].getLong(8 * i);
+            long bits = cols[4].getLong(8 * i);
+            for (long j = 0; j < perSlice; j++) {
+                long end = sliceEnd + j * slide;
+                if (cleanupTime(end) <= wm || (purging && end - 1 <= wm)) {
+                    continue;   // cleared (clearAllState), or fired and purged
+                }
+                Map<Long, Long> w = contents.computeIfAbsent(end, x -> new HashMap<>());
+                Long prev = w.get(key);
+                w.put(key, prev == null ? bits : reduceBits(prev, bits));
+            }
+        }
+        for (Map.Entry<Long, Map<Long, Long>> e : contents.entrySet()) {
+            long end = e.getKey();
+            TimeWindow window = new TimeWindow(end - spec.sizeMs, end);
+            long cleanup = cleanupTime(end);
+            for (Map.Entry<Long, Long> kv : e.getValue().entrySet()) {
+                setCurrentKey(kv.getKey());
+                windowState.setCurrentNamespace(window);
+                windowState.updateInternal(Tuple2.of(kv.getKey(), valueOf(kv.getValue())));
+                if (window.maxTimestamp() > wm) {   // EventTimeTrigger.onElement's timer
+                    timers.registerEventTimeTimer(window, window.maxTimestamp());
+                }
+                if (cleanup != Long.MAX_VALUE) {   // registerCleanupTimer
+                    timers.registerEventTimeTimer(window, cleanup);
+                }
+            }
+        }
     }
 
-    private void restore() throws Exception {
-        List<Tuple2<Object, Long>> entries =
-                getKeyedStateBackend().<Long>getKeysAndNamespaces(STATE_NAME)
-                        .map(t -> Tuple2.<Object, Long>of(t.f0, t.f1))
+    /** initializeState's image: the (key, window) contents and which triggers are pending. */
+    private void restoreImage() throws Exception {
+        List<Tuple2<Long, TimeWindow>> entries =
+                getKeyedStateBackend().<TimeWindow>getKeysAndNamespaces(WINDOW_STATE_NAME)
+                        .map(t -> Tuple2.of((Long) t.f0, t.f1))
                         .collect(Collectors.toList());
         if (entries.isEmpty()) {
             return;
         }
-        int n = entries.size();
-        ByteBuffer[] c = new ByteBuffer[5];
-        for (int j = 0; j < 5; j++) {
-            c[j] = direct(8L * n);
+        // the pending trigger timers: (key, window) of every event-time timer at maxTimestamp
+        Set<Tuple2<Long, TimeWindow>> pending = new HashSet<>();
+        timers.forEachEventTimeTimer(
+                (window, ts) -> {
+                    if (ts == window.maxTimestamp()) {
+                        pending.add(Tuple2.of((Long) getCurrentKey(), window));
+                    }
+                });
+        Map<TimeWindow, List<long[]>> byWindow = new HashMap<>();
+        for (Tuple2<Long, TimeWindow> kn : entries) {
+            setCurrentKey(kn.f0);
+            windowState.setCurrentNamespace(kn.f1);
+            Tuple2<Long, V> v = windowState.get();
+            if (v == null) {
+                continue;
+            }
+            byWindow.computeIfAbsent(kn.f1, x -> new ArrayList<>())
+                    .add(new long[] {kn.f0, bitsOf(v.f1), pending.contains(kn) ? 1 : 0});
         }
-        long timerWm = Long.MIN_VALUE;
-        for (int i = 0; i < n; i++) {
-            setCurrentKey(entries.get(i).f0);
-            long[] acc = stateFor(entries.get(i).f1).value();
-            c[0].putLong(8 * i, (Long) entries.get(i).f0);
-            c[1].putLong(8 * i, entries.get(i).f1);
-            c[2].putLong(8 * i, acc[0]);
-            c[3].putLong(8 * i, acc[1]);
-            c[4].putLong(8 * i, acc[2]);
-            timerWm = acc[3];
+        for (Map.Entry<TimeWindow, List<long[]>> e : byWindow.entrySet()) {
+            List<long[]> l = e.getValue();
+            l.sort((a, b) -> Long.compare(a[0], b[0]));
+            long[] k = new long[l.size()];
+            long[] v = new long[l.size()];
+            boolean[] p = new boolean[l.size()];
+            for (int j = 0; j < l.size(); j++) {
+                k[j] = l.get(j)[0];
+                v[j] = l.get(j)[1];
+                p[j] = l.get(j)[2] != 0;
+            }
+            restored.put(e.getKey().getEnd(), new Restored(e.getKey(), k, v, p));
         }
-        FlinkGpu.restore(handle, n, c[0], c[1], c[2], c[3], c[4], null, null, timerWm);
     }
 
     @Override

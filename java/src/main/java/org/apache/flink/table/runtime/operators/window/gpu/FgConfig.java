@@ -54,6 +54,7 @@ public final class FgConfig {
     public static final int FLAG_LOCAL_PARTIALS = 2;
     public static final int FLAG_PROCTIME = 4;
     public static final int FLAG_WINDOWED = 8;
+    public static final int FLAG_PURGING_TRIGGER = 16;
 
     private FgConfig() {}
 

@@ -935,6 +935,69 @@ or_op* or_restore_copy(const or_op* src) {
     return op;   /* progress, next trigger and timer watermark back at Long.MIN_VALUE */
 }
 
+/* DataStream WindowOperator keyed state as its heap backend holds it: "window-contents" (one
+ * reduced value per (key, TimeWindow), WindowOperatorBuilder.java:71,165-167) and the
+ * "window-timers" queue (WindowOperator.java:225; trigger timers at maxTimestamp, cleanup timers
+ * at maxTimestamp + allowedLateness, :630-642). or_ds_export_state writes per entry the key, the
+ * window end, COUNT(*) and the SUM / MIN / MAX bits of the value field (i64, or f64 bits); the
+ * arrays hold or_state_entries() entries. or_export_timers: or_pending_timers() timers. */
+int64_t or_ds_export_state(const or_op* op, int64_t* key, int64_t* end, int64_t* cnt, int64_t* sum, int64_t* mn,
+                           int64_t* mx) {
+    int64_t j = 0;
+    const int f = op->cfg.val_type == OR_VAL_F64;
+    for (int64_t i = 0; i < op->state.cap; i++) {
+        if (!op->state.used[i]) continue;
+        const or_acc* a = &op->accs[op->state.v[i]];
+        key[j] = op->state.ka[i];
+        end[j] = op->state.kb[i];
+        cnt[j] = a->cnt_star;
+        if (f) {
+            memcpy(&sum[j], &a->sum_d, 8);
+            memcpy(&mn[j], &a->min_d, 8);
+            memcpy(&mx[j], &a->max_d, 8);
+        } else {
+            sum[j] = a->sum_i;
+            mn[j] = a->min_i;
+            mx[j] = a->max_i;
+        }
+        j++;
+    }
+    return j;
+}
+int64_t or_export_timers(const or_op* op, int64_t* key, int64_t* ns, int64_t* ts) {
+    for (int64_t i = 0; i < op->heap_n; i++) {
+        key[i] = op->heap[i].key;
+        ns[i] = op->heap[i].ns;
+        ts[i] = op->heap[i].ts;
+    }
+    return op->heap_n;
+}
+/* A DataStream operator restored from such an image (initializeState of the heap backend): the
+ * reduced value of each (key, window) is all the reference keeps -- its COUNT(*) is taken as 1
+ * (never emitted by a DataStream aggregation); the timers are registered as they were. The
+ * timer watermark restarts at Long.MIN_VALUE (InternalTimerServiceImpl). */
+or_op* or_ds_import(const or_config* cfg, int64_t n, const int64_t* key, const int64_t* end, const int64_t* val,
+                    int64_t nt, const int64_t* tkey, const int64_t* tns, const int64_t* tts, char* err, int errlen) {
+    or_op* op = or_open(cfg, err, errlen);
+    if (!op) return NULL;
+    const int f = cfg->val_type == OR_VAL_F64;
+    for (int64_t i = 0; i < n; i++) {
+        or_acc* a = state_put(op, key[i], end[i]);
+        a->cnt_star = 1;
+        a->cnt_val = 1;
+        a->sum_null = 0;
+        if (f) {
+            memcpy(&a->sum_d, &val[i], 8);
+            memcpy(&a->min_d, &val[i], 8);
+            memcpy(&a->max_d, &val[i], 8);
+        } else {
+            a->sum_i = a->min_i = a->max_i = val[i];
+        }
+    }
+    for (int64_t i = 0; i < nt; i++) register_timer(op, tkey[i], tns[i], tts[i]);
+    return op;
+}
+
 int64_t or_num_rows(const or_op* op) { return op->rows_n; }
 const or_row* or_rows(const or_op* op) { return op->rows; }
 void or_clear_rows(or_op* op) { op->rows_n = 0; }

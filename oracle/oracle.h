@@ -99,6 +99,12 @@ void    or_clear_rows(or_op* op);
 int64_t or_late_dropped(const or_op* op);
 int64_t or_state_entries(const or_op* op);
 int64_t or_pending_timers(const or_op* op);
+/* DataStream WindowOperator keyed state image ("window-contents" + "window-timers") */
+int64_t or_ds_export_state(const or_op* op, int64_t* key, int64_t* end, int64_t* cnt, int64_t* sum, int64_t* mn,
+                           int64_t* mx);
+int64_t or_export_timers(const or_op* op, int64_t* key, int64_t* ns, int64_t* ts);
+or_op*  or_ds_import(const or_config* cfg, int64_t n, const int64_t* key, const int64_t* end, const int64_t* val,
+                     int64_t nt, const int64_t* tkey, const int64_t* tns, const int64_t* tts, char* err, int errlen);
 
 /* --- slice assigner restatement (SliceAssigners.java) ------------------------- */
 int64_t or_assign_slice_end(const or_op* op, int64_t ts);

@@ -153,6 +153,12 @@ def lib():
             C.POINTER(C.c_void_p), i64p, i64p,
         ]
         L.or_free.argtypes = [P]
+        L.or_ds_export_state.restype = C.c_int64
+        L.or_ds_export_state.argtypes = [P, P, P, P, P, P, P]
+        L.or_export_timers.restype = C.c_int64
+        L.or_export_timers.argtypes = [P, P, P, P]
+        L.or_ds_import.restype = P
+        L.or_ds_import.argtypes = [C.POINTER(Config), C.c_int64, P, P, P, C.c_int64, P, P, P, C.c_char_p, C.c_int]
         _lib = L
     return _lib
 
@@ -237,6 +243,41 @@ class OracleOperator:
         return OracleOperator(c.mode, c.kind, c.size, c.slide, c.offset, c.tz_offset_ms, c.val_type,
                               c.count_star_index, _handle=h, zone=self.zone, windowed=bool(c.windowed),
                               phase=c.phase)
+
+    # DataStream WindowOperator keyed state ("window-contents" + "window-timers")
+    def ds_state_image(self, agg: str = "sum") -> dict:
+        """The operator's heap-backend image: per (key, TimeWindow) the reduced value's field bits
+        (agg: the aggregator's field -- "sum", "min" or "max"), and every pending timer
+        (key, window end, timestamp)."""
+        L = lib()
+        n = self.state_entries
+        a = {k: np.zeros(n, dtype=np.int64) for k in ("key", "window_end", "cnt", "sum", "min", "max")}
+        L.or_ds_export_state(self._h, *(_ptr(a[k]) for k in ("key", "window_end", "cnt", "sum", "min", "max")))
+        nt = self.pending_timers
+        t = {k: np.zeros(nt, dtype=np.int64) for k in ("timer_key", "timer_window_end", "timer_ts")}
+        L.or_export_timers(self._h, *(_ptr(t[k]) for k in ("timer_key", "timer_window_end", "timer_ts")))
+        img = dict(key=a["key"], window_end=a["window_end"], window_start=a["window_end"] - self.cfg.size,
+                   value=a[agg])
+        img.update(t)
+        return img
+
+    @classmethod
+    def from_ds_state_image(cls, image: dict, kind=TUMBLE, size=1000, slide=0, offset=0, val_type=VAL_I64,
+                            allowed_lateness=0, purging=False) -> "OracleOperator":
+        """A DataStream operator restored from a ds_state_image-shaped image."""
+        cfg = Config(MODE_DATASTREAM, kind, size, slide, offset, 0, val_type, 0, 0, 0)
+        cfg.allowed_lateness = int(allowed_lateness)
+        cfg.purging = 1 if purging else 0
+        c = {k: np.ascontiguousarray(image[k], dtype=np.int64) for k in
+             ("key", "window_end", "value", "timer_key", "timer_window_end", "timer_ts")}
+        err = C.create_string_buffer(512)
+        h = lib().or_ds_import(C.byref(cfg), len(c["key"]), _ptr(c["key"]), _ptr(c["window_end"]), _ptr(c["value"]),
+                               len(c["timer_key"]), _ptr(c["timer_key"]), _ptr(c["timer_window_end"]),
+                               _ptr(c["timer_ts"]), err, 512)
+        if not h:
+            raise ValueError(err.value.decode())
+        return cls(MODE_DATASTREAM, kind, size, slide, offset, 0, val_type, 0, _handle=h,
+                   allowed_lateness=allowed_lateness, purging=purging)
 
     def take_rows(self) -> np.ndarray:
         L = lib()

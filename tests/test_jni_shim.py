@@ -38,7 +38,7 @@ def test_enum_values_match_header():
     k = _java_consts()
     for name in ("MODE_SQL", "MODE_DATASTREAM", "TUMBLE", "HOP", "CUMULATE", "VAL_NONE", "VAL_I64", "VAL_F64",
                  "AGG_COUNT_STAR", "AGG_COUNT", "AGG_SUM", "AGG_AVG", "AGG_SUM0", "AGG_MIN", "AGG_MAX",
-                 "FLAG_LOCAL_PARTIALS", "FLAG_PROCTIME", "FLAG_WINDOWED"):
+                 "FLAG_LOCAL_PARTIALS", "FLAG_PROCTIME", "FLAG_WINDOWED", "FLAG_PURGING_TRIGGER"):
         assert k[name] == getattr(L, name), name
 
 
