@@ -1154,7 +1154,7 @@ bool tile_fire_ok(const fg_handle* h, const Lane& ln, bool allow_skew = false) {
 bool tile_split_ok(const fg_handle* h) { return h->tile_split && (h->w.kind == TUMBLE || h->local); }
 
 // The split fire of a lane holding a skewed tile pass (fg_kernels.h TileSplit): k_tile_plan cuts
-// the buckets above max(kTileChunk, 4x the lane's mean) into chunk items, k_tile_fire aggregates
+// the buckets above max(kTileChunk, the lane's mean) into chunk items, k_tile_fire aggregates
 // every item (chunks into partial entries), k_tile_merge_parts merges each split bucket's chunks
 // into its rows. f is the job's TileFire (tile_job_params).
 int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f) {
@@ -1172,12 +1172,13 @@ int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f) {
     HIPCHK(h, h->sp_pcs.ensure(4 * (size_t)part_cap));
     HIPCHK(h, h->sp_pv.ensure(8 * (size_t)part_cap));
     HIPCHK(h, h->sp_bfail.ensure(4 * (size_t)nb));
-    HIPCHK(h, hipMemsetAsync(h->sp_n.p, 0, 16, h->stream));   // n_items, n_split, part_fill
+    HIPCHK(h, hipMemsetAsync(h->sp_n.p, 0, 16, h->stream));   // n_items, n_split, part_fill, next_item
     TileSplit& sp = f.sp;
     sp.items = h->sp_items.as<TileItem>();
     sp.n_items = h->sp_n.as<uint32_t>();
     sp.n_split = h->sp_n.as<uint32_t>() + 1;
     sp.part_fill = h->sp_n.as<uint32_t>() + 2;
+    sp.next_item = h->sp_n.as<uint32_t>() + 3;
     sp.max_items = (int32_t)max_items;
     sp.max_split = nb;
     sp.split_b = h->sp_split.as<int32_t>();

@@ -478,6 +478,7 @@ struct TileSplit {
     uint32_t* part_off;       // per chunk ordinal: first partial entry, entries (kChunkFailed: failed)
     uint32_t* part_n;
     uint32_t* part_fill;      // partial entries written (reservation counter)
+    uint32_t* next_item;      // the fire's dynamic item counter (zeroed with the counts)
     uint32_t part_cap;
     int32_t* p_key;           // partial entries: int32 key, COUNT(*), value bits (the LDS repr)
     uint32_t* p_cs;
@@ -495,7 +496,7 @@ struct TileFire {
     // items: the lane's buckets 0 .. (1 << (tbits - kTileBits)) - 1, or (retry) regions at
     // m.region_bits: m.retry_list[0 .. m.n_retry), or (split) sp.items[0 .. *sp.n_items)
     int32_t split;            // sp holds a plan (k_tile_plan): a skewed pass's fire
-    int32_t hot;              // pre-combine a wave's records of its first lane's key (skewed passes)
+    int32_t hot;              // split fire: pre-combine a wave's records of a hot key (SUM-family ops)
     TileSplit sp;
 };
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s);

@@ -3336,7 +3336,10 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
 // straight from the tiles, no staged pass 2). A region holding more than kRegionCap keys fails
 // the item like a full table: nothing is written or emitted and its regions are redone.
 // m.emit = 0: a flush (the table written, no rows).
-template <int VTC, bool TAB>   // TAB: source / destination tables (compiled out of the plain fire)
+// HOT (a skewed pass's split fire, SUM-family value ops): the insert pre-combines a wave's records of
+// a hot key; the plain fire keeps the one-probe-loop-per-record insert (A/B, round 5: 0.89 vs 1.08
+// ms per 100M records for the branch-free insert with a dummy slot)
+template <int VTC, bool TAB, bool HOT>   // TAB: source / destination tables (compiled out of the plain fire)
 __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     constexpr int T = kTileFireThreads, W = T / 64, S = kTileSlots;
     constexpr int kRounds = S / T + 1;   // + 1: the sentinel slot (thread 0)
@@ -3364,14 +3367,21 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     const int sub = p.region_bits - f.tbits;          // current region bits above the passes'
     const bool retry = p.retry_list != nullptr;
     const bool split = !TAB && f.split != 0;          // items planned by k_tile_plan (a skewed pass)
-    const bool hot = f.hot != 0 && vt >= 0 && vt <= 2;   // (SUM-family value ops: pre-combine hot keys)
+    __shared__ int s_item;   // split: the item fetched by workgroup (dynamic: chunk items vary in size)
     const int NI = retry ? p.n_retry : split ? (int)*gbl(f.sp.n_items) : 1 << (f.tbits - kTileBits);
     const int G = gridDim.x;
     const bool xcd = !retry && !split && G % 8 == 0;  // consecutive buckets on one XCD (shared L2 lines)
     for (int k = 0;; k++) {
         const int b = (int)blockIdx.x;
-        const int x = xcd ? k * G + (b % 8) * (G / 8) + b / 8 : b + k * G;
-        if (k * G >= NI) break;
+        int x = xcd ? k * G + (b % 8) * (G / 8) + b / 8 : b + k * G;
+        if (split) {   // (s_item's previous value was read before this iteration's barriers)
+            if (tid == 0) s_item = (int)atomicAdd(f.sp.next_item, 1u);
+            __syncthreads();
+            x = s_item;
+            if (x >= NI) break;
+        } else if (k * G >= NI) {
+            break;
+        }
         const bool live = x < NI;
         int r_lo = 0, r_hi = 0, item = 0;
         int32_t g_lo = 0, g_hi = 0x7fffffff, part = -1;   // (split: the item's tile range, chunk ordinal)
@@ -3492,8 +3502,8 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
         }
         if (live) {
-#ifdef FG_EXP_OLD_INSERT   // (A/B: the round-4 insert, one probe loop per record)
-            auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+            // one window's records into the table, one probe loop per record (the plain fire)
+            auto insert_plain = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
                 uint32_t hm[kTileRpl];
                 int4 bq[kTileRpl];
 #pragma unroll
@@ -3544,14 +3554,14 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     lds_val(&t_v[sl], vr[u], vt, true);
                 }
             };
-#else
-            // one window's records into the table. A bucket fills in slot order and keys are never
+            // the split fire's insert. A bucket fills in slot order and keys are never
             // removed, so a key present in a bucket sits before its first empty slot: the common
             // case -- the key in its home bucket -- is four compares and a select, no branch; the
             // lanes whose key is not there (its first record in this fire, or a full home bucket)
             // claim a slot by CAS or probe on, in a loop entered only when some lane needs it; the
             // adds are unconditional (lanes without a record add into the dummy slot)
-            auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+            auto insert_hot = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+                const bool hot = vt >= 0 && vt <= 2;   // (SUM-family value ops: pre-combine hot keys)
                 uint32_t hm[kTileRpl];
                 int4 bq[kTileRpl];
                 int sl[kTileRpl];
@@ -3642,7 +3652,10 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     lds_val(&t_v[sl[u]], va[u], vt, true);
                 }
             };
-#endif
+            auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+                if constexpr (HOT) insert_hot(kr, vr, nrec);
+                else insert_plain(kr, vr, nrec);
+            };
             for (int pi = 0; pi < f.n_passes; pi++) {
                 const TilePass tp = f.n_passes == 1 ? f.one : f.passes[pi];
                 int32_t t_lo = 0, t_hi = tp.nt;
@@ -3849,10 +3862,13 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
     const dim3 g((unsigned)workgroups), b(kTileFireThreads);
     const bool tab = f.m.has_dst || f.m.n_src > 0;
     // the value op compiled in: SUM / AVG over DOUBLE, BIGINT, or COUNT only
+    if (f.split && (tab || !f.sp.next_item)) return hipErrorInvalidValue;
+    const bool hot = f.hot && f.split && f.m.val_type >= 0 && f.m.val_type <= 2;
 #define FG_TILE_FIRE(V)                                                     \
     do {                                                                    \
-        if (tab) fg_launch((k_tile_fire<V, true>), g, b, 0, s, f);         \
-        else fg_launch((k_tile_fire<V, false>), g, b, 0, s, f);            \
+        if (tab) fg_launch((k_tile_fire<V, true, false>), g, b, 0, s, f);  \
+        else if (hot) fg_launch((k_tile_fire<V, false, true>), g, b, 0, s, f); \
+        else fg_launch((k_tile_fire<V, false, false>), g, b, 0, s, f);     \
     } while (0)
     switch (f.m.val_type) {
         case 2: FG_TILE_FIRE(2); break;
@@ -3890,10 +3906,11 @@ __global__ __launch_bounds__(kTilePlanThreads) void k_tile_plan(TileFire f) {
         }
         mine += tb[q];
     }
-    // chunk size: kTileChunk records, at least 4x the lane's mean bucket (only hot buckets split)
+    // chunk size: kTileChunk records, at least the lane's mean bucket -- a split bucket's chunks are
+    // items of a normal bucket's size (the fire fetches items dynamically)
     uint32_t lane_total;
     (void)block_exclusive_scan(mine, s_wave, &lane_total);
-    const uint64_t chunk = max((uint64_t)kTileChunk, 4 * ((uint64_t)lane_total / (uint64_t)nb));
+    const uint64_t chunk = max((uint64_t)kTileChunk, (uint64_t)lane_total / (uint64_t)nb);
 #pragma unroll
     for (int q = 0; q < BPT; q++) {
         const int bk = tid * BPT + q;
@@ -4078,19 +4095,22 @@ hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStr
 }
 
 // Materialize a tile pass's lane into a regular narrow staged pass. Workgroup (bucket, y) takes
-// kTileMatThreads tiles of the bucket's column (a hot key's bucket is spread over the whole
+// kTileMatTiles tiles of the bucket's column (a hot key's bucket is spread over the whole
 // column's workgroups, not one): its fragments' lengths scanned into a flat record sequence, the
 // records' regions at `bits` counted in LDS. COUNT: the counts added into hist[region] (zeroed by
 // the host). SCATTER: each region's block reserved at once from cursor[region] (the exclusive
 // scan of the counts, copied), the records read again and written at their rank (order inside a
-// region is immaterial).
+// region is immaterial). Every thread keeps kTileMatU records in flight.
 constexpr int kTileMatThreads = 256;
+constexpr int kTileMatTiles = 64;
+constexpr int kTileMatU = 4;
 template <bool SCATTER>
 __global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32_t bits, uint32_t* hist,
                                                               uint32_t* cursor, void* out) {
-    constexpr int T = kTileMatThreads;
+    constexpr int T = kTileMatThreads, TT = kTileMatTiles, U = kTileMatU;
     __shared__ uint32_t s_c[kTileMaxSub];
-    __shared__ uint32_t s_pre[T + 1];
+    __shared__ uint32_t s_pre[TT + 1];
+    __shared__ uint32_t s_x[TT];
     __shared__ uint32_t s_wave[T / 64];
     const int item = blockIdx.x;
     const int sub = bits - tp.bits;
@@ -4099,29 +4119,45 @@ __global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32
     const int tid = threadIdx.x;
     if (tid < nsub) s_c[tid] = 0u;
     const uint32_t* col = tp.dt + (int64_t)((tp.lane << (tp.bits - kTileBits)) | item) * tp.nt;
-    const int t = (int)blockIdx.y * T + tid;
-    const uint32_t x = t < tp.nt ? gbl(col)[t] : 0u;
+    const int t0 = (int)blockIdx.y * TT;
+    const uint32_t x = tid < TT && t0 + tid < tp.nt ? gbl(col)[t0 + tid] : 0u;
     uint32_t total;
     const uint32_t ex = block_exclusive_scan(x >> 16, s_wave, &total);   // (synchronizes: s_c is zeroed)
-    s_pre[tid] = ex;
-    if (tid == 0) s_pre[T] = total;
+    if (tid < TT) {
+        s_pre[tid] = ex;
+        s_x[tid] = x;
+    }
+    if (tid == 0) s_pre[TT] = total;
     __syncthreads();
     if (total == 0) return;   // (uniform)
-    // record i of the flat sequence: its tile (the last prefix <= i) and batch index
+    // record i of the flat sequence: its batch index (its tile: the last prefix <= i)
     auto rec_at = [&](uint32_t i) -> uint64_t {
-        int lo = 0, hi = T;
+        int lo = 0, hi = TT;
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
             if (s_pre[mid] <= i) lo = mid;
             else hi = mid;
         }
-        const uint32_t xt = gbl(col)[(int)blockIdx.y * T + lo];
-        return ((uint64_t)blockIdx.y * T + lo) * kTileRecs + (xt & 0xffffu) + (i - s_pre[lo]);
+        return (uint64_t)(t0 + lo) * kTileRecs + (s_x[lo] & 0xffffu) + (i - s_pre[lo]);
     };
-    for (uint32_t i = tid; i < total; i += T) {
-        const Rec12 r = ld_rec12(tp.rec, rec_at(i));
-        const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
-        atomicAdd(&s_c[region - r_lo], 1u);
+    auto regions = [&](uint32_t i0, Rec12 (&r)[U], int (&rg)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = i0 + u * T + tid;
+            if (i < total) r[u] = ld_rec12(tp.rec, rec_at(i));
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            rg[u] = i0 + u * T + tid < total
+                        ? (int)((uint64_t)mix_of((int64_t)(int32_t)r[u].k) >> (64 - bits)) - r_lo : -1;
+    };
+    for (uint32_t i0 = 0; i0 < total; i0 += U * T) {
+        Rec12 r[U];
+        int rg[U];
+        regions(i0, r, rg);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (rg[u] >= 0) atomicAdd(&s_c[rg[u]], 1u);
     }
     __syncthreads();
     if (!SCATTER) {
@@ -4130,24 +4166,29 @@ __global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32
     }
     if (tid < nsub && s_c[tid]) s_c[tid] = atomicAdd(&cursor[r_lo + tid], s_c[tid]);
     __syncthreads();
-    for (uint32_t i = tid; i < total; i += T) {
-        const Rec12 r = ld_rec12(tp.rec, rec_at(i));
-        const int region = (int)((uint64_t)mix_of((int64_t)(int32_t)r.k) >> (64 - bits));
-        const uint32_t pos = atomicAdd(&s_c[region - r_lo], 1u);
-        st_rec12(out, pos, (int64_t)(int32_t)r.k, rec12_val(r));
+    for (uint32_t i0 = 0; i0 < total; i0 += U * T) {
+        Rec12 r[U];
+        int rg[U];
+        regions(i0, r, rg);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (rg[u] < 0) continue;
+            const uint32_t pos = atomicAdd(&s_c[rg[u]], 1u);
+            st_rec12(out, pos, (int64_t)(int32_t)r[u].k, rec12_val(r[u]));
+        }
     }
 }
 
 hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s) {
     if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0) return hipErrorInvalidValue;   // (kTileMaxSub regions per bucket)
-    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatThreads - 1) / kTileMatThreads));
+    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatTiles - 1) / kTileMatTiles));
     fg_launch(k_tile_mat<false>, g, dim3(kTileMatThreads), 0, s, tp, bits, hist, (uint32_t*)nullptr, (void*)nullptr);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, uint32_t* cursor, void* out_rec, hipStream_t s) {
     if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0) return hipErrorInvalidValue;
-    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatThreads - 1) / kTileMatThreads));
+    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatTiles - 1) / kTileMatTiles));
     fg_launch(k_tile_mat<true>, g, dim3(kTileMatThreads), 0, s, tp, bits, (uint32_t*)nullptr, cursor, out_rec);
     return hipGetLastError();
 }

@@ -152,4 +152,32 @@ public final class FlinkGpu {
 
     /** fg_host_unregister (at close, before the segment is released to the MemoryManager). */
     public static native void hostUnregister(int device, ByteBuffer segment);
+
+    // ---- the keyBy edge local -> global over RCCL (fg_comm; INTEGRATION.md section 7) ----
+
+    /** Bytes of a communicator id (FG_COMM_ID_BYTES). */
+    public static final int COMM_ID_BYTES = 128;
+
+    /** fg_comm_unique_id: a new id into a direct buffer of COMM_ID_BYTES (the coordinator's). */
+    public static native void commUniqueId(ByteBuffer id);
+
+    /** fg_comm_open: this subtask's communicator (blocks until all `world` ranks joined). */
+    public static native long commOpen(int device, int world, int rank, ByteBuffer id);
+
+    /**
+     * fg_comm_exchange_fired: the local handle's collected fires exchanged by key-group owner and
+     * merged into the global handle; returns the combined watermark to advance the global to.
+     */
+    public static native long commExchangeFired(
+            long comm, long local, int keyHash, int maxParallelism, long watermark, long global);
+
+    /** fg_comm_exchange_flushed: the same for the local flush before a checkpoint barrier. */
+    public static native long commExchangeFlushed(
+            long comm, long local, int keyHash, int maxParallelism, long watermark, long global);
+
+    /** fg_comm_bytes_sent. */
+    public static native long commBytesSent(long comm);
+
+    /** fg_comm_close. */
+    public static native void commClose(long comm);
 }

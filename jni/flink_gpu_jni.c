@@ -22,6 +22,8 @@
  *   dict*           fg_key_dict_*        (BinaryRowDataKeySelector rows of any key type)
  *   hostRegister    fg_host_register     (page-lock a managed-memory segment at open: direct DMA)
  *   hostUnregister  fg_host_unregister   (at close)
+ *   comm*           fg_comm_*            (the keyBy edge local -> global over RCCL: KeyGroupStreamPartitioner
+ *                                         + RecordWriter + StatusWatermarkValve between co-located subtasks)
  *
  * Buffers: every ByteBuffer argument is a DIRECT buffer (MemorySegment.wrap of an off-heap
  * segment, MemorySegment.java:288,307, or ByteBuffer.allocateDirect) in native byte order;
@@ -393,4 +395,79 @@ JNIEXPORT void JNICALL FN(hostUnregister)(JNIEnv* env, jclass cls, jint device, 
     void* p = addr(env, segment);
     if ((*env)->ExceptionCheck(env)) return;
     check(env, NULL, fg_host_unregister(device, p));
+}
+
+/* ---- the keyBy edge over RCCL (fg_comm) ----------------------------------------------------------- */
+
+static int ccheck(JNIEnv* env, fg_comm* c, int rc) {
+    if (rc != FG_OK) throw_code(env, rc, fg_comm_last_error(c));
+    return rc;
+}
+
+/* void commUniqueId(ByteBuffer id): FG_COMM_ID_BYTES bytes of a new RCCL unique id (the
+ * coordinator makes it once and ships it with the deployment) */
+JNIEXPORT void JNICALL FN(commUniqueId)(JNIEnv* env, jclass cls, jobject id) {
+    (void)cls;
+    uint8_t* p = (uint8_t*)addr(env, id);
+    if ((*env)->ExceptionCheck(env)) return;
+    if ((*env)->GetDirectBufferCapacity(env, id) < FG_COMM_ID_BYTES) {
+        throw_code(env, FG_EINVAL, "commUniqueId: the id buffer holds FG_COMM_ID_BYTES bytes");
+        return;
+    }
+    ccheck(env, NULL, fg_comm_unique_id(p));
+}
+
+/* long commOpen(int device, int world, int rank, ByteBuffer id): blocks until every rank joined */
+JNIEXPORT jlong JNICALL FN(commOpen)(JNIEnv* env, jclass cls, jint device, jint world, jint rank, jobject id) {
+    (void)cls;
+    const uint8_t* p = (const uint8_t*)addr(env, id);
+    if ((*env)->ExceptionCheck(env)) return 0;
+    if ((*env)->GetDirectBufferCapacity(env, id) < FG_COMM_ID_BYTES) {
+        throw_code(env, FG_EINVAL, "commOpen: the id buffer holds FG_COMM_ID_BYTES bytes");
+        return 0;
+    }
+    fg_comm* c = NULL;
+    if (ccheck(env, NULL, fg_comm_open(device, world, rank, p, &c))) return 0;
+    return (jlong)(intptr_t)c;
+}
+
+/* long commExchangeFired(long comm, long local, int keyHash, int maxParallelism, long watermark,
+ * long global): the local handle's collected async fires exchanged by key-group owner and merged
+ * into `global`; returns the combined watermark (min over the ranks) to advance `global` to */
+JNIEXPORT jlong JNICALL FN(commExchangeFired)(JNIEnv* env, jclass cls, jlong cp, jlong lp, jint keyHash,
+                                              jint maxPar, jlong wm, jlong gp) {
+    (void)cls;
+    int64_t mw = 0;
+    fg_comm* c = (fg_comm*)(intptr_t)cp;
+    if (ccheck(env, c, fg_comm_exchange_fired(c, (fg_handle*)(intptr_t)lp, keyHash, maxPar, wm,
+                                              (fg_handle*)(intptr_t)gp, &mw)))
+        return 0;
+    return mw;
+}
+
+/* long commExchangeFlushed(long comm, long local, int keyHash, int maxParallelism, long watermark,
+ * long global): the same for the local buffer's flush before a checkpoint barrier */
+JNIEXPORT jlong JNICALL FN(commExchangeFlushed)(JNIEnv* env, jclass cls, jlong cp, jlong lp, jint keyHash,
+                                                jint maxPar, jlong wm, jlong gp) {
+    (void)cls;
+    int64_t mw = 0;
+    fg_comm* c = (fg_comm*)(intptr_t)cp;
+    if (ccheck(env, c, fg_comm_exchange_flushed(c, (fg_handle*)(intptr_t)lp, keyHash, maxPar, wm,
+                                                (fg_handle*)(intptr_t)gp, &mw)))
+        return 0;
+    return mw;
+}
+
+/* long commBytesSent(long comm) */
+JNIEXPORT jlong JNICALL FN(commBytesSent)(JNIEnv* env, jclass cls, jlong cp) {
+    (void)env;
+    (void)cls;
+    return fg_comm_bytes_sent((fg_comm*)(intptr_t)cp);
+}
+
+/* void commClose(long comm) */
+JNIEXPORT void JNICALL FN(commClose)(JNIEnv* env, jclass cls, jlong cp) {
+    (void)env;
+    (void)cls;
+    fg_comm_close((fg_comm*)(intptr_t)cp);
 }

@@ -12,9 +12,8 @@ build() {   # name, defines
         -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 }
 mkdir -p var
-build old_insert "-DFG_EXP_OLD_INSERT" &
 build shfl_scan "-DFG_EXP_SHFL_SCAN" &
 build cond_loads "-DFG_EXP_COND_LOADS" &
-build all_old "-DFG_EXP_OLD_INSERT -DFG_EXP_SHFL_SCAN -DFG_EXP_COND_LOADS" &
+build all_old "-DFG_EXP_SHFL_SCAN -DFG_EXP_COND_LOADS" &
 wait
 ls -la build_var/*/libflinkgpu.so

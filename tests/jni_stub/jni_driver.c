@@ -111,6 +111,11 @@ jlong FN(flushPartials)(JNIEnv*, jclass, jlong, jobjectArray);
 jlong FN(lateDropped)(JNIEnv*, jclass, jlong);
 void FN(close)(JNIEnv*, jclass, jlong);
 void FN(hostRegister)(JNIEnv*, jclass, jint, jobject);
+void FN(commUniqueId)(JNIEnv*, jclass, jobject);
+jlong FN(commOpen)(JNIEnv*, jclass, jint, jint, jint, jobject);
+jlong FN(commExchangeFired)(JNIEnv*, jclass, jlong, jlong, jint, jint, jlong, jlong);
+jlong FN(commBytesSent)(JNIEnv*, jclass, jlong);
+void FN(commClose)(JNIEnv*, jclass, jlong);
 
 static jobject direct(void* p, jlong cap) { return f_new_direct(env, p, cap); }
 static jobject objarr(jsize n) {
@@ -263,6 +268,29 @@ static int gpu_mode(void) {
         printf("partials rows %lld cnt_star %lld cnt_val %lld sum %.1f\n", (long long)n, a, b, t);
     }
     FN(close)(env, NULL, h);
+    {   /* the two-phase edge over RCCL at world size 1: local partials -> exchange -> global */
+        static uint8_t id[FG_COMM_ID_BYTES];
+        FN(commUniqueId)(env, NULL, direct(id, sizeof id));
+        jlong comm = FN(commOpen)(env, NULL, 0, 1, 0, direct(id, sizeof id));
+        if (!comm) {
+            printf("FAIL commOpen: %s %s\n", exc_class, exc_msg);
+            return 1;
+        }
+        fg_config lc = config(FG_TUMBLE, 1000, 0, 0, 1);
+        lc.flags = FG_FLAG_LOCAL_PARTIALS;
+        fg_config gc = config(FG_TUMBLE, 1000, 0, 0, 1);
+        jlong loc = FN(open)(env, NULL, direct(&lc, sizeof lc), NULL, NULL);
+        jlong glob = FN(open)(env, NULL, direct(&gc, sizeof gc), NULL, NULL);
+        FN(addBatch)(env, NULL, loc, direct(key, sizeof key), direct(rt, sizeof rt), direct(val, sizeof val), NULL, N);
+        FN(advanceProgressAsync)(env, NULL, loc, 2999);
+        jlong mw = FN(commExchangeFired)(env, NULL, comm, loc, FG_KEYHASH_BINARYROW_BIGINT, 128, 2999, glob);
+        printf("comm_wm %lld sent %lld\n", (long long)mw, (long long)FN(commBytesSent)(env, NULL, comm));
+        n = FN(advanceProgress)(env, NULL, glob, mw, cols);
+        totals("comm", cols, n, 3);
+        FN(close)(env, NULL, loc);
+        FN(close)(env, NULL, glob);
+        FN(commClose)(env, NULL, comm);
+    }
     if (pending) {
         printf("FAIL pending exception %s: %s\n", exc_class, exc_msg);
         return 1;

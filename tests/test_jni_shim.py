@@ -124,7 +124,9 @@ def test_jni_glue_errors_through_fake_jnienv(tmp_path):
 def test_jni_glue_on_gpu_host_columns(tmp_path):
     """open / addBatch / advanceProgressAsync + collectFired / advanceProgress / flushPartials
     through the glue on the GPU: the driver reads every fired column on the HOST (the direct
-    buffers a JVM would read), totals against numpy"""
+    buffers a JVM would read), totals against numpy; then the two-phase edge through the comm
+    natives at world size 1 (commUniqueId / commOpen / commExchangeFired over RCCL): the global
+    handle fires what the single-phase operator fired"""
     exe = _build_jni_driver(tmp_path)
     p = subprocess.run([exe, "gpu"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "gpu done" in p.stdout, p.stdout + p.stderr
@@ -137,7 +139,8 @@ def test_jni_glue_on_gpu_host_columns(tmp_path):
         pairs = set(zip(key[sel], we))
         return (len(pairs), int(sel.sum()), float(val[sel].sum()), sum(k for k, _ in pairs), sum(w for _, w in pairs))
 
-    for tag, sel in (("async", rt < 3000), ("sync", rt >= 3000)):
+    assert out["comm_wm"] == ["2999", "sent", "0"]   # (world size 1: nothing leaves the rank)
+    for tag, sel in (("async", rt < 3000), ("sync", rt >= 3000), ("comm", rt < 3000)):
         f = out[tag]
         got = (int(f[1]), int(f[3]), float(f[5]), int(f[7]), int(f[9]))
         assert got == expect(sel), (tag, got, expect(sel))
