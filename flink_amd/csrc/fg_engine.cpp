@@ -2278,7 +2278,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
         p.grid = (int)std::max<int64_t>(1, (n + seg - 1) / seg);
         p.n_coarse = h->F >> kTileBits;
         const int64_t NT = (int64_t)p.grid * p.max_tiles;
-        HIPCHK(h, st->t_rec.ensure((size_t)(n / 64 + 2) * kRec12Block));
+        HIPCHK(h, st->t_rec.ensure((size_t)(n / 64 + 2) * kRec12Block));   // (packed 12-B tile records: 12 n)
         HIPCHK(h, st->t_dt.ensure(4 * (size_t)p.n_coarse * NT));
         HIPCHK(h, st->t_btot.ensure(4 * (size_t)p.n_coarse));
         p.tile_btot = st->t_btot.as<uint32_t>();

@@ -443,7 +443,7 @@ constexpr int kTileMaxRegions = 1 << kTileMaxRegionBits;
 
 // One tile-staged pass as the fire / materialize kernels read it (lane `lane`'s buckets)
 struct TilePass {
-    const void* rec;          // block-laid 12-B records at their absolute batch index
+    const void* rec;          // packed 12-B tile records at their absolute batch index (ld_tile_rec)
     const uint32_t* dt;       // [nc][nt]: offset | length << 16 of bucket c's fragment of tile t
     int64_t n;                // records of the pass (tile t holds records [t * kTileRecs, ...): pass 1's
                               // segments are whole tiles, so a tile's first record needs no division)

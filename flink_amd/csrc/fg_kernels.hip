@@ -72,6 +72,35 @@ __device__ __forceinline__ void st_rec12(void* base, uint64_t i, int64_t key, in
     *((uint64_t __attribute__((address_space(1)))*)(b + 256) + (i & 63)) = (uint64_t)val;
 }
 
+// Tile-staged records (k_tile_part1 -> k_tile_fire / k_tile_mat): packed 12-B records {int32 key,
+// value bits} at 12 * i, one dwordx3 access each (4-B aligned). The tiles are written whole and in
+// order (a wave's stores are 768 contiguous bytes), and the fire gathers a bucket's fragments of a
+// few records each: a fragment is one contiguous range -- with the block layout above its keys
+// and its values were two ranges in different cache lines, two loads per record.
+// (FG_EXP_TILE_BLOCK: the block layout, A/B)
+__device__ __forceinline__ Rec12 ld_tile_rec(const void* base, uint64_t i) {
+#ifdef FG_EXP_TILE_BLOCK
+    return ld_rec12(base, i);
+#else
+    const uint32_t __attribute__((address_space(1)))* q = (const uint32_t __attribute__((address_space(1)))*)base + 3 * i;
+    Rec12 r;   // (three adjacent dwords: one global_load_dwordx3)
+    r.k = q[0];
+    r.lo = q[1];
+    r.hi = q[2];
+    return r;
+#endif
+}
+__device__ __forceinline__ void st_tile_rec(void* base, uint64_t i, int64_t key, int64_t val) {
+#ifdef FG_EXP_TILE_BLOCK
+    st_rec12(base, i, key, val);
+#else
+    uint32_t __attribute__((address_space(1)))* q = (uint32_t __attribute__((address_space(1)))*)base + 3 * i;
+    q[0] = (uint32_t)key;   // (one global_store_dwordx3)
+    q[1] = (uint32_t)val;
+    q[2] = (uint32_t)((uint64_t)val >> 32);
+#endif
+}
+
 // A pointer every lane of the wave holds (loaded from LDS, so the compiler cannot tell):
 // moved to SGPRs, so loads off it take the scalar-base + 32-bit-offset form (no 64-bit
 // address arithmetic per lane).
@@ -3022,7 +3051,7 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
         }
         if (t0 + TILE < end) load(t0 + TILE, ka, ta);   // the next tile's first half, across the write-out
         lds_barrier();
-        for (uint32_t i = tid; i < tile_total; i += T) st_rec12(p.tmp, (uint64_t)(t0 + i), (int64_t)s_k[i], (int64_t)s_v[i]);
+        for (uint32_t i = tid; i < tile_total; i += T) st_tile_rec(p.tmp, (uint64_t)(t0 + i), (int64_t)s_k[i], (int64_t)s_v[i]);
         lds_barrier();   // staging and the directory row have read the offsets
         for (int w = tid; w <= NW; w += T) s_cw[w] = 0;
         lds_barrier();
@@ -3312,7 +3341,7 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             w.bad = true;
             src = 0;
         }
-        const Rec12 r = ld_rec12(w.rec, (uint64_t)src);
+        const Rec12 r = ld_tile_rec(w.rec, (uint64_t)src);
         kr[u] = (int32_t)r.k;
         vr[u] = rec12_val(r);
     }
@@ -4144,7 +4173,7 @@ __global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t i = i0 + u * T + tid;
-            if (i < total) r[u] = ld_rec12(tp.rec, rec_at(i));
+            if (i < total) r[u] = ld_tile_rec(tp.rec, rec_at(i));
         }
 #pragma unroll
         for (int u = 0; u < U; u++)

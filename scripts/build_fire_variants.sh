@@ -15,5 +15,6 @@ mkdir -p var
 build shfl_scan "-DFG_EXP_SHFL_SCAN" &
 build cond_loads "-DFG_EXP_COND_LOADS" &
 build all_old "-DFG_EXP_SHFL_SCAN -DFG_EXP_COND_LOADS" &
+build tile_block "-DFG_EXP_TILE_BLOCK" &
 wait
 ls -la build_var/*/libflinkgpu.so
