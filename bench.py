@@ -549,9 +549,10 @@ def main():
     if args.checkpoint_every is None:
         # configs[4] checkpoints every 10 s; a step is 1B records = 10 event-seconds at the
         # workload's 100M records per event-second, and its wall time is well under 10 s: one
-        # checkpoint per step is as often as the config asks, or more
+        # checkpoint per step (at its middle micro-batch: each step restarts at batch 0) is as
+        # often as the config asks, or more
         nb = -(-args.records // args.batch)
-        args.checkpoint_every = nb if args.workload == "zipf" else 0
+        args.checkpoint_every = max(1, nb // 2) if args.workload == "zipf" else 0
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
