@@ -313,7 +313,7 @@ struct fg_handle {
     // tiles; its fire splits the hot buckets into chunk items (k_tile_plan / k_tile_merge_parts)
     bool tile_split = true;
     DevBuf tile_dir, tile_hist;
-    DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail;   // split fire plan + partials
+    DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail, sp_icnt;   // split plans + partials
     // skewed-region plan and chunk partial tables
     DevBuf hv_flags, hv_list, hv_n, hv_chunk0, hv_clist, hv_v0, hv_v1, hv_key, hv_cs, hv_cn, hv_sum, hv_pn;
     DevBuf hv_mv1, hv_mv2;   // multi-value operator: value slots 1 and 2 of the chunks' partial rows
@@ -1088,6 +1088,7 @@ std::unique_ptr<Staged> pass_from_pool(fg_handle* h) {
 // (k_tile_scatter). Every consumer other than the fire straight from the tiles -- a flush into
 // the slice table, a checkpoint, a restore re-fire, the heavy pass -- then reads the lane as it
 // reads any staged pass.
+int split_buffers(fg_handle* h, int nb, int64_t fill, uint32_t chunk, bool icnt, TileSplit* out);
 int materialize_lane(fg_handle* h, int l) {
     Lane& ln = h->lane[l];
     for (size_t i = 0; i < ln.passes.size(); i++) {
@@ -1106,13 +1107,26 @@ int materialize_lane(fg_handle* h, int l) {
         uint32_t* bo = m->bucket_off.as<uint32_t>() + ((int64_t)l << bits);
         {
             KTimer kt(h, K_TILE_MAT, s->lane_n[l]);
+            // items of at most ~kTileMatChunk records (a hot key's bucket spread over many)
+            TileFire f{};
+            f.one = tp;
+            f.n_passes = 1;
+            f.tbits = s->bits;
+            f.split = 1;
+            f.m.overflow = h->scalars.as<unsigned int>();
+            int rc = split_buffers(h, 1 << (s->bits - kTileBits), s->lane_n[l], kTileMatChunk, true, &f.sp);
+            if (rc) return rc;
+            f.sp.gpre[0] = 0;
+            f.sp.gpre[1] = tp.nt;
+            HIPCHK(h, launch_tile_plan(f, h->stream));
+            const int wg = 4 * h->merge_grid;
             uint32_t* hist = h->tile_hist.as<uint32_t>();
             HIPCHK(h, hipMemsetAsync(hist, 0, 4 * (size_t)P, h->stream));
-            HIPCHK(h, launch_tile_count(tp, bits, hist, h->stream));
+            HIPCHK(h, launch_tile_count(tp, bits, f.sp, hist, wg, h->stream));
             HIPCHK(h, launch_scan_u32(hist, bo, P, h->scan_tmp.as<uint32_t>(), h->stream));
-            // (the scan's bases copied: the scatter's workgroups reserve their blocks from them)
+            // (the scan's bases copied: each item reserves its regions' blocks from them)
             HIPCHK(h, hipMemcpyAsync(hist, bo, 4 * (size_t)P, hipMemcpyDeviceToDevice, h->stream));
-            HIPCHK(h, launch_tile_scatter(tp, bits, hist, m->own_rec.p, h->stream));
+            HIPCHK(h, launch_tile_scatter(tp, bits, f.sp, hist, m->own_rec.p, wg, h->stream));
         }
         m->bits = bits;
         m->is_acc = false;
@@ -1149,6 +1163,8 @@ bool tile_fire_ok(const fg_handle* h, const Lane& ln, bool allow_skew = false) {
     return true;
 }
 
+constexpr int64_t kTileSpreadMin = 1 << 18;     // records of a lane worth a spread (split) fire
+constexpr int64_t kTileSpreadChunk = 1 << 12;   // smallest chunk item of a spread fire
 // A skewed tile pass stays on the tiles (FG_TILE_SPLIT): TUMBLE windows and local-phase slices,
 // whose lanes fire straight from the tiles by the split fire (anything else materializes them)
 bool tile_split_ok(const fg_handle* h) { return h->tile_split && (h->w.kind == TUMBLE || h->local); }
@@ -1157,13 +1173,15 @@ bool tile_split_ok(const fg_handle* h) { return h->tile_split && (h->w.kind == T
 // the buckets above max(kTileChunk, the lane's mean) into chunk items, k_tile_fire aggregates
 // every item (chunks into partial entries), k_tile_merge_parts merges each split bucket's chunks
 // into its rows. f is the job's TileFire (tile_job_params).
-int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f) {
-    const int nb = 1 << (f.tbits - kTileBits);
-    const int64_t fill = ln.fill;
-    const int64_t max_chunks = fill / kTileChunk + nb + 1;   // (chunks >= kTileChunk records, + 1 per bucket)
+// The plan's buffers (TileSplit) for `fill` records over nb buckets in items of at least `chunk`
+// records (0: kTileChunk), the counts zeroed on the stream; materialize also keeps per-item
+// sub-region counts (icnt).
+int split_buffers(fg_handle* h, int nb, int64_t fill, uint32_t chunk, bool icnt, TileSplit* out) {
+    const int64_t max_chunks = fill / (chunk ? chunk : kTileChunk) + nb + 1;   // (chunks >= chunk records, + 1 per bucket)
     const int64_t max_items = max_chunks + nb;
-    const int64_t part_cap = std::min<int64_t>(fill, max_chunks * (kTileSlots + 1)) + 1;
-    if (part_cap >= ((int64_t)1 << 32)) return h->fail(FG_ECAPACITY, "internal: split fire partials above 2^32");
+    const int64_t part_cap = icnt ? 1 : std::min<int64_t>(fill, max_chunks * (kTileSlots + 1)) + 1;
+    if (part_cap >= ((int64_t)1 << 32) || max_items >= ((int64_t)1 << 31))
+        return h->fail(FG_ECAPACITY, "internal: split plan of %lld records above its index range", (long long)fill);
     HIPCHK(h, h->sp_items.ensure(sizeof(TileItem) * (size_t)max_items));
     HIPCHK(h, h->sp_n.ensure(16));
     HIPCHK(h, h->sp_split.ensure(4 * 3 * (size_t)nb));
@@ -1172,8 +1190,10 @@ int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f) {
     HIPCHK(h, h->sp_pcs.ensure(4 * (size_t)part_cap));
     HIPCHK(h, h->sp_pv.ensure(8 * (size_t)part_cap));
     HIPCHK(h, h->sp_bfail.ensure(4 * (size_t)nb));
+    if (icnt) HIPCHK(h, h->sp_icnt.ensure(4 * (size_t)kTileMaxSub * (size_t)max_items));
     HIPCHK(h, hipMemsetAsync(h->sp_n.p, 0, 16, h->stream));   // n_items, n_split, part_fill, next_item
-    TileSplit& sp = f.sp;
+    TileSplit& sp = *out;
+    sp = TileSplit{};
     sp.items = h->sp_items.as<TileItem>();
     sp.n_items = h->sp_n.as<uint32_t>();
     sp.n_split = h->sp_n.as<uint32_t>() + 1;
@@ -1191,6 +1211,16 @@ int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f) {
     sp.p_cs = h->sp_pcs.as<uint32_t>();
     sp.p_v = h->sp_pv.as<unsigned long long>();
     sp.bfail = h->sp_bfail.as<uint32_t>();
+    sp.chunk = chunk;
+    sp.icnt = icnt ? h->sp_icnt.as<uint32_t>() : nullptr;
+    return FG_OK;
+}
+
+int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f, uint32_t chunk) {
+    const int nb = 1 << (f.tbits - kTileBits);
+    if (int rc = split_buffers(h, nb, ln.fill, chunk, false, &f.sp)) return rc;
+    TileSplit& sp = f.sp;
+    const int64_t max_items = sp.max_items;
     int32_t g = 0;
     for (size_t i = 0; i < ln.passes.size(); i++) {
         sp.gpre[i] = g;
@@ -1327,10 +1357,17 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 if (rc) return rc;
                 bool skewed = false;
                 for (const Staged* st : ln.passes) skewed = skewed || st->skew;
+                // a lane of fewer buckets than CUs (a small key space, configs[0]) is split too, into
+                // ~2 items per CU: one workgroup per bucket would leave most of the GPU idle
+                const int nbk = 1 << (f.tbits - kTileBits);
+                const bool spread = h->tile_split && nbk < h->merge_grid && ln.fill >= kTileSpreadMin &&
+                                    ln.passes.size() <= (size_t)kMaxTilePasses;
+                const uint32_t chunk =
+                    skewed ? 0u : (uint32_t)std::max<int64_t>(kTileSpreadChunk, ln.fill / (2 * h->merge_grid));
                 {
-                    KTimer kt(h, skewed ? K_TILE_SPLIT : K_TILE_FIRE, ln.fill);
-                    if (skewed) {
-                        rc = tile_split_fire(h, ln, f);
+                    KTimer kt(h, skewed || spread ? K_TILE_SPLIT : K_TILE_FIRE, ln.fill);
+                    if (skewed || spread) {
+                        rc = tile_split_fire(h, ln, f, chunk);
                         if (rc) return rc;
                     } else {
                         HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));

@@ -479,6 +479,8 @@ struct TileSplit {
     uint32_t* part_n;
     uint32_t* part_fill;      // partial entries written (reservation counter)
     uint32_t* next_item;      // the fire's dynamic item counter (zeroed with the counts)
+    uint32_t chunk;           // records per chunk item; 0: max(kTileChunk, the lane's mean bucket)
+    uint32_t* icnt;           // materialize: [items][kTileMaxSub] records per sub-region of an item
     uint32_t part_cap;
     int32_t* p_key;           // partial entries: int32 key, COUNT(*), value bits (the LDS repr)
     uint32_t* p_cs;
@@ -508,11 +510,16 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
 // a split fire: the plan (one workgroup), the fire over its items, the merge of split buckets
 hipError_t launch_tile_plan(const TileFire& f, hipStream_t s);
 hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStream_t s);
-// materialize: per-region counts of one tile pass's lane added into hist[P] at `bits` (zeroed
-// first), then -- after the exclusive scan into bucket_off, copied into `cursor` -- the records
-// into a regular narrow staged area (each workgroup reserves its regions' blocks from cursor)
-hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s);
-hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, uint32_t* cursor, void* out_rec, hipStream_t s);
+// materialize, over the items of a plan (launch_tile_plan of the one pass with sp.chunk =
+// kTileMatChunk): per-region counts of the pass's lane added into hist[P] at `bits` (zeroed
+// first) and kept per item in plan.icnt, then -- after the exclusive scan into bucket_off, copied
+// into `cursor` -- the records into a regular narrow staged area (each item reserves its regions'
+// blocks from cursor)
+constexpr uint32_t kTileMatChunk = 1u << 14;
+hipError_t launch_tile_count(const TilePass& tp, int32_t bits, const TileSplit& plan, uint32_t* hist,
+                             int32_t workgroups, hipStream_t s);
+hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, const TileSplit& plan, uint32_t* cursor, void* out_rec,
+                               int32_t workgroups, hipStream_t s);
 
 constexpr int kMaxOwnerCols = 8;
 struct OwnerCols {

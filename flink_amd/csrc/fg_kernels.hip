@@ -3939,7 +3939,7 @@ __global__ __launch_bounds__(kTilePlanThreads) void k_tile_plan(TileFire f) {
     // items of a normal bucket's size (the fire fetches items dynamically)
     uint32_t lane_total;
     (void)block_exclusive_scan(mine, s_wave, &lane_total);
-    const uint64_t chunk = max((uint64_t)kTileChunk, (uint64_t)lane_total / (uint64_t)nb);
+    const uint64_t chunk = sp.chunk ? (uint64_t)sp.chunk : max((uint64_t)kTileChunk, (uint64_t)lane_total / (uint64_t)nb);
 #pragma unroll
     for (int q = 0; q < BPT; q++) {
         const int bk = tid * BPT + q;
@@ -4123,102 +4123,108 @@ hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStr
     return hipGetLastError();
 }
 
-// Materialize a tile pass's lane into a regular narrow staged pass. Workgroup (bucket, y) takes
-// kTileMatTiles tiles of the bucket's column (a hot key's bucket is spread over the whole
-// column's workgroups, not one): its fragments' lengths scanned into a flat record sequence, the
-// records' regions at `bits` counted in LDS. COUNT: the counts added into hist[region] (zeroed by
-// the host). SCATTER: each region's block reserved at once from cursor[region] (the exclusive
-// scan of the counts, copied), the records read again and written at their rank (order inside a
-// region is immaterial). Every thread keeps kTileMatU records in flight.
+// Materialize a tile pass's lane into a regular narrow staged pass, over the items of a plan
+// (k_tile_plan with sp.chunk = kTileMatChunk: a bucket above that many records is cut into equal
+// tile ranges, so a hot key's bucket is spread over many workgroups and no workgroup gets more
+// than ~kTileMatChunk records). Persistent workgroups take items in turn; an item's tiles are
+// walked kTileMatThreads at a time (one directory entry per thread, their lengths scanned into a
+// flat record sequence, kTileMatU records in flight per thread). COUNT: the item's records per
+// region at `bits` into icnt[item][sub-region] and added into hist (zeroed by the host). SCATTER:
+// each region's block of the item reserved at once from cursor[region] (the exclusive scan of
+// hist, copied) by its icnt, the records written at their rank (order inside a region is
+// immaterial).
 constexpr int kTileMatThreads = 256;
-constexpr int kTileMatTiles = 64;
 constexpr int kTileMatU = 4;
 template <bool SCATTER>
-__global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32_t bits, uint32_t* hist,
-                                                              uint32_t* cursor, void* out) {
-    constexpr int T = kTileMatThreads, TT = kTileMatTiles, U = kTileMatU;
+__global__ __launch_bounds__(kTileMatThreads) void k_tile_mat(TilePass tp, int32_t bits, const TileItem* items,
+                                                              const uint32_t* n_items, uint32_t* icnt,
+                                                              uint32_t* hist_or_cursor, void* out) {
+    constexpr int T = kTileMatThreads, U = kTileMatU;
     __shared__ uint32_t s_c[kTileMaxSub];
-    __shared__ uint32_t s_pre[TT + 1];
-    __shared__ uint32_t s_x[TT];
+    __shared__ uint32_t s_pre[T + 1];
+    __shared__ uint32_t s_x[T];
     __shared__ uint32_t s_wave[T / 64];
-    const int item = blockIdx.x;
     const int sub = bits - tp.bits;
     const int nsub = 1 << (kTileBits + sub);   // (host: kTileBits + sub <= 6)
-    const int r_lo = item << (kTileBits + sub);
     const int tid = threadIdx.x;
-    if (tid < nsub) s_c[tid] = 0u;
-    const uint32_t* col = tp.dt + (int64_t)((tp.lane << (tp.bits - kTileBits)) | item) * tp.nt;
-    const int t0 = (int)blockIdx.y * TT;
-    const uint32_t x = tid < TT && t0 + tid < tp.nt ? gbl(col)[t0 + tid] : 0u;
-    uint32_t total;
-    const uint32_t ex = block_exclusive_scan(x >> 16, s_wave, &total);   // (synchronizes: s_c is zeroed)
-    if (tid < TT) {
-        s_pre[tid] = ex;
-        s_x[tid] = x;
-    }
-    if (tid == 0) s_pre[TT] = total;
-    __syncthreads();
-    if (total == 0) return;   // (uniform)
-    // record i of the flat sequence: its batch index (its tile: the last prefix <= i)
-    auto rec_at = [&](uint32_t i) -> uint64_t {
-        int lo = 0, hi = TT;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (s_pre[mid] <= i) lo = mid;
-            else hi = mid;
+    const uint32_t NI = *gbl(n_items);
+    for (uint32_t x = blockIdx.x; x < NI; x += gridDim.x) {
+        const TileItem it = items[x];
+        const int r_lo = it.bucket << (kTileBits + sub);
+        const uint32_t* col = tp.dt + (int64_t)((tp.lane << (tp.bits - kTileBits)) | it.bucket) * tp.nt;
+        if (tid < nsub) {
+            uint32_t c0 = 0;
+            if (SCATTER) {
+                const uint32_t c = icnt[(uint64_t)x * kTileMaxSub + tid];
+                if (c) c0 = atomicAdd(&hist_or_cursor[r_lo + tid], c);
+            }
+            s_c[tid] = c0;
         }
-        return (uint64_t)(t0 + lo) * kTileRecs + (s_x[lo] & 0xffffu) + (i - s_pre[lo]);
-    };
-    auto regions = [&](uint32_t i0, Rec12 (&r)[U], int (&rg)[U]) {
+        const int32_t g_hi = it.g_hi < tp.nt ? it.g_hi : tp.nt;
+        for (int32_t t0 = it.g_lo; t0 < g_hi; t0 += T) {
+            const uint32_t xd = t0 + tid < g_hi ? gbl(col)[t0 + tid] : 0u;
+            uint32_t total;
+            const uint32_t ex = block_exclusive_scan(xd >> 16, s_wave, &total);   // (synchronizes)
+            s_pre[tid] = ex;
+            s_x[tid] = xd;
+            if (tid == 0) s_pre[T] = total;
+            __syncthreads();
+            if (total > 0) {   // (uniform)
+                auto rec_at = [&](uint32_t i) -> uint64_t {   // its tile: the last prefix <= i
+                    int lo = 0, hi = T;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_pre[mid] <= i) lo = mid;
+                        else hi = mid;
+                    }
+                    return (uint64_t)(t0 + lo) * kTileRecs + (s_x[lo] & 0xffffu) + (i - s_pre[lo]);
+                };
+                for (uint32_t i0 = 0; i0 < total; i0 += U * T) {
+                    Rec12 r[U];
+                    int rg[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t i = i0 + u * T + tid;
-            if (i < total) r[u] = ld_tile_rec(tp.rec, rec_at(i));
+                    for (int u = 0; u < U; u++) {
+                        const uint32_t i = i0 + u * T + tid;
+                        if (i < total) r[u] = ld_tile_rec(tp.rec, rec_at(i));
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; u++)
+                        rg[u] = i0 + u * T + tid < total
+                                    ? (int)((uint64_t)mix_of((int64_t)(int32_t)r[u].k) >> (64 - bits)) - r_lo : -1;
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        if (rg[u] < 0) continue;
+                        const uint32_t pos = atomicAdd(&s_c[rg[u]], 1u);
+                        if (SCATTER) st_rec12(out, pos, (int64_t)(int32_t)r[u].k, rec12_val(r[u]));
+                    }
+                }
+            }
+            __syncthreads();   // (s_pre / s_x are rewritten by the next tile range)
         }
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            rg[u] = i0 + u * T + tid < total
-                        ? (int)((uint64_t)mix_of((int64_t)(int32_t)r[u].k) >> (64 - bits)) - r_lo : -1;
-    };
-    for (uint32_t i0 = 0; i0 < total; i0 += U * T) {
-        Rec12 r[U];
-        int rg[U];
-        regions(i0, r, rg);
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (rg[u] >= 0) atomicAdd(&s_c[rg[u]], 1u);
-    }
-    __syncthreads();
-    if (!SCATTER) {
-        if (tid < nsub && s_c[tid]) atomicAdd(&hist[r_lo + tid], s_c[tid]);
-        return;
-    }
-    if (tid < nsub && s_c[tid]) s_c[tid] = atomicAdd(&cursor[r_lo + tid], s_c[tid]);
-    __syncthreads();
-    for (uint32_t i0 = 0; i0 < total; i0 += U * T) {
-        Rec12 r[U];
-        int rg[U];
-        regions(i0, r, rg);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (rg[u] < 0) continue;
-            const uint32_t pos = atomicAdd(&s_c[rg[u]], 1u);
-            st_rec12(out, pos, (int64_t)(int32_t)r[u].k, rec12_val(r[u]));
+        if (!SCATTER && tid < nsub) {
+            const uint32_t c = s_c[tid];
+            icnt[(uint64_t)x * kTileMaxSub + tid] = c;
+            if (c) atomicAdd(&hist_or_cursor[r_lo + tid], c);
         }
+        __syncthreads();   // (s_c is reset by the next item)
     }
 }
 
-hipError_t launch_tile_count(const TilePass& tp, int32_t bits, uint32_t* hist, hipStream_t s) {
-    if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0) return hipErrorInvalidValue;   // (kTileMaxSub regions per bucket)
-    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatTiles - 1) / kTileMatTiles));
-    fg_launch(k_tile_mat<false>, g, dim3(kTileMatThreads), 0, s, tp, bits, hist, (uint32_t*)nullptr, (void*)nullptr);
+hipError_t launch_tile_count(const TilePass& tp, int32_t bits, const TileSplit& plan, uint32_t* hist,
+                             int32_t workgroups, hipStream_t s) {
+    if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0 || !plan.items || !plan.n_items || !plan.icnt || workgroups < 1)
+        return hipErrorInvalidValue;   // (kTileMaxSub regions per bucket)
+    fg_launch(k_tile_mat<false>, dim3((unsigned)workgroups), dim3(kTileMatThreads), 0, s, tp, bits,
+              (const TileItem*)plan.items, (const uint32_t*)plan.n_items, plan.icnt, hist, (void*)nullptr);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, uint32_t* cursor, void* out_rec, hipStream_t s) {
-    if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0) return hipErrorInvalidValue;
-    const dim3 g(1u << (tp.bits - kTileBits), (unsigned)((tp.nt + kTileMatTiles - 1) / kTileMatTiles));
-    fg_launch(k_tile_mat<true>, g, dim3(kTileMatThreads), 0, s, tp, bits, (uint32_t*)nullptr, cursor, out_rec);
+hipError_t launch_tile_scatter(const TilePass& tp, int32_t bits, const TileSplit& plan, uint32_t* cursor, void* out_rec,
+                               int32_t workgroups, hipStream_t s) {
+    if (bits - tp.bits + kTileBits > 6 || tp.nt <= 0 || !plan.items || !plan.n_items || !plan.icnt || workgroups < 1)
+        return hipErrorInvalidValue;
+    fg_launch(k_tile_mat<true>, dim3((unsigned)workgroups), dim3(kTileMatThreads), 0, s, tp, bits,
+              (const TileItem*)plan.items, (const uint32_t*)plan.n_items, plan.icnt, cursor, out_rec);
     return hipGetLastError();
 }
 

@@ -44,3 +44,24 @@ def test_zipf_split_off_takes_heavy_path(oracle_mod, monkeypatch):
     drive_both(oracle_mod, cfg_of("tumble", 1000), kstats=ks, **dict(BIG, n=6_000_000, delay=0, jitter=0))
     assert ks.get("tile_split_fire", {}).get("launches", 0) == 0, ks
     assert ks.get("merge_heavy", {}).get("launches", 0) > 0, ks
+
+
+# few buckets (a small key space, configs[0]-shaped): a lane of fewer buckets than CUs fires as
+# ~2 chunk items per CU ("spread"), merged per bucket -- same rows as the one-workgroup fire
+SPREAD = [
+    ("ds_tumble_i64_10k_keys", cfg_of("tumble", 1000, vt="i64", mode="datastream"),
+     dict(n=6_000_000, keys=10_000, batch=1_000_000, rate_per_ms=1_000, delay=0, jitter=0)),
+    ("tumble_f64_4k_keys_ooo", cfg_of("tumble", 1000), dict(n=6_000_000, keys=4_000, batch=1_000_000,
+                                                              rate_per_ms=2_000, delay=300, jitter=500)),
+    ("ds_tumble_f64_min_specials", dict(cfg_of("tumble", 1000, mode="datastream"), aggs=("count_star", "min")),
+     dict(n=4_000_000, keys=10_000, batch=1_000_000, rate_per_ms=1_000, delay=0, jitter=0, specials=0.02)),
+    ("tumble_i64_max", dict(cfg_of("tumble", 1000, vt="i64"), aggs=("count_star", "count", "max")),
+     dict(n=4_000_000, keys=8_000, batch=1_000_000, rate_per_ms=1_000, delay=0, jitter=0)),
+]
+
+
+@pytest.mark.parametrize("name,cfg,kw", SPREAD, ids=[c[0] for c in SPREAD])
+def test_spread_fire_parity(oracle_mod, name, cfg, kw):
+    ks = {}
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    assert ks.get("tile_split_fire", {}).get("launches", 0) > 0, ks
