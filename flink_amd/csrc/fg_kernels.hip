@@ -3695,6 +3695,23 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 }
                 TileWalk w;
                 tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane, t_lo, t_hi);
+#ifdef FG_EXP_PIPE3   // (A/B: three windows in flight per wave, unrolled by three)
+                int32_t ka[kTileRpl], kb[kTileRpl], kc[kTileRpl];
+                int64_t va[kTileRpl], vb[kTileRpl], vc[kTileRpl];
+                uint32_t na = 0, nb = 0, nc = 0;
+                bool ha = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
+                bool hb = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kb, vb, nb);
+                while (ha) {
+                    const bool hc = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kc, vc, nc);
+                    insert(ka, va, na);
+                    if (!hb) break;
+                    ha = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
+                    insert(kb, vb, nb);
+                    if (!hc) break;
+                    hb = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kb, vb, nb);
+                    insert(kc, vc, nc);
+                }
+#else
                 int32_t ka[kTileRpl], kb[kTileRpl];
                 int64_t va[kTileRpl], vb[kTileRpl];
                 uint32_t na = 0, nb = 0;
@@ -3706,6 +3723,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
                     insert(kb, vb, nb);
                 }
+#endif
                 if (__ballot(w.bad) != 0 && lane == 0) atomicOr(p.overflow, 8u);
             }
         }

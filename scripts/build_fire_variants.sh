@@ -16,5 +16,6 @@ build shfl_scan "-DFG_EXP_SHFL_SCAN" &
 build cond_loads "-DFG_EXP_COND_LOADS" &
 build all_old "-DFG_EXP_SHFL_SCAN -DFG_EXP_COND_LOADS" &
 build tile_block "-DFG_EXP_TILE_BLOCK" &
+build pipe3 "-DFG_EXP_PIPE3" &
 wait
 ls -la build_var/*/libflinkgpu.so
