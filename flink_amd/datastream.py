@@ -1,7 +1,17 @@
-"""DataStream keyBy(f0).window(Tumbling|SlidingEventTimeWindows).sum / min / max(1) on
+"""DataStream keyBy(f0).window(Tumbling|SlidingEventTimeWindows).sum / min / max(1), and
+.aggregate(AggregateFunction) with the GPU's COUNT / SUM / AVG / MIN / MAX functions, on
 Tuple2<Long, Long | Double> -- the Python mirror of the JVM shim
-java/.../streaming/runtime/operators/windowing/gpu/GpuWindowOperator.java, with the reference
-WindowOperator's keyed-state layout on both sides of a checkpoint.
+java/.../streaming/runtime/operators/windowing/gpu/GpuWindowOperator.java (and
+GpuAggregateFunctions.java), with the reference WindowOperator's keyed-state layout on both sides
+of a checkpoint.
+
+aggregate (api="aggregate"): WindowedStream.aggregate (WindowedStream.java:283-349) ->
+WindowOperatorBuilder.aggregate (:198-224): an AggregatingStateDescriptor "window-contents" of the
+function's accumulator type. The accumulators of the GPU functions: COUNT a long count; SUM the
+field's sum; AVG (sum, count); MIN / MAX the field's extreme under the field's compareTo (the
+identity when empty: Long.MAX_VALUE / NaN for MIN, Long.MIN_VALUE / -inf for MAX); the result
+(getResult): the count, the sum, sum / count as a double, the extreme. The engine keeps COUNT(*)
+and the value accumulator per (key, slice); a window's accumulator is their merge.
 
 The reference (flink-streaming-java):
   WindowedStream.sum / min / max / minBy / maxBy (WindowedStream.java:671-850) -> aggregate ->
@@ -98,21 +108,34 @@ def _group_reduce(agg: str, f64: bool, key, end, val):
 
 
 class DataStreamWindowOperator:
-    """keyBy(f0).window(...).{sum, min, max}(1) over Tuple2<Long, Long | Double> on the GPU."""
+    """keyBy(f0).window(...).{sum, min, max}(1) (api="reduce"), or .aggregate(f) for the GPU's
+    f in {count, sum, avg, min, max} (api="aggregate"), over Tuple2<Long, Long | Double>.
+
+    Internally every (key, window) holds an accumulator (a0, a1): a0 the value accumulator's bits
+    (sum / min / max), a1 the record count."""
 
     def __init__(self, kind: str, size: int, slide: int = 0, offset: int = 0, val_type: str = "i64",
-                 agg: str = "sum", allowed_lateness: int = 0, purging: bool = False, **engine):
-        if agg not in ("sum", "min", "max"):
+                 agg: str = "sum", allowed_lateness: int = 0, purging: bool = False, api: str = "reduce",
+                 **engine):
+        if api == "reduce" and agg not in ("sum", "min", "max"):
             raise ValueError(f"aggregation {agg!r}: sum, min or max (minBy / maxBy: min / max)")
+        if api == "aggregate" and agg not in ("count", "sum", "avg", "min", "max"):
+            raise ValueError(f"GPU aggregate function {agg!r}: count, sum, avg, min or max")
+        if api not in ("reduce", "aggregate"):
+            raise ValueError(f"api {api!r}: reduce or aggregate")
         self.kind, self.size = kind, int(size)
         self.slide = int(size if kind == "tumble" else slide)
         self.offset = int(offset)
-        self.agg, self.f64 = agg, val_type == "f64"
+        self.api, self.agg, self.f64 = api, agg, val_type == "f64"
+        # the value accumulator's merge: sum (SUM, AVG) or the extreme; COUNT has none
+        self.vkind = "sum" if agg in ("sum", "avg") else agg if agg in ("min", "max") else None
         self.lateness, self.purging = int(allowed_lateness), bool(purging)
         self._engine_kw = dict(engine)
         win = tumbling(size, offset) if kind == "tumble" else hopping(size, slide, offset)
-        self.op = WindowAggOperator(win, aggs=("count_star", agg), val_type=val_type, mode="datastream",
-                                    allowed_lateness=allowed_lateness, purging_trigger=purging, **engine)
+        aggs = ("count_star",) + ((self.vkind,) if self.vkind else ())
+        self.op = WindowAggOperator(win, aggs=aggs, val_type=val_type if self.vkind else "none",
+                                    mode="datastream", allowed_lateness=allowed_lateness,
+                                    purging_trigger=purging, **engine)
         self.watermark = JMIN
         self.restored = {}   # window end -> dict(key, value, pending) of restored (key, window) entries
 
@@ -121,7 +144,7 @@ class DataStreamWindowOperator:
 
     # -- processElement / processWatermark ----------------------------------------------------
     def process_batch(self, key, ts, val):
-        self.op.process_batch(key, ts, val)
+        self.op.process_batch(key, ts, val if self.vkind else None)   # (COUNT reads no field)
 
     def _cleanup_time(self, end):
         """WindowOperator.cleanupTime (:669-673): maxTimestamp + allowedLateness, Long.MAX_VALUE
@@ -132,14 +155,41 @@ class DataStreamWindowOperator:
         c = np.where(c >= max_ts, c, np.int64(JMAX))
         return int(c) if c.ndim == 0 else c
 
+    # accumulators (a0 value bits, a1 count) -------------------------------------------------
+    def _merge(self, a0, a1, b0, b1):
+        """merge(acc a, acc b), a the earlier (restored) one: the value accumulator by its kind,
+        the counts added"""
+        v = reduce_bits(self.vkind, self.f64, a0, b0) if self.vkind else np.zeros(len(a0), np.int64)
+        with np.errstate(over="ignore"):
+            return v, np.asarray(a1, np.int64) + np.asarray(b1, np.int64)
+
+    def _result(self, a0, a1):
+        """the emitted value's bits: the reduced field (reduce), or getResult of the accumulator"""
+        if self.api == "reduce" or self.agg in ("sum", "min", "max"):
+            return a0
+        if self.agg == "count":
+            return a1.astype(np.int64)
+        s = a0.view(np.float64) if self.f64 else a0.astype(np.float64)   # AVG: (double) sum / count
+        return (s / a1.astype(np.float64)).view(np.int64)
+
+    def _image_acc(self, image):
+        """(a0, a1) of an image's entries: reduce keeps the value; aggregate's accumulators --
+        COUNT its count, SUM / MIN / MAX the value, AVG (sum, count)"""
+        n = len(image["key"])
+        a0 = np.asarray(image["value"], np.int64) if "value" in image else np.zeros(n, np.int64)
+        a1 = np.asarray(image["count"], np.int64) if "count" in image else np.ones(n, np.int64)
+        return a0, a1
+
     def process_watermark(self, wm: int) -> np.ndarray:
         """Rows fired by the watermark: (key, value bits, timestamp = window.maxTimestamp(),
         window_end) -- with restored windows reduced in (WindowOperator.emitWindowContents)."""
         r = self.op.process_watermark(wm)
         key = r["key"].astype(np.int64)
         end = r["window_end"].astype(np.int64)
-        val = np.ascontiguousarray(r[self.agg]).view(np.int64).copy()
-        extra_k, extra_e, extra_v = [], [], []
+        a1 = r["count_star"].astype(np.int64).copy()
+        a0 = (np.ascontiguousarray(r[self.vkind]).view(np.int64).copy() if self.vkind
+              else np.zeros(len(key), np.int64))
+        extra_k, extra_e, extra_0, extra_1 = [], [], [], []
         if self.restored:
             for e in list(self.restored):
                 R = self.restored[e]
@@ -150,7 +200,7 @@ class DataStreamWindowOperator:
                     hit = (pos < len(R["key"])) & (R["key"][pos_c] == key[sel])
                     hit &= R["alive"][pos_c]   # (a purged (key, window) holds only the new elements)
                     hs = sel[hit]
-                    val[hs] = reduce_bits(self.agg, self.f64, R["value"][pos_c[hit]], val[hs])
+                    a0[hs], a1[hs] = self._merge(R["a0"][pos_c[hit]], R["a1"][pos_c[hit]], a0[hs], a1[hs])
                     R["pending"][pos_c[hit]] = False
                     if self.purging:   # a fired (key, window) is purged
                         R["alive"][pos_c[hit]] = False
@@ -158,7 +208,8 @@ class DataStreamWindowOperator:
                     fire = R["pending"] & R["alive"]
                     extra_k.append(R["key"][fire])
                     extra_e.append(np.full(int(fire.sum()), e, dtype=np.int64))
-                    extra_v.append(R["value"][fire])
+                    extra_0.append(R["a0"][fire])
+                    extra_1.append(R["a1"][fire])
                     R["pending"][:] = False
                     if self.purging:
                         R["alive"][fire] = False
@@ -168,9 +219,10 @@ class DataStreamWindowOperator:
         if extra_k:
             key = np.concatenate([key] + extra_k)
             end = np.concatenate([end] + extra_e)
-            val = np.concatenate([val] + extra_v)
+            a0 = np.concatenate([a0] + extra_0)
+            a1 = np.concatenate([a1] + extra_1)
         out = np.zeros(len(key), dtype=[("key", "<i8"), ("value", "<i8"), ("timestamp", "<i8"), ("window_end", "<i8")])
-        out["key"], out["value"], out["window_end"], out["timestamp"] = key, val, end, end - 1
+        out["key"], out["value"], out["window_end"], out["timestamp"] = key, self._result(a0, a1), end, end - 1
         return out
 
     @property
@@ -180,26 +232,32 @@ class DataStreamWindowOperator:
     # -- checkpoint ------------------------------------------------------------------------------
     def snapshot(self) -> dict:
         """prepareSnapshotPreBarrier + snapshotState: the reference WindowOperator's keyed state --
-        "window-contents" (key, window_start, window_end, value bits) and "window-timers"
-        (timer_key, timer_window_end, timer_ts)."""
+        "window-contents" (key, window_start, window_end, and the state's value: the reduced
+        field's bits for reduce; the accumulator for aggregate -- `value` (SUM / AVG sum, MIN,
+        MAX bits) and `count` (COUNT, AVG)) and "window-timers" (timer_key, timer_window_end,
+        timer_ts)."""
         self.op.prepare_snapshot_pre_barrier()
         img, _ = self.op.snapshot_state()
         wm = self.watermark
-        k, s, v = img["key"], img["slice_end"], img["sum"]
+        k, s = img["key"], img["slice_end"]
+        v0 = img["sum"] if self.vkind else np.zeros(len(k), np.int64)
+        v1 = img["cnt_star"]
         n = self.size // self.slide
         ks = np.repeat(k, n)
         es = (np.repeat(s, n).reshape(-1, n) + np.arange(n, dtype=np.int64) * self.slide).reshape(-1)
-        vs = np.repeat(v, n)
+        v0s, v1s = np.repeat(v0, n), np.repeat(v1, n)
         live = self._cleanup_time(es) > wm
         if self.purging:   # a fired window's contents were purged
             live &= es - 1 > wm
-        ks, es, vs = ks[live], es[live], vs[live]
+        ks, es, v0s, v1s = ks[live], es[live], v0s[live], v1s[live]
         for e, R in self.restored.items():
-            a = R["alive"]
-            ks = np.concatenate([R["key"][a], ks])   # (restored value first: value1 of the reduce)
+            a = R["alive"]   # (restored accumulator first: value1 of the reduce / merge)
+            ks = np.concatenate([R["key"][a], ks])
             es = np.concatenate([np.full(int(a.sum()), e, dtype=np.int64), es])
-            vs = np.concatenate([R["value"][a], vs])
-        key, end, val = _group_reduce(self.agg, self.f64, ks, es, vs)
+            v0s = np.concatenate([R["a0"][a], v0s])
+            v1s = np.concatenate([R["a1"][a], v1s])
+        key, end, val = _group_reduce(self.vkind or "sum", self.f64 and self.vkind is not None, ks, es, v0s)
+        _, _, cnt = _group_reduce("sum", False, ks, es, v1s)
         # timers: the trigger of a window not fired yet, the cleanup timer with allowed lateness
         trig = end - 1 > wm
         cl = self._cleanup_time(end)
@@ -207,8 +265,13 @@ class DataStreamWindowOperator:
         tk = np.concatenate([key[trig], key[has_cl]])
         te = np.concatenate([end[trig], end[has_cl]])
         tt = np.concatenate([end[trig] - 1, cl[has_cl]])
-        return dict(key=key, window_start=end - self.size, window_end=end, value=val,
-                    timer_key=tk, timer_window_end=te, timer_ts=tt)
+        out = dict(key=key, window_start=end - self.size, window_end=end,
+                   timer_key=tk, timer_window_end=te, timer_ts=tt)
+        if self.vkind:
+            out["value"] = val
+        if self.api == "aggregate" and self.agg in ("count", "avg"):
+            out["count"] = cnt
+        return out
 
     def restore(self, image: dict):
         """initializeState from a reference (or GPU) WindowOperator image: the engine restarts empty
@@ -218,7 +281,7 @@ class DataStreamWindowOperator:
         self.restored = {}
         key = np.asarray(image["key"], dtype=np.int64)
         end = np.asarray(image["window_end"], dtype=np.int64)
-        val = np.asarray(image["value"], dtype=np.int64)
+        a0, a1 = self._image_acc(image)
         tk = np.asarray(image["timer_key"], dtype=np.int64)
         te = np.asarray(image["timer_window_end"], dtype=np.int64)
         tt = np.asarray(image["timer_ts"], dtype=np.int64)
@@ -228,7 +291,7 @@ class DataStreamWindowOperator:
             sel = np.flatnonzero(end == e)
             o = sel[np.argsort(key[sel], kind="stable")]
             kk = key[o]
-            self.restored[int(e)] = dict(key=kk, value=val[o].copy(),
+            self.restored[int(e)] = dict(key=kk, a0=a0[o].copy(), a1=a1[o].copy(),
                                          pending=np.array([(int(x), int(e)) in pend for x in kk], dtype=bool),
                                          alive=np.ones(len(kk), dtype=bool))
 

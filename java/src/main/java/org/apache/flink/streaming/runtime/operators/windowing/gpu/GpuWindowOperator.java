@@ -1,7 +1,10 @@
 /*
  * DataStream keyBy(f0).window(Tumbling|SlidingEventTimeWindows).sum / min / max(1) (and minBy /
- * maxBy, which give the same Tuple2) on Tuple2<Long, Long> or Tuple2<Long, Double> as one operator
- * backed by the GPU engine in FG_MODE_DATASTREAM. Replaces WindowOperator + EventTimeTrigger +
+ * maxBy, which give the same Tuple2) -- GpuWindowOperator.reduce -- and .aggregate(f) with the
+ * GPU's AggregateFunctions (GpuAggregateFunctions: COUNT, SUM, AVG, MIN, MAX) --
+ * GpuWindowOperator.aggregate, WindowedStream.java:283-349 -> WindowOperatorBuilder.aggregate
+ * :198-224, state an AggregatingState of the function's accumulator -- on Tuple2<Long, Long> or
+ * Tuple2<Long, Double> as one operator backed by the GPU engine in FG_MODE_DATASTREAM. Replaces WindowOperator + EventTimeTrigger +
  * HeapReducingState (WindowOperator.java:300-503, built by WindowOperatorBuilder.java:150-172 from
  * WindowedStream.sum / min / max, WindowedStream.java:671-850), with the reference's keyed-state
  * layout on both sides of a checkpoint:
@@ -31,8 +34,10 @@
  */
 package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
+import org.apache.flink.api.common.ExecutionConfig;
 import org.apache.flink.api.common.functions.ReduceFunction;
 import org.apache.flink.api.common.state.ReducingStateDescriptor;
+import org.apache.flink.api.common.state.StateDescriptor;
 import org.apache.flink.api.common.typeinfo.BasicTypeInfo;
 import org.apache.flink.api.common.typeinfo.TypeInformation;
 import org.apache.flink.api.java.tuple.Tuple2;
@@ -41,7 +46,7 @@ import org.apache.flink.metrics.Counter;
 import org.apache.flink.runtime.state.CheckpointableKeyedStateBackend;
 import org.apache.flink.runtime.state.KeyGroupRange;
 import org.apache.flink.runtime.state.StateInitializationContext;
-import org.apache.flink.runtime.state.internal.InternalReducingState;
+import org.apache.flink.runtime.state.internal.InternalAppendingState;
 import org.apache.flink.streaming.api.functions.aggregation.AggregationFunction;
 import org.apache.flink.streaming.api.functions.aggregation.ComparableAggregator;
 import org.apache.flink.streaming.api.functions.aggregation.SumAggregator;
@@ -58,6 +63,7 @@ import org.apache.flink.table.runtime.operators.window.gpu.FgConfig;
 import org.apache.flink.table.runtime.operators.window.gpu.FlinkGpu;
 import org.apache.flink.table.runtime.operators.window.gpu.GpuWindowAggSpec;
 
+import java.io.Serializable;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayList;
@@ -71,24 +77,114 @@ import java.util.Set;
 import java.util.TreeMap;
 import java.util.stream.Collectors;
 
-/** keyBy(f0).window(...).sum / min / max(1) over Tuple2<Long, V> (V = Long or Double) on the GPU. */
-public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Long, V>>
-        implements OneInputStreamOperator<Tuple2<Long, V>, Tuple2<Long, V>>, Triggerable<Long, TimeWindow> {
-    private static final long serialVersionUID = 2L;
+/** keyBy(f0).window(...) reduce / aggregate over Tuple2<Long, V> (V = Long or Double) on the GPU. */
+public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator<OUT>
+        implements OneInputStreamOperator<Tuple2<Long, V>, OUT>, Triggerable<Long, TimeWindow> {
+    private static final long serialVersionUID = 3L;
     private static final String WINDOW_STATE_NAME = "window-contents";   // WindowOperatorBuilder.java:71
     private static final String WINDOW_TIMERS_NAME = "window-timers";    // WindowOperator.java:225
 
-    /** The WindowedStream aggregation: sum(1), min(1) / minBy(1), max(1) / maxBy(1). */
+    /** The WindowedStream reduce: sum(1), min(1) / minBy(1), max(1) / maxBy(1). */
     public enum Aggregation {
         SUM,
         MIN,
         MAX
     }
 
+    /**
+     * The map between a window's state value (ACC: the reduced Tuple2, or an AggregateFunction's
+     * accumulator), its output and the engine's per-(key, window) accumulator: the value
+     * accumulator's bits a0 (SUM / MIN / MAX of f1) and the record count a1.
+     */
+    public interface Accumulation<V, ACC, OUT> extends Serializable {
+        /** the engine's value aggregate (FgConfig.AGG_SUM / AGG_MIN / AGG_MAX), -1: none (COUNT) */
+        int valueAgg();
+
+        /** "window-contents": WindowOperatorBuilder's descriptor for this reduce / aggregate */
+        StateDescriptor<?, ACC> stateDescriptor(String name, TypeInformation<Tuple2<Long, V>> in, ExecutionConfig config);
+
+        ACC fromBits(long key, long a0, long a1);
+
+        long[] toBits(ACC acc);
+
+        /** merge(a, b), a the earlier accumulator (value1 of a reduce) */
+        long[] merge(long a0, long a1, long b0, long b1) throws Exception;
+
+        OUT output(long key, long a0, long a1);
+    }
+
+    /** WindowedStream.sum / min / max: the reference's own SumAggregator / ComparableAggregator. */
+    static final class ReduceAccumulation<V> implements Accumulation<V, Tuple2<Long, V>, Tuple2<Long, V>> {
+        private static final long serialVersionUID = 1L;
+        private final Aggregation aggregation;
+        private final boolean isDouble;
+        private transient ReduceFunction<Tuple2<Long, V>> reducer;
+
+        ReduceAccumulation(Aggregation aggregation, boolean isDouble) {
+            this.aggregation = aggregation;
+            this.isDouble = isDouble;
+        }
+
+        @Override
+        public int valueAgg() {
+            return aggregation == Aggregation.SUM
+                    ? FgConfig.AGG_SUM
+                    : aggregation == Aggregation.MIN ? FgConfig.AGG_MIN : FgConfig.AGG_MAX;
+        }
+
+        @Override
+        public StateDescriptor<?, Tuple2<Long, V>> stateDescriptor(
+                String name, TypeInformation<Tuple2<Long, V>> in, ExecutionConfig config) {
+            // WindowedStream.sum / min / max build exactly these aggregators (:671-850), and
+            // WindowOperatorBuilder.reduce their ReducingStateDescriptor (:165-167)
+            reducer =
+                    aggregation == Aggregation.SUM
+                            ? new SumAggregator<>(1, in, config)
+                            : new ComparableAggregator<>(
+                                    1,
+                                    in,
+                                    aggregation == Aggregation.MIN
+                                            ? AggregationFunction.AggregationType.MIN
+                                            : AggregationFunction.AggregationType.MAX,
+                                    config);
+            return new ReducingStateDescriptor<>(name, reducer, in.createSerializer(config));
+        }
+
+        private long bits(V v) {
+            return isDouble ? Double.doubleToRawLongBits((Double) v) : (Long) v;
+        }
+
+        @SuppressWarnings("unchecked")
+        private V value(long bits) {
+            return (V) (isDouble ? (Object) Double.longBitsToDouble(bits) : (Object) bits);
+        }
+
+        @Override
+        public Tuple2<Long, V> fromBits(long key, long a0, long a1) {
+            return Tuple2.of(key, value(a0));
+        }
+
+        @Override
+        public long[] toBits(Tuple2<Long, V> acc) {
+            return new long[] {bits(acc.f1), 1L};
+        }
+
+        @Override
+        public long[] merge(long a0, long a1, long b0, long b1) throws Exception {
+            return new long[] {bits(reducer.reduce(fromBits(0L, a0, a1), fromBits(0L, b0, b1)).f1), a1 + b1};
+        }
+
+        @Override
+        public Tuple2<Long, V> output(long key, long a0, long a1) {
+            return fromBits(key, a0, a1);
+        }
+    }
+
     private final GpuWindowAggSpec spec;
     private final TypeInformation<Tuple2<Long, V>> inputType;
-    private final Aggregation aggregation;
+    private final Accumulation<V, ACC, OUT> acc;
     private final boolean isDouble;
+    private final boolean hasValue;
     private final boolean purging;
 
     private transient long handle;
@@ -97,25 +193,24 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
     private transient long droppedSeen;
     private transient long currentWatermark;
     private transient Counter numLateRecordsDropped;
-    private transient TimestampedCollector<Tuple2<Long, V>> collector;
-    private transient ReduceFunction<Tuple2<Long, V>> reducer;
-    private transient InternalReducingState<Long, TimeWindow, Tuple2<Long, V>> windowState;
+    private transient TimestampedCollector<OUT> collector;
+    private transient InternalAppendingState<Long, TimeWindow, Tuple2<Long, V>, ACC, ?> windowState;
     private transient InternalTimerService<TimeWindow> timers;
     /** Restored window contents by window end (initializeState), until their cleanup time. */
     private transient TreeMap<Long, Restored> restored;
 
-    /** A restored window: its keys (sorted), value bits, trigger pending, still holding state. */
+    /** A restored window: keys (sorted), accumulators (a0, a1), trigger pending, holding state. */
     private static final class Restored {
-        final TimeWindow window;
         final long[] keys;
-        final long[] values;
+        final long[] a0;
+        final long[] a1;
         final boolean[] pending;
         final boolean[] alive;
 
-        Restored(TimeWindow window, long[] keys, long[] values, boolean[] pending) {
-            this.window = window;
+        Restored(long[] keys, long[] a0, long[] a1, boolean[] pending) {
             this.keys = keys;
-            this.values = values;
+            this.a0 = a0;
+            this.a1 = a1;
             this.pending = pending;
             this.alive = new boolean[keys.length];
             Arrays.fill(alive, true);
@@ -123,52 +218,55 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
     }
 
     /**
-     * spec: windowKind TUMBLE or HOP (sliding), sizeMs / slideMs / offsetMs, allowedLatenessMs,
-     * flags FgConfig.FLAG_PURGING_TRIGGER for PurgingTrigger.of(EventTimeTrigger).
+     * WindowedStream.sum / min / max(1). spec: windowKind TUMBLE or HOP (sliding), sizeMs /
+     * slideMs / offsetMs, allowedLatenessMs, flags FgConfig.FLAG_PURGING_TRIGGER for
+     * PurgingTrigger.of(EventTimeTrigger).
      */
-    public GpuWindowOperator(
+    public static <V> GpuWindowOperator<V, Tuple2<Long, V>, Tuple2<Long, V>> reduce(
             GpuWindowAggSpec spec, TypeInformation<Tuple2<Long, V>> inputType, Aggregation aggregation) {
+        return new GpuWindowOperator<>(spec, inputType, new ReduceAccumulation<>(aggregation, isDouble(inputType)));
+    }
+
+    /** WindowedStream.aggregate(f) with one of GpuAggregateFunctions' functions. */
+    public static <V, ACC, R> GpuWindowOperator<V, ACC, R> aggregate(
+            GpuWindowAggSpec spec,
+            TypeInformation<Tuple2<Long, V>> inputType,
+            GpuAggregateFunctions.GpuAggregate<V, ACC, R> function) {
+        if (function.isDouble != isDouble(inputType)) {
+            throw new IllegalArgumentException("the aggregate function's field type differs from the input's");
+        }
+        return new GpuWindowOperator<>(spec, inputType, function);
+    }
+
+    private static boolean isDouble(TypeInformation<?> inputType) {
         TypeInformation<?> f1 = ((TupleTypeInfo<?>) inputType).getTypeAt(1);
         if (!f1.equals(BasicTypeInfo.LONG_TYPE_INFO) && !f1.equals(BasicTypeInfo.DOUBLE_TYPE_INFO)) {
             throw new IllegalArgumentException("GPU window aggregation of a Long or Double field, got " + f1);
         }
-        this.isDouble = f1.equals(BasicTypeInfo.DOUBLE_TYPE_INFO);
+        return f1.equals(BasicTypeInfo.DOUBLE_TYPE_INFO);
+    }
+
+    private GpuWindowOperator(
+            GpuWindowAggSpec spec, TypeInformation<Tuple2<Long, V>> inputType, Accumulation<V, ACC, OUT> acc) {
+        this.isDouble = isDouble(inputType);
+        this.hasValue = acc.valueAgg() >= 0;
         spec.mode = FgConfig.MODE_DATASTREAM;
-        spec.valType = isDouble ? FgConfig.VAL_F64 : FgConfig.VAL_I64;
-        int agg =
-                aggregation == Aggregation.SUM
-                        ? FgConfig.AGG_SUM
-                        : aggregation == Aggregation.MIN ? FgConfig.AGG_MIN : FgConfig.AGG_MAX;
-        spec.aggs = new int[] {FgConfig.AGG_COUNT_STAR, agg};
+        spec.valType = !hasValue ? FgConfig.VAL_NONE : isDouble ? FgConfig.VAL_F64 : FgConfig.VAL_I64;
+        spec.aggs = hasValue ? new int[] {FgConfig.AGG_COUNT_STAR, acc.valueAgg()} : new int[] {FgConfig.AGG_COUNT_STAR};
         this.spec = spec;
         this.inputType = inputType;
-        this.aggregation = aggregation;
+        this.acc = acc;
         this.purging = (spec.flags & FgConfig.FLAG_PURGING_TRIGGER) != 0;
     }
 
     @Override
+    @SuppressWarnings({"unchecked", "rawtypes"})
     public void initializeState(StateInitializationContext context) throws Exception {
         super.initializeState(context);
-        // the reference's reduce function and state: WindowedStream.sum / min / max build
-        // exactly these aggregators (WindowedStream.java:671-850)
-        reducer =
-                aggregation == Aggregation.SUM
-                        ? new SumAggregator<>(1, inputType, getExecutionConfig())
-                        : new ComparableAggregator<>(
-                                1,
-                                inputType,
-                                aggregation == Aggregation.MIN
-                                        ? AggregationFunction.AggregationType.MIN
-                                        : AggregationFunction.AggregationType.MAX,
-                                getExecutionConfig());
-        ReducingStateDescriptor<Tuple2<Long, V>> desc =
-                new ReducingStateDescriptor<>(
-                        WINDOW_STATE_NAME, reducer, inputType.createSerializer(getExecutionConfig()));
-        @SuppressWarnings("unchecked")
-        InternalReducingState<Long, TimeWindow, Tuple2<Long, V>> st =
-                (InternalReducingState<Long, TimeWindow, Tuple2<Long, V>>)
+        StateDescriptor desc = acc.stateDescriptor(WINDOW_STATE_NAME, inputType, getExecutionConfig());
+        windowState =
+                (InternalAppendingState<Long, TimeWindow, Tuple2<Long, V>, ACC, ?>)
                         getOrCreateKeyedState(new TimeWindow.Serializer(), desc);
-        windowState = st;
     }
 
     @Override
@@ -191,7 +289,7 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
                         null);
         keys = direct(8L * spec.batchRecords);
         timestamps = direct(8L * spec.batchRecords);
-        vals = direct(8L * spec.batchRecords);
+        vals = hasValue ? direct(8L * spec.batchRecords) : null;
         currentWatermark = Long.MIN_VALUE;
         restored = new TreeMap<>();
         restoreImage();
@@ -205,15 +303,6 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
         return isDouble ? Double.doubleToRawLongBits((Double) v) : (Long) v;
     }
 
-    @SuppressWarnings("unchecked")
-    private V valueOf(long bits) {
-        return (V) (isDouble ? (Object) Double.longBitsToDouble(bits) : (Object) bits);
-    }
-
-    private long reduceBits(long a, long b) throws Exception {   // value1 = a (the earlier value)
-        return bitsOf(reducer.reduce(Tuple2.of(0L, valueOf(a)), Tuple2.of(0L, valueOf(b))).f1);
-    }
-
     /** WindowOperator.cleanupTime (:669-673). */
     private long cleanupTime(long end) {
         long maxTs = end - 1;
@@ -225,7 +314,9 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
     public void processElement(StreamRecord<Tuple2<Long, V>> element) throws Exception {
         keys.putLong(8 * count, element.getValue().f0);
         timestamps.putLong(8 * count, element.getTimestamp());
-        vals.putLong(8 * count, bitsOf(element.getValue().f1));
+        if (hasValue) {
+            vals.putLong(8 * count, bitsOf(element.getValue().f1));
+        }
         if (++count == spec.batchRecords) {
             flushBatch();
         }
@@ -238,9 +329,9 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
         }
     }
 
-    private void emit(long key, long end, long bits) {
+    private void emit(long key, long end, long a0, long a1) {
         collector.setAbsoluteTimestamp(end - 1);   // window.maxTimestamp()
-        collector.collect(Tuple2.of(key, valueOf(bits)));
+        collector.collect(acc.output(key, a0, a1));
     }
 
     @Override
@@ -254,23 +345,26 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
                 c.order(ByteOrder.nativeOrder());
             }
         }
-        // columns: key, window_start, window_end, COUNT(*), the aggregate, null mask, rowtime
+        // columns: key, window_start, window_end, COUNT(*)[, the value aggregate], null mask, rowtime
         for (int i = 0; i < n; i++) {
             long key = cols[0].getLong(8 * i);
             long end = cols[2].getLong(8 * i);
-            long bits = cols[4].getLong(8 * i);
+            long a1 = cols[3].getLong(8 * i);
+            long a0 = hasValue ? cols[4].getLong(8 * i) : 0L;
             Restored r = restored.get(end);
             if (r != null) {
                 int at = Arrays.binarySearch(r.keys, key);
                 if (at >= 0 && r.alive[at]) {
-                    bits = reduceBits(r.values[at], bits);
+                    long[] m = acc.merge(r.a0[at], r.a1[at], a0, a1);
+                    a0 = m[0];
+                    a1 = m[1];
                     r.pending[at] = false;
                     if (purging) {
                         r.alive[at] = false;
                     }
                 }
             }
-            emit(key, end, bits);
+            emit(key, end, a0, a1);
         }
         for (Iterator<Map.Entry<Long, Restored>> it = restored.entrySet().iterator(); it.hasNext(); ) {
             Map.Entry<Long, Restored> e = it.next();
@@ -279,7 +373,7 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
             if (end - 1 <= wm) {   // the trigger: pending restored contents without a GPU row
                 for (int j = 0; j < r.keys.length; j++) {
                     if (r.pending[j] && r.alive[j]) {
-                        emit(r.keys[j], end, r.values[j]);
+                        emit(r.keys[j], end, r.a0[j], r.a1[j]);
                         if (purging) {
                             r.alive[j] = false;
                         }
@@ -345,14 +439,14 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
         long wm = currentWatermark;
         long slide = spec.windowKind == FgConfig.TUMBLE ? spec.sizeMs : spec.slideMs;
         long perSlice = spec.sizeMs / slide;
-        // per (key, window): the restored value first (value1 of the reduce), then every slice
-        Map<Long, Map<Long, Long>> contents = new HashMap<>();   // window end -> key -> value bits
+        // per (key, window): the restored accumulator first (value1 of the merge), then every slice
+        Map<Long, Map<Long, long[]>> contents = new HashMap<>();   // window end -> key -> (a0, a1)
         for (Map.Entry<Long, Restored> e : restored.entrySet()) {
             Restored r = e.getValue();
-            Map<Long, Long> w = contents.computeIfAbsent(e.getKey(), x -> new HashMap<>());
+            Map<Long, long[]> w = contents.computeIfAbsent(e.getKey(), x -> new HashMap<>());
             for (int j = 0; j < r.keys.length; j++) {
                 if (r.alive[j]) {
-                    w.put(r.keys[j], r.values[j]);
+                    w.put(r.keys[j], new long[] {r.a0[j], r.a1[j]});
                 }
             }
         }
@@ -360,25 +454,26 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
         for (int i = 0; i < n; i++) {
             long key = cols[0].getLong(8 * i);
             long sliceEnd = cols[1].getLong(8 * i);
-            long bits = cols[4].getLong(8 * i);
+            long a1 = cols[2].getLong(8 * i);
+            long a0 = hasValue ? cols[4].getLong(8 * i) : 0L;
             for (long j = 0; j < perSlice; j++) {
                 long end = sliceEnd + j * slide;
                 if (cleanupTime(end) <= wm || (purging && end - 1 <= wm)) {
                     continue;   // cleared (clearAllState), or fired and purged
                 }
-                Map<Long, Long> w = contents.computeIfAbsent(end, x -> new HashMap<>());
-                Long prev = w.get(key);
-                w.put(key, prev == null ? bits : reduceBits(prev, bits));
+                Map<Long, long[]> w = contents.computeIfAbsent(end, x -> new HashMap<>());
+                long[] prev = w.get(key);
+                w.put(key, prev == null ? new long[] {a0, a1} : acc.merge(prev[0], prev[1], a0, a1));
             }
         }
-        for (Map.Entry<Long, Map<Long, Long>> e : contents.entrySet()) {
+        for (Map.Entry<Long, Map<Long, long[]>> e : contents.entrySet()) {
             long end = e.getKey();
             TimeWindow window = new TimeWindow(end - spec.sizeMs, end);
             long cleanup = cleanupTime(end);
-            for (Map.Entry<Long, Long> kv : e.getValue().entrySet()) {
+            for (Map.Entry<Long, long[]> kv : e.getValue().entrySet()) {
                 setCurrentKey(kv.getKey());
                 windowState.setCurrentNamespace(window);
-                windowState.updateInternal(Tuple2.of(kv.getKey(), valueOf(kv.getValue())));
+                windowState.updateInternal(acc.fromBits(kv.getKey(), kv.getValue()[0], kv.getValue()[1]));
                 if (window.maxTimestamp() > wm) {   // EventTimeTrigger.onElement's timer
                     timers.registerEventTimeTimer(window, window.maxTimestamp());
                 }
@@ -389,7 +484,7 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
         }
     }
 
-    /** initializeState's image: the (key, window) contents and which triggers are pending. */
+    /** initializeState's image: the (key, window) accumulators and which triggers are pending. */
     private void restoreImage() throws Exception {
         List<Tuple2<Long, TimeWindow>> entries =
                 getKeyedStateBackend().<TimeWindow>getKeysAndNamespaces(WINDOW_STATE_NAME)
@@ -410,25 +505,29 @@ public final class GpuWindowOperator<V> extends AbstractStreamOperator<Tuple2<Lo
         for (Tuple2<Long, TimeWindow> kn : entries) {
             setCurrentKey(kn.f0);
             windowState.setCurrentNamespace(kn.f1);
-            Tuple2<Long, V> v = windowState.get();
-            if (v == null) {
+            ACC a = windowState.getInternal();
+            if (a == null) {
                 continue;
             }
+            long[] b = acc.toBits(a);
             byWindow.computeIfAbsent(kn.f1, x -> new ArrayList<>())
-                    .add(new long[] {kn.f0, bitsOf(v.f1), pending.contains(kn) ? 1 : 0});
+                    .add(new long[] {kn.f0, b[0], b[1], pending.contains(kn) ? 1 : 0});
         }
         for (Map.Entry<TimeWindow, List<long[]>> e : byWindow.entrySet()) {
             List<long[]> l = e.getValue();
-            l.sort((a, b) -> Long.compare(a[0], b[0]));
-            long[] k = new long[l.size()];
-            long[] v = new long[l.size()];
-            boolean[] p = new boolean[l.size()];
-            for (int j = 0; j < l.size(); j++) {
+            l.sort((x, y) -> Long.compare(x[0], y[0]));
+            int m = l.size();
+            long[] k = new long[m];
+            long[] a0 = new long[m];
+            long[] a1 = new long[m];
+            boolean[] p = new boolean[m];
+            for (int j = 0; j < m; j++) {
                 k[j] = l.get(j)[0];
-                v[j] = l.get(j)[1];
-                p[j] = l.get(j)[2] != 0;
+                a0[j] = l.get(j)[1];
+                a1[j] = l.get(j)[2];
+                p[j] = l.get(j)[3] != 0;
             }
-            restored.put(e.getKey().getEnd(), new Restored(e.getKey(), k, v, p));
+            restored.put(e.getKey().getEnd(), new Restored(k, a0, a1, p));
         }
     }
 

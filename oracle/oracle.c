@@ -973,18 +973,20 @@ int64_t or_export_timers(const or_op* op, int64_t* key, int64_t* ns, int64_t* ts
     return op->heap_n;
 }
 /* A DataStream operator restored from such an image (initializeState of the heap backend): the
- * reduced value of each (key, window) is all the reference keeps -- its COUNT(*) is taken as 1
- * (never emitted by a DataStream aggregation); the timers are registered as they were. The
+ * reduced value of each (key, window) is all a reduce keeps -- its COUNT(*) is taken as 1 (never
+ * emitted by a DataStream reduce) unless `cnt` gives it (an aggregate function's accumulator
+ * with a count: COUNT, AVG); the timers are registered as they were. The
  * timer watermark restarts at Long.MIN_VALUE (InternalTimerServiceImpl). */
 or_op* or_ds_import(const or_config* cfg, int64_t n, const int64_t* key, const int64_t* end, const int64_t* val,
-                    int64_t nt, const int64_t* tkey, const int64_t* tns, const int64_t* tts, char* err, int errlen) {
+                    const int64_t* cnt, int64_t nt, const int64_t* tkey, const int64_t* tns, const int64_t* tts,
+                    char* err, int errlen) {
     or_op* op = or_open(cfg, err, errlen);
     if (!op) return NULL;
     const int f = cfg->val_type == OR_VAL_F64;
     for (int64_t i = 0; i < n; i++) {
         or_acc* a = state_put(op, key[i], end[i]);
-        a->cnt_star = 1;
-        a->cnt_val = 1;
+        a->cnt_star = cnt ? cnt[i] : 1;   /* (an AggregateFunction's accumulator may hold its count) */
+        a->cnt_val = a->cnt_star;
         a->sum_null = 0;
         if (f) {
             memcpy(&a->sum_d, &val[i], 8);

@@ -104,7 +104,8 @@ int64_t or_ds_export_state(const or_op* op, int64_t* key, int64_t* end, int64_t*
                            int64_t* mx);
 int64_t or_export_timers(const or_op* op, int64_t* key, int64_t* ns, int64_t* ts);
 or_op*  or_ds_import(const or_config* cfg, int64_t n, const int64_t* key, const int64_t* end, const int64_t* val,
-                     int64_t nt, const int64_t* tkey, const int64_t* tns, const int64_t* tts, char* err, int errlen);
+                     const int64_t* cnt, int64_t nt, const int64_t* tkey, const int64_t* tns, const int64_t* tts,
+                     char* err, int errlen);
 
 /* --- slice assigner restatement (SliceAssigners.java) ------------------------- */
 int64_t or_assign_slice_end(const or_op* op, int64_t ts);

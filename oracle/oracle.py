@@ -158,7 +158,7 @@ def lib():
         L.or_export_timers.restype = C.c_int64
         L.or_export_timers.argtypes = [P, P, P, P]
         L.or_ds_import.restype = P
-        L.or_ds_import.argtypes = [C.POINTER(Config), C.c_int64, P, P, P, C.c_int64, P, P, P, C.c_char_p, C.c_int]
+        L.or_ds_import.argtypes = [C.POINTER(Config), C.c_int64, P, P, P, P, C.c_int64, P, P, P, C.c_char_p, C.c_int]
         _lib = L
     return _lib
 
@@ -247,8 +247,9 @@ class OracleOperator:
     # DataStream WindowOperator keyed state ("window-contents" + "window-timers")
     def ds_state_image(self, agg: str = "sum") -> dict:
         """The operator's heap-backend image: per (key, TimeWindow) the reduced value's field bits
-        (agg: the aggregator's field -- "sum", "min" or "max"), and every pending timer
-        (key, window end, timestamp)."""
+        (agg: the aggregator's field -- "sum", "min" or "max"; "avg" / "count": the sum) and the
+        record count (an aggregate function's count), and every pending timer (key, window end,
+        timestamp)."""
         L = lib()
         n = self.state_entries
         a = {k: np.zeros(n, dtype=np.int64) for k in ("key", "window_end", "cnt", "sum", "min", "max")}
@@ -257,7 +258,7 @@ class OracleOperator:
         t = {k: np.zeros(nt, dtype=np.int64) for k in ("timer_key", "timer_window_end", "timer_ts")}
         L.or_export_timers(self._h, *(_ptr(t[k]) for k in ("timer_key", "timer_window_end", "timer_ts")))
         img = dict(key=a["key"], window_end=a["window_end"], window_start=a["window_end"] - self.cfg.size,
-                   value=a[agg])
+                   value=a["sum" if agg in ("avg", "count") else agg], count=a["cnt"])
         img.update(t)
         return img
 
@@ -269,9 +270,12 @@ class OracleOperator:
         cfg.allowed_lateness = int(allowed_lateness)
         cfg.purging = 1 if purging else 0
         c = {k: np.ascontiguousarray(image[k], dtype=np.int64) for k in
-             ("key", "window_end", "value", "timer_key", "timer_window_end", "timer_ts")}
+             ("key", "window_end", "timer_key", "timer_window_end", "timer_ts")}
+        n = len(c["key"])
+        c["value"] = np.ascontiguousarray(image["value"], dtype=np.int64) if "value" in image else np.zeros(n, np.int64)
+        cnt = np.ascontiguousarray(image["count"], dtype=np.int64) if "count" in image else None
         err = C.create_string_buffer(512)
-        h = lib().or_ds_import(C.byref(cfg), len(c["key"]), _ptr(c["key"]), _ptr(c["window_end"]), _ptr(c["value"]),
+        h = lib().or_ds_import(C.byref(cfg), n, _ptr(c["key"]), _ptr(c["window_end"]), _ptr(c["value"]), _ptr(cnt),
                                len(c["timer_key"]), _ptr(c["timer_key"]), _ptr(c["timer_window_end"]),
                                _ptr(c["timer_ts"]), err, 512)
         if not h:

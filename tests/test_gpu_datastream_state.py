@@ -34,6 +34,17 @@ CASES = [
     ("sliding_max_f64_late", "hop",    3000, 1000, "f64", "max", 800,     False,  2000,  200),
     ("sliding_sum_purging",  "hop",    3000, 1000, "i64", "sum", 1000,    True,   2500,  100),
 ]
+# WindowedStream.aggregate(AggregateFunction) with the GPU's functions (GpuAggregateFunctions):
+# "window-contents" is an AggregatingState of the accumulator (count; sum; (sum, count); extreme)
+AGG_CASES = [
+    ("agg_tumble_count",       "tumble", 1000, 0,    "i64", "count", 0,   False, 600,  200),
+    ("agg_tumble_avg_f64",     "tumble", 1000, 0,    "f64", "avg",   700, False, 1500, 100),
+    ("agg_tumble_sum_i64",     "tumble", 1000, 0,    "i64", "sum",   0,   False, 600,  200),
+    ("agg_sliding_avg_i64",    "hop",    3000, 1000, "i64", "avg",   0,   False, 900,  300),
+    ("agg_sliding_min_f64",    "hop",    3000, 1000, "f64", "min",   800, False, 2000, 200),
+    ("agg_sliding_max_i64",    "hop",    2000, 500,  "i64", "max",   0,   False, 700,  100),
+    ("agg_sliding_count_late", "hop",    3000, 1000, "f64", "count", 1200, False, 2500, 100),
+]
 
 
 def _oracle(O, kind, size, slide, vt, lateness, purging):
@@ -46,13 +57,24 @@ def _oracle_field(agg, vt):
     return {"sum": "sum", "min": "min", "max": "max"}[agg] + ("_i" if vt == "i64" else "_d")
 
 
+def _oracle_value(rows, agg, vt):
+    """the emitted value's bits from oracle rows: the field, or the GPU aggregate function's
+    getResult -- COUNT the count, AVG (double) sum / count"""
+    if agg == "count":
+        return rows["cnt_star"].astype(np.int64)
+    if agg == "avg":
+        s = rows["sum_d"] if vt == "f64" else rows["sum_i"].astype(np.float64)
+        return (s / rows["cnt_star"].astype(np.float64)).view(np.int64)
+    return np.ascontiguousarray(rows[_oracle_field(agg, vt)]).view(np.int64)
+
+
 def _sorted(k, e, v):
     o = np.lexsort((e, k))
     return k[o], e[o], v[o]
 
 
 def _assert_values(a, b, vt, agg, ctx):
-    if vt == "f64" and agg == "sum":
+    if (vt == "f64" and agg == "sum") or agg == "avg":
         x, y = a.view(np.float64), b.view(np.float64)
         ok = np.abs(x - y) <= REL * np.maximum(np.abs(x), np.abs(y)) + 1e-300
         assert ok.all(), f"{ctx}: f64 sums differ: {x[~ok][:5]} vs {y[~ok][:5]}"
@@ -62,8 +84,7 @@ def _assert_values(a, b, vt, agg, ctx):
 
 
 def _rows_equal(g, o_rows, vt, agg, ctx):
-    f = _oracle_field(agg, vt)
-    ov = np.ascontiguousarray(o_rows[f]).view(np.int64)
+    ov = _oracle_value(o_rows, agg, vt)
     gk, ge, gv = _sorted(g["key"], g["window_end"], g["value"])
     ok_, oe, ov = _sorted(o_rows["key"].astype(np.int64), o_rows["window_end"].astype(np.int64), ov)
     assert len(gk) == len(ok_), f"{ctx}: {len(gk)} rows vs {len(ok_)}"
@@ -86,11 +107,12 @@ def _drive(g, o, key, ts, val, lo_hi_wm, vt, agg, tag):
             yield orow
 
 
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+@pytest.mark.parametrize("case", CASES + AGG_CASES, ids=[c[0] for c in CASES + AGG_CASES])
 def test_datastream_window_contents_both_ways(oracle_mod, case):
     from flink_amd.datastream import DataStreamWindowOperator
     O = oracle_mod
     name, kind, size, slide, vt, agg, lateness, purging, jitter, delay = case
+    api = "aggregate" if name.startswith("agg_") else "reduce"
     n, keys, batch = 240_000, 3000, 8_000
     key, ts, val, _ = make_stream(n, keys, vt, jitter_ms=jitter, rate_per_ms=20,
                                   specials=0.05 if "spec" in name else 0.0)
@@ -98,7 +120,7 @@ def test_datastream_window_contents_both_ways(oracle_mod, case):
     steps = list(batches_with_watermarks(n, batch, ts, delay))
     cut = len(steps) // 2
     mk = lambda: DataStreamWindowOperator(kind, size, slide, val_type=vt, agg=agg, allowed_lateness=lateness,
-                                          purging=purging, expected_keys=keys, buffer_records=1 << 18)
+                                          purging=purging, api=api, expected_keys=keys, buffer_records=1 << 18)
     g = mk()
     o = _oracle(O, kind, size, slide, vt, lateness, purging)
     for _ in _drive(g, o, key, ts, val, steps[:cut], vt, agg, "before"):
@@ -107,11 +129,23 @@ def test_datastream_window_contents_both_ways(oracle_mod, case):
     img_g = g.snapshot()
     o.prepare_snapshot()
     img_o = o.ds_state_image(agg)
-    gk, ge, gv = _sorted(img_g["key"], img_g["window_end"], img_g["value"])
+    zeros_g = np.zeros(len(img_g["key"]), np.int64)
+    gk, ge, gv = _sorted(img_g["key"], img_g["window_end"], img_g.get("value", zeros_g))
     ok_, oe, ov = _sorted(img_o["key"], img_o["window_end"], img_o["value"])
     assert len(gk) == len(ok_) and np.array_equal(gk, ok_) and np.array_equal(ge, oe), \
         f"window-contents entries differ: {len(gk)} vs {len(ok_)}"
-    _assert_values(gv, ov, vt, agg, "window-contents")
+    if "value" in img_g:   # (the accumulator's value part: SUM / AVG sum, MIN, MAX, the reduced field)
+        _assert_values(gv, ov, vt, "sum" if agg == "avg" else agg, "window-contents")
+    if "count" in img_g:   # (COUNT, AVG: the accumulator's count)
+        _, _, gc = _sorted(img_g["key"], img_g["window_end"], img_g["count"])
+        _, _, oc = _sorted(img_o["key"], img_o["window_end"], img_o["count"])
+        assert np.array_equal(gc, oc), "window-contents counts differ"
+    if api == "reduce":   # (a reduce's image carries no count: the reference's state is the Tuple2)
+        img_o = {k: v for k, v in img_o.items() if k != "count"}
+    elif agg not in ("count", "avg"):
+        img_o = {k: v for k, v in img_o.items() if k != "count"}
+    if agg == "count":
+        img_o = {k: v for k, v in img_o.items() if k != "value"}
     assert np.array_equal(img_g["window_start"], img_g["window_end"] - size)
     live = set(zip(ok_.tolist(), oe.tolist()))
     t_o = {(k, e, t) for k, e, t in zip(img_o["timer_key"].tolist(), img_o["timer_window_end"].tolist(),
@@ -125,10 +159,9 @@ def test_datastream_window_contents_both_ways(oracle_mod, case):
     o_from_g = O.OracleOperator.from_ds_state_image(img_g, **cfg)
     exp = list(_drive(None, o_self, key, ts, val, steps[cut:], vt, agg, "self"))
     got = list(_drive(None, o_from_g, key, ts, val, steps[cut:], vt, agg, "from-gpu"))
-    f = _oracle_field(agg, vt)
     for i, (a, b) in enumerate(zip(got, exp)):
-        ak, ae, av = _sorted(a["key"], a["window_end"], np.ascontiguousarray(a[f]).view(np.int64))
-        bk, be, bv = _sorted(b["key"], b["window_end"], np.ascontiguousarray(b[f]).view(np.int64))
+        ak, ae, av = _sorted(a["key"], a["window_end"], _oracle_value(a, agg, vt))
+        bk, be, bv = _sorted(b["key"], b["window_end"], _oracle_value(b, agg, vt))
         assert np.array_equal(ak, bk) and np.array_equal(ae, be), f"GPU->CPU step {i}: rows differ"
         _assert_values(av, bv, vt, agg, f"GPU->CPU step {i}")
     # -- CPU -> GPU: the GPU restored from the oracle's image continues as that oracle
