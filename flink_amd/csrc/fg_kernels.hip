@@ -3186,6 +3186,7 @@ struct TileWalk {
     bool bad;                   // (reported as overflow flag 8, the record not read)
     int32_t nt;                 // the walk's end tile (exclusive)
     int32_t t0, stride;         // current group's first tile, groups' stride
+    int32_t gsz;                // tiles per group (kTileGroup, fewer for a short tile range)
     uint32_t xn[kTileTPL];      // the next group's directory entries (prefetched)
     uint32_t g_len[kTileTPL], g_st[kTileTPL], g_tot, b;
 };
@@ -3218,15 +3219,21 @@ __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp,
     w.n = (uint32_t)tp.n;
     w.bad = false;
     w.nt = t_hi;
-    w.stride = W * kTileGroup;
-    w.t0 = t_lo + wave * kTileGroup - w.stride;
+    // a short tile range (a small batch: a few hundred tiles) is spread over every wave -- groups
+    // of kTileGroup tiles would leave most waves without one
+    const int32_t per = (t_hi - t_lo + W - 1) / W;
+    w.gsz = per >= kTileGroup ? kTileGroup : (per + kTileTPL - 1) / kTileTPL * kTileTPL;
+    if (w.gsz < kTileTPL) w.gsz = kTileTPL;
+    w.stride = W * w.gsz;
+    w.t0 = t_lo + wave * w.gsz - w.stride;
 #pragma unroll
     for (int q = 0; q < kTileTPL; q++) {
         // (every load issued, the index clamped and the entry masked: a load under a branch would
         // keep the compiler from counting the wave's loads in flight -- s_waitcnt vmcnt(0))
-        const int t = t_lo + wave * kTileGroup + lane * kTileTPL + q;
-        const uint32_t x = gbl(w.col)[t < w.nt ? t : 0];
-        w.xn[q] = t < w.nt ? x : 0u;
+        const int t = t_lo + wave * w.gsz + lane * kTileTPL + q;
+        const bool ok = t < w.nt && lane * kTileTPL + q < w.gsz;
+        const uint32_t x = gbl(w.col)[ok ? t : 0];
+        w.xn[q] = ok ? x : 0u;
         w.g_len[q] = w.g_st[q] = 0;
     }
     w.g_tot = w.b = 0;
@@ -3254,8 +3261,9 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             const int t = w.t0 + lane * kTileTPL + q;
             const uint32_t x = w.xn[q];
             const int tn = t + w.stride;
-            const uint32_t xn = gbl(w.col)[tn < w.nt ? tn : 0];
-            w.xn[q] = tn < w.nt ? xn : 0u;
+            const bool okn = tn < w.nt && lane * kTileTPL + q < w.gsz;
+            const uint32_t xn = gbl(w.col)[okn ? tn : 0];
+            w.xn[q] = okn ? xn : 0u;
             w.g_len[q] = x >> 16;
             base[q] = (uint32_t)t * (uint32_t)kTileRecs + (x & 0xffffu);   // (whole-tile segments)
             w.g_st[q] = sum;   // (local prefix; the wave's exclusive prefix added below)

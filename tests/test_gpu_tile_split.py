@@ -61,7 +61,10 @@ SPREAD = [
 
 
 @pytest.mark.parametrize("name,cfg,kw", SPREAD, ids=[c[0] for c in SPREAD])
-def test_spread_fire_parity(oracle_mod, name, cfg, kw):
+def test_spread_fire_parity(oracle_mod, name, cfg, kw, monkeypatch):
+    # 2^8 regions: 64 buckets per lane, fewer than the CUs (the default 2^10 from 4,096 expected
+    # keys gives 256 buckets, one per CU, and needs no spread)
+    monkeypatch.setenv("FG_MIN_REGION_BITS", "8")
     ks = {}
     drive_both(oracle_mod, cfg, kstats=ks, **kw)
     assert ks.get("tile_split_fire", {}).get("launches", 0) > 0, ks
