@@ -51,7 +51,7 @@ def test_zipf_split_off_takes_heavy_path(oracle_mod, monkeypatch):
 SPREAD = [
     ("ds_tumble_i64_10k_keys", cfg_of("tumble", 1000, vt="i64", mode="datastream"),
      dict(n=6_000_000, keys=10_000, batch=1_000_000, rate_per_ms=1_000, delay=0, jitter=0)),
-    ("tumble_f64_4k_keys_ooo", cfg_of("tumble", 1000), dict(n=6_000_000, keys=4_000, batch=1_000_000,
+    ("tumble_f64_6k_keys_ooo", cfg_of("tumble", 1000), dict(n=6_000_000, keys=6_000, batch=1_000_000,
                                                               rate_per_ms=2_000, delay=300, jitter=500)),
     ("ds_tumble_f64_min_specials", dict(cfg_of("tumble", 1000, mode="datastream"), aggs=("count_star", "min")),
      dict(n=4_000_000, keys=10_000, batch=1_000_000, rate_per_ms=1_000, delay=0, jitter=0, specials=0.02)),
