@@ -102,6 +102,10 @@ struct SliceTable {
     int64_t upper = 0;    // host-side upper bound of entries
     int bits = 0;         // region bits of its layout
     bool has_null = false;   // some entry may count NULL values (else its cnt_null column is all 0)
+    // 16-B entries (fg_kernels.h TableRef): written only by the tile fire with tables, read by
+    // every reader; a table takes the layout of the first writer that finds it empty, and is
+    // widened in place (k_widen_table) before a writer of the wide layout or a region split
+    bool narrow = false;
 };
 
 // One ingest pass: the bucket scan of its records over all lanes; lane l's records sit at
@@ -312,6 +316,7 @@ struct fg_handle {
     // FG_TILE_SPLIT (default on): a skewed tile pass of a TUMBLE / local-phase operator stays on the
     // tiles; its fire splits the hot buckets into chunk items (k_tile_plan / k_tile_merge_parts)
     bool tile_split = true;
+    bool narrow_tables = true;   // FG_NARROW_TABLES: tables written by the tile fire take 16-B entries
     DevBuf tile_dir, tile_hist;
     DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail, sp_icnt;   // split plans + partials
     // skewed-region plan and chunk partial tables
@@ -549,6 +554,7 @@ int table_new(fg_handle* h, int64_t slice_end, std::unique_ptr<SliceTable>* out)
     t->upper = 0;
     t->bits = h->region_bits;
     t->has_null = false;
+    t->narrow = false;
     return FG_OK;
 }
 
@@ -598,7 +604,15 @@ int side_create(fg_handle* h, std::map<int64_t, std::unique_ptr<SliceTable>>& m,
     return FG_OK;
 }
 
-TableRef ref_of(SliceTable* t) { return TableRef{t->data.as<int64_t>(), t->counts.as<uint32_t>()}; }
+TableRef ref_of(SliceTable* t) {
+    return TableRef{t->data.as<int64_t>(), t->counts.as<uint32_t>(), t->narrow ? 1 : 0, 0};
+}
+int widen_table(fg_handle* h, SliceTable* t) {
+    if (!t || !t->narrow) return FG_OK;
+    HIPCHK(h, launch_widen_table(ref_of(t), t->bits, h->stream));
+    t->narrow = false;
+    return FG_OK;
+}
 
 // device scalars: [0] overflow flags (u32), [4] fail count (u32), [8] fired-row counter (u64)
 // (flags and fail count adjacent: one 8-B fill zeroes both and keeps the counter)
@@ -702,6 +716,9 @@ bool ub_cnt_fits(const fg_handle* h) { return h->cnt_bound < ((int64_t)1 << 32);
 
 int job_params(fg_handle* h, int ji, MergeParams* p) {
     const MergeJob& j = h->jobs[(size_t)ji];
+    // the general merge writes the wide layout: a narrow destination is widened first (before the
+    // sources' refs are taken -- it may be one of them)
+    if (int rc = widen_table(h, j.dst)) return rc;
     std::vector<StagedBatch> sb;
     for (const JobBatch& jb : j.batches) sb.push_back(batch_of(h, jb));
     std::vector<TableRef> srcs;
@@ -822,6 +839,7 @@ int grow(fg_handle* h, int nb) {
     const int64_t P2 = (int64_t)1 << nb;
     std::vector<std::unique_ptr<DevBuf>> old;   // freed once the split kernels are done
     auto split = [&](SliceTable* t) -> int {
+        if (int rc0 = widen_table(h, t)) return rc0;   // (the split copies the wide layout)
         std::unique_ptr<DevBuf> nd(new DevBuf()), nc(new DevBuf());
         HIPCHK(h, nd->ensure(sizeof(int64_t) * table_cols(h->mv) * (size_t)table_cap(h->mv) * P2));
         HIPCHK(h, nc->ensure(sizeof(uint32_t) * P2));
@@ -1491,6 +1509,8 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                     job.batches.push_back(JobBatch{st, l, StagedBatch{}, 0});
                     st->busy = true;
                 }
+                // an empty destination takes the 16-B layout (FG_NARROW_TABLES=0: wide, A/B)
+                if (job.dst && job.dst->upper == 0 && h->narrow_tables && !h->mv) job.dst->narrow = true;
                 job.tile = true;
                 job.tbits = ln.passes[0]->bits;
                 job.kclass = job.emit ? K_TILE_FIRE : K_TILE_FLUSH;
@@ -3475,6 +3495,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_TILE_STATE")) hp->tile_state = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_GRID")) hp->tile_grid_force = std::atoi(e);
     if (const char* e = getenv("FG_TILE_SPLIT")) hp->tile_split = std::atoi(e) != 0;
+    if (const char* e = getenv("FG_NARROW_TABLES")) hp->narrow_tables = std::atoi(e) != 0;
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";

@@ -76,10 +76,17 @@ constexpr int kPart2Tile = 8 * kPart2Threads;  // pass-2 records per sub-tile (8
 //   [key i64 x cap][cnt_star i64 x cap][cnt_null i64 x cap][sum (i64 | f64 bits) x cap]
 // cnt_val = cnt_star - cnt_null. A multi-value operator's regions hold kRegionCapMV entries
 // and kNV value columns: [key][cnt_star][cnt_null][v0][v1][v2].
+// A narrow table (round 5: `narrow`, keys32 operators without NULL counts, one value slot, COUNT(*)
+// below 2^32) keeps 16 B per entry in the first half of each region's block: [int32 key][u32
+// cnt_star][value] (cap 4-B keys, cap 4-B counts, then cap 8-B values; the region stride stays
+// the wide one). Its readers recompute the key's mix.
 struct TableRef {
     int64_t* base;
     uint32_t* counts;   // entries per region
+    int32_t narrow;
+    int32_t pad;
 };
+
 
 // One staged batch of one slice lane. The records of region r are
 //   rec[bucket_off[r] - bucket_off[0] .. bucket_off[r + 1] - bucket_off[0])
@@ -403,6 +410,8 @@ hipError_t launch_emit_table(const MergeParams& p, const TableRef& t, hipStream_
 hipError_t launch_export(const ExportParams& p, int32_t regions, hipStream_t s);
 // region split: the table `src` at old_bits -> `dst` at old_bits + shift (each region's
 // entries go to its 2^shift child regions by the next bits of their key mix)
+// a narrow table rewritten wide in place (regions 2^bits)
+hipError_t launch_widen_table(const TableRef& t, int32_t bits, hipStream_t s);
 hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift, int32_t mv,
                               hipStream_t s);
 hipError_t launch_heavy_plan(const HeavyPlan& hp, hipStream_t s);

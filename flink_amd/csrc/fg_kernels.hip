@@ -72,6 +72,23 @@ __device__ __forceinline__ void st_rec12(void* base, uint64_t i, int64_t key, in
     *((uint64_t __attribute__((address_space(1)))*)(b + 256) + (i & 63)) = (uint64_t)val;
 }
 
+// Slice-table entry i of a region block b, wide ([mix][cnt_star][cnt_null][v0..]) or narrow
+// ([int32 key][u32 cnt_star][v], fg_kernels.h TableRef)
+typedef const int64_t __attribute__((address_space(1)))* gtab_t;
+__device__ __forceinline__ int64_t tab_mix(gtab_t b, int cap, uint32_t i, bool nar) {
+    return nar ? mix_of((int64_t)((const int32_t __attribute__((address_space(1)))*)b)[i]) : b[i];
+}
+__device__ __forceinline__ int32_t tab_key32(gtab_t b, int cap, uint32_t i, bool nar) {
+    return nar ? ((const int32_t __attribute__((address_space(1)))*)b)[i] : (int32_t)key_of(b[i]);
+}
+__device__ __forceinline__ int64_t tab_cs(gtab_t b, int cap, uint32_t i, bool nar) {
+    return nar ? (int64_t)((const uint32_t __attribute__((address_space(1)))*)b)[cap + i] : b[cap + i];
+}
+__device__ __forceinline__ int64_t tab_cn(gtab_t b, int cap, uint32_t i, bool nar) { return nar ? 0 : b[2 * cap + i]; }
+__device__ __forceinline__ int64_t tab_v(gtab_t b, int cap, uint32_t i, bool nar, int q = 0) {
+    return nar ? b[cap + i] : b[(3 + q) * cap + i];
+}
+
 // Tile-staged records (k_tile_part1 -> k_tile_fire / k_tile_mat): packed 12-B records {int32 key,
 // value bits} at 12 * i, one dwordx3 access each (4-B aligned). The tiles are written whole and in
 // order (a wave's stores are 768 contiguous bytes), and the fire gathers a bucket's fragments of a
@@ -1763,6 +1780,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     __shared__ uint32_t s_rng[3][kMaxMergeBatches][2];         // fast path: [ri % 3][batch] = (beg, end)
     __shared__ uint32_t s_soff[kMaxSrcFlat + 1];               // source tables: entry prefix of the region
     __shared__ const int64_t* s_sbase[kMaxSrcFlat];            //   and each table's region base
+    __shared__ uint8_t s_snar[kMaxSrcFlat];                     //   and layout (narrow tables)
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     constexpr int cap = MV ? kRegionCapMV : kRegionCap;   // table entries per region
@@ -2014,6 +2032,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             if (tid < nsrc) {
                 s_soff[tid + 1] = x;
                 s_sbase[tid] = p.src[tid].base + (int64_t)r * cols * cap;
+                s_snar[tid] = p.src[tid].narrow ? 1 : 0;
             }
             if (tid == 0) s_soff[0] = 0;
         }
@@ -2053,9 +2072,10 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     while (s_soff[j + 1] <= f) j++;
                     const uint32_t i = f - s_soff[j];
                     const auto base = gbl(s_sbase[j]);
-                    k[u] = base[i];
-                    cs[u] = base[cap + i];
-                    sm[u][0] = base[3 * cap + i];
+                    const bool nar = s_snar[j] != 0;
+                    k[u] = tab_mix(base, cap, i, nar);
+                    cs[u] = tab_cs(base, cap, i, nar);
+                    sm[u][0] = tab_v(base, cap, i, nar);
                 }
                 uint32_t home[kSrcU];
                 int4 bq[kSrcU];
@@ -2098,11 +2118,12 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     while (s_soff[j + 1] <= f) j++;
                     const uint32_t i = f - s_soff[j];
                     const auto base = gbl(s_sbase[j]);
-                    k[u] = base[i];
-                    cs[u] = base[cap + i];
-                    cn[u] = ((p.src_null_mask >> j) & 1ull) ? base[2 * cap + i] : 0;
+                    const bool nar = s_snar[j] != 0;   // (narrow: one value slot, no NULL counts)
+                    k[u] = tab_mix(base, cap, i, nar);
+                    cs[u] = tab_cs(base, cap, i, nar);
+                    cn[u] = ((p.src_null_mask >> j) & 1ull) ? tab_cn(base, cap, i, nar) : 0;
 #pragma unroll
-                    for (int q = 0; q < NVS; q++) sm[u][q] = base[(3 + q) * cap + i];
+                    for (int q = 0; q < NVS; q++) sm[u][q] = tab_v(base, cap, i, nar, q);
                     mk[u] = ((p.mark_mask >> j) & 1ull) != 0;
                     if ((p.markonly_mask >> j) & 1ull) cs[u] = 0;   // a mark-only source adds nothing
                 }
@@ -2129,16 +2150,18 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 const TableRef src = p.src[j];
                 const uint32_t n = gbl(src.counts)[r];
                 const auto base = gbl(src.base + (int64_t)r * cols * cap);
+                const bool nar = src.narrow != 0;
                 const bool mkj = j < 64 && ((p.mark_mask >> j) & 1ull) != 0;
                 const bool moj = j < 64 && ((p.markonly_mask >> j) & 1ull) != 0;
                 for (uint32_t i = tid; i < n; i += T) {
-                    const int slot = lds_find_or_insert<C, MV>(t, base[i], full);
+                    const int slot = lds_find_or_insert<C, MV>(t, tab_mix(base, cap, i, nar), full);
                     if (slot < 0) continue;
-                    if (base[cap + i] && !moj) {
+                    const int64_t csi = tab_cs(base, cap, i, nar);
+                    if (csi && !moj) {
                         int64_t vv[NVS];
 #pragma unroll
-                        for (int q = 0; q < NVS; q++) vv[q] = base[(3 + q) * cap + i];
-                        lds_add<C, MV>(t, slot, (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i],
+                        for (int q = 0; q < NVS; q++) vv[q] = tab_v(base, cap, i, nar, q);
+                        lds_add<C, MV>(t, slot, (unsigned long long)csi, (unsigned long long)tab_cn(base, cap, i, nar),
                                        vv, vt, p);
                     }
                     if constexpr (!C) if (mkj) atomicOr(&t.cn[slot], kMarkBit);
@@ -2392,11 +2415,12 @@ __global__ __launch_bounds__(kEmitThreads) void k_emit_table(MergeParams p, Tabl
     if ((int64_t)(b + n) > p.out_cap) return;
     const int cap = table_cap(p.mv);
     const auto base = gbl(t.base + (int64_t)r * table_cols(p.mv) * cap);
+    const bool nar = t.narrow != 0;
     for (uint32_t i = threadIdx.x; i < n; i += kEmitThreads) {
         int64_t vv[kNV];
-        for (int q = 0; q < (p.mv ? kNV : 1); q++) vv[q] = base[(3 + q) * cap + i];
-        write_row(p, b + i, base[i], (unsigned long long)base[cap + i], (unsigned long long)base[2 * cap + i], vv,
-                  p.val_type);
+        for (int q = 0; q < (p.mv ? kNV : 1); q++) vv[q] = tab_v(base, cap, i, nar, q);
+        write_row(p, b + i, tab_mix(base, cap, i, nar), (unsigned long long)tab_cs(base, cap, i, nar),
+                  (unsigned long long)tab_cn(base, cap, i, nar), vv, p.val_type);
     }
 }
 
@@ -2678,15 +2702,16 @@ __global__ __launch_bounds__(256) void k_export(ExportParams p) {
     const int r = blockIdx.x;
     const uint32_t n = p.t.counts[r];
     const int cap = table_cap(p.mv);
-    const int64_t* base = p.t.base + (int64_t)r * table_cols(p.mv) * cap;
+    const auto base = gbl(p.t.base + (int64_t)r * table_cols(p.mv) * cap);
+    const bool nar = p.t.narrow != 0;
     const uint64_t o = p.region_off[r];
     for (uint32_t i = threadIdx.x; i < n; i += 256) {
-        const int64_t cs = base[cap + i], cn = base[2 * cap + i];
-        p.out_key[o + i] = key_of(base[i]);
+        const int64_t cs = tab_cs(base, cap, i, nar), cn = tab_cn(base, cap, i, nar);
+        p.out_key[o + i] = nar ? (int64_t)tab_key32(base, cap, i, nar) : key_of(base[i]);
         p.out_slice[o + i] = p.slice_end;
         p.out_cnt_star[o + i] = cs;
         p.out_cnt_val[o + i] = cs - cn;
-        p.out_sum[o + i] = base[3 * cap + i];
+        p.out_sum[o + i] = tab_v(base, cap, i, nar);
         if (p.mv) {
             p.out_v1[o + i] = base[4 * cap + i];
             p.out_v2[o + i] = base[5 * cap + i];
@@ -2728,9 +2753,49 @@ __global__ __launch_bounds__(kSplitThreads) void k_split_table(TableRef src, Tab
     for (int c = threadIdx.x; c < nch; c += kSplitThreads) dst.counts[(int64_t)r * nch + c] = s_cnt[c];
 }
 
+// A narrow table widened in place (a writer that writes the wide layout -- the general merge --
+// or a region split): one workgroup per region reads its entries (the narrow block is the first
+// half of the wide one), then writes them wide.
+constexpr int kWidenThreads = 1024;
+__global__ __launch_bounds__(kWidenThreads) void k_widen_table(TableRef t) {
+    constexpr int PER = (kRegionCap + kWidenThreads - 1) / kWidenThreads;
+    const int r = blockIdx.x;
+    constexpr int cap = kRegionCap;
+    const uint32_t n = gbl(t.counts)[r];
+    int64_t* b = t.base + (int64_t)r * 4 * cap;
+    int32_t k[PER];
+    int64_t cs[PER], v[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const uint32_t i = threadIdx.x + q * kWidenThreads;
+        if (i < n) {
+            k[q] = tab_key32(gbl(b), cap, i, true);
+            cs[q] = tab_cs(gbl(b), cap, i, true);
+            v[q] = tab_v(gbl(b), cap, i, true);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const uint32_t i = threadIdx.x + q * kWidenThreads;
+        if (i < n) {
+            b[i] = mix_of((int64_t)k[q]);
+            b[cap + i] = cs[q];
+            b[2 * cap + i] = 0;
+            b[3 * cap + i] = v[q];
+        }
+    }
+}
+
+hipError_t launch_widen_table(const TableRef& t, int32_t bits, hipStream_t s) {
+    if (!t.narrow || bits < 0 || bits > 13) return hipErrorInvalidValue;
+    fg_launch(k_widen_table, dim3(1u << bits), dim3(kWidenThreads), 0, s, t);
+    return hipGetLastError();
+}
+
 hipError_t launch_split_table(const TableRef& src, const TableRef& dst, int32_t old_bits, int32_t shift, int32_t mv,
                               hipStream_t s) {
-    if (shift < 1 || old_bits < 0 || old_bits + shift > 13) return hipErrorInvalidValue;
+    if (shift < 1 || old_bits < 0 || old_bits + shift > 13 || src.narrow || dst.narrow) return hipErrorInvalidValue;
     fg_launch(k_split_table, dim3(1u << old_bits), dim3(kSplitThreads), 0, s, src, dst, old_bits, shift, mv);
     return hipGetLastError();
 }
@@ -3507,11 +3572,13 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             __syncthreads();
             const uint32_t NE = nrange ? s_total : 0u;
             for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
-                int64_t mk[kSrcU], cs[kSrcU], v[kSrcU];
+                int64_t cs[kSrcU], v[kSrcU];
+                int32_t mk[kSrcU];
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
                     const uint32_t i = i0 + u * T + tid;
-                    mk[u] = cs[u] = v[u] = 0;
+                    mk[u] = 0;
+                    cs[u] = v[u] = 0;
                     if (i >= NE) continue;
                     int lo = 0, hi = nrange;   // the range of entry i: the last base <= i
                     while (hi - lo > 1) {
@@ -3519,16 +3586,18 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                         if (s_rb[mid] <= i) lo = mid;
                         else hi = mid;
                     }
-                    const int64_t* base = p.src[lo / nreg].base + (int64_t)(r_lo + lo % nreg) * 4 * cap;
+                    const TableRef& sr = p.src[lo / nreg];
+                    const auto base = gbl(sr.base + (int64_t)(r_lo + lo % nreg) * 4 * cap);
                     const uint32_t e = i - s_rb[lo];
-                    mk[u] = gbl(base)[e];
-                    cs[u] = gbl(base)[cap + e];
-                    v[u] = gbl(base)[3 * cap + e];
+                    const bool nar = sr.narrow != 0;   // (the operator's keys fit 32 bits: a mix's key is its int32)
+                    mk[u] = tab_key32(base, cap, e, nar);
+                    cs[u] = tab_cs(base, cap, e, nar);
+                    v[u] = tab_v(base, cap, e, nar);
                 }
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
                     if (i0 + u * T + tid >= NE) continue;
-                    const int sl = slot_of((int32_t)key_of(mk[u]));
+                    const int sl = slot_of(mk[u]);
                     if (sl < 0) {
                         full = true;
                         continue;
@@ -3893,10 +3962,17 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 const int sl = s_map[i];
                 const uint32_t at = i - s_rb[lo];
                 int64_t* db = p.dst.base + (int64_t)(r_lo + lo) * 4 * cap;
-                db[at] = mix_of(sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl]);
-                db[cap + at] = (int64_t)t_cs[sl];
-                db[2 * cap + at] = 0;
-                db[3 * cap + at] = lds_repr(vt, (int64_t)t_v[sl]);
+                const int32_t k32 = sl == S ? kEmpty32 : t_key[sl];
+                if (p.dst.narrow) {   // 16-B entries: [int32 key][u32 COUNT(*)][value]
+                    reinterpret_cast<int32_t*>(db)[at] = k32;
+                    reinterpret_cast<uint32_t*>(db)[cap + at] = t_cs[sl];
+                    db[cap + at] = lds_repr(vt, (int64_t)t_v[sl]);
+                } else {
+                    db[at] = mix_of((int64_t)k32);
+                    db[cap + at] = (int64_t)t_cs[sl];
+                    db[2 * cap + at] = 0;
+                    db[3 * cap + at] = lds_repr(vt, (int64_t)t_v[sl]);
+                }
             }
         }
         __syncthreads();   // the table is cleared for the next item
