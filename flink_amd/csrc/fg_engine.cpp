@@ -314,7 +314,7 @@ struct fg_handle {
     bool tile_skew = false;   // a tile pass saw hot-key skew: later batches take the two-pass partition
                               // (a performance hint kept across fg_reset)
     // FG_TILE_SPLIT (default on): a skewed tile pass of a TUMBLE / local-phase operator stays on the
-    // tiles; its fire splits the hot buckets into chunk items (k_tile_plan / k_tile_merge_parts)
+    // tiles; its fire splits the hot buckets into chunk items (k_tile_plan, k_tile_fire's merge)
     bool tile_split = true;
     bool narrow_tables = true;   // FG_NARROW_TABLES: tables written by the tile fire take 16-B entries
     DevBuf tile_dir, tile_hist;
@@ -1189,7 +1189,8 @@ bool tile_split_ok(const fg_handle* h) { return h->tile_split && (h->w.kind == T
 
 // The split fire of a lane holding a skewed tile pass (fg_kernels.h TileSplit): k_tile_plan cuts
 // the buckets above max(kTileChunk, the lane's mean) into chunk items, k_tile_fire aggregates
-// every item (chunks into partial entries), k_tile_merge_parts merges each split bucket's chunks
+// every item (chunks into partial entries), and again over the split buckets (merge = 1), each
+// merging its chunks -- with the job's source and destination tables when it has them
 // into its rows. f is the job's TileFire (tile_job_params).
 // The plan's buffers (TileSplit) for `fill` records over nb buckets in items of at least `chunk`
 // records (0: kTileChunk), the counts zeroed on the stream; materialize also keeps per-item
@@ -1249,7 +1250,10 @@ int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f, uint32_t chunk) {
     f.hot = 1;
     HIPCHK(h, launch_tile_plan(f, h->stream));
     HIPCHK(h, launch_tile_fire(f, (int)std::min<int64_t>(max_items, h->merge_grid), h->stream));
-    HIPCHK(h, launch_tile_merge_parts(f, std::min(nb, h->merge_grid), h->stream));
+    TileFire fm = f;   // the split buckets: their chunks' partial entries merged (+ tables, rows)
+    fm.merge = 1;
+    fm.hot = 0;
+    HIPCHK(h, launch_tile_fire(fm, std::min(nb, h->merge_grid), h->stream));
     return FG_OK;
 }
 
@@ -1499,7 +1503,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             // written back by the same workgroups -- no materialized pass, no staged pass 2
             // (an item's (source, region) ranges fit the kernel's kTileMaxRegions prefix slots)
             const int tsub = kTileBits + h->region_bits - ln.passes[0]->bits;
-            bool ok = tile_fire_ok(h, ln) && h->keys32 && ub_cnt_fits(h) && job.srcs.size() <= 8 &&
+            bool ok = tile_fire_ok(h, ln, tile_split_ok(h)) && h->keys32 && ub_cnt_fits(h) && job.srcs.size() <= 8 &&
                       tsub <= kTileMaxRegionBits &&
                       ((int64_t)job.srcs.size() << tsub) <= (int64_t)kTileMaxRegions &&
                       !(job.emit && h->retain && !h->local);
@@ -1521,9 +1525,16 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 TileFire f{};
                 rc = tile_job_params(h, ji, &f);
                 if (rc) return rc;
+                bool skewed = false;   // (a skewed pass: the split fire, with the job's tables)
+                for (const Staged* st : ln.passes) skewed = skewed || st->skew;
                 {
-                    KTimer kt(h, kc, ln.fill);
-                    HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                    KTimer kt(h, skewed ? K_TILE_SPLIT : kc, ln.fill);
+                    if (skewed) {
+                        rc = tile_split_fire(h, ln, f, 0);
+                        if (rc) return rc;
+                    } else {
+                        HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                    }
                 }
                 if (kc == K_TILE_FIRE) fire_class = K_TILE_FIRE;
                 goto merged;

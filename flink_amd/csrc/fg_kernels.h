@@ -466,7 +466,8 @@ struct TilePass {
 // Skewed tile passes (hot keys, Zipf): a bucket whose records exceed kTileChunk is fired by
 // several workgroups -- chunk items over equal ranges of its tiles, each aggregating its range in
 // an LDS table (hot keys pre-combined across the wave) and writing the table as partial entries
-// -- and the chunks' partials are then merged per bucket (k_tile_merge_parts) into the rows; the
+// -- and the chunks' partials are then merged per bucket (k_tile_fire with merge = 1) into the
+// rows / the destination table; the
 // other buckets fire as usual. k_tile_plan lists the items on the device.
 constexpr int kTileChunk = 1 << 16;           // records per chunk item of a split bucket
 constexpr int kMaxTilePasses = 8;             // passes one split fire walks
@@ -508,6 +509,8 @@ struct TileFire {
     // m.region_bits: m.retry_list[0 .. m.n_retry), or (split) sp.items[0 .. *sp.n_items)
     int32_t split;            // sp holds a plan (k_tile_plan): a skewed pass's fire
     int32_t hot;              // split fire: pre-combine a wave's records of a hot key (SUM-family ops)
+    int32_t merge;            // split fire, second launch: items = the split buckets (sp.split_b), each
+                              // merging its chunks' partial entries (with its tables, rows, destination)
     TileSplit sp;
 };
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s);
@@ -516,9 +519,10 @@ hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s);
 hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
                             const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot, hipStream_t s);
 hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s);
-// a split fire: the plan (one workgroup), the fire over its items, the merge of split buckets
+// a split fire: the plan (one workgroup), then launch_tile_fire over its items and again with
+// merge = 1 over the split buckets
 hipError_t launch_tile_plan(const TileFire& f, hipStream_t s);
-hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStream_t s);
+
 // materialize, over the items of a plan (launch_tile_plan of the one pass with sp.chunk =
 // kTileMatChunk): per-region counts of the pass's lane added into hist[P] at `bits` (zeroed
 // first) and kept per item in plan.icnt, then -- after the exclusive scan into bucket_off, copied

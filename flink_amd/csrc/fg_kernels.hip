@@ -3468,15 +3468,19 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     const int64_t vinit = lds_repr(vt, val_identity(vt));
     const int sub = p.region_bits - f.tbits;          // current region bits above the passes'
     const bool retry = p.retry_list != nullptr;
-    const bool split = !TAB && f.split != 0;          // items planned by k_tile_plan (a skewed pass)
+    const bool split = f.split != 0;                  // items planned by k_tile_plan (a skewed pass)
+    const bool merge = split && f.merge != 0;         // the split buckets' merge of their chunks' partials
     __shared__ int s_item;   // split: the item fetched by workgroup (dynamic: chunk items vary in size)
-    const int NI = retry ? p.n_retry : split ? (int)*gbl(f.sp.n_items) : 1 << (f.tbits - kTileBits);
+    const int NI = retry ? p.n_retry
+                   : merge ? (int)*gbl(f.sp.n_split)
+                   : split ? (int)*gbl(f.sp.n_items)
+                           : 1 << (f.tbits - kTileBits);
     const int G = gridDim.x;
     const bool xcd = !retry && !split && G % 8 == 0;  // consecutive buckets on one XCD (shared L2 lines)
     for (int k = 0;; k++) {
         const int b = (int)blockIdx.x;
         int x = xcd ? k * G + (b % 8) * (G / 8) + b / 8 : b + k * G;
-        if (split) {   // (s_item's previous value was read before this iteration's barriers)
+        if (split && !merge) {   // (s_item's previous value was read before this iteration's barriers)
             if (tid == 0) s_item = (int)atomicAdd(f.sp.next_item, 1u);
             __syncthreads();
             x = s_item;
@@ -3484,11 +3488,19 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
         } else if (k * G >= NI) {
             break;
         }
-        const bool live = x < NI;
+        bool live = x < NI;
         int r_lo = 0, r_hi = 0, item = 0;
         int32_t g_lo = 0, g_hi = 0x7fffffff, part = -1;   // (split: the item's tile range, chunk ordinal)
+        int32_t mc0 = 0, mck = 0;                          // (merge: the bucket's chunks)
         if (live) {
-            if (retry) {
+            if (merge) {
+                item = f.sp.split_b[x];
+                mc0 = f.sp.split_c0[x];
+                mck = f.sp.split_k[x];
+                r_lo = item << (sub + kTileBits);
+                r_hi = (item + 1) << (sub + kTileBits);
+                live = *gbl(&f.sp.bfail[item]) == 0u;   // (a failed chunk: the retry redoes the bucket)
+            } else if (retry) {
                 r_lo = gbl(p.retry_list)[x];
                 r_hi = r_lo + 1;
                 item = r_lo >> (sub + kTileBits);
@@ -3506,6 +3518,8 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 r_hi = (x + 1) << (sub + kTileBits);
             }
         }
+        // a chunk of a split bucket writes partial entries only (no resident state, rows or table)
+        const bool to_part = split && !merge && part >= 0;
         for (int i = tid; i <= S + 1; i += T) {
             t_key[i] = kEmpty32;
             t_cs[i] = 0;
@@ -3539,7 +3553,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
             return -1;
         };
-        if (TAB && p.n_src > 0) {
+        if (TAB && p.n_src > 0 && !to_part) {
             // resident state first: the item's regions of every source table (keys as mixes; the
             // operator's keys fit 32 bits, so a mix's key is its int32) -- one flat sequence over
             // the (source, region) ranges (their counts' exclusive prefix in s_rb, wave 0), every
@@ -3607,7 +3621,26 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 }
             }
         }
-        if (live) {
+        if (live && merge) {
+            // the split bucket's chunks: their partial entries (int32 key, COUNT(*), the value's LDS
+            // form) into the table -- the value combined as the chunks combined their records
+            for (int c = mc0; c < mc0 + mck; c++) {
+                const uint32_t off = f.sp.part_off[c], n = f.sp.part_n[c];
+                if ((uint64_t)off + n > (uint64_t)f.sp.part_cap) {   // (never: a failed chunk fails its bucket)
+                    if (tid == 0) atomicOr(p.overflow, 2u);
+                    continue;
+                }
+                for (uint32_t i = tid; i < n; i += T) {
+                    const int sl = slot_of(f.sp.p_key[off + i]);
+                    if (sl < 0) {
+                        full = true;
+                        continue;
+                    }
+                    atomicAdd(&t_cs[sl], f.sp.p_cs[off + i]);
+                    lds_val(&t_v[sl], lds_repr(vt, (int64_t)f.sp.p_v[off + i]), vt, true);
+                }
+            }
+        } else if (live) {
             // one window's records into the table, one probe loop per record (the plain fire)
             auto insert_plain = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
                 uint32_t hm[kTileRpl];
@@ -3821,7 +3854,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             const uint64_t bal = __ballot(occ);
             if (occ) occ_mask |= 1u << r;
             if (lane == 0) s_grp[r * W + wave] = (uint32_t)__popcll(bal);
-            if (dst && occ && live) atomicAdd(&s_rc[region_of(slot)], 1u);
+            if (dst && !to_part && occ && live) atomicAdd(&s_rc[region_of(slot)], 1u);
         }
         __syncthreads();
         if (wave == 0) {
@@ -3847,12 +3880,11 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
             const uint32_t total = __shfl(xs, 63);
             bool over = false;   // a destination region above its capacity: the item fails
-            if (dst)
+            if (dst && !to_part)
                 for (int q = lane; q < r_hi - r_lo; q += 64) over = over || s_rc[q] > (uint32_t)kRegionCap;
             over = __ballot(over) != 0;
             if (lane == 0) {
                 unsigned int fl = s_flags | (over ? 4u : 0u);
-                const bool to_part = split && part >= 0;
                 if (live && !(fl & 4u) && !to_part && (!TAB || p.emit)) {
                     const unsigned long long ob = atomicAdd(p.out_count, (unsigned long long)total);
                     s_out_base = ob;
@@ -3890,7 +3922,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 (uint16_t)(r < kRounds - 1 ? r * T + tid : S);
         }
         __syncthreads();
-        if (live && split && part >= 0 && !(fl & 6u)) {   // partial entries (LDS repr), merged later
+        if (live && to_part && !(fl & 6u)) {   // partial entries (LDS repr), merged later
             const uint32_t total = s_total;
             const uint32_t ob = (uint32_t)s_out_base;
             for (uint32_t i = tid; i < total; i += T) {
@@ -3908,7 +3940,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 write_row_k(p, ob + i, sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl], t_cs[sl], 0ull, &v, vt);
             }
         }
-        if (TAB && dst && live && !(fl & 5u)) {
+        if (TAB && dst && live && !to_part && !(fl & 5u)) {
             // the regions' counts and bases (exclusive prefix, wave 0), the rank -> slot map
             // rebuilt region-major (s_map is free once the rows are out), then every region's
             // entries written at consecutive ranks: full-width stores into each SoA column
@@ -3993,11 +4025,13 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
     const dim3 g((unsigned)workgroups), b(kTileFireThreads);
     const bool tab = f.m.has_dst || f.m.n_src > 0;
     // the value op compiled in: SUM / AVG over DOUBLE, BIGINT, or COUNT only
-    if (f.split && (tab || !f.sp.next_item)) return hipErrorInvalidValue;
-    const bool hot = f.hot && f.split && f.m.val_type >= 0 && f.m.val_type <= 2;
+    if (f.split && !f.merge && !f.sp.next_item) return hipErrorInvalidValue;
+    if (f.merge && (!f.split || !f.sp.split_b || !f.sp.n_split)) return hipErrorInvalidValue;
+    const bool hot = f.hot && f.split && !f.merge && f.m.val_type >= 0 && f.m.val_type <= 2;
 #define FG_TILE_FIRE(V)                                                     \
     do {                                                                    \
-        if (tab) fg_launch((k_tile_fire<V, true, false>), g, b, 0, s, f);  \
+        if (tab && hot) fg_launch((k_tile_fire<V, true, true>), g, b, 0, s, f); \
+        else if (tab) fg_launch((k_tile_fire<V, true, false>), g, b, 0, s, f);  \
         else if (hot) fg_launch((k_tile_fire<V, false, true>), g, b, 0, s, f); \
         else fg_launch((k_tile_fire<V, false, false>), g, b, 0, s, f);     \
     } while (0)
@@ -4016,7 +4050,8 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
 // passes' btot); a bucket above kTileChunk records becomes K = ceil(records / kTileChunk) chunk
 // items over equal ranges of the passes' concatenated tiles (records of a Zipf hot key spread
 // evenly over the tiles, as the stream does), the others one item each; the items, the split
-// entries and the counts are written for k_tile_fire / k_tile_merge_parts.
+// entries and the counts are written for k_tile_fire (its items, then its merge of the split
+// buckets).
 constexpr int kTilePlanThreads = 1024;
 __global__ __launch_bounds__(kTilePlanThreads) void k_tile_plan(TileFire f) {
     __shared__ uint32_t s_wave[kTilePlanThreads / 64];
@@ -4098,130 +4133,6 @@ hipError_t launch_tile_plan(const TileFire& f, hipStream_t s) {
         !f.sp.items || !f.sp.n_items || !f.sp.split_b || !f.sp.n_split || !f.sp.bfail)
         return hipErrorInvalidValue;
     fg_launch(k_tile_plan, dim3(1), dim3(kTilePlanThreads), 0, s, f);
-    return hipGetLastError();
-}
-
-// k_tile_merge_parts: one split bucket per workgroup (persistent): its chunks' partial entries
-// into one LDS table (COUNT(*) and the value accumulator added; the value's LDS repr as the chunks
-// left it), then one row per key (a6: write_row_k). A bucket whose chunk failed is skipped -- the
-// region split-and-retry redoes its regions from the tiles. A full table fails the bucket the same
-// way (its regions listed, nothing emitted).
-template <int VTC>
-__global__ __launch_bounds__(kTileFireThreads) void k_tile_merge_parts(TileFire f) {
-    constexpr int T = kTileFireThreads, S = kTileSlots;
-    __shared__ __attribute__((aligned(16))) int32_t t_key[S + 1];
-    __shared__ uint32_t t_cs[S + 1];
-    __shared__ unsigned long long t_v[S + 1];
-    __shared__ unsigned int s_full;
-    const MergeParams& p = f.m;
-    const TileSplit& sp = f.sp;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int vt = VTC >= 0 ? VTC : p.val_type;
-    const int64_t vinit = lds_repr(vt, val_identity(vt));
-    const int sub = p.region_bits - f.tbits;
-    const uint32_t NS = *gbl(sp.n_split);
-    for (uint32_t si = blockIdx.x; si < NS; si += gridDim.x) {
-        const int bk = sp.split_b[si];
-        if (*gbl(&sp.bfail[bk])) continue;   // (uniform: the retry redoes it)
-        for (int i = tid; i <= S; i += T) {
-            t_key[i] = kEmpty32;
-            t_cs[i] = 0;
-            t_v[i] = (unsigned long long)vinit;
-        }
-        if (tid == 0) s_full = 0;
-        __syncthreads();
-        bool full = false;
-        const int c0 = sp.split_c0[si], K = sp.split_k[si];
-        for (int c = c0; c < c0 + K; c++) {
-            const uint32_t off = sp.part_off[c], n = sp.part_n[c];
-            if ((uint64_t)off + n > (uint64_t)sp.part_cap) {   // (a failed chunk -- its bucket is listed -- or
-                if (tid == 0) atomicOr(p.overflow, 2u);        // partials past the capacity: none read)
-                continue;
-            }
-            for (uint32_t i = tid; i < n; i += T) {
-                const int32_t key = sp.p_key[off + i];
-                int sl = -1;
-                if (key == kEmpty32) {
-                    sl = S;
-                } else {
-                    uint32_t home = __umulhi((uint32_t)key * 0x9E3779B1u, (uint32_t)(S / 4)) * 4;
-                    for (int probe = 0; probe < S / 4 && sl < 0; probe++) {
-                        const int4 q4 = *reinterpret_cast<const int4*>(&t_key[home]);
-                        const int32_t qq[4] = {q4.x, q4.y, q4.z, q4.w};
-                        int hit = -1, emp = -1;
-#pragma unroll
-                        for (int z = 3; z >= 0; z--) {
-                            if (qq[z] == key) hit = z;
-                            if (qq[z] == kEmpty32) emp = z;
-                        }
-                        if (hit >= 0 && (emp < 0 || hit < emp)) {
-                            sl = (int)home + hit;
-                        } else if (emp >= 0) {
-                            const int old = atomicCAS(&t_key[home + emp], kEmpty32, key);
-                            if (old == kEmpty32 || old == key) sl = (int)home + emp;
-                        } else {
-                            home = (home + 4) & (S - 1);
-                        }
-                    }
-                }
-                if (sl < 0) {
-                    full = true;
-                    continue;
-                }
-                atomicAdd(&t_cs[sl], sp.p_cs[off + i]);
-                // (the partial holds the LDS repr: combine it as the fire combined the records --
-                // the SUM family adds, an ordered-int MIN / MAX image takes the integer min / max)
-                lds_val(&t_v[sl], (int64_t)lds_repr(vt, (int64_t)sp.p_v[off + i]), vt, true);
-            }
-        }
-        if (full) atomicOr(&s_full, 1u);
-        __syncthreads();
-        if (s_full) {
-            if (tid == 0) {
-                atomicOr(p.overflow, 4u);
-                if (p.fail_list && atomicExch(&sp.bfail[bk], 1u) == 0u) {
-                    const int r_lo = bk << (sub + kTileBits);
-                    const uint32_t nr = 1u << (sub + kTileBits);
-                    const uint32_t at = atomicAdd(p.fail_n, nr);
-                    for (uint32_t q = 0; q < nr; q++)
-                        if (at + q < (uint32_t)p.fail_cap)
-                            p.fail_list[at + q] = ((uint32_t)p.job << kFailJobShift) | (uint32_t)(r_lo + (int)q);
-                }
-            }
-            __syncthreads();
-            continue;
-        }
-        // one row per occupied slot (rows reserved per wave: a ballot, one atomic)
-        for (int i0 = 0; i0 <= S; i0 += T) {
-            const int sl = i0 + tid;
-            const bool occ = sl <= S && t_cs[sl] != 0;
-            const uint64_t bal = __ballot(occ);
-            unsigned long long base = 0;
-            if (lane == 0 && bal) base = atomicAdd(p.out_count, (unsigned long long)__popcll(bal));
-            base = __shfl(base, 0);
-            if (occ) {
-                const unsigned long long o = base + (unsigned long long)__popcll(bal & ((1ull << lane) - 1));
-                if ((int64_t)o < p.out_cap) {
-                    const int64_t v = lds_repr(vt, (int64_t)t_v[sl]);
-                    write_row_k(p, o, sl == S ? (int64_t)kEmpty32 : (int64_t)t_key[sl], t_cs[sl], 0ull, &v, vt);
-                } else {
-                    atomicOr(p.overflow, 2u);
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
-hipError_t launch_tile_merge_parts(const TileFire& f, int32_t workgroups, hipStream_t s) {
-    if (!f.split || workgroups < 1) return hipErrorInvalidValue;
-    const dim3 g((unsigned)workgroups), b(kTileFireThreads);
-    switch (f.m.val_type) {
-        case 2: fg_launch(k_tile_merge_parts<2>, g, b, 0, s, f); break;
-        case 1: fg_launch(k_tile_merge_parts<1>, g, b, 0, s, f); break;
-        case 0: fg_launch(k_tile_merge_parts<0>, g, b, 0, s, f); break;
-        default: fg_launch(k_tile_merge_parts<-1>, g, b, 0, s, f); break;
-    }
     return hipGetLastError();
 }
 
