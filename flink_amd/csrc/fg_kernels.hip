@@ -2051,6 +2051,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             const uint32_t NE = skip ? 0u : s_soff[p.n_src];   // (compact: n_src <= kMaxSrcFlat)
             for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
                 int64_t k[kSrcU], cs[kSrcU], sm[kSrcU][1];
+                int32_t k32[kSrcU];   // (the int32 key: loaded from a narrow table, the mix's from a wide one)
                 int j = 0;
                 {
                     const uint32_t f = i0 + tid;
@@ -2066,6 +2067,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 for (int u = 0; u < kSrcU; u++) {
                     const uint32_t f = i0 + u * T + tid;
                     k[u] = 0;
+                    k32[u] = 0;
                     cs[u] = 0;
                     sm[u][0] = 0;
                     if (f >= NE) continue;
@@ -2073,7 +2075,13 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     const uint32_t i = f - s_soff[j];
                     const auto base = gbl(s_sbase[j]);
                     const bool nar = s_snar[j] != 0;
-                    k[u] = tab_mix(base, cap, i, nar);
+                    if (nar) {
+                        k32[u] = tab_key32(base, cap, i, true);
+                        k[u] = mix_of((int64_t)k32[u]);
+                    } else {   // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
+                        k[u] = base[i];
+                        k32[u] = (int32_t)key_of(k[u]);
+                    }
                     cs[u] = tab_cs(base, cap, i, nar);
                     sm[u][0] = tab_v(base, cap, i, nar);
                 }
@@ -2087,8 +2095,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
                     if (i0 + u * T + tid >= NE) continue;
-                    // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
-                    const int slot = nt_bucket_slot(t, (int32_t)key_of(k[u]), home[u], bq[u], full);
+                    const int slot = nt_bucket_slot(t, k32[u], home[u], bq[u], full);
                     if (slot >= 0 && cs[u]) lds_add<C, MV>(t, slot, (unsigned long long)cs[u], 0ull, sm[u], vt, p);
                 }
             }
