@@ -260,7 +260,9 @@ class TwoPhase:
         else:
             got, sent, _ = self._ship(self.local.flush_partials(device_output=True), self.wm)
         self.glob.prepare_snapshot_pre_barrier()
-        return got, sent, self.glob.snapshot_state(copy=not self.host_rows)
+        # (a copy: the image outlives the operator -- a failover closes it and restores a new one
+        # from the image; copy=False would leave views of the closed handle's pinned memory)
+        return got, sent, self.glob.snapshot_state(copy=True)
 
     def finish(self):
         """end of input (Long.MAX_VALUE); returns (rows of both last fires, bytes sent)"""
