@@ -3745,7 +3745,18 @@ int fg_add_rows(fg_handle* h, const fg_row_batch* b) {
     return fg_add_batch(h, &cb);
 }
 
+static int add_partials(fg_handle* h, const fg_partials* b);
+
 int fg_add_partials(fg_handle* h, const fg_partials* b) {
+    const int rc = add_partials(h, b);
+    // FG_DEVICE columns have been read when the call returns (include/flinkgpu.h): the last
+    // pass's scatter reads them after the counters' round trip, so wait for it -- a caller's
+    // allocator may hand the columns' blocks to other work on another stream at once
+    if (rc == FG_OK && b && b->n > 0 && b->location == FG_DEVICE) HIPCHK(h, hipStreamSynchronize(h->stream));
+    return rc;
+}
+
+static int add_partials(fg_handle* h, const fg_partials* b) {
     if (h) {
         h->cnt_bound = JMAX;
         h->keys32 = false;
