@@ -316,6 +316,7 @@ struct fg_handle {
     // FG_TILE_SPLIT (default on): a skewed tile pass of a TUMBLE / local-phase operator stays on the
     // tiles; its fire splits the hot buckets into chunk items (k_tile_plan, k_tile_fire's merge)
     bool tile_split = true;
+    uint32_t tile_chunk = 0;     // FG_TILE_CHUNK: a skewed bucket's chunk records (0: k_tile_plan's default)
     bool narrow_tables = true;   // FG_NARROW_TABLES: tables written by the tile fire take 16-B entries
     DevBuf tile_dir, tile_hist;
     DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail, sp_icnt;   // split plans + partials
@@ -1385,7 +1386,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 const bool spread = h->tile_split && nbk < h->merge_grid && ln.fill >= kTileSpreadMin &&
                                     ln.passes.size() <= (size_t)kMaxTilePasses;
                 const uint32_t chunk =
-                    skewed ? 0u : (uint32_t)std::max<int64_t>(kTileSpreadChunk, ln.fill / (2 * h->merge_grid));
+                    skewed ? h->tile_chunk : (uint32_t)std::max<int64_t>(kTileSpreadChunk, ln.fill / (2 * h->merge_grid));
                 {
                     KTimer kt(h, skewed || spread ? K_TILE_SPLIT : K_TILE_FIRE, ln.fill);
                     if (skewed || spread) {
@@ -1530,7 +1531,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 {
                     KTimer kt(h, skewed ? K_TILE_SPLIT : kc, ln.fill);
                     if (skewed) {
-                        rc = tile_split_fire(h, ln, f, 0);
+                        rc = tile_split_fire(h, ln, f, h->tile_chunk);
                         if (rc) return rc;
                     } else {
                         HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
@@ -3507,6 +3508,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_TILE_GRID")) hp->tile_grid_force = std::atoi(e);
     if (const char* e = getenv("FG_TILE_SPLIT")) hp->tile_split = std::atoi(e) != 0;
     if (const char* e = getenv("FG_NARROW_TABLES")) hp->narrow_tables = std::atoi(e) != 0;
+    if (const char* e = getenv("FG_TILE_CHUNK")) hp->tile_chunk = (uint32_t)std::max(0, std::atoi(e));
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";

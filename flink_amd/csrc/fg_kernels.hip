@@ -3630,21 +3630,78 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
         }
         if (live && merge) {
             // the split bucket's chunks: their partial entries (int32 key, COUNT(*), the value's LDS
-            // form) into the table -- the value combined as the chunks combined their records
-            for (int c = mc0; c < mc0 + mck; c++) {
-                const uint32_t off = f.sp.part_off[c], n = f.sp.part_n[c];
-                if ((uint64_t)off + n > (uint64_t)f.sp.part_cap) {   // (never: a failed chunk fails its bucket)
-                    if (tid == 0) atomicOr(p.overflow, 2u);
-                    continue;
-                }
-                for (uint32_t i = tid; i < n; i += T) {
-                    const int sl = slot_of(f.sp.p_key[off + i]);
-                    if (sl < 0) {
-                        full = true;
-                        continue;
+            // form) into the table -- the value combined as the chunks combined their records.
+            // Up to kTileMaxRegions chunks at a time form one flat sequence (their counts' exclusive
+            // prefix in s_rb, wave 0), every thread kPartU entries per round with their loads issued
+            // before any insert: a hot bucket has hundreds of chunks of a few thousand entries each,
+            // which chunk by chunk left one load round trip per few entries
+            constexpr int kPartU = 4;
+            for (int c0 = mc0; c0 < mc0 + mck; c0 += kTileMaxRegions) {
+                const int nc = min(kTileMaxRegions, mc0 + mck - c0);
+                __syncthreads();   // (s_rb: the source ranges' or the previous group's readers are done)
+                if (wave == 0) {
+                    constexpr int RPL = kTileMaxRegions / 64;
+                    uint32_t c[RPL], x = 0;
+#pragma unroll
+                    for (int q = 0; q < RPL; q++) {
+                        const int g = RPL * lane + q;
+                        c[q] = 0;
+                        if (g < nc) {
+                            const uint32_t off = f.sp.part_off[c0 + g], n = f.sp.part_n[c0 + g];
+                            if ((uint64_t)off + n <= (uint64_t)f.sp.part_cap) c[q] = n;
+                            else atomicOr(p.overflow, 2u);   // (never: a failed chunk fails its bucket)
+                        }
+                        x += c[q];
                     }
-                    atomicAdd(&t_cs[sl], f.sp.p_cs[off + i]);
-                    lds_val(&t_v[sl], lds_repr(vt, (int64_t)f.sp.p_v[off + i]), vt, true);
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const uint32_t y = __shfl_up(x, off);
+                        if (lane >= off) x += y;
+                    }
+                    uint32_t ex = x;
+#pragma unroll
+                    for (int q = 0; q < RPL; q++) ex -= c[q];
+#pragma unroll
+                    for (int q = 0; q < RPL; q++) {
+                        if (RPL * lane + q < nc) s_rb[RPL * lane + q] = ex;
+                        ex += c[q];
+                    }
+                    if (lane == 63) s_total = x;
+                }
+                __syncthreads();
+                const uint32_t NE = s_total;
+                for (uint32_t i0 = 0; i0 < NE; i0 += kPartU * T) {
+                    int32_t pk[kPartU];
+                    uint32_t pc[kPartU];
+                    unsigned long long pv[kPartU];
+#pragma unroll
+                    for (int u = 0; u < kPartU; u++) {
+                        const uint32_t i = i0 + u * T + tid;
+                        pk[u] = kEmpty32;
+                        pc[u] = 0;
+                        pv[u] = 0;
+                        if (i >= NE) continue;
+                        int lo = 0, hi = nc;   // the chunk of entry i: the last base <= i
+                        while (hi - lo > 1) {
+                            const int mid = (lo + hi) >> 1;
+                            if (s_rb[mid] <= i) lo = mid;
+                            else hi = mid;
+                        }
+                        const uint32_t e = f.sp.part_off[c0 + lo] + (i - s_rb[lo]);
+                        pk[u] = f.sp.p_key[e];
+                        pc[u] = f.sp.p_cs[e];
+                        pv[u] = f.sp.p_v[e];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kPartU; u++) {
+                        if (i0 + u * T + tid >= NE) continue;
+                        const int sl = slot_of(pk[u]);
+                        if (sl < 0) {
+                            full = true;
+                            continue;
+                        }
+                        atomicAdd(&t_cs[sl], pc[u]);
+                        lds_val(&t_v[sl], lds_repr(vt, (int64_t)pv[u]), vt, true);
+                    }
                 }
             }
         } else if (live) {
