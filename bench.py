@@ -510,6 +510,12 @@ def main():
                          "host); default: the zipf workload (configs[4]) checkpoints once per step, others never")
     ap.add_argument("--aggs", default=None, help="comma-separated aggregate list (default: the workload's), "
                     "e.g. count_star,min")
+    ap.add_argument("--sync-snapshot", action="store_true",
+                    help="checkpoints copy the state image to the host inside snapshotState (A/B; default: "
+                         "fg_snapshot_state_async, the copy overlapping the next micro-batches, collected in the step)")
+    ap.add_argument("--jitter", type=int, default=None, help="rowtime jitter ms (diagnostic override of the workload's; "
+                    "the watermark delay follows it)")
+    ap.add_argument("--zipf", type=float, default=None, help="Zipf exponent (diagnostic override; 0 = uniform keys)")
     ap.add_argument("--expected-keys", type=int, default=None,
                     help="operator sizing hint: distinct keys per slice (default: the key space x 1.05)")
     ap.add_argument("--wm-sync", action="store_true",
@@ -533,7 +539,11 @@ def main():
                     help="records of the pinned-host leg (SURVEY 8(d) contract timing: FG_HOST batches, "
                          "double-buffered H2D overlapping the kernels); 0 skips it. Never the headline value")
     args = ap.parse_args()
-    wl = WORKLOADS[args.workload]
+    wl = dict(WORKLOADS[args.workload])
+    if args.jitter is not None:
+        wl["jitter"] = wl["delay"] = args.jitter
+    if args.zipf is not None:
+        wl["zipf"] = args.zipf
     keys_default = args.keys is None
     if args.keys is None:
         args.keys = wl["keys"]
@@ -646,14 +656,29 @@ def main():
         c0 = time.perf_counter()
         if tp is not None:
             got, sent, (img, _) = tp.checkpoint()
+            ckpt["state_rows"] += len(img["key"])
         else:
             got, sent = 0, 0
+            snapshot_collect()
             op.prepare_snapshot_pre_barrier()
-            img, _ = op.snapshot_state(copy=False)   # the pinned image a JNI shim hands to the backend
-        ckpt["state_rows"] += len(img["key"])
+            if args.sync_snapshot:
+                img, _ = op.snapshot_state(copy=False)   # the pinned image a JNI shim hands to the backend
+                ckpt["state_rows"] += len(img["key"])
+            else:   # the synchronous part; the image's copy to the host overlaps the next batches
+                op.snapshot_state_async()
+                ckpt["pending"] = True
         ckpt["n"] += 1
         ckpt["s"] += time.perf_counter() - c0
         return got, sent
+
+    def snapshot_collect():
+        """snapshotState's asynchronous part: the host image of the pending snapshot (the
+        state backend takes it; within the step, so the timed region pays for its copy)"""
+        if ckpt.pop("pending", False):
+            c0 = time.perf_counter()
+            img, _ = op.snapshot_state_wait(copy=False)
+            ckpt["state_rows"] += len(img["key"])
+            ckpt["s"] += time.perf_counter() - c0
 
     def intern(lo):
         """BinaryRowDataKeySelector.getKey rows -> dictionary ids (on the GPU, the dictionary's
@@ -746,6 +771,7 @@ def main():
             return rows + nr, xgmi + sent
         if held:
             rows += op.collect_fired().n
+        snapshot_collect()
         r = op.process_watermark(JMAX, device_output=True)
         rows += r.n
         assert args.wm_sync or rows == op.stats()["rows_fired"] - rows0
@@ -852,6 +878,7 @@ def main():
             "workload": wl["desc"],
             "records_per_gpu": n, "keys": args.keys, "records_per_event_second": args.rate,
             "micro_batch": args.batch, "watermark_every": args.wm_every, "expected_keys": expected_keys,
+            "jitter_ms": wl["jitter"], "zipf_s": wl["zipf"],
             "parallelism": f"key-group sharded x{world}" + (
                 (" + RCCL all-to-all of partial accumulators (two-phase)" if two_phase else
                  " + RCCL all-to-all of records") if world > 1 else ""),

@@ -106,7 +106,7 @@ EXPORTS = (
     "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_advance_progress_async",
     "fg_advance_progress_async_n",
     "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials", "fg_snapshot_state",
-    "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
+    "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
     "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async",
@@ -159,6 +159,8 @@ def load():
     L.fg_flush_partials.argtypes = [P, C.c_int32, C.POINTER(FgRows)]
     L.fg_flush.argtypes = [P]
     L.fg_snapshot_state.argtypes = [P, C.POINTER(FgStateRows), C.POINTER(C.c_int64)]
+    L.fg_snapshot_state_async.argtypes = [P]
+    L.fg_snapshot_state_wait.argtypes = [P, C.POINTER(FgStateRows), C.POINTER(C.c_int64)]
     L.fg_restore.argtypes = [P, C.POINTER(FgStateRows), C.c_int64]
     L.fg_late_dropped.argtypes = [P, C.POINTER(C.c_int64)]
     L.fg_get_stats.argtypes = [P, C.POINTER(FgStats)]
@@ -228,7 +230,7 @@ def load():
         getattr(L, fn).restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress",
                "fg_advance_progress_async", "fg_advance_progress_async_n", "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials",
-               "fg_snapshot_state", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
+               "fg_snapshot_state", "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int
     _lib = L

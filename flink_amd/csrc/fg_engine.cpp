@@ -297,6 +297,12 @@ struct fg_handle {
     // batch i + 1 overlaps the kernels of batch i (the engine stream waits for the copy's
     // event; a buffer is rewritten only after the kernels that read it)
     hipStream_t copy_stream = nullptr;
+    // asynchronous snapshot (fg_snapshot_state_async): the image's D2H copy runs on its own
+    // stream after the export kernels (event ev_snap), collected by fg_snapshot_state_wait
+    hipStream_t snap_stream = nullptr;
+    hipEvent_t ev_snap = nullptr;
+    bool snap_pending = false;
+    int64_t snap_total = 0, snap_wm = 0;
     DevBuf hb_key[2], hb_ts[2], hb_val[2], hb_null[2];
     DevBuf hb_narrow[2];   // FG_HOST narrow columns (fg_batch.format) before widening
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -316,7 +322,11 @@ struct fg_handle {
     // FG_TILE_SPLIT (default on): a skewed tile pass of a TUMBLE / local-phase operator stays on the
     // tiles; its fire splits the hot buckets into chunk items (k_tile_plan, k_tile_fire's merge)
     bool tile_split = true;
-    uint32_t tile_chunk = 0;     // FG_TILE_CHUNK: a skewed bucket's chunk records (0: k_tile_plan's default)
+    uint32_t tile_chunk = 0;
+    // FG_TILE_HOT=1: the split fire's wave pre-combine of a hot key. Off by default: configs[4]
+    // A/B (profiles/r05/zipf_ab): split fire 1.485 vs 1.072 ms per 100M-record window with it on --
+    // the ballot + butterflies cost more than the same-slot LDS atomics they save
+    bool tile_hot = false;     // FG_TILE_CHUNK: a skewed bucket's chunk records (0: k_tile_plan's default)
     bool narrow_tables = true;   // FG_NARROW_TABLES: tables written by the tile fire take 16-B entries
     DevBuf tile_dir, tile_hist;
     DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail, sp_icnt;   // split plans + partials
@@ -1248,7 +1258,7 @@ int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f, uint32_t chunk) {
     }
     sp.gpre[ln.passes.size()] = g;
     f.split = 1;
-    f.hot = 1;
+    f.hot = h->tile_hot ? 1 : 0;
     HIPCHK(h, launch_tile_plan(f, h->stream));
     HIPCHK(h, launch_tile_fire(f, (int)std::min<int64_t>(max_items, h->merge_grid), h->stream));
     TileFire fm = f;   // the split buckets: their chunks' partial entries merged (+ tables, rows)
@@ -3508,6 +3518,7 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_TILE_GRID")) hp->tile_grid_force = std::atoi(e);
     if (const char* e = getenv("FG_TILE_SPLIT")) hp->tile_split = std::atoi(e) != 0;
     if (const char* e = getenv("FG_NARROW_TABLES")) hp->narrow_tables = std::atoi(e) != 0;
+    if (const char* e = getenv("FG_TILE_HOT")) hp->tile_hot = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_CHUNK")) hp->tile_chunk = (uint32_t)std::max(0, std::atoi(e));
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
@@ -4070,9 +4081,10 @@ int fg_advance_progress(fg_handle* h, int64_t wm, int32_t out_location, fg_rows*
     return FG_OK;
 }
 
-int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark) {
-    if (!h || !out) return FG_EINVAL;
-    HIPCHK(h, hipSetDevice(h->device));
+// snapshotState's synchronous part: the staged records flushed, every resident slice exported
+// into the device image columns (s_*, in stream order: the image is the state as of this call)
+// and their copy into the pinned host image (hs_*) queued on the snapshot stream
+static int snapshot_begin(fg_handle* h) {
     if (int rc0 = settle_pending(h)) return rc0;
     int rc = flush(h);
     if (rc) return rc;
@@ -4143,18 +4155,35 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
         HIPCHK(h, h->hs_v2.ensure(b8));
     }
     if (total > 0) {
-        if (h->mv) {
-            HIPCHK(h, hipMemcpyAsync(h->hs_v1.p, h->s_v1.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(h, hipMemcpyAsync(h->hs_v2.p, h->s_v2.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        if (!h->snap_stream) {
+            HIPCHK(h, hipStreamCreateWithFlags(&h->snap_stream, hipStreamNonBlocking));
+            HIPCHK(h, hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming));
         }
-        HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipMemcpyAsync(h->hs_sum.p, h->s_sum.p, 8 * total, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipEventRecord(h->ev_snap, h->stream));   // (after the export kernels)
+        HIPCHK(h, hipStreamWaitEvent(h->snap_stream, h->ev_snap, 0));
+        hipStream_t cs = h->snap_stream;
+        if (h->mv) {
+            HIPCHK(h, hipMemcpyAsync(h->hs_v1.p, h->s_v1.p, 8 * total, hipMemcpyDeviceToHost, cs));
+            HIPCHK(h, hipMemcpyAsync(h->hs_v2.p, h->s_v2.p, 8 * total, hipMemcpyDeviceToHost, cs));
+        }
+        HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, hipMemcpyDeviceToHost, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, hipMemcpyDeviceToHost, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, hipMemcpyDeviceToHost, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, hipMemcpyDeviceToHost, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_sum.p, h->s_sum.p, 8 * total, hipMemcpyDeviceToHost, cs));
     }
-    rc = sync(h);
-    if (rc) return rc;
+    h->snap_pending = true;
+    h->snap_total = total;
+    h->snap_wm = h->timer_wm;
+    return FG_OK;
+}
+
+// snapshotState's asynchronous part: the host image once its copy has completed
+static int snapshot_end(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark) {
+    if (!h->snap_pending) return h->fail(FG_ESTATE, "fg_snapshot_state_wait without fg_snapshot_state_async");
+    if (h->snap_stream) HIPCHK(h, hipStreamSynchronize(h->snap_stream));
+    h->snap_pending = false;
+    const int64_t total = h->snap_total;
     out->n = total;
     out->key = h->hs_key.as<int64_t>();
     out->slice_end = h->hs_slice.as<int64_t>();
@@ -4163,8 +4192,29 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
     out->sum = h->hs_sum.as<int64_t>();
     out->min = h->mv ? h->hs_v1.as<int64_t>() : nullptr;   // multi-value operators: the MIN / MAX slots
     out->max = h->mv ? h->hs_v2.as<int64_t>() : nullptr;
-    if (timer_watermark) *timer_watermark = h->timer_wm;
+    if (timer_watermark) *timer_watermark = h->snap_wm;
     return FG_OK;
+}
+
+int fg_snapshot_state_async(fg_handle* h) {
+    if (!h) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->snap_pending) return h->fail(FG_ESTATE, "an asynchronous snapshot is not collected yet (fg_snapshot_state_wait)");
+    return snapshot_begin(h);
+}
+
+int fg_snapshot_state_wait(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark) {
+    if (!h || !out) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    return snapshot_end(h, out, timer_watermark);
+}
+
+int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark) {
+    if (!h || !out) return FG_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->snap_pending) return h->fail(FG_ESTATE, "an asynchronous snapshot is not collected yet (fg_snapshot_state_wait)");
+    if (int rc = snapshot_begin(h)) return rc;
+    return snapshot_end(h, out, timer_watermark);
 }
 
 int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
@@ -4437,6 +4487,11 @@ void fg_close(fg_handle* h) {
         (void)hipStreamSynchronize(h->copy_stream);
         (void)hipStreamDestroy(h->copy_stream);
     }
+    if (h->snap_stream) {
+        (void)hipStreamSynchronize(h->snap_stream);
+        (void)hipStreamDestroy(h->snap_stream);
+    }
+    if (h->ev_snap) (void)hipEventDestroy(h->ev_snap);
     hipStream_t s = h->stream;
     delete h;
     if (s) (void)hipStreamDestroy(s);

@@ -461,6 +461,22 @@ class WindowAggOperator:
         s = L.FgStateRows()
         wm = C.c_int64()
         L.check(self._lib.fg_snapshot_state(self._h, C.byref(s), C.byref(wm)), self._h)
+        return self._image(s, wm, copy)
+
+    def snapshot_state_async(self):
+        """snapshotState's synchronous part (fg_snapshot_state_async): the state as of this call
+        is exported on the GPU and its copy to the host image queued; the operator takes
+        batches and watermarks meanwhile. snapshot_state_wait returns the image."""
+        L.check(self._lib.fg_snapshot_state_async(self._h), self._h)
+
+    def snapshot_state_wait(self, copy: bool = True):
+        """the image of the last snapshot_state_async (as snapshot_state returns it)"""
+        s = L.FgStateRows()
+        wm = C.c_int64()
+        L.check(self._lib.fg_snapshot_state_wait(self._h, C.byref(s), C.byref(wm)), self._h)
+        return self._image(s, wm, copy)
+
+    def _image(self, s, wm, copy):
         n = s.n
 
         def col(p):

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 14
+#define FG_ABI_VERSION 15
 
 enum fg_status {
     FG_OK = 0,
@@ -328,6 +328,16 @@ int  fg_flush(fg_handle* h);
  * progress does not move. Rows as fg_advance_progress at out_location. */
 int  fg_flush_partials(fg_handle* h, int32_t out_location, fg_rows* fired);
 int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
+/* snapshotState in two parts (ABI 15; StreamOperatorStateHandler.snapshotState's synchronous
+ * part and the AsyncSnapshotCallable of a heap state backend, SnapshotStrategyRunner.snapshot):
+ * _async flushes the staged records and exports every resident slice into a device image (the
+ * state as of this call) and queues its copy into the pinned host image on a stream of its own;
+ * the operator takes batches, watermarks and partials meanwhile. _wait returns that image (the
+ * fg_snapshot_state layout, valid until the next snapshot call) once the copy has completed.
+ * One snapshot at a time: fg_snapshot_state[_async] fails with FG_ESTATE while one is not
+ * collected. fg_snapshot_state is _async + _wait. */
+int  fg_snapshot_state_async(fg_handle* h);
+int  fg_snapshot_state_wait(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
 int  fg_late_dropped(fg_handle* h, int64_t* out);
 int  fg_get_stats(fg_handle* h, fg_stats* out);

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 14
+    assert lib.fg_abi_version() == 15
 
 
 def test_struct_layouts_match_header_sizes(tmp_path):

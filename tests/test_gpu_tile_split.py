@@ -1,6 +1,6 @@
 """Skewed tile passes (Zipf hot keys) on the tile path: the split fire (k_tile_plan ->
-k_tile_fire over chunk items with hot-key wave pre-combine -> k_tile_merge_parts) against the
-oracle, and the parallel materialize of a skewed lane (checkpoint). A hot key's bucket above
+k_tile_fire over chunk items -> k_tile_fire's merge launch over the split buckets' partial
+entries; FG_TILE_HOT=1 adds the hot-key wave pre-combine) against the oracle, and the parallel materialize of a skewed lane (checkpoint). A hot key's bucket above
 max(kTileChunk, 4x the lane's mean) records is cut into chunk items over its tiles
 (fg_kernels.h TileSplit); results must equal the oracle's exactly as any other fire's
 (bit-exact keys, counts, i64 sums, MIN / MAX; f64 sums within the north_star tolerance)."""
@@ -35,6 +35,15 @@ def test_zipf_split_fire_parity(oracle_mod, name, cfg, kw):
         return
     assert ks.get("tile_split_fire", {}).get("launches", 0) > 0, ks
     assert ks.get("merge_heavy", {}).get("launches", 0) == 0, ks   # (the skewed passes stayed on the tiles)
+
+
+@pytest.mark.parametrize("name,cfg,kw", [CASES[1], CASES[2], CASES[4]], ids=[CASES[i][0] + "_hot" for i in (1, 2, 4)])
+def test_zipf_split_fire_hot_precombine_parity(oracle_mod, name, cfg, kw, monkeypatch):
+    """FG_TILE_HOT=1: chunk items pre-combine a wave's records of a hot key (off by default)."""
+    monkeypatch.setenv("FG_TILE_HOT", "1")
+    ks = {}
+    drive_both(oracle_mod, cfg, kstats=ks, **kw)
+    assert ks.get("tile_split_fire", {}).get("launches", 0) > 0, ks
 
 
 def test_zipf_split_off_takes_heavy_path(oracle_mod, monkeypatch):
