@@ -3184,7 +3184,7 @@ hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t NT, int32_t NC, int32_t lshift,
                                                    const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot) {
     __shared__ uint16_t s[64][67];
-    __shared__ uint32_t s_tot[64];   // the block's records per bucket (btot: per-bucket totals of the pass)
+    __shared__ uint32_t s_q[4][64];   // btot: quarter sums of the block's 64 tiles per column
     const int tb = blockIdx.x * 64, cb = blockIdx.y * 64;
     const unsigned long long lm = *gbl(lane_mask);
     const int l0 = cb >> lshift, l1 = (cb + 63 < NC ? cb + 63 : NC - 1) >> lshift;
@@ -3202,7 +3202,6 @@ __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t 
         s[tt][2 * k] = (uint16_t)w;
         s[tt][2 * k + 1] = (uint16_t)(w >> 16);
     }
-    if (threadIdx.x < 64) s_tot[threadIdx.x] = 0;
     __syncthreads();
     for (int i = threadIdx.x; i < 64 * 64; i += 256) {
         const int cc = i / 64, tt = i % 64;
@@ -3210,13 +3209,25 @@ __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t 
         if (t < NT && c < NC && ((lm >> (c >> lshift)) & 1)) {
             const uint32_t a = s[tt][cc], b = s[tt][cc + 1];
             dt[(int64_t)c * NT + t] = a | ((b - a) << 16);
-            if (btot) atomicAdd(&s_tot[cc], b - a);
         }
     }
+    // btot: the block's records per bucket column -- 4 threads per column sum 16 tiles each
+    // (conflict-free LDS reads), then one global add per column. Per-lane LDS adds into the column's
+    // counter (64 lanes, one address) took 164 vs 76 us per 100M-record pass (round 5)
     if (btot) {
+        const int cc = threadIdx.x & 63, q = threadIdx.x >> 6;
+        uint32_t sum = 0;
+        for (int j = 0; j < 16; j++) {
+            const int tt = q * 16 + j;
+            if (tb + tt < NT) sum += (uint32_t)s[tt][cc + 1] - s[tt][cc];
+        }
+        s_q[q][cc] = sum;
         __syncthreads();
-        if (threadIdx.x < 64 && cb + (int)threadIdx.x < NC && s_tot[threadIdx.x])
-            atomicAdd(&btot[cb + threadIdx.x], s_tot[threadIdx.x]);
+        const int c = cb + (int)threadIdx.x;
+        if (threadIdx.x < 64 && c < NC && ((lm >> (c >> lshift)) & 1)) {
+            const uint32_t t4 = s_q[0][threadIdx.x] + s_q[1][threadIdx.x] + s_q[2][threadIdx.x] + s_q[3][threadIdx.x];
+            if (t4) atomicAdd(&btot[c], t4);
+        }
     }
 }
 
@@ -3448,8 +3459,11 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
 // HOT (a skewed pass's split fire, SUM-family value ops): the insert pre-combines a wave's records of
 // a hot key; the plain fire keeps the one-probe-loop-per-record insert (A/B, round 5: 0.89 vs 1.08
 // ms per 100M records for the branch-free insert with a dummy slot)
-template <int VTC, bool TAB, bool HOT>   // TAB: source / destination tables (compiled out of the plain fire)
+// SM: 0 the plain fire (no split code: the split and merge paths cost it 4 spilled VGPRs, round 5),
+// 1 a split fire's launches (chunk items, then the merge launch), 2 chunk items with HOT
+template <int VTC, bool TAB, int SM>   // TAB: source / destination tables (compiled out of the plain fire)
 __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
+    constexpr bool HOT = SM == 2;
     constexpr int T = kTileFireThreads, W = T / 64, S = kTileSlots;
     constexpr int kRounds = S / T + 1;   // + 1: the sentinel slot (thread 0)
     static_assert(S % T == 0 && (S & (S - 1)) == 0, "table rounds");
@@ -3475,7 +3489,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
     const int64_t vinit = lds_repr(vt, val_identity(vt));
     const int sub = p.region_bits - f.tbits;          // current region bits above the passes'
     const bool retry = p.retry_list != nullptr;
-    const bool split = f.split != 0;                  // items planned by k_tile_plan (a skewed pass)
+    const bool split = SM != 0 && f.split != 0;       // items planned by k_tile_plan (a skewed pass)
     const bool merge = split && f.merge != 0;         // the split buckets' merge of their chunks' partials
     __shared__ int s_item;   // split: the item fetched by workgroup (dynamic: chunk items vary in size)
     const int NI = retry ? p.n_retry
@@ -4092,12 +4106,17 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
     if (f.split && !f.merge && !f.sp.next_item) return hipErrorInvalidValue;
     if (f.merge && (!f.split || !f.sp.split_b || !f.sp.n_split)) return hipErrorInvalidValue;
     const bool hot = f.hot && f.split && !f.merge && f.m.val_type >= 0 && f.m.val_type <= 2;
-#define FG_TILE_FIRE(V)                                                     \
-    do {                                                                    \
-        if (tab && hot) fg_launch((k_tile_fire<V, true, true>), g, b, 0, s, f); \
-        else if (tab) fg_launch((k_tile_fire<V, true, false>), g, b, 0, s, f);  \
-        else if (hot) fg_launch((k_tile_fire<V, false, true>), g, b, 0, s, f); \
-        else fg_launch((k_tile_fire<V, false, false>), g, b, 0, s, f);     \
+    const int sm = !f.split ? 0 : hot ? 2 : 1;
+#define FG_TILE_FIRE_SM(V, TB)                                                     \
+    do {                                                                           \
+        if (sm == 0) fg_launch((k_tile_fire<V, TB, 0>), g, b, 0, s, f);            \
+        else if (sm == 1) fg_launch((k_tile_fire<V, TB, 1>), g, b, 0, s, f);       \
+        else fg_launch((k_tile_fire<V, TB, 2>), g, b, 0, s, f);                    \
+    } while (0)
+#define FG_TILE_FIRE(V)                          \
+    do {                                         \
+        if (tab) FG_TILE_FIRE_SM(V, true);       \
+        else FG_TILE_FIRE_SM(V, false);          \
     } while (0)
     switch (f.m.val_type) {
         case 2: FG_TILE_FIRE(2); break;
@@ -4106,6 +4125,7 @@ hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s
         default: FG_TILE_FIRE(-1); break;
     }
 #undef FG_TILE_FIRE
+#undef FG_TILE_FIRE_SM
     return hipGetLastError();
 }
 
