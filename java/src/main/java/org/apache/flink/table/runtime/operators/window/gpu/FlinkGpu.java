@@ -101,6 +101,15 @@ public final class FlinkGpu {
      */
     public static native long snapshotState(long h, ByteBuffer[] cols, long[] timerWatermark);
 
+    /**
+     * fg_snapshot_state_async (ABI 15): the staged records flushed, the resident state exported on
+     * the GPU and its copy into the host image queued; the handle takes further calls meanwhile.
+     */
+    public static native void snapshotStateAsync(long h);
+
+    /** fg_snapshot_state_wait: the image of the last snapshotStateAsync, as snapshotState. */
+    public static native long snapshotStateWait(long h, ByteBuffer[] cols, long[] timerWatermark);
+
     /** fg_restore. */
     public static native void restore(
             long h,

@@ -18,7 +18,7 @@
  *                       the watermark (SlicingWindowOperator.java:207-210)
  *   advanceAsync / collectHeld   fg_advance_progress_async + fg_collect_fired for an operator that
  *                       holds the watermark while the fires complete (GpuSlicingWindowAggOperator)
- *   prepareCheckpoint   fg_flush + fg_snapshot_state: the resident accumulators are written to the
+ *   prepareCheckpoint   fg_flush + fg_snapshot_state_async / _wait: the resident accumulators are written to the
  *                       reference's own keyed state "window-aggs" (namespace = slice end, the
  *                       accumulator row in the accSerializer layout, GpuAccRows) and the window
  *                       timers AggCombiner would hold are registered -- a savepoint the reference
@@ -324,6 +324,8 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         flushBatch();
         collectHeld();
         FlinkGpu.flush(handle);
+        // the image's export and host copy run on the GPU while the previous image is cleared
+        FlinkGpu.snapshotStateAsync(handle);
         writeKeyedState();
     }
 
@@ -357,7 +359,7 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
 
         ByteBuffer[] cols = new ByteBuffer[7];
         long[] wm = new long[1];
-        int n = (int) FlinkGpu.snapshotState(handle, cols, wm);
+        int n = (int) FlinkGpu.snapshotStateWait(handle, cols, wm);
         for (ByteBuffer c : cols) {
             if (c != null) {
                 c.order(ByteOrder.nativeOrder());

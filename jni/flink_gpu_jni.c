@@ -16,6 +16,8 @@
  *   flush           fg_flush             (prepareSnapshotPreBarrier)
  *   flushPartials   fg_flush_partials    (local phase: WindowBuffer.flush of LocalSlicingWindowAggOperator)
  *   snapshotState   fg_snapshot_state    (snapshotState: the window-aggs image)
+ *   snapshotStateAsync / snapshotStateWait   fg_snapshot_state_async / _wait (the image exported
+ *                   and its host copy queued; the shim clears the previous image meanwhile)
  *   restore         fg_restore           (initializeState)
  *   lateDropped     fg_late_dropped      (numLateRecordsDropped)
  *   close           fg_close
@@ -274,6 +276,29 @@ JNIEXPORT jlong JNICALL FN(snapshotState)(JNIEnv* env, jclass cls, jlong hp, job
     fg_state_rows s;
     int64_t wm = 0;
     if (check(env, h, fg_snapshot_state(h, &s, &wm))) return 0;
+    const jlong bytes = 8 * s.n;
+    const int64_t* c[7] = {s.key, s.slice_end, s.cnt_star, s.cnt_val, s.sum, s.min, s.max};
+    for (int i = 0; i < 7; i++) (*env)->SetObjectArrayElement(env, cols, i, c[i] ? wrap(env, c[i], bytes) : NULL);
+    jlong w = wm;
+    (*env)->SetLongArrayRegion(env, timerWm, 0, 1, &w);
+    return s.n;
+}
+
+/* void snapshotStateAsync(long h): fg_snapshot_state_async (ABI 15) */
+JNIEXPORT void JNICALL FN(snapshotStateAsync)(JNIEnv* env, jclass cls, jlong hp) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    (void)check(env, h, fg_snapshot_state_async(h));
+}
+
+/* long snapshotStateWait(long h, ByteBuffer[] cols, long[] timerWatermark): the image of the last
+ * snapshotStateAsync, as snapshotState returns it (fg_snapshot_state_wait) */
+JNIEXPORT jlong JNICALL FN(snapshotStateWait)(JNIEnv* env, jclass cls, jlong hp, jobjectArray cols, jlongArray timerWm) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_state_rows s;
+    int64_t wm = 0;
+    if (check(env, h, fg_snapshot_state_wait(h, &s, &wm))) return 0;
     const jlong bytes = 8 * s.n;
     const int64_t* c[7] = {s.key, s.slice_end, s.cnt_star, s.cnt_val, s.sum, s.min, s.max};
     for (int i = 0; i < 7; i++) (*env)->SetObjectArrayElement(env, cols, i, c[i] ? wrap(env, c[i], bytes) : NULL);

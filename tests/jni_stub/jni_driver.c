@@ -108,6 +108,8 @@ jlong FN(advanceProgress)(JNIEnv*, jclass, jlong, jlong, jobjectArray);
 void FN(advanceProgressAsync)(JNIEnv*, jclass, jlong, jlong);
 jlong FN(collectFired)(JNIEnv*, jclass, jlong, jobjectArray);
 jlong FN(flushPartials)(JNIEnv*, jclass, jlong, jobjectArray);
+void FN(snapshotStateAsync)(JNIEnv*, jclass, jlong);
+jlong FN(snapshotStateWait)(JNIEnv*, jclass, jlong, jobjectArray, jlongArray);
 jlong FN(lateDropped)(JNIEnv*, jclass, jlong);
 void FN(close)(JNIEnv*, jclass, jlong);
 void FN(hostRegister)(JNIEnv*, jclass, jint, jobject);
@@ -245,8 +247,19 @@ static int gpu_mode(void) {
     jobjectArray cols = objarr(10);
     jlong n = FN(collectFired)(env, NULL, h, cols);
     totals("async", cols, n, 3);
+    /* the state as of here (windows ending 4000 and 5000), collected after the next advance fired them */
+    FN(snapshotStateAsync)(env, NULL, h);
     n = FN(advanceProgress)(env, NULL, h, 10000, cols);
     totals("sync", cols, n, 3);
+    {
+        jobjectArray sc = objarr(7);
+        jlongArray swm = longarr(1);
+        jlong sn = FN(snapshotStateWait)(env, NULL, h, sc, swm);
+        const int64_t* cs = (const int64_t*)sc->objs[2]->addr;
+        long long t = 0;
+        for (jlong i = 0; i < sn; i++) t += cs[i];
+        printf("snapshot entries %lld cnt_star %lld wm %lld\n", (long long)sn, t, (long long)swm->longs[0]);
+    }
     printf("late %lld\n", (long long)FN(lateDropped)(env, NULL, h));
     FN(close)(env, NULL, h);
     /* the local phase: partial rows of every buffered slice */

@@ -122,8 +122,8 @@ def test_jni_glue_errors_through_fake_jnienv(tmp_path):
 
 @pytest.mark.gpu
 def test_jni_glue_on_gpu_host_columns(tmp_path):
-    """open / addBatch / advanceProgressAsync + collectFired / advanceProgress / flushPartials
-    through the glue on the GPU: the driver reads every fired column on the HOST (the direct
+    """open / addBatch / advanceProgressAsync + collectFired / snapshotStateAsync / advanceProgress /
+    snapshotStateWait / flushPartials through the glue on the GPU: the driver reads every fired column on the HOST (the direct
     buffers a JVM would read), totals against numpy; then the two-phase edge through the comm
     natives at world size 1 (commUniqueId / commOpen / commExchangeFired over RCCL): the global
     handle fires what the single-phase operator fired"""
@@ -145,5 +145,9 @@ def test_jni_glue_on_gpu_host_columns(tmp_path):
         got = (int(f[1]), int(f[3]), float(f[5]), int(f[7]), int(f[9]))
         assert got == expect(sel), (tag, got, expect(sel))
     assert out["late"] == ["0"]
+    # snapshotStateAsync after the 2999 watermark, collected after the 10000 advance fired the rest:
+    # the image holds the state as of the async call -- the 400 records (10 keys x 2 windows) of the
+    # windows ending 4000 and 5000 -- and that call's timer watermark
+    assert out["snapshot"] == ["entries", "20", "cnt_star", "400", "wm", "2999"], out["snapshot"]
     f = out["partials"]
     assert (int(f[1]), int(f[3]), int(f[5]), float(f[7])) == (50, 1000, 1000, float(val.sum()))
