@@ -737,8 +737,10 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     // may hold NULL counts iff something merged into it may
     unsigned long long null_mask = 0;
     bool dst_null = false;
+    bool src_narrow = false;
     for (size_t i = 0; i < j.srcs.size(); i++) {
         srcs.push_back(ref_of(j.srcs[i]));
+        src_narrow = src_narrow || j.srcs[i]->narrow;
         if (j.srcs[i]->has_null) {
             if (i < 64) null_mask |= 1ull << i;
             dst_null = true;
@@ -751,6 +753,7 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     *p = MergeParams{};
     p->region_bits = h->region_bits;
     p->n_src = (int)srcs.size();
+    p->src_narrow = src_narrow ? 1 : 0;
     if (!srcs.empty()) {
         int rc = arena_put(h, srcs.data(), srcs.size(), &p->src);
         if (rc) return rc;
@@ -807,7 +810,10 @@ int tile_job_params(fg_handle* h, int ji, TileFire* f) {
         p.emit = 1;
     }
     std::vector<TableRef> srcs;
-    for (SliceTable* x : j.srcs) srcs.push_back(ref_of(x));
+    for (SliceTable* x : j.srcs) {
+        srcs.push_back(ref_of(x));
+        if (x->narrow) p.src_narrow = 1;
+    }
     p.n_src = (int)srcs.size();
     if (!srcs.empty()) {
         int rc = arena_put(h, srcs.data(), srcs.size(), &p.src);

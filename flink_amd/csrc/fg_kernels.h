@@ -213,6 +213,7 @@ struct MergeParams {
     int32_t narrow;            // fast stream of narrow 12-B records (every batch stride 3)
     int32_t compact;           // compact LDS table (fast_stream, no src tables, < 2^32 records)
     int32_t n_src;
+    int32_t src_narrow;        // some source table holds narrow (16-B) entries
     const TableRef* src;       // device array [n_src]
     int32_t n_batches;
     int32_t val_type;          // 0 none, 1 i64, 2 f64

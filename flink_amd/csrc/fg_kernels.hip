@@ -2047,7 +2047,54 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         //    the entries of all source tables form one flat sequence (prefix of the
         //    tables' counts in s_soff), loaded kSrcU per thread at a time and inserted with
         //    the bucketed probe (compact: plain sources only -- no NULL counts, no marks)
-        if constexpr (NT) if (p.n_src > 0) {   // narrow table: a source entry's key from its mix
+        if constexpr (NT) if (p.n_src > 0 && !p.src_narrow) {   // wide sources only (HOP's tables)
+            // (a loop of its own: the narrow-aware one below costs the wide case 12 %, round 5 --
+            // 0.429 vs 0.384 ms per HOP fire)
+            const uint32_t NE = skip ? 0u : s_soff[p.n_src];
+            for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
+                int64_t k[kSrcU], cs[kSrcU], sm[kSrcU][1];
+                int j = 0;
+                {
+                    const uint32_t f = i0 + tid;
+                    int lo = 0, hi = p.n_src;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_soff[mid] <= f) lo = mid;
+                        else hi = mid;
+                    }
+                    j = lo;
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    const uint32_t f = i0 + u * T + tid;
+                    k[u] = 0;
+                    cs[u] = 0;
+                    sm[u][0] = 0;
+                    if (f >= NE) continue;
+                    while (s_soff[j + 1] <= f) j++;
+                    const uint32_t i = f - s_soff[j];
+                    const auto base = gbl(s_sbase[j]);
+                    k[u] = base[i];
+                    cs[u] = base[cap + i];
+                    sm[u][0] = base[3 * cap + i];
+                }
+                uint32_t home[kSrcU];
+                int4 bq[kSrcU];
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    home[u] = lds_home<C, MV>(k[u]);
+                    bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    if (i0 + u * T + tid >= NE) continue;
+                    // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
+                    const int slot = nt_bucket_slot(t, (int32_t)key_of(k[u]), home[u], bq[u], full);
+                    if (slot >= 0 && cs[u]) lds_add<C, MV>(t, slot, (unsigned long long)cs[u], 0ull, sm[u], vt, p);
+                }
+            }
+        }
+        if constexpr (NT) if (p.n_src > 0 && p.src_narrow) {   // narrow table: a source entry's key from its mix
             const uint32_t NE = skip ? 0u : s_soff[p.n_src];   // (compact: n_src <= kMaxSrcFlat)
             for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
                 int64_t k[kSrcU], cs[kSrcU], sm[kSrcU][1];
@@ -3606,7 +3653,38 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
             __syncthreads();
             const uint32_t NE = nrange ? s_total : 0u;
-            for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
+            for (uint32_t i0 = 0; !p.src_narrow && i0 < NE; i0 += kSrcU * T) {   // wide sources (a loop of its own)
+                int64_t mk[kSrcU], cs[kSrcU], v[kSrcU];
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    const uint32_t i = i0 + u * T + tid;
+                    mk[u] = cs[u] = v[u] = 0;
+                    if (i >= NE) continue;
+                    int lo = 0, hi = nrange;   // the range of entry i: the last base <= i
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_rb[mid] <= i) lo = mid;
+                        else hi = mid;
+                    }
+                    const auto base = gbl(p.src[lo / nreg].base + (int64_t)(r_lo + lo % nreg) * 4 * cap);
+                    const uint32_t e = i - s_rb[lo];
+                    mk[u] = base[e];
+                    cs[u] = base[cap + e];
+                    v[u] = base[3 * cap + e];
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    if (i0 + u * T + tid >= NE) continue;
+                    const int sl = slot_of((int32_t)key_of(mk[u]));   // (keys32: a mix's key is its int32)
+                    if (sl < 0) {
+                        full = true;
+                        continue;
+                    }
+                    atomicAdd(&t_cs[sl], (uint32_t)cs[u]);
+                    lds_val(&t_v[sl], v[u], vt, true);
+                }
+            }
+            for (uint32_t i0 = 0; p.src_narrow && i0 < NE; i0 += kSrcU * T) {
                 int64_t cs[kSrcU], v[kSrcU];
                 int32_t mk[kSrcU];
 #pragma unroll
