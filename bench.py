@@ -252,17 +252,25 @@ class TwoPhase:
         self.held = True
         return got, sent
 
-    def checkpoint(self):
+    def checkpoint(self, asynchronous=False):
         """prepareSnapshotPreBarrier + snapshotState; returns (collected rows, bytes sent,
-        (global image, timer watermark))"""
+        (global image, timer watermark)) -- asynchronous: the image is None, its copy to the host
+        overlaps the next rounds and snapshot_wait returns it"""
         if self.comm is not None:
             got, sent, _ = self._ship_capi(True)
         else:
             got, sent, _ = self._ship(self.local.flush_partials(device_output=True), self.wm)
         self.glob.prepare_snapshot_pre_barrier()
+        if asynchronous:
+            self.glob.snapshot_state_async()
+            return got, sent, None
         # (a copy: the image outlives the operator -- a failover closes it and restores a new one
         # from the image; copy=False would leave views of the closed handle's pinned memory)
         return got, sent, self.glob.snapshot_state(copy=True)
+
+    def snapshot_wait(self):
+        """the image of the last asynchronous checkpoint (views of the operator's pinned image)"""
+        return self.glob.snapshot_state_wait(copy=False)
 
     def finish(self):
         """end of input (Long.MAX_VALUE); returns (rows of both last fires, bytes sent)"""
@@ -655,8 +663,12 @@ def main():
         torch.cuda.synchronize()
         c0 = time.perf_counter()
         if tp is not None:
-            got, sent, (img, _) = tp.checkpoint()
-            ckpt["state_rows"] += len(img["key"])
+            snapshot_collect()
+            got, sent, image = tp.checkpoint(asynchronous=not args.sync_snapshot)
+            if image is None:
+                ckpt["pending"] = True
+            else:
+                ckpt["state_rows"] += len(image[0]["key"])
         else:
             got, sent = 0, 0
             snapshot_collect()
@@ -676,7 +688,7 @@ def main():
         state backend takes it; within the step, so the timed region pays for its copy)"""
         if ckpt.pop("pending", False):
             c0 = time.perf_counter()
-            img, _ = op.snapshot_state_wait(copy=False)
+            img, _ = tp.snapshot_wait() if tp is not None else op.snapshot_state_wait(copy=False)
             ckpt["state_rows"] += len(img["key"])
             ckpt["s"] += time.perf_counter() - c0
 
@@ -767,6 +779,7 @@ def main():
                         k_next = intern_async(hi)
                     kdict.intern_wait()
         if two_phase:
+            snapshot_collect()
             nr, sent = tp.finish()
             return rows + nr, xgmi + sent
         if held:
