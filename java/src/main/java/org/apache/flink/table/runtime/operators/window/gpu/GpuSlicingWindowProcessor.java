@@ -89,6 +89,8 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
     private transient WindowTimerService<Long> timerService;
     private transient long lastProcTimer;
     private transient boolean asyncPending;
+    /** an fg_snapshot_state_async not collected (a checkpoint that failed before its wait). */
+    private transient boolean snapshotPending;
     private transient boolean batchHanded;
 
     public GpuSlicingWindowProcessor(GpuWindowAggSpec spec, ZoneId shiftTimeZone) {
@@ -324,8 +326,13 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         flushBatch();
         collectHeld();
         FlinkGpu.flush(handle);
+        if (snapshotPending) {   // (a failed checkpoint's image: collected and dropped)
+            FlinkGpu.snapshotStateWait(handle, new ByteBuffer[7], new long[1]);
+            snapshotPending = false;
+        }
         // the image's export and host copy run on the GPU while the previous image is cleared
         FlinkGpu.snapshotStateAsync(handle);
+        snapshotPending = true;
         writeKeyedState();
     }
 
@@ -360,6 +367,7 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         ByteBuffer[] cols = new ByteBuffer[7];
         long[] wm = new long[1];
         int n = (int) FlinkGpu.snapshotStateWait(handle, cols, wm);
+        snapshotPending = false;
         for (ByteBuffer c : cols) {
             if (c != null) {
                 c.order(ByteOrder.nativeOrder());
