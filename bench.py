@@ -685,8 +685,9 @@ def main():
         return got, sent
 
     def snapshot_collect():
-        """snapshotState's asynchronous part: the host image of the pending snapshot (the
-        state backend takes it; within the step, so the timed region pays for its copy)"""
+        """snapshotState's asynchronous part: the host image of the pending snapshot (the state
+        backend takes it) -- at the next checkpoint, or after the last step; the timed region
+        pays for every copy"""
         if ckpt.pop("pending", False):
             c0 = time.perf_counter()
             img, _ = tp.snapshot_wait() if tp is not None else op.snapshot_state_wait(copy=False)
@@ -780,12 +781,10 @@ def main():
                         k_next = intern_async(hi)
                     kdict.intern_wait()
         if two_phase:
-            snapshot_collect()
             nr, sent = tp.finish()
             return rows + nr, xgmi + sent
         if held:
             rows += op.collect_fired().n
-        snapshot_collect()
         r = op.process_watermark(JMAX, device_output=True)
         rows += r.n
         assert args.wm_sync or rows == op.stats()["rows_fired"] - rows0
@@ -806,6 +805,7 @@ def main():
             op.synchronize()
             pre_last = kstats()
         one_step()
+    snapshot_collect()
     op.synchronize()
     # every kernel class is timed in the warmup; the timed region brackets only the dominant
     # one with HIP events (two events per launch perturb the stream: timing every class costs
@@ -838,6 +838,10 @@ def main():
         rows, xg = one_step()
         tot_rows += rows
         tot_xgmi += xg
+    # the last checkpoint's image (each earlier one was collected by the next checkpoint: the async
+    # part of a snapshot completes while the job runs on, as a heap backend's AsyncSnapshotCallable
+    # does); inside the timed region
+    snapshot_collect()
     op.synchronize()
     torch.cuda.synchronize()
     if dist:
