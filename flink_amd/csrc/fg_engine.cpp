@@ -301,6 +301,12 @@ struct fg_handle {
     // stream after the export kernels (event ev_snap), collected by fg_snapshot_state_wait
     hipStream_t snap_stream = nullptr;
     hipEvent_t ev_snap = nullptr;
+    unsigned snap_host_flags = hipHostMallocDefault;   // FG_SNAP_HOST_FLAGS (A/B)
+    hipMemcpyKind snap_copy_kind = hipMemcpyDeviceToHost;   // FG_SNAP_COPY_KIND (A/B: 1024 = no CUs)
+    // FG_SNAP_CUS: CUs the snapshot copy's stream may use (0: all, the default). Masked to 8-64 CUs
+    // the concurrent kernels keep their speed but the copy crawls: configs[4] 35.3 vs 24.9 ms per
+    // step (profiles/r05/zipf_ab/snap_cus)
+    int snap_cus = 0;
     bool snap_pending = false;
     int64_t snap_total = 0, snap_wm = 0;
     DevBuf hb_key[2], hb_ts[2], hb_val[2], hb_null[2];
@@ -3529,6 +3535,9 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
     if (const char* e = getenv("FG_TILE_SPLIT")) hp->tile_split = std::atoi(e) != 0;
     if (const char* e = getenv("FG_NARROW_TABLES")) hp->narrow_tables = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_HOT")) hp->tile_hot = std::atoi(e) != 0;
+    if (const char* e = getenv("FG_SNAP_HOST_FLAGS")) hp->snap_host_flags = (unsigned)std::strtoul(e, nullptr, 0);
+    if (const char* e = getenv("FG_SNAP_CUS")) hp->snap_cus = std::max(0, std::atoi(e));
+    if (const char* e = getenv("FG_SNAP_COPY_KIND")) hp->snap_copy_kind = (hipMemcpyKind)std::atoi(e);
     if (const char* e = getenv("FG_TILE_CHUNK")) hp->tile_chunk = (uint32_t)std::max(0, std::atoi(e));
     hp->tile_ok = hp->tile_env;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
@@ -4155,32 +4164,49 @@ static int snapshot_begin(fg_handle* h) {
         }
         ti++;
     }
-    HIPCHK(h, h->hs_key.ensure(b8));
-    HIPCHK(h, h->hs_slice.ensure(b8));
-    HIPCHK(h, h->hs_cs.ensure(b8));
-    HIPCHK(h, h->hs_cv.ensure(b8));
-    HIPCHK(h, h->hs_sum.ensure(b8));
+    HIPCHK(h, h->hs_key.ensure(b8, h->snap_host_flags));
+    HIPCHK(h, h->hs_slice.ensure(b8, h->snap_host_flags));
+    HIPCHK(h, h->hs_cs.ensure(b8, h->snap_host_flags));
+    HIPCHK(h, h->hs_cv.ensure(b8, h->snap_host_flags));
+    HIPCHK(h, h->hs_sum.ensure(b8, h->snap_host_flags));
     if (h->mv) {
-        HIPCHK(h, h->hs_v1.ensure(b8));
-        HIPCHK(h, h->hs_v2.ensure(b8));
+        HIPCHK(h, h->hs_v1.ensure(b8, h->snap_host_flags));
+        HIPCHK(h, h->hs_v2.ensure(b8, h->snap_host_flags));
     }
     if (total > 0) {
         if (!h->snap_stream) {
-            HIPCHK(h, hipStreamCreateWithFlags(&h->snap_stream, hipStreamNonBlocking));
+            // the runtime copies device -> host with blit kernels, which slow a concurrent fire or
+            // pass 1 4-10x; a CU mask (FG_SNAP_CUS, spread over the XCDs) keeps the kernels' speed
+            // but slows the copy more than it saves (A/B above), so the default leaves it unmasked
+            bool masked = false;
+            if (h->snap_cus > 0) {
+                int ncu = 0;
+                if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess &&
+                    ncu > h->snap_cus) {
+                    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+                    for (int i = 0; i < h->snap_cus; i++) {
+                        const int cu = (int)((int64_t)i * ncu / h->snap_cus);
+                        mask[(size_t)cu / 32] |= 1u << (cu % 32);
+                    }
+                    masked = hipExtStreamCreateWithCUMask(&h->snap_stream, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+                }
+            }
+            if (!masked) HIPCHK(h, hipStreamCreateWithFlags(&h->snap_stream, hipStreamNonBlocking));
             HIPCHK(h, hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming));
         }
         HIPCHK(h, hipEventRecord(h->ev_snap, h->stream));   // (after the export kernels)
         HIPCHK(h, hipStreamWaitEvent(h->snap_stream, h->ev_snap, 0));
         hipStream_t cs = h->snap_stream;
+        const hipMemcpyKind kd = h->snap_copy_kind;
         if (h->mv) {
-            HIPCHK(h, hipMemcpyAsync(h->hs_v1.p, h->s_v1.p, 8 * total, hipMemcpyDeviceToHost, cs));
-            HIPCHK(h, hipMemcpyAsync(h->hs_v2.p, h->s_v2.p, 8 * total, hipMemcpyDeviceToHost, cs));
+            HIPCHK(h, hipMemcpyAsync(h->hs_v1.p, h->s_v1.p, 8 * total, kd, cs));
+            HIPCHK(h, hipMemcpyAsync(h->hs_v2.p, h->s_v2.p, 8 * total, kd, cs));
         }
-        HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, hipMemcpyDeviceToHost, cs));
-        HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, hipMemcpyDeviceToHost, cs));
-        HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, hipMemcpyDeviceToHost, cs));
-        HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, hipMemcpyDeviceToHost, cs));
-        HIPCHK(h, hipMemcpyAsync(h->hs_sum.p, h->s_sum.p, 8 * total, hipMemcpyDeviceToHost, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, kd, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, kd, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, kd, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, kd, cs));
+        HIPCHK(h, hipMemcpyAsync(h->hs_sum.p, h->s_sum.p, 8 * total, kd, cs));
     }
     h->snap_pending = true;
     h->snap_total = total;
