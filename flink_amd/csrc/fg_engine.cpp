@@ -308,6 +308,7 @@ struct fg_handle {
     // step (profiles/r05/zipf_ab/snap_cus)
     int snap_cus = 0;
     bool snap_pending = false;
+    bool snap_cv_alias = false;   // the pending image's cnt_val column is its cnt_star column
     int64_t snap_total = 0, snap_wm = 0;
     DevBuf hb_key[2], hb_ts[2], hb_val[2], hb_null[2];
     DevBuf hb_narrow[2];   // FG_HOST narrow columns (fg_batch.format) before widening
@@ -4205,7 +4206,12 @@ static int snapshot_begin(fg_handle* h) {
         HIPCHK(h, hipMemcpyAsync(h->hs_key.p, h->s_key.p, 8 * total, kd, cs));
         HIPCHK(h, hipMemcpyAsync(h->hs_slice.p, h->s_slice.p, 8 * total, kd, cs));
         HIPCHK(h, hipMemcpyAsync(h->hs_cs.p, h->s_cs.p, 8 * total, kd, cs));
-        HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, kd, cs));
+        // no table counts NULL values: COUNT(v) = COUNT(*) for every entry, and the image's
+        // cnt_val column is its cnt_star column (a fifth less to copy while the job runs on)
+        bool any_null = false;
+        for (auto& kv : h->tables) any_null = any_null || kv.second->has_null;
+        h->snap_cv_alias = !any_null;
+        if (any_null) HIPCHK(h, hipMemcpyAsync(h->hs_cv.p, h->s_cv.p, 8 * total, kd, cs));
         HIPCHK(h, hipMemcpyAsync(h->hs_sum.p, h->s_sum.p, 8 * total, kd, cs));
     }
     h->snap_pending = true;
@@ -4224,7 +4230,7 @@ static int snapshot_end(fg_handle* h, fg_state_rows* out, int64_t* timer_waterma
     out->key = h->hs_key.as<int64_t>();
     out->slice_end = h->hs_slice.as<int64_t>();
     out->cnt_star = h->hs_cs.as<int64_t>();
-    out->cnt_val = h->hs_cv.as<int64_t>();
+    out->cnt_val = h->snap_cv_alias ? h->hs_cs.as<int64_t>() : h->hs_cv.as<int64_t>();
     out->sum = h->hs_sum.as<int64_t>();
     out->min = h->mv ? h->hs_v1.as<int64_t>() : nullptr;   // multi-value operators: the MIN / MAX slots
     out->max = h->mv ? h->hs_v2.as<int64_t>() : nullptr;

@@ -335,7 +335,8 @@ int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermar
  * the operator takes batches, watermarks and partials meanwhile. _wait returns that image (the
  * fg_snapshot_state layout, valid until the next snapshot call) once the copy has completed.
  * One snapshot at a time: fg_snapshot_state[_async] fails with FG_ESTATE while one is not
- * collected. fg_snapshot_state is _async + _wait. */
+ * collected. fg_snapshot_state is _async + _wait. An image of an operator that never saw a NULL
+ * value may return the same column for cnt_star and cnt_val (they are equal). */
 int  fg_snapshot_state_async(fg_handle* h);
 int  fg_snapshot_state_wait(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
