@@ -761,7 +761,9 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     p->region_bits = h->region_bits;
     p->n_src = (int)srcs.size();
     p->src_narrow = src_narrow ? 1 : 0;
-    if (!srcs.empty()) {
+    if (srcs.size() <= 2) {   // by value in the arguments (no descriptor copy on the stream)
+        for (size_t i = 0; i < srcs.size(); i++) p->src_in[i] = srcs[i];
+    } else {
         int rc = arena_put(h, srcs.data(), srcs.size(), &p->src);
         if (rc) return rc;
     }
@@ -822,7 +824,9 @@ int tile_job_params(fg_handle* h, int ji, TileFire* f) {
         if (x->narrow) p.src_narrow = 1;
     }
     p.n_src = (int)srcs.size();
-    if (!srcs.empty()) {
+    if (srcs.size() <= 2) {   // by value in the arguments (no descriptor copy on the stream)
+        for (size_t i = 0; i < srcs.size(); i++) p.src_in[i] = srcs[i];
+    } else {
         int rc = arena_put(h, srcs.data(), srcs.size(), &p.src);
         if (rc) return rc;
     }

@@ -214,7 +214,8 @@ struct MergeParams {
     int32_t compact;           // compact LDS table (fast_stream, no src tables, < 2^32 records)
     int32_t n_src;
     int32_t src_narrow;        // some source table holds narrow (16-B) entries
-    const TableRef* src;       // device array [n_src]
+    const TableRef* src;       // device array [n_src]; null: n_src <= 2, the tables in src_in
+    TableRef src_in[2];        // up to two source tables by value (no descriptor copy per merge)
     int32_t n_batches;
     int32_t val_type;          // 0 none, 1 i64, 2 f64
     const StagedBatch* batches;  // device array [n_batches]

@@ -1624,6 +1624,12 @@ __device__ __forceinline__ void write_row(const MergeParams& p, unsigned long lo
     write_row_k(p, o, key_of(h), cs, cn, vals, vt);   // state holds the key's mix
 }
 
+// source table j of a merge: by value in the arguments (n_src <= 2) or from the device array
+// (static indices into the arguments: a runtime index would copy them to scratch)
+__device__ __forceinline__ TableRef src_at(const MergeParams& p, int j) {
+    if (p.src) return p.src[j];
+    return j == 0 ? p.src_in[0] : p.src_in[1];
+}
 constexpr int kSrcU = 2;   // source-table entries per thread per round (1, 3, 4 measured +-2 % or slower)
 constexpr unsigned long long kMarkBit = 1ull << 63;   // wide table: entry touched by a marking source (NULL-count word)
 constexpr int kMaxSrcFlat = 64;   // source tables of one merge (hop: size / slide)
@@ -2023,7 +2029,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
         if (tid == 0) s_flags = 0;
         if ((!C || p.n_src > 0) && tid < 64) {   // source tables: per-region entry counts -> flat prefix
             const int nsrc = p.n_src <= kMaxSrcFlat ? p.n_src : 0;
-            const uint32_t v = tid < nsrc ? gbl(p.src[tid].counts)[r] : 0u;
+            const uint32_t v = tid < nsrc ? gbl(src_at(p, tid).counts)[r] : 0u;
             uint32_t x = v;
             for (int off = 1; off < 64; off <<= 1) {
                 const uint32_t y = __shfl_up(x, off);
@@ -2031,8 +2037,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
             }
             if (tid < nsrc) {
                 s_soff[tid + 1] = x;
-                s_sbase[tid] = p.src[tid].base + (int64_t)r * cols * cap;
-                s_snar[tid] = p.src[tid].narrow ? 1 : 0;
+                s_sbase[tid] = src_at(p, tid).base + (int64_t)r * cols * cap;
+                s_snar[tid] = src_at(p, tid).narrow ? 1 : 0;
             }
             if (tid == 0) s_soff[0] = 0;
         }
@@ -2201,7 +2207,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 }
             }
             for (int j = 0; !skip && p.n_src > kMaxSrcFlat && j < p.n_src; j++) {   // many tables: one by one
-                const TableRef src = p.src[j];
+                const TableRef src = src_at(p, j);
                 const uint32_t n = gbl(src.counts)[r];
                 const auto base = gbl(src.base + (int64_t)r * cols * cap);
                 const bool nar = src.narrow != 0;
@@ -3634,7 +3640,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
 #pragma unroll
                 for (int q = 0; q < RPL; q++) {
                     const int g = RPL * lane + q;
-                    c[q] = g < nrange ? gbl(p.src[g / nreg].counts)[r_lo + g % nreg] : 0u;
+                    c[q] = g < nrange ? gbl(src_at(p, g / nreg).counts)[r_lo + g % nreg] : 0u;
                     x += c[q];
                 }
                 for (int off = 1; off < 64; off <<= 1) {
@@ -3666,7 +3672,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                         if (s_rb[mid] <= i) lo = mid;
                         else hi = mid;
                     }
-                    const auto base = gbl(p.src[lo / nreg].base + (int64_t)(r_lo + lo % nreg) * 4 * cap);
+                    const auto base = gbl(src_at(p, lo / nreg).base + (int64_t)(r_lo + lo % nreg) * 4 * cap);
                     const uint32_t e = i - s_rb[lo];
                     mk[u] = base[e];
                     cs[u] = base[cap + e];
@@ -3699,7 +3705,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                         if (s_rb[mid] <= i) lo = mid;
                         else hi = mid;
                     }
-                    const TableRef& sr = p.src[lo / nreg];
+                    const TableRef sr = src_at(p, lo / nreg);
                     const auto base = gbl(sr.base + (int64_t)(r_lo + lo % nreg) * 4 * cap);
                     const uint32_t e = i - s_rb[lo];
                     const bool nar = sr.narrow != 0;   // (the operator's keys fit 32 bits: a mix's key is its int32)
