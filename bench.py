@@ -818,7 +818,7 @@ def main():
     for k, v in last.items():
         b = pre_last.get(k, dict(launches=0, total_ms=0.0, records=0, rows=0))
         if v["launches"] - b["launches"] > 0:
-            warm[k] = dict(v, launches=v["launches"] - b["launches"], total_ms=v["total_ms"] - b["total_ms"])
+            warm[k] = {f: v[f] - b[f] for f in ("launches", "total_ms", "records", "rows")}
     dom_class = max(warm.items(), key=lambda kv: kv[1]["total_ms"])[0] if warm else None
     if dom_class and args.warmup > 0:
         is_local = dom_class.startswith("local_")

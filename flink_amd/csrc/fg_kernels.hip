@@ -3485,9 +3485,14 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             w.bad = true;
             src = 0;
         }
+#if defined(FG_DIAG_FIRE) && (FG_DIAG_FIRE & 1)   // (diagnostic: no record loads, keys from the source index)
+        kr[u] = (int32_t)((src * 2654435761u) >> 20);
+        vr[u] = (int64_t)src;
+#else
         const Rec12 r = ld_tile_rec(w.rec, (uint64_t)src);
         kr[u] = (int32_t)r.k;
         vr[u] = rec12_val(r);
+#endif
     }
     w.b += kTileWin;
     return !done;
@@ -3604,6 +3609,9 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
         if (tid == 0) s_flags = 0;
         __syncthreads();
         bool full = false;
+#if defined(FG_DIAG_FIRE)
+        uint64_t diag_sink = 0;
+#endif
         // the slot of `key` in the table (claimed if new), -1 when the table is full
         auto slot_of = [&](int32_t key) -> int {
             if (key == kEmpty32) return S;
@@ -3805,6 +3813,12 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
         } else if (live) {
             // one window's records into the table, one probe loop per record (the plain fire)
             auto insert_plain = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+#if defined(FG_DIAG_FIRE) && (FG_DIAG_FIRE & 2)   // (diagnostic: no inserts, the records consumed)
+#pragma unroll
+                for (int u = 0; u < kTileRpl; u++)
+                    if (lane + 64 * u < nrec) diag_sink ^= (uint64_t)kr[u] ^ (uint64_t)vr[u];
+                return;
+#endif
                 uint32_t hm[kTileRpl];
                 int4 bq[kTileRpl];
 #pragma unroll
@@ -4000,6 +4014,9 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             }
         }
         if (full) atomicOr(&s_flags, 4u);
+#if defined(FG_DIAG_FIRE)
+        if (diag_sink == 0x5EEDull) atomicOr(p.overflow, 0u);
+#endif
         __syncthreads();
         // compaction: the occupied slots' ranks (round k covers slots [k*T, (k+1)*T); the last
         // round the sentinel slot), a dense rank -> slot map, then one row per lane

@@ -1,21 +1,18 @@
-# A/B variant libraries of the tile fire (round 5): flink_amd/build_var/<name>/libflinkgpu.so
-# Usage: bash scripts/build_fire_variants.sh  (then FLINKGPU_LIB=... python bench.py)
+# Diagnostic variant libraries of the tile fire: flink_amd/build_var/<name>/libflinkgpu.so
+# Usage: bash scripts/build_fire_variants.sh name "defines" [name "defines" ...]
+#        (then FLINKGPU_LIB=flink_amd/build_var/<name>/libflinkgpu.so python bench.py ...)
 set -e
 cd "$(dirname "$0")/../flink_amd"
+make -s -j4 libflinkgpu.so
 HIPCC=/opt/rocm/bin/hipcc
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result"
 build() {   # name, defines
     d=build_var/$1; mkdir -p $d
-    for f in fg_engine.cpp fg_keydict.hip fg_late.hip fg_comm.cpp; do [ -f $d/$f.o ] || cp build/$f.o $d/$f.o; done
+    for f in fg_engine.cpp fg_keydict.hip fg_late.hip fg_comm.cpp; do cp build/$f.o $d/$f.o; done
     $HIPCC $F $2 -x hip -c csrc/fg_kernels.hip -o $d/fg_kernels.hip.o
     $HIPCC --offload-arch=gfx950 -shared -fPIC -Wl,--version-script=csrc/libflinkgpu.map -o $d/libflinkgpu.so $d/*.o \
         -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 }
-mkdir -p var
-build shfl_scan "-DFG_EXP_SHFL_SCAN" &
-build cond_loads "-DFG_EXP_COND_LOADS" &
-build all_old "-DFG_EXP_SHFL_SCAN -DFG_EXP_COND_LOADS" &
-build tile_block "-DFG_EXP_TILE_BLOCK" &
-build pipe3 "-DFG_EXP_PIPE3" &
+while [ $# -ge 2 ]; do build "$1" "$2" & shift 2; done
 wait
 ls -la build_var/*/libflinkgpu.so
