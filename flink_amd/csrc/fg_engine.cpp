@@ -1201,12 +1201,16 @@ int materialize_lane(fg_handle* h, int l) {
 
 // Lane l fires straight from its tile passes: every pass a tile pass of the same bits, no skew,
 // COUNT(*) below 2^32
+// (the split fire walks at most kMaxTilePasses passes: a skewed lane of more passes is materialized;
+// the plain fire takes any number -- a window of many small micro-batches stays on the tiles)
 bool tile_fire_ok(const fg_handle* h, const Lane& ln, bool allow_skew = false) {
     if (ln.passes.empty() || ln.acc_fill != 0 || ln.fill >= ((int64_t)1 << 32) || h->mv) return false;
-    if (allow_skew && ln.passes.size() > (size_t)kMaxTilePasses) return false;
-    for (const Staged* s : ln.passes)
+    bool skew = false;
+    for (const Staged* s : ln.passes) {
         if (!s->tiles || (s->skew && !allow_skew) || s->bits != ln.passes[0]->bits) return false;
-    return true;
+        skew = skew || s->skew;
+    }
+    return !(skew && ln.passes.size() > (size_t)kMaxTilePasses);
 }
 
 constexpr int64_t kTileSpreadMin = 1 << 18;     // records of a lane worth a spread (split) fire

@@ -89,33 +89,26 @@ __device__ __forceinline__ int64_t tab_v(gtab_t b, int cap, uint32_t i, bool nar
     return nar ? b[cap + i] : b[(3 + q) * cap + i];
 }
 
-// Tile-staged records (k_tile_part1 -> k_tile_fire / k_tile_mat): packed 12-B records {int32 key,
-// value bits} at 12 * i, one dwordx3 access each (4-B aligned). The tiles are written whole and in
+// Tile-staged records (k_tile_part1 -> k_tile_fire / k_tile_mat): packed 12-B records {value bits,
+// int32 key} at 12 * i, one dwordx3 access each (4-B aligned). The tiles are written whole and in
 // order (a wave's stores are 768 contiguous bytes), and the fire gathers a bucket's fragments of a
-// few records each: a fragment is one contiguous range -- with the block layout above its keys
-// and its values were two ranges in different cache lines, two loads per record.
-// (FG_EXP_TILE_BLOCK: the block layout, A/B)
+// few records each: a fragment is one contiguous range. The value comes first so that a record
+// loads into three VGPRs whose first two are an aligned 64-bit pair: with the key first the
+// compiler realigned the value with two moves right after each load -- and waited for the load
+// there (s_waitcnt vmcnt(0) per record: the fire's gathers were never in flight across its inserts)
 __device__ __forceinline__ Rec12 ld_tile_rec(const void* base, uint64_t i) {
-#ifdef FG_EXP_TILE_BLOCK
-    return ld_rec12(base, i);
-#else
     const uint32_t __attribute__((address_space(1)))* q = (const uint32_t __attribute__((address_space(1)))*)base + 3 * i;
     Rec12 r;   // (three adjacent dwords: one global_load_dwordx3)
-    r.k = q[0];
-    r.lo = q[1];
-    r.hi = q[2];
+    r.lo = q[0];
+    r.hi = q[1];
+    r.k = q[2];
     return r;
-#endif
 }
 __device__ __forceinline__ void st_tile_rec(void* base, uint64_t i, int64_t key, int64_t val) {
-#ifdef FG_EXP_TILE_BLOCK
-    st_rec12(base, i, key, val);
-#else
     uint32_t __attribute__((address_space(1)))* q = (uint32_t __attribute__((address_space(1)))*)base + 3 * i;
-    q[0] = (uint32_t)key;   // (one global_store_dwordx3)
-    q[1] = (uint32_t)val;
-    q[2] = (uint32_t)((uint64_t)val >> 32);
-#endif
+    q[0] = (uint32_t)val;   // (one global_store_dwordx3)
+    q[1] = (uint32_t)((uint64_t)val >> 32);
+    q[2] = (uint32_t)key;
 }
 
 // A pointer every lane of the wave holds (loaded from LDS, so the compiler cannot tell):
@@ -145,13 +138,14 @@ __device__ __forceinline__ void lds_barrier() {
 // *h_out = fmix64(key), the form in which the key is staged and kept (fg_window.h)
 __device__ __forceinline__ int classify(const IngestParams& p, int64_t key, int64_t ts, int64_t* q_out,
                                         int64_t* h_out) {
-    int64_t target, q;
+    int64_t q;
     const uint64_t d = (uint64_t)ts + (uint64_t)p.w.tz - (uint64_t)p.tbase;
     const uint64_t qq = __umul64hi(d, p.div_m);
     const int64_t end_fast = p.tbase + (int64_t)((qq + 1) * (uint64_t)p.w.slice);
     if (p.div_m != 0 && d < (1ull << 32) && ts != JMAX && end_fast > p.fired_lim) {
         q = p.qbase + (int64_t)qq;              // assignSliceEnd, not fired: no late handling
     } else {
+        int64_t target;
         if (!target_slice(p.w, ts, p.progress, &target)) return -1;
         q = floor_div_fast(target, p.w.slice, p.w.rslice);
     }
@@ -3120,6 +3114,11 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
             if (H > 1 && t0 + HALF < end) load(t0 + HALF, kb, tb);   // (in flight across the first half's ranking)
             classify_half(t0, ka, ta, rcb[0], k32[0]);
             if (H > 1) {
+                // the first half's ranks and keys wait in LDS (s_k is free until the staging): a tile of
+                // two halves then holds one half's classification state in registers at a time
+#pragma unroll
+                for (int u = 0; u < R; u++)
+                    reinterpret_cast<uint2*>(s_k)[u * T + tid] = make_uint2(rcb[0][u], k32[0][u]);
                 if (t0 + HALF < end) {
                     classify_half(t0 + HALF, kb, tb, rcb[H - 1], k32[H - 1]);
                 } else {
@@ -3128,10 +3127,19 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
                 }
             }
         }
+        if (H > 1) asm volatile("" ::: "memory");   // (the value loads not hoisted into the classification)
         longlong2 va[H][R / 2];
 #pragma unroll
         for (int hh = 0; hh < H; hh++) load_vals(t0 + (int64_t)hh * HALF, va[hh]);   // (in flight across the scan)
         lds_barrier();
+        if (H > 1) {   // (each thread its own stash entries, read before the barrier that precedes the staging)
+#pragma unroll
+            for (int u = 0; u < R; u++) {
+                const uint2 q = reinterpret_cast<const uint2*>(s_k)[u * T + tid];
+                rcb[0][u] = q.x;
+                k32[0][u] = q.y;
+            }
+        }
         {   // exclusive scan of the tile's bucket counts, u16 pairs per word, consecutive words per thread
             constexpr int kPw = (kMaxTileBuckets / 2 + T - 1) / T;
             uint32_t c[kPw], run = 0;
@@ -3174,6 +3182,7 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
                 s_v[slot] = (unsigned long long)((u & 1) ? va[hh][u >> 1].y : va[hh][u >> 1].x);
             }
         }
+        if (H > 1) asm volatile("" ::: "memory");   // (the next tile's loads not hoisted into the staging)
         if (t0 + TILE < end) load(t0 + TILE, ka, ta);   // the next tile's first half, across the write-out
         lds_barrier();
         for (uint32_t i = tid; i < tile_total; i += T) st_tile_rec(p.tmp, (uint64_t)(t0 + i), (int64_t)s_k[i], (int64_t)s_v[i]);
@@ -3405,15 +3414,7 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
             w.g_st[q] = sum;   // (local prefix; the wave's exclusive prefix added below)
             sum += w.g_len[q];
         }
-#ifdef FG_EXP_SHFL_SCAN   // (A/B: __shfl_up scans)
-        uint32_t inc = sum;
-        for (int sft = 1; sft < 64; sft <<= 1) {
-            const uint32_t y = __shfl_up(inc, sft);
-            if (lane >= sft) inc += y;
-        }
-#else
         uint32_t inc = wave_incl_scan<false>(sum);
-#endif
         // (the scan materialized: the compiler otherwise folds `base - (prefix + inc - sum)` into a
         // chain of DPP subtracts, which produced wrong fragment bases -- DESIGN section 8)
         asm volatile("" : "+v"(inc));
@@ -3446,17 +3447,7 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
     e1 = e1 > e0 ? e1 : e0;
     e2 = e2 > e1 ? e2 : e1;
     e3 = e3 > e2 ? e3 : e2;
-#ifdef FG_EXP_SHFL_SCAN
-    uint32_t mm = e3;
-    for (int sft = 1; sft < 64; sft <<= 1) {
-        const uint32_t y = __shfl_up(mm, sft);
-        if (lane >= sft) mm = mm > y ? mm : y;
-    }
-    uint32_t pre = __shfl_up(mm, 1);
-    if (lane == 0) pre = 0;
-#else
     const uint32_t pre = wave_shr1(wave_incl_scan<true>(e3));
-#endif
     e0 = e0 > pre ? e0 : pre;
     e1 = e1 > pre ? e1 : pre;
     e2 = e2 > pre ? e2 : pre;
@@ -3464,17 +3455,17 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
     fm32[lane] = e0 | e1 << 8 | e2 << 16 | e3 << 24;
     wave_lds_sync();
     nrec = w.g_tot - w.b < (uint32_t)kTileWin ? w.g_tot - w.b : (uint32_t)kTileWin;
+    // every position's fragment, then every fragment's base: two LDS round trips for the window's
+    // records, no branch (a position past nrec reads a garbage map entry, masked below)
+    uint32_t fq[kTileRpl], dq[kTileRpl];
+#pragma unroll
+    for (int u = 0; u < kTileRpl; u++) fq[u] = fm[lane + 64 * u] & (uint32_t)(kTileGroup - 1);
+#pragma unroll
+    for (int u = 0; u < kTileRpl; u++) dq[u] = dl[fq[u]];
 #pragma unroll
     for (int u = 0; u < kTileRpl; u++) {
         const uint32_t jr = lane + 64 * u;
-#ifdef FG_EXP_COND_LOADS   // (A/B: loads only for records in the window)
-        if (jr >= nrec) {
-            kr[u] = 0;
-            vr[u] = 0;
-            continue;
-        }
-#endif
-        uint32_t src = jr < nrec ? dl[fm[jr]] + w.b + jr : 0u;
+        uint32_t src = jr < nrec ? dq[u] + w.b + jr : 0u;
         if (src >= w.n) {   // (never, if the directory and the walk agree: reported, not read)
 #ifdef FG_DEBUG_WALK
             if (!w.bad)
@@ -3981,23 +3972,6 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                 }
                 TileWalk w;
                 tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane, t_lo, t_hi);
-#ifdef FG_EXP_PIPE3   // (A/B: three windows in flight per wave, unrolled by three)
-                int32_t ka[kTileRpl], kb[kTileRpl], kc[kTileRpl];
-                int64_t va[kTileRpl], vb[kTileRpl], vc[kTileRpl];
-                uint32_t na = 0, nb = 0, nc = 0;
-                bool ha = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
-                bool hb = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kb, vb, nb);
-                while (ha) {
-                    const bool hc = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kc, vc, nc);
-                    insert(ka, va, na);
-                    if (!hb) break;
-                    ha = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
-                    insert(kb, vb, nb);
-                    if (!hc) break;
-                    hb = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kb, vb, nb);
-                    insert(kc, vc, nc);
-                }
-#else
                 int32_t ka[kTileRpl], kb[kTileRpl];
                 int64_t va[kTileRpl], vb[kTileRpl];
                 uint32_t na = 0, nb = 0;
@@ -4009,7 +3983,6 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
                     insert(kb, vb, nb);
                 }
-#endif
                 if (__ballot(w.bad) != 0 && lane == 0) atomicOr(p.overflow, 8u);
             }
         }

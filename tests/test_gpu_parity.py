@@ -111,14 +111,15 @@ def assert_rows_equal(got, exp, vt, ctx="", sum0=True, minmax=(), vmax=None, sum
 
 
 def drive_both(O, cfg, n, keys, batch, delay, jitter, null_frac=0.0, snapshot_at=None, end_wm=JMAX,
-               expected_keys=None, kstats=None, stats=None, **gen):
+               expected_keys=None, kstats=None, stats=None, buffer_records=None, **gen):
     key, ts, val, isnull = make_stream(n, keys, cfg["val_type"], jitter_ms=jitter, null_frac=null_frac, **gen)
     vmax = 1000.0 if gen.get("signed") and cfg["val_type"] == "f64" else None
     mm = tuple(a for a in cfg.get("aggs", ()) if a in ("min", "max"))
     aggs = cfg.get("aggs")
     chk = dict(minmax=mm, vmax=vmax, sums=aggs is None or any(a in ("sum", "avg", "sum0") for a in aggs),
                sum0=aggs is None or "sum0" in aggs, aggs=aggs)
-    g = gpu_mk(cfg, expected_keys=keys if expected_keys is None else expected_keys, buffer_records=max(batch * 4, 1 << 16),
+    g = gpu_mk(cfg, expected_keys=keys if expected_keys is None else expected_keys,
+               buffer_records=buffer_records or max(batch * 4, 1 << 16),
                kernel_timing=kstats is not None)
     o = oracle_mk(O, cfg)
     o_base = 0

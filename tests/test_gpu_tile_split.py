@@ -77,3 +77,16 @@ def test_spread_fire_parity(oracle_mod, name, cfg, kw, monkeypatch):
     ks = {}
     drive_both(oracle_mod, cfg, kstats=ks, **kw)
     assert ks.get("tile_split_fire", {}).get("launches", 0) > 0, ks
+
+
+def test_window_of_many_micro_batches_fires_from_the_tiles(oracle_mod):
+    """A window spanning more micro-batches than the split fire walks (kMaxTilePasses = 8): 10
+    uniform 100k-record batches per 1 s window (a shim with a small batchRecords). No pass is
+    skewed, so the plain fire takes every pass from the tiles -- no lane is materialized (ADVICE
+    round 5: the pass limit applied to unskewed lanes too)."""
+    ks = {}
+    drive_both(oracle_mod, cfg_of("tumble", 1000), kstats=ks,
+               n=3_000_000, keys=1_000_000, batch=100_000, rate_per_ms=1_000, delay=0, jitter=0,
+               buffer_records=4_000_000)
+    assert ks.get("tile_fire", {}).get("launches", 0) > 0, ks
+    assert ks.get("tile_materialize", {}).get("launches", 0) == 0, ks
