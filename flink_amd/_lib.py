@@ -81,6 +81,18 @@ class FgExchanged(C.Structure):
 
 
 COMM_ID_BYTES = 128
+ROUND_FIRED, ROUND_FLUSHED, ROUND_IDLE = 0, 1, 2
+
+
+class FgRound(C.Structure):
+    _fields_ = [("min_watermark", C.c_int64), ("min_epoch", C.c_int64), ("rows_sent", C.c_int64),
+                ("rows_received", C.c_int64), ("bytes_sent", C.c_int64), ("failed_rank", C.c_int32),
+                ("reserved0", C.c_int32)]
+
+
+class FgImageSlices(C.Structure):
+    _fields_ = [("n", C.c_int64), ("slice_end", C.c_void_p), ("first_row", C.c_void_p), ("rows", C.c_void_p),
+                ("changed", C.c_void_p)]
 
 
 class FgStats(C.Structure):
@@ -106,7 +118,7 @@ EXPORTS = (
     "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_advance_progress_async",
     "fg_advance_progress_async_n",
     "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials", "fg_snapshot_state",
-    "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
+    "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_snapshot_slices", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
     "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async",
@@ -115,7 +127,8 @@ EXPORTS = (
     "fg_key_dict_kernel_stats", "fg_key_dict_last_error", "fg_key_dict_close",
     "fg_binaryrow_hash", "fg_host_register", "fg_host_unregister",
     "fg_comm_unique_id", "fg_comm_open", "fg_comm_exchange_columns", "fg_comm_exchange_partials",
-    "fg_comm_exchange_fired", "fg_comm_exchange_flushed", "fg_comm_stream", "fg_comm_bytes_sent", "fg_comm_last_error", "fg_comm_close",
+    "fg_comm_exchange_fired", "fg_comm_exchange_flushed", "fg_comm_round_begin", "fg_comm_round_exchange",
+    "fg_comm_round_end", "fg_comm_stream", "fg_comm_bytes_sent", "fg_comm_last_error", "fg_comm_close",
 )
 
 _lib = None
@@ -213,6 +226,10 @@ def load():
                                             C.POINTER(C.c_int64)]
     L.fg_comm_exchange_fired.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int64, P, C.POINTER(C.c_int64)]
     L.fg_comm_exchange_flushed.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int64, P, C.POINTER(C.c_int64)]
+    L.fg_comm_round_begin.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int64, C.c_int64]
+    L.fg_comm_round_exchange.argtypes = [P, C.POINTER(FgRound)]
+    L.fg_comm_round_end.argtypes = [P, P]
+    L.fg_snapshot_slices.argtypes = [P, C.POINTER(FgImageSlices)]
     L.fg_comm_bytes_sent.argtypes = [P]
     L.fg_comm_bytes_sent.restype = C.c_int64
     L.fg_comm_stream.argtypes = [P]
@@ -222,7 +239,8 @@ def load():
     L.fg_comm_close.argtypes = [P]
     L.fg_comm_close.restype = None
     for fn in ("fg_comm_unique_id", "fg_comm_open", "fg_comm_exchange_columns", "fg_comm_exchange_partials",
-               "fg_comm_exchange_fired", "fg_comm_exchange_flushed"):
+               "fg_comm_exchange_fired", "fg_comm_exchange_flushed", "fg_comm_round_begin", "fg_comm_round_exchange",
+               "fg_comm_round_end"):
         getattr(L, fn).restype = C.c_int
     for fn in ("fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async", "fg_key_dict_intern_wait",
                "fg_key_dict_lookup", "fg_key_dict_arena",
@@ -230,7 +248,7 @@ def load():
         getattr(L, fn).restype = C.c_int
     for fn in ("fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress",
                "fg_advance_progress_async", "fg_advance_progress_async_n", "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials",
-               "fg_snapshot_state", "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
+               "fg_snapshot_state", "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_snapshot_slices", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_key_groups",
                "fg_partition_by_owner", "fg_partition_columns_by_owner"):
         getattr(L, fn).restype = C.c_int
     _lib = L

@@ -106,6 +106,9 @@ struct SliceTable {
     // every reader; a table takes the layout of the first writer that finds it empty, and is
     // widened in place (k_widen_table) before a writer of the wide layout or a region split
     bool narrow = false;
+    // written since the last snapshot image (fg_snapshot_slices: a shim rewrites only the keyed
+    // state of the slices whose tables changed between two checkpoints)
+    bool changed = true;
 };
 
 // One ingest pass: the bucket scan of its records over all lanes; lane l's records sit at
@@ -310,6 +313,11 @@ struct fg_handle {
     bool snap_pending = false;
     bool snap_cv_alias = false;   // the pending image's cnt_val column is its cnt_star column
     int64_t snap_total = 0, snap_wm = 0;
+    // the slices of the last image (fg_snapshot_slices): ends, row ranges, changed since the image
+    // before (SliceTable.changed, cleared at each snapshot)
+    std::vector<int64_t> img_se, img_first, img_rows;
+    std::vector<uint8_t> img_changed;
+    bool img_ready = false;   // an image was returned since the last snapshot call
     DevBuf hb_key[2], hb_ts[2], hb_val[2], hb_null[2];
     DevBuf hb_narrow[2];   // FG_HOST narrow columns (fg_batch.format) before widening
     hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -573,6 +581,7 @@ int table_new(fg_handle* h, int64_t slice_end, std::unique_ptr<SliceTable>* out)
     t->bits = h->region_bits;
     t->has_null = false;
     t->narrow = false;
+    t->changed = true;
     return FG_OK;
 }
 
@@ -672,6 +681,7 @@ int job_add(fg_handle* h, MergeJob&& j, int* id) {
     if (h->jobs.empty() && !h->fail_zeroed) HIPCHK(h, hipMemsetAsync(h->scalars.as<char>() + 4, 0, 4, h->stream));
     h->fail_zeroed = false;
     j.bits = h->region_bits;
+    if (j.dst) j.dst->changed = true;   // (every table write goes through a job, or sets upper below)
     h->jobs.push_back(std::move(j));
     *id = (int)h->jobs.size() - 1;
     return FG_OK;
@@ -1469,6 +1479,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 KTimer kt(h, K_FLUSH, ln.fill);
                 HIPCHK(h, launch_merge(p, merge_grid(h), h->stream));
                 x->upper = std::min<int64_t>(x->upper + ln.fill + ln.acc_fill, kStateCapMax);
+                x->changed = true;
             }
             continue;
         }
@@ -1668,6 +1679,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         if (fire_now) {
             if (h->retain && !h->local) {
                 t->upper = ub;
+                t->changed = true;
                 retained.push_back(se);
             } else if (t) {
                 fired_tables.push_back(se);
@@ -1676,7 +1688,10 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         } else if (cum_fire) {
             any_emit = true;
             h->fused_fired.insert(se);   // fire_windows must not fire W again
-            if (dstt) dstt->upper = ub;
+            if (dstt) {
+                dstt->upper = ub;
+                dstt->changed = true;
+            }
             if (se == cum_last) {        // the cumulative window is complete
                 fired_tables.push_back(se);
                 if (se != cum_first) fired_tables.push_back(cum_first);
@@ -1685,6 +1700,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
             }
         } else {
             t->upper = std::min<int64_t>(t->upper + ln.fill + ln.acc_fill, kStateCapMax);
+            t->changed = true;
         }
     }
     if (h->async_advance && any_emit) {
@@ -1812,7 +1828,10 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
         }
 #endif
     }
-    if (dst) dst->upper = ub;
+    if (dst) {
+        dst->upper = ub;
+        dst->changed = true;
+    }
     if (defer) {
         h->pending_out += ub;
         return FG_OK;
@@ -2016,6 +2035,7 @@ int refire_job(fg_handle* h, const std::vector<SliceTable*>& vals, const std::ve
         int64_t u = 0;
         for (SliceTable* t : h->jobs.back().srcs) u += t->upper;
         dst->upper = std::min<int64_t>(u, kStateCapMax);
+        dst->changed = true;
     }
     return FG_OK;
 }
@@ -3126,7 +3146,10 @@ int late_fire(fg_handle* h, int64_t nl) {
         for (int64_t se : ses) {
             SliceTable* t = nullptr;
             table_get(h, se, false, &t);
-            if (t) t->upper = std::min<int64_t>(t->upper + nl, kStateCapMax);
+            if (t) {
+                t->upper = std::min<int64_t>(t->upper + nl, kStateCapMax);
+                t->changed = true;
+            }
         }
     return FG_OK;
 }
@@ -4141,6 +4164,25 @@ static int snapshot_begin(fg_handle* h) {
             total += h->hs_counts.as<uint32_t>()[t * h->P + r];
         }
     }
+    // the image's slices: its rows are grouped by slice, in the tables' (ascending) order
+    h->img_ready = false;
+    h->img_se.clear();
+    h->img_first.clear();
+    h->img_rows.clear();
+    h->img_changed.clear();
+    {
+        size_t t = 0;
+        for (auto& kv : h->tables) {
+            const int64_t first = (int64_t)h->hs_off.as<uint64_t>()[t * h->P];
+            const int64_t next = t + 1 < nt ? (int64_t)h->hs_off.as<uint64_t>()[(t + 1) * h->P] : total;
+            h->img_se.push_back(kv.first);
+            h->img_first.push_back(first);
+            h->img_rows.push_back(next - first);
+            h->img_changed.push_back(kv.second->changed ? 1 : 0);
+            kv.second->changed = false;
+            t++;
+        }
+    }
     const size_t b8 = 8 * (size_t)std::max<int64_t>(total, 1);
     HIPCHK(h, h->s_key.ensure(b8));
     HIPCHK(h, h->s_slice.ensure(b8));
@@ -4243,6 +4285,18 @@ static int snapshot_end(fg_handle* h, fg_state_rows* out, int64_t* timer_waterma
     out->min = h->mv ? h->hs_v1.as<int64_t>() : nullptr;   // multi-value operators: the MIN / MAX slots
     out->max = h->mv ? h->hs_v2.as<int64_t>() : nullptr;
     if (timer_watermark) *timer_watermark = h->snap_wm;
+    h->img_ready = true;
+    return FG_OK;
+}
+
+int fg_snapshot_slices(fg_handle* h, fg_image_slices* out) {
+    if (!h || !out) return FG_EINVAL;
+    if (!h->img_ready) return h->fail(FG_ESTATE, "fg_snapshot_slices: no image returned since the last snapshot call");
+    out->n = (int64_t)h->img_se.size();
+    out->slice_end = h->img_se.data();
+    out->first_row = h->img_first.data();
+    out->rows = h->img_rows.data();
+    out->changed = h->img_changed.data();
     return FG_OK;
 }
 
@@ -4269,6 +4323,7 @@ int fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark
 
 int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
     if (!h || !in) return FG_EINVAL;
+    const bool was_empty = h->tables.empty();   // (restored into a new handle: its tables equal the image)
     h->cnt_bound = JMAX;
     h->keys32 = false;
     HIPCHK(h, hipSetDevice(h->device));
@@ -4383,6 +4438,7 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
         rc = check_overflow(h);
         if (rc) return rc;
         t->upper = std::min<int64_t>(t->upper + m, kStateCapMax);
+        t->changed = true;
     }
     // open(): processor progress restarts at Long.MIN_VALUE, and so does the restored timer
     // service's watermark (InternalTimerServiceImpl.currentWatermark is not part of the
@@ -4416,6 +4472,10 @@ int fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark) {
             if (ds_fired(last, timer_watermark)) h->retire_at[kv.first] = ds_cleanup(last, h->lateness);
         }
     }
+    // the keyed state backend holds exactly this image: a restored table is not "changed" until a
+    // write reaches it (the shim's next checkpoint rewrites only the slices that change)
+    if (was_empty)
+        for (auto& kv : h->tables) kv.second->changed = false;
     return FG_OK;
 }
 

@@ -491,6 +491,20 @@ class WindowAggOperator:
             img["min"], img["max"] = col(s.min), col(s.max)
         return img, wm.value
 
+    def snapshot_slices(self) -> dict:
+        """fg_snapshot_slices: the slices of the image the last snapshot returned -- slice_end,
+        first_row, rows (its rows in the image), changed (written since the image before)."""
+        s = L.FgImageSlices()
+        L.check(self._lib.fg_snapshot_slices(self._h, C.byref(s)), self._h)
+        n = int(s.n)
+
+        def col(p, ct, dt):
+            if n == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,)).copy()
+        return dict(slice_end=col(s.slice_end, C.c_int64, np.int64), first_row=col(s.first_row, C.c_int64, np.int64),
+                    rows=col(s.rows, C.c_int64, np.int64), changed=col(s.changed, C.c_uint8, np.uint8).astype(bool))
+
     def restore_state(self, image, timer_watermark: int):
         names = ("key", "slice_end", "cnt_star", "cnt_val", "sum") + (("min", "max") if "min" in image else ())
         cols = {k: np.ascontiguousarray(image[k], dtype=np.int64) for k in names}

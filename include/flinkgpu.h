@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define FG_ABI_VERSION 15
+#define FG_ABI_VERSION 16
 
 enum fg_status {
     FG_OK = 0,
@@ -339,6 +339,22 @@ int  fg_snapshot_state(fg_handle* h, fg_state_rows* out, int64_t* timer_watermar
  * value may return the same column for cnt_star and cnt_val (they are equal). */
 int  fg_snapshot_state_async(fg_handle* h);
 int  fg_snapshot_state_wait(fg_handle* h, fg_state_rows* out, int64_t* timer_watermark);
+/* The slices of the image the last fg_snapshot_state / fg_snapshot_state_wait returned (ABI 16):
+ * the image's rows are grouped by slice, ascending; `changed` tells whether the slice's state was
+ * written since the previous image of this handle (a new slice, a flush or fold into it, a late
+ * record; every slice of a handle's first image; a table restored into an empty handle by fg_restore
+ * counts as unchanged -- the backend holds it). A shim keeps its keyed state between checkpoints and
+ * rewrites only the changed slices' entries, clearing the namespaces of slices no longer in the image
+ * (AbstractWindowAggProcessor.prepareCheckpoint :195-197 flushes only the buffer; AggCombiner.combine
+ * :76-115 touches only the (key, slice) pairs a flush saw). Valid until the next snapshot call. */
+typedef struct fg_image_slices {
+    int64_t n;
+    const int64_t* slice_end;   /* [n] */
+    const int64_t* first_row;   /* [n] the slice's rows are image rows [first_row, first_row + rows) */
+    const int64_t* rows;        /* [n] */
+    const uint8_t* changed;     /* [n] 1 / 0 */
+} fg_image_slices;
+int  fg_snapshot_slices(fg_handle* h, fg_image_slices* out);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
 int  fg_late_dropped(fg_handle* h, int64_t* out);
 int  fg_get_stats(fg_handle* h, fg_stats* out);
@@ -424,6 +440,32 @@ int  fg_comm_exchange_fired(fg_comm* c, fg_handle* local, int32_t key_hash, int3
  * the local buffer crosses the edge before the barrier). */
 int  fg_comm_exchange_flushed(fg_comm* c, fg_handle* local, int32_t key_hash, int32_t max_parallelism,
                               int64_t watermark, fg_handle* global, int64_t* min_watermark);
+/* The exchange as a round of three calls (ABI 16), for a subtask whose edge runs on a thread of its
+ * own: the operators are touched only in _begin (the local rows collected or flushed and grouped by
+ * owner) and _end (the received rows merged into `global`), never while _exchange waits for the
+ * peers. Every rank runs the same sequence of rounds: a rank with nothing to send still begins an
+ * FG_ROUND_IDLE round. The meta words of a round carry each rank's watermark and epoch (the id of
+ * the last checkpoint whose pre-barrier flush it has sent) and a failure flag: a rank whose _begin
+ * failed still takes part, sending no rows, and _exchange then fails on EVERY rank with FG_EDEVICE
+ * (fg_round.failed_rank) instead of leaving the peers blocked in the data collective. After a
+ * _begin -- whatever it returned -- the caller calls _exchange; _end after an _exchange that
+ * returned FG_OK. */
+#define FG_ROUND_FIRED 0     /* the local handle's uncollected async fires (fg_collect_fired) */
+#define FG_ROUND_FLUSHED 1   /* the local buffer (fg_flush_partials: before a checkpoint barrier) */
+#define FG_ROUND_IDLE 2      /* nothing to send (local may be NULL) */
+typedef struct fg_round {
+    int64_t min_watermark;   /* min over the ranks of the watermarks passed to _begin (StatusWatermarkValve) */
+    int64_t min_epoch;       /* min over the ranks of the epochs passed to _begin */
+    int64_t rows_sent;       /* this rank's rows (to every rank, itself included) */
+    int64_t rows_received;
+    int64_t bytes_sent;      /* to other ranks */
+    int32_t failed_rank;     /* -1, or the lowest rank whose round failed (world: column counts disagree) */
+    int32_t reserved0;
+} fg_round;
+int  fg_comm_round_begin(fg_comm* c, fg_handle* local, int32_t mode, int32_t key_hash, int32_t max_parallelism,
+                         int64_t watermark, int64_t epoch);
+int  fg_comm_round_exchange(fg_comm* c, fg_round* out);
+int  fg_comm_round_end(fg_comm* c, fg_handle* global);
 void* fg_comm_stream(fg_comm* c);
 int64_t fg_comm_bytes_sent(fg_comm* c);      /* bytes sent to other ranks by every exchange so far */
 const char* fg_comm_last_error(fg_comm* c);   /* c may be NULL: last error of fg_comm_open / _unique_id */

@@ -198,6 +198,8 @@ public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator
     private transient InternalTimerService<TimeWindow> timers;
     /** Restored window contents by window end (initializeState), until their cleanup time. */
     private transient TreeMap<Long, Restored> restored;
+    /** window ends the backend holds from the last image written (or restored) */
+    private transient Set<Long> imageWindows;
 
     /** A restored window: keys (sorted), accumulators (a0, a1), trigger pending, holding state. */
     private static final class Restored {
@@ -292,7 +294,9 @@ public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator
         vals = hasValue ? direct(8L * spec.batchRecords) : null;
         currentWatermark = Long.MIN_VALUE;
         restored = new TreeMap<>();
+        imageWindows = new HashSet<>();
         restoreImage();
+        imageWindows.addAll(restored.keySet());
     }
 
     private static ByteBuffer direct(long bytes) {
@@ -417,17 +421,13 @@ public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator
         writeImage();
     }
 
+    /**
+     * The image into "window-contents" and the timers, incrementally: a window's entries are
+     * rewritten only when one of its slices was written since the previous image
+     * (fg_snapshot_slices, ABI 16); windows no longer in the image are cleared; the others stay as
+     * an earlier barrier wrote them (round 5 cleared and rewrote the whole state every barrier).
+     */
     private void writeImage() throws Exception {
-        // the previous image goes: every (key, window) of the state is written again below
-        List<Tuple2<Long, TimeWindow>> old =
-                getKeyedStateBackend().<TimeWindow>getKeysAndNamespaces(WINDOW_STATE_NAME)
-                        .map(t -> Tuple2.of((Long) t.f0, t.f1))
-                        .collect(Collectors.toList());
-        for (Tuple2<Long, TimeWindow> kn : old) {
-            setCurrentKey(kn.f0);
-            windowState.setCurrentNamespace(kn.f1);
-            windowState.clear();
-        }
         ByteBuffer[] cols = new ByteBuffer[7];
         long[] wmOut = new long[1];
         long n = FlinkGpu.snapshotState(handle, cols, wmOut);
@@ -439,6 +439,14 @@ public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator
         long wm = currentWatermark;
         long slide = spec.windowKind == FgConfig.TUMBLE ? spec.sizeMs : spec.slideMs;
         long perSlice = spec.sizeMs / slide;
+        long[] sl = FlinkGpu.snapshotSlices(handle);
+        int nsl = (int) sl[0];
+        Set<Long> changedSlices = new HashSet<>();
+        for (int i = 0; i < nsl; i++) {
+            if (sl[1 + 3 * nsl + i] != 0) {
+                changedSlices.add(sl[1 + i]);
+            }
+        }
         // per (key, window): the restored accumulator first (value1 of the merge), then every slice
         Map<Long, Map<Long, long[]>> contents = new HashMap<>();   // window end -> key -> (a0, a1)
         for (Map.Entry<Long, Restored> e : restored.entrySet()) {
@@ -466,8 +474,30 @@ public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator
                 w.put(key, prev == null ? new long[] {a0, a1} : acc.merge(prev[0], prev[1], a0, a1));
             }
         }
+        // windows gone since the previous image: cleared (their keys from the backend)
+        for (Long end : imageWindows) {
+            if (!contents.containsKey(end)) {
+                TimeWindow window = new TimeWindow(end - spec.sizeMs, end);
+                List<Long> ks =
+                        getKeyedStateBackend().<TimeWindow>getKeys(WINDOW_STATE_NAME, window)
+                                .map(k -> (Long) k)
+                                .collect(Collectors.toList());
+                for (Long k : ks) {
+                    setCurrentKey(k);
+                    windowState.setCurrentNamespace(window);
+                    windowState.clear();
+                }
+            }
+        }
         for (Map.Entry<Long, Map<Long, long[]>> e : contents.entrySet()) {
             long end = e.getKey();
+            boolean write = !imageWindows.contains(end);
+            for (long j = 0; j < perSlice && !write; j++) {
+                write = changedSlices.contains(end - j * slide);
+            }
+            if (!write) {
+                continue;   // (as an earlier barrier wrote it: none of its slices changed since)
+            }
             TimeWindow window = new TimeWindow(end - spec.sizeMs, end);
             long cleanup = cleanupTime(end);
             for (Map.Entry<Long, long[]> kv : e.getValue().entrySet()) {
@@ -482,6 +512,7 @@ public final class GpuWindowOperator<V, ACC, OUT> extends AbstractStreamOperator
                 }
             }
         }
+        imageWindows = new HashSet<>(contents.keySet());
     }
 
     /** initializeState's image: the (key, window) accumulators and which triggers are pending. */

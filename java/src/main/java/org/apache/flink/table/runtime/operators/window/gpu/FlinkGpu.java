@@ -110,6 +110,12 @@ public final class FlinkGpu {
     /** fg_snapshot_state_wait: the image of the last snapshotStateAsync, as snapshotState. */
     public static native long snapshotStateWait(long h, ByteBuffer[] cols, long[] timerWatermark);
 
+    /**
+     * fg_snapshot_slices (ABI 16): the slices of the image the last snapshotState / snapshotStateWait
+     * returned, as [n, sliceEnd[n], firstRow[n], rows[n], changed[n] (1 / 0)].
+     */
+    public static native long[] snapshotSlices(long h);
+
     /** fg_restore. */
     public static native void restore(
             long h,
@@ -183,6 +189,29 @@ public final class FlinkGpu {
     /** fg_comm_exchange_flushed: the same for the local flush before a checkpoint barrier. */
     public static native long commExchangeFlushed(
             long comm, long local, int keyHash, int maxParallelism, long watermark, long global);
+
+    /** fg_comm_round_begin modes (FG_ROUND_*). */
+    public static final int ROUND_FIRED = 0;
+
+    public static final int ROUND_FLUSHED = 1;
+    public static final int ROUND_IDLE = 2;
+
+    /**
+     * fg_comm_round_begin (ABI 16): the local rows of the round grouped by owner (the operators are
+     * touched here and in {@link #commRoundEnd}, never while {@link #commRoundExchange} waits). A
+     * failed begin still takes part: call commRoundExchange after it whatever it threw.
+     */
+    public static native void commRoundBegin(
+            long comm, long local, int mode, int keyHash, int maxParallelism, long watermark, long epoch);
+
+    /**
+     * fg_comm_round_exchange: the round's collectives; out[0..4] = min watermark, min epoch, rows
+     * sent, rows received, bytes sent. Throws on every rank when one rank's round failed.
+     */
+    public static native void commRoundExchange(long comm, long[] out);
+
+    /** fg_comm_round_end: the received partial rows merged into the global handle. */
+    public static native void commRoundEnd(long comm, long global);
 
     /** fg_comm_bytes_sent. */
     public static native long commBytesSent(long comm);

@@ -22,7 +22,8 @@
  *                       reference's own keyed state "window-aggs" (namespace = slice end, the
  *                       accumulator row in the accSerializer layout, GpuAccRows) and the window
  *                       timers AggCombiner would hold are registered -- a savepoint the reference
- *                       processors restore, and restore from (INTEGRATION.md section 6)
+ *                       processors restore, and restore from (INTEGRATION.md section 6); only the
+ *                       slices written since the last checkpoint (fg_snapshot_slices) are rewritten
  *   fireWindow / clearWindow  no-ops: the engine fires windows; the timers registered at a
  *                       checkpoint fire into these no-ops
  *
@@ -92,6 +93,10 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
     /** an fg_snapshot_state_async not collected (a checkpoint that failed before its wait). */
     private transient boolean snapshotPending;
     private transient boolean batchHanded;
+    /** the namespaces the backend holds from the last image written (or restored), and their slices */
+    private transient Map<Long, Set<Long>> imageContrib;
+    /** the next window end the key timers of fired state were registered at */
+    private transient long lastNextEnd;
 
     public GpuSlicingWindowProcessor(GpuWindowAggSpec spec, ZoneId shiftTimeZone) {
         this.spec = spec;
@@ -145,6 +150,8 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
         windowState = new WindowValueState<>((InternalValueState<RowData, Long, RowData>) state);
         timerService = new WindowTimerServiceImpl(ctx.getTimerService(), shiftTimeZone);
         lastProcTimer = Long.MIN_VALUE;
+        imageContrib = new HashMap<>();
+        lastNextEnd = Long.MIN_VALUE;
         restoreFromKeyedState(backend);
     }
 
@@ -338,35 +345,31 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
 
     /**
      * The engine's (key, slice) accumulators into "window-aggs" as the reference keeps them, and
-     * the window timers AggCombiner / SliceSharedWindowAggProcessor would hold:
-     *  - one accumulator row per (key, slice end) in the accSerializer layout; CUMULATE slices of
-     *    windows that have fired are merged into the window's first slice, as
-     *    CumulativeSliceAssigner.mergeSlices leaves them (SliceAssigners.java:359-370);
-     *  - an event-time window timer at every unfired slice end holding state (AggCombiner.java:
-     *    104-112) and, for a key holding state of fired slices only (HOP / CUMULATE), at the next
-     *    window end after the progress (fireWindow's nextTriggerWindow registration).
-     * The image of the previous checkpoint (entries, timers) is replaced.
+     * the window timers AggCombiner / SliceSharedWindowAggProcessor would hold -- incrementally: the
+     * backend keeps what earlier checkpoints wrote, and a barrier rewrites only what changed since
+     * (the reference's prepareCheckpoint flushes its buffer into state it already keeps,
+     * AbstractWindowAggProcessor.java:195-197; AggCombiner.combine touches only the (key, slice)
+     * pairs a flush saw, AggCombiner.java:76-115). Per image slice the engine says whether its table
+     * was written since the previous image (fg_snapshot_slices, ABI 16):
+     *  - a slice's namespace is its end; a CUMULATE slice of a fired window maps to the window's first
+     *    slice, where CumulativeSliceAssigner.mergeSlices keeps the fired state (SliceAssigners.java:
+     *    359-370). A namespace is rewritten -- its accumulator rows put, its window timer registered
+     *    (AggCombiner.java:104-112; the timer service deduplicates) -- iff one of its slices changed;
+     *    a namespace whose slices are not the ones it held at the last image is rebuilt (cleared first);
+     *  - namespaces of the previous image that are gone (fired, expired) are cleared; their timers
+     *    have fired: the operator forwards a watermark only after the engine fired its windows;
+     *  - a key holding state of fired slices (HOP / CUMULATE) holds a timer at the next window end
+     *    after the progress (fireWindow's nextTriggerWindow registration): registered for the keys of
+     *    rewritten namespaces, and for every such key when that next window end moved.
+     * Round 5 cleared every entry, deleted every timer and wrote the whole image at every barrier on
+     * the task thread. Mirror: flink_amd/keyed_state.py (tests/test_gpu_incremental_state.py checks
+     * it against that full rewrite, and a failover restored from the written backend).
      */
     private void writeKeyedState() throws Exception {
         KeyedStateBackend<RowData> backend = ctx.getKeyedStateBackend();
-        InternalTimerService<Long> timers = ctx.getTimerService();
-        List<Tuple2<RowData, Long>> old = backend.<Long>getKeysAndNamespaces(STATE_NAME).collect(Collectors.toList());
-        for (Tuple2<RowData, Long> kn : old) {
-            backend.setCurrentKey(kn.f0);
-            windowState.clear(kn.f1);
-        }
-        // (forEachEventTimeTimer sets each timer's key as the current key before the action)
-        List<Tuple2<RowData, Tuple2<Long, Long>>> oldTimers = new ArrayList<>();
-        timers.forEachEventTimeTimer(
-                (w, ts) -> oldTimers.add(Tuple2.of(backend.getCurrentKey(), Tuple2.of(w, ts))));
-        for (Tuple2<RowData, Tuple2<Long, Long>> kt : oldTimers) {
-            backend.setCurrentKey(kt.f0);
-            timers.deleteEventTimeTimer(kt.f1.f0, kt.f1.f1);
-        }
-
         ByteBuffer[] cols = new ByteBuffer[7];
         long[] wm = new long[1];
-        int n = (int) FlinkGpu.snapshotStateWait(handle, cols, wm);
+        FlinkGpu.snapshotStateWait(handle, cols, wm);
         snapshotPending = false;
         for (ByteBuffer c : cols) {
             if (c != null) {
@@ -374,47 +377,111 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
             }
         }
         final long progress = wm[0];
-        RowData[] keyRows = keys.rows(cols[0], n);
-        Map<BinaryRowData, Map<Long, RowData>> image = new HashMap<>();
-        Set<BinaryRowData> needNextTimer = new HashSet<>();
-        for (int i = 0; i < n; i++) {
-            long slice = cols[1].getLong(8 * i);
-            GenericRowData acc =
-                    accRows.fromPartial(
-                            cols[2].getLong(8 * i),
-                            cols[3].getLong(8 * i),
-                            cols[4].getLong(8 * i),
-                            cols[5] == null ? cols[4].getLong(8 * i) : cols[5].getLong(8 * i),
-                            cols[6] == null ? cols[4].getLong(8 * i) : cols[6].getLong(8 * i));
-            BinaryRowData key = (BinaryRowData) keyRows[i];
-            boolean fired = isWindowFired(slice, progress, shiftTimeZone);
-            long target = slice;
-            if (fired && spec.windowKind == FgConfig.CUMULATE) {
-                target = TimeWindow.getWindowStartWithOffset(slice - 1, spec.offsetMs, spec.sizeMs) + spec.slideMs;
+        final long[] sl = FlinkGpu.snapshotSlices(handle);
+        final int ns = (int) sl[0];
+        // namespaces of the image: their slices, whether one changed
+        Map<Long, Set<Long>> contrib = new HashMap<>();
+        Map<Long, Boolean> changed = new HashMap<>();
+        long[] nsOf = new long[ns];
+        for (int i = 0; i < ns; i++) {
+            long slice = sl[1 + i];
+            nsOf[i] = namespaceOf(slice, progress);
+            contrib.computeIfAbsent(nsOf[i], k -> new HashSet<>()).add(slice);
+            changed.merge(nsOf[i], sl[1 + 3 * ns + i] != 0, Boolean::logicalOr);
+        }
+        Set<Long> rebuild = new HashSet<>();
+        for (Map.Entry<Long, Set<Long>> e : contrib.entrySet()) {
+            Set<Long> before = imageContrib.get(e.getKey());
+            if (before != null && !before.equals(e.getValue())) {
+                rebuild.add(e.getKey());
+                changed.put(e.getKey(), true);
             }
-            Map<Long, RowData> m = image.computeIfAbsent(key, k -> new HashMap<>());
-            RowData prev = m.get(target);
-            m.put(target, prev == null ? acc : accRows.merge(prev, acc));
-            if (fired) {
-                needNextTimer.add(key);
+        }
+        Set<Long> clear = new HashSet<>(rebuild);
+        for (Long n : imageContrib.keySet()) {
+            if (!contrib.containsKey(n)) {
+                clear.add(n);
+            }
+        }
+        for (Long n : clear) {   // (gone, or rebuilt: its keys from the backend)
+            List<RowData> keysOfNs = backend.<Long>getKeys(STATE_NAME, n).collect(Collectors.toList());
+            for (RowData k : keysOfNs) {
+                backend.setCurrentKey(k);
+                windowState.clear(n);
             }
         }
         long interval = windowInterval();
         long nextEnd =
                 TimeWindow.getWindowStartWithOffset(toUtcTimestampMills(progress, shiftTimeZone), spec.offsetMs, interval)
                         + interval;
-        for (Map.Entry<BinaryRowData, Map<Long, RowData>> e : image.entrySet()) {
-            backend.setCurrentKey(e.getKey());
-            for (Map.Entry<Long, RowData> s : e.getValue().entrySet()) {
-                windowState.update(s.getKey(), s.getValue());
-                if (!proctime() && !isWindowFired(s.getKey(), progress, shiftTimeZone)) {
-                    timerService.registerEventTimeWindowTimer(s.getKey());
-                }
+        boolean nextMoved = nextEnd != lastNextEnd;
+        // the rows of the slices to read: those of rewritten namespaces, and of fired slices when the
+        // next window end moved (their keys' next-window timers)
+        Map<Long, Map<BinaryRowData, RowData>> image = new HashMap<>();
+        Set<BinaryRowData> needNextTimer = new HashSet<>();
+        for (int i = 0; i < ns; i++) {
+            long slice = sl[1 + i];
+            boolean write = changed.get(nsOf[i]);
+            boolean fired = isWindowFired(slice, progress, shiftTimeZone);
+            if (!write && !(fired && nextMoved)) {
+                continue;
             }
-            if (!proctime() && needNextTimer.contains(e.getKey())) {
-                timerService.registerEventTimeWindowTimer(nextEnd);
+            int first = (int) sl[1 + ns + i], rows = (int) sl[1 + 2 * ns + i];
+            RowData[] keyRows = keys.rows(slice(cols[0], first, rows), rows);
+            for (int r = 0; r < rows; r++) {
+                BinaryRowData key = (BinaryRowData) keyRows[r];
+                if (fired && !proctime()) {
+                    needNextTimer.add(key);
+                }
+                if (!write) {
+                    continue;
+                }
+                int at = first + r;
+                GenericRowData acc =
+                        accRows.fromPartial(
+                                cols[2].getLong(8 * at),
+                                cols[3].getLong(8 * at),
+                                cols[4].getLong(8 * at),
+                                cols[5] == null ? cols[4].getLong(8 * at) : cols[5].getLong(8 * at),
+                                cols[6] == null ? cols[4].getLong(8 * at) : cols[6].getLong(8 * at));
+                Map<BinaryRowData, RowData> m = image.computeIfAbsent(nsOf[i], k -> new HashMap<>());
+                RowData prev = m.get(key);
+                m.put(key, prev == null ? acc : accRows.merge(prev, acc));
             }
         }
+        for (Map.Entry<Long, Map<BinaryRowData, RowData>> e : image.entrySet()) {
+            long n = e.getKey();
+            boolean timer = !proctime() && !isWindowFired(n, progress, shiftTimeZone);
+            for (Map.Entry<BinaryRowData, RowData> kv : e.getValue().entrySet()) {
+                backend.setCurrentKey(kv.getKey());
+                windowState.update(n, kv.getValue());
+                if (timer) {
+                    timerService.registerEventTimeWindowTimer(n);
+                }
+            }
+        }
+        for (BinaryRowData key : needNextTimer) {
+            backend.setCurrentKey(key);
+            timerService.registerEventTimeWindowTimer(nextEnd);
+        }
+        imageContrib = contrib;
+        lastNextEnd = nextEnd;
+    }
+
+    /** the namespace of a slice's state at `progress` (CUMULATE: a fired slice's window's first slice) */
+    private long namespaceOf(long slice, long progress) {
+        if (spec.windowKind == FgConfig.CUMULATE && isWindowFired(slice, progress, shiftTimeZone)) {
+            return TimeWindow.getWindowStartWithOffset(slice - 1, spec.offsetMs, spec.sizeMs) + spec.slideMs;
+        }
+        return slice;
+    }
+
+    /** rows [first, first + n) of an 8-byte image column, as a buffer of their own */
+    private static ByteBuffer slice(ByteBuffer col, int first, int n) {
+        ByteBuffer d = col.duplicate();
+        d.position(8 * first);
+        d.limit(8 * (first + n));
+        return d.slice().order(ByteOrder.nativeOrder());
     }
 
     /**
@@ -452,6 +519,11 @@ public final class GpuSlicingWindowProcessor implements SlicingWindowProcessor<L
             }
         }
         keys.internRows(rows, c[0]);
+        // the backend holds these namespaces (each its own slice: which slices folded into a restored
+        // CUMULATE namespace is not kept -- the first checkpoint rebuilds those)
+        for (Tuple2<RowData, Long> kn : entries) {
+            imageContrib.computeIfAbsent(kn.f1, k -> new HashSet<>()).add(kn.f1);
+        }
         long[] minTimer = {Long.MAX_VALUE};
         ctx.getTimerService()
                 .forEachEventTimeTimer((w, ts) -> minTimer[0] = Math.min(minTimer[0], ts));

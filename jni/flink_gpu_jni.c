@@ -24,8 +24,10 @@
  *   dict*           fg_key_dict_*        (BinaryRowDataKeySelector rows of any key type)
  *   hostRegister    fg_host_register     (page-lock a managed-memory segment at open: direct DMA)
  *   hostUnregister  fg_host_unregister   (at close)
+ *   snapshotSlices  fg_snapshot_slices   (the image's slices and which changed: the incremental keyed-state write)
  *   comm*           fg_comm_*            (the keyBy edge local -> global over RCCL: KeyGroupStreamPartitioner
- *                                         + RecordWriter + StatusWatermarkValve between co-located subtasks)
+ *                                         + RecordWriter + StatusWatermarkValve between co-located subtasks;
+ *                                         commRoundBegin / Exchange / End: a round on the subtask's edge thread)
  *
  * Buffers: every ByteBuffer argument is a DIRECT buffer (MemorySegment.wrap of an off-heap
  * segment, MemorySegment.java:288,307, or ByteBuffer.allocateDirect) in native byte order;
@@ -307,6 +309,34 @@ JNIEXPORT jlong JNICALL FN(snapshotStateWait)(JNIEnv* env, jclass cls, jlong hp,
     return s.n;
 }
 
+/* long[] snapshotSlices(long h): the slices of the image the last snapshotState / snapshotStateWait
+ * returned (fg_snapshot_slices, ABI 16) as one array: [n, slice_end[n], first_row[n], rows[n],
+ * changed[n] (1 / 0)] -- the shim rewrites only the changed slices' keyed state */
+JNIEXPORT jlongArray JNICALL FN(snapshotSlices)(JNIEnv* env, jclass cls, jlong hp) {
+    (void)cls;
+    fg_handle* h = (fg_handle*)(intptr_t)hp;
+    fg_image_slices s;
+    if (check(env, h, fg_snapshot_slices(h, &s))) return NULL;
+    const jsize n = (jsize)s.n;
+    jlongArray out = (*env)->NewLongArray(env, 1 + 4 * n);
+    if (!out) return NULL;
+    jlong* buf = (jlong*)malloc(sizeof(jlong) * (size_t)(1 + 4 * n));
+    if (!buf) {
+        throw_code(env, FG_EDEVICE, "snapshotSlices: out of host memory");
+        return NULL;
+    }
+    buf[0] = n;
+    for (jsize i = 0; i < n; i++) {
+        buf[1 + i] = s.slice_end[i];
+        buf[1 + n + i] = s.first_row[i];
+        buf[1 + 2 * n + i] = s.rows[i];
+        buf[1 + 3 * n + i] = s.changed[i] ? 1 : 0;
+    }
+    (*env)->SetLongArrayRegion(env, out, 0, 1 + 4 * n, buf);
+    free(buf);
+    return out;
+}
+
 /* void restore(long h, int n, ByteBuffer key, ByteBuffer sliceEnd, ByteBuffer cntStar, ByteBuffer cntVal,
  *              ByteBuffer sum, ByteBuffer min, ByteBuffer max, long timerWatermark) */
 JNIEXPORT void JNICALL FN(restore)(JNIEnv* env, jclass cls, jlong hp, jint n, jobject key, jobject sliceEnd,
@@ -481,6 +511,36 @@ JNIEXPORT jlong JNICALL FN(commExchangeFlushed)(JNIEnv* env, jclass cls, jlong c
                                                 (fg_handle*)(intptr_t)gp, &mw)))
         return 0;
     return mw;
+}
+
+/* void commRoundBegin(long comm, long local, int mode, int keyHash, int maxParallelism, long watermark,
+ * long epoch): fg_comm_round_begin -- the local rows collected (ROUND_FIRED) or flushed
+ * (ROUND_FLUSHED) and grouped by owner, or nothing (ROUND_IDLE, local may be 0). Whatever it throws,
+ * the caller calls commRoundExchange next (a failed begin still takes part in the round). */
+JNIEXPORT void JNICALL FN(commRoundBegin)(JNIEnv* env, jclass cls, jlong cp, jlong lp, jint mode, jint keyHash,
+                                          jint maxPar, jlong wm, jlong epoch) {
+    (void)cls;
+    fg_comm* c = (fg_comm*)(intptr_t)cp;
+    (void)ccheck(env, c, fg_comm_round_begin(c, (fg_handle*)(intptr_t)lp, mode, keyHash, maxPar, wm, epoch));
+}
+
+/* void commRoundExchange(long comm, long[] out): fg_comm_round_exchange (blocks for the peers; touches
+ * no operator); out[0..4] = min watermark, min epoch, rows sent, rows received, bytes sent */
+JNIEXPORT void JNICALL FN(commRoundExchange)(JNIEnv* env, jclass cls, jlong cp, jlongArray out) {
+    (void)cls;
+    fg_comm* c = (fg_comm*)(intptr_t)cp;
+    fg_round r;
+    memset(&r, 0, sizeof r);
+    if (ccheck(env, c, fg_comm_round_exchange(c, &r))) return;
+    jlong v[5] = {r.min_watermark, r.min_epoch, r.rows_sent, r.rows_received, r.bytes_sent};
+    (*env)->SetLongArrayRegion(env, out, 0, 5, v);
+}
+
+/* void commRoundEnd(long comm, long global): fg_comm_round_end -- the received rows merged into global */
+JNIEXPORT void JNICALL FN(commRoundEnd)(JNIEnv* env, jclass cls, jlong cp, jlong gp) {
+    (void)cls;
+    fg_comm* c = (fg_comm*)(intptr_t)cp;
+    (void)ccheck(env, c, fg_comm_round_end(c, (fg_handle*)(intptr_t)gp));
 }
 
 /* long commBytesSent(long comm) */

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = L.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.fg_abi_version() == 15
+    assert lib.fg_abi_version() == 16
 
 
 def test_struct_layouts_match_header_sizes(tmp_path):
@@ -37,7 +37,8 @@ def test_struct_layouts_match_header_sizes(tmp_path):
     import subprocess
     structs = {"fg_config": L.FgConfig, "fg_batch": L.FgBatch, "fg_rows": L.FgRows, "fg_partials": L.FgPartials,
                "fg_state_rows": L.FgStateRows, "fg_row_batch": L.FgRowBatch, "fg_kernel_stat": L.FgKernelStat,
-               "fg_stats": L.FgStats, "fg_exchanged": L.FgExchanged}
+               "fg_stats": L.FgStats, "fg_exchanged": L.FgExchanged, "fg_round": L.FgRound,
+               "fg_image_slices": L.FgImageSlices}
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "flinkgpu.h"', "int main(void) {"]
     for cname, py in structs.items():
         src.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
