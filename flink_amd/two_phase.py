@@ -68,7 +68,6 @@ class GpuPair:
         import torch
         self.local, self.glob = local, glob
         self.device = device if device is not None else torch.device("cuda", 0)
-        self.rows = []   # the global operator's fired rows, drained by the task thread
 
     def local_batch(self, key, ts, val):
         self.local.process_batch(key, ts, val)
@@ -354,10 +353,8 @@ def union_image_for(images, key_group_range, max_parallelism=128, key_groups=Non
     hash of BIGINT keys)."""
     cat = {c: np.concatenate([np.asarray(im[c]) for im, _ in images]) for c in images[0][0]}
     if key_groups is None:
-        import torch
-
         from .window_agg import key_groups as kg_dev
-        kg = kg_dev(torch.from_numpy(cat["key"]).cuda(), max_parallelism).cpu().numpy()
+        kg = kg_dev(cat["key"], max_parallelism)
     else:
         kg = key_groups(cat["key"])
     lo, hi = key_group_range

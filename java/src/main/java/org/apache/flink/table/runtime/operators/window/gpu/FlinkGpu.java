@@ -170,6 +170,9 @@ public final class FlinkGpu {
 
     // ---- the keyBy edge local -> global over RCCL (fg_comm; INTEGRATION.md section 7) ----
 
+    /** fg_key_hash: a BIGINT key hashed as its BinaryRowData key row (FG_KEYHASH_BINARYROW_BIGINT). */
+    public static final int KEYHASH_BINARYROW_BIGINT = 0;
+
     /** Bytes of a communicator id (FG_COMM_ID_BYTES). */
     public static final int COMM_ID_BYTES = 128;
 

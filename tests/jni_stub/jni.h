@@ -41,6 +41,7 @@ struct JNINativeInterface_ {
     jobject (*NewDirectByteBuffer)(JNIEnv* env, void* address, jlong capacity);
     void* (*GetDirectBufferAddress)(JNIEnv* env, jobject buf);
     jlong (*GetDirectBufferCapacity)(JNIEnv* env, jobject buf);
+    jlongArray (*NewLongArray)(JNIEnv* env, jsize len);
 };
 
 #endif

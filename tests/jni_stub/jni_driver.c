@@ -94,9 +94,17 @@ static jlong f_direct_cap(JNIEnv* env, jobject b) {
     return b && b->kind == K_DIRECT ? b->cap : -1;
 }
 
+static jlongArray f_new_longs(JNIEnv* env, jsize len) {
+    (void)env;
+    jobject o = mk(K_LONGARR);
+    o->len = len;
+    o->longs = (jlong*)calloc((size_t)(len > 0 ? len : 1), sizeof(jlong));
+    return o;
+}
+
 static const struct JNINativeInterface_ table = {
     f_find_class,  f_throw_new,     f_exception_check, f_array_length, f_set_obj, f_get_longs,
-    f_release_longs, f_set_long_region, f_new_direct, f_direct_addr,   f_direct_cap,
+    f_release_longs, f_set_long_region, f_new_direct, f_direct_addr,   f_direct_cap, f_new_longs,
 };
 static JNIEnv envp = &table;
 static JNIEnv* env = &envp;
@@ -118,6 +126,10 @@ jlong FN(commOpen)(JNIEnv*, jclass, jint, jint, jint, jobject);
 jlong FN(commExchangeFired)(JNIEnv*, jclass, jlong, jlong, jint, jint, jlong, jlong);
 jlong FN(commBytesSent)(JNIEnv*, jclass, jlong);
 void FN(commClose)(JNIEnv*, jclass, jlong);
+jlongArray FN(snapshotSlices)(JNIEnv*, jclass, jlong);
+void FN(commRoundBegin)(JNIEnv*, jclass, jlong, jlong, jint, jint, jint, jlong, jlong);
+void FN(commRoundExchange)(JNIEnv*, jclass, jlong, jlongArray);
+void FN(commRoundEnd)(JNIEnv*, jclass, jlong, jlong);
 
 static jobject direct(void* p, jlong cap) { return f_new_direct(env, p, cap); }
 static jobject objarr(jsize n) {
@@ -259,6 +271,17 @@ static int gpu_mode(void) {
         long long t = 0;
         for (jlong i = 0; i < sn; i++) t += cs[i];
         printf("snapshot entries %lld cnt_star %lld wm %lld\n", (long long)sn, t, (long long)swm->longs[0]);
+        /* the image's slices: [n, ends, first rows, rows, changed] */
+        jlongArray sl = FN(snapshotSlices)(env, NULL, h);
+        const jlong* v = sl->longs;
+        const jlong ns = v[0];
+        long long rows = 0, changed = 0;
+        for (jlong i = 0; i < ns; i++) {
+            rows += v[1 + 2 * ns + i];
+            changed += v[1 + 3 * ns + i];
+        }
+        printf("slices %lld first_end %lld rows %lld changed %lld\n", (long long)ns, (long long)(ns ? v[1] : 0), rows,
+               changed);
     }
     printf("late %lld\n", (long long)FN(lateDropped)(env, NULL, h));
     FN(close)(env, NULL, h);
@@ -300,6 +323,23 @@ static int gpu_mode(void) {
         printf("comm_wm %lld sent %lld\n", (long long)mw, (long long)FN(commBytesSent)(env, NULL, comm));
         n = FN(advanceProgress)(env, NULL, glob, mw, cols);
         totals("comm", cols, n, 3);
+        /* the same edge as a round (commRoundBegin / Exchange / End: the fused operator's edge
+         * thread): the records of the windows ending 4000 .. 5000 at the final watermark */
+        FN(advanceProgressAsync)(env, NULL, loc, 10000);
+        FN(commRoundBegin)(env, NULL, comm, loc, 0 /* ROUND_FIRED */, FG_KEYHASH_BINARYROW_BIGINT, 128, 10000, 7);
+        jlongArray ro = longarr(5);
+        FN(commRoundExchange)(env, NULL, comm, ro);
+        FN(commRoundEnd)(env, NULL, comm, glob);
+        printf("round_wm %lld epoch %lld sent %lld received %lld\n", (long long)ro->longs[0], (long long)ro->longs[1],
+               (long long)ro->longs[2], (long long)ro->longs[3]);
+        n = FN(advanceProgress)(env, NULL, glob, ro->longs[0], cols);
+        totals("round", cols, n, 3);
+        /* an idle round (nothing to send; local may be 0) */
+        FN(commRoundBegin)(env, NULL, comm, 0, 2 /* ROUND_IDLE */, FG_KEYHASH_BINARYROW_BIGINT, 128, 10001, 8);
+        FN(commRoundExchange)(env, NULL, comm, ro);
+        FN(commRoundEnd)(env, NULL, comm, glob);
+        printf("idle_wm %lld epoch %lld received %lld\n", (long long)ro->longs[0], (long long)ro->longs[1],
+               (long long)ro->longs[3]);
         FN(close)(env, NULL, loc);
         FN(close)(env, NULL, glob);
         FN(commClose)(env, NULL, comm);

@@ -227,3 +227,74 @@ def test_capi_comm_world1_two_phase(oracle_mod):
     ok = e["sum_null"] == 0
     a, bb = g["sum"][ok], e["sum_d"][ok]
     assert (np.abs(a - bb) <= 1e-9 * np.maximum(np.abs(a), np.abs(bb))).all()
+
+
+def _rounds_child(q):
+    """the fused subtask (flink_amd.two_phase) over the C-ABI's RCCL rounds at world size 1
+    (fg_comm_round_begin / _exchange / _end on the edge thread), with a checkpoint aligned through
+    the rounds' epoch"""
+    try:
+        import torch
+
+        import flink_amd as F
+        from flink_amd.comm import Communicator, unique_id
+        from flink_amd.two_phase import CapiRounds, GpuPair, TwoPhaseSubtask
+        from tests.streams import make_stream
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        comm = Communicator(0, 1, 0, unique_id())
+        key, ts, val, _ = make_stream(N, KEYS, "f64", seed=79, jitter_ms=300)
+        aggs = ("count_star", "count", "sum", "avg")
+        w = F.tumbling(1000)
+        local = F.WindowAggOperator(w, aggs=aggs, expected_keys=KEYS, local_partials=True)
+        glob = F.WindowAggOperator(w, aggs=aggs, expected_keys=KEYS)
+        sub = TwoPhaseSubtask(GpuPair(local, glob, dev), CapiRounds(comm), device=dev)
+        mx, img = -(1 << 63), None
+        for bi, lo in enumerate(range(0, N, BATCH)):
+            hi = lo + BATCH
+            sub.process_batch(torch.from_numpy(key[lo:hi]).to(dev), torch.from_numpy(ts[lo:hi]).to(dev),
+                              torch.from_numpy(val[lo:hi]).to(dev))
+            mx = max(mx, int(ts[lo:hi].max()))
+            sub.process_watermark(mx - 401)
+            sub.drain()
+            if bi == 1:
+                img, _ = sub.prepare_snapshot_pre_barrier(1)
+        sub.end_input()
+        rows = np.concatenate([r for k, r in sub.output if k == "rows"])
+        assert img is not None and len(img["key"]) > 0 and sub.rounds_run > 2
+        local.close()
+        glob.close()
+        comm.close()
+        q.put((rows.tobytes(), rows.dtype.descr, None))
+    except Exception as e:
+        import traceback
+        q.put((None, None, traceback.format_exc() + repr(e)))
+
+
+def test_capi_rounds_world1_fused_subtask(oracle_mod):
+    """the fused two-phase subtask's edge thread over fg_comm_round_* (ABI 16) at world size 1:
+    its rows equal the single-phase operator's (no late record: jitter < delay)"""
+    import torch.multiprocessing as mp
+
+    from tests.streams import make_stream
+    O = oracle_mod
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rounds_child, args=(q,))
+    p.start()
+    b, descr, err = q.get(timeout=240)
+    p.join(timeout=60)
+    assert err is None, err
+    got = np.frombuffer(b, dtype=np.dtype([tuple(x) for x in descr]))
+    key, ts, val, _ = make_stream(N, KEYS, "f64", seed=79, jitter_ms=300)
+    op = O.OracleOperator(kind=O.TUMBLE, size=1000, val_type=O.VAL_F64)
+    op.process_batch(key, ts, val)
+    op.process_watermark((1 << 63) - 1)
+    e = op.take_rows()
+    assert op.late_dropped == 0
+    op.close()
+    g = got[np.lexsort((got["key"], got["window_end"]))]
+    e = e[np.lexsort((e["key"], e["window_end"]))]
+    assert len(g) == len(e), (len(g), len(e))
+    for f, fe in (("key", "key"), ("window_end", "window_end"), ("count_star", "cnt_star"), ("count", "cnt_val")):
+        assert np.array_equal(g[f], e[fe]), f

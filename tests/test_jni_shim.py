@@ -140,7 +140,11 @@ def test_jni_glue_on_gpu_host_columns(tmp_path):
         return (len(pairs), int(sel.sum()), float(val[sel].sum()), sum(k for k, _ in pairs), sum(w for _, w in pairs))
 
     assert out["comm_wm"] == ["2999", "sent", "0"]   # (world size 1: nothing leaves the rank)
-    for tag, sel in (("async", rt < 3000), ("sync", rt >= 3000), ("comm", rt < 3000)):
+    # the round form (ABI 16): watermark and epoch in-band, the rest of the windows merged into the global
+    r = out["round_wm"]
+    assert (r[0], r[2]) == ("10000", "7") and int(r[4]) == int(r[6]) > 0, r
+    assert out["idle_wm"] == ["10001", "epoch", "8", "received", "0"], out["idle_wm"]
+    for tag, sel in (("async", rt < 3000), ("sync", rt >= 3000), ("comm", rt < 3000), ("round", rt >= 3000)):
         f = out[tag]
         got = (int(f[1]), int(f[3]), float(f[5]), int(f[7]), int(f[9]))
         assert got == expect(sel), (tag, got, expect(sel))
@@ -149,5 +153,28 @@ def test_jni_glue_on_gpu_host_columns(tmp_path):
     # the image holds the state as of the async call -- the 400 records (10 keys x 2 windows) of the
     # windows ending 4000 and 5000 -- and that call's timer watermark
     assert out["snapshot"] == ["entries", "20", "cnt_star", "400", "wm", "2999"], out["snapshot"]
+    # its slices (fg_snapshot_slices): the two open windows' slices, 10 keys each, both new (changed)
+    assert out["slices"] == ["2", "first_end", "4000", "rows", "20", "changed", "2"], out["slices"]
     f = out["partials"]
     assert (int(f[1]), int(f[3]), int(f[5]), float(f[7])) == (50, 1000, 1000, float(val.sum()))
+
+
+def test_fused_two_phase_operator_drives_the_rccl_edge():
+    """The fused two-phase operator (GpuTwoPhaseWindowAggOperator) runs the keyBy edge over RCCL on
+    the Flink path: it opens the communicator from the id its coordinator distributes and exchanges
+    in rounds on its edge thread (ABI 16) -- the natives a Java operator must call for the edge to
+    carry a job's partial rows instead of Netty. The incremental checkpoint reads the image's slices."""
+    def calls(name):
+        return set(re.findall(r"FlinkGpu\.(\w+)\(", open(os.path.join(JAVA, name)).read()))
+    fused = calls("GpuTwoPhaseWindowAggOperator.java")
+    for n in ("commUniqueId", "commOpen", "commRoundBegin", "commRoundExchange", "commRoundEnd", "commClose",
+              "advanceProgressAsync", "collectFired", "snapshotStateAsync", "snapshotStateWait", "restore"):
+        assert n in fused, n
+    coord = open(os.path.join(JAVA, "GpuCommCoordinator.java")).read()
+    assert "handleEventFromOperator" in coord and "failJob" in coord and "sendEvent" in coord
+    fac = open(os.path.join(JAVA, "GpuTwoPhaseWindowAggOperatorFactory.java")).read()
+    assert "CoordinatedOperatorFactory" in fac and "GpuCommCoordinator.Provider" in fac
+    assert "snapshotSlices" in calls("GpuSlicingWindowProcessor.java")
+    assert "snapshotSlices" in set(re.findall(r"FlinkGpu\.(\w+)\(", open(os.path.join(
+        ROOT, "java", "src", "main", "java", "org", "apache", "flink", "streaming", "runtime", "operators",
+        "windowing", "gpu", "GpuWindowOperator.java")).read()))
