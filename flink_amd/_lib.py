@@ -118,7 +118,7 @@ EXPORTS = (
     "fg_open", "fg_add_batch", "fg_add_rows", "fg_add_partials", "fg_advance_progress", "fg_advance_progress_async",
     "fg_advance_progress_async_n",
     "fg_collect_fired", "fg_collect_fired_to", "fg_flush", "fg_flush_partials", "fg_snapshot_state",
-    "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_snapshot_slices", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
+    "fg_snapshot_state_async", "fg_snapshot_state_wait", "fg_snapshot_slices", "fg_selftest", "fg_restore", "fg_late_dropped", "fg_get_stats", "fg_synchronize", "fg_reset", "fg_kernel_stats", "fg_set_kernel_timing",
     "fg_stream",
     "fg_last_error", "fg_close", "fg_key_groups", "fg_partition_by_owner", "fg_partition_columns_by_owner",
     "fg_abi_version", "fg_key_dict_open", "fg_key_dict_intern", "fg_key_dict_intern_async",
@@ -230,6 +230,8 @@ def load():
     L.fg_comm_round_exchange.argtypes = [P, C.POINTER(FgRound)]
     L.fg_comm_round_end.argtypes = [P, P]
     L.fg_snapshot_slices.argtypes = [P, C.POINTER(FgImageSlices)]
+    L.fg_selftest.argtypes = [C.c_int32, C.c_char_p, C.c_int32]
+    L.fg_selftest.restype = C.c_int
     L.fg_comm_bytes_sent.argtypes = [P]
     L.fg_comm_bytes_sent.restype = C.c_int64
     L.fg_comm_stream.argtypes = [P]

@@ -25,6 +25,7 @@
 #include <csignal>
 #include <execinfo.h>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <string>
 #include <set>
@@ -304,12 +305,6 @@ struct fg_handle {
     // stream after the export kernels (event ev_snap), collected by fg_snapshot_state_wait
     hipStream_t snap_stream = nullptr;
     hipEvent_t ev_snap = nullptr;
-    unsigned snap_host_flags = hipHostMallocDefault;   // FG_SNAP_HOST_FLAGS (A/B)
-    hipMemcpyKind snap_copy_kind = hipMemcpyDeviceToHost;   // FG_SNAP_COPY_KIND (A/B: 1024 = no CUs)
-    // FG_SNAP_CUS: CUs the snapshot copy's stream may use (0: all, the default). Masked to 8-64 CUs
-    // the concurrent kernels keep their speed but the copy crawls: configs[4] 35.3 vs 24.9 ms per
-    // step (profiles/r05/zipf_ab/snap_cus)
-    int snap_cus = 0;
     bool snap_pending = false;
     bool snap_cv_alias = false;   // the pending image's cnt_val column is its cnt_star column
     int64_t snap_total = 0, snap_wm = 0;
@@ -326,7 +321,6 @@ struct fg_handle {
     // tile staging (FG_TILE=0 turns it off, A/B): in-order TUMBLE and local-phase batches of 32-bit
     // keys stay in their pass-1 tiles until the fire; off for good once a wider key is seen
     bool tile_ok = true;
-    bool tile_env = true;     // FG_TILE (fg_reset restores tile_ok from it)
     // FG_TILE_STATE: tile passes of HOP / CUMULATE (and TUMBLE lanes with resident state) flush
     // into their slice tables straight from the tiles (k_tile_fire with tables); 0: TUMBLE and
     // local fires only, anything else materialized (the round-4 first tile build)
@@ -341,8 +335,9 @@ struct fg_handle {
     // FG_TILE_HOT=1: the split fire's wave pre-combine of a hot key. Off by default: configs[4]
     // A/B (profiles/r05/zipf_ab): split fire 1.485 vs 1.072 ms per 100M-record window with it on --
     // the ballot + butterflies cost more than the same-slot LDS atomics they save
-    bool tile_hot = false;     // FG_TILE_CHUNK: a skewed bucket's chunk records (0: k_tile_plan's default)
-    bool narrow_tables = true;   // FG_NARROW_TABLES: tables written by the tile fire take 16-B entries
+    bool tile_hot = false;
+    // tables written by the tile fire take 16-B entries (round 5: CUMULATE 62.7 -> 59.0 ms per 1B)
+    bool narrow_tables = true;
     DevBuf tile_dir, tile_hist;
     DevBuf sp_items, sp_n, sp_split, sp_parts, sp_pkey, sp_pcs, sp_pv, sp_bfail, sp_icnt;   // split plans + partials
     // skewed-region plan and chunk partial tables
@@ -445,8 +440,6 @@ struct fg_handle {
     // the compact merge may key its LDS table by the int32 key of a resident entry's mix
     bool keys32 = true;
     bool skew_seen = false;     // some ingest pass saw hot-key skew (pass-2 units of one workgroup)
-    int32_t p2_skew_group = 0;  // FG_P2_SKEW_GROUP=k: pass-2 units of k pass-1 workgroups for skewed
-                                // streams (A/B on Zipf: k = 1 19.3, 2 12.6, default 10.9 ms per step)
     bool timing = false;
     uint32_t timing_mask = ~0u;   // kernel classes bracketed with events (fg_set_kernel_timing)
     KStat kstat[K_NCLASS];
@@ -1804,9 +1797,8 @@ int fire_one(fg_handle* h, int64_t wend, const std::vector<SliceTable*>& srcs, S
 #endif
         // the compact merge (two workgroups per CU, 20-B LDS slots) when the window is plain
         // resident state: source tables without NULL counts or marks, nothing written back, one
-        // value accumulator, COUNT(*)s below 2^32 (FG_COMPACT_FIRE=0: the wide merge, A/B)
-        static const bool compact_fire = !getenv("FG_COMPACT_FIRE") || std::atoi(getenv("FG_COMPACT_FIRE")) != 0;
-        p.compact = compact_fire && !h->mv && !dst && p.n_batches == 0 && p.src_null_mask == 0 && !p.mark_mask &&
+        // value accumulator, COUNT(*)s below 2^32
+        p.compact = !h->mv && !dst && p.n_batches == 0 && p.src_null_mask == 0 && !p.mark_mask &&
                             !p.markonly_mask && !p.emit_marked && p.dst_mode == 0 && p.n_src <= 64 &&
                             ub_cnt_fits(h)
                         ? 1
@@ -2444,7 +2436,7 @@ int ingest_launch(fg_handle* h, int64_t n, const int64_t* key, const int64_t* ts
     if (!p.narrow) h->keys32 = false;
     // a stream seen skewed (hot keys) partitions in pass-2 units of one pass-1 workgroup: the
     // hot key's coarse bucket is then spread over as many units as there are workgroups
-    p.p2_group = h->skew_seen ? h->p2_skew_group : 0;
+    p.p2_group = 0;
     if (tiles) {
         {
             KTimer kt(h, K_TILE1, n);
@@ -3243,6 +3235,25 @@ extern "C" {
 
 int fg_abi_version(void) { return FG_ABI_VERSION; }
 
+int fg_selftest(int32_t device_id, char* msg, int32_t cap) {
+    static std::mutex mu;
+    static std::map<int, std::pair<int, std::string>> done;   // device -> (result, message)
+    std::lock_guard<std::mutex> g(mu);
+    auto it = done.find(device_id);
+    if (it == done.end()) {
+        char m[160] = "";
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || device_id < 0 || device_id >= ndev) {
+            if (msg && cap > 0) snprintf(msg, (size_t)cap, "no such HIP device");
+            return FG_EDEVICE;
+        }
+        const int r = run_selftest(device_id, m, sizeof m);
+        it = done.emplace(device_id, std::make_pair(r, std::string(m))).first;
+    }
+    if (msg && cap > 0) snprintf(msg, (size_t)cap, "%s", it->second.second.c_str());
+    return it->second.first == 0 ? FG_OK : FG_EDEVICE;
+}
+
 // Page-locking caller memory (the shim's off-heap MemorySegments): an FG_HOST batch read from
 // a registered range is DMA'd straight from it by hipMemcpyAsync; pageable memory is first
 // staged through the runtime's bounce buffers, chunk by chunk, at about half the link rate.
@@ -3407,6 +3418,14 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         g_open_error = "device_id out of range";
         return FG_EINVAL;
     }
+    {   // the device self-check, once per process and device: a build whose scans or tile walk came
+        // out wrong (a compiler fold) fails here instead of firing wrong rows
+        char m[160];
+        if (fg_selftest(cfg->device_id, m, sizeof m) != FG_OK) {
+            g_open_error = m;
+            return FG_EDEVICE;
+        }
+    }
     std::unique_ptr<fg_handle> h(new fg_handle());
     h->cfg = c;
     h->kvt = c.val_type;   // kernel value op: val_type | op << 2 (op 1 MIN, 2 MAX; fg_kernels.hip lds_add)
@@ -3556,22 +3575,14 @@ int fg_open(const fg_config* cfg, fg_handle** out) {
         return FG_EDEVICE;
     }
     if (const char* e = getenv("FG_SPECULATE")) hp->speculate = std::atoi(e) != 0;
-    // narrow 12-B staging for the two-pass partition of a one-value operator (FG_NARROW=0: off, A/B)
+    // narrow 12-B staging for the two-pass partition of a one-value operator
     hp->narrow = hp->st_stride == 2 && !hp->mv && hp->region_bits >= kFineBits;
-    if (const char* e = getenv("FG_NARROW")) hp->narrow = hp->narrow && std::atoi(e) != 0;
-    if (const char* e = getenv("FG_P2_SKEW_GROUP")) hp->p2_skew_group = std::max(0, std::atoi(e));
     hp->narrow_ok = hp->narrow;
-    if (const char* e = getenv("FG_TILE")) hp->tile_env = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_STATE")) hp->tile_state = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_GRID")) hp->tile_grid_force = std::atoi(e);
     if (const char* e = getenv("FG_TILE_SPLIT")) hp->tile_split = std::atoi(e) != 0;
-    if (const char* e = getenv("FG_NARROW_TABLES")) hp->narrow_tables = std::atoi(e) != 0;
     if (const char* e = getenv("FG_TILE_HOT")) hp->tile_hot = std::atoi(e) != 0;
-    if (const char* e = getenv("FG_SNAP_HOST_FLAGS")) hp->snap_host_flags = (unsigned)std::strtoul(e, nullptr, 0);
-    if (const char* e = getenv("FG_SNAP_CUS")) hp->snap_cus = std::max(0, std::atoi(e));
-    if (const char* e = getenv("FG_SNAP_COPY_KIND")) hp->snap_copy_kind = (hipMemcpyKind)std::atoi(e);
-    if (const char* e = getenv("FG_TILE_CHUNK")) hp->tile_chunk = (uint32_t)std::max(0, std::atoi(e));
-    hp->tile_ok = hp->tile_env;
+    hp->tile_ok = true;
     if (hipEventCreateWithFlags(&hp->ev_pending, hipEventDisableTiming) != hipSuccess) {
         g_open_error = "hipEventCreate failed";
         return FG_EDEVICE;
@@ -4215,40 +4226,27 @@ static int snapshot_begin(fg_handle* h) {
         }
         ti++;
     }
-    HIPCHK(h, h->hs_key.ensure(b8, h->snap_host_flags));
-    HIPCHK(h, h->hs_slice.ensure(b8, h->snap_host_flags));
-    HIPCHK(h, h->hs_cs.ensure(b8, h->snap_host_flags));
-    HIPCHK(h, h->hs_cv.ensure(b8, h->snap_host_flags));
-    HIPCHK(h, h->hs_sum.ensure(b8, h->snap_host_flags));
+    HIPCHK(h, h->hs_key.ensure(b8));
+    HIPCHK(h, h->hs_slice.ensure(b8));
+    HIPCHK(h, h->hs_cs.ensure(b8));
+    HIPCHK(h, h->hs_cv.ensure(b8));
+    HIPCHK(h, h->hs_sum.ensure(b8));
     if (h->mv) {
-        HIPCHK(h, h->hs_v1.ensure(b8, h->snap_host_flags));
-        HIPCHK(h, h->hs_v2.ensure(b8, h->snap_host_flags));
+        HIPCHK(h, h->hs_v1.ensure(b8));
+        HIPCHK(h, h->hs_v2.ensure(b8));
     }
     if (total > 0) {
         if (!h->snap_stream) {
-            // the runtime copies device -> host with blit kernels, which slow a concurrent fire or
-            // pass 1 4-10x; a CU mask (FG_SNAP_CUS, spread over the XCDs) keeps the kernels' speed
-            // but slows the copy more than it saves (A/B above), so the default leaves it unmasked
-            bool masked = false;
-            if (h->snap_cus > 0) {
-                int ncu = 0;
-                if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) == hipSuccess &&
-                    ncu > h->snap_cus) {
-                    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-                    for (int i = 0; i < h->snap_cus; i++) {
-                        const int cu = (int)((int64_t)i * ncu / h->snap_cus);
-                        mask[(size_t)cu / 32] |= 1u << (cu % 32);
-                    }
-                    masked = hipExtStreamCreateWithCUMask(&h->snap_stream, (uint32_t)mask.size(), mask.data()) == hipSuccess;
-                }
-            }
-            if (!masked) HIPCHK(h, hipStreamCreateWithFlags(&h->snap_stream, hipStreamNonBlocking));
+            // (the runtime copies device -> host with blit kernels that share the CUs with a
+            // concurrent fire or pass 1; restricting the copy's stream to 8-64 CUs kept the kernels'
+            // speed but slowed the copy more than it saved, round 5: profiles/r05/zipf_ab/snap_cus)
+            HIPCHK(h, hipStreamCreateWithFlags(&h->snap_stream, hipStreamNonBlocking));
             HIPCHK(h, hipEventCreateWithFlags(&h->ev_snap, hipEventDisableTiming));
         }
         HIPCHK(h, hipEventRecord(h->ev_snap, h->stream));   // (after the export kernels)
         HIPCHK(h, hipStreamWaitEvent(h->snap_stream, h->ev_snap, 0));
         hipStream_t cs = h->snap_stream;
-        const hipMemcpyKind kd = h->snap_copy_kind;
+        const hipMemcpyKind kd = hipMemcpyDeviceToHost;
         if (h->mv) {
             HIPCHK(h, hipMemcpyAsync(h->hs_v1.p, h->s_v1.p, 8 * total, kd, cs));
             HIPCHK(h, hipMemcpyAsync(h->hs_v2.p, h->s_v2.p, 8 * total, kd, cs));
@@ -4540,7 +4538,7 @@ int fg_reset(fg_handle* h) {
     h->late_rows = 0;
     h->late_horizon = JMIN;
     h->narrow = h->narrow_ok;
-    h->tile_ok = h->tile_env;
+    h->tile_ok = true;
     return FG_OK;
 }
 

@@ -521,6 +521,8 @@ hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s);
 hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
                             const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot, hipStream_t s);
 hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s);
+// the device self-check of the DPP scans and the tile walk (fg_selftest): 0 when they are right
+int run_selftest(int device, char* msg, size_t cap);
 // a split fire: the plan (one workgroup), then launch_tile_fire over its items and again with
 // merge = 1 over the split buckets
 hipError_t launch_tile_plan(const TileFire& f, hipStream_t s);

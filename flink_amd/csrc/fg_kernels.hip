@@ -19,6 +19,10 @@
 // (ds_cmpst_rtn_b64 / ds_add_u64 / ds_add_f64), never as global atomics.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
 #include <type_traits>
 
 #include "fg_kernels.h"
@@ -3487,6 +3491,149 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
     }
     w.b += kTileWin;
     return !done;
+}
+
+// ---- device self-check (fg_selftest): the DPP wave scans and the tile walk as compiled here -----
+// Round 5 found the compiler folding the walk's DPP scan into a wrong subtract chain;
+// these kernels run the SAME inline functions the fire runs, on inputs whose answer the host knows.
+__global__ __launch_bounds__(256) void k_selftest_scan(const uint32_t* in, uint32_t* out) {
+    const uint32_t v = in[threadIdx.x];
+    const uint32_t a = wave_incl_scan<false>(v);
+    const uint32_t m = wave_incl_scan<true>(v & 255u);
+    out[3 * threadIdx.x] = a;
+    out[3 * threadIdx.x + 1] = m;
+    out[3 * threadIdx.x + 2] = wave_shr1(m);
+}
+// one wave per bucket column: the walk's records in walk order (the key of record i is i)
+__global__ __launch_bounds__(64) void k_selftest_walk(TilePass tp, uint32_t cap, uint32_t* out, uint32_t* n_out,
+                                                      unsigned int* bad) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_fm[kTileWin];
+    __shared__ uint32_t s_dl[kTileGroup];
+    const int lane = threadIdx.x;
+    const int32_t cb = blockIdx.x;
+    TileWalk w;
+    tile_walk_begin(w, tp, cb, 0, 1, lane, 0, tp.nt);
+    int32_t kr[kTileRpl];
+    int64_t vr[kTileRpl];
+    uint32_t nrec = 0, pos = 0;
+    while (tile_walk_next(w, s_fm, s_dl, lane, kr, vr, nrec)) {
+#pragma unroll
+        for (int u = 0; u < kTileRpl; u++) {
+            const uint32_t jr = lane + 64 * u;
+            if (jr < nrec && pos + jr < cap) out[(uint64_t)cb * cap + pos + jr] = (uint32_t)kr[u];
+        }
+        pos += nrec;
+    }
+    if (lane == 0) n_out[cb] = pos;
+    if (__ballot(w.bad) != 0 && lane == 0) atomicOr(bad, 1u);
+}
+__global__ void k_selftest_fill(uint32_t* rec, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        rec[3 * i] = (uint32_t)i;   // (value lo = hi = the index's low word: only the key is checked)
+        rec[3 * i + 1] = 0u;
+        rec[3 * i + 2] = (uint32_t)i;
+    }
+}
+
+int run_selftest(int device, char* msg, size_t cap_msg) {
+    auto say = [&](const char* m) {
+        if (msg && cap_msg) snprintf(msg, cap_msg, "%s", m);
+    };
+    if (hipSetDevice(device) != hipSuccess) {
+        say("hipSetDevice failed");
+        return 1;
+    }
+    uint64_t x = 0x5EEDF11Cull;
+    auto rnd = [&]() {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        return (uint32_t)(x >> 33);
+    };
+    // 1. the scans over 4 waves of random values
+    std::vector<uint32_t> in(256), got(3 * 256);
+    for (auto& v : in) v = rnd() & 1023u;
+    // 2. a tile pass of NT tiles, NB buckets; fragment lengths 0..20 (a fifth empty), offsets packed
+    constexpr int NT = 300, NB = 3;
+    std::vector<uint32_t> dt((size_t)NB * NT);
+    std::vector<std::vector<uint32_t>> want(NB);
+    for (int t = 0; t < NT; t++) {
+        uint32_t off = rnd() % 64;
+        for (int b = 0; b < NB; b++) {
+            const uint32_t len = rnd() % 5 == 0 ? 0 : rnd() % 21;
+            dt[(size_t)b * NT + t] = off | len << 16;
+            for (uint32_t i = 0; i < len; i++) want[b].push_back((uint32_t)t * (uint32_t)kTileRecs + off + i);
+            off += len;
+        }
+    }
+    const uint64_t nrec = (uint64_t)NT * kTileRecs;
+    uint32_t cap = 0;
+    for (auto& v : want) cap = std::max<uint32_t>(cap, (uint32_t)v.size());
+    void *d_in = nullptr, *d_out = nullptr, *d_rec = nullptr, *d_dt = nullptr, *d_w = nullptr, *d_n = nullptr,
+         *d_bad = nullptr;
+    int rc = 0;
+    const char* what = nullptr;
+    auto cleanup = [&]() {
+        for (void* q : {d_in, d_out, d_rec, d_dt, d_w, d_n, d_bad})
+            if (q) (void)hipFree(q);
+    };
+    if (hipMalloc(&d_in, 4 * 256) != hipSuccess || hipMalloc(&d_out, 4 * 3 * 256) != hipSuccess ||
+        hipMalloc(&d_rec, 12 * nrec) != hipSuccess || hipMalloc(&d_dt, 4 * dt.size()) != hipSuccess ||
+        hipMalloc(&d_w, 4 * (size_t)NB * cap + 4) != hipSuccess || hipMalloc(&d_n, 4 * NB) != hipSuccess ||
+        hipMalloc(&d_bad, 4) != hipSuccess) {
+        cleanup();
+        say("self-check: device allocation failed");
+        return 1;
+    }
+    (void)hipMemcpy(d_in, in.data(), 4 * 256, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_dt, dt.data(), 4 * dt.size(), hipMemcpyHostToDevice);
+    (void)hipMemset(d_bad, 0, 4);
+    k_selftest_scan<<<1, 256>>>(static_cast<const uint32_t*>(d_in), static_cast<uint32_t*>(d_out));
+    k_selftest_fill<<<256, 256>>>(static_cast<uint32_t*>(d_rec), nrec);
+    TilePass tp{};
+    tp.rec = d_rec;
+    tp.dt = static_cast<const uint32_t*>(d_dt);
+    tp.n = (int64_t)nrec;
+    tp.nt = NT;
+    tp.mt = NT;
+    tp.nc = NB;
+    k_selftest_walk<<<NB, 64>>>(tp, cap, static_cast<uint32_t*>(d_w), static_cast<uint32_t*>(d_n),
+                                static_cast<unsigned int*>(d_bad));
+    std::vector<uint32_t> walk((size_t)NB * cap), wn(NB);
+    unsigned int bad = 0;
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(got.data(), d_out, 4 * 3 * 256, hipMemcpyDeviceToHost) ||
+        hipMemcpy(walk.data(), d_w, 4 * walk.size(), hipMemcpyDeviceToHost) ||
+        hipMemcpy(wn.data(), d_n, 4 * NB, hipMemcpyDeviceToHost) || hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost)) {
+        cleanup();
+        say("self-check: a kernel or copy failed");
+        return 1;
+    }
+    cleanup();
+    for (int wv = 0; wv < 4 && !what; wv++) {
+        uint32_t a = 0, m = 0, prev = 0;
+        for (int l = 0; l < 64; l++) {
+            const uint32_t v = in[64 * wv + l];
+            a += v;
+            m = (v & 255u) > m ? (v & 255u) : m;
+            const uint32_t* o = &got[3 * (64 * wv + l)];
+            if (o[0] != a) what = "self-check: the DPP add scan (wave_incl_scan) is wrong";
+            else if (o[1] != m) what = "self-check: the DPP max scan (wave_incl_scan) is wrong";
+            else if (o[2] != (l ? prev : 0u)) what = "self-check: the DPP lane shift (wave_shr1) is wrong";
+            if (what) break;
+            prev = m;
+        }
+    }
+    for (int b = 0; b < NB && !what; b++) {
+        if (wn[b] != want[b].size()) what = "self-check: the tile walk visited a wrong number of records";
+        for (size_t i = 0; !what && i < want[b].size(); i++)
+            if (walk[(size_t)b * cap + i] != want[b][i]) what = "self-check: the tile walk read a wrong record";
+    }
+    if (!what && bad) what = "self-check: the tile walk addressed a record past its pass";
+    if (what) {
+        say(what);
+        rc = 1;
+    } else {
+        say("ok");
+    }
+    return rc;
 }
 
 // Fire from tile passes: one workgroup per item -- a bucket of the lane (4 << (bits - tbits)

@@ -355,6 +355,12 @@ typedef struct fg_image_slices {
     const uint8_t* changed;     /* [n] 1 / 0 */
 } fg_image_slices;
 int  fg_snapshot_slices(fg_handle* h, fg_image_slices* out);
+/* The device self-check (ABI 16): the DPP wave scans and the tile walk the fire runs, as this
+ * library's code object compiled them, on inputs whose answers the host knows (msg: "ok" or what is
+ * wrong). fg_open runs it once per process and device and fails with FG_EDEVICE (its message in
+ * fg_last_error(NULL)) if it does not pass: a miscompiled build fails loudly instead of firing wrong
+ * rows. */
+int  fg_selftest(int32_t device_id, char* msg, int32_t cap);
 int  fg_restore(fg_handle* h, const fg_state_rows* in, int64_t timer_watermark);
 int  fg_late_dropped(fg_handle* h, int64_t* out);
 int  fg_get_stats(fg_handle* h, fg_stats* out);

@@ -225,3 +225,17 @@ def test_dictionary_reads_device_rows_after_their_producer():
         assert np.array_equal(ids, first), f"rep {rep}: ids not stable"
     assert len(d) == len(rows)
     d.close()
+
+
+def test_device_selfcheck_of_scans_and_tile_walk():
+    """fg_selftest (ABI 16): the DPP wave scans (wave_incl_scan add / max, wave_shr1) and the tile
+    walk's group setup, fragment map and record sources, as this library's code object compiled
+    them, against host answers (round 5: a compiler fold of the walk's DPP scan produced a fragment
+    base of -3). fg_open runs the same check once per process."""
+    import ctypes as C
+
+    from flink_amd import _lib as L
+    lib = L.load()
+    buf = C.create_string_buffer(160)
+    rc = lib.fg_selftest(0, buf, 160)
+    assert rc == 0 and buf.value == b"ok", buf.value
