@@ -126,6 +126,14 @@ __device__ __forceinline__ T* wave_uniform(T* q) {
     return (T*)(((uint64_t)hi << 32) | lo);
 }
 
+// A 0 the compiler cannot see through (an SGPR): `(&kernel_arg)[opaque_zero()]` re-reads a kernel
+// argument where it is used instead of at the kernel's entry (loop-invariant loads are hoisted).
+__device__ __forceinline__ int opaque_zero() {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
 // Workgroup barrier that orders LDS only: waits for this wave's LDS ops, not for its
 // global loads/stores (a __syncthreads() also drains vmcnt, stalling on in-flight stores).
 __device__ __forceinline__ void lds_barrier() {
@@ -3297,11 +3305,69 @@ __global__ __launch_bounds__(256) void k_tile_dirt(const uint16_t* dir, int32_t 
     }
 }
 
+// The same transpose in wide blocks of TT tiles x TC buckets (nc >= TC): a block reads TT row
+// segments of TC + 2 offsets (516 B at TC = 256: whole 64-B lines, where the 64 x 64 blocks read
+// 132-B pieces of 4-KB rows, each line shared with a block launched far away) and writes TC
+// columns of TT entries (one 128-B line each at TT = 32)
+template <int TT, int TC>
+__global__ __launch_bounds__(256) void k_tile_dirt_w(const uint16_t* dir, int32_t NT, int32_t NC, int32_t lshift,
+                                                     const unsigned long long* lane_mask, uint32_t* dt,
+                                                     uint32_t* btot) {
+    static_assert(TC % 64 == 0 && 256 % TC == 0 || TC == 256, "dirt block shape");
+    constexpr int RS = TC + 4;        // LDS row stride (u16): TC + 1 entries, padded
+    constexpr int WPR = TC / 2 + 1;   // 4-B words per row segment: entries [cb, cb + TC + 2)
+    constexpr int Q = 256 / TC;       // threads per column summing btot
+    __shared__ uint16_t s[TT][RS];
+    __shared__ uint32_t s_q[Q][TC];
+    const int tb = blockIdx.x * TT, cb = blockIdx.y * TC;
+    const unsigned long long lm = *gbl(lane_mask);
+    const int l0 = cb >> lshift, l1 = (cb + TC - 1 < NC ? cb + TC - 1 : NC - 1) >> lshift;
+    bool any = false;
+    for (int l = l0; l <= l1; l++) any = any || ((lm >> l) & 1);
+    if (!any) return;
+    for (int i = threadIdx.x; i < TT * WPR; i += 256) {
+        const int tt = i / WPR, k = i % WPR;
+        const int t = tb + tt, c = cb + 2 * k;
+        uint32_t w = 0;
+        if (t < NT && c <= NC) w = *gbl(reinterpret_cast<const uint32_t*>(dir + (int64_t)t * kTileDirStride(NC) + c));
+        *reinterpret_cast<uint32_t*>(&s[tt][2 * k]) = w;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TT * TC; i += 256) {
+        const int cc = i / TT, tt = i % TT;
+        const int t = tb + tt, c = cb + cc;
+        if (t < NT && c < NC && ((lm >> (c >> lshift)) & 1)) {
+            const uint32_t a = s[tt][cc], b = s[tt][cc + 1];
+            dt[(int64_t)c * NT + t] = a | ((b - a) << 16);
+        }
+    }
+    if (btot) {
+        const int cc = threadIdx.x % TC, q = threadIdx.x / TC;
+        uint32_t sum = 0;
+        for (int j = q; j < TT; j += Q)
+            if (tb + j < NT) sum += (uint32_t)s[j][cc + 1] - s[j][cc];
+        s_q[q][cc] = sum;
+        __syncthreads();
+        const int c = cb + (int)threadIdx.x;
+        if ((int)threadIdx.x < TC && c < NC && ((lm >> (c >> lshift)) & 1)) {
+            uint32_t t4 = 0;
+#pragma unroll
+            for (int j = 0; j < Q; j++) t4 += s_q[j][threadIdx.x];
+            if (t4) atomicAdd(&btot[c], t4);
+        }
+    }
+}
+
 hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int32_t lane_shift,
                             const unsigned long long* lane_mask, uint32_t* dt, uint32_t* btot, hipStream_t s) {
     if (tiles <= 0 || nc <= 0) return hipSuccess;
-    fg_launch(k_tile_dirt, dim3((unsigned)((tiles + 63) / 64), (unsigned)((nc + 63) / 64)), dim3(256), 0, s, dir,
-              tiles, nc, lane_shift, lane_mask, dt, btot);
+    if (nc >= 256) {   // (A/B round 6, 64 x 128 blocks alike: 15.9-16.0 vs 16.1 ms per step)
+        fg_launch((k_tile_dirt_w<32, 256>), dim3((unsigned)((tiles + 31) / 32), (unsigned)((nc + 255) / 256)), dim3(256),
+                  0, s, dir, tiles, nc, lane_shift, lane_mask, dt, btot);
+    } else {
+        fg_launch(k_tile_dirt, dim3((unsigned)((tiles + 63) / 64), (unsigned)((nc + 63) / 64)), dim3(256), 0, s, dir,
+                  tiles, nc, lane_shift, lane_mask, dt, btot);
+    }
     return hipGetLastError();
 }
 
@@ -3658,7 +3724,8 @@ int run_selftest(int device, char* msg, size_t cap_msg) {
 // SM: 0 the plain fire (no split code: the split and merge paths cost it 4 spilled VGPRs, round 5),
 // 1 a split fire's launches (chunk items, then the merge launch), 2 chunk items with HOT
 template <int VTC, bool TAB, int SM>   // TAB: source / destination tables (compiled out of the plain fire)
-__global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
+__global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
+    const TileFire& f = fa;
     constexpr bool HOT = SM == 2;
     constexpr int T = kTileFireThreads, W = T / 64, S = kTileSlots;
     constexpr int kRounds = S / T + 1;   // + 1: the sentinel slot (thread 0)
@@ -3706,6 +3773,13 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
             break;
         }
         bool live = x < NI;
+#if !defined(FG_FIRE_HOIST)
+        // (the parameters re-read through an opaque offset per item and again for the compaction:
+        // hoisted to the kernel's entry they held ~100 SGPRs across the record loop, 80 of them
+        // spilled to VGPR lanes, and left one SGPR pair for every compare of the probe loop)
+        const TileFire& f = (&fa)[opaque_zero()];
+        const MergeParams& p = f.m;
+#endif
         int r_lo = 0, r_hi = 0, item = 0;
         int32_t g_lo = 0, g_hi = 0x7fffffff, part = -1;   // (split: the item's tile range, chunk ordinal)
         int32_t mc0 = 0, mck = 0;                          // (merge: the bucket's chunks)
@@ -4138,6 +4212,11 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
         if (diag_sink == 0x5EEDull) atomicOr(p.overflow, 0u);
 #endif
         __syncthreads();
+        {
+#if !defined(FG_FIRE_HOIST)
+        const TileFire& f = (&fa)[opaque_zero()];
+        const MergeParams& p = f.m;
+#endif
         // compaction: the occupied slots' ranks (round k covers slots [k*T, (k+1)*T); the last
         // round the sentinel slot), a dense rank -> slot map, then one row per lane
         uint32_t occ_mask = 0;
@@ -4305,6 +4384,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire f) {
                     db[3 * cap + at] = lds_repr(vt, (int64_t)t_v[sl]);
                 }
             }
+        }
         }
         __syncthreads();   // the table is cleared for the next item
     }
