@@ -652,6 +652,35 @@ int zero_scalars(fg_handle* h, bool with_out) {
     return FG_OK;
 }
 
+// Every tile fire goes through here. FG_STAMPS builds with FG_STAMPS set in the environment print
+// the fire's phase cycles per wave (k_tile_fire's FSTAMP phases) after each launch.
+hipError_t tile_fire_launch(fg_handle* h, TileFire& f, int32_t workgroups, hipStream_t s) {
+#ifdef FG_STAMPS
+    static DevBuf d_fs;
+    const bool st = getenv("FG_STAMPS") != nullptr && d_fs.ensure(64) == hipSuccess;
+    if (st) {
+        (void)hipMemsetAsync(d_fs.p, 0, 64, s);
+        f.m.stamps = d_fs.as<unsigned long long>();
+    }
+    const hipError_t e = launch_tile_fire(f, workgroups, s);
+    if (st) {
+        unsigned long long v[8];
+        (void)hipMemcpyAsync(v, d_fs.p, sizeof v, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const double waves = (double)workgroups * kTileFireThreads / 64;
+        fprintf(stderr, "[fg stamps] tile_fire split=%d merge=%d srcs=%d dst=%d passes=%d: clear %.0f walk %.0f wait %.0f "
+                "insert %.0f sources %.0f barrier %.0f compact %.0f emit %.0f (cycles/wave)\n", f.split, f.merge,
+                f.m.n_src, f.m.has_dst, f.n_passes, v[0] / waves, v[1] / waves, v[2] / waves, v[3] / waves,
+                v[4] / waves, v[5] / waves, v[6] / waves, v[7] / waves);
+        f.m.stamps = nullptr;
+    }
+    return e;
+#else
+    (void)h;
+    return launch_tile_fire(f, workgroups, s);
+#endif
+}
+
 int check_overflow(fg_handle* h) {
     // region overflows (bits 0 and 2) are handled by the fail list (settle_jobs)
     unsigned int fl = h->h_scalars.as<unsigned int>()[0];
@@ -947,7 +976,7 @@ int retry_failed(fg_handle* h) {
                 if (rc) return rc;
                 f.m.n_retry = (int)regs.size();
                 KTimer kt(h, j.kclass, 0);
-                HIPCHK(h, launch_tile_fire(f, std::min<int>((int)regs.size(), merge_grid(h)), h->stream));
+                HIPCHK(h, tile_fire_launch(h, f, std::min<int>((int)regs.size(), merge_grid(h)), h->stream));
                 continue;
             }
             MergeParams p{};
@@ -1284,11 +1313,11 @@ int tile_split_fire(fg_handle* h, const Lane& ln, TileFire& f, uint32_t chunk) {
     f.split = 1;
     f.hot = h->tile_hot ? 1 : 0;
     HIPCHK(h, launch_tile_plan(f, h->stream));
-    HIPCHK(h, launch_tile_fire(f, (int)std::min<int64_t>(max_items, h->merge_grid), h->stream));
+    HIPCHK(h, tile_fire_launch(h, f, (int)std::min<int64_t>(max_items, h->merge_grid), h->stream));
     TileFire fm = f;   // the split buckets: their chunks' partial entries merged (+ tables, rows)
     fm.merge = 1;
     fm.hot = 0;
-    HIPCHK(h, launch_tile_fire(fm, std::min(nb, h->merge_grid), h->stream));
+    HIPCHK(h, tile_fire_launch(h, fm, std::min(nb, h->merge_grid), h->stream));
     return FG_OK;
 }
 
@@ -1427,7 +1456,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                         rc = tile_split_fire(h, ln, f, chunk);
                         if (rc) return rc;
                     } else {
-                        HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                        HIPCHK(h, tile_fire_launch(h, f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
                     }
                 }
                 if (t0) fired_tables.push_back(se);
@@ -1573,7 +1602,7 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                         rc = tile_split_fire(h, ln, f, h->tile_chunk);
                         if (rc) return rc;
                     } else {
-                        HIPCHK(h, launch_tile_fire(f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
+                        HIPCHK(h, tile_fire_launch(h, f, std::min(1 << (f.tbits - kTileBits), h->merge_grid), h->stream));
                     }
                 }
                 if (kc == K_TILE_FIRE) fire_class = K_TILE_FIRE;

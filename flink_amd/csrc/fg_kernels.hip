@@ -3400,7 +3400,10 @@ struct TileWalk {
     uint32_t n;                 // records of the pass: a source at or past it is a walk error
     bool bad;                   // (reported as overflow flag 8, the record not read)
     int32_t nt;                 // the walk's end tile (exclusive)
-    int32_t t0, stride;         // current group's first tile, groups' stride
+    int32_t t0, tn;             // current group's first tile, the next group's (its entries in xn)
+    int32_t t_base, ng;         // the walk's first tile, its groups
+    int32_t gk, wave, W;        // groups taken (static assignment: group wave + W * k)
+    uint32_t* q;                // LDS group counter the waves take groups from (nullptr: static)
     int32_t gsz;                // tiles per group (kTileGroup, fewer for a short tile range)
     uint32_t xn[kTileTPL];      // the next group's directory entries (prefetched)
     uint32_t g_len[kTileTPL], g_st[kTileTPL], g_tot, b;
@@ -3426,9 +3429,19 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// the walk's next group: from the workgroup's LDS counter (the waves of an item finish together:
+// a wave that ran ahead takes more groups -- with a fixed share per wave the item's slowest wave
+// held the others at the barrier after the inserts, 14 % of the headline fire's wave cycles, 5 %
+// with the counter; fire 0.727 -> 0.677 ms per 100M records, round 6), or the static share
+__device__ __forceinline__ int32_t tile_walk_grab(TileWalk& w, int lane) {
+    if (!w.q) return w.wave + w.W * (w.gk++);
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(w.q, 1u);
+    return (int32_t)__builtin_amdgcn_readfirstlane(g);
+}
 // (the walk covers the pass's tiles [t_lo, t_hi): all of them, or a split bucket's chunk)
 __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp, int32_t cb, int wave, int W,
-                                                int lane, int32_t t_lo, int32_t t_hi) {
+                                                int lane, int32_t t_lo, int32_t t_hi, uint32_t* q = nullptr) {
     w.col = tp.dt + (int64_t)cb * tp.nt;
     w.rec = tp.rec;
     w.n = (uint32_t)tp.n;
@@ -3439,17 +3452,25 @@ __device__ __forceinline__ void tile_walk_begin(TileWalk& w, const TilePass& tp,
     const int32_t per = (t_hi - t_lo + W - 1) / W;
     w.gsz = per >= kTileGroup ? kTileGroup : (per + kTileTPL - 1) / kTileTPL * kTileTPL;
     if (w.gsz < kTileTPL) w.gsz = kTileTPL;
-    w.stride = W * w.gsz;
-    w.t0 = t_lo + wave * w.gsz - w.stride;
+    w.t_base = t_lo;
+    w.ng = t_hi > t_lo ? (t_hi - t_lo + w.gsz - 1) / w.gsz : 0;
+    w.gk = 0;
+    w.wave = wave;
+    w.W = W;
+    // (passes of a few groups per wave keep the static share: the table fires' 2-3K-tile passes
+    // ran 5-15 % slower taking groups from the counter, A/B round 6)
+    w.q = w.ng >= 4 * W ? q : nullptr;
+    const int32_t g0 = tile_walk_grab(w, lane);
+    w.tn = g0 < w.ng ? t_lo + g0 * w.gsz : t_hi;
 #pragma unroll
-    for (int q = 0; q < kTileTPL; q++) {
+    for (int q4 = 0; q4 < kTileTPL; q4++) {
         // (every load issued, the index clamped and the entry masked: a load under a branch would
         // keep the compiler from counting the wave's loads in flight -- s_waitcnt vmcnt(0))
-        const int t = t_lo + wave * w.gsz + lane * kTileTPL + q;
-        const bool ok = t < w.nt && lane * kTileTPL + q < w.gsz;
+        const int t = w.tn + lane * kTileTPL + q4;
+        const bool ok = t < w.nt && lane * kTileTPL + q4 < w.gsz;
         const uint32_t x = gbl(w.col)[ok ? t : 0];
-        w.xn[q] = ok ? x : 0u;
-        w.g_len[q] = w.g_st[q] = 0;
+        w.xn[q4] = ok ? x : 0u;
+        w.g_len[q4] = w.g_st[q4] = 0;
     }
     w.g_tot = w.b = 0;
 }
@@ -3465,17 +3486,19 @@ __device__ __forceinline__ bool tile_walk_next(TileWalk& w, uint8_t* fm, uint32_
     // compiler count the loads of the window just issued as possibly absent)
     bool done = false;
     while (w.b >= w.g_tot) {   // the next group with records
-        w.t0 += w.stride;
+        w.t0 = w.tn;
         if (w.t0 >= w.nt) {
             done = true;
             break;
         }
+        const int32_t gn = tile_walk_grab(w, lane);
+        w.tn = gn < w.ng ? w.t_base + gn * w.gsz : w.nt;
         uint32_t base[kTileTPL], sum = 0;
 #pragma unroll
         for (int q = 0; q < kTileTPL; q++) {
             const int t = w.t0 + lane * kTileTPL + q;
             const uint32_t x = w.xn[q];
-            const int tn = t + w.stride;
+            const int tn = w.tn + lane * kTileTPL + q;
             const bool okn = tn < w.nt && lane * kTileTPL + q < w.gsz;
             const uint32_t xn = gbl(w.col)[okn ? tn : 0];
             w.xn[q] = okn ? xn : 0u;
@@ -3745,9 +3768,32 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
     __shared__ unsigned long long s_out_base;
     __shared__ uint32_t s_rc[kTileMaxRegions];   // destination: keys per region of the item
     __shared__ uint32_t s_rb[kTileMaxRegions];   // destination: each region's first rank
+    __shared__ uint32_t s_gnext[kMaxTilePasses];  // per pass: the next tile group a wave takes
     const MergeParams& p = f.m;
     const bool dst = TAB && p.has_dst != 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef FG_STAMPS
+    // diagnostic build only: cycles per phase summed over the waves -- 0 table clear, 1 tile walk
+    // (fragment map, sources, loads issued), 2 waiting for a window's records, 3 inserts, 4 resident
+    // sources / chunk partials, 5 the barrier after the inserts (the item's slowest wave), 6
+    // compaction (occupancy ranks, row reservation, rank -> slot map), 7 emit / write-back
+    unsigned long long fst_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long fst_prev = __builtin_amdgcn_s_memtime();
+#define FSTAMP(i)                                                     \
+    do {                                                              \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+        fst_acc[i] += now_ - fst_prev;                                \
+        fst_prev = now_;                                              \
+    } while (0)
+#define FWAIT(kk, vv) asm volatile("" ::"v"(kk[kTileRpl - 1]), "v"(vv[kTileRpl - 1]))
+#else
+#define FSTAMP(i) \
+    do {          \
+    } while (0)
+#define FWAIT(kk, vv) \
+    do {              \
+    } while (0)
+#endif
     const int vt = VTC >= 0 ? VTC : p.val_type;
     const int64_t vinit = lds_repr(vt, val_identity(vt));
     const int sub = p.region_bits - f.tbits;          // current region bits above the passes'
@@ -3818,8 +3864,10 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
         }
         if (TAB)
             for (int i = tid; i < kTileMaxRegions; i += T) s_rc[i] = 0;
+        if (tid < kMaxTilePasses) s_gnext[tid] = 0;
         if (tid == 0) s_flags = 0;
         __syncthreads();
+        FSTAMP(0);
         bool full = false;
 #if defined(FG_DIAG_FIRE)
         uint64_t diag_sink = 0;
@@ -3946,6 +3994,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
                 }
             }
         }
+        FSTAMP(4);
         if (live && merge) {
             // the split bucket's chunks: their partial entries (int32 key, COUNT(*), the value's LDS
             // form) into the table -- the value combined as the chunks combined their records.
@@ -4192,17 +4241,31 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
                     if (t_lo >= t_hi) continue;
                 }
                 TileWalk w;
-                tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane, t_lo, t_hi);
+                tile_walk_begin(w, tp, (tp.lane << (f.tbits - kTileBits)) | item, wave, W, lane, t_lo, t_hi,
+#if defined(FG_WALK_STATIC)
+                                nullptr);
+#else
+                                pi < kMaxTilePasses ? &s_gnext[pi] : nullptr);
+#endif
                 int32_t ka[kTileRpl], kb[kTileRpl];
                 int64_t va[kTileRpl], vb[kTileRpl];
                 uint32_t na = 0, nb = 0;
                 bool more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
+                FSTAMP(1);
                 while (more) {   // (buffer roles static: the loop is unrolled by two)
                     const bool hb = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, kb, vb, nb);
+                    FSTAMP(1);
+                    FWAIT(ka, va);
+                    FSTAMP(2);
                     insert(ka, va, na);
+                    FSTAMP(3);
                     if (!hb) break;
                     more = tile_walk_next(w, s_fm[wave], s_dl[wave], lane, ka, va, na);
+                    FSTAMP(1);
+                    FWAIT(kb, vb);
+                    FSTAMP(2);
                     insert(kb, vb, nb);
+                    FSTAMP(3);
                 }
                 if (__ballot(w.bad) != 0 && lane == 0) atomicOr(p.overflow, 8u);
             }
@@ -4211,7 +4274,9 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
 #if defined(FG_DIAG_FIRE)
         if (diag_sink == 0x5EEDull) atomicOr(p.overflow, 0u);
 #endif
+        FSTAMP(4);
         __syncthreads();
+        FSTAMP(5);
         {
 #if !defined(FG_FIRE_HOIST)
         const TileFire& f = (&fa)[opaque_zero()];
@@ -4300,6 +4365,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
                 (uint16_t)(r < kRounds - 1 ? r * T + tid : S);
         }
         __syncthreads();
+        FSTAMP(6);
         if (live && to_part && !(fl & 6u)) {   // partial entries (LDS repr), merged later
             const uint32_t total = s_total;
             const uint32_t ob = (uint32_t)s_out_base;
@@ -4387,7 +4453,14 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
         }
         }
         __syncthreads();   // the table is cleared for the next item
+        FSTAMP(7);
     }
+#ifdef FG_STAMPS
+    if (fa.m.stamps && lane == 0)
+        for (int i = 0; i < 8; i++) atomicAdd(&fa.m.stamps[i], fst_acc[i]);
+#endif
+#undef FSTAMP
+#undef FWAIT
 }
 
 hipError_t launch_tile_fire(const TileFire& f, int32_t workgroups, hipStream_t s) {
