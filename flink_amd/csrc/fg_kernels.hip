@@ -4073,7 +4073,10 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
             }
         } else if (live) {
             // one window's records into the table, one probe loop per record (the plain fire)
-            auto insert_plain = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
+            // (FULL: a whole window, every lane's records present; RETRY: the region filter --
+            // compile-time tags, so the common case's loop carries neither per-record test)
+            auto insert_plain = [&](auto FULL, auto RETRY, const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl],
+                                    uint32_t nrec) {
 #if defined(FG_DIAG_FIRE) && (FG_DIAG_FIRE & 2)   // (diagnostic: no inserts, the records consumed)
 #pragma unroll
                 for (int u = 0; u < kTileRpl; u++)
@@ -4089,9 +4092,11 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
                 }
 #pragma unroll
                 for (int u = 0; u < kTileRpl; u++) {
-                    if (lane + 64 * u >= nrec) continue;
+                    if (!decltype(FULL)::value && lane + 64 * u >= nrec) continue;
                     const int32_t key = kr[u];
-                    if (retry && (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) != r_lo) continue;
+                    if (decltype(RETRY)::value && retry &&
+                        (int)((uint64_t)mix_of((int64_t)key) >> (64 - p.region_bits)) != r_lo)
+                        continue;
                     int sl = -1;
                     if (key == kEmpty32) {
                         sl = S;
@@ -4229,8 +4234,17 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
                 }
             };
             auto insert = [&](const int32_t (&kr)[kTileRpl], const int64_t (&vr)[kTileRpl], uint32_t nrec) {
-                if constexpr (HOT) insert_hot(kr, vr, nrec);
-                else insert_plain(kr, vr, nrec);
+                if constexpr (HOT) {
+                    insert_hot(kr, vr, nrec);
+                } else {
+#if defined(FG_INSERT_GENERIC)
+                    insert_plain(std::false_type{}, std::true_type{}, kr, vr, nrec);
+#else
+                    if (retry) insert_plain(std::false_type{}, std::true_type{}, kr, vr, nrec);
+                    else if (nrec == (uint32_t)kTileWin) insert_plain(std::true_type{}, std::false_type{}, kr, vr, nrec);
+                    else insert_plain(std::false_type{}, std::false_type{}, kr, vr, nrec);
+#endif
+                }
             };
             for (int pi = 0; pi < f.n_passes; pi++) {
                 const TilePass tp = f.n_passes == 1 ? f.one : f.passes[pi];
