@@ -872,8 +872,9 @@ int tile_job_params(fg_handle* h, int ji, TileFire* f) {
     p.job = ji;
     f->n_passes = (int32_t)tps.size();
     f->tbits = j.tbits;
-    if (tps.size() == 1) {   // (the common case: one pass per lane, in the kernel's arguments)
-        f->one = tps[0];
+    if (tps.size() <= 2) {   // (one or two passes per lane -- TUMBLE, HOP / CUMULATE flushes: in the
+        f->one = tps[0];     // kernel's arguments, no descriptor copy queued before the fire)
+        if (tps.size() == 2) f->two = tps[1];
         return FG_OK;
     }
     return arena_put(h, tps.data(), tps.size(), &f->passes);

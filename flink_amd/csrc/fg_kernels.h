@@ -503,8 +503,9 @@ struct TileSplit {
 };
 struct TileFire {
     MergeParams m;            // emit fields, value op, overflow / out_count / fail list, job, region_bits
-    const TilePass* passes;   // device array [n_passes], all at bits `tbits` (n_passes > 1)
+    const TilePass* passes;   // device array [n_passes], all at bits `tbits` (n_passes > 2)
     TilePass one;             // the pass, by value, when n_passes == 1 (no descriptor copy)
+    TilePass two;             // n_passes == 2: the passes are `one` and `two` (by value, no copy either)
     int32_t n_passes;
     int32_t tbits;
     // items: the lane's buckets 0 .. (1 << (tbits - kTileBits)) - 1, or (retry) regions at

@@ -3371,6 +3371,13 @@ hipError_t launch_tile_dirt(const uint16_t* dir, int32_t tiles, int32_t nc, int3
     return hipGetLastError();
 }
 
+// pass pi of a tile fire: one or two passes ride in the kernel arguments, more in a device array
+__device__ __forceinline__ TilePass tile_pass(const TileFire& f, int pi) {
+    if (f.n_passes == 1 || (f.n_passes == 2 && pi == 0)) return f.one;
+    if (f.n_passes == 2) return f.two;
+    return f.passes[pi];
+}
+
 // Order a wave's LDS writes before its other lanes' reads (wave-private scratch, no barrier).
 __device__ __forceinline__ void wave_lds_sync() {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -4247,7 +4254,7 @@ __global__ __launch_bounds__(kTileFireThreads) void k_tile_fire(TileFire fa) {
                 }
             };
             for (int pi = 0; pi < f.n_passes; pi++) {
-                const TilePass tp = f.n_passes == 1 ? f.one : f.passes[pi];
+                const TilePass tp = tile_pass(f, pi);
                 int32_t t_lo = 0, t_hi = tp.nt;
                 if (split) {   // the item's range of the concatenated tile sequence, in this pass
                     t_lo = g_lo - f.sp.gpre[pi] > 0 ? g_lo - f.sp.gpre[pi] : 0;
@@ -4539,7 +4546,7 @@ __global__ __launch_bounds__(kTilePlanThreads) void k_tile_plan(TileFire f) {
         tb[q] = 0;
         if (bk >= nb) continue;
         for (int pi = 0; pi < f.n_passes; pi++) {
-            const TilePass& tp = f.n_passes == 1 ? f.one : f.passes[pi];
+            const TilePass tp = tile_pass(f, pi);
             if (tp.btot) tb[q] += gbl(tp.btot)[(tp.lane << (f.tbits - kTileBits)) | bk];
         }
         mine += tb[q];
