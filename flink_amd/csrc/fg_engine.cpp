@@ -776,10 +776,11 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     // may hold NULL counts iff something merged into it may
     unsigned long long null_mask = 0;
     bool dst_null = false;
-    bool src_narrow = false;
+    bool src_narrow = false, all_narrow = !j.srcs.empty();
     for (size_t i = 0; i < j.srcs.size(); i++) {
         srcs.push_back(ref_of(j.srcs[i]));
         src_narrow = src_narrow || j.srcs[i]->narrow;
+        all_narrow = all_narrow && j.srcs[i]->narrow;
         if (j.srcs[i]->has_null) {
             if (i < 64) null_mask |= 1ull << i;
             dst_null = true;
@@ -792,7 +793,7 @@ int job_params(fg_handle* h, int ji, MergeParams* p) {
     *p = MergeParams{};
     p->region_bits = h->region_bits;
     p->n_src = (int)srcs.size();
-    p->src_narrow = src_narrow ? 1 : 0;
+    p->src_narrow = all_narrow ? 2 : src_narrow ? 1 : 0;
     if (srcs.size() <= 2) {   // by value in the arguments (no descriptor copy on the stream)
         for (size_t i = 0; i < srcs.size(); i++) p->src_in[i] = srcs[i];
     } else {
@@ -1583,7 +1584,11 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
                 // for HOP, whose fires read the slice tables through the compact merge: A/B on one box
                 // (profiles/r05/hop_narrow) 0.507 vs 0.445 ms per merge fire reading narrow vs wide
                 // entries, 46.1 vs 44.4 ms per 1B records; CUMULATE's tile fire gains (59.0 vs 62.7)
+#if defined(FG_HOP_WIDE)
                 if (job.dst && job.dst->upper == 0 && h->narrow_tables && !h->mv && h->w.kind != HOP)
+#else
+                if (job.dst && job.dst->upper == 0 && h->narrow_tables && !h->mv)
+#endif
                     job.dst->narrow = true;
                 job.tile = true;
                 job.tbits = ln.passes[0]->bits;

@@ -213,7 +213,7 @@ struct MergeParams {
     int32_t narrow;            // fast stream of narrow 12-B records (every batch stride 3)
     int32_t compact;           // compact LDS table (fast_stream, no src tables, < 2^32 records)
     int32_t n_src;
-    int32_t src_narrow;        // some source table holds narrow (16-B) entries
+    int32_t src_narrow;        // 1: some source table holds narrow (16-B) entries; 2: every one does
     const TableRef* src;       // device array [n_src]; null: n_src <= 2, the tables in src_in
     TableRef src_in[2];        // up to two source tables by value (no descriptor copy per merge)
     int32_t n_batches;

@@ -1537,6 +1537,19 @@ __device__ __forceinline__ uint32_t lds_home(int64_t h) {
 
 // linear probe from `slot` (keys never leave the table during a region, so a key is at the
 // first slot from its home that was empty or held it when it was inserted)
+// The narrow (int32-keyed) LDS table's home bucket: a multiplicative hash of the key itself -- the
+// records, narrow entries and wide entries of one merge all reach it from the int32 key, so a narrow
+// entry needs no fmix64 of its key (the wide one's stored mix was its home: a 64-bit mix per narrow
+// entry made HOP's fires over narrow tables slower than over wide ones, round 5)
+template <bool C, bool MV>
+__device__ __forceinline__ uint32_t nt_home(int32_t k) {
+    constexpr uint32_t NB = (uint32_t)(MergeCfg<C, MV>::kSlotsT / kBucket);
+#if defined(FG_NT_HOME_MIX)
+    return lds_home<C, MV>(mix_of((int64_t)k));
+#else
+    return __umulhi((uint32_t)k * 0x9E3779B1u, NB) * kBucket;
+#endif
+}
 template <bool C, bool MV>
 __device__ __forceinline__ int lds_find_or_insert_from(LdsTableT<C, MV>& t, int64_t k, uint32_t slot, bool& full) {
     constexpr int S = MergeCfg<C, MV>::kSlotsT;
@@ -1904,7 +1917,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
 #pragma unroll
         for (int u = 0; u < kMergeU; u++) {
             if constexpr (NT) {
-                home[u] = lds_home<C, MV>(mix_of(c[u].x));
+                home[u] = nt_home<C, MV>((int32_t)c[u].x);
                 bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
             } else {
             home[u] = lds_home<C, MV>(c[u].x);
@@ -2110,21 +2123,69 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 }
                 uint32_t home[kSrcU];
                 int4 bq[kSrcU];
+                int32_t k32[kSrcU];   // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
-                    home[u] = lds_home<C, MV>(k[u]);
+                    k32[u] = (int32_t)key_of(k[u]);
+                    home[u] = nt_home<C, MV>(k32[u]);
                     bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
                 }
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
                     if (i0 + u * T + tid >= NE) continue;
-                    // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
-                    const int slot = nt_bucket_slot(t, (int32_t)key_of(k[u]), home[u], bq[u], full);
+                    const int slot = nt_bucket_slot(t, k32[u], home[u], bq[u], full);
                     if (slot >= 0 && cs[u]) lds_add<C, MV>(t, slot, (unsigned long long)cs[u], 0ull, sm[u], vt, p);
                 }
             }
         }
-        if constexpr (NT) if (p.n_src > 0 && p.src_narrow) {   // narrow table: a source entry's key from its mix
+        if constexpr (NT) if (p.n_src > 0 && p.src_narrow == 2) {   // every source narrow (HOP's slice tables)
+            // (a loop of its own: the entry's three columns loaded at clamped indices, no per-entry
+            // layout test; the layout-aware loop below made HOP's fires over narrow tables slower
+            // than over wide ones)
+            const uint32_t NE = skip ? 0u : s_soff[p.n_src];
+            for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
+                int32_t k32[kSrcU];
+                uint32_t cs[kSrcU];
+                int64_t sm[kSrcU][1];
+                int j = 0;
+                {   // (the clamped index, as below: past NE the search would land on an empty last table,
+                    // whose first entry lies past the clamped index)
+                    const uint32_t f = i0 + tid < NE ? i0 + tid : NE - 1;
+                    int lo = 0, hi = p.n_src;
+                    while (hi - lo > 1) {
+                        const int mid = (lo + hi) >> 1;
+                        if (s_soff[mid] <= f) lo = mid;
+                        else hi = mid;
+                    }
+                    j = lo;
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    const uint32_t f0 = i0 + u * T + tid;
+                    const uint32_t f = f0 < NE ? f0 : NE - 1;   // (clamped: every load issued)
+                    while (s_soff[j + 1] <= f) j++;
+                    const uint32_t i = f - s_soff[j];
+                    const auto base = gbl(s_sbase[j]);
+                    k32[u] = reinterpret_cast<const int32_t __attribute__((address_space(1)))*>(base)[i];
+                    cs[u] = reinterpret_cast<const uint32_t __attribute__((address_space(1)))*>(base)[cap + i];
+                    sm[u][0] = base[cap + i];
+                }
+                uint32_t home[kSrcU];
+                int4 bq[kSrcU];
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    home[u] = nt_home<C, MV>(k32[u]);
+                    bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
+                }
+#pragma unroll
+                for (int u = 0; u < kSrcU; u++) {
+                    if (i0 + u * T + tid >= NE) continue;
+                    const int slot = nt_bucket_slot(t, k32[u], home[u], bq[u], full);
+                    if (slot >= 0 && cs[u]) lds_add<C, MV>(t, slot, (unsigned long long)cs[u], 0ull, sm[u], vt, p);
+                }
+            }
+        }
+        if constexpr (NT) if (p.n_src > 0 && p.src_narrow == 1) {   // narrow and wide tables: per entry
             const uint32_t NE = skip ? 0u : s_soff[p.n_src];   // (compact: n_src <= kMaxSrcFlat)
             for (uint32_t i0 = 0; i0 < NE; i0 += kSrcU * T) {
                 int64_t k[kSrcU], cs[kSrcU], sm[kSrcU][1];
@@ -2154,10 +2215,8 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                     const bool nar = s_snar[j] != 0;
                     if (nar) {
                         k32[u] = tab_key32(base, cap, i, true);
-                        k[u] = mix_of((int64_t)k32[u]);
                     } else {   // (the operator's keys fit 32 bits: the mix's key is its int32 sign-extended)
-                        k[u] = base[i];
-                        k32[u] = (int32_t)key_of(k[u]);
+                        k32[u] = (int32_t)key_of(base[i]);
                     }
                     cs[u] = tab_cs(base, cap, i, nar);
                     sm[u][0] = tab_v(base, cap, i, nar);
@@ -2166,7 +2225,7 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
                 int4 bq[kSrcU];
 #pragma unroll
                 for (int u = 0; u < kSrcU; u++) {
-                    home[u] = lds_home<C, MV>(k[u]);
+                    home[u] = nt_home<C, MV>(k32[u]);
                     bq[u] = *reinterpret_cast<const int4*>(&t.key[home[u]]);
                 }
 #pragma unroll
