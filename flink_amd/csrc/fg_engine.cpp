@@ -1636,9 +1636,8 @@ int flush_lanes(fg_handle* h, const std::vector<int>& sel_in, const FireRange* f
         // (resident sources: plain ones -- no NULL counts, marks or chains -- at a COUNT(*) bound
         // below 2^32, keyed by their int32 keys under narrow staging; a fired window that keeps
         // its state (allowed lateness) takes the wide merge)
-        static const bool compact_src = !getenv("FG_COMPACT_FIRE") || std::atoi(getenv("FG_COMPACT_FIRE")) != 0;
         const bool src_ok = p.n_src == 0 ||
-                            (compact_src && !h->mv && p.src_null_mask == 0 && !p.mark_mask && !p.markonly_mask &&
+                            (!h->mv && p.src_null_mask == 0 && !p.mark_mask && !p.markonly_mask &&
                              !p.emit_marked && p.dst_mode == 0 && p.n_src <= 64 && ub_cnt_fits(h) &&
                              (!p.narrow || h->keys32));
         p.compact = plain && src_ok && ln.fill < ((int64_t)1 << 32) && !(p.emit && p.has_dst && h->retain) ? 1 : 0;
