@@ -1801,7 +1801,8 @@ struct MergeCursor {
 template <bool C, int VTC, bool MV = false, bool N12 = false>
 // waves_per_eu(4): 128 VGPRs, so two 512-thread compact workgroups (16 waves) fit a CU (8 and 64
 // VGPRs for two 1,024-thread ones, FG_COMPACT_T)
-__global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_waves_per_eu(MergeCfg<C, MV>::kWavesPerEu))) void k_merge(MergeParams p) {
+__global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_waves_per_eu(MergeCfg<C, MV>::kWavesPerEu))) void k_merge(MergeParams pa) {
+    const MergeParams& p = pa;
     constexpr int S = MergeCfg<C, MV>::kSlotsT;
     constexpr int T = MergeCfg<C, MV>::kThreads;
     constexpr int kWaves = T / 64;
@@ -2053,6 +2054,11 @@ __global__ __launch_bounds__((MergeCfg<C, MV>::kThreads)) __attribute__((amdgpu_
     }
 
     for (int ri = 0; ri < nreg; ri++) {
+#if !defined(FG_MERGE_HOIST)
+        // (the arguments re-read per region, as in the tile fire: hoisted to the kernel's entry they
+        // are held -- and spilled -- across the region's loops)
+        const MergeParams& p = (&pa)[opaque_zero()];
+#endif
         const int r = region_at(ri);
         const bool skip = skipped(r);
         for (int i = tid; i <= S; i += T) {
@@ -3079,7 +3085,11 @@ hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, cons
 // one classification round allow, and the fire reads half as many fragments. Bucket counts are
 // u16 pairs in one LDS word (ds_add_u32 of 1 << 16 * (b & 1): a tile has < 2^16 records).
 // *p.max_bucket: the largest bucket count of one tile (skew).
-__global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
+__global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams pa) {
+    // (the arguments re-read per tile through an opaque offset, as in the fire: hoisted to the
+    // kernel's entry they were held across the tile loop, 103 SGPRs spilled to VGPR lanes)
+    const IngestParams* pp = &pa;
+#define p (*pp)
     constexpr int T = kTileThreads;
     constexpr int R = kTileR;
     constexpr int H = kTileH;
@@ -3197,6 +3207,9 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     if (beg < end) load(beg, ka, ta);
     int j = 0;
     for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
+#if !defined(FG_P1_HOIST)
+        pp = &(&pa)[opaque_zero()];
+#endif
         uint32_t rcb[H][R], k32[H][R];
         {
             longlong2 kb[R / 2], tb[R / 2];
@@ -3319,6 +3332,7 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
         if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
         if (s_qnext != JMAX) atomicMin(p.qnext, s_qnext);
     }
+#undef p
 }
 
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
