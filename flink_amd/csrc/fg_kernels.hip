@@ -3085,11 +3085,7 @@ hipError_t launch_partition_by_owner(const int64_t* key, const int64_t* ts, cons
 // one classification round allow, and the fire reads half as many fragments. Bucket counts are
 // u16 pairs in one LDS word (ds_add_u32 of 1 << 16 * (b & 1): a tile has < 2^16 records).
 // *p.max_bucket: the largest bucket count of one tile (skew).
-__global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams pa) {
-    // (the arguments re-read per tile through an opaque offset, as in the fire: hoisted to the
-    // kernel's entry they were held across the tile loop, 103 SGPRs spilled to VGPR lanes)
-    const IngestParams* pp = &pa;
-#define p (*pp)
+__global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams p) {
     constexpr int T = kTileThreads;
     constexpr int R = kTileR;
     constexpr int H = kTileH;
@@ -3207,9 +3203,6 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams pa) {
     if (beg < end) load(beg, ka, ta);
     int j = 0;
     for (int64_t t0 = beg; t0 < end; t0 += TILE, j++) {
-#if !defined(FG_P1_HOIST)
-        pp = &(&pa)[opaque_zero()];
-#endif
         uint32_t rcb[H][R], k32[H][R];
         {
             longlong2 kb[R / 2], tb[R / 2];
@@ -3332,7 +3325,6 @@ __global__ __launch_bounds__(kTileThreads) void k_tile_part1(IngestParams pa) {
         if (s_qmax != JMIN) atomicMax(p.qmax, s_qmax);
         if (s_qnext != JMAX) atomicMin(p.qnext, s_qnext);
     }
-#undef p
 }
 
 hipError_t launch_tile_part1(const IngestParams& p, hipStream_t s) {
