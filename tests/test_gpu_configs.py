@@ -134,7 +134,7 @@ def compare_rows(g, e, S, ctx, aggs):
 
 
 def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch=None, keys=None,
-               final_wm_after=None, async_wm=False):
+               final_wm_after=None, async_wm=False, batch=None):
     """final_wm_after: end with the watermark `final_wm_after` ms past the last regular one
     instead of Long.MAX_VALUE (CUMULATE: MAX_VALUE would fire every remaining step window of
     the hour for every key -- 60 x 12.5M rows)."""
@@ -145,7 +145,7 @@ def run_config(workload, n, aggs, oracle_kind, size, slide, snapshot_after_batch
     B = _bench()
     wl = B.WORKLOADS[workload]
     keys = keys or wl["keys"]
-    rate, batch = wl["rate"], wl.get("batch", 50_000_000)
+    rate, batch = wl["rate"], batch or wl.get("batch", 50_000_000)
     wm_every = wl.get("wm_every", 1_000_000)
     dev = torch.device("cuda", 0)
     key, ts, val = B.gen_columns(n, keys, rate, 0, dev, jitter=wl["jitter"], zipf=wl["zipf"])
@@ -211,6 +211,17 @@ def test_config0_datastream_forced_tile_grid(monkeypatch, grid):
     monkeypatch.setenv("FG_TILE_GRID", grid)
     nrows, _ = run_config("datastream", 4_000_000, ("sum",), O.TUMBLE, 1000, 0)
     assert nrows == 4 * 10_000
+
+
+def test_config1_tumble_two_passes_per_window():
+    """configs[1] in 50M-record micro-batches: every window fires from two tile passes of 8.1k tiles
+    each, large enough that the fire's waves take their tile groups from the per-pass LDS counters
+    (tile_walk_grab; one counter per pass, the second pass's groups taken while slower waves still
+    walk the first)."""
+    from oracle import oracle as O
+    nrows, late = run_config("tumble", 200_000_000, ("count_star", "count", "sum", "avg"), O.TUMBLE, 1000, 0,
+                             async_wm=True, batch=50_000_000)
+    assert nrows > 19_000_000 and late == 0
 
 
 @pytest.mark.parametrize("wm", ["sync", "async"])
